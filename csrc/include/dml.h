@@ -1,0 +1,95 @@
+// dml.h — shared declarations for the MI355X-native inference runtime.
+//
+// Everything here is plain C ABI so the Python side can bind it with ctypes
+// (no torch headers, no pybind: the .so is built by one hipcc line in seconds
+// and resolves libamdhip64.so.7 to the copy torch already loaded).
+//
+// Layout conventions (all kernels):
+//   activations : NHWC bf16, with an explicit per-pixel channel stride (ld*) so
+//                 that Inception's channel concat is a strided write into one
+//                 buffer (no concat kernel) and a branch can read a channel slice.
+//   weights     : [Cout_pad][K_pad] bf16, K ordered (r, s, c) — one output channel
+//                 per row, BatchNorm already folded in on the host.
+//   bias        : fp32 [Cout_pad] (folded BN shift / conv bias).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// Implicit-GEMM convolution (GEMM view: M = N*Ho*Wo pixels, N = Cout, K = kh*kw*Cin)
+// with fused epilogue  y = act(acc + bias[c] (+ res[m, c])).
+typedef struct {
+  const void* x;      // bf16 NHWC input, already offset to the first input channel
+  const void* w;      // bf16 [Coutp][Kpad]
+  const float* bias;  // fp32 [Coutp]
+  const void* res;    // optional bf16 residual (same pixel grid as y), or null
+  void* y;            // output (bf16 or fp32), already offset to the first output channel
+  int N, H, W, Cin, ldx;
+  int kh, kw, sh, sw, ph, pw;
+  int Ho, Wo, Cout, K, Kpad;
+  int ldy, ldr;
+  int relu, out_f32;
+} DmlConvArgs;
+
+typedef struct {
+  const void* x;  // bf16 NHWC
+  void* y;        // bf16 NHWC
+  int N, H, W, C, ldx;
+  int Ho, Wo, ldy;
+  int k, stride, pad;  // square window
+  int mode;            // 0 = max (padding never wins), 1 = avg with padding excluded from the divisor
+} DmlPoolArgs;
+
+typedef struct {
+  const void* src;  // uint8 [N][Hs][Ws][3] RGB
+  void* y;          // bf16 NHWC, C = 8 (RGB/BGR + 5 zero channels)
+  int N, Hs, Ws, Ho, Wo;
+  int mode;         // 0 = caffe (BGR, minus ImageNet mean), 1 = tf (x/127.5 - 1)
+} DmlPreprocArgs;
+
+// ---- single-op launches (used by tests and by the plan executor) ----
+int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
+int dml_conv_pick_cfg(const DmlConvArgs* a);
+int dml_pool(const DmlPoolArgs* a, hipStream_t s);
+int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);
+int dml_softmax_top5(const float* logits, int B, int classes, int ld, float* probs_out,
+                     int* top_idx, float* top_p, hipStream_t s);
+int dml_preprocess(const DmlPreprocArgs* a, hipStream_t s);
+
+// ---- plan executor (C++ runtime, csrc/runtime/plan.cpp) ----
+void* dml_plan_create(void);
+void dml_plan_destroy(void* plan);
+int dml_plan_add_conv(void* plan, const DmlConvArgs* a, int cfg);
+int dml_plan_add_pool(void* plan, const DmlPoolArgs* a);
+int dml_plan_add_gap(void* plan, const void* x, void* y, int N, int HW, int C, int ldx);
+int dml_plan_add_softmax_top5(void* plan, const float* logits, int B, int classes, int ld,
+                              float* probs, int* idx, float* p);
+int dml_plan_add_preprocess(void* plan, const DmlPreprocArgs* a);
+int dml_plan_size(void* plan);
+int dml_plan_run(void* plan, hipStream_t s);
+int dml_plan_run_range(void* plan, int begin, int end, hipStream_t s);
+int dml_plan_capture(void* plan, hipStream_t s);   // capture the whole plan into a hipGraph
+int dml_plan_replay(void* plan, hipStream_t s);    // launch the captured graph
+int dml_plan_time_ops(void* plan, hipStream_t s, float* ms_out, int n);  // per-op hipEvent timing
+
+// ---- pinned-host staging ring (csrc/runtime/staging.cpp) ----
+void* dml_ring_create(int slots, size_t slot_bytes);
+void dml_ring_destroy(void* ring);
+void* dml_ring_slot(void* ring, int slot);
+int dml_ring_h2d(void* ring, int slot, void* dst, size_t bytes, hipStream_t copy_stream);
+int dml_ring_wait(void* ring, int slot, hipStream_t compute_stream);  // compute waits for copy
+int dml_ring_sync(void* ring, int slot);                               // host waits (slot reusable)
+void* dml_host_alloc(size_t bytes);
+void dml_host_free(void* p);
+int dml_memcpy_h2d_async(void* dst, const void* src, size_t bytes, hipStream_t s);
+int dml_memcpy_d2h_async(void* dst, const void* src, size_t bytes, hipStream_t s);
+
+const char* dml_last_error(void);
+int dml_device_info(int* cus, int* arch_major, int* arch_minor);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,227 @@
+// misc.hip — the memory-bound kernels around the convolutions (gfx950).
+//
+//   pool3x3   : max (ResNet pool1 / Inception stem, mixed3, mixed8) and
+//               avg 'same' with padding excluded from the divisor (Inception
+//               pool branches; TF SAME avg_pool semantics).
+//   gap       : global average pool, NHWC -> [N][C].
+//   softmax_top5 : row softmax over the classes + wave-level top-5 (replaces
+//               Keras decode_predictions(top=5), reference models.py:42,67).
+//   preprocess: uint8 RGB -> nearest resize -> caffe/tf normalisation -> bf16
+//               NHWC with the channel dim padded to 8 (reference models.py:34-38,
+//               59-63 do this per image on the CPU).
+// All bf16 traffic is 16 bytes per lane (8 channels), per the CDNA4 guide's
+// vectorisation rule; every kernel is a grid-stride loop capped near 8 blocks/CU.
+#include "common.h"
+#include "dml.h"
+
+namespace dml {
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = bf2f(v.x & 0xffff); f[1] = bf2f(v.x >> 16);
+  f[2] = bf2f(v.y & 0xffff); f[3] = bf2f(v.y >> 16);
+  f[4] = bf2f(v.z & 0xffff); f[5] = bf2f(v.z >> 16);
+  f[6] = bf2f(v.w & 0xffff); f[7] = bf2f(v.w >> 16);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+static inline unsigned grid_for(long work, int block) {
+  long g = (work + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+__global__ __launch_bounds__(256) void pool3x3_kernel(DmlPoolArgs a) {
+  const int C8 = a.C / 8;
+  const long total = (long)a.N * a.Ho * a.Wo * C8;
+  const bf16* x = (const bf16*)a.x;
+  bf16* y = (bf16*)a.y;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % C8);
+    long p = t / C8;
+    const int ow = (int)(p % a.Wo); p /= a.Wo;
+    const int oh = (int)(p % a.Ho);
+    const int n = (int)(p / a.Ho);
+    const int h0 = oh * a.stride - a.pad, w0 = ow * a.stride - a.pad;
+    float acc[8];
+    const float init = a.mode == 0 ? -3.0e38f : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = init;
+    int cnt = 0;
+    for (int r = 0; r < a.k; ++r) {
+      const int ih = h0 + r;
+      if ((unsigned)ih >= (unsigned)a.H) continue;
+      for (int s = 0; s < a.k; ++s) {
+        const int iw = w0 + s;
+        if ((unsigned)iw >= (unsigned)a.W) continue;
+        const uint4 v = *(const uint4*)(x + ((long)(n * a.H + ih) * a.W + iw) * a.ldx + cg * 8);
+        float f[8];
+        unpack8(v, f);
+        if (a.mode == 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] = fmaxf(acc[j], f[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += f[j];
+        }
+        ++cnt;
+      }
+    }
+    if (a.mode == 1) {
+      const float inv = 1.f / (float)(cnt > 0 ? cnt : 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= inv;
+    }
+    *(uint4*)(y + ((long)(n * a.Ho + oh) * a.Wo + ow) * a.ldy + cg * 8) = pack8(acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void gap_kernel(const bf16* x, bf16* y, int N, int HW, int C, int ldx) {
+  const int C8 = C / 8;
+  const long total = (long)N * C8;
+  const float inv = 1.f / (float)HW;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % C8);
+    const int n = (int)(t / C8);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16* base = x + (long)n * HW * ldx + cg * 8;
+    for (int p = 0; p < HW; ++p) {
+      float f[8];
+      unpack8(*(const uint4*)(base + (long)p * ldx), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= inv;
+    *(uint4*)(y + (long)n * C + cg * 8) = pack8(acc);
+  }
+}
+
+// One wave (64 lanes) per row. Lane l owns classes l, l+64, ... (coalesced).
+template <int PER_LANE>
+__global__ __launch_bounds__(256) void softmax_top5_kernel(const float* logits, int B, int classes, int ld,
+                                                           float* probs, int* top_idx, float* top_p) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float* lr = logits + (long)row * ld;
+  float v[PER_LANE];
+  float mx = -3.0e38f;
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int c = lane + i * 64;
+    v[i] = c < classes ? lr[c] : -3.0e38f;
+    mx = fmaxf(mx, v[i]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int c = lane + i * 64;
+    const float e = c < classes ? __expf(v[i] - mx) : 0.f;
+    sum += e;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  const float inv = 1.f / sum;
+  if (probs) {
+#pragma unroll
+    for (int i = 0; i < PER_LANE; ++i) {
+      const int c = lane + i * 64;
+      if (c < classes) probs[(long)row * classes + c] = __expf(v[i] - mx) * inv;
+    }
+  }
+  // top-5: 5 rounds of (lane-local argmax -> wave argmax, ties to the lower class id)
+  unsigned taken = 0;
+  for (int k = 0; k < 5; ++k) {
+    float bv = -3.0e38f;
+    int bi = 0x7fffffff, bslot = -1;
+#pragma unroll
+    for (int i = 0; i < PER_LANE; ++i) {
+      const int c = lane + i * 64;
+      if (c < classes && !(taken >> i & 1u) && v[i] > bv) { bv = v[i]; bi = c; bslot = i; }
+    }
+    float wv = bv;
+    int wi = bi;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(wv, o);
+      const int oi = __shfl_xor(wi, o);
+      if (ov > wv || (ov == wv && oi < wi)) { wv = ov; wi = oi; }
+    }
+    if (wi == bi && bslot >= 0) taken |= 1u << bslot;
+    if (lane == 0) {
+      top_idx[row * 5 + k] = wi;
+      top_p[row * 5 + k] = __expf(wv - mx) * inv;
+    }
+  }
+}
+
+// Pillow NEAREST resize (Keras load_img default): src = floor((dst + 0.5) * Ssrc / Sdst).
+__global__ __launch_bounds__(256) void preprocess_kernel(DmlPreprocArgs a) {
+  const long total = (long)a.N * a.Ho * a.Wo;
+  const float sy = (float)a.Hs / (float)a.Ho, sx = (float)a.Ws / (float)a.Wo;
+  const unsigned char* src = (const unsigned char*)a.src;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int ow = (int)(t % a.Wo);
+    long p = t / a.Wo;
+    const int oh = (int)(p % a.Ho);
+    const int n = (int)(p / a.Ho);
+    int iy = (int)(((float)oh + 0.5f) * sy), ix = (int)(((float)ow + 0.5f) * sx);
+    iy = min(iy, a.Hs - 1);
+    ix = min(ix, a.Ws - 1);
+    const unsigned char* px = src + (((long)n * a.Hs + iy) * a.Ws + ix) * 3;
+    const float r = px[0], g = px[1], b = px[2];
+    float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (a.mode == 0) {  // caffe: RGB->BGR, subtract BGR mean, no scaling
+      f[0] = b - 103.939f; f[1] = g - 116.779f; f[2] = r - 123.68f;
+    } else {            // tf: scale to [-1, 1]
+      f[0] = r / 127.5f - 1.f; f[1] = g / 127.5f - 1.f; f[2] = b / 127.5f - 1.f;
+    }
+    *(uint4*)((bf16*)a.y + t * 8) = pack8(f);
+  }
+}
+
+}  // namespace dml
+
+extern "C" int dml_pool(const DmlPoolArgs* a, hipStream_t s) {
+  if (a->C % 8 || a->ldx % 8 || a->ldy % 8) { dml_set_error("dml_pool: channels must be %8"); return -1; }
+  const long work = (long)a->N * a->Ho * a->Wo * (a->C / 8);
+  hipLaunchKernelGGL(dml::pool3x3_kernel, dim3(dml::grid_for(work, 256)), dim3(256), 0, s, *a);
+  DML_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s) {
+  if (C % 8 || ldx % 8) { dml_set_error("dml_global_avgpool: channels must be %8"); return -1; }
+  const long work = (long)N * (C / 8);
+  hipLaunchKernelGGL(dml::gap_kernel, dim3(dml::grid_for(work, 256)), dim3(256), 0, s, (const bf16*)x,
+                     (bf16*)y, N, HW, C, ldx);
+  DML_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dml_softmax_top5(const float* logits, int B, int classes, int ld, float* probs, int* top_idx,
+                                float* top_p, hipStream_t s) {
+  const dim3 grid((B + 3) / 4), block(256);
+  if (classes <= 16 * 64) {
+    hipLaunchKernelGGL(dml::softmax_top5_kernel<16>, grid, block, 0, s, logits, B, classes, ld, probs, top_idx, top_p);
+  } else if (classes <= 32 * 64) {
+    hipLaunchKernelGGL(dml::softmax_top5_kernel<32>, grid, block, 0, s, logits, B, classes, ld, probs, top_idx, top_p);
+  } else {
+    dml_set_error("dml_softmax_top5: classes > 2048");
+    return -1;
+  }
+  DML_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dml_preprocess(const DmlPreprocArgs* a, hipStream_t s) {
+  const long work = (long)a->N * a->Ho * a->Wo;
+  hipLaunchKernelGGL(dml::preprocess_kernel, dim3(dml::grid_for(work, 256)), dim3(256), 0, s, *a);
+  DML_CHECK_LAUNCH();
+  return 0;
+}

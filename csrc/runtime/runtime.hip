@@ -1,0 +1,230 @@
+// runtime.hip — the native host runtime around the kernels.
+//
+//  * Plan executor: the model graph (built once by the Python planner from the
+//    layer IR) is a flat vector of launch records replayed per batch. It can be
+//    captured into a hipGraph so a forward is one graph launch (the reference
+//    rebuilds the Keras model for every batch instead, models.py:18-21,84-91).
+//  * Pinned staging ring: hipHostMalloc'd slots + one event per slot. A copy
+//    stream moves batch k+1 host->HBM (hipMemcpyAsync) while the compute stream
+//    runs batch k; the compute stream waits on the slot's event, not on the host.
+//    This replaces the reference's per-image scp pull (worker.py:1365-1366,
+//    file_service.py:116-124).
+#include <hip/hip_runtime.h>
+#include <string>
+#include <vector>
+#include <mutex>
+#include <cstring>
+#include "dml.h"
+
+static thread_local std::string g_err;
+extern "C" void dml_set_error(const char* msg) { g_err = msg ? msg : ""; }
+extern "C" const char* dml_last_error(void) { return g_err.c_str(); }
+
+#define HIP_OK(expr)                                       \
+  do {                                                     \
+    hipError_t _e = (expr);                                \
+    if (_e != hipSuccess) {                                \
+      g_err = std::string(#expr) + ": " + hipGetErrorString(_e); \
+      return -1;                                           \
+    }                                                      \
+  } while (0)
+
+extern "C" int dml_device_info(int* cus, int* arch_major, int* arch_minor) {
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  hipDeviceProp_t p;
+  HIP_OK(hipGetDeviceProperties(&p, dev));
+  *cus = p.multiProcessorCount;
+  *arch_major = p.major;
+  *arch_minor = p.minor;
+  return 0;
+}
+
+// ----------------------------------------------------------------- plan ----
+namespace {
+enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC };
+struct GapArgs { const void* x; void* y; int N, HW, C, ldx; };
+struct SmArgs { const float* logits; int B, classes, ld; float* probs; int* idx; float* p; };
+struct Op {
+  OpKind kind;
+  int cfg;
+  DmlConvArgs conv;
+  DmlPoolArgs pool;
+  GapArgs gap;
+  SmArgs sm;
+  DmlPreprocArgs pre;
+};
+struct Plan {
+  std::vector<Op> ops;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  ~Plan() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+  }
+};
+
+int run_op(const Op& o, hipStream_t s) {
+  switch (o.kind) {
+    case OP_CONV: return dml_conv(&o.conv, o.cfg, s);
+    case OP_POOL: return dml_pool(&o.pool, s);
+    case OP_GAP: return dml_global_avgpool(o.gap.x, o.gap.y, o.gap.N, o.gap.HW, o.gap.C, o.gap.ldx, s);
+    case OP_SMTOP5: return dml_softmax_top5(o.sm.logits, o.sm.B, o.sm.classes, o.sm.ld, o.sm.probs, o.sm.idx, o.sm.p, s);
+    case OP_PREPROC: return dml_preprocess(&o.pre, s);
+  }
+  return -1;
+}
+}  // namespace
+
+extern "C" void* dml_plan_create(void) { return new Plan(); }
+extern "C" void dml_plan_destroy(void* p) { delete (Plan*)p; }
+extern "C" int dml_plan_size(void* p) { return (int)((Plan*)p)->ops.size(); }
+
+extern "C" int dml_plan_add_conv(void* p, const DmlConvArgs* a, int cfg) {
+  Op o{};
+  o.kind = OP_CONV;
+  o.conv = *a;
+  o.cfg = cfg < 0 ? dml_conv_pick_cfg(a) : cfg;
+  ((Plan*)p)->ops.push_back(o);
+  return o.cfg;
+}
+extern "C" int dml_plan_add_pool(void* p, const DmlPoolArgs* a) {
+  Op o{};
+  o.kind = OP_POOL;
+  o.pool = *a;
+  ((Plan*)p)->ops.push_back(o);
+  return 0;
+}
+extern "C" int dml_plan_add_gap(void* p, const void* x, void* y, int N, int HW, int C, int ldx) {
+  Op o{};
+  o.kind = OP_GAP;
+  o.gap = GapArgs{x, y, N, HW, C, ldx};
+  ((Plan*)p)->ops.push_back(o);
+  return 0;
+}
+extern "C" int dml_plan_add_softmax_top5(void* p, const float* logits, int B, int classes, int ld, float* probs,
+                                         int* idx, float* pr) {
+  Op o{};
+  o.kind = OP_SMTOP5;
+  o.sm = SmArgs{logits, B, classes, ld, probs, idx, pr};
+  ((Plan*)p)->ops.push_back(o);
+  return 0;
+}
+extern "C" int dml_plan_add_preprocess(void* p, const DmlPreprocArgs* a) {
+  Op o{};
+  o.kind = OP_PREPROC;
+  o.pre = *a;
+  ((Plan*)p)->ops.push_back(o);
+  return 0;
+}
+
+extern "C" int dml_plan_run_range(void* p, int begin, int end, hipStream_t s) {
+  Plan* pl = (Plan*)p;
+  if (end < 0 || end > (int)pl->ops.size()) end = (int)pl->ops.size();
+  for (int i = begin; i < end; ++i)
+    if (run_op(pl->ops[i], s)) return -1 - i;
+  return 0;
+}
+extern "C" int dml_plan_run(void* p, hipStream_t s) { return dml_plan_run_range(p, 0, -1, s); }
+
+extern "C" int dml_plan_capture(void* p, hipStream_t s) {
+  Plan* pl = (Plan*)p;
+  if (pl->exec) { (void)hipGraphExecDestroy(pl->exec); pl->exec = nullptr; }
+  if (pl->graph) { (void)hipGraphDestroy(pl->graph); pl->graph = nullptr; }
+  HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  int rc = dml_plan_run(p, s);
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(s, &g);
+  if (rc) return rc;
+  if (e != hipSuccess) { g_err = hipGetErrorString(e); return -1; }
+  pl->graph = g;
+  HIP_OK(hipGraphInstantiate(&pl->exec, g, nullptr, nullptr, 0));
+  return 0;
+}
+extern "C" int dml_plan_replay(void* p, hipStream_t s) {
+  Plan* pl = (Plan*)p;
+  if (!pl->exec) { g_err = "dml_plan_replay: not captured"; return -1; }
+  HIP_OK(hipGraphLaunch(pl->exec, s));
+  return 0;
+}
+
+extern "C" int dml_plan_time_ops(void* p, hipStream_t s, float* ms_out, int n) {
+  Plan* pl = (Plan*)p;
+  const int cnt = (int)pl->ops.size() < n ? (int)pl->ops.size() : n;
+  std::vector<hipEvent_t> ev(cnt + 1);
+  for (auto& e : ev) HIP_OK(hipEventCreate(&e));
+  HIP_OK(hipEventRecord(ev[0], s));
+  for (int i = 0; i < cnt; ++i) {
+    if (run_op(pl->ops[i], s)) return -1;
+    HIP_OK(hipEventRecord(ev[i + 1], s));
+  }
+  HIP_OK(hipEventSynchronize(ev[cnt]));
+  for (int i = 0; i < cnt; ++i) HIP_OK(hipEventElapsedTime(&ms_out[i], ev[i], ev[i + 1]));
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return 0;
+}
+
+// ---------------------------------------------------------- staging ring ----
+namespace {
+struct Ring {
+  std::vector<void*> host;
+  std::vector<hipEvent_t> ev;
+  size_t slot_bytes = 0;
+};
+}  // namespace
+
+extern "C" void* dml_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) { g_err = "hipHostMalloc failed"; return nullptr; }
+  return p;
+}
+extern "C" void dml_host_free(void* p) { if (p) (void)hipHostFree(p); }
+
+extern "C" int dml_memcpy_h2d_async(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+  return 0;
+}
+extern "C" int dml_memcpy_d2h_async(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+  return 0;
+}
+
+extern "C" void* dml_ring_create(int slots, size_t slot_bytes) {
+  Ring* r = new Ring();
+  r->slot_bytes = slot_bytes;
+  for (int i = 0; i < slots; ++i) {
+    void* h = dml_host_alloc(slot_bytes);
+    hipEvent_t e;
+    if (!h || hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      for (void* q : r->host) dml_host_free(q);
+      delete r;
+      return nullptr;
+    }
+    r->host.push_back(h);
+    r->ev.push_back(e);
+  }
+  return r;
+}
+extern "C" void dml_ring_destroy(void* rp) {
+  Ring* r = (Ring*)rp;
+  if (!r) return;
+  for (auto e : r->ev) (void)hipEventSynchronize(e), (void)hipEventDestroy(e);
+  for (void* h : r->host) dml_host_free(h);
+  delete r;
+}
+extern "C" void* dml_ring_slot(void* rp, int slot) { return ((Ring*)rp)->host[slot]; }
+extern "C" int dml_ring_h2d(void* rp, int slot, void* dst, size_t bytes, hipStream_t cs) {
+  Ring* r = (Ring*)rp;
+  if (bytes > r->slot_bytes) { g_err = "dml_ring_h2d: bytes > slot"; return -1; }
+  HIP_OK(hipMemcpyAsync(dst, r->host[slot], bytes, hipMemcpyHostToDevice, cs));
+  HIP_OK(hipEventRecord(r->ev[slot], cs));
+  return 0;
+}
+extern "C" int dml_ring_wait(void* rp, int slot, hipStream_t s) {
+  HIP_OK(hipStreamWaitEvent(s, ((Ring*)rp)->ev[slot], 0));
+  return 0;
+}
+extern "C" int dml_ring_sync(void* rp, int slot) {
+  HIP_OK(hipEventSynchronize(((Ring*)rp)->ev[slot]));
+  return 0;
+}

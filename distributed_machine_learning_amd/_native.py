@@ -1,0 +1,135 @@
+"""ctypes binding of the native HIP library (csrc/ -> libdml_hip.so).
+
+``lib()`` loads the in-tree library (building it first if the sources changed
+and hipcc is available). On a machine with a GPU the native path is the ONLY
+path: every op raises if the library cannot be loaded rather than silently
+falling back to PyTorch.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+from . import _build
+
+_lock = threading.Lock()
+_lib = None
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p), ("w", C.c_void_p), ("bias", C.c_void_p), ("res", C.c_void_p), ("y", C.c_void_p),
+        ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("Cin", C.c_int), ("ldx", C.c_int),
+        ("kh", C.c_int), ("kw", C.c_int), ("sh", C.c_int), ("sw", C.c_int), ("ph", C.c_int), ("pw", C.c_int),
+        ("Ho", C.c_int), ("Wo", C.c_int), ("Cout", C.c_int), ("K", C.c_int), ("Kpad", C.c_int),
+        ("ldy", C.c_int), ("ldr", C.c_int),
+        ("relu", C.c_int), ("out_f32", C.c_int),
+    ]
+
+
+class PoolArgs(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p), ("y", C.c_void_p),
+        ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("C", C.c_int), ("ldx", C.c_int),
+        ("Ho", C.c_int), ("Wo", C.c_int), ("ldy", C.c_int),
+        ("k", C.c_int), ("stride", C.c_int), ("pad", C.c_int), ("mode", C.c_int),
+    ]
+
+
+class PreprocArgs(C.Structure):
+    _fields_ = [
+        ("src", C.c_void_p), ("y", C.c_void_p),
+        ("N", C.c_int), ("Hs", C.c_int), ("Ws", C.c_int), ("Ho", C.c_int), ("Wo", C.c_int), ("mode", C.c_int),
+    ]
+
+
+_SIGS = {
+    "dml_conv": (C.c_int, [C.POINTER(ConvArgs), C.c_int, C.c_void_p]),
+    "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),
+    "dml_pool": (C.c_int, [C.POINTER(PoolArgs), C.c_void_p]),
+    "dml_global_avgpool": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]),
+    "dml_softmax_top5": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_void_p]),
+    "dml_preprocess": (C.c_int, [C.POINTER(PreprocArgs), C.c_void_p]),
+    "dml_plan_create": (C.c_void_p, []),
+    "dml_plan_destroy": (None, [C.c_void_p]),
+    "dml_plan_add_conv": (C.c_int, [C.c_void_p, C.POINTER(ConvArgs), C.c_int]),
+    "dml_plan_add_pool": (C.c_int, [C.c_void_p, C.POINTER(PoolArgs)]),
+    "dml_plan_add_gap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "dml_plan_add_softmax_top5": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_void_p, C.c_void_p]),
+    "dml_plan_add_preprocess": (C.c_int, [C.c_void_p, C.POINTER(PreprocArgs)]),
+    "dml_plan_size": (C.c_int, [C.c_void_p]),
+    "dml_plan_run": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dml_plan_run_range": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "dml_plan_capture": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dml_plan_replay": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dml_plan_time_ops": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_float), C.c_int]),
+    "dml_ring_create": (C.c_void_p, [C.c_int, C.c_size_t]),
+    "dml_ring_destroy": (None, [C.c_void_p]),
+    "dml_ring_slot": (C.c_void_p, [C.c_void_p, C.c_int]),
+    "dml_ring_h2d": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "dml_ring_wait": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
+    "dml_ring_sync": (C.c_int, [C.c_void_p, C.c_int]),
+    "dml_host_alloc": (C.c_void_p, [C.c_size_t]),
+    "dml_host_free": (None, [C.c_void_p]),
+    "dml_memcpy_h2d_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "dml_memcpy_d2h_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "dml_last_error": (C.c_char_p, []),
+    "dml_device_info": (C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (building if needed) libdml_hip.so. Raises NativeError on failure."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  -- load torch's libamdhip64.so.7 first so ours binds to it
+
+        path = _build.LIB_PATH
+        if os.environ.get("DML_SKIP_BUILD") != "1":
+            try:
+                path = _build.build()
+            except Exception as e:  # hipcc missing on a runtime-only box: use the shipped .so
+                if not path.exists():
+                    raise NativeError(f"cannot build libdml_hip.so: {e}") from e
+        if not path.exists():
+            raise NativeError(f"{path} missing; run python -m distributed_machine_learning_amd._build")
+        L = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+        return _lib
+
+
+def check(rc: int, what: str) -> int:
+    if rc != 0 and rc is not None and not (isinstance(rc, int) and rc > 0):
+        msg = lib().dml_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed (rc={rc}): {msg}")
+    return rc
+
+
+def stream_ptr(stream=None) -> int:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False

@@ -1,0 +1,234 @@
+"""The MI355X inference engine: layer IR -> native launch plan.
+
+Lowering (SURVEY §7.1 "C++/HIP graph executor"):
+
+* BatchNorm is folded into the conv weights/bias once, on the host
+  (``weights.fold_conv``); weights become bf16 ``[Cout_pad][K_pad]`` with K in
+  (r, s, c) order, resident in HBM for the life of the process (the reference
+  rebuilds the Keras model per batch, models.py:84-91).
+* Every tensor is an NHWC bf16 buffer; Inception concats are channel-offset
+  writes into one buffer; a liveness pass reuses buffers.
+* The forward is recorded once into the native plan (csrc/runtime/runtime.hip):
+  preprocess -> convs/pools -> global-avg-pool -> FC (1x1 implicit GEMM, fp32
+  out) -> softmax+top-5, and can be captured into a hipGraph.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from .graph import Conv, Dense, Graph, GlobalAvgPool, Pool
+from .weights import Weights, fold_conv
+
+
+def _r(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def pack_conv_weight(kernel_hwio: np.ndarray, cin_eff: int, cout_pad: int, k_pad: int) -> np.ndarray:
+    kh, kw, cin, cout = kernel_hwio.shape
+    k = np.zeros((kh, kw, cin_eff, cout), np.float32)
+    k[:, :, :cin, :] = kernel_hwio
+    k = k.transpose(3, 0, 1, 2).reshape(cout, kh * kw * cin_eff)
+    out = np.zeros((cout_pad, k_pad), np.float32)
+    out[:cout, : k.shape[1]] = k
+    return out
+
+
+class Engine:
+    """Batch-``batch`` executor of ``graph`` on the current CUDA (HIP) device."""
+
+    def __init__(self, graph: Graph, weights: Weights, batch: int, device: str = "cuda",
+                 src_hw: Optional[Tuple[int, int]] = None, cfg_overrides: Optional[Dict[str, int]] = None,
+                 src_slots: int = 1):
+        self.g, self.batch, self.device = graph, batch, torch.device(device)
+        self.src_slots = src_slots
+        self.lib = N.lib()
+        self.src_hw = src_hw or graph.input_hw
+        self.cfg_overrides = cfg_overrides or {}
+        self._keep = []  # keep ctypes structs / tensors alive
+        self._upload_weights(weights)
+        self._alloc_buffers()
+        self._build_plan()
+
+    # ------------------------------------------------------------ weights ----
+    def _upload_weights(self, w: Weights) -> None:
+        self.wdev: Dict[str, Tuple[torch.Tensor, torch.Tensor, int, int, int]] = {}
+        for n in self.g.nodes:
+            if isinstance(n, Conv):
+                k, b = fold_conv(n, w)
+                cin_eff = _r(n.cin, 8)
+                K = n.kh * n.kw * cin_eff
+                coutp, kpad = _r(n.cout, 128), _r(K, 64)
+                wk = pack_conv_weight(k, cin_eff, coutp, kpad)
+            elif isinstance(n, Dense):
+                k = w[f"{n.name}/kernel"][None, None]  # 1x1xCinxCout
+                b = w[f"{n.name}/bias"]
+                cin_eff = _r(n.cin, 8)
+                K = cin_eff
+                coutp, kpad = _r(n.cout, 128), _r(K, 64)
+                wk = pack_conv_weight(k, cin_eff, coutp, kpad)
+            else:
+                continue
+            bias = np.zeros(coutp, np.float32)
+            bias[: len(b)] = b
+            self.wdev[n.name] = (
+                torch.from_numpy(wk).to(self.device, torch.bfloat16).contiguous(),
+                torch.from_numpy(bias).to(self.device),
+                K, kpad, cin_eff,
+            )
+
+    # ------------------------------------------------------------ buffers ----
+    def _alloc_buffers(self) -> None:
+        g, B = self.g, self.batch
+        nodes = g.nodes
+        first_def, last_use = {g.input: -1}, {}
+        for i, n in enumerate(nodes):
+            first_def.setdefault(n.out, i)
+            for src in (n.inp, getattr(n, "residual", None)):
+                if src:
+                    last_use[src] = i
+        last_use[g.logits] = len(nodes)
+        self.cbuf = {name: _r(t.c, 8) for name, t in g.tensors.items()}
+        self.cbuf[g.input] = 8
+        self.buf: Dict[str, torch.Tensor] = {}
+        free: Dict[int, List[torch.Tensor]] = {}
+        order = sorted(first_def.items(), key=lambda kv: kv[1])
+        release_at: Dict[int, List[str]] = {}
+        for name, lu in last_use.items():
+            release_at.setdefault(lu, []).append(name)
+        pending_release: List[str] = []
+        idx = 0
+        for step in range(-1, len(nodes) + 1):
+            # tensors whose last use was before this step can be recycled
+            for name in pending_release:
+                t = self.buf[name]
+                free.setdefault(t.numel(), []).append(t)
+            pending_release = release_at.get(step, [])
+            while idx < len(order) and order[idx][1] == step:
+                name = order[idx][0]
+                idx += 1
+                t = g.tensors[name]
+                numel = B * t.h * t.w * self.cbuf[name]
+                if name in (g.logits,):
+                    self.buf[name] = torch.empty((B, t.c), device=self.device, dtype=torch.float32)
+                    continue
+                lst = free.get(numel)
+                buf = lst.pop() if lst else torch.empty(numel, device=self.device, dtype=torch.bfloat16)
+                self.buf[name] = buf
+        # uint8 source slots (double-buffered: the copy stream fills slot k+1
+        # while the compute stream consumes slot k)
+        self.srcs = [torch.zeros((B, self.src_hw[0], self.src_hw[1], 3), device=self.device, dtype=torch.uint8)
+                     for _ in range(self.src_slots)]
+        self.src = self.srcs[0]
+        # one packed result tensor [2][B][5]: top-5 class ids (int32) and their
+        # probabilities (fp32 bits) -> a single RCCL gather per batch
+        self.result = torch.zeros((2, B, 5), device=self.device, dtype=torch.int32)
+        self.top_idx = self.result[0]
+        self.top_p = self.result[1].view(torch.float32)
+        self.probs = torch.zeros((B, g.classes), device=self.device, dtype=torch.float32)
+
+    def view(self, name: str) -> torch.Tensor:
+        """NHWC view of a tensor buffer (for tests / debugging)."""
+        t = self.g.tensors[name]
+        if name == self.g.logits:
+            return self.buf[name]
+        return self.buf[name].view(self.batch, t.h, t.w, self.cbuf[name])
+
+    # --------------------------------------------------------------- plan ----
+    def _build_plan(self) -> None:
+        self.plans = [self._build_one_plan(self.srcs[i]) for i in range(self.src_slots)]
+        self.plan = self.plans[0]
+        self.graph_captured = [False] * self.src_slots
+
+    def _build_one_plan(self, src: torch.Tensor):
+        g, B, L = self.g, self.batch, self.lib
+        plan = L.dml_plan_create()
+        self.op_names: List[str] = []
+        self.op_cfg: Dict[str, int] = {}
+        pa = N.PreprocArgs(src.data_ptr(), self.buf[g.input].data_ptr(), B, self.src_hw[0], self.src_hw[1],
+                           g.input_hw[0], g.input_hw[1], 0 if g.preprocess == "caffe" else 1)
+        N.check(L.dml_plan_add_preprocess(plan, C.byref(pa)), "plan preprocess")
+        self.op_names.append("preprocess")
+        for n in g.nodes:
+            if isinstance(n, (Conv, Dense)):
+                a = self._conv_args(n)
+                cfg = self.cfg_overrides.get(n.name, -1)
+                used = L.dml_plan_add_conv(plan, C.byref(a), cfg)
+                self.op_cfg[n.name] = used
+                self._keep.append(a)
+            elif isinstance(n, Pool):
+                h, w, c = g.shape(n.inp)
+                ho, wo, co = g.shape(n.out)
+                y = self.buf[n.out].data_ptr() + 2 * n.out_coff
+                a = N.PoolArgs(self.buf[n.inp].data_ptr(), y, B, h, w, c, self.cbuf[n.inp], ho, wo, self.cbuf[n.out],
+                               n.k, n.stride, n.pad, 0 if n.mode == "max" else 1)
+                N.check(L.dml_plan_add_pool(plan, C.byref(a)), "plan pool")
+            elif isinstance(n, GlobalAvgPool):
+                h, w, c = g.shape(n.inp)
+                N.check(L.dml_plan_add_gap(plan, self.buf[n.inp].data_ptr(), self.buf[n.out].data_ptr(),
+                                           B, h * w, c, self.cbuf[n.inp]), "plan gap")
+            self.op_names.append(n.name)
+        N.check(L.dml_plan_add_softmax_top5(plan, self.buf[g.logits].data_ptr(), B, g.classes, g.classes,
+                                            self.probs.data_ptr(), self.top_idx.data_ptr(), self.top_p.data_ptr()),
+                "plan softmax_top5")
+        self.op_names.append("softmax_top5")
+        return plan
+
+    def _conv_args(self, n) -> N.ConvArgs:
+        g, B = self.g, self.batch
+        wk, bias, K, kpad, cin_eff = self.wdev[n.name]
+        if isinstance(n, Dense):
+            x = self.buf[n.inp]
+            return N.ConvArgs(x.data_ptr(), wk.data_ptr(), bias.data_ptr(), None, self.buf[n.out].data_ptr(),
+                              B, 1, 1, cin_eff, self.cbuf[n.inp], 1, 1, 1, 1, 0, 0, 1, 1, n.cout, K, kpad,
+                              n.cout, 0, 0, 1)
+        h, w, _ = g.shape(n.inp)
+        ho, wo, _ = g.shape(n.out)
+        x = self.buf[n.inp].data_ptr() + 2 * n.in_coff
+        y = self.buf[n.out].data_ptr() + 2 * n.out_coff
+        res = self.buf[n.residual].data_ptr() if n.residual else None
+        ldr = self.cbuf[n.residual] if n.residual else 0
+        return N.ConvArgs(x, wk.data_ptr(), bias.data_ptr(), res, y, B, h, w, cin_eff, self.cbuf[n.inp],
+                          n.kh, n.kw, n.sh, n.sw, n.ph, n.pw, ho, wo, n.cout, K, kpad,
+                          self.cbuf[n.out], ldr, int(n.relu), int(n.out_f32))
+
+    # ---------------------------------------------------------------- run ----
+    def run(self, stream=None, use_graph: bool = False, slot: int = 0) -> None:
+        s = N.stream_ptr(stream)
+        plan = self.plans[slot]
+        if use_graph:
+            if not self.graph_captured[slot]:
+                N.check(self.lib.dml_plan_capture(plan, s), "plan capture")
+                self.graph_captured[slot] = True
+            N.check(self.lib.dml_plan_replay(plan, s), "plan replay")
+        else:
+            N.check(self.lib.dml_plan_run(plan, s), "plan run")
+
+    def run_from_preprocessed(self, stream=None) -> None:
+        N.check(self.lib.dml_plan_run_range(self.plan, 1, -1, N.stream_ptr(stream)), "plan run_range")
+
+    def infer(self, images_u8: torch.Tensor, stream=None):
+        """images_u8: [B, Hs, Ws, 3] uint8 (any device). Returns (top_idx, top_p) on device."""
+        self.src.copy_(images_u8, non_blocking=True)
+        self.run(stream)
+        return self.top_idx, self.top_p
+
+    def time_ops(self, stream=None) -> List[Tuple[str, float]]:
+        n = len(self.op_names)
+        arr = (C.c_float * n)()
+        N.check(self.lib.dml_plan_time_ops(self.plan, N.stream_ptr(stream), arr, n), "time_ops")
+        return list(zip(self.op_names, list(arr)))
+
+    def __del__(self):
+        try:
+            for p in getattr(self, "plans", []):
+                self.lib.dml_plan_destroy(p)
+            self.plans = []
+            self.plan = None
+        except Exception:
+            pass

@@ -1,0 +1,133 @@
+"""Plain-PyTorch fp32 executor of the layer IR — the numerics oracle.
+
+Runs NCHW on any device (CPU in tests) with BatchNorm applied UNFUSED from its
+raw statistics, so a bug in the engine's BN folding, channel-offset concat,
+implicit-GEMM padding or pooling divisor shows up as a mismatch. Also provides
+the preprocessing oracle (Pillow-NEAREST resize + caffe/tf normalisation,
+reference models.py:34-38 / 59-63).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .graph import Conv, Dense, Graph, GlobalAvgPool, Pool
+from .weights import Weights
+
+CAFFE_MEAN_BGR = (103.939, 116.779, 123.68)
+
+
+def preprocess_reference(images_u8: torch.Tensor, out_hw, mode: str) -> torch.Tensor:
+    """uint8 [N, Hs, Ws, 3] RGB -> fp32 NCHW [N, 3, Ho, Wo]."""
+    n, hs, ws, _ = images_u8.shape
+    ho, wo = out_hw
+    iy = torch.clamp(((torch.arange(ho, dtype=torch.float32) + 0.5) * (hs / ho)).floor().long(), max=hs - 1)
+    ix = torch.clamp(((torch.arange(wo, dtype=torch.float32) + 0.5) * (ws / wo)).floor().long(), max=ws - 1)
+    x = images_u8[:, iy][:, :, ix].float()  # N, Ho, Wo, 3 (RGB)
+    if mode == "caffe":
+        x = x[..., [2, 1, 0]] - torch.tensor(CAFFE_MEAN_BGR)
+    else:
+        x = x / 127.5 - 1.0
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+class OracleExecutor:
+    def __init__(self, g: Graph, w: Weights, device="cpu", dtype=torch.float32):
+        self.g, self.device, self.dtype = g, device, dtype
+        self.p = {k: torch.from_numpy(np.ascontiguousarray(v)).to(device, dtype) for k, v in w.items()}
+
+    def _bn(self, n: Conv, y: torch.Tensor) -> torch.Tensor:
+        p = self.p
+        gamma = p.get(f"{n.name}/gamma")
+        mean, var, beta = p[f"{n.name}/mean"], p[f"{n.name}/var"], p[f"{n.name}/beta"]
+        y = (y - mean[None, :, None, None]) / torch.sqrt(var[None, :, None, None] + n.bn_eps)
+        if gamma is not None:
+            y = y * gamma[None, :, None, None]
+        return y + beta[None, :, None, None]
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, keep: bool = False) -> Dict[str, torch.Tensor]:
+        """x: preprocessed NCHW fp32. Returns tensors dict (logits, probs, and all if keep)."""
+        g, p = self.g, self.p
+        n_img = x.shape[0]
+        t: Dict[str, torch.Tensor] = {g.input: x.to(self.device, self.dtype)}
+        for n in g.nodes:
+            if isinstance(n, Conv):
+                src = t[n.inp][:, n.in_coff:n.in_coff + n.cin]
+                k = p[f"{n.name}/kernel"].permute(3, 2, 0, 1)  # HWIO -> OIHW
+                y = F.conv2d(src, k, p.get(f"{n.name}/bias"), stride=(n.sh, n.sw), padding=(n.ph, n.pw))
+                if n.bn:
+                    y = self._bn(n, y)
+                if n.residual:
+                    y = y + t[n.residual]
+                if n.relu:
+                    y = F.relu(y)
+                self._write(t, n.out, y, n.out_coff, n_img)
+            elif isinstance(n, Pool):
+                src = t[n.inp]
+                if n.mode == "max":
+                    y = F.max_pool2d(F.pad(src, (n.pad,) * 4), n.k, n.stride)  # Keras ZeroPadding2D + valid pool
+                else:
+                    y = F.avg_pool2d(src, n.k, n.stride, padding=n.pad, count_include_pad=False)
+                self._write(t, n.out, y, n.out_coff, n_img)
+            elif isinstance(n, GlobalAvgPool):
+                t[n.out] = t[n.inp].mean(dim=(2, 3), keepdim=True)
+            elif isinstance(n, Dense):
+                y = t[n.inp].flatten(1) @ p[f"{n.name}/kernel"] + p[f"{n.name}/bias"]
+                t[n.out] = y
+        out = {"logits": t[g.logits], "probs": torch.softmax(t[g.logits], dim=-1)}
+        if keep:
+            out.update(t)
+        return out
+
+    def _write(self, t, name, y, coff, n_img):
+        h, w, c = self.g.shape(name)
+        if coff == 0 and y.shape[1] == c:
+            t[name] = y
+            return
+        if name not in t:
+            t[name] = torch.zeros((n_img, c, h, w), device=y.device, dtype=y.dtype)
+        t[name][:, coff:coff + y.shape[1]] = y
+
+
+@torch.no_grad()
+def calibrate_bn(g: Graph, w: Weights, x: torch.Tensor) -> Weights:
+    """Set every BN's mean/var to the batch statistics of its conv output on x
+    (data-dependent init), so activations stay normalised through the depth."""
+    w = dict(w)
+    ex = OracleExecutor(g, w)
+    p = ex.p
+    n_img = x.shape[0]
+    t = {g.input: x.float()}
+    for n in g.nodes:
+        if isinstance(n, Conv):
+            src = t[n.inp][:, n.in_coff:n.in_coff + n.cin]
+            k = p[f"{n.name}/kernel"].permute(3, 2, 0, 1)
+            y = F.conv2d(src, k, p.get(f"{n.name}/bias"), stride=(n.sh, n.sw), padding=(n.ph, n.pw))
+            if n.bn:
+                mean = y.mean(dim=(0, 2, 3))
+                var = y.var(dim=(0, 2, 3), unbiased=False)
+                w[f"{n.name}/mean"] = mean.numpy().astype(np.float32)
+                w[f"{n.name}/var"] = var.numpy().astype(np.float32)
+                p[f"{n.name}/mean"], p[f"{n.name}/var"] = mean, var
+                y = ex._bn(n, y)
+            if n.residual:
+                y = y + t[n.residual]
+            if n.relu:
+                y = F.relu(y)
+            ex._write(t, n.out, y, n.out_coff, n_img)
+        elif isinstance(n, Pool):
+            src = t[n.inp]
+            if n.mode == "max":
+                y = F.max_pool2d(F.pad(src, (n.pad,) * 4), n.k, n.stride)
+            else:
+                y = F.avg_pool2d(src, n.k, n.stride, padding=n.pad, count_include_pad=False)
+            ex._write(t, n.out, y, n.out_coff, n_img)
+        elif isinstance(n, GlobalAvgPool):
+            t[n.out] = t[n.inp].mean(dim=(2, 3), keepdim=True)
+        elif isinstance(n, Dense):
+            t[n.out] = t[n.inp].flatten(1) @ p[f"{n.name}/kernel"] + p[f"{n.name}/bias"]
+    return w

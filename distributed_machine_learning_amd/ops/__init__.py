@@ -1,0 +1,105 @@
+"""Functional wrappers over the hand-written gfx950 kernels (csrc/kernels/).
+
+Each op takes/returns torch tensors on the HIP device and launches exactly one
+native kernel on the current stream. There is NO PyTorch fallback: if the native
+library is missing these raise (tests on the GPU box therefore prove the HIP
+path ran). CPU-side fp32 oracles for each op live in ``ops.reference``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native as N
+
+__all__ = ["conv2d_nhwc", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight"]
+
+
+def _r(x, m):
+    return (x + m - 1) // m * m
+
+
+def pack_weight(w_oihw: torch.Tensor, cin_eff: Optional[int] = None) -> Tuple[torch.Tensor, int, int]:
+    """OIHW fp32 -> bf16 [Cout_pad][K_pad] in (r, s, c) order. Returns (w, K, Kpad)."""
+    co, ci, kh, kw = w_oihw.shape
+    cin_eff = cin_eff or _r(ci, 8)
+    k = torch.zeros((co, kh, kw, cin_eff), dtype=torch.float32)
+    k[..., :ci] = w_oihw.permute(0, 2, 3, 1).float().cpu()
+    K = kh * kw * cin_eff
+    out = torch.zeros((_r(co, 128), _r(K, 64)), dtype=torch.float32)
+    out[:co, :K] = k.reshape(co, K)
+    return out.to(torch.bfloat16), K, _r(K, 64)
+
+
+def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cout: int, kh: int, kw: int,
+                stride=(1, 1), pad=(0, 0), relu: bool = False, residual: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None, out_coff: int = 0, in_coff: int = 0, cin: Optional[int] = None,
+                out_f32: bool = False, cfg: int = -1, K: Optional[int] = None) -> torch.Tensor:
+    """x: NHWC bf16 [N,H,W,Cbuf] (Cbuf % 8 == 0). Returns/updates NHWC output."""
+    n, h, w_, cbuf = x.shape
+    cin = cin if cin is not None else cbuf - in_coff
+    ho = (h + 2 * pad[0] - kh) // stride[0] + 1
+    wo = (w_ + 2 * pad[1] - kw) // stride[1] + 1
+    if out is None:
+        out = torch.empty((n, ho, wo, _r(cout, 8)), device=x.device,
+                          dtype=torch.float32 if out_f32 else torch.bfloat16)
+    assert out.is_contiguous() and x.is_contiguous()
+    kpad = w_packed.shape[1]
+    K = K if K is not None else kh * kw * cin
+    bias_p = torch.zeros(w_packed.shape[0], device=x.device, dtype=torch.float32)
+    bias_p[: bias.numel()] = bias.to(x.device, torch.float32)
+    esz = out.element_size()
+    a = N.ConvArgs(x.data_ptr() + 2 * in_coff, w_packed.data_ptr(), bias_p.data_ptr(),
+                   residual.data_ptr() if residual is not None else None, out.data_ptr() + esz * out_coff,
+                   n, h, w_, cin, cbuf, kh, kw, stride[0], stride[1], pad[0], pad[1], ho, wo, cout, K, kpad,
+                   out.shape[-1], residual.shape[-1] if residual is not None else 0, int(relu), int(out_f32))
+    L = N.lib()
+    if cfg < 0:
+        cfg = L.dml_conv_pick_cfg(C.byref(a))
+    N.check(L.dml_conv(C.byref(a), cfg, N.stream_ptr()), "dml_conv")
+    out._keep = bias_p  # keep alive until the kernel ran (caller syncs)
+    return out
+
+
+def pool3x3(x: torch.Tensor, mode: str, k: int = 3, stride: int = 2, pad: int = 0,
+            out: Optional[torch.Tensor] = None, out_coff: int = 0) -> torch.Tensor:
+    n, h, w, c = x.shape
+    ho = (h + 2 * pad - k) // stride + 1
+    wo = (w + 2 * pad - k) // stride + 1
+    if out is None:
+        out = torch.empty((n, ho, wo, c), device=x.device, dtype=torch.bfloat16)
+    a = N.PoolArgs(x.data_ptr(), out.data_ptr() + 2 * out_coff, n, h, w, c, c, ho, wo, out.shape[-1], k, stride, pad,
+                   0 if mode == "max" else 1)
+    N.check(N.lib().dml_pool(C.byref(a), N.stream_ptr()), "dml_pool")
+    return out
+
+
+def global_avgpool(x: torch.Tensor) -> torch.Tensor:
+    n, h, w, c = x.shape
+    out = torch.empty((n, c), device=x.device, dtype=torch.bfloat16)
+    N.check(N.lib().dml_global_avgpool(x.data_ptr(), out.data_ptr(), n, h * w, c, c, N.stream_ptr()), "gap")
+    return out
+
+
+def softmax_top5(logits: torch.Tensor, want_probs: bool = True):
+    b, classes = logits.shape
+    logits = logits.contiguous().float()
+    probs = torch.empty_like(logits) if want_probs else None
+    idx = torch.empty((b, 5), device=logits.device, dtype=torch.int32)
+    p = torch.empty((b, 5), device=logits.device, dtype=torch.float32)
+    N.check(N.lib().dml_softmax_top5(logits.data_ptr(), b, classes, classes,
+                                     probs.data_ptr() if probs is not None else None, idx.data_ptr(), p.data_ptr(),
+                                     N.stream_ptr()), "softmax_top5")
+    return probs, idx, p
+
+
+def preprocess(images_u8: torch.Tensor, out_hw, mode: str) -> torch.Tensor:
+    n, hs, ws, _ = images_u8.shape
+    out = torch.empty((n, out_hw[0], out_hw[1], 8), device=images_u8.device, dtype=torch.bfloat16)
+    a = N.PreprocArgs(images_u8.data_ptr(), out.data_ptr(), n, hs, ws, out_hw[0], out_hw[1],
+                      0 if mode == "caffe" else 1)
+    N.check(N.lib().dml_preprocess(C.byref(a), N.stream_ptr()), "preprocess")
+    return out

@@ -1,0 +1,119 @@
+"""The per-GPU serving pipeline: dispatch -> stage -> compute -> gather.
+
+Used by bench.py and by the GPU worker runtime. Three HIP streams per rank:
+
+  copy stream     hipMemcpyAsync of batch k+1 (pinned host arena -> HBM slot)
+  compute stream  preprocess + forward + softmax/top-5 of batch k (one hipGraph)
+  dispatch stream RCCL broadcast of the descriptor table for batch k+1
+
+so staging and dispatch of the next batch hide under the current batch's
+compute, and the coordinator (rank 0) consumes batch k-1's gathered results
+while batch k runs. Reference equivalent: worker.py:1361-1386 (sequential scp
+download of each image, then a fresh ProcessPoolExecutor + model per batch).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional
+
+import numpy as np
+import torch
+
+from .dataplane import DataPlane, F_COUNT, F_START
+from .staging import PinnedImageStore
+
+
+@dataclass
+class BatchRecord:
+    step: int
+    t_dispatch: float
+    t_done: float = 0.0
+    results: Optional[List[torch.Tensor]] = None  # rank 0 only (host copies)
+
+
+@dataclass
+class PipelineStats:
+    latencies_s: List[float] = field(default_factory=list)
+    images: int = 0
+
+    def percentiles(self):
+        if not self.latencies_s:
+            return {}
+        a = np.asarray(self.latencies_s) * 1e3
+        return {"p50_ms": float(np.percentile(a, 50)), "p90_ms": float(np.percentile(a, 90)),
+                "p99_ms": float(np.percentile(a, 99)), "mean_ms": float(a.mean())}
+
+
+class ServingPipeline:
+    def __init__(self, engine, store: PinnedImageStore, dp: DataPlane, use_graph: bool = True,
+                 on_results: Optional[Callable[[BatchRecord], None]] = None):
+        assert engine.src_slots >= 2, "engine needs 2 source slots for double buffering"
+        self.eng, self.store, self.dp = engine, store, dp
+        self.use_graph = use_graph
+        self.on_results = on_results
+        dev = engine.device
+        self.copy_stream = torch.cuda.Stream(dev)
+        self.compute_stream = torch.cuda.Stream(dev)
+        self.ev_copied = [torch.cuda.Event() for _ in range(2)]
+        self.ev_consumed = [torch.cuda.Event() for _ in range(2)]
+        self.ev_res = [torch.cuda.Event() for _ in range(2)]
+        B = engine.batch
+        self.host_res = [torch.empty((dp.world, 2, B, 5), dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        self.stats = PipelineStats()
+
+    def _stage(self, step: int, row: np.ndarray) -> None:
+        slot = step % 2
+        cs = self.copy_stream
+        cs.wait_event(self.ev_consumed[slot])  # WAR: compute(step-2) finished reading this slot
+        count = int(row[F_COUNT])
+        self.store.h2d(self.eng.srcs[slot], int(row[F_START]), count, cs)
+        self.ev_copied[slot].record(cs)
+
+    def run(self, steps: int, table_fn: Callable[[int], np.ndarray], record: bool = True) -> PipelineStats:
+        """Serve `steps` batches; table_fn(k) -> descriptor table (used on rank 0)."""
+        dp, eng = self.dp, self.eng
+        is0 = dp.rank == 0
+        recs: List[BatchRecord] = []
+        t0 = time.perf_counter()
+        recs.append(BatchRecord(0, t0))
+        row = dp.dispatch(table_fn(0) if is0 else None)
+        self._stage(0, row)
+        prev: Optional[BatchRecord] = None
+        for k in range(steps):
+            slot = k % 2
+            cs = self.compute_stream
+            cs.wait_event(self.ev_copied[slot])
+            with torch.cuda.stream(cs):
+                eng.run(cs, use_graph=self.use_graph, slot=slot)
+            self.ev_consumed[slot].record(cs)
+            if k + 1 < steps:  # dispatch + stage the next batch while this one computes
+                recs.append(BatchRecord(k + 1, time.perf_counter()))
+                row = dp.dispatch(table_fn(k + 1) if is0 else None)
+                self._stage(k + 1, row)
+            with torch.cuda.stream(cs):
+                bufs = dp.gather(eng.result)
+                if is0:
+                    hr = self.host_res[slot]
+                    for r, b in enumerate(bufs):
+                        hr[r].copy_(b, non_blocking=True)
+                    self.ev_res[slot].record(cs)
+            if prev is not None:
+                self._finish(prev, record)
+            prev = recs[k]
+        if prev is not None:
+            self._finish(prev, record)
+        self.compute_stream.synchronize()
+        return self.stats
+
+    def _finish(self, rec: BatchRecord, record: bool) -> None:
+        slot = rec.step % 2
+        if self.dp.rank == 0:
+            self.ev_res[slot].synchronize()
+            rec.t_done = time.perf_counter()
+            if record:
+                self.stats.latencies_s.append(rec.t_done - rec.t_dispatch)
+                self.stats.images += self.dp.world * self.eng.batch
+            if self.on_results is not None:
+                rec.results = [self.host_res[slot][r].clone() for r in range(self.dp.world)]
+                self.on_results(rec)

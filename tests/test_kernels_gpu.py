@@ -1,0 +1,167 @@
+"""Numerics of every hand-written gfx950 kernel against a plain-PyTorch fp32
+reference of the same op (inputs pre-rounded to bf16 so only the kernel's
+accumulation/rounding differs). Shapes cover every conv class of SURVEY §2.7:
+1x1 s1/s2, 3x3, 5x5, 7x7/2 stem (Cin padded 3->8), 1x7 / 7x1 / 1x3 / 3x1,
+Cin=80 (K-tile straddles taps), channel-offset concat stores, residual+ReLU,
+fp32 output (FC)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from distributed_machine_learning_amd import ops  # noqa: E402
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def _rel(a, b):
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+CONV_CASES = [
+    # n, h, w, cin, cout, kh, kw, stride, pad, relu, residual
+    (2, 14, 14, 64, 64, 1, 1, 1, 0, True, False),
+    (2, 14, 14, 256, 128, 1, 1, 2, 0, True, False),
+    (2, 28, 28, 64, 256, 1, 1, 1, 0, True, True),
+    (2, 9, 11, 64, 96, 3, 3, 1, 1, True, False),
+    (1, 35, 35, 48, 64, 5, 5, 1, 2, True, False),
+    (2, 17, 17, 128, 192, 1, 7, 1, 0, True, False),
+    (2, 17, 17, 128, 192, 7, 1, 1, 0, True, False),
+    (2, 8, 8, 384, 384, 1, 3, 1, 0, True, False),
+    (2, 8, 8, 384, 384, 3, 1, 1, 0, True, False),
+    (1, 73, 73, 80, 192, 3, 3, 1, 0, True, False),
+    (2, 35, 35, 288, 384, 3, 3, 2, 0, True, False),
+    (2, 7, 7, 512, 2048, 1, 1, 1, 0, False, True),
+]
+
+
+def _pads(kh, kw, pad):
+    return (pad if kh > 1 else 0, pad if kw > 1 else 0) if pad else (0, 0)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4])
+def test_conv_matches_fp32(case, cfg):
+    n, h, w, cin, cout, kh, kw, s, pad, relu, has_res = case
+    ph, pw = (kh // 2, kw // 2) if pad else (0, 0)
+    torch.manual_seed(0)
+    x = _bf(torch.randn(n, cin, h, w))
+    wt = _bf(torch.randn(cout, cin, kh, kw) * (2.0 / (cin * kh * kw)) ** 0.5)
+    b = torch.randn(cout) * 0.1
+    ref = F.conv2d(x, wt, b, stride=s, padding=(ph, pw))
+    res = None
+    if has_res:
+        res = _bf(torch.randn_like(ref))
+        ref = ref + res
+    if relu:
+        ref = F.relu(ref)
+    wp, K, _ = ops.pack_weight(wt)
+    xd = x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
+    rd = res.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16) if res is not None else None
+    y = ops.conv2d_nhwc(xd, wp.cuda(), b.cuda(), cout, kh, kw, (s, s), (ph, pw), relu=relu, residual=rd, cfg=cfg)
+    torch.cuda.synchronize()
+    got = y[..., :cout].float().cpu().permute(0, 3, 1, 2)
+    assert got.shape == ref.shape
+    assert _rel(got, ref) < 1.5e-2, _rel(got, ref)
+
+
+def test_conv_stem_padded_input():
+    """7x7/2 stem on a 3-channel image stored as 8 channels (zeros in 3..7)."""
+    torch.manual_seed(1)
+    x = _bf(torch.randn(2, 3, 40, 40))
+    wt = _bf(torch.randn(64, 3, 7, 7) * 0.1)
+    b = torch.randn(64) * 0.1
+    ref = F.relu(F.conv2d(x, wt, b, stride=2, padding=3))
+    x8 = torch.zeros(2, 40, 40, 8)
+    x8[..., :3] = x.permute(0, 2, 3, 1)
+    wp, K, _ = ops.pack_weight(wt, cin_eff=8)
+    y = ops.conv2d_nhwc(x8.cuda().to(torch.bfloat16), wp.cuda(), b.cuda(), 64, 7, 7, (2, 2), (3, 3), relu=True)
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu().permute(0, 3, 1, 2), ref) < 1.5e-2
+
+
+def test_conv_channel_offsets_concat():
+    """Two convs writing disjoint channel ranges of one buffer + reading a slice."""
+    torch.manual_seed(2)
+    x = _bf(torch.randn(2, 96, 9, 9))
+    w1 = _bf(torch.randn(32, 64, 1, 1) * 0.1)
+    w2 = _bf(torch.randn(48, 32, 3, 3) * 0.1)
+    b1, b2 = torch.randn(32) * 0.1, torch.randn(48) * 0.1
+    xd = x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
+    out = torch.full((2, 9, 9, 96), 7.0, device="cuda", dtype=torch.bfloat16)
+    wp1, _, _ = ops.pack_weight(w1)
+    wp2, _, _ = ops.pack_weight(w2)
+    # conv1 reads channels [32:96) of x, writes channels [16:48) of out
+    ops.conv2d_nhwc(xd, wp1.cuda(), b1.cuda(), 32, 1, 1, in_coff=32, cin=64, out=out, out_coff=16, relu=True)
+    # conv2 reads channels [16:48) of out, writes channels [48:96) of out
+    ops.conv2d_nhwc(out, wp2.cuda(), b2.cuda(), 48, 3, 3, pad=(1, 1), in_coff=16, cin=32, out=out, out_coff=48,
+                    relu=True)
+    torch.cuda.synchronize()
+    r1 = F.relu(F.conv2d(x[:, 32:96], w1, b1))
+    got = out.float().cpu().permute(0, 3, 1, 2)
+    assert _rel(got[:, 16:48], r1) < 1.5e-2
+    r2 = F.relu(F.conv2d(_bf(got[:, 16:48]), w2, b2, padding=1))
+    assert _rel(got[:, 48:96], r2) < 1.5e-2
+    assert torch.all(got[:, :16] == 7.0)
+
+
+def test_fc_fp32_out():
+    torch.manual_seed(3)
+    x = _bf(torch.randn(5, 2048))
+    wt = _bf(torch.randn(1000, 2048) * 0.02)
+    b = torch.randn(1000) * 0.1
+    ref = x @ wt.t() + b
+    wp, K, _ = ops.pack_weight(wt[:, :, None, None])
+    y = ops.conv2d_nhwc(x.view(5, 1, 1, 2048).cuda().to(torch.bfloat16), wp.cuda(), b.cuda(), 1000, 1, 1,
+                        out_f32=True)
+    torch.cuda.synchronize()
+    assert _rel(y.view(5, -1)[:, :1000].cpu(), ref) < 5e-3
+
+
+@pytest.mark.parametrize("mode,k,s,pad", [("max", 3, 2, 0), ("max", 3, 2, 1), ("avg", 3, 1, 1)])
+def test_pool(mode, k, s, pad):
+    torch.manual_seed(4)
+    x = _bf(torch.relu(torch.randn(2, 32, 17, 19)))
+    if mode == "max":
+        ref = F.max_pool2d(F.pad(x, (pad,) * 4), k, s)
+    else:
+        ref = F.avg_pool2d(x, k, s, padding=pad, count_include_pad=False)
+    y = ops.pool3x3(x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16), mode, k, s, pad)
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu().permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_global_avgpool():
+    x = _bf(torch.randn(3, 7, 7, 2048))
+    y = ops.global_avgpool(x.cuda().to(torch.bfloat16))
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu(), x.mean(dim=(1, 2))) < 1e-2
+
+
+def test_softmax_top5():
+    torch.manual_seed(5)
+    logits = torch.randn(37, 1000) * 3
+    probs, idx, p = ops.softmax_top5(logits.cuda())
+    torch.cuda.synchronize()
+    ref = torch.softmax(logits, -1)
+    assert torch.allclose(probs.cpu(), ref, atol=1e-6, rtol=1e-4)
+    rv, ri = ref.topk(5, dim=-1)
+    assert torch.equal(idx.cpu().long(), ri)
+    assert torch.allclose(p.cpu(), rv, atol=1e-6, rtol=1e-4)
+
+
+@pytest.mark.parametrize("mode,hw", [("caffe", (224, 224)), ("tf", (299, 299))])
+def test_preprocess(mode, hw):
+    from distributed_machine_learning_amd.models.oracle import preprocess_reference
+
+    torch.manual_seed(6)
+    img = torch.randint(0, 256, (3, 300, 241, 3), dtype=torch.uint8)
+    y = ops.preprocess(img.cuda(), hw, mode)
+    torch.cuda.synchronize()
+    ref = preprocess_reference(img, hw, mode)
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    assert torch.all(got[:, 3:] == 0)
+    assert (got[:, :3] - ref).abs().max().item() < 0.6  # bf16 rounding of values up to ~150

@@ -1,0 +1,94 @@
+"""CPU tests of the model IR, weights and oracle (no GPU)."""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from distributed_machine_learning_amd.models import build_graph, build_model
+from distributed_machine_learning_amd.models.graph import Conv
+from distributed_machine_learning_amd.models.oracle import OracleExecutor, preprocess_reference
+from distributed_machine_learning_amd.models.weights import fold_conv, init_weights, load_weights, save_weights
+from distributed_machine_learning_amd.models.engine import pack_conv_weight
+
+
+def test_param_counts_match_keras():
+    # Keras model.count_params() for the two applications models
+    assert build_graph("ResNet50").param_count() == 25_636_712
+    assert build_graph("InceptionV3").param_count() == 23_851_784
+
+
+def test_graph_shapes():
+    r = build_graph("ResNet50")
+    assert len(r.conv_nodes()) == 53
+    assert r.shape("conv5_block3_out") == (7, 7, 2048)
+    i = build_graph("InceptionV3")
+    assert len(i.conv_nodes()) == 94
+    assert i.shape("mixed10") == (8, 8, 2048)
+    assert i.shape("mixed7") == (17, 17, 768)
+    assert i.shape("mixed2") == (35, 35, 288)
+
+
+def test_bn_folding_equivalence():
+    g = build_graph("ResNet50")
+    w = init_weights(g, seed=3)
+    n = next(x for x in g.conv_nodes() if x.kh == 3)
+    x = torch.randn(2, n.cin, 9, 9)
+    ex = OracleExecutor(g, w)
+    k = torch.from_numpy(w[f"{n.name}/kernel"]).permute(3, 2, 0, 1)
+    y = F.conv2d(x, k, torch.from_numpy(w[f"{n.name}/bias"]), padding=1)
+    ref = ex._bn(n, y)
+    kf, bf = fold_conv(n, w)
+    got = F.conv2d(x, torch.from_numpy(kf).permute(3, 2, 0, 1), torch.from_numpy(bf), padding=1)
+    assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4)
+
+
+def test_pack_conv_weight_order():
+    k = np.arange(3 * 3 * 5 * 4, dtype=np.float32).reshape(3, 3, 5, 4)  # HWIO
+    p = pack_conv_weight(k, 8, 128, 128)
+    # row = cout, col = (r*kw + s)*cin_eff + c
+    assert p[2, (1 * 3 + 2) * 8 + 4] == k[1, 2, 4, 2]
+    assert p[2, (1 * 3 + 2) * 8 + 5] == 0  # padded channel
+    assert p[4:].sum() == 0
+
+
+def test_weights_roundtrip(tmp_path):
+    g = build_graph("InceptionV3")
+    w = init_weights(g, seed=1)
+    path = str(tmp_path / "w.safetensors")
+    save_weights(path, w)
+    w2 = load_weights(path)
+    assert set(w) == set(w2)
+    assert all(np.array_equal(w[k], w2[k]) for k in w)
+
+
+def test_preprocess_reference_modes():
+    img = torch.zeros(1, 4, 4, 3, dtype=torch.uint8)
+    img[..., 0] = 200  # R
+    c = preprocess_reference(img, (2, 2), "caffe")
+    assert torch.allclose(c[0, 2], torch.full((2, 2), 200 - 123.68))  # R lands in channel 2 (BGR)
+    assert torch.allclose(c[0, 0], torch.full((2, 2), -103.939))
+    t = preprocess_reference(img, (2, 2), "tf")
+    assert torch.allclose(t[0, 0], torch.full((2, 2), 200 / 127.5 - 1))
+
+
+def test_oracle_forward_and_calibration():
+    g, w = build_model("ResNet50", seed=0, calibrate=True)
+    imgs = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8)
+    out = OracleExecutor(g, w).forward(preprocess_reference(imgs, g.input_hw, g.preprocess), keep=True)
+    assert out["probs"].shape == (2, 1000)
+    assert torch.allclose(out["probs"].sum(-1), torch.ones(2), atol=1e-5)
+    # calibrated BN keeps activations O(1) deep in the net
+    assert 0.05 < out["conv5_block3_out"].std().item() < 20
+
+
+def test_inception_concat_offsets():
+    g = build_graph("InceptionV3")
+    writers = {}
+    for n in g.nodes:
+        if getattr(n, "out", "").startswith("mixed") and "_" not in n.out:
+            cout = n.cout if isinstance(n, Conv) else g.shape(n.inp)[2]
+            writers.setdefault(n.out, []).append((n.out_coff, n.out_coff + cout))
+    for name, ranges in writers.items():
+        ranges.sort()
+        assert ranges[0][0] == 0 and ranges[-1][1] == g.shape(name)[2], name
+        for (a0, a1), (b0, b1) in zip(ranges, ranges[1:]):
+            assert a1 == b0, (name, ranges)
