@@ -44,9 +44,10 @@ class Engine:
 
     def __init__(self, graph: Graph, weights: Weights, batch: int, device: str = "cuda",
                  src_hw: Optional[Tuple[int, int]] = None, cfg_overrides: Optional[Dict[str, int]] = None,
-                 src_slots: int = 1):
+                 src_slots: int = 1, reuse_buffers: bool = True):
         self.g, self.batch, self.device = graph, batch, torch.device(device)
         self.src_slots = src_slots
+        self.reuse_buffers = reuse_buffers
         self.lib = N.lib()
         self.src_hw = src_hw or graph.input_hw
         self.cfg_overrides = cfg_overrides or {}
@@ -105,7 +106,7 @@ class Engine:
         idx = 0
         for step in range(-1, len(nodes) + 1):
             # tensors whose last use was before this step can be recycled
-            for name in pending_release:
+            for name in pending_release if self.reuse_buffers else []:
                 t = self.buf[name]
                 free.setdefault(t.numel(), []).append(t)
             pending_release = release_at.get(step, [])

@@ -34,10 +34,31 @@ def preprocess_reference(images_u8: torch.Tensor, out_hw, mode: str) -> torch.Te
     return x.permute(0, 3, 1, 2).contiguous()
 
 
+def _bf16(x: torch.Tensor) -> torch.Tensor:
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
 class OracleExecutor:
-    def __init__(self, g: Graph, w: Weights, device="cpu", dtype=torch.float32):
+    """fp32 reference. With ``emulate_bf16=True`` it reproduces the engine's
+    rounding points instead (BN folded, weights and every stored activation
+    rounded to bf16, fp32 accumulation) — the tight reference for whole-network
+    tests, since random-init deep nets amplify bf16 rounding chaotically."""
+
+    def __init__(self, g: Graph, w: Weights, device="cpu", dtype=torch.float32, emulate_bf16: bool = False):
         self.g, self.device, self.dtype = g, device, dtype
+        self.emulate = emulate_bf16
         self.p = {k: torch.from_numpy(np.ascontiguousarray(v)).to(device, dtype) for k, v in w.items()}
+        if emulate_bf16:
+            from .weights import fold_conv
+
+            self.folded = {}
+            for n in g.nodes:
+                if isinstance(n, Conv):
+                    k, b = fold_conv(n, w)
+                    self.folded[n.name] = (_bf16(torch.from_numpy(k).permute(3, 2, 0, 1).to(device, dtype)),
+                                           torch.from_numpy(b).to(device, dtype))
+                elif isinstance(n, Dense):
+                    self.folded[n.name] = (_bf16(self.p[f"{n.name}/kernel"]), self.p[f"{n.name}/bias"])
 
     def _bn(self, n: Conv, y: torch.Tensor) -> torch.Tensor:
         p = self.p
@@ -53,30 +74,40 @@ class OracleExecutor:
         """x: preprocessed NCHW fp32. Returns tensors dict (logits, probs, and all if keep)."""
         g, p = self.g, self.p
         n_img = x.shape[0]
-        t: Dict[str, torch.Tensor] = {g.input: x.to(self.device, self.dtype)}
+        em = self.emulate
+        rnd = _bf16 if em else (lambda v: v)
+        t: Dict[str, torch.Tensor] = {g.input: rnd(x.to(self.device, self.dtype))}
         for n in g.nodes:
             if isinstance(n, Conv):
                 src = t[n.inp][:, n.in_coff:n.in_coff + n.cin]
-                k = p[f"{n.name}/kernel"].permute(3, 2, 0, 1)  # HWIO -> OIHW
-                y = F.conv2d(src, k, p.get(f"{n.name}/bias"), stride=(n.sh, n.sw), padding=(n.ph, n.pw))
-                if n.bn:
-                    y = self._bn(n, y)
+                if em:
+                    k, b = self.folded[n.name]
+                    y = F.conv2d(src, k, b, stride=(n.sh, n.sw), padding=(n.ph, n.pw))
+                else:
+                    k = p[f"{n.name}/kernel"].permute(3, 2, 0, 1)  # HWIO -> OIHW
+                    y = F.conv2d(src, k, p.get(f"{n.name}/bias"), stride=(n.sh, n.sw), padding=(n.ph, n.pw))
+                    if n.bn:
+                        y = self._bn(n, y)
                 if n.residual:
                     y = y + t[n.residual]
                 if n.relu:
                     y = F.relu(y)
-                self._write(t, n.out, y, n.out_coff, n_img)
+                self._write(t, n.out, rnd(y), n.out_coff, n_img)
             elif isinstance(n, Pool):
                 src = t[n.inp]
                 if n.mode == "max":
                     y = F.max_pool2d(F.pad(src, (n.pad,) * 4), n.k, n.stride)  # Keras ZeroPadding2D + valid pool
                 else:
                     y = F.avg_pool2d(src, n.k, n.stride, padding=n.pad, count_include_pad=False)
-                self._write(t, n.out, y, n.out_coff, n_img)
+                self._write(t, n.out, rnd(y), n.out_coff, n_img)
             elif isinstance(n, GlobalAvgPool):
-                t[n.out] = t[n.inp].mean(dim=(2, 3), keepdim=True)
+                t[n.out] = rnd(t[n.inp].mean(dim=(2, 3), keepdim=True))
             elif isinstance(n, Dense):
-                y = t[n.inp].flatten(1) @ p[f"{n.name}/kernel"] + p[f"{n.name}/bias"]
+                if em:
+                    k, b = self.folded[n.name]
+                    y = t[n.inp].flatten(1) @ k + b
+                else:
+                    y = t[n.inp].flatten(1) @ p[f"{n.name}/kernel"] + p[f"{n.name}/bias"]
                 t[n.out] = y
         out = {"logits": t[g.logits], "probs": torch.softmax(t[g.logits], dim=-1)}
         if keep:
