@@ -52,6 +52,8 @@ typedef struct {
 
 // ---- single-op launches (used by tests and by the plan executor) ----
 int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
+int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
+int dml_conv_v2_init(void);
 int dml_conv_pick_cfg(const DmlConvArgs* a);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);

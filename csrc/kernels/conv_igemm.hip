@@ -233,7 +233,16 @@ static int launch_conv(const DmlConvArgs* a, hipStream_t s) {
 //   2:  64 px x 128 ch x BK64   (small M, wide Cout)
 //   3: 128 px x 128 ch x BK32   (short K)
 //   4:  64 px x  64 ch x BK64   (tiny layers)
+extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
+
 extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
+  if (cfg >= 10) {
+    if (a->Cin % 8 || a->ldx % 8 || a->Cout % 8 || a->Kpad % 64 || a->ldy % 8 || (a->res && a->ldr % 8)) {
+      dml_set_error("dml_conv(v2): need Cin, ldx, Cout, ldy, ldr %8==0 and Kpad%64==0");
+      return -1;
+    }
+    return dml_conv_v2(a, cfg, s);
+  }
   if (a->Cin % 8 || a->ldx % 8 || a->Cout % 4 || a->Kpad % 64) {
     dml_set_error("dml_conv: need Cin%8==0, ldx%8==0, Cout%4==0, Kpad%64==0");
     return -1;
@@ -254,6 +263,12 @@ extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
 extern "C" int dml_conv_pick_cfg(const DmlConvArgs* a) {
   const long M = (long)a->N * a->Ho * a->Wo;
   const int C = a->Cout;
+  const bool v2ok = !(a->Cin % 8 || a->ldx % 8 || C % 8 || a->ldy % 8 || (a->res && a->ldr % 8));
+  if (v2ok) {  // measured defaults (tools/conv_bench.py); the engine autotunes per shape
+    if (C <= 64) return 15;
+    if (a->Kpad <= 512 || M < 16384) return 14;
+    return 11;
+  }
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((C + bn - 1) / bn); };
   if (C <= 64) return tiles(256, 64) >= 512 ? 1 : 4;
   if (tiles(128, 128) >= 512) return 0;

@@ -1,0 +1,272 @@
+// conv_igemm_v2.hip — LDS-DMA pipelined MFMA implicit-GEMM convolution (gfx950).
+//
+// Same contract as conv_igemm.hip (DmlConvArgs, transposed GEMM D[c][m] with
+// v_mfma_f32_16x16x32_bf16, channels on MFMA rows), re-built around the CDNA4
+// memory path:
+//
+//  * Operand tiles go global -> LDS by LDS-DMA (no VGPR round trip):
+//      activations: buffer_load_dwordx4 ... lds through a raw buffer descriptor.
+//        The implicit-im2col zero padding (out-of-image taps, K tail, M tail)
+//        is produced by the hardware range check: such lanes get an offset past
+//        num_records and the DMA writes zeros.
+//      weights:     global_load_lds_dwordx4.
+//    A wave-instruction writes 1 KiB = 8 tile rows of 128 B contiguously, so the
+//    bank-conflict swizzle (16-B chunk ^= row & 7) is applied on the SOURCE side:
+//    lane L always fetches logical chunk (L & 7) ^ (L >> 3) of its row.
+//  * STAGES-deep LDS ring with counted `s_waitcnt vmcnt(N)` + raw s_barrier —
+//    one barrier per 64-deep K tile, loads for tiles kt+1..kt+STAGES-2 stay in
+//    flight across it (never __syncthreads() in the loop: its fence would drain
+//    the DMA).
+//  * Epilogue staged through LDS: fp32 accumulators -> LDS -> each thread
+//    handles 8 consecutive output channels of one pixel: bias + residual (16-B
+//    coalesced load) + ReLU -> one 16-B coalesced NHWC store. Rows of a pixel
+//    are contiguous across 16 lanes, so stores/residual loads are full lines.
+//  * XCD-aware bijective block remap; channel tiles fastest so the blocks on
+//    one XCD share the activation rows in its L2.
+#include "common.h"
+#include "dml.h"
+
+namespace dml {
+namespace v2 {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES>
+struct Cfg {
+  static constexpr int NW = WM * WN;          // waves
+  static constexpr int NT = NW * 64;          // threads
+  static constexpr int WTP = BM / WM;         // pixels per wave
+  static constexpr int WTC = BN / WN;         // channels per wave
+  static constexpr int FJ = WTP / 16;         // fragments along pixels
+  static constexpr int FI = WTC / 16;         // fragments along channels
+  static constexpr int BK = 64;
+  static constexpr int ROWB = BK * 2;         // 128 B per tile row
+  static constexpr int XI = BM / 8 / NW;      // X DMA instructions per wave per K tile
+  static constexpr int WI = BN / 8 / NW;      // W DMA instructions per wave per K tile
+  static constexpr int L = XI + WI;           // vm ops per thread per K tile
+  static constexpr int STAGE_BYTES = (BM + BN) * ROWB;
+  static constexpr int PIPE_BYTES = STAGES * STAGE_BYTES;
+  static constexpr int CROW = BN * 4 + 16;    // epilogue fp32 row stride (+16 B pad)
+  static constexpr int EPI_BYTES = BM * CROW;
+  static constexpr int LDS = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
+  static_assert(XI >= 1 && WI >= 1, "each wave needs >=1 DMA instruction per operand");
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split evenly across waves");
+  static_assert(FI >= 1 && FJ >= 1, "wave tile too small");
+  static_assert((STAGES - 2) * L < 64, "vmcnt overflow");
+};
+
+__device__ __forceinline__ int lds_swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+template <int BM, int BN, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
+  using T = Cfg<BM, BN, WM, WN, STAGES>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int M = a.N * a.Ho * a.Wo;
+  const int ntc = (a.Cout + BN - 1) / BN;
+  const int Lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int tc = Lb % ntc, tm = Lb / ntc;
+  const int m0 = tm * BM, c0 = tc * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // ---- per-lane DMA bookkeeping ----
+  const int lrow = lane >> 3;                  // row within an 8-row DMA piece
+  const int lchunk = (lane & 7) ^ lrow;        // logical K chunk this lane always fetches
+  // X rows of this lane: piece q = wid*XI + j -> row 8q + lrow
+  int pix0[T::XI], ih0[T::XI], iw0[T::XI];
+  const int HoWo = a.Ho * a.Wo;
+#pragma unroll
+  for (int j = 0; j < T::XI; ++j) {
+    const int m = m0 + (wid * T::XI + j) * 8 + lrow;
+    if (m < M) {
+      const int n = m / HoWo;
+      const int rem = m - n * HoWo;
+      const int oh = rem / a.Wo;
+      const int ow = rem - oh * a.Wo;
+      pix0[j] = n * a.H * a.W;
+      ih0[j] = oh * a.sh - a.ph;
+      iw0[j] = ow * a.sw - a.pw;
+    } else {
+      pix0[j] = 0;
+      ih0[j] = -(1 << 28);
+      iw0[j] = 0;
+    }
+  }
+  int cc = lchunk * 8, ss = 0, rr = 0;
+  while (cc >= a.Cin) { cc -= a.Cin; if (++ss == a.kw) { ss = 0; ++rr; } }
+
+  // buffer descriptor over the activations (range check -> zero fill)
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, 0x7ffffff0, 0x00020000);
+  const unsigned OOB = 0x80000000u;
+  const char* wbase = (const char*)a.w + ((long)(c0 + wid * T::WI * 8 + lrow) * a.Kpad + lchunk * 8) * 2;
+  const long wstep_row = (long)8 * a.Kpad * 2;  // next 8-row piece
+
+  const int nk = a.Kpad / T::BK;
+
+  auto issue = [&](int kt, int stage) {
+    char* sx = smem + stage * T::STAGE_BYTES;
+    char* sw = sx + BM * T::ROWB;
+    const bool kval = rr < a.kh;
+#pragma unroll
+    for (int j = 0; j < T::XI; ++j) {
+      const int ih = ih0[j] + rr, iw = iw0[j] + ss;
+      const bool ok = kval && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const unsigned off = ok ? (unsigned)(((pix0[j] + ih * a.W + iw) * a.ldx + cc) * 2) : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < T::WI; ++j) {
+      const char* src = wbase + j * wstep_row + (long)kt * T::BK * 2;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sw + (wid * T::WI + j) * 1024), 16, 0, 0);
+    }
+    cc += T::BK;
+    while (cc >= a.Cin) { cc -= a.Cin; if (++ss == a.kw) { ss = 0; ++rr; } }
+  };
+
+  f32x4 acc[T::FI][T::FJ];
+#pragma unroll
+  for (int i = 0; i < T::FI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::FJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int wc = wid % WN, wp = wid / WN;
+  const int frow = lane & 15, fq = lane >> 4;
+
+  // prologue: tiles 0 .. STAGES-2 in flight
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire tile kt (leave the younger STAGES-2 tiles in flight), then barrier
+    if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * T::L>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    // refill the stage freed by tile kt-1 (every wave passed the barrier => done reading it)
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const char* sx = smem + (kt % STAGES) * T::STAGE_BYTES;
+    const char* sw = sx + BM * T::ROWB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 4 + fq;
+      bf16x8 fa[T::FI], fb[T::FJ];
+#pragma unroll
+      for (int i = 0; i < T::FI; ++i) fa[i] = *(const bf16x8*)(sw + lds_swz(wc * T::WTC + i * 16 + frow, ch));
+#pragma unroll
+      for (int j = 0; j < T::FJ; ++j) fb[j] = *(const bf16x8*)(sx + lds_swz(wp * T::WTP + j * 16 + frow, ch));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < T::FI; ++i)
+#pragma unroll
+        for (int j = 0; j < T::FJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  // ---- epilogue: acc -> LDS (fp32) -> coalesced bias/residual/ReLU/store ----
+  __syncthreads();  // all DMA retired (vmcnt(0) above) and all LDS reads done
+#pragma unroll
+  for (int i = 0; i < T::FI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::FJ; ++j) {
+      const int px = wp * T::WTP + j * 16 + frow;
+      const int ch = wc * T::WTC + i * 16 + fq * 4;
+      *(f32x4*)(smem + px * T::CROW + ch * 4) = acc[i][j];
+    }
+  __syncthreads();
+  constexpr int CG = BN / 8;  // 8-channel groups per pixel row
+  const unsigned short* __restrict__ rg = (const unsigned short*)a.res;
+  for (int e = tid; e < BM * CG; e += T::NT) {
+    const int px = e / CG, cg = e % CG;
+    const int m = m0 + px, ch = c0 + cg * 8;
+    if (m >= M || ch >= a.Cout) continue;
+    const float4 v0 = *(const float4*)(smem + px * T::CROW + cg * 32);
+    const float4 v1 = *(const float4*)(smem + px * T::CROW + cg * 32 + 16);
+    const float4 b0 = *(const float4*)(a.bias + ch);
+    const float4 b1 = *(const float4*)(a.bias + ch + 4);
+    float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
+                  v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
+    if (rg) {
+      const uint4 r = *(const uint4*)(rg + (long)m * a.ldr + ch);
+      f[0] += bf2f(r.x & 0xffff); f[1] += bf2f(r.x >> 16);
+      f[2] += bf2f(r.y & 0xffff); f[3] += bf2f(r.y >> 16);
+      f[4] += bf2f(r.z & 0xffff); f[5] += bf2f(r.z >> 16);
+      f[6] += bf2f(r.w & 0xffff); f[7] += bf2f(r.w >> 16);
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) f[q] = fmaxf(f[q], 0.f);
+    }
+    if (a.out_f32) {
+      float* yp = (float*)a.y + (long)m * a.ldy + ch;
+      *(float4*)yp = make_float4(f[0], f[1], f[2], f[3]);
+      *(float4*)(yp + 4) = make_float4(f[4], f[5], f[6], f[7]);
+    } else {
+      *(uint4*)((unsigned short*)a.y + (long)m * a.ldy + ch) =
+          make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES>
+static int launch(const DmlConvArgs* a, hipStream_t s) {
+  using T = Cfg<BM, BN, WM, WN, STAGES>;
+  const long M = (long)a->N * a->Ho * a->Wo;
+  const long tiles = ((M + BM - 1) / BM) * ((a->Cout + BN - 1) / BN);
+  hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES>), dim3((unsigned)tiles), dim3(T::NT), T::LDS, s, *a);
+  DML_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES>
+static int set_attr() {
+  using T = Cfg<BM, BN, WM, WN, STAGES>;
+  return (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
+}
+
+}  // namespace v2
+}  // namespace dml
+
+// Raise the dynamic-LDS limit of every v2 instantiation once (before any
+// launch or graph capture). Called by the Python loader.
+extern "C" int dml_conv_v2_init(void) {
+  using namespace dml::v2;
+  int rc = 0;
+  rc |= set_attr<256, 128, 4, 2, 3>();
+  rc |= set_attr<128, 128, 2, 2, 2>();
+  rc |= set_attr<256, 64, 4, 1, 2>();
+  rc |= set_attr<128, 256, 2, 4, 3>();
+  rc |= set_attr<64, 128, 1, 4, 2>();
+  rc |= set_attr<128, 64, 2, 2, 2>();
+  rc |= set_attr<256, 128, 4, 2, 2>();
+  rc |= set_attr<128, 128, 2, 2, 3>();
+  if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  return rc ? -1 : 0;
+}
+
+// v2 configurations (ids >= 10; see dml_conv in conv_igemm.hip for dispatch)
+extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
+  using namespace dml::v2;
+  switch (cfg) {
+    case 10: return launch<256, 128, 4, 2, 3>(a, s);  // 8 waves, 64x64 per wave
+    case 11: return launch<128, 128, 2, 2, 2>(a, s);  // 4 waves, 64x64 per wave, 2 blocks/CU
+    case 12: return launch<256, 64, 4, 1, 2>(a, s);   // 4 waves, 64x64 per wave
+    case 13: return launch<128, 256, 2, 4, 3>(a, s);  // 8 waves, 64x64 per wave
+    case 14: return launch<64, 128, 1, 4, 2>(a, s);   // 4 waves, 64px x 32ch per wave
+    case 15: return launch<128, 64, 2, 2, 2>(a, s);   // 4 waves, 64px x 32ch per wave
+    case 16: return launch<256, 128, 4, 2, 2>(a, s);  // 8 waves, 2-stage
+    case 17: return launch<128, 128, 2, 2, 3>(a, s);  // 4 waves, 3-stage
+    default: dml_set_error("dml_conv_v2: bad cfg"); return -1;
+  }
+}

@@ -24,6 +24,7 @@ ARCH = os.environ.get("DML_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [
     CSRC / "kernels" / "conv_igemm.hip",
+    CSRC / "kernels" / "conv_igemm_v2.hip",
     CSRC / "kernels" / "misc.hip",
     CSRC / "runtime" / "runtime.hip",
 ]

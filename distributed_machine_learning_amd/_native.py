@@ -47,6 +47,7 @@ class PreprocArgs(C.Structure):
 _SIGS = {
     "dml_conv": (C.c_int, [C.POINTER(ConvArgs), C.c_int, C.c_void_p]),
     "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),
+    "dml_conv_v2_init": (C.c_int, []),
     "dml_pool": (C.c_int, [C.POINTER(PoolArgs), C.c_void_p]),
     "dml_global_avgpool": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "dml_softmax_top5": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -113,6 +114,17 @@ def lib():
         return _lib
 
 
+_inited = False
+
+
+def ensure_device_init() -> None:
+    """Per-process device-side setup (kernel attributes); call before launching."""
+    global _inited
+    if not _inited:
+        check(lib().dml_conv_v2_init(), "dml_conv_v2_init")
+        _inited = True
+
+
 def check(rc: int, what: str) -> int:
     if rc != 0 and rc is not None and not (isinstance(rc, int) and rc > 0):
         msg = lib().dml_last_error().decode(errors="replace")
@@ -123,6 +135,7 @@ def check(rc: int, what: str) -> int:
 def stream_ptr(stream=None) -> int:
     import torch
 
+    ensure_device_init()
     s = stream if stream is not None else torch.cuda.current_stream()
     return int(s.cuda_stream)
 

@@ -44,10 +44,11 @@ class Engine:
 
     def __init__(self, graph: Graph, weights: Weights, batch: int, device: str = "cuda",
                  src_hw: Optional[Tuple[int, int]] = None, cfg_overrides: Optional[Dict[str, int]] = None,
-                 src_slots: int = 1, reuse_buffers: bool = True):
+                 src_slots: int = 1, reuse_buffers: bool = True, autotune: bool = True):
         self.g, self.batch, self.device = graph, batch, torch.device(device)
         self.src_slots = src_slots
         self.reuse_buffers = reuse_buffers
+        self.autotune = autotune
         self.lib = N.lib()
         self.src_hw = src_hw or graph.input_hw
         self.cfg_overrides = cfg_overrides or {}
@@ -64,14 +65,14 @@ class Engine:
                 k, b = fold_conv(n, w)
                 cin_eff = _r(n.cin, 8)
                 K = n.kh * n.kw * cin_eff
-                coutp, kpad = _r(n.cout, 128), _r(K, 64)
+                coutp, kpad = _r(n.cout, 256), _r(K, 64)
                 wk = pack_conv_weight(k, cin_eff, coutp, kpad)
             elif isinstance(n, Dense):
                 k = w[f"{n.name}/kernel"][None, None]  # 1x1xCinxCout
                 b = w[f"{n.name}/bias"]
                 cin_eff = _r(n.cin, 8)
                 K = cin_eff
-                coutp, kpad = _r(n.cout, 128), _r(K, 64)
+                coutp, kpad = _r(n.cout, 256), _r(K, 64)
                 wk = pack_conv_weight(k, cin_eff, coutp, kpad)
             else:
                 continue
@@ -142,6 +143,14 @@ class Engine:
 
     # --------------------------------------------------------------- plan ----
     def _build_plan(self) -> None:
+        self.tuned: Dict[str, int] = {}
+        if self.autotune and self.device.type == "cuda":
+            from ..ops import tuning
+
+            convs = [self._conv_args(n) for n in self.g.nodes if isinstance(n, (Conv, Dense))]
+            table = tuning.autotune(convs)
+            for n, a in zip([n for n in self.g.nodes if isinstance(n, (Conv, Dense))], convs):
+                self.tuned[n.name] = table.get(tuning.shape_key(a), -1)
         self.plans = [self._build_one_plan(self.srcs[i]) for i in range(self.src_slots)]
         self.plan = self.plans[0]
         self.graph_captured = [False] * self.src_slots
@@ -158,7 +167,7 @@ class Engine:
         for n in g.nodes:
             if isinstance(n, (Conv, Dense)):
                 a = self._conv_args(n)
-                cfg = self.cfg_overrides.get(n.name, -1)
+                cfg = self.cfg_overrides.get(n.name, self.tuned.get(n.name, -1))
                 used = L.dml_plan_add_conv(plan, C.byref(a), cfg)
                 self.op_cfg[n.name] = used
                 self._keep.append(a)

@@ -29,7 +29,7 @@ def pack_weight(w_oihw: torch.Tensor, cin_eff: Optional[int] = None) -> Tuple[to
     k = torch.zeros((co, kh, kw, cin_eff), dtype=torch.float32)
     k[..., :ci] = w_oihw.permute(0, 2, 3, 1).float().cpu()
     K = kh * kw * cin_eff
-    out = torch.zeros((_r(co, 128), _r(K, 64)), dtype=torch.float32)
+    out = torch.zeros((_r(co, 256), _r(K, 64)), dtype=torch.float32)
     out[:co, :K] = k.reshape(co, K)
     return out.to(torch.bfloat16), K, _r(K, 64)
 

@@ -1,0 +1,96 @@
+"""Per-shape tile selection for the implicit-GEMM conv kernel.
+
+Different layers want different tiles (measured on MI355X, tools/conv_bench.py):
+the 3x3 convs of ResNet50 run best on 128x128 (2 blocks/CU), the memory-bound
+1x1 convs with narrow K on 64x128 / 128x64 tiles (more workgroups in flight).
+``autotune`` times every candidate config on the engine's real buffers once
+per unique shape (a few hundred launches, well under a second) and caches the
+winners in a JSON table keyed by the shape signature, so later processes load
+it instead of re-timing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import threading
+from typing import Dict, Iterable, List, Optional, Tuple
+
+from .. import _native as N
+
+V2_CFGS = (10, 11, 12, 13, 14, 15, 16)
+CACHE_PATH = os.environ.get(
+    "DML_TUNING_CACHE",
+    os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))
+_lock = threading.Lock()
+
+
+def shape_key(a: N.ConvArgs) -> str:
+    return (f"n{a.N}_h{a.H}_w{a.W}_c{a.Cin}_ld{a.ldx}_k{a.kh}x{a.kw}_s{a.sh}x{a.sw}_p{a.ph}x{a.pw}"
+            f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}")
+
+
+def load_cache(path: str = CACHE_PATH) -> Dict[str, int]:
+    try:
+        with open(path) as f:
+            return {k: int(v) for k, v in json.load(f).items()}
+    except (OSError, ValueError):
+        return {}
+
+
+def save_cache(table: Dict[str, int], path: str = CACHE_PATH) -> None:
+    with _lock:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        cur = load_cache(path)
+        cur.update(table)
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(dict(sorted(cur.items())), f, indent=0)
+        os.replace(tmp, path)
+
+
+def valid_cfgs(a: N.ConvArgs) -> List[int]:
+    if a.Cout % 8 or a.Cin % 8 or a.ldx % 8 or a.ldy % 8:
+        return [0]
+    return list(V2_CFGS)
+
+
+def time_cfg(a: N.ConvArgs, cfg: int, iters: int = 3) -> float:
+    import torch
+
+    L = N.lib()
+    s = N.stream_ptr()
+    N.check(L.dml_conv(C.byref(a), cfg, s), "conv warmup")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        L.dml_conv(C.byref(a), cfg, s)
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None, persist: bool = True
+             ) -> Dict[str, int]:
+    """Return {shape_key: best cfg} for every ConvArgs (timing the uncached ones)."""
+    cache = dict(load_cache() if cache is None else cache)
+    new: Dict[str, int] = {}
+    for a in args:
+        k = shape_key(a)
+        if k in cache or k in new:
+            continue
+        best: Tuple[float, int] = (float("inf"), -1)
+        for cfg in valid_cfgs(a):
+            try:
+                t = time_cfg(a, cfg)
+            except N.NativeError:
+                continue
+            best = min(best, (t, cfg))
+        new[k] = best[1]
+    if new and persist:
+        try:
+            save_cache(new)
+        except OSError:
+            pass
+    cache.update(new)
+    return cache

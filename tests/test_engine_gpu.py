@@ -43,7 +43,7 @@ def test_every_conv_layer_isolated(name):
         k, b = fold_conv(n, w)
         cin_eff = _r(n.cin, 8)
         K = n.kh * n.kw * cin_eff
-        wp = torch.from_numpy(pack_conv_weight(k, cin_eff, _r(n.cout, 128), _r(K, 64))).to(torch.bfloat16)
+        wp = torch.from_numpy(pack_conv_weight(k, cin_eff, _r(n.cout, 256), _r(K, 64))).to(torch.bfloat16)
         kf, bf = ex.folded[n.name]
         ref = F.conv2d(src[:, n.in_coff:n.in_coff + n.cin], kf, bf, stride=(n.sh, n.sw), padding=(n.ph, n.pw))
         res = None

@@ -14,3 +14,4 @@ timeout -k 10 600 python bench.py --steps $STEPS --warmup 5 --op-times gpurun_ou
 if [ -n "$PROFILE" ]; then
   cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 && echo profiled || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/prof.log; exit 1; }
 fi
+cp $GRAFT_REPO_ROOT/distributed_machine_learning_amd/tuning/conv_tuning.json $GRAFT_REPO_ROOT/gpurun_out/ 2>/dev/null || true
