@@ -1,0 +1,280 @@
+"""The replicated, versioned store ("SDFS") protocol: leader, replica, client.
+
+Reference protocol (worker.py:651-883 handlers, 1201-1354 client, leader.py):
+PUT -> leader picks 4 replicas, each scp-pulls from the client, leader reports
+success when all did; GET asks the leader for holders then pulls from the first
+that works (R = 1); DELETE fans out; LS / LS-ALL / GET-VERSIONS are leader
+queries; after failures the leader re-replicates under-replicated files.
+
+Same semantics here, over request/reply frames (per-request futures) and the
+blob data plane (store/blob.py). Fixed reference defects: failed PUTs are
+reported (leader.py:132 typo), a dead replica of an in-flight PUT is replaced
+(worker.py:1264 inverted test), placement never loops forever (leader.py:60),
+``put`` never waits without a timeout (worker.py:1546).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+from typing import Callable, Dict, List, Optional, Tuple
+
+from ..cluster.frames import Frame, MsgType
+from ..cluster.membership import MembershipList
+from ..cluster.transport import Endpoint
+from .blob import BlobSource
+from .local_store import LocalFileStore
+from .metadata import FAILED, SUCCESS, StoreMetadata
+
+log = logging.getLogger(__name__)
+
+
+class StoreService:
+    def __init__(self, ep: Endpoint, ml: MembershipList, local: LocalFileStore, source: BlobSource, blobs,
+                 leader_fn: Callable[[], Optional[str]], replication: int = 4, timeout: float = 10.0,
+                 storage_role: Optional[Callable[[str], bool]] = None):
+        self.ep, self.ml, self.local, self.source, self.blobs = ep, ml, local, source, blobs
+        self.leader_fn = leader_fn
+        self.meta = StoreMetadata(replication)
+        self.timeout = timeout
+        self.storage_role = storage_role or (lambda n: True)
+        on = ep.on
+        # leader-side
+        on(MsgType.PUT_REQUEST, self._l_put)
+        on(MsgType.DELETE_FILE_REQUEST, self._l_delete)
+        on(MsgType.LIST_FILE_REQUEST, self._l_ls)
+        on(MsgType.GET_FILE_REQUEST, self._l_get)
+        on(MsgType.GET_FILE_NAMES_REQUEST, self._l_ls_all)
+        on(MsgType.ALL_LOCAL_FILES, self._l_all_local_files)
+        # replica-side
+        on(MsgType.DOWNLOAD_FILE, self._r_download)
+        on(MsgType.DELETE_FILE, self._r_delete)
+        on(MsgType.REPLICATE_FILE, self._r_replicate)
+
+    # ------------------------------------------------------------ helpers --
+    @property
+    def me(self) -> str:
+        return self.ep.name
+
+    def is_leader(self) -> bool:
+        return self.leader_fn() == self.me
+
+    def storage_nodes(self) -> List[str]:
+        return [n for n in self.ml.alive() if self.storage_role(n)]
+
+    async def _leader_request(self, mtype: MsgType, payload: dict, timeout: Optional[float] = None) -> Optional[Frame]:
+        leader = self.leader_fn()
+        if leader is None:
+            return None
+        return await self.ep.request(leader, mtype, payload, timeout=timeout or self.timeout, retries=1)
+
+    # ========================================================== client API ==
+    async def put(self, data: bytes, name: str) -> Tuple[bool, str]:
+        tok = self.source.stage(data)
+        try:
+            r = await self._leader_request(MsgType.PUT_REQUEST, {"filename": name, "token": tok},
+                                           timeout=self.timeout * 3)
+        finally:
+            self.source.unstage(tok)
+        if r is None:
+            return False, "leader unreachable"
+        return r.type == MsgType.PUT_REQUEST_SUCCESS, r.payload.get("error", "")
+
+    async def put_file(self, path: str, name: str) -> Tuple[bool, str]:
+        with open(path, "rb") as f:
+            return await self.put(f.read(), name)
+
+    async def locate(self, name: str) -> Dict[str, List[int]]:
+        r = await self._leader_request(MsgType.GET_FILE_REQUEST, {"filename": name})
+        return {} if r is None else r.payload.get("machineids_with_file_versions", {})
+
+    async def get(self, name: str, version: Optional[int] = None) -> Optional[Tuple[int, bytes]]:
+        if self.local.has(name, version):
+            v = version if version is not None else self.local.latest(name)
+            return v, self.local.get_bytes(name, v)
+        holders = await self.locate(name)
+        return await self.fetch_from(holders, name, version)
+
+    async def fetch_from(self, holders: Dict[str, List[int]], name: str, version: Optional[int] = None
+                         ) -> Optional[Tuple[int, bytes]]:
+        """R = 1: first holder that answers (the local replica first)."""
+        order = sorted(holders, key=lambda n: (n != self.me, n))
+        for node in order:
+            if version is not None and version not in holders[node]:
+                continue
+            try:
+                items = await self.blobs.fetch(node, {"op": "get", "name": name, "version": version})
+            except (ConnectionError, OSError, asyncio.TimeoutError):
+                continue
+            if items:
+                return items[0]
+        return None
+
+    async def delete(self, name: str) -> Tuple[bool, str]:
+        r = await self._leader_request(MsgType.DELETE_FILE_REQUEST, {"filename": name})
+        if r is None:
+            return False, "leader unreachable"
+        return r.type == MsgType.DELETE_FILE_REQUEST_SUCCESS, r.payload.get("error", "")
+
+    async def ls(self, name: str) -> List[str]:
+        r = await self._leader_request(MsgType.LIST_FILE_REQUEST, {"filename": name})
+        return [] if r is None else r.payload.get("machines", [])
+
+    async def ls_all(self, pattern: str) -> List[str]:
+        r = await self._leader_request(MsgType.GET_FILE_NAMES_REQUEST, {"filepattern": pattern})
+        return [] if r is None else r.payload.get("files", [])
+
+    async def get_versions(self, name: str, n: int) -> List[Tuple[int, bytes]]:
+        holders = await self.locate(name)
+        vers = sorted({v for vs in holders.values() for v in vs})[-n:]
+        out = []
+        for v in reversed(vers):
+            got = await self.fetch_from(holders, name, v)
+            if got:
+                out.append(got)
+        return out
+
+    async def announce_files(self) -> None:
+        """Tell the (new) leader what this node holds (reference ALL_LOCAL_FILES, worker.py:593)."""
+        leader = self.leader_fn()
+        if leader and leader != self.me:
+            await self.ep.send(leader, MsgType.ALL_LOCAL_FILES, {"all_files": self.local.all_files()})
+        elif leader == self.me:
+            self.meta.set_node_files(self.me, self.local.all_files())
+
+    # ======================================================= leader handlers ==
+    async def _l_put(self, fr: Frame) -> None:
+        name = fr.payload["filename"]
+        if self.meta.in_progress(name):
+            await self.ep.reply(fr, MsgType.PUT_REQUEST_FAIL, {"filename": name, "error": "upload in progress"})
+            return
+        targets = self.meta.targets_for_put(name, self.storage_nodes())
+        if not targets:
+            await self.ep.reply(fr, MsgType.PUT_REQUEST_FAIL, {"filename": name, "error": "no storage nodes"})
+            return
+        version = self.meta.latest_version(name) + 1
+        self.meta.begin(name, targets)
+        req = {"filename": name, "version": version, "source": fr.sender, "token": fr.payload.get("token")}
+        outcome = await self._fan_out(name, targets, req)
+        self.meta.finish(name)
+        if outcome == SUCCESS:
+            await self.ep.reply(fr, MsgType.PUT_REQUEST_SUCCESS, {"filename": name, "version": version,
+                                                                  "replicas": targets})
+        else:
+            await self.ep.reply(fr, MsgType.PUT_REQUEST_FAIL, {"filename": name, "error": "replica failed"})
+
+    async def _fan_out(self, name: str, targets: List[str], req: dict) -> str:
+        pending = list(targets)
+        tried = set(targets)
+        outcome = None
+        while pending:
+            rs = await asyncio.gather(*(self.ep.request(t, MsgType.DOWNLOAD_FILE, req, timeout=self.timeout)
+                                        for t in pending))
+            retry = []
+            for t, r in zip(pending, rs):
+                ok = r is not None and r.type == MsgType.DOWNLOAD_FILE_SUCCESS
+                if r is not None:
+                    self.meta.set_node_files(t, r.payload.get("all_files", {}))
+                if not ok and not self.ml.is_alive(t):
+                    # replica died mid-PUT: substitute another node
+                    self.meta.requests.get(name, {}).pop(t, None)
+                    subs = [n for n in self.meta.place(name, self.storage_nodes(), 64) if n not in tried]
+                    if subs:
+                        tried.add(subs[0])
+                        self.meta.requests.setdefault(name, {})[subs[0]] = "Waiting"
+                        retry.append(subs[0])
+                    continue
+                outcome = self.meta.update(name, t, ok) or outcome
+            pending = retry
+        st = self.meta.requests.get(name, {})
+        if st and all(v == SUCCESS for v in st.values()):
+            return SUCCESS
+        return FAILED
+
+    async def _l_delete(self, fr: Frame) -> None:
+        name = fr.payload["filename"]
+        holders = list(self.meta.holders(name))
+        if not holders:
+            await self.ep.reply(fr, MsgType.DELETE_FILE_REQUEST_FAIL, {"filename": name, "error": "no such file"})
+            return
+        rs = await asyncio.gather(*(self.ep.request(h, MsgType.DELETE_FILE, {"filename": name}, timeout=self.timeout)
+                                    for h in holders))
+        ok = True
+        for h, r in zip(holders, rs):
+            if r is None:
+                ok = ok and not self.ml.is_alive(h)
+                continue
+            self.meta.set_node_files(h, r.payload.get("all_files", {}))
+            ok = ok and r.type == MsgType.DELETE_FILE_ACK
+        await self.ep.reply(fr, MsgType.DELETE_FILE_REQUEST_SUCCESS if ok else MsgType.DELETE_FILE_REQUEST_FAIL,
+                            {"filename": name})
+
+    async def _l_ls(self, fr: Frame) -> None:
+        name = fr.payload["filename"]
+        await self.ep.reply(fr, MsgType.LIST_FILE_REQUEST_ACK, {"filename": name,
+                                                                "machines": sorted(self.meta.holders(name))})
+
+    async def _l_get(self, fr: Frame) -> None:
+        name = fr.payload["filename"]
+        await self.ep.reply(fr, MsgType.GET_FILE_REQUEST_ACK, {"filename": name,
+                                                               "machineids_with_file_versions": self.meta.holders(name)})
+
+    async def _l_ls_all(self, fr: Frame) -> None:
+        pat = fr.payload.get("filepattern", "*")
+        await self.ep.reply(fr, MsgType.GET_FILE_NAMES_REQUEST_ACK, {"filepattern": pat,
+                                                                     "files": self.meta.matching(pat)})
+
+    async def _l_all_local_files(self, fr: Frame) -> None:
+        self.meta.set_node_files(fr.sender, fr.payload.get("all_files", {}))
+
+    def adopt(self, acks: Dict[str, dict]) -> None:
+        """New leader: rebuild the file map from COORDINATE_ACK payloads."""
+        self.meta.file_map.clear()
+        self.meta.set_node_files(self.me, self.local.all_files())
+        for node, p in acks.items():
+            self.meta.set_node_files(node, p.get("all_files", {}))
+
+    async def node_failed(self, node: str) -> int:
+        """Leader: drop the node's files and restore the replication factor."""
+        if not self.is_leader():
+            return 0
+        self.meta.remove_node(node)
+        plan = self.meta.under_replicated(self.storage_nodes())
+        n = 0
+        for name, src, new_nodes in plan:
+            for t in new_nodes:
+                r = await self.ep.request(t, MsgType.REPLICATE_FILE, {"filename": name, "source": src},
+                                          timeout=self.timeout)
+                if r is not None and r.type == MsgType.REPLICATE_FILE_SUCCESS:
+                    self.meta.set_node_files(t, r.payload.get("all_files", {}))
+                    n += 1
+        return n
+
+    # ====================================================== replica handlers ==
+    async def _r_download(self, fr: Frame) -> None:
+        p = fr.payload
+        try:
+            items = await self.blobs.fetch(p["source"], {"op": "outbox", "token": p.get("token")})
+            if not items:
+                raise FileNotFoundError("outbox empty")
+            self.local.put_bytes(p["filename"], items[0][1], version=p.get("version"))
+            mt = MsgType.DOWNLOAD_FILE_SUCCESS
+        except (ConnectionError, OSError, asyncio.TimeoutError) as e:
+            log.warning("%s: download %s failed: %s", self.me, p["filename"], e)
+            mt = MsgType.DOWNLOAD_FILE_FAIL
+        await self.ep.reply(fr, mt, {"filename": p["filename"], "all_files": self.local.all_files()})
+
+    async def _r_delete(self, fr: Frame) -> None:
+        ok = self.local.delete(fr.payload["filename"])
+        await self.ep.reply(fr, MsgType.DELETE_FILE_ACK if ok else MsgType.DELETE_FILE_NAK,
+                            {"filename": fr.payload["filename"], "all_files": self.local.all_files()})
+
+    async def _r_replicate(self, fr: Frame) -> None:
+        p = fr.payload
+        try:
+            items = await self.blobs.fetch(p["source"], {"op": "get_all", "name": p["filename"]})
+            for v, data in items:
+                self.local.put_bytes(p["filename"], data, version=v)
+            mt = MsgType.REPLICATE_FILE_SUCCESS if items else MsgType.REPLICATE_FILE_FAIL
+        except (ConnectionError, OSError, asyncio.TimeoutError):
+            mt = MsgType.REPLICATE_FILE_FAIL
+        await self.ep.reply(fr, mt, {"filename": p["filename"], "all_files": self.local.all_files()})
