@@ -1,0 +1,173 @@
+"""Inference backends used by a worker.
+
+Reference (models.py:23-106): per image ``load_img(target_size)`` (Pillow,
+NEAREST) -> preprocess -> ``model.predict`` at batch 1 -> ``decode_predictions``;
+the Keras model is rebuilt for EVERY batch in a fresh ProcessPoolExecutor.
+
+Backends here keep the model resident:
+ * ``GpuBackend`` — the native MI355X engine (hand-written gfx950 kernels), one
+   engine per batch-size bucket, weights resident in HBM; images are decoded on
+   CPU threads into a pinned arena and staged with hipMemcpyAsync.
+ * ``CpuBackend`` — the fp32 PyTorch executor of the same layer IR, for the
+   BASELINE "plumbing" config (ResNet50, batch 1, CPU worker on JPEGs).
+ * ``FakeBackend`` — deterministic pseudo-results for control-plane tests.
+"""
+from __future__ import annotations
+
+import hashlib
+import io
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..models import build_model, canonical_name
+
+INPUT_HW = {"ResNet50": (224, 224), "InceptionV3": (299, 299)}
+
+
+def load_image(data: bytes, target_hw: Tuple[int, int]) -> np.ndarray:
+    """Keras ``load_img(target_size=...)``: decode, RGB, Pillow NEAREST resize."""
+    from PIL import Image
+
+    im = Image.open(io.BytesIO(data)).convert("RGB")
+    if im.size != (target_hw[1], target_hw[0]):
+        im = im.resize((target_hw[1], target_hw[0]), Image.NEAREST)
+    return np.asarray(im, dtype=np.uint8)
+
+
+class Backend:
+    name = "base"
+
+    def predict(self, model: str, images: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        raise NotImplementedError
+
+    def decode_batch(self, model: str, blobs: Sequence[bytes]) -> np.ndarray:
+        hw = INPUT_HW[canonical_name(model)]
+        return np.stack([load_image(b, hw) for b in blobs]) if blobs else np.zeros((0, *hw, 3), np.uint8)
+
+
+class FakeBackend(Backend):
+    name = "fake"
+
+    def __init__(self, delay: float = 0.0):
+        self.delay = delay
+        self.calls = 0
+
+    def predict(self, model, images):
+        self.calls += 1
+        if self.delay:
+            time.sleep(self.delay)
+        n = len(images)
+        idx = np.zeros((n, 5), np.int32)
+        p = np.zeros((n, 5), np.float32)
+        for i in range(n):
+            h = hashlib.sha256(images[i].tobytes()).digest()
+            idx[i] = [int.from_bytes(h[2 * k:2 * k + 2], "big") % 1000 for k in range(5)]
+            p[i] = np.sort(np.frombuffer(h[16:36], dtype=np.uint8)[:5].astype(np.float32) / 1275.0)[::-1]
+        return idx, p
+
+    def decode_batch(self, model, blobs):
+        hw = (8, 8)
+        out = np.zeros((len(blobs), *hw, 3), np.uint8)
+        for i, b in enumerate(blobs):
+            h = np.frombuffer(hashlib.sha256(b).digest() * 6, np.uint8)[: 8 * 8 * 3]
+            out[i] = h.reshape(8, 8, 3)
+        return out
+
+
+class CpuBackend(Backend):
+    """fp32 PyTorch executor of the IR (plumbing config)."""
+
+    name = "cpu"
+
+    def __init__(self, seed: int = 0, calibrate: bool = True):
+        self.seed, self.calibrate = seed, calibrate
+        self._ex: Dict[str, object] = {}
+        self._lock = threading.Lock()
+
+    def _executor(self, model):
+        from ..models.oracle import OracleExecutor
+
+        model = canonical_name(model)
+        with self._lock:
+            if model not in self._ex:
+                g, w = build_model(model, seed=self.seed, calibrate=self.calibrate)
+                self._ex[model] = (g, OracleExecutor(g, w))
+            return self._ex[model]
+
+    def predict(self, model, images):
+        import torch
+
+        from ..models.oracle import preprocess_reference
+
+        g, ex = self._executor(model)
+        x = preprocess_reference(torch.from_numpy(np.ascontiguousarray(images)), g.input_hw, g.preprocess)
+        probs = ex.forward(x)["probs"]
+        p, idx = probs.topk(5, dim=-1)
+        return idx.numpy().astype(np.int32), p.numpy().astype(np.float32)
+
+
+class GpuBackend(Backend):
+    """The native engine on this process's GPU. Engines are cached per padded
+    batch-size bucket (powers of two up to max_batch) so any task size runs."""
+
+    name = "gpu"
+
+    def __init__(self, seed: int = 0, device: str = "cuda", max_batch: int = 256, use_graph: bool = True):
+        import torch
+
+        self.seed, self.device, self.max_batch, self.use_graph = seed, device, max_batch, use_graph
+        self._engines: Dict[Tuple[str, int], object] = {}
+        self._models: Dict[str, tuple] = {}
+        self._lock = threading.Lock()
+        self.stream = torch.cuda.Stream(torch.device(device))
+        self.decode_pool = ThreadPoolExecutor(max_workers=8)
+
+    def _bucket(self, n: int) -> int:
+        b = 1
+        while b < n:
+            b *= 2
+        return min(b, self.max_batch)
+
+    def engine(self, model: str, n: int):
+        from ..models.engine import Engine
+
+        model = canonical_name(model)
+        b = self._bucket(n)
+        with self._lock:
+            if model not in self._models:
+                self._models[model] = build_model(model, seed=self.seed, calibrate=True)
+            key = (model, b)
+            if key not in self._engines:
+                g, w = self._models[model]
+                self._engines[key] = Engine(g, w, batch=b, device=self.device)
+            return self._engines[key]
+
+    def decode_batch(self, model, blobs):
+        hw = INPUT_HW[canonical_name(model)]
+        return np.stack(list(self.decode_pool.map(lambda b: load_image(b, hw), blobs))) if blobs else \
+            np.zeros((0, *hw, 3), np.uint8)
+
+    def predict(self, model, images):
+        import torch
+
+        n = len(images)
+        out_i, out_p = [], []
+        for s in range(0, n, self.max_batch):
+            chunk = images[s:s + self.max_batch]
+            eng = self.engine(model, len(chunk))
+            with torch.cuda.stream(self.stream):
+                src = torch.from_numpy(np.ascontiguousarray(chunk)).pin_memory()
+                eng.src[: len(chunk)].copy_(src, non_blocking=True)
+                eng.run(self.stream, use_graph=self.use_graph)
+                res = eng.result.cpu()
+            out_i.append(res[0, : len(chunk)].numpy())
+            out_p.append(res[1, : len(chunk)].view(torch.float32).numpy())
+        return np.concatenate(out_i), np.concatenate(out_p)
+
+
+def make_backend(kind: str, **kw) -> Backend:
+    return {"fake": FakeBackend, "cpu": CpuBackend, "gpu": GpuBackend}[kind](**kw)

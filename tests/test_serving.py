@@ -1,0 +1,224 @@
+"""Serving layer: batching, fair-share scheduler, metrics, output format, and
+an in-process cluster (coordinator + standby + workers + client on the loopback
+network) exercising submit -> schedule -> infer -> store output -> ACK ->
+get-output, worker kill re-dispatch and coordinator failover."""
+import asyncio
+import json
+import os
+
+import numpy as np
+import pytest
+
+from distributed_machine_learning_amd.cluster.transport import LoopbackNetwork
+from distributed_machine_learning_amd.serving.cost_model import REFERENCE_PARAMS, CostModel
+from distributed_machine_learning_amd.serving.inference import FakeBackend
+from distributed_machine_learning_amd.serving.jobs import JobManager, make_batches, pick_images
+from distributed_machine_learning_amd.serving.metrics import Metrics
+from distributed_machine_learning_amd.serving.node import Node, NodeConfig
+from distributed_machine_learning_amd.serving.output import FAILED_DOWNLOAD, decode_top5, dumps, output_name
+from distributed_machine_learning_amd.serving.scheduler import best_split, plan
+from distributed_machine_learning_amd.store.blob import InProcBlobNetwork
+
+REF = os.environ.get("DML_REFERENCE", "/root/reference")
+
+
+# ----------------------------------------------------------------- batching --
+def test_cyclic_pick_and_exact_batches():
+    imgs = [f"{i}.jpeg" for i in range(7)]
+    assert pick_images(sorted(imgs), 10) == sorted(imgs) + sorted(imgs)[:3]
+    bs = make_batches(31, "ResNet50", [str(i) for i in range(100)], 10)
+    # the reference produced [11 x 9, 1] here (worker.py:215-227); exact batches now
+    assert [len(b.images) for b in bs] == [10] * 10 and [b.batch_id for b in bs] == list(range(1, 11))
+
+
+def test_job_ids_start_at_31_and_requeue_front():
+    jm = JobManager({"ResNet50": 4, "InceptionV3": 4})
+    j = jm.submit("ResNet50", 10, [f"{i}.jpeg" for i in range(20)], "client")
+    assert j.job_id == 31 and j.batches_total == 3
+    b1 = jm.pop_next("ResNet50")
+    jm.requeue_front(b1.key)
+    assert jm.queues["ResNet50"][0].key == b1.key
+    for _ in range(3):
+        b = jm.pop_next("ResNet50")
+        jm.complete(b.key)
+    assert jm.jobs[31].done
+
+
+def test_snapshot_restore_roundtrip():
+    jm = JobManager()
+    jm.submit("InceptionV3", 25, [f"{i}.jpeg" for i in range(9)], "c")
+    b = jm.pop_next("InceptionV3")
+    snap = json.loads(json.dumps(jm.snapshot()))
+    jm2 = JobManager()
+    jm2.restore(snap)
+    assert jm2.queues["InceptionV3"][0].key == b.key and jm2.pending() == jm.pending() + 1
+
+
+# ---------------------------------------------------------------- scheduler --
+def test_best_split_matches_reference_examples():
+    cm = CostModel()
+    ri = cm.rate_per_worker("InceptionV3", 10)
+    rr = cm.rate_per_worker("ResNet50", 10)
+    # n=8 -> 4/4, n=7 -> 4/3, n=6 -> 3/3 (default batch 10)
+    assert best_split(8, ri, rr) == (4, 4)
+    assert best_split(7, ri, rr) == (4, 3)
+    assert best_split(6, ri, rr) == (3, 3)
+
+
+def test_plan_single_model_fills_free_workers():
+    a = plan({"ResNet50": 3, "InceptionV3": 0}, ["w1", "w2", "w3", "w4"], {}, ["w1", "w2", "w3", "w4"],
+             CostModel(), {"ResNet50": 10, "InceptionV3": 10})
+    assert len(a) == 3 and all(x.model == "ResNet50" and x.preempt is None for x in a)
+
+
+def test_plan_two_models_preempts_to_fair_share():
+    ws = [f"w{i}" for i in range(8)]
+    running = {w: ("ResNet50", (31, i + 1)) for i, w in enumerate(ws)}  # ResNet holds every worker
+    a = plan({"ResNet50": 20, "InceptionV3": 20}, [], running, ws, CostModel(), {"ResNet50": 10, "InceptionV3": 10})
+    pre = [x for x in a if x.preempt]
+    assert len(pre) == 4 and all(x.model == "InceptionV3" and x.preempt[0] == "ResNet50" for x in pre)
+
+
+def test_cost_model_uses_measurements():
+    cm = CostModel()
+    assert cm.batch_time("ResNet50", 10) == REFERENCE_PARAMS["ResNet50"].execution_time_per_vm(10) == 16.75
+    cm.observe("ResNet50", 256, 0.01)
+    assert cm.batch_time("ResNet50", 256) == 0.01 and abs(cm.batch_time("ResNet50", 128) - 0.005) < 1e-12
+
+
+# ------------------------------------------------------------------ metrics --
+def test_metrics_c1_window_and_c2():
+    t = [0.0]
+    m = Metrics(window=10, clock=lambda: t[0])
+    for i in range(5):
+        t[0] = float(i)
+        m.record("ResNet50", latency=0.5 + i, service=1.0, images=10)
+    t[0] = 12.0
+    c1 = m.c1()["ResNet50"]
+    assert c1["query_count"] == 50 and c1["query_rate_10s"] == 3 * 10 / 10  # records at t=2,3,4
+    c2 = m.c2()["ResNet50"]
+    assert c2["per_image_avg"] == pytest.approx(0.1) and c2["query_latency_p50"] == pytest.approx(2.5)
+    ref = m.c2_reference_payload()
+    assert set(ref) >= {"resnet50_avg", "resnet50_std", "resnet50_quantiles", "inceptionv3_avg"}
+
+
+# ------------------------------------------------------------------- output --
+def test_output_format_matches_reference_sample():
+    out = decode_top5(["/tmp/1.jpeg"], np.array([[3, 2, 1, 0, 9]]), np.array([[0.5, 0.2, 0.1, 0.05, 0.01]]),
+                      failed=["2.jpeg"])
+    assert output_name(31, 2, "fa22-cs425-6903.cs.illinois.edu") == "output_31_2_fa22-cs425-6903.json"
+    doc = json.loads(dumps(out))
+    assert doc["2.jpeg"] == FAILED_DOWNLOAD
+    top = doc["1.jpeg"]
+    assert len(top) == 1 and len(top[0]) == 5 and len(top[0][0]) == 3 and isinstance(top[0][0][2], float)
+    sample = os.path.join(REF, "download", "output_1_127.json")
+    if os.path.exists(sample):  # same nesting as the reference's own output file
+        ref = json.load(open(sample))
+        k = next(iter(ref))
+        assert len(ref[k]) == 1 and len(ref[k][0]) == 5 and len(ref[k][0][0]) == 3
+        assert dumps(out).startswith("{\n    \"")  # indent 4
+
+
+# ---------------------------------------------------------------- cluster --
+async def _cluster(tmp, n_workers=4, delay=0.01, standby=True):
+    net, blobs = LoopbackNetwork(), InProcBlobNetwork()
+    base = dict(store_dir=str(tmp), backend="fake", period=0.05, ping_timeout=0.05, suspect_timeout=0.3,
+                cleanup_time=2.0, store_timeout=1.0, batch_sizes={"ResNet50": 4, "InceptionV3": 4})
+    specs = [("c0", "coordinator")] + ([("s0", "standby")] if standby else []) + \
+            [(f"w{i}", "worker") for i in range(n_workers)] + [("cli", "client")]
+    nodes = {}
+    for name, role in specs:
+        cfg = NodeConfig(role=role, seeds=["c0"], **base)
+        be = FakeBackend(delay=delay) if role == "worker" else None
+        nodes[name] = await Node(cfg, net=net, blob_net=blobs, name=name, backend=be).start()
+    await nodes["c0"].join()
+    for name in nodes:
+        if name != "c0":
+            await nodes[name].join()
+    await asyncio.sleep(0.3)
+    return net, blobs, nodes
+
+
+async def _load_images(cli, n):
+    for i in range(n):
+        ok, err = await cli.store.put(f"image-{i}".encode() * 10, f"{i}.jpeg")
+        assert ok, err
+
+
+async def _stop(nodes):
+    for n in nodes.values():
+        await n.stop()
+
+
+def test_cluster_job_end_to_end(tmp_path):
+    async def main():
+        net, blobs, nodes = await _cluster(tmp_path)
+        cli = nodes["cli"]
+        await _load_images(cli, 12)
+        jid = await cli.submit_job("ResNet50", 30)
+        assert jid == 31
+        assert await cli.wait_job(jid, timeout=20)
+        path = await cli.get_output(jid, str(tmp_path / "out"))
+        doc = json.load(open(path))
+        assert len(doc) == 12 and all(len(v[0]) == 5 for v in doc.values())
+        c1 = (await cli.leader_request(__import__("distributed_machine_learning_amd.cluster.frames",
+                                                  fromlist=["MsgType"]).MsgType.GET_C1_COMMAND)).payload["c1"]
+        assert c1["ResNet50"]["query_count"] == 30
+        await _stop(nodes)
+
+    asyncio.run(main())
+
+
+def test_concurrent_jobs_fair_share(tmp_path):
+    async def main():
+        net, blobs, nodes = await _cluster(tmp_path, n_workers=4, delay=0.05)
+        cli = nodes["cli"]
+        await _load_images(cli, 8)
+        j1 = await cli.submit_job("ResNet50", 400)
+        await asyncio.sleep(0.2)
+        j2 = await cli.submit_job("InceptionV3", 400)
+        await asyncio.sleep(0.25)
+        models = [a["model"] for a in nodes["c0"].coordinator.assignments().values()]
+        assert models.count("InceptionV3") >= 1 and models.count("ResNet50") >= 1
+        assert nodes["c0"].coordinator.preemptions >= 1  # ResNet held every worker before j2
+        assert await cli.wait_job(j1, 60) and await cli.wait_job(j2, 60)
+        await _stop(nodes)
+
+    asyncio.run(main())
+
+
+def test_worker_kill_mid_job_requeues(tmp_path):
+    async def main():
+        net, blobs, nodes = await _cluster(tmp_path, n_workers=4, delay=0.1)
+        cli = nodes["cli"]
+        await _load_images(cli, 8)
+        jid = await cli.submit_job("ResNet50", 64)
+        await asyncio.sleep(0.25)
+        victims = [w for w in ("w1", "w2") if w in nodes["c0"].coordinator.running]
+        for v in ("w1", "w2"):
+            net.kill(v)
+            blobs.dead.add(v)
+        assert await cli.wait_job(jid, timeout=30)
+        assert nodes["c0"].coordinator.requeues >= len(victims)
+        path = await cli.get_output(jid, str(tmp_path / "out"))
+        assert len(json.load(open(path))) == 8
+        await _stop(nodes)
+
+    asyncio.run(main())
+
+
+def test_coordinator_failover_to_standby(tmp_path):
+    async def main():
+        net, blobs, nodes = await _cluster(tmp_path, n_workers=3, delay=0.05)
+        cli = nodes["cli"]
+        await _load_images(cli, 6)
+        jid = await cli.submit_job("InceptionV3", 48)
+        await asyncio.sleep(0.3)
+        net.kill("c0")
+        blobs.dead.add("c0")
+        await asyncio.sleep(2.0)
+        assert nodes["s0"].is_leader()
+        assert await cli.wait_job(jid, timeout=30)
+        await _stop(nodes)
+
+    asyncio.run(main())
