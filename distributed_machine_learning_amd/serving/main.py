@@ -1,0 +1,104 @@
+"""Node entry point (reference main.py:15-77: ``python3 main.py --hostname=H
+--port=P [-t]``; logging to debug.log + stdout; SIGINT/SIGTERM stop the node).
+
+  python -m distributed_machine_learning_amd.serving.main --hostname 127.0.0.1 --port 8001 \
+      --role coordinator --introducer 127.0.0.1:8888 [--backend gpu|cpu|fake] [-t] \
+      [--cmd "5 /path/to/testfiles" --cmd "submit-job ResNet50 100" ...]
+
+With no ``--cmd`` the node runs the interactive stdin menu (cli.py); with
+``--cmd`` it executes the commands in order and keeps serving until
+``--exit-after`` seconds (or forever).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import signal
+import sys
+
+from .cli import MENU, Cli
+from .node import Node, NodeConfig
+
+
+def parse(argv=None) -> argparse.Namespace:
+    ap = argparse.ArgumentParser(description="distributed inference node")
+    ap.add_argument("-H", "--hostname", default="127.0.0.1")
+    ap.add_argument("-p", "--port", type=int, required=True)
+    ap.add_argument("-t", "--testing", action="store_true", help="3%% send drop + bps/false-positive meters")
+    ap.add_argument("--role", default="worker", choices=["coordinator", "standby", "worker", "client"])
+    ap.add_argument("--introducer", default="127.0.0.1:8888")
+    ap.add_argument("--seed-node", action="append", default=[])
+    ap.add_argument("--store-dir", default="./sdfs")
+    ap.add_argument("--download-dir", default="./download")
+    ap.add_argument("--testfiles", default="")
+    ap.add_argument("--backend", default="cpu", choices=["gpu", "cpu", "fake"])
+    ap.add_argument("--gpu", type=int, default=0)
+    ap.add_argument("--period", type=float, default=0.5)
+    ap.add_argument("--ping-timeout", type=float, default=0.25)
+    ap.add_argument("--suspect-timeout", type=float, default=2.0)
+    ap.add_argument("--cleanup", type=float, default=10.0)
+    ap.add_argument("--batch-size", type=int, default=10)
+    ap.add_argument("--cmd", action="append", default=[])
+    ap.add_argument("--exit-after", type=float, default=0.0)
+    ap.add_argument("--log", default="debug.log")
+    return ap.parse_args(argv)
+
+
+async def amain(a: argparse.Namespace) -> int:
+    kw = {}
+    if a.backend == "gpu":
+        kw = {"device": f"cuda:{a.gpu}"}
+    cfg = NodeConfig(host=a.hostname, port=a.port, role=a.role, introducer=a.introducer or None,
+                     seeds=a.seed_node, store_dir=a.store_dir, out_dir=None, backend=a.backend, backend_kw=kw,
+                     testing=a.testing, period=a.period, ping_timeout=a.ping_timeout,
+                     suspect_timeout=a.suspect_timeout, cleanup_time=a.cleanup,
+                     batch_sizes={"ResNet50": a.batch_size, "InceptionV3": a.batch_size})
+    node = await Node(cfg).start()
+    await node.join()
+    cli = Cli(node, testfiles=a.testfiles, download_dir=a.download_dir)
+    loop = asyncio.get_running_loop()
+    stop = asyncio.Event()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        try:
+            loop.add_signal_handler(sig, stop.set)
+        except NotImplementedError:  # pragma: no cover
+            pass
+    if a.cmd:
+        for line in a.cmd:
+            print(await cli.run_line(line), flush=True)
+        if a.exit_after:
+            try:
+                await asyncio.wait_for(stop.wait(), a.exit_after)
+            except asyncio.TimeoutError:
+                pass
+            await node.stop()
+            return 0
+    else:
+        print(MENU, flush=True)
+        q: asyncio.Queue = asyncio.Queue()
+        loop.add_reader(sys.stdin, lambda: q.put_nowait(sys.stdin.readline()))
+
+        async def reader():
+            while True:
+                line = await q.get()
+                if not line:
+                    stop.set()
+                    return
+                print(await cli.run_line(line), flush=True)
+
+        loop.create_task(reader())
+    await stop.wait()
+    await node.stop()
+    return 0
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s",
+                        handlers=[logging.FileHandler(a.log), logging.StreamHandler(sys.stderr)])
+    return asyncio.run(amain(a))
+
+
+if __name__ == "__main__":
+    sys.exit(main())
