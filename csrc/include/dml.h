@@ -32,6 +32,7 @@ typedef struct {
   int Ho, Wo, Cout, K, Kpad;
   int ldy, ldr;
   int relu, out_f32;
+  int dh, dw;         // tap dilation (0 is treated as 1); dw = 2 serves the pair-packed stem
 } DmlConvArgs;
 
 typedef struct {
@@ -48,6 +49,8 @@ typedef struct {
   void* y;          // bf16 NHWC, C = 8 (RGB/BGR + 5 zero channels)
   int N, Hs, Ws, Ho, Wo;
   int mode;         // 0 = caffe (BGR, minus ImageNet mean), 1 = tf (x/127.5 - 1)
+  int pair;         // 1: channels 4..6 hold the NEXT pixel's 3 values (pair-packed stem input)
+  int lpad;         // pair mode: zero columns on the left; output width = Wo + lpad
 } DmlPreprocArgs;
 
 // ---- single-op launches (used by tests and by the plan executor) ----

@@ -107,6 +107,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(DmlConvArgs a) {
   const bf16* __restrict__ xg = (const bf16*)a.x;
   const bf16* __restrict__ wg = (const bf16*)a.w;
   const int nk = a.Kpad / BK;
+  const int dh = a.dh > 0 ? a.dh : 1, dw = a.dw > 0 ? a.dw : 1;
 
   uint4 xr[T::XCH], wr[T::WCH];
 
@@ -114,7 +115,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(DmlConvArgs a) {
     const bool kval = rr < a.kh;
 #pragma unroll
     for (int i = 0; i < T::XCH; ++i) {
-      const int ih = ih0[i] + rr, iw = iw0[i] + ss;
+      const int ih = ih0[i] + rr * dh, iw = iw0[i] + ss * dw;
       const bool ok = kval && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       if (ok) {
         const long off = (long)(pix0[i] + ih * a.W + iw) * a.ldx + cc;

@@ -111,6 +111,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   const long wstep_row = (long)8 * a.Kpad * 2;  // next 8-row piece
 
   const int nk = a.Kpad / T::BK;
+  const int dh = a.dh > 0 ? a.dh : 1, dw = a.dw > 0 ? a.dw : 1;
 
   auto issue = [&](int kt, int stage) {
     char* sx = smem + stage * T::STAGE_BYTES;
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
     const bool kval = rr < a.kh;
 #pragma unroll
     for (int j = 0; j < T::XI; ++j) {
-      const int ih = ih0[j] + rr, iw = iw0[j] + ss;
+      const int ih = ih0[j] + rr * dh, iw = iw0[j] + ss * dw;
       const bool ok = kval && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       const unsigned off = ok ? (unsigned)(((pix0[j] + ih * a.W + iw) * a.ldx + cc) * 2) : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 0);
@@ -145,6 +146,30 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s, s);
+
+  // Epilogue operands prefetched behind the first DMA tiles: this thread's
+  // 8-channel group is fixed (NT % CG == 0), so its bias is 2 float4 and its
+  // residual is one 16-byte row segment per epilogue iteration. On the
+  // memory-bound 1x1 layers (K = 64..256) this hides the residual read under
+  // the operand loads instead of exposing it after the last MFMA.
+  constexpr int CG = BN / 8;  // 8-channel groups per pixel row
+  constexpr int EIT = BM * CG / T::NT;
+  static_assert(T::NT % CG == 0 && (BM * CG) % T::NT == 0, "epilogue mapping");
+  const int cg_t = tid % CG;
+  const int ch_t = c0 + cg_t * 8;
+  const bool ch_ok = ch_t < a.Cout;
+  const unsigned short* __restrict__ rg = (const unsigned short*)a.res;
+  float4 bias0 = make_float4(0.f, 0.f, 0.f, 0.f), bias1 = bias0;
+  if (ch_ok) {
+    bias0 = *(const float4*)(a.bias + ch_t);
+    bias1 = *(const float4*)(a.bias + ch_t + 4);
+  }
+  uint4 rpre[EIT];
+#pragma unroll
+  for (int it = 0; it < EIT; ++it) {
+    const int m = m0 + (tid + it * T::NT) / CG;
+    rpre[it] = (rg && ch_ok && m < M) ? *(const uint4*)(rg + (long)m * a.ldr + ch_t) : make_uint4(0, 0, 0, 0);
+  }
 
   for (int kt = 0; kt < nk; ++kt) {
     // retire tile kt (leave the younger STAGES-2 tiles in flight), then barrier
@@ -184,20 +209,19 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
       *(f32x4*)(smem + px * T::CROW + ch * 4) = acc[i][j];
     }
   __syncthreads();
-  constexpr int CG = BN / 8;  // 8-channel groups per pixel row
-  const unsigned short* __restrict__ rg = (const unsigned short*)a.res;
-  for (int e = tid; e < BM * CG; e += T::NT) {
-    const int px = e / CG, cg = e % CG;
-    const int m = m0 + px, ch = c0 + cg * 8;
-    if (m >= M || ch >= a.Cout) continue;
+#pragma unroll
+  for (int it = 0; it < EIT; ++it) {
+    const int e = tid + it * T::NT;
+    const int px = e / CG, cg = cg_t;
+    const int m = m0 + px, ch = ch_t;
+    if (m >= M || !ch_ok) continue;
     const float4 v0 = *(const float4*)(smem + px * T::CROW + cg * 32);
     const float4 v1 = *(const float4*)(smem + px * T::CROW + cg * 32 + 16);
-    const float4 b0 = *(const float4*)(a.bias + ch);
-    const float4 b1 = *(const float4*)(a.bias + ch + 4);
+    const float4 b0 = bias0, b1 = bias1;
     float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
                   v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
     if (rg) {
-      const uint4 r = *(const uint4*)(rg + (long)m * a.ldr + ch);
+      const uint4 r = rpre[it];
       f[0] += bf2f(r.x & 0xffff); f[1] += bf2f(r.x >> 16);
       f[2] += bf2f(r.y & 0xffff); f[3] += bf2f(r.y >> 16);
       f[4] += bf2f(r.z & 0xffff); f[5] += bf2f(r.z >> 16);
@@ -251,6 +275,7 @@ extern "C" int dml_conv_v2_init(void) {
   rc |= set_attr<128, 64, 2, 2, 2>();
   rc |= set_attr<256, 128, 4, 2, 2>();
   rc |= set_attr<128, 128, 2, 2, 3>();
+  rc |= set_attr<256, 32, 4, 1, 2>();
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   return rc ? -1 : 0;
 }
@@ -267,6 +292,7 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
     case 15: return launch<128, 64, 2, 2, 2>(a, s);   // 4 waves, 64px x 32ch per wave
     case 16: return launch<256, 128, 4, 2, 2>(a, s);  // 8 waves, 2-stage
     case 17: return launch<128, 128, 2, 2, 3>(a, s);  // 4 waves, 3-stage
+    case 18: return launch<256, 32, 4, 1, 2>(a, s);   // 4 waves, 64px x 32ch per wave (Cout = 32 layers)
     default: dml_set_error("dml_conv_v2: bad cfg"); return -1;
   }
 }

@@ -161,26 +161,37 @@ __global__ __launch_bounds__(256) void softmax_top5_kernel(const float* logits, 
 }
 
 // Pillow NEAREST resize (Keras load_img default): src = floor((dst + 0.5) * Ssrc / Sdst).
+__device__ __forceinline__ void preprocess_pixel(const DmlPreprocArgs& a, const unsigned char* src, int n, int oh,
+                                                 int ow, float sy, float sx, float* f) {
+  int iy = (int)(((float)oh + 0.5f) * sy), ix = (int)(((float)ow + 0.5f) * sx);
+  iy = min(iy, a.Hs - 1);
+  ix = min(ix, a.Ws - 1);
+  const unsigned char* px = src + (((long)n * a.Hs + iy) * a.Ws + ix) * 3;
+  const float r = px[0], g = px[1], b = px[2];
+  if (a.mode == 0) {  // caffe: RGB->BGR, subtract BGR mean, no scaling
+    f[0] = b - 103.939f; f[1] = g - 116.779f; f[2] = r - 123.68f;
+  } else {            // tf: scale to [-1, 1]
+    f[0] = r / 127.5f - 1.f; f[1] = g / 127.5f - 1.f; f[2] = b / 127.5f - 1.f;
+  }
+}
+
+// pair == 0: y[n][oh][ow][8] = (c0, c1, c2, 0 x5)
+// pair == 1: y[n][oh][j][8] = (pixel j-lpad: c0..c2, 0, pixel j-lpad+1: c0..c2, 0), zero outside the
+//            image — the stem conv then sees two horizontal taps per 16-byte chunk (dilation 2).
 __global__ __launch_bounds__(256) void preprocess_kernel(DmlPreprocArgs a) {
-  const long total = (long)a.N * a.Ho * a.Wo;
+  const int Wout = a.Wo + (a.pair ? a.lpad : 0);
+  const long total = (long)a.N * a.Ho * Wout;
   const float sy = (float)a.Hs / (float)a.Ho, sx = (float)a.Ws / (float)a.Wo;
   const unsigned char* src = (const unsigned char*)a.src;
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int ow = (int)(t % a.Wo);
-    long p = t / a.Wo;
+    const int j = (int)(t % Wout);
+    long p = t / Wout;
     const int oh = (int)(p % a.Ho);
     const int n = (int)(p / a.Ho);
-    int iy = (int)(((float)oh + 0.5f) * sy), ix = (int)(((float)ow + 0.5f) * sx);
-    iy = min(iy, a.Hs - 1);
-    ix = min(ix, a.Ws - 1);
-    const unsigned char* px = src + (((long)n * a.Hs + iy) * a.Ws + ix) * 3;
-    const float r = px[0], g = px[1], b = px[2];
     float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (a.mode == 0) {  // caffe: RGB->BGR, subtract BGR mean, no scaling
-      f[0] = b - 103.939f; f[1] = g - 116.779f; f[2] = r - 123.68f;
-    } else {            // tf: scale to [-1, 1]
-      f[0] = r / 127.5f - 1.f; f[1] = g / 127.5f - 1.f; f[2] = b / 127.5f - 1.f;
-    }
+    const int ow = a.pair ? j - a.lpad : j;
+    if (ow >= 0 && ow < a.Wo) preprocess_pixel(a, src, n, oh, ow, sy, sx, f);
+    if (a.pair && ow + 1 >= 0 && ow + 1 < a.Wo) preprocess_pixel(a, src, n, oh, ow + 1, sy, sx, f + 4);
     *(uint4*)((bf16*)a.y + t * 8) = pack8(f);
   }
 }
@@ -220,7 +231,7 @@ extern "C" int dml_softmax_top5(const float* logits, int B, int classes, int ld,
 }
 
 extern "C" int dml_preprocess(const DmlPreprocArgs* a, hipStream_t s) {
-  const long work = (long)a->N * a->Ho * a->Wo;
+  const long work = (long)a->N * a->Ho * (a->Wo + (a->pair ? a->lpad : 0));
   hipLaunchKernelGGL(dml::preprocess_kernel, dim3(dml::grid_for(work, 256)), dim3(256), 0, s, *a);
   DML_CHECK_LAUNCH();
   return 0;

@@ -60,11 +60,26 @@ def _stamp() -> str:
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile csrc/ into LIB_PATH if sources changed; return the library path."""
+    """Compile csrc/ into LIB_PATH if sources changed; return the library path.
+    Serialised with a file lock: every rank of a multi-GPU launch calls this."""
+    import fcntl
+
     stamp_file = PKG_DIR / ".libdml_hip.stamp"
     stamp = _stamp()
     if not force and LIB_PATH.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
         return LIB_PATH
+    BUILD_DIR.mkdir(parents=True, exist_ok=True)
+    with open(BUILD_DIR / ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if not force and LIB_PATH.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
+                return LIB_PATH  # another rank built it while we waited
+            return _build_locked(stamp, stamp_file, verbose)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_locked(stamp: str, stamp_file: Path, verbose: bool) -> Path:
     BUILD_DIR.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
 

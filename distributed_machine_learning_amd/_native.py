@@ -25,6 +25,7 @@ class ConvArgs(C.Structure):
         ("Ho", C.c_int), ("Wo", C.c_int), ("Cout", C.c_int), ("K", C.c_int), ("Kpad", C.c_int),
         ("ldy", C.c_int), ("ldr", C.c_int),
         ("relu", C.c_int), ("out_f32", C.c_int),
+        ("dh", C.c_int), ("dw", C.c_int),
     ]
 
 
@@ -41,6 +42,7 @@ class PreprocArgs(C.Structure):
     _fields_ = [
         ("src", C.c_void_p), ("y", C.c_void_p),
         ("N", C.c_int), ("Hs", C.c_int), ("Ws", C.c_int), ("Ho", C.c_int), ("Wo", C.c_int), ("mode", C.c_int),
+        ("pair", C.c_int), ("lpad", C.c_int),
     ]
 
 

@@ -29,6 +29,18 @@ def _r(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+def pair_pack_kernel(kernel_hwio: np.ndarray) -> np.ndarray:
+    """[kh, kw, 3, cout] -> [kh, ceil(kw/2), 8, cout]: tap s' holds taps 2s' (channels 0-2)
+    and 2s'+1 (channels 4-6) to match the pair-packed stem input."""
+    kh, kw, cin, cout = kernel_hwio.shape
+    assert cin <= 4
+    kw2 = (kw + 1) // 2
+    out = np.zeros((kh, kw2, 8, cout), np.float32)
+    for s in range(kw):
+        out[:, s // 2, 4 * (s % 2): 4 * (s % 2) + cin, :] = kernel_hwio[:, s]
+    return out
+
+
 def pack_conv_weight(kernel_hwio: np.ndarray, cin_eff: int, cout_pad: int, k_pad: int) -> np.ndarray:
     kh, kw, cin, cout = kernel_hwio.shape
     k = np.zeros((kh, kw, cin_eff, cout), np.float32)
@@ -53,6 +65,14 @@ class Engine:
         self.src_hw = src_hw or graph.input_hw
         self.cfg_overrides = cfg_overrides or {}
         self._keep = []  # keep ctypes structs / tensors alive
+        # Pair-packed stem: if the only consumer of the 3-channel input is one conv,
+        # the preprocess kernel writes two horizontally adjacent pixels per 16-byte
+        # chunk and that conv runs with dilation 2 over half as many taps — K drops
+        # from kh*kw*8 to kh*ceil(kw/2)*8 (ResNet50 7x7: 392 -> 224).
+        readers = [n for n in graph.nodes if getattr(n, "inp", None) == graph.input]
+        self.stem = readers[0] if (len(readers) == 1 and isinstance(readers[0], Conv) and readers[0].cin == 3
+                                   and readers[0].in_coff == 0 and readers[0].kw > 1) else None
+        self.stem_lpad = self.stem.pw if self.stem is not None else 0
         self._upload_weights(weights)
         self._alloc_buffers()
         self._build_plan()
@@ -63,8 +83,14 @@ class Engine:
         for n in self.g.nodes:
             if isinstance(n, Conv):
                 k, b = fold_conv(n, w)
-                cin_eff = _r(n.cin, 8)
-                K = n.kh * n.kw * cin_eff
+                if n is self.stem:
+                    k = pair_pack_kernel(k)
+                    kw = k.shape[1]
+                    cin_eff = 8
+                    K = n.kh * kw * cin_eff
+                else:
+                    cin_eff = _r(n.cin, 8)
+                    K = n.kh * n.kw * cin_eff
                 coutp, kpad = _r(n.cout, 256), _r(K, 64)
                 wk = pack_conv_weight(k, cin_eff, coutp, kpad)
             elif isinstance(n, Dense):
@@ -116,6 +142,8 @@ class Engine:
                 idx += 1
                 t = g.tensors[name]
                 numel = B * t.h * t.w * self.cbuf[name]
+                if name == g.input and self.stem is not None:
+                    numel = B * t.h * (t.w + self.stem_lpad) * 8
                 if name in (g.logits,):
                     self.buf[name] = torch.empty((B, t.c), device=self.device, dtype=torch.float32)
                     continue
@@ -139,6 +167,8 @@ class Engine:
         t = self.g.tensors[name]
         if name == self.g.logits:
             return self.buf[name]
+        if name == self.g.input and self.stem is not None:
+            return self.buf[name].view(self.batch, t.h, t.w + self.stem_lpad, 8)
         return self.buf[name].view(self.batch, t.h, t.w, self.cbuf[name])
 
     # --------------------------------------------------------------- plan ----
@@ -161,7 +191,8 @@ class Engine:
         self.op_names: List[str] = []
         self.op_cfg: Dict[str, int] = {}
         pa = N.PreprocArgs(src.data_ptr(), self.buf[g.input].data_ptr(), B, self.src_hw[0], self.src_hw[1],
-                           g.input_hw[0], g.input_hw[1], 0 if g.preprocess == "caffe" else 1)
+                           g.input_hw[0], g.input_hw[1], 0 if g.preprocess == "caffe" else 1,
+                           int(self.stem is not None), self.stem_lpad)
         N.check(L.dml_plan_add_preprocess(plan, C.byref(pa)), "plan preprocess")
         self.op_names.append("preprocess")
         for n in g.nodes:
@@ -196,16 +227,19 @@ class Engine:
             x = self.buf[n.inp]
             return N.ConvArgs(x.data_ptr(), wk.data_ptr(), bias.data_ptr(), None, self.buf[n.out].data_ptr(),
                               B, 1, 1, cin_eff, self.cbuf[n.inp], 1, 1, 1, 1, 0, 0, 1, 1, n.cout, K, kpad,
-                              n.cout, 0, 0, 1)
+                              n.cout, 0, 0, 1, 1, 1)
         h, w, _ = g.shape(n.inp)
         ho, wo, _ = g.shape(n.out)
         x = self.buf[n.inp].data_ptr() + 2 * n.in_coff
         y = self.buf[n.out].data_ptr() + 2 * n.out_coff
         res = self.buf[n.residual].data_ptr() if n.residual else None
         ldr = self.cbuf[n.residual] if n.residual else 0
-        return N.ConvArgs(x, wk.data_ptr(), bias.data_ptr(), res, y, B, h, w, cin_eff, self.cbuf[n.inp],
-                          n.kh, n.kw, n.sh, n.sw, n.ph, n.pw, ho, wo, n.cout, K, kpad,
-                          self.cbuf[n.out], ldr, int(n.relu), int(n.out_f32))
+        kw, pw, dw, ldx = n.kw, n.pw, 1, self.cbuf[n.inp]
+        if n is self.stem:  # pair-packed input: physical col = logical col + lpad, 2 taps per chunk
+            kw, pw, dw, w, ldx = (n.kw + 1) // 2, n.pw - self.stem_lpad, 2, w + self.stem_lpad, 8
+        return N.ConvArgs(x, wk.data_ptr(), bias.data_ptr(), res, y, B, h, w, cin_eff, ldx,
+                          n.kh, kw, n.sh, n.sw, n.ph, pw, ho, wo, n.cout, K, kpad,
+                          self.cbuf[n.out], ldr, int(n.relu), int(n.out_f32), 1, dw)
 
     # ---------------------------------------------------------------- run ----
     def run(self, stream=None, use_graph: bool = False, slot: int = 0) -> None:

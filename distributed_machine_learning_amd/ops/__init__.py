@@ -37,12 +37,15 @@ def pack_weight(w_oihw: torch.Tensor, cin_eff: Optional[int] = None) -> Tuple[to
 def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cout: int, kh: int, kw: int,
                 stride=(1, 1), pad=(0, 0), relu: bool = False, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, out_coff: int = 0, in_coff: int = 0, cin: Optional[int] = None,
-                out_f32: bool = False, cfg: int = -1, K: Optional[int] = None) -> torch.Tensor:
+                out_f32: bool = False, cfg: int = -1, K: Optional[int] = None, dilation=(1, 1),
+                out_hw: Optional[Tuple[int, int]] = None) -> torch.Tensor:
     """x: NHWC bf16 [N,H,W,Cbuf] (Cbuf % 8 == 0). Returns/updates NHWC output."""
     n, h, w_, cbuf = x.shape
     cin = cin if cin is not None else cbuf - in_coff
-    ho = (h + 2 * pad[0] - kh) // stride[0] + 1
-    wo = (w_ + 2 * pad[1] - kw) // stride[1] + 1
+    ho = (h + 2 * pad[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    wo = (w_ + 2 * pad[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    if out_hw is not None:
+        ho, wo = out_hw
     if out is None:
         out = torch.empty((n, ho, wo, _r(cout, 8)), device=x.device,
                           dtype=torch.float32 if out_f32 else torch.bfloat16)
@@ -55,7 +58,8 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
     a = N.ConvArgs(x.data_ptr() + 2 * in_coff, w_packed.data_ptr(), bias_p.data_ptr(),
                    residual.data_ptr() if residual is not None else None, out.data_ptr() + esz * out_coff,
                    n, h, w_, cin, cbuf, kh, kw, stride[0], stride[1], pad[0], pad[1], ho, wo, cout, K, kpad,
-                   out.shape[-1], residual.shape[-1] if residual is not None else 0, int(relu), int(out_f32))
+                   out.shape[-1], residual.shape[-1] if residual is not None else 0, int(relu), int(out_f32),
+                   dilation[0], dilation[1])
     L = N.lib()
     if cfg < 0:
         cfg = L.dml_conv_pick_cfg(C.byref(a))
@@ -96,10 +100,13 @@ def softmax_top5(logits: torch.Tensor, want_probs: bool = True):
     return probs, idx, p
 
 
-def preprocess(images_u8: torch.Tensor, out_hw, mode: str) -> torch.Tensor:
+def preprocess(images_u8: torch.Tensor, out_hw, mode: str, pair: bool = False, lpad: int = 0) -> torch.Tensor:
+    """uint8 NHWC -> bf16 NHWC8. pair=True writes the pair-packed stem layout
+    [n][h][lpad + w][pixel j-lpad (3ch), 0, pixel j-lpad+1 (3ch), 0]."""
     n, hs, ws, _ = images_u8.shape
-    out = torch.empty((n, out_hw[0], out_hw[1], 8), device=images_u8.device, dtype=torch.bfloat16)
+    wout = out_hw[1] + (lpad if pair else 0)
+    out = torch.empty((n, out_hw[0], wout, 8), device=images_u8.device, dtype=torch.bfloat16)
     a = N.PreprocArgs(images_u8.data_ptr(), out.data_ptr(), n, hs, ws, out_hw[0], out_hw[1],
-                      0 if mode == "caffe" else 1)
+                      0 if mode == "caffe" else 1, int(pair), lpad)
     N.check(N.lib().dml_preprocess(C.byref(a), N.stream_ptr()), "preprocess")
     return out

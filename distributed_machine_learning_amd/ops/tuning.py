@@ -18,7 +18,7 @@ from typing import Dict, Iterable, List, Optional, Tuple
 
 from .. import _native as N
 
-V2_CFGS = (10, 11, 12, 13, 14, 15, 16)
+V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18)
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))
@@ -27,7 +27,7 @@ _lock = threading.Lock()
 
 def shape_key(a: N.ConvArgs) -> str:
     return (f"n{a.N}_h{a.H}_w{a.W}_c{a.Cin}_ld{a.ldx}_k{a.kh}x{a.kw}_s{a.sh}x{a.sw}_p{a.ph}x{a.pw}"
-            f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}")
+            f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}_d{max(a.dh, 1)}x{max(a.dw, 1)}")
 
 
 def load_cache(path: str = CACHE_PATH) -> Dict[str, int]:

@@ -43,7 +43,7 @@ def _pads(kh, kw, pad):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 15, 16, 17])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 15, 16, 17, 18])
 def test_conv_matches_fp32(case, cfg):
     n, h, w, cin, cout, kh, kw, s, pad, relu, has_res = case
     ph, pw = (kh // 2, kw // 2) if pad else (0, 0)
@@ -165,3 +165,28 @@ def test_preprocess(mode, hw):
     got = y.float().cpu().permute(0, 3, 1, 2)
     assert torch.all(got[:, 3:] == 0)
     assert (got[:, :3] - ref).abs().max().item() < 0.6  # bf16 rounding of values up to ~150
+
+
+@pytest.mark.parametrize("kh,kw,s,p,hw,mode", [(7, 7, 2, 3, (224, 224), "caffe"), (3, 3, 2, 0, (299, 299), "tf")])
+@pytest.mark.parametrize("cfg", [-1, 0, 15])
+def test_pair_packed_stem(kh, kw, s, p, hw, mode, cfg):
+    """preprocess(pair=True) + dilation-2 conv with pair-packed weights == the plain
+    stem conv on the normal preprocess output."""
+    from distributed_machine_learning_amd.models.engine import _r, pack_conv_weight, pair_pack_kernel
+    from distributed_machine_learning_amd.models.oracle import preprocess_reference
+
+    torch.manual_seed(7)
+    img = torch.randint(0, 256, (2, hw[0], hw[1], 3), dtype=torch.uint8)
+    k = torch.randn(kh, kw, 3, 64) * 0.05
+    b = torch.randn(64) * 0.1
+    x = _bf(preprocess_reference(img, hw, mode))
+    ref = F.relu(F.conv2d(x, _bf(k.permute(3, 2, 0, 1)), b, stride=s, padding=p))
+    xp = ops.preprocess(img.cuda(), hw, mode, pair=True, lpad=p)
+    kp = pair_pack_kernel(k.numpy())
+    K = kh * kp.shape[1] * 8
+    wp = torch.from_numpy(pack_conv_weight(kp, 8, 256, _r(K, 64))).to(torch.bfloat16).cuda()
+    y = ops.conv2d_nhwc(xp, wp, b.cuda(), 64, kh, kp.shape[1], (s, s), (p, 0), relu=True, dilation=(1, 2),
+                        K=K, cfg=cfg, out_hw=tuple(ref.shape[2:]))
+    torch.cuda.synchronize()
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    assert _rel(got, ref) < 1.5e-2, _rel(got, ref)

@@ -92,3 +92,30 @@ def test_inception_concat_offsets():
         assert ranges[0][0] == 0 and ranges[-1][1] == g.shape(name)[2], name
         for (a0, a1), (b0, b1) in zip(ranges, ranges[1:]):
             assert a1 == b0, (name, ranges)
+
+
+def test_pair_packed_stem_equivalence():
+    """The engine's stem lowering: 2 horizontal taps per 8-channel chunk + dilation 2
+    over a left-padded pair-packed input == the original conv (ResNet 7x7/2 p3, Inception 3x3/2 p0)."""
+    from distributed_machine_learning_amd.models.engine import pair_pack_kernel
+
+    torch.manual_seed(0)
+    for kh, kw, s, p in ((7, 7, 2, 3), (3, 3, 2, 0)):
+        x = torch.randn(2, 3, 23, 21)
+        k = torch.randn(kh, kw, 3, 16)  # HWIO
+        ref = F.conv2d(x, k.permute(3, 2, 0, 1), stride=s, padding=p)
+        lpad = p
+        n, c, h, w = x.shape
+        xp = torch.zeros(n, 8, h, w + lpad)
+        for j in range(w + lpad):
+            q = j - lpad
+            if 0 <= q < w:
+                xp[:, 0:3, :, j] = x[:, :, :, q]
+            if 0 <= q + 1 < w:
+                xp[:, 4:7, :, j] = x[:, :, :, q + 1]
+        kp = torch.from_numpy(pair_pack_kernel(k.numpy()))  # [kh, kw2, 8, co]
+        # physical pad: left pad already materialised, right side zero-fill, vertical p
+        xpp = F.pad(xp, (0, 2 * kp.shape[1], p, p))
+        got = F.conv2d(xpp, kp.permute(3, 2, 0, 1), stride=s, dilation=(1, 2))
+        got = got[:, :, : ref.shape[2], : ref.shape[3]]
+        assert torch.allclose(got, ref, atol=1e-4), (kh, (got - ref).abs().max())
