@@ -82,7 +82,12 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   const int lrow = lane >> 3;                  // row within an 8-row DMA piece
   const int lchunk = (lane & 7) ^ lrow;        // logical K chunk this lane always fetches
   // X rows of this lane: piece q = wid*XI + j -> row 8q + lrow
-  int pix0[T::XI], ih0[T::XI], iw0[T::XI];
+  // Element offset of (row, k) = base[row] + koff(k) with
+  //   base[row] = (pix0 + ih0*W + iw0) * ldx          (per row, fixed)
+  //   koff(k)   = (rr*dh*W + ss*dw) * ldx + cc        (per lane, row-independent)
+  // so the K loop does one add per row (no multiplies); the bounds test uses the
+  // running tap displacement (dih, diw).
+  int base[T::XI], ih0[T::XI], iw0[T::XI];
   const int HoWo = a.Ho * a.Wo;
 #pragma unroll
   for (int j = 0; j < T::XI; ++j) {
@@ -92,17 +97,36 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
       const int rem = m - n * HoWo;
       const int oh = rem / a.Wo;
       const int ow = rem - oh * a.Wo;
-      pix0[j] = n * a.H * a.W;
       ih0[j] = oh * a.sh - a.ph;
       iw0[j] = ow * a.sw - a.pw;
+      base[j] = (n * a.H * a.W + ih0[j] * a.W + iw0[j]) * a.ldx;
     } else {
-      pix0[j] = 0;
-      ih0[j] = -(1 << 28);
+      base[j] = 0;
+      ih0[j] = -(1 << 28);  // fails every bounds test: zero row
       iw0[j] = 0;
     }
   }
-  int cc = lchunk * 8, ss = 0, rr = 0;
-  while (cc >= a.Cin) { cc -= a.Cin; if (++ss == a.kw) { ss = 0; ++rr; } }
+  const int dh = a.dh > 0 ? a.dh : 1, dw = a.dw > 0 ? a.dw : 1;
+  const int step_s = dw * a.ldx;                 // koff change for ss += 1
+  const int step_r = dh * a.W * a.ldx;           // koff change for rr += 1
+  int cc = lchunk * 8, ss = 0, rr = 0, dih = 0, diw = 0, koff = lchunk * 8;
+  auto advance = [&](int by) {
+    cc += by;
+    koff += by;
+    while (cc >= a.Cin) {
+      cc -= a.Cin;
+      koff += step_s - a.Cin;
+      diw += dw;
+      if (++ss == a.kw) {
+        ss = 0;
+        koff += step_r - a.kw * step_s;
+        diw = 0;
+        ++rr;
+        dih = rr < a.kh ? dih + dh : (1 << 28);  // K tail: every row out of bounds -> zeros
+      }
+    }
+  };
+  advance(0);
 
   // buffer descriptor over the activations (range check -> zero fill)
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, 0x7ffffff0, 0x00020000);
@@ -111,17 +135,16 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   const long wstep_row = (long)8 * a.Kpad * 2;  // next 8-row piece
 
   const int nk = a.Kpad / T::BK;
-  const int dh = a.dh > 0 ? a.dh : 1, dw = a.dw > 0 ? a.dw : 1;
 
   auto issue = [&](int kt, int stage) {
     char* sx = smem + stage * T::STAGE_BYTES;
     char* sw = sx + BM * T::ROWB;
-    const bool kval = rr < a.kh;
 #pragma unroll
     for (int j = 0; j < T::XI; ++j) {
-      const int ih = ih0[j] + rr * dh, iw = iw0[j] + ss * dw;
-      const bool ok = kval && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const unsigned off = ok ? (unsigned)(((pix0[j] + ih * a.W + iw) * a.ldx + cc) * 2) : OOB;
+      const int ih = ih0[j] + dih, iw = iw0[j] + diw;
+      const unsigned ok = ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
+      const unsigned msk = 0u - ok;  // branch-free select (no exec-mask split around the DMA)
+      const unsigned off = ((unsigned)((base[j] + koff) * 2) & msk) | (OOB & ~msk);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 0);
     }
 #pragma unroll
@@ -129,8 +152,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
       const char* src = wbase + j * wstep_row + (long)kt * T::BK * 2;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sw + (wid * T::WI + j) * 1024), 16, 0, 0);
     }
-    cc += T::BK;
-    while (cc >= a.Cin) { cc -= a.Cin; if (++ss == a.kw) { ss = 0; ++rr; } }
+    advance(T::BK);
   };
 
   f32x4 acc[T::FI][T::FJ];
@@ -180,22 +202,27 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const char* sx = smem + (kt % STAGES) * T::STAGE_BYTES;
     const char* sw = sx + BM * T::ROWB;
+    // Both 32-deep k-steps' fragments are read up front (separate registers), so
+    // the second step's ds_reads are in flight while the first step's MFMAs run;
+    // hipcc emits a counted lgkmcnt before each MFMA group.
+    bf16x8 fa[2][T::FI], fb[2][T::FJ];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + fq;
-      bf16x8 fa[T::FI], fb[T::FJ];
 #pragma unroll
-      for (int i = 0; i < T::FI; ++i) fa[i] = *(const bf16x8*)(sw + lds_swz(wc * T::WTC + i * 16 + frow, ch));
+      for (int i = 0; i < T::FI; ++i) fa[ks][i] = *(const bf16x8*)(sw + lds_swz(wc * T::WTC + i * 16 + frow, ch));
 #pragma unroll
-      for (int j = 0; j < T::FJ; ++j) fb[j] = *(const bf16x8*)(sx + lds_swz(wp * T::WTP + j * 16 + frow, ch));
-      __builtin_amdgcn_s_setprio(1);
+      for (int j = 0; j < T::FJ; ++j) fb[ks][j] = *(const bf16x8*)(sx + lds_swz(wp * T::WTP + j * 16 + frow, ch));
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < T::FI; ++i)
 #pragma unroll
         for (int j = 0; j < T::FJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
   }
 
   // ---- epilogue: acc -> LDS (fp32) -> coalesced bias/residual/ReLU/store ----
