@@ -1,0 +1,75 @@
+"""Host-side SWIM failure detector for the ranks of one collective job.
+
+Each rank runs the cluster/ SWIM detector (UDP on 127.0.0.1:base_port+rank) in
+a daemon thread with its own asyncio loop; a rank confirmed dead is added to
+``ElasticGroup.dead`` so pending collectives abort and the coordinator starts a
+new communicator epoch. This keeps liveness independent of RCCL, which cannot
+report a dead peer (SURVEY §2.6 "gossip all-to-all" row).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import threading
+from typing import Callable, Optional, Set
+
+from ..cluster.failure_detector import FailureDetector
+from ..cluster.membership import MembershipList
+from ..cluster.transport import Endpoint, UdpTransport
+
+log = logging.getLogger(__name__)
+
+
+class RankFailureDetector:
+    def __init__(self, grank: int, world: int, base_port: int, on_dead: Callable[[int], None],
+                 host: str = "127.0.0.1", period: float = 0.1, ping_timeout: float = 0.1,
+                 suspect_timeout: float = 0.5):
+        self.grank, self.world, self.base, self.host = grank, world, base_port, host
+        self.on_dead = on_dead
+        self.period, self.ping_timeout, self.suspect_timeout = period, ping_timeout, suspect_timeout
+        self.loop: Optional[asyncio.AbstractEventLoop] = None
+        self.ready = threading.Event()
+        self.thread = threading.Thread(target=self._main, daemon=True, name=f"swim-{grank}")
+        self.dead: Set[int] = set()
+
+    def name(self, r: int) -> str:
+        return f"{self.host}:{self.base + r}"
+
+    def rank_of(self, name: str) -> int:
+        return int(name.rsplit(":", 1)[1]) - self.base
+
+    def start(self) -> "RankFailureDetector":
+        self.thread.start()
+        self.ready.wait(10)
+        return self
+
+    def _main(self) -> None:
+        self.loop = asyncio.new_event_loop()
+        asyncio.set_event_loop(self.loop)
+        self.loop.run_until_complete(self._run())
+
+    async def _run(self) -> None:
+        t = await UdpTransport(self.host, self.base + self.grank).start()
+        ep = Endpoint(t)
+        ml = MembershipList(t.name, suspect_timeout=self.suspect_timeout, cleanup_time=30.0,
+                            meta={"role": "worker", "rank": self.grank})
+        # every rank knows the static job membership up front (torchrun world)
+        ml.merge({self.name(r): [0, 1, {"rank": r}] for r in range(self.world) if r != self.grank})
+
+        def failed(name: str) -> None:
+            r = self.rank_of(name)
+            if r not in self.dead:
+                self.dead.add(r)
+                log.warning("rank %d: SWIM confirmed rank %d dead", self.grank, r)
+                self.on_dead(r)
+
+        ml.on_fail.append(failed)
+        self.fd = FailureDetector(ep, ml, period=self.period, ping_timeout=self.ping_timeout)
+        ep.start()
+        self.fd.start()
+        self.ready.set()
+        await asyncio.Event().wait()
+
+    def stop(self) -> None:
+        if self.loop is not None:
+            self.loop.call_soon_threadsafe(self.loop.stop)

@@ -91,6 +91,15 @@ class JobManager:
         self.queues[model].extend(batches)
         return job
 
+    def submit_images(self, model: str, images: List[str], requester: str, now: float = 0.0) -> Job:
+        """Submit an explicit image list (already selected) as one job."""
+        jid = self.next_id()
+        batches = make_batches(jid, model, list(images), self.batch_sizes[model])
+        job = Job(jid, model, len(images), requester, len(batches), 0, now)
+        self.jobs[jid] = job
+        self.queues[model].extend(batches)
+        return job
+
     def set_batch_size(self, model: str, bs: int) -> None:
         if bs < 1:
             raise ValueError("batch size must be >= 1")

@@ -14,6 +14,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--model", default="ResNet50"); ap.add_argument("--batch", type=int, default=256)
 ap.add_argument("--cfgs", default="0,1,2,10,11,12,13,14,15,16,17"); ap.add_argument("--out", default="")
 ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--only", default="", help="comma list of layer-name substrings to keep")
 args = ap.parse_args()
 g = build_graph(args.model); B = args.batch
 L = N.lib(); N.ensure_device_init()
@@ -27,6 +28,8 @@ for n in g.conv_nodes():
 res = []
 s = torch.cuda.current_stream()
 for key, names in shapes.items():
+    if args.only and not any(o in names[0] for o in args.only.split(",")):
+        continue
     h, w, cin, cout, kh, kw, st, ph, pw, hasres = key
     ho = (h + 2 * ph - kh) // st + 1; wo = (w + 2 * pw - kw) // st + 1
     K = kh * kw * cin; Kp = r(K, 64)
