@@ -46,7 +46,9 @@ class RankFailureDetector:
     def _main(self) -> None:
         self.loop = asyncio.new_event_loop()
         asyncio.set_event_loop(self.loop)
-        self.loop.run_until_complete(self._run())
+        self.loop.create_task(self._run())
+        self.loop.run_forever()
+        self.loop.close()
 
     async def _run(self) -> None:
         t = await UdpTransport(self.host, self.base + self.grank).start()
@@ -70,6 +72,21 @@ class RankFailureDetector:
         self.ready.set()
         await asyncio.Event().wait()
 
+    async def _shutdown(self) -> None:
+        self.fd.stop()
+        self.fd.ep.stop()
+        tasks = [t for t in asyncio.all_tasks() if t is not asyncio.current_task()]
+        for t in tasks:
+            t.cancel()
+        await asyncio.gather(*tasks, return_exceptions=True)
+
     def stop(self) -> None:
-        if self.loop is not None:
-            self.loop.call_soon_threadsafe(self.loop.stop)
+        """Cancel the detector's tasks, close its socket and join the thread."""
+        if self.loop is None or not self.thread.is_alive():
+            return
+        try:
+            asyncio.run_coroutine_threadsafe(self._shutdown(), self.loop).result(timeout=5)
+        except Exception:  # pragma: no cover - best effort at exit
+            pass
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self.thread.join(timeout=5)

@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""BASELINE configs 4 and 5 on GPUs: concurrent ResNet50 + InceptionV3 jobs
+served by the elastic collective service (one process per GPU, RCCL data
+plane, SWIM liveness, fair-share scheduler with per-model batch sizes = C3),
+optionally with injected worker kills mid-job.
+
+  torchrun --nproc-per-node N tools/serve_bench.py --resnet-images 20480 --inception-images 10240 \
+      [--kill 3:5 --kill 6:9]          # kill global rank 3 at step 5, rank 6 at step 9
+  python tools/serve_bench.py ...      # N = 1
+
+Prints one JSON line (rank 0): total images/s, per-model images/s, p50/p90
+query (batch) latency, steps, rebuilds.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--resnet-images", type=int, default=20480)
+    ap.add_argument("--inception-images", type=int, default=10240)
+    ap.add_argument("--resnet-batch", type=int, default=256)
+    ap.add_argument("--inception-batch", type=int, default=128)
+    ap.add_argument("--kill", action="append", default=[], help="rank:step")
+    ap.add_argument("--out-dir", default="")
+    ap.add_argument("--store-port", type=int, default=0)
+    ap.add_argument("--swim-port", type=int, default=0)
+    a = ap.parse_args()
+
+    import torch
+
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+    from distributed_machine_learning_amd.parallel.fd_thread import RankFailureDetector
+    from distributed_machine_learning_amd.parallel.service import (CollectiveCoordinator, CollectiveService,
+                                                                   GpuRankBackend)
+
+    grank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    base = int(os.environ.get("MASTER_PORT", 29500))
+    store_port = a.store_port or base + 17
+    swim_port = a.swim_port or base + 100
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    bs = {"ResNet50": a.resnet_batch, "InceptionV3": a.inception_batch}
+    backend = GpuRankBackend(dev, bs, arena_images=2 * max(bs.values()))
+    eg = ElasticGroup(grank, world, port=store_port, backend="nccl", device=dev, timeout_s=120)
+    fd = RankFailureDetector(grank, world, swim_port, on_dead=eg.dead.add).start()
+    kills = [tuple(int(x) for x in k.split(":")) for k in a.kill]
+    kr, ks = (kills[0] if kills else (-1, -1))
+    for r, s in kills:
+        if r == grank:
+            kr, ks = r, s
+    coord = None
+    if grank == 0:
+        coord = CollectiveCoordinator(bs, {"ResNet50": 2 * bs["ResNet50"], "InceptionV3": 2 * bs["InceptionV3"]},
+                                      out_dir=a.out_dir or None, host_tag="mi355x")
+        jobs = []
+        if a.resnet_images:
+            jobs.append(coord.submit("ResNet50", a.resnet_images))
+        if a.inception_images:
+            jobs.append(coord.submit("InceptionV3", a.inception_images))
+    svc = CollectiveService(eg, backend, coord, kill_rank=kr, kill_at_step=ks, on_device=True)
+    # warm both engines (graph capture) outside the timed region
+    for m in ("ResNet50", "InceptionV3"):
+        backend.run(m, 0, bs[m])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    steps = svc.serve()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if grank == 0:
+        coord.flush()
+        c1, c2 = coord.metrics.c1(), coord.metrics.c2()
+        n_r = coord.metrics.query_count.get("ResNet50", 0)
+        n_i = coord.metrics.query_count.get("InceptionV3", 0)
+        out = {"metric": "concurrent ResNet50+InceptionV3 serving (images/s, whole job)",
+               "value": round((n_r + n_i) / el, 1), "unit": "images/s", "n_gpus": world,
+               "resnet50_images_per_s": round(n_r / el, 1), "inceptionv3_images_per_s": round(n_i / el, 1),
+               "elapsed_s": round(el, 3), "steps": steps, "rebuilds": svc.rebuilds, "final_members": eg.members,
+               "requeued_batches": coord.requeued,
+               "jobs_done": [coord.jobs.jobs[j].done for j in jobs],
+               "p50_latency_ms": {m: round(v["query_latency_p50"] * 1e3, 3) for m, v in c2.items()},
+               "p90_latency_ms": {m: round(v["query_latency_p90"] * 1e3, 3) for m, v in c2.items()},
+               "batch_sizes": bs, "kills": a.kill, "dtype": "bf16", "data": "synthetic"}
+        print(json.dumps(out), flush=True)
+    fd.stop()
+    eg.close()
+
+
+if __name__ == "__main__":
+    main()
