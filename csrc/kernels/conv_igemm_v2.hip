@@ -63,7 +63,7 @@ struct Cfg {
 
 __device__ __forceinline__ int lds_swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
-template <int BM, int BN, int WM, int WN, int STAGES>
+template <int BM, int BN, int WM, int WN, int STAGES, bool RES>
 __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   using T = Cfg<BM, BN, WM, WN, STAGES>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -186,11 +186,15 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
     bias0 = *(const float4*)(a.bias + ch_t);
     bias1 = *(const float4*)(a.bias + ch_t + 4);
   }
-  uint4 rpre[EIT];
+  // RES is a template parameter: the residual prefetch costs 4*EIT VGPRs,
+  // which would cut occupancy of the (residual-free) compute-bound 3x3 layers.
+  uint4 rpre[RES ? EIT : 1];
+  if constexpr (RES) {
 #pragma unroll
-  for (int it = 0; it < EIT; ++it) {
-    const int m = m0 + (tid + it * T::NT) / CG;
-    rpre[it] = (rg && ch_ok && m < M) ? *(const uint4*)(rg + (long)m * a.ldr + ch_t) : make_uint4(0, 0, 0, 0);
+    for (int it = 0; it < EIT; ++it) {
+      const int m = m0 + (tid + it * T::NT) / CG;
+      rpre[it] = (ch_ok && m < M) ? *(const uint4*)(rg + (long)m * a.ldr + ch_t) : make_uint4(0, 0, 0, 0);
+    }
   }
 
   for (int kt = 0; kt < nk; ++kt) {
@@ -247,7 +251,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
     const float4 b0 = bias0, b1 = bias1;
     float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
                   v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
-    if (rg) {
+    if constexpr (RES) {
       const uint4 r = rpre[it];
       f[0] += bf2f(r.x & 0xffff); f[1] += bf2f(r.x >> 16);
       f[2] += bf2f(r.y & 0xffff); f[3] += bf2f(r.y >> 16);
@@ -274,7 +278,12 @@ static int launch(const DmlConvArgs* a, hipStream_t s) {
   using T = Cfg<BM, BN, WM, WN, STAGES>;
   const long M = (long)a->N * a->Ho * a->Wo;
   const long tiles = ((M + BM - 1) / BM) * ((a->Cout + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES>), dim3((unsigned)tiles), dim3(T::NT), T::LDS, s, *a);
+  if (a->res)
+    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, true>), dim3((unsigned)tiles), dim3(T::NT), T::LDS, s,
+                       *a);
+  else
+    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, false>), dim3((unsigned)tiles), dim3(T::NT), T::LDS,
+                       s, *a);
   DML_CHECK_LAUNCH();
   return 0;
 }
@@ -282,7 +291,9 @@ static int launch(const DmlConvArgs* a, hipStream_t s) {
 template <int BM, int BN, int WM, int WN, int STAGES>
 static int set_attr() {
   using T = Cfg<BM, BN, WM, WN, STAGES>;
-  return (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES>,
+  return (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS) |
+         (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
@@ -303,6 +314,10 @@ extern "C" int dml_conv_v2_init(void) {
   rc |= set_attr<256, 128, 4, 2, 2>();
   rc |= set_attr<128, 128, 2, 2, 3>();
   rc |= set_attr<256, 32, 4, 1, 2>();
+  rc |= set_attr<128, 128, 2, 4, 3>();
+  rc |= set_attr<128, 128, 4, 2, 3>();
+  rc |= set_attr<128, 256, 2, 4, 2>();
+  rc |= set_attr<64, 256, 1, 4, 2>();
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   return rc ? -1 : 0;
 }
@@ -320,6 +335,10 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
     case 16: return launch<256, 128, 4, 2, 2>(a, s);  // 8 waves, 2-stage
     case 17: return launch<128, 128, 2, 2, 3>(a, s);  // 4 waves, 3-stage
     case 18: return launch<256, 32, 4, 1, 2>(a, s);   // 4 waves, 64px x 32ch per wave (Cout = 32 layers)
+    case 19: return launch<128, 128, 2, 4, 3>(a, s);  // 8 waves, 64px x 32ch per wave, 3-stage
+    case 20: return launch<128, 128, 4, 2, 3>(a, s);  // 8 waves, 32px x 64ch per wave, 3-stage
+    case 21: return launch<128, 256, 2, 4, 2>(a, s);  // 8 waves, 64x64 per wave, 2-stage
+    case 22: return launch<64, 256, 1, 4, 2>(a, s);   // 4 waves, 64px x 64ch per wave
     default: dml_set_error("dml_conv_v2: bad cfg"); return -1;
   }
 }
