@@ -33,6 +33,15 @@ typedef struct {
   int ldy, ldr;
   int relu, out_f32;
   int dh, dw;         // tap dilation (0 is treated as 1); dw = 2 serves the pair-packed stem
+  // Output segments (v2 kernels only): when nseg > 0, output channels
+  // [seg_c0[s], seg_c0[s+1]) go to seg_y[s] (+ channel - seg_c0[s]) with row
+  // stride seg_ldy[s] and ReLU flag seg_relu[s] — sibling 1x1 convs that read the
+  // same input run as ONE GEMM scattering into their own destinations.
+  int nseg;
+  int seg_c0[4];
+  int seg_ldy[4];
+  int seg_relu[4];
+  void* seg_y[4];
 } DmlConvArgs;
 
 typedef struct {
@@ -42,6 +51,7 @@ typedef struct {
   int Ho, Wo, ldy;
   int k, stride, pad;  // square window
   int mode;            // 0 = max (padding never wins), 1 = avg with padding excluded from the divisor
+  int relu;            // apply ReLU to the pooled value (avg-pool after a pre-pool 1x1 conv)
 } DmlPoolArgs;
 
 typedef struct {

@@ -242,7 +242,15 @@ extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
       dml_set_error("dml_conv(v2): need Cin, ldx, Cout, ldy, ldr %8==0 and Kpad%64==0");
       return -1;
     }
+    if (a->nseg < 0 || a->nseg > 4) {
+      dml_set_error("dml_conv(v2): nseg must be 0..4");
+      return -1;
+    }
     return dml_conv_v2(a, cfg, s);
+  }
+  if (a->nseg > 0) {
+    dml_set_error("dml_conv: output segments need a v2 config (cfg >= 10)");
+    return -1;
   }
   if (a->Cin % 8 || a->ldx % 8 || a->Cout % 4 || a->Kpad % 64) {
     dml_set_error("dml_conv: need Cin%8==0, ldx%8==0, Cout%4==0, Kpad%64==0");

@@ -240,11 +240,25 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
       *(f32x4*)(smem + px * T::CROW + ch * 4) = acc[i][j];
     }
   __syncthreads();
+  // Destination of this thread's channel group: the plain output, or (fused
+  // sibling convs) the segment that owns channel ch_t. Resolved once per thread.
+  void* ybase = a.y;
+  int ldy = a.ldy, relu = a.relu, choff = ch_t;
+  if (a.nseg > 0) {
+    int sgi = 0;
+#pragma unroll
+    for (int q = 1; q < 4; ++q)
+      if (q < a.nseg && ch_t >= a.seg_c0[q]) sgi = q;
+    ybase = a.seg_y[sgi];
+    ldy = a.seg_ldy[sgi];
+    relu = a.seg_relu[sgi];
+    choff = ch_t - a.seg_c0[sgi];
+  }
 #pragma unroll
   for (int it = 0; it < EIT; ++it) {
     const int e = tid + it * T::NT;
     const int px = e / CG, cg = cg_t;
-    const int m = m0 + px, ch = ch_t;
+    const int m = m0 + px, ch = choff;
     if (m >= M || !ch_ok) continue;
     const float4 v0 = *(const float4*)(smem + px * T::CROW + cg * 32);
     const float4 v1 = *(const float4*)(smem + px * T::CROW + cg * 32 + 16);
@@ -258,16 +272,16 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
       f[4] += bf2f(r.z & 0xffff); f[5] += bf2f(r.z >> 16);
       f[6] += bf2f(r.w & 0xffff); f[7] += bf2f(r.w >> 16);
     }
-    if (a.relu) {
+    if (relu) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) f[q] = fmaxf(f[q], 0.f);
     }
     if (a.out_f32) {
-      float* yp = (float*)a.y + (long)m * a.ldy + ch;
+      float* yp = (float*)ybase + (long)m * ldy + ch;
       *(float4*)yp = make_float4(f[0], f[1], f[2], f[3]);
       *(float4*)(yp + 4) = make_float4(f[4], f[5], f[6], f[7]);
     } else {
-      *(uint4*)((unsigned short*)a.y + (long)m * a.ldy + ch) =
+      *(uint4*)((unsigned short*)ybase + (long)m * ldy + ch) =
           make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
     }
   }

@@ -74,6 +74,10 @@ __global__ __launch_bounds__(256) void pool3x3_kernel(DmlPoolArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] *= inv;
     }
+    if (a.relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fmaxf(acc[j], 0.f);
+    }
     *(uint4*)(y + ((long)(n * a.Ho + oh) * a.Wo + ow) * a.ldy + cg * 8) = pack8(acc);
   }
 }

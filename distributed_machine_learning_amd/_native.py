@@ -26,6 +26,8 @@ class ConvArgs(C.Structure):
         ("ldy", C.c_int), ("ldr", C.c_int),
         ("relu", C.c_int), ("out_f32", C.c_int),
         ("dh", C.c_int), ("dw", C.c_int),
+        ("nseg", C.c_int), ("seg_c0", C.c_int * 4), ("seg_ldy", C.c_int * 4), ("seg_relu", C.c_int * 4),
+        ("seg_y", C.c_void_p * 4),
     ]
 
 
@@ -34,7 +36,7 @@ class PoolArgs(C.Structure):
         ("x", C.c_void_p), ("y", C.c_void_p),
         ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("C", C.c_int), ("ldx", C.c_int),
         ("Ho", C.c_int), ("Wo", C.c_int), ("ldy", C.c_int),
-        ("k", C.c_int), ("stride", C.c_int), ("pad", C.c_int), ("mode", C.c_int),
+        ("k", C.c_int), ("stride", C.c_int), ("pad", C.c_int), ("mode", C.c_int), ("relu", C.c_int),
     ]
 
 

@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from .. import _native as N
-from .graph import Conv, Dense, Graph, GlobalAvgPool, Pool
+from .graph import Conv, Dense, FusedConv, Graph, GlobalAvgPool, Pool, node_outputs
 from .weights import Weights, fold_conv
 
 
@@ -56,7 +56,11 @@ class Engine:
 
     def __init__(self, graph: Graph, weights: Weights, batch: int, device: str = "cuda",
                  src_hw: Optional[Tuple[int, int]] = None, cfg_overrides: Optional[Dict[str, int]] = None,
-                 src_slots: int = 1, reuse_buffers: bool = True, autotune: bool = True):
+                 src_slots: int = 1, reuse_buffers: bool = True, autotune: bool = True, optimize: bool = True):
+        if optimize:  # graph rewrites: conv-before-avgpool, sibling 1x1 fusion (models/optimize.py)
+            from .optimize import optimize as _opt
+
+            graph = _opt(graph)
         self.g, self.batch, self.device = graph, batch, torch.device(device)
         self.src_slots = src_slots
         self.reuse_buffers = reuse_buffers
@@ -100,6 +104,15 @@ class Engine:
                 K = cin_eff
                 coutp, kpad = _r(n.cout, 256), _r(K, 64)
                 wk = pack_conv_weight(k, cin_eff, coutp, kpad)
+            elif isinstance(n, FusedConv):
+                # members' folded 1x1 kernels concatenated along Cout (segment order)
+                folded = [fold_conv(m, w) for m in n.members]
+                k = np.concatenate([f[0] for f in folded], axis=3)
+                b = np.concatenate([f[1] for f in folded])
+                cin_eff = _r(n.cin, 8)
+                K = cin_eff
+                coutp, kpad = _r(n.cout, 256), _r(K, 64)
+                wk = pack_conv_weight(k, cin_eff, coutp, kpad)
             else:
                 continue
             bias = np.zeros(coutp, np.float32)
@@ -116,7 +129,8 @@ class Engine:
         nodes = g.nodes
         first_def, last_use = {g.input: -1}, {}
         for i, n in enumerate(nodes):
-            first_def.setdefault(n.out, i)
+            for o in node_outputs(n):
+                first_def.setdefault(o, i)
             for src in (n.inp, getattr(n, "residual", None)):
                 if src:
                     last_use[src] = i
@@ -177,9 +191,10 @@ class Engine:
         if self.autotune and self.device.type == "cuda":
             from ..ops import tuning
 
-            convs = [self._conv_args(n) for n in self.g.nodes if isinstance(n, (Conv, Dense))]
+            cnodes = [n for n in self.g.nodes if isinstance(n, (Conv, Dense, FusedConv))]
+            convs = [self._conv_args(n) for n in cnodes]
             table = tuning.autotune(convs)
-            for n, a in zip([n for n in self.g.nodes if isinstance(n, (Conv, Dense))], convs):
+            for n, a in zip(cnodes, convs):
                 self.tuned[n.name] = table.get(tuning.shape_key(a), -1)
         self.plans = [self._build_one_plan(self.srcs[i]) for i in range(self.src_slots)]
         self.plan = self.plans[0]
@@ -196,7 +211,7 @@ class Engine:
         N.check(L.dml_plan_add_preprocess(plan, C.byref(pa)), "plan preprocess")
         self.op_names.append("preprocess")
         for n in g.nodes:
-            if isinstance(n, (Conv, Dense)):
+            if isinstance(n, (Conv, Dense, FusedConv)):
                 a = self._conv_args(n)
                 cfg = self.cfg_overrides.get(n.name, self.tuned.get(n.name, -1))
                 used = L.dml_plan_add_conv(plan, C.byref(a), cfg)
@@ -207,7 +222,7 @@ class Engine:
                 ho, wo, co = g.shape(n.out)
                 y = self.buf[n.out].data_ptr() + 2 * n.out_coff
                 a = N.PoolArgs(self.buf[n.inp].data_ptr(), y, B, h, w, c, self.cbuf[n.inp], ho, wo, self.cbuf[n.out],
-                               n.k, n.stride, n.pad, 0 if n.mode == "max" else 1)
+                               n.k, n.stride, n.pad, 0 if n.mode == "max" else 1, int(n.relu))
                 N.check(L.dml_plan_add_pool(plan, C.byref(a)), "plan pool")
             elif isinstance(n, GlobalAvgPool):
                 h, w, c = g.shape(n.inp)
@@ -228,6 +243,23 @@ class Engine:
             return N.ConvArgs(x.data_ptr(), wk.data_ptr(), bias.data_ptr(), None, self.buf[n.out].data_ptr(),
                               B, 1, 1, cin_eff, self.cbuf[n.inp], 1, 1, 1, 1, 0, 0, 1, 1, n.cout, K, kpad,
                               n.cout, 0, 0, 1, 1, 1)
+        if isinstance(n, FusedConv):
+            m0 = n.members[0]
+            h, w, _ = g.shape(n.inp)
+            ho, wo, _ = g.shape(m0.out)
+            a = N.ConvArgs(self.buf[n.inp].data_ptr(), wk.data_ptr(), bias.data_ptr(), None,
+                           self.buf[m0.out].data_ptr() + 2 * m0.out_coff, B, h, w, cin_eff, self.cbuf[n.inp],
+                           1, 1, m0.sh, m0.sw, 0, 0, ho, wo, n.cout, K, kpad, self.cbuf[m0.out], 0, int(m0.relu), 0,
+                           1, 1)
+            a.nseg = len(n.members)
+            c0 = 0
+            for s, m in enumerate(n.members):
+                a.seg_c0[s] = c0
+                a.seg_ldy[s] = self.cbuf[m.out]
+                a.seg_relu[s] = int(m.relu)
+                a.seg_y[s] = self.buf[m.out].data_ptr() + 2 * m.out_coff
+                c0 += m.cout
+            return a
         h, w, _ = g.shape(n.inp)
         ho, wo, _ = g.shape(n.out)
         x = self.buf[n.inp].data_ptr() + 2 * n.in_coff

@@ -64,6 +64,29 @@ class Pool:
     stride: int = 2
     pad: int = 0   # symmetric; max: zero pad == ignored (inputs are post-ReLU), avg: excluded
     out_coff: int = 0
+    relu: bool = False  # ReLU after pooling (set when a 1x1 conv is moved in front of an avg pool)
+
+
+@dataclass
+class FusedConv:
+    """Sibling 1x1 convs that read the same input, run as one GEMM whose output
+    channels are scattered to each member's destination (models/optimize.py)."""
+    name: str
+    inp: str
+    cin: int
+    members: List["Conv"] = field(default_factory=list)
+
+    @property
+    def out(self) -> str:
+        return self.members[0].out
+
+    @property
+    def outs(self) -> List[str]:
+        return [m.out for m in self.members]
+
+    @property
+    def cout(self) -> int:
+        return sum(m.cout for m in self.members)
 
 
 @dataclass
@@ -156,8 +179,12 @@ class Graph:
                 eh = (h + 2 * n.pad - n.k) // n.stride + 1
                 assert eh == ho, f"{n.name}: {eh} != {ho}"
                 assert n.out_coff + c <= co, n.name
-            produced.add(n.out)
+            produced.update(node_outputs(n))
         assert self.logits in produced
+
+
+def node_outputs(n) -> List[str]:
+    return list(n.outs) if isinstance(n, FusedConv) else [n.out]
 
 
 def same_pad(k: int) -> int:

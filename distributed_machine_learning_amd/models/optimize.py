@@ -1,0 +1,104 @@
+"""Graph-level rewrites applied before lowering to the native plan.
+
+1. ``conv_before_avgpool`` — Inception's pool branch is AvgPool3x3(s1, same)
+   -> Conv1x1(+BN) -> ReLU. A 1x1 conv is a per-pixel linear map, so it commutes
+   with spatial averaging; the folded-BN bias is constant per channel and the
+   padding-excluded average of a constant is that constant. Hence
+       relu(conv(avgpool(x)) + b) == relu(avgpool(conv(x) + b))
+   exactly in real arithmetic. Running the conv first makes the pool touch
+   ``cout`` channels instead of ``cin`` (192/256/288/768/1280/2048 -> 32..192).
+2. ``fuse_sibling_1x1`` — 1x1 convs that read the same full input tensor
+   (every Inception mixed block has 3-4: the 1x1 branch, the reductions of the
+   5x5/3x3/7x7 branches and — after rewrite 1 — the pool branch's conv) become
+   one GEMM with N = sum of their Couts whose epilogue scatters each column
+   segment to its own destination (concat buffer at an offset, or a temporary).
+   One read of the input, one launch, wider N.
+
+Both rewrites keep the weights dict unchanged (members keep their names); the
+fp32 oracle can execute the rewritten graph too (tests compare both forms).
+"""
+from __future__ import annotations
+
+import copy
+from dataclasses import replace
+from typing import Dict, List
+
+from .graph import Conv, FusedConv, Graph, Pool, node_outputs
+
+
+def _consumers(g: Graph) -> Dict[str, List[object]]:
+    out: Dict[str, List[object]] = {}
+    for n in g.nodes:
+        for src in (getattr(n, "inp", None), getattr(n, "residual", None)):
+            if src:
+                out.setdefault(src, []).append(n)
+    return out
+
+
+def conv_before_avgpool(g: Graph) -> Graph:
+    g = copy.deepcopy(g)
+    cons = _consumers(g)
+    nodes = list(g.nodes)
+    for i, p in enumerate(list(nodes)):
+        if not (isinstance(p, Pool) and p.mode == "avg" and p.stride == 1 and p.out_coff == 0 and not p.relu):
+            continue
+        users = cons.get(p.out, [])
+        if len(users) != 1 or not isinstance(users[0], Conv):
+            continue
+        c = users[0]
+        ph, pw, pc = g.shape(p.out)
+        if not (c.kh == c.kw == 1 and c.sh == c.sw == 1 and c.ph == c.pw == 0 and c.in_coff == 0
+                and c.cin == pc and c.residual is None and not c.out_f32):
+            continue
+        tmp = f"{c.name}_prepool"
+        g.tensor(tmp, ph, pw, c.cout)
+        c2 = replace(c, inp=p.inp, out=tmp, out_coff=0, relu=False)
+        p2 = replace(p, inp=tmp, out=c.out, out_coff=c.out_coff, relu=c.relu)
+        j = nodes.index(c)
+        nodes[nodes.index(p)] = c2
+        nodes[j] = p2
+    g.nodes = nodes
+    g.validate()
+    return g
+
+
+def fuse_sibling_1x1(g: Graph, max_members: int = 4) -> Graph:
+    g = copy.deepcopy(g)
+    groups: Dict[tuple, List[Conv]] = {}
+    for n in g.nodes:
+        if (isinstance(n, Conv) and n.kh == n.kw == 1 and n.ph == n.pw == 0
+                and n.in_coff == 0 and n.residual is None and not n.out_f32 and n.cin == g.shape(n.inp)[2]
+                and n.cout % 8 == 0 and n.out_coff % 8 == 0):
+            # same input and same stride (ResNet's projection shortcut + first 1x1 of a stage)
+            groups.setdefault((n.inp, n.sh, n.sw), []).append(n)
+    fused_of: Dict[str, FusedConv] = {}
+    for (inp, _, _), ms in groups.items():
+        if len(ms) < 2:
+            continue
+        for k in range(0, len(ms), max_members):
+            chunk = ms[k:k + max_members]
+            if len(chunk) < 2:
+                continue
+            f = FusedConv(name="+".join(m.name for m in chunk), inp=inp, cin=chunk[0].cin, members=chunk)
+            for m in chunk:
+                fused_of[m.name] = f
+    nodes: List[object] = []
+    placed = set()
+    for n in g.nodes:
+        f = fused_of.get(getattr(n, "name", None)) if isinstance(n, Conv) else None
+        if f is None:
+            nodes.append(n)
+        elif f.name not in placed:
+            nodes.append(f)  # at the first member's position (all inputs exist by then)
+            placed.add(f.name)
+    g.nodes = nodes
+    g.validate()
+    return g
+
+
+def optimize(g: Graph, pool_reorder: bool = True, fuse: bool = True) -> Graph:
+    if pool_reorder:
+        g = conv_before_avgpool(g)
+    if fuse:
+        g = fuse_sibling_1x1(g)
+    return g

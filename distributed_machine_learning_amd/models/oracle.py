@@ -14,7 +14,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from .graph import Conv, Dense, Graph, GlobalAvgPool, Pool
+from .graph import Conv, Dense, FusedConv, Graph, GlobalAvgPool, Pool
 from .weights import Weights
 
 CAFFE_MEAN_BGR = (103.939, 116.779, 123.68)
@@ -53,11 +53,11 @@ class OracleExecutor:
 
             self.folded = {}
             for n in g.nodes:
-                if isinstance(n, Conv):
-                    k, b = fold_conv(n, w)
-                    self.folded[n.name] = (_bf16(torch.from_numpy(k).permute(3, 2, 0, 1).to(device, dtype)),
+                for c in (n.members if isinstance(n, FusedConv) else ([n] if isinstance(n, Conv) else [])):
+                    k, b = fold_conv(c, w)
+                    self.folded[c.name] = (_bf16(torch.from_numpy(k).permute(3, 2, 0, 1).to(device, dtype)),
                                            torch.from_numpy(b).to(device, dtype))
-                elif isinstance(n, Dense):
+                if isinstance(n, Dense):
                     self.folded[n.name] = (_bf16(self.p[f"{n.name}/kernel"]), self.p[f"{n.name}/bias"])
 
     def _bn(self, n: Conv, y: torch.Tensor) -> torch.Tensor:
@@ -78,27 +78,30 @@ class OracleExecutor:
         rnd = _bf16 if em else (lambda v: v)
         t: Dict[str, torch.Tensor] = {g.input: rnd(x.to(self.device, self.dtype))}
         for n in g.nodes:
-            if isinstance(n, Conv):
-                src = t[n.inp][:, n.in_coff:n.in_coff + n.cin]
+            convs = n.members if isinstance(n, FusedConv) else ([n] if isinstance(n, Conv) else [])
+            for c in convs:
+                src = t[c.inp][:, c.in_coff:c.in_coff + c.cin]
                 if em:
-                    k, b = self.folded[n.name]
-                    y = F.conv2d(src, k, b, stride=(n.sh, n.sw), padding=(n.ph, n.pw))
+                    k, b = self.folded[c.name]
+                    y = F.conv2d(src, k, b, stride=(c.sh, c.sw), padding=(c.ph, c.pw))
                 else:
-                    k = p[f"{n.name}/kernel"].permute(3, 2, 0, 1)  # HWIO -> OIHW
-                    y = F.conv2d(src, k, p.get(f"{n.name}/bias"), stride=(n.sh, n.sw), padding=(n.ph, n.pw))
-                    if n.bn:
-                        y = self._bn(n, y)
-                if n.residual:
-                    y = y + t[n.residual]
-                if n.relu:
+                    k = p[f"{c.name}/kernel"].permute(3, 2, 0, 1)  # HWIO -> OIHW
+                    y = F.conv2d(src, k, p.get(f"{c.name}/bias"), stride=(c.sh, c.sw), padding=(c.ph, c.pw))
+                    if c.bn:
+                        y = self._bn(c, y)
+                if c.residual:
+                    y = y + t[c.residual]
+                if c.relu:
                     y = F.relu(y)
-                self._write(t, n.out, rnd(y), n.out_coff, n_img)
-            elif isinstance(n, Pool):
+                self._write(t, c.out, rnd(y), c.out_coff, n_img)
+            if isinstance(n, Pool):
                 src = t[n.inp]
                 if n.mode == "max":
                     y = F.max_pool2d(F.pad(src, (n.pad,) * 4), n.k, n.stride)  # Keras ZeroPadding2D + valid pool
                 else:
                     y = F.avg_pool2d(src, n.k, n.stride, padding=n.pad, count_include_pad=False)
+                if n.relu:
+                    y = F.relu(y)
                 self._write(t, n.out, rnd(y), n.out_coff, n_img)
             elif isinstance(n, GlobalAvgPool):
                 t[n.out] = rnd(t[n.inp].mean(dim=(2, 3), keepdim=True))

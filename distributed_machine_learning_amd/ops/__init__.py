@@ -69,14 +69,14 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
 
 
 def pool3x3(x: torch.Tensor, mode: str, k: int = 3, stride: int = 2, pad: int = 0,
-            out: Optional[torch.Tensor] = None, out_coff: int = 0) -> torch.Tensor:
+            out: Optional[torch.Tensor] = None, out_coff: int = 0, relu: bool = False) -> torch.Tensor:
     n, h, w, c = x.shape
     ho = (h + 2 * pad - k) // stride + 1
     wo = (w + 2 * pad - k) // stride + 1
     if out is None:
         out = torch.empty((n, ho, wo, c), device=x.device, dtype=torch.bfloat16)
     a = N.PoolArgs(x.data_ptr(), out.data_ptr() + 2 * out_coff, n, h, w, c, c, ho, wo, out.shape[-1], k, stride, pad,
-                   0 if mode == "max" else 1)
+                   0 if mode == "max" else 1, int(relu))
     N.check(N.lib().dml_pool(C.byref(a), N.stream_ptr()), "dml_pool")
     return out
 
@@ -110,3 +110,36 @@ def preprocess(images_u8: torch.Tensor, out_hw, mode: str, pair: bool = False, l
                       0 if mode == "caffe" else 1, int(pair), lpad)
     N.check(N.lib().dml_preprocess(C.byref(a), N.stream_ptr()), "preprocess")
     return out
+
+
+def fused_conv1x1(x: torch.Tensor, members, stride: int = 1, cfg: int = -1) -> None:
+    """Sibling 1x1 convs on the same input as ONE segmented GEMM.
+    members: list of (w_oihw fp32 [co, ci, 1, 1], bias [co], out NHWC tensor, out_coff, relu)."""
+    n, h, w_, cbuf = x.shape
+    ws = [m[0] for m in members]
+    w_all = torch.cat(ws, dim=0)
+    b_all = torch.cat([m[1].float().cpu() for m in members])
+    wp, K, kpad = pack_weight(w_all)
+    wp = wp.to(x.device)
+    cout = w_all.shape[0]
+    bias_p = torch.zeros(wp.shape[0], device=x.device, dtype=torch.float32)
+    bias_p[:cout] = b_all.to(x.device)
+    ho = (h - 1) // stride + 1
+    wo = (w_ - 1) // stride + 1
+    out0 = members[0][2]
+    a = N.ConvArgs(x.data_ptr(), wp.data_ptr(), bias_p.data_ptr(), None, out0.data_ptr() + 2 * members[0][3],
+                   n, h, w_, cbuf, cbuf, 1, 1, stride, stride, 0, 0, ho, wo, cout, K, kpad, out0.shape[-1], 0,
+                   int(members[0][4]), 0, 1, 1)
+    a.nseg = len(members)
+    c0 = 0
+    for s, (wt, b, out, coff, relu) in enumerate(members):
+        a.seg_c0[s] = c0
+        a.seg_ldy[s] = out.shape[-1]
+        a.seg_relu[s] = int(relu)
+        a.seg_y[s] = out.data_ptr() + 2 * coff
+        c0 += wt.shape[0]
+    L = N.lib()
+    if cfg < 0:
+        cfg = L.dml_conv_pick_cfg(C.byref(a))
+    N.check(L.dml_conv(C.byref(a), cfg, N.stream_ptr()), "dml_conv(fused)")
+    torch.cuda.current_stream().synchronize()

@@ -74,7 +74,8 @@ def test_engine_matches_oracle(name):
     torch.cuda.synchronize()
     x = preprocess_reference(imgs, hw, g.preprocess)
     got = eng.buf[g.logits].float().cpu()
-    emu = OracleExecutor(g, w, emulate_bf16=True).forward(x)["logits"]
+    # the engine runs the rewritten graph (models/optimize.py); emulate ITS rounding points
+    emu = OracleExecutor(eng.g, w, emulate_bf16=True).forward(x)["logits"]
     ref = OracleExecutor(g, w).forward(x)
     rel_emu, rel_fp32 = _rel(got, emu), _rel(got, ref["logits"])
     print(name, "logits rel err vs bf16-emulating oracle", rel_emu, "vs fp32 oracle", rel_fp32)

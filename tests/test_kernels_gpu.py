@@ -190,3 +190,36 @@ def test_pair_packed_stem(kh, kw, s, p, hw, mode, cfg):
     torch.cuda.synchronize()
     got = y.float().cpu().permute(0, 3, 1, 2)
     assert _rel(got, ref) < 1.5e-2, _rel(got, ref)
+
+
+@pytest.mark.parametrize("cfg", [-1, 11, 14, 15])
+@pytest.mark.parametrize("stride", [1, 2])
+def test_fused_sibling_1x1_segments(cfg, stride):
+    """One segmented GEMM == three separate 1x1 convs writing to a concat buffer
+    at offsets and to a temporary (Inception mixed-block / ResNet stage-entry fusion)."""
+    torch.manual_seed(8)
+    x = _bf(torch.randn(2, 96, 13, 11))
+    specs = [(64, True), (48, False), (32, True)]
+    ws = [_bf(torch.randn(co, 96, 1, 1) * 0.1) for co, _ in specs]
+    bs = [torch.randn(co) * 0.1 for co, _ in specs]
+    ho, wo = (13 - 1) // stride + 1, (11 - 1) // stride + 1
+    concat = torch.full((2, ho, wo, 160), 3.0, device="cuda", dtype=torch.bfloat16)
+    tmp = torch.zeros((2, ho, wo, 48), device="cuda", dtype=torch.bfloat16)
+    xd = x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
+    ops.fused_conv1x1(xd, [(ws[0], bs[0], concat, 0, True), (ws[1], bs[1], tmp, 0, False),
+                           (ws[2], bs[2], concat, 96, True)], stride=stride, cfg=cfg)
+    refs = [F.conv2d(x, w, b, stride=stride) for w, b in zip(ws, bs)]
+    got = concat.float().cpu().permute(0, 3, 1, 2)
+    assert _rel(got[:, 0:64], F.relu(refs[0])) < 1.5e-2
+    assert _rel(tmp.float().cpu().permute(0, 3, 1, 2), refs[1]) < 1.5e-2
+    assert _rel(got[:, 96:128], F.relu(refs[2])) < 1.5e-2
+    assert torch.all(got[:, 64:96] == 3.0) and torch.all(got[:, 128:] == 3.0)
+
+
+def test_avgpool_relu_flag():
+    torch.manual_seed(9)
+    x = _bf(torch.randn(2, 16, 9, 9))
+    y = ops.pool3x3(x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16), "avg", 3, 1, 1, relu=True)
+    torch.cuda.synchronize()
+    ref = F.relu(F.avg_pool2d(x, 3, 1, padding=1, count_include_pad=False))
+    assert _rel(y.float().cpu().permute(0, 3, 1, 2), ref) < 1e-2
