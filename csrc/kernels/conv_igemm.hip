@@ -246,7 +246,7 @@ extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
       dml_set_error("dml_conv(v2): nseg must be 0..4");
       return -1;
     }
-    return dml_conv_v2(a, cfg, s);
+    return cfg >= 40 ? dml_conv_halo(a, cfg, s) : dml_conv_v2(a, cfg, s);
   }
   if (a->nseg > 0) {
     dml_set_error("dml_conv: output segments need a v2 config (cfg >= 10)");

@@ -23,19 +23,14 @@
 //    are contiguous across 16 lanes, so stores/residual loads are full lines.
 //  * XCD-aware bijective block remap; channel tiles fastest so the blocks on
 //    one XCD share the activation rows in its L2.
-#include "common.h"
-#include "dml.h"
+#include "conv_shared.h"
 
 namespace dml {
 namespace v2 {
 
-typedef __attribute__((address_space(3))) void lds_void;
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
+using convk::lds_swz;
+using convk::lds_void;
+using convk::wait_vmcnt;
 
 template <int BM, int BN, int WM, int WN, int STAGES>
 struct Cfg {
@@ -52,16 +47,13 @@ struct Cfg {
   static constexpr int L = XI + WI;           // vm ops per thread per K tile
   static constexpr int STAGE_BYTES = (BM + BN) * ROWB;
   static constexpr int PIPE_BYTES = STAGES * STAGE_BYTES;
-  static constexpr int CROW = BN * 4 + 16;    // epilogue fp32 row stride (+16 B pad)
-  static constexpr int EPI_BYTES = BM * CROW;
+  static constexpr int EPI_BYTES = BM * (BN * 4 + 16);  // = convk::Epilogue<BM, BN, NT, *>::BYTES
   static constexpr int LDS = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
   static_assert(XI >= 1 && WI >= 1, "each wave needs >=1 DMA instruction per operand");
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split evenly across waves");
   static_assert(FI >= 1 && FJ >= 1, "wave tile too small");
   static_assert((STAGES - 2) * L < 64, "vmcnt overflow");
 };
-
-__device__ __forceinline__ int lds_swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
 template <int BM, int BN, int WM, int WN, int STAGES, bool RES>
 __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
@@ -169,40 +161,19 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s, s);
 
-  // Epilogue operands prefetched behind the first DMA tiles: this thread's
-  // 8-channel group is fixed (NT % CG == 0), so its bias is 2 float4 and its
-  // residual is one 16-byte row segment per epilogue iteration. On the
-  // memory-bound 1x1 layers (K = 64..256) this hides the residual read under
-  // the operand loads instead of exposing it after the last MFMA.
-  constexpr int CG = BN / 8;  // 8-channel groups per pixel row
-  constexpr int EIT = BM * CG / T::NT;
-  static_assert(T::NT % CG == 0 && (BM * CG) % T::NT == 0, "epilogue mapping");
-  const int cg_t = tid % CG;
-  const int ch_t = c0 + cg_t * 8;
-  const bool ch_ok = ch_t < a.Cout;
-  const unsigned short* __restrict__ rg = (const unsigned short*)a.res;
-  float4 bias0 = make_float4(0.f, 0.f, 0.f, 0.f), bias1 = bias0;
-  if (ch_ok) {
-    bias0 = *(const float4*)(a.bias + ch_t);
-    bias1 = *(const float4*)(a.bias + ch_t + 4);
-  }
-  // RES is a template parameter: the residual prefetch costs 4*EIT VGPRs,
-  // which would cut occupancy of the (residual-free) compute-bound 3x3 layers.
-  uint4 rpre[RES ? EIT : 1];
-  if constexpr (RES) {
-#pragma unroll
-    for (int it = 0; it < EIT; ++it) {
-      const int m = m0 + (tid + it * T::NT) / CG;
-      rpre[it] = (ch_ok && m < M) ? *(const uint4*)(rg + (long)m * a.ldr + ch_t) : make_uint4(0, 0, 0, 0);
-    }
-  }
+  // epilogue operands (bias, residual) prefetched behind the first DMA tiles
+  convk::Epilogue<BM, BN, T::NT, RES> epi;
+  epi.prefetch(a, m0, c0, M, tid);
 
   for (int kt = 0; kt < nk; ++kt) {
     // retire tile kt (leave the younger STAGES-2 tiles in flight), then barrier
     if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * T::L>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    // refill the stage freed by tile kt-1 (every wave passed the barrier => done reading it)
+    // Refill the stage freed by tile kt-1 right after the barrier, before the
+    // fragment reads. A/B-measured (profiles/r1_v5/sched_ab_v*.json): issuing it
+    // between the two k-steps, or interleaving it among the MFMAs with
+    // sched_group_barrier, was 8-15 % slower on both 3x3 and 1x1 layers.
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const char* sx = smem + (kt % STAGES) * T::STAGE_BYTES;
     const char* sw = sx + BM * T::ROWB;
@@ -229,62 +200,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
     __builtin_amdgcn_s_setprio(0);
   }
 
-  // ---- epilogue: acc -> LDS (fp32) -> coalesced bias/residual/ReLU/store ----
-  __syncthreads();  // all DMA retired (vmcnt(0) above) and all LDS reads done
-#pragma unroll
-  for (int i = 0; i < T::FI; ++i)
-#pragma unroll
-    for (int j = 0; j < T::FJ; ++j) {
-      const int px = wp * T::WTP + j * 16 + frow;
-      const int ch = wc * T::WTC + i * 16 + fq * 4;
-      *(f32x4*)(smem + px * T::CROW + ch * 4) = acc[i][j];
-    }
-  __syncthreads();
-  // Destination of this thread's channel group: the plain output, or (fused
-  // sibling convs) the segment that owns channel ch_t. Resolved once per thread.
-  void* ybase = a.y;
-  int ldy = a.ldy, relu = a.relu, choff = ch_t;
-  if (a.nseg > 0) {
-    int sgi = 0;
-#pragma unroll
-    for (int q = 1; q < 4; ++q)
-      if (q < a.nseg && ch_t >= a.seg_c0[q]) sgi = q;
-    ybase = a.seg_y[sgi];
-    ldy = a.seg_ldy[sgi];
-    relu = a.seg_relu[sgi];
-    choff = ch_t - a.seg_c0[sgi];
-  }
-#pragma unroll
-  for (int it = 0; it < EIT; ++it) {
-    const int e = tid + it * T::NT;
-    const int px = e / CG, cg = cg_t;
-    const int m = m0 + px, ch = choff;
-    if (m >= M || !ch_ok) continue;
-    const float4 v0 = *(const float4*)(smem + px * T::CROW + cg * 32);
-    const float4 v1 = *(const float4*)(smem + px * T::CROW + cg * 32 + 16);
-    const float4 b0 = bias0, b1 = bias1;
-    float f[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
-                  v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
-    if constexpr (RES) {
-      const uint4 r = rpre[it];
-      f[0] += bf2f(r.x & 0xffff); f[1] += bf2f(r.x >> 16);
-      f[2] += bf2f(r.y & 0xffff); f[3] += bf2f(r.y >> 16);
-      f[4] += bf2f(r.z & 0xffff); f[5] += bf2f(r.z >> 16);
-      f[6] += bf2f(r.w & 0xffff); f[7] += bf2f(r.w >> 16);
-    }
-    if (relu) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) f[q] = fmaxf(f[q], 0.f);
-    }
-    if (a.out_f32) {
-      float* yp = (float*)ybase + (long)m * ldy + ch;
-      *(float4*)yp = make_float4(f[0], f[1], f[2], f[3]);
-      *(float4*)(yp + 4) = make_float4(f[4], f[5], f[6], f[7]);
-    } else {
-      *(uint4*)((unsigned short*)ybase + (long)m * ldy + ch) =
-          make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
-    }
-  }
+  // all DMA retired (vmcnt(0) on the last tile); epilogue through LDS
+  epi.template store<T::FI, T::FJ, T::WTP, T::WTC>(a, smem, acc, wp, wc, lane, tid);
 }
 
 template <int BM, int BN, int WM, int WN, int STAGES>

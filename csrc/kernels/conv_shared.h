@@ -1,0 +1,129 @@
+// conv_shared.h — pieces shared by the LDS-DMA convolution kernels
+// (conv_igemm_v2.hip: generic implicit GEMM; conv_halo.hip: stride-1 halo tiles).
+//
+//  * counted vmcnt waits (LDS-DMA completes in issue order with other VMEM ops)
+//  * the 16-B-chunk XOR swizzle of a 128-B LDS tile row
+//  * the LDS-staged epilogue: fp32 accumulators -> LDS -> each thread owns one
+//    8-channel group of a pixel: bias (+ residual, prefetched before the main
+//    loop) (+ ReLU) -> one 16-B NHWC store at a channel offset, or into one of up
+//    to 4 output segments (fused sibling convs).
+#pragma once
+#include "common.h"
+#include "dml.h"
+
+namespace dml {
+namespace convk {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// byte offset of 16-B chunk `chunk` (0..7) of 128-B tile row `row`
+__device__ __forceinline__ int lds_swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+// Epilogue of a BM(pixels) x BN(channels) tile computed by NT threads.
+template <int BM, int BN, int NT, bool RES>
+struct Epilogue {
+  static constexpr int CG = BN / 8;            // 8-channel groups per pixel
+  static constexpr int EIT = BM * CG / NT;     // pixels handled per thread
+  static constexpr int CROW = BN * 4 + 16;     // fp32 staging row stride (+16 B pad)
+  static constexpr int BYTES = BM * CROW;
+  static_assert(NT % CG == 0 && (BM * CG) % NT == 0, "epilogue mapping");
+
+  int cg_t, ch_t, m0, M;
+  bool ch_ok;
+  float4 bias0, bias1;
+  uint4 rpre[RES ? EIT : 1];
+
+  // Issue the bias / residual loads early: on memory-bound layers the residual
+  // read then hides under the operand DMA instead of following the last MFMA.
+  __device__ __forceinline__ void prefetch(const DmlConvArgs& a, int m0_, int c0, int M_, int tid) {
+    m0 = m0_;
+    M = M_;
+    cg_t = tid % CG;
+    ch_t = c0 + cg_t * 8;
+    ch_ok = ch_t < a.Cout;
+    bias0 = make_float4(0.f, 0.f, 0.f, 0.f);
+    bias1 = bias0;
+    if (ch_ok) {
+      bias0 = *(const float4*)(a.bias + ch_t);
+      bias1 = *(const float4*)(a.bias + ch_t + 4);
+    }
+    if constexpr (RES) {
+      const unsigned short* __restrict__ rg = (const unsigned short*)a.res;
+#pragma unroll
+      for (int it = 0; it < EIT; ++it) {
+        const int m = m0 + (tid + it * NT) / CG;
+        rpre[it] = (ch_ok && m < M) ? *(const uint4*)(rg + (long)m * a.ldr + ch_t) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+
+  // acc[i][j]: channel fragment i (16 ch) x pixel fragment j (16 px) of this
+  // wave's (WTC x WTP) sub-tile at (wc, wp). Caller must have retired all DMA.
+  template <int FI, int FJ, int WTP, int WTC>
+  __device__ __forceinline__ void store(const DmlConvArgs& a, char* smem, f32x4 (&acc)[FI][FJ], int wp, int wc,
+                                        int lane, int tid) {
+    const int frow = lane & 15, fq = lane >> 4;
+    __syncthreads();  // every wave is done reading the operand tiles
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int px = wp * WTP + j * 16 + frow;
+        const int ch = wc * WTC + i * 16 + fq * 4;
+        *(f32x4*)(smem + px * CROW + ch * 4) = acc[i][j];
+      }
+    __syncthreads();
+    // destination of this thread's channel group: the plain output, or the
+    // segment (fused sibling conv) that owns channel ch_t
+    void* ybase = a.y;
+    int ldy = a.ldy, relu = a.relu, choff = ch_t;
+    if (a.nseg > 0) {
+      int sgi = 0;
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+        if (q < a.nseg && ch_t >= a.seg_c0[q]) sgi = q;
+      ybase = a.seg_y[sgi];
+      ldy = a.seg_ldy[sgi];
+      relu = a.seg_relu[sgi];
+      choff = ch_t - a.seg_c0[sgi];
+    }
+#pragma unroll
+    for (int it = 0; it < EIT; ++it) {
+      const int px = (tid + it * NT) / CG;
+      const int m = m0 + px;
+      if (m >= M || !ch_ok) continue;
+      const float4 v0 = *(const float4*)(smem + px * CROW + cg_t * 32);
+      const float4 v1 = *(const float4*)(smem + px * CROW + cg_t * 32 + 16);
+      float f[8] = {v0.x + bias0.x, v0.y + bias0.y, v0.z + bias0.z, v0.w + bias0.w,
+                    v1.x + bias1.x, v1.y + bias1.y, v1.z + bias1.z, v1.w + bias1.w};
+      if constexpr (RES) {
+        const uint4 r = rpre[it];
+        f[0] += bf2f(r.x & 0xffff); f[1] += bf2f(r.x >> 16);
+        f[2] += bf2f(r.y & 0xffff); f[3] += bf2f(r.y >> 16);
+        f[4] += bf2f(r.z & 0xffff); f[5] += bf2f(r.z >> 16);
+        f[6] += bf2f(r.w & 0xffff); f[7] += bf2f(r.w >> 16);
+      }
+      if (relu) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) f[q] = fmaxf(f[q], 0.f);
+      }
+      if (a.out_f32) {
+        float* yp = (float*)ybase + (long)m * ldy + choff;
+        *(float4*)yp = make_float4(f[0], f[1], f[2], f[3]);
+        *(float4*)(yp + 4) = make_float4(f[4], f[5], f[6], f[7]);
+      } else {
+        *(uint4*)((unsigned short*)ybase + (long)m * ldy + choff) =
+            make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+      }
+    }
+  }
+};
+
+}  // namespace convk
+}  // namespace dml

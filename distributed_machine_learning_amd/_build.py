@@ -25,10 +25,11 @@ ARCH = os.environ.get("DML_OFFLOAD_ARCH", "gfx950")
 SOURCES = [
     CSRC / "kernels" / "conv_igemm.hip",
     CSRC / "kernels" / "conv_igemm_v2.hip",
+    CSRC / "kernels" / "conv_halo.hip",
     CSRC / "kernels" / "misc.hip",
     CSRC / "runtime" / "runtime.hip",
 ]
-HEADERS = [CSRC / "include" / "dml.h", CSRC / "kernels" / "common.h"]
+HEADERS = [CSRC / "include" / "dml.h", CSRC / "kernels" / "common.h", CSRC / "kernels" / "conv_shared.h"]
 
 
 def _hipcc() -> str:

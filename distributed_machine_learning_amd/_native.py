@@ -52,6 +52,8 @@ _SIGS = {
     "dml_conv": (C.c_int, [C.POINTER(ConvArgs), C.c_int, C.c_void_p]),
     "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),
     "dml_conv_v2_init": (C.c_int, []),
+    "dml_conv_halo_init": (C.c_int, []),
+    "dml_conv_halo_ok": (C.c_int, [C.POINTER(ConvArgs), C.c_int]),
     "dml_pool": (C.c_int, [C.POINTER(PoolArgs), C.c_void_p]),
     "dml_global_avgpool": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "dml_softmax_top5": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -101,7 +103,11 @@ def lib():
         import torch  # noqa: F401  -- load torch's libamdhip64.so.7 first so ours binds to it
 
         path = _build.LIB_PATH
-        if os.environ.get("DML_SKIP_BUILD") != "1":
+        if os.environ.get("DML_LIB"):  # explicit library (A/B experiments between kernel variants)
+            from pathlib import Path
+
+            path = Path(os.environ["DML_LIB"])
+        elif os.environ.get("DML_SKIP_BUILD") != "1":
             try:
                 path = _build.build()
             except Exception as e:  # hipcc missing on a runtime-only box: use the shipped .so
@@ -126,6 +132,7 @@ def ensure_device_init() -> None:
     global _inited
     if not _inited:
         check(lib().dml_conv_v2_init(), "dml_conv_v2_init")
+        check(lib().dml_conv_halo_init(), "dml_conv_halo_init")
         _inited = True
 
 

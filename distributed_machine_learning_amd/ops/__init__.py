@@ -15,7 +15,12 @@ import torch
 
 from .. import _native as N
 
-__all__ = ["conv2d_nhwc", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight"]
+__all__ = ["conv2d_nhwc", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight",
+           "pack_weight_halo", "HALO_CFGS"]
+
+# stride-1 halo-tile conv configs (csrc/kernels/conv_halo.hip); they take
+# chunk-major weights from pack_weight_halo
+from .tuning import HALO_CFGS  # noqa: E402
 
 
 def _r(x, m):
@@ -32,6 +37,32 @@ def pack_weight(w_oihw: torch.Tensor, cin_eff: Optional[int] = None) -> Tuple[to
     out = torch.zeros((_r(co, 256), _r(K, 64)), dtype=torch.float32)
     out[:co, :K] = k.reshape(co, K)
     return out.to(torch.bfloat16), K, _r(K, 64)
+
+
+def halo_layout(kernel_tco: np.ndarray, cout_pad: int) -> np.ndarray:
+    """[cout][taps][cin] fp32 -> the halo kernel's chunk-major [cout_pad][ceil(cin/64)][taps][64]."""
+    co, taps, ci = kernel_tco.shape
+    nch = (ci + 63) // 64
+    out = np.zeros((cout_pad, nch, taps, 64), np.float32)
+    for c in range(nch):
+        w = min(64, ci - 64 * c)
+        out[:co, c, :, :w] = kernel_tco[:, :, 64 * c: 64 * c + w]
+    return out.reshape(cout_pad, nch * taps * 64)
+
+
+def pack_weight_halo(w_oihw: torch.Tensor, cin_eff: Optional[int] = None) -> Tuple[torch.Tensor, int, int]:
+    """OIHW fp32 -> bf16 halo layout (see halo_layout). Returns (w, K, Kpad)."""
+    co, ci, kh, kw = w_oihw.shape
+    cin_eff = cin_eff or _r(ci, 8)
+    k = np.zeros((co, kh * kw, cin_eff), np.float32)
+    k[..., :ci] = w_oihw.permute(0, 2, 3, 1).reshape(co, kh * kw, ci).float().cpu().numpy()
+    out = halo_layout(k, _r(co, 256))
+    return torch.from_numpy(out).to(torch.bfloat16), kh * kw * cin_eff, out.shape[1]
+
+
+def halo_ok(a, cfg: int) -> bool:
+    """True if halo config `cfg` can run the conv described by ConvArgs `a`."""
+    return N.lib().dml_conv_halo_ok(C.byref(a), cfg) == 0
 
 
 def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cout: int, kh: int, kw: int,

@@ -25,9 +25,15 @@ CACHE_PATH = os.environ.get(
 _lock = threading.Lock()
 
 
-def shape_key(a: N.ConvArgs) -> str:
+HALO_CFGS = (40, 41, 42, 43, 44, 45, 46, 47)  # conv_halo.hip (stride-1, chunk-major weights)
+
+
+def shape_key(a: N.ConvArgs, halo: bool = False) -> str:
+    """Cache key of a conv shape; `halo` marks shapes that also had the halo
+    configs as candidates (so entries tuned before they existed are re-timed)."""
     return (f"n{a.N}_h{a.H}_w{a.W}_c{a.Cin}_ld{a.ldx}_k{a.kh}x{a.kw}_s{a.sh}x{a.sw}_p{a.ph}x{a.pw}"
-            f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}_d{max(a.dh, 1)}x{max(a.dw, 1)}")
+            f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}_d{max(a.dh, 1)}x{max(a.dw, 1)}"
+            + ("_halo" if halo else ""))
 
 
 def load_cache(path: str = CACHE_PATH) -> Dict[str, int]:
@@ -70,19 +76,27 @@ def time_cfg(a: N.ConvArgs, cfg: int, iters: int = 3) -> float:
     return e0.elapsed_time(e1) / iters
 
 
-def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None, persist: bool = True
-             ) -> Dict[str, int]:
-    """Return {shape_key: best cfg} for every ConvArgs (timing the uncached ones)."""
+def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None, persist: bool = True,
+             halo_args: Optional[Iterable[Optional[N.ConvArgs]]] = None) -> Dict[str, int]:
+    """Return {shape_key: best cfg} for every ConvArgs (timing the uncached ones).
+    halo_args[i], if not None, is the same conv with halo-packed weights: the
+    halo configs are timed on it and a winning id >= 40 means "use halo_args"."""
+    args = list(args)
+    halo_args = list(halo_args) if halo_args is not None else [None] * len(args)
     cache = dict(load_cache() if cache is None else cache)
     new: Dict[str, int] = {}
-    for a in args:
-        k = shape_key(a)
+    L = N.lib()
+    for a, ah in zip(args, halo_args):
+        k = shape_key(a, ah is not None)
         if k in cache or k in new:
             continue
         best: Tuple[float, int] = (float("inf"), -1)
-        for cfg in valid_cfgs(a):
+        cands = [(cfg, a) for cfg in valid_cfgs(a)]
+        if ah is not None:
+            cands += [(cfg, ah) for cfg in HALO_CFGS if L.dml_conv_halo_ok(C.byref(ah), cfg) == 0]
+        for cfg, aa in cands:
             try:
-                t = time_cfg(a, cfg)
+                t = time_cfg(aa, cfg)
             except N.NativeError:
                 continue
             best = min(best, (t, cfg))

@@ -6,7 +6,7 @@ Prints per-shape time and TFLOP/s for each cfg; one process, interleaved rounds.
 import argparse, ctypes as C, json, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
-from distributed_machine_learning_amd import _native as N
+from distributed_machine_learning_amd import _native as N, ops
 from distributed_machine_learning_amd.models import build_graph
 from distributed_machine_learning_amd.models.graph import Conv
 
@@ -34,7 +34,11 @@ for key, names in shapes.items():
     ho = (h + 2 * ph - kh) // st + 1; wo = (w + 2 * pw - kw) // st + 1
     K = kh * kw * cin; Kp = r(K, 64)
     x = torch.randn(B, h, w, cin, device="cuda").to(torch.bfloat16)
-    wt = (torch.randn(r(cout, 256), Kp, device="cuda") * 0.05).to(torch.bfloat16)
+    w_oihw = torch.randn(cout, cin, kh, kw) * (2.0 / K) ** 0.5
+    wt = ops.pack_weight(w_oihw)[0].cuda()
+    halo = st == 1 and kh * kw > 1
+    wh, _, Kh = ops.pack_weight_halo(w_oihw) if halo else (None, 0, 0)
+    wh = wh.cuda() if halo else None
     bias = torch.zeros(r(cout, 256), device="cuda")
     y = torch.empty(B, ho, wo, cout, device="cuda", dtype=torch.bfloat16)
     rs = torch.randn(B, ho, wo, cout, device="cuda").to(torch.bfloat16) if hasres else None
@@ -46,9 +50,18 @@ for key, names in shapes.items():
     row = {"layers": names, "M": B * ho * wo, "N": cout, "K": K, "kh": kh, "kw": kw, "stride": st,
            "gflop": flops / 1e9, "mb": nbytes / 1e6, "ms": {}}
     ref = None
+    ah = None
+    if halo:
+        ah = N.ConvArgs.from_buffer_copy(a)
+        ah.w, ah.Kpad = wh.data_ptr(), Kh
     for cfg in cfgs:
+        aa = a
+        if cfg >= 40:
+            if ah is None or not ops.halo_ok(ah, cfg):
+                continue
+            aa = ah
         try:
-            N.check(L.dml_conv(C.byref(a), cfg, N.stream_ptr()), "conv")
+            N.check(L.dml_conv(C.byref(aa), cfg, N.stream_ptr()), "conv")
             torch.cuda.synchronize()
             out = y.float()
             if ref is None: ref = out
@@ -56,7 +69,7 @@ for key, names in shapes.items():
             e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
             e0.record()
             for _ in range(args.iters):
-                L.dml_conv(C.byref(a), cfg, N.stream_ptr())
+                L.dml_conv(C.byref(aa), cfg, N.stream_ptr())
             e1.record(); torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.iters
             row["ms"][cfg] = round(ms, 4)
@@ -69,7 +82,7 @@ for key, names in shapes.items():
     row["best_tflops"] = round(flops / best[0] / 1e9, 1)
     res.append(row)
     print(f"{names[0]:22s} x{len(names)} M={row['M']:8d} N={cout:5d} K={K:5d} " +
-          " ".join(f"{c}:{row['ms'][c]}" for c in cfgs) + f" best={best[1]} {row['best_tflops']}TF err={row.get('err')}",
+          " ".join(f"{c}:{row['ms'][c]}" for c in cfgs if c in row["ms"]) + f" best={best[1]} {row['best_tflops']}TF err={row.get('err')}",
           flush=True)
 tot = {c: sum((row["ms"].get(c) or 1e9) * len(row["layers"]) for row in res) for c in cfgs}
 best_tot = sum(min(v for v in row["ms"].values() if v) * len(row["layers"]) for row in res)
