@@ -48,6 +48,12 @@ class RankFailureDetector:
         asyncio.set_event_loop(self.loop)
         self.loop.create_task(self._run())
         self.loop.run_forever()
+        # drain anything stop() did not reach (e.g. it timed out) before closing
+        pending = [t for t in asyncio.all_tasks(self.loop) if not t.done()]
+        for t in pending:
+            t.cancel()
+        if pending:
+            self.loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
         self.loop.close()
 
     async def _run(self) -> None:
@@ -73,8 +79,12 @@ class RankFailureDetector:
         await asyncio.Event().wait()
 
     async def _shutdown(self) -> None:
-        self.fd.stop()
-        self.fd.ep.stop()
+        for stop in (getattr(self.fd, "stop", None), getattr(getattr(self.fd, "ep", None), "stop", None)):
+            try:
+                if stop is not None:
+                    stop()
+            except Exception:  # pragma: no cover - best effort at exit
+                pass
         tasks = [t for t in asyncio.all_tasks() if t is not asyncio.current_task()]
         for t in tasks:
             t.cancel()

@@ -46,12 +46,24 @@ IDLE, STOP = -1, -2
 
 # ------------------------------------------------------------- backends ----
 class RankBackend:
-    """Runs one batch of images [start, start+count) of `model` on this rank."""
+    """Runs one batch of images [start, start+count) of `model` on this rank.
+
+    ``launch`` is asynchronous on GPU backends: it enqueues staging + forward and
+    returns (result [2, max_batch, 5] int32, completion event or None), so the
+    service can gather the previous step's results while this batch computes.
+    """
 
     max_batch: int = 256
+    device = torch.device("cpu")
 
-    def run(self, model: str, start: int, count: int) -> torch.Tensor:  # [2, max_batch, 5] int32
+    def launch(self, model: str, start: int, count: int, slot: int):
         raise NotImplementedError
+
+    def run(self, model: str, start: int, count: int) -> torch.Tensor:
+        res, ev = self.launch(model, start, count, 0)
+        if ev is not None:
+            ev.synchronize()
+        return res
 
 
 class FakeRankBackend(RankBackend):
@@ -60,19 +72,21 @@ class FakeRankBackend(RankBackend):
     def __init__(self, max_batch: int = 16, delay_per_image: float = 0.0):
         self.max_batch, self.delay = max_batch, delay_per_image
 
-    def run(self, model, start, count):
+    def launch(self, model, start, count, slot):
         if self.delay:
             time.sleep(self.delay * count)
         out = torch.zeros((2, self.max_batch, 5), dtype=torch.int32)
         i = torch.arange(count, dtype=torch.int32)[:, None] + start
         out[0, :count] = (i * 7 + torch.arange(5, dtype=torch.int32)[None] + MODEL_IDS[model] * 100) % 1000
         out[1, :count] = torch.tensor([0.5, 0.2, 0.1, 0.05, 0.01]).view(torch.int32)
-        return out
+        return out, None
 
 
 class GpuRankBackend(RankBackend):
     """Native engines for both models resident in this GPU's HBM, fed from
-    per-model pinned host image arenas."""
+    per-model pinned host image arenas. Two source slots per engine: the H2D
+    copy of step k (copy stream) overlaps the forward of step k-1 (compute
+    stream); results land in one of two output slots."""
 
     def __init__(self, device: torch.device, batch_sizes: Dict[str, int], arena_images: int = 512, seed: int = 0,
                  models: Sequence[str] = MODELS):
@@ -84,24 +98,33 @@ class GpuRankBackend(RankBackend):
         self.max_batch = max(batch_sizes.values())
         self.engines, self.stores = {}, {}
         self.stream = torch.cuda.Stream(device)
+        self.copy_stream = torch.cuda.Stream(device)
         for m in models:
             g, w = build_model(m, seed=seed, calibrate=True)
-            self.engines[m] = Engine(g, w, batch=batch_sizes[m], device=str(device))
+            self.engines[m] = Engine(g, w, batch=batch_sizes[m], device=str(device), src_slots=2)
             st = PinnedImageStore(arena_images, g.input_hw)
             st.fill_synthetic(seed=1000 + MODEL_IDS[m])
             self.stores[m] = st
-        self.out = torch.zeros((2, self.max_batch, 5), dtype=torch.int32, device=device)
+        self.out = [torch.zeros((2, self.max_batch, 5), dtype=torch.int32, device=device) for _ in range(2)]
+        self.ev_copied = torch.cuda.Event()
+        self.ev_consumed = {(m, k): torch.cuda.Event() for m in models for k in range(2)}
+        self.ev_done = [torch.cuda.Event() for _ in range(2)]
 
-    def run(self, model, start, count):
+    def launch(self, model, start, count, slot):
         eng = self.engines[model]
-        s = self.stream
-        self.stores[model].h2d(eng.src, start, min(count, eng.batch), s)
+        cs, s = self.copy_stream, self.stream
+        cs.wait_event(self.ev_consumed[(model, slot)])  # WAR: the forward that last read this source slot
+        self.stores[model].h2d(eng.srcs[slot], start, min(count, eng.batch), cs)
+        self.ev_copied.record(cs)
+        s.wait_event(self.ev_copied)
+        out = self.out[slot]
         with torch.cuda.stream(s):
-            eng.run(s, use_graph=True)
-            self.out.zero_()
-            self.out[:, : eng.batch].copy_(eng.result)
-        s.synchronize()
-        return self.out
+            eng.run(s, use_graph=True, slot=slot)
+            self.ev_consumed[(model, slot)].record(s)
+            out.zero_()
+            out[:, : eng.batch].copy_(eng.result)
+            self.ev_done[slot].record(s)
+        return out, self.ev_done[slot]
 
 
 # ---------------------------------------------------------- coordinator ----
@@ -113,7 +136,9 @@ class Inflight:
 
 
 class CollectiveCoordinator:
-    """Rank-0 scheduling state (the reference leader's job service)."""
+    """Rank-0 scheduling state (the reference leader's job service). Batches are
+    tracked per dispatch step, so with the pipelined service two steps (the one
+    computing and the one being gathered) can be in flight."""
 
     def __init__(self, batch_sizes: Dict[str, int], arena_images: Dict[str, int], out_dir: Optional[str] = None,
                  host_tag: str = "node"):
@@ -121,8 +146,8 @@ class CollectiveCoordinator:
         self.cost = CostModel()
         self.metrics = Metrics()
         self.arena = arena_images
-        self.inflight: Dict[int, Inflight] = {}
-        self.step_t0 = 0.0
+        self.inflight: Dict[int, Dict[int, Inflight]] = {}  # step -> global rank -> batch
+        self.step_t0: Dict[int, float] = {}
         self.requeued = 0
         self.steps = 0
         self.out_dir = out_dir
@@ -144,6 +169,7 @@ class CollectiveCoordinator:
         return self.jobs.pending() == 0 and not self.jobs.inprogress
 
     def next_table(self, members: List[int], stop_when_idle: bool = True) -> np.ndarray:
+        """Descriptor table of dispatch step ``self.steps`` (then increments it)."""
         t = np.full((len(members), DESC_FIELDS), 0, np.int64)
         t[:, F_MODEL] = IDLE
         if stop_when_idle and self.idle():
@@ -152,9 +178,8 @@ class CollectiveCoordinator:
         queued = {m: len(self.jobs.queues[m]) for m in MODELS}
         workers = [f"rank{g}" for g in members]
         assigns = plan(queued, workers, {}, workers, self.cost, self.jobs.batch_sizes)
-        self.inflight = {}
         now = time.monotonic()
-        self.step_t0 = now
+        cur: Dict[int, Inflight] = {}
         for a in assigns:
             g = int(a.worker[4:])
             b = self.jobs.pop_next(a.model)
@@ -163,33 +188,44 @@ class CollectiveCoordinator:
             r = members.index(g)
             start = int(b.images[0])
             t[r] = (b.job_id, b.batch_id, MODEL_IDS[b.model], start, len(b.images), 0)
-            self.inflight[g] = Inflight(g, b, now)
+            cur[g] = Inflight(g, b, now)
+        self.inflight[self.steps] = cur
+        self.step_t0[self.steps] = now
         self.steps += 1
         return t
 
-    def complete(self, members: List[int], table: np.ndarray, gathered: Optional[List[torch.Tensor]]) -> None:
+    def complete(self, members: List[int], gathered: Optional[List[torch.Tensor]], step: Optional[int] = None
+                 ) -> None:
+        """Results of dispatch step ``step`` (default: the oldest in flight) arrived."""
+        if step is None:
+            if not self.inflight:
+                return
+            step = min(self.inflight)
         now = time.monotonic()
-        service = now - self.step_t0
-        for g, inf in list(self.inflight.items()):
+        service = now - self.step_t0.pop(step, now)
+        for g, inf in self.inflight.pop(step, {}).items():
             b = inf.batch
-            job = self.jobs.complete(b.key, now=now)
+            self.jobs.complete(b.key, now=now)
             n = len(b.images)
             self.metrics.record(b.model, now - inf.t_dispatch, service, n)
             self.cost.observe(b.model, n, service)
-            if self._writer is not None and gathered is not None:
+            if self._writer is not None and gathered is not None and g in members:
                 res = gathered[members.index(g)].cpu().numpy()
                 try:
                     self._wq.put_nowait((b, res[0, :n].copy(), res[1, :n].view(np.float32).copy(), g))
                 except queue.Full:
                     pass
-        self.inflight = {}
 
     def requeue_inflight(self) -> int:
+        """Failure: every batch of every in-flight step goes back to the FRONT
+        of its queue (newest step first, so queue order is preserved)."""
         n = 0
-        for g, inf in self.inflight.items():
-            if self.jobs.requeue_front(inf.batch.key) is not None:
-                n += 1
-        self.inflight = {}
+        for step in sorted(self.inflight, reverse=True):
+            for g, inf in self.inflight[step].items():
+                if self.jobs.requeue_front(inf.batch.key) is not None:
+                    n += 1
+        self.inflight.clear()
+        self.step_t0.clear()
         self.requeued += n
         return n
 
@@ -212,6 +248,16 @@ class CollectiveCoordinator:
 
 # -------------------------------------------------------------- service ----
 class CollectiveService:
+    """Lag-1 pipelined serving loop, identical on every rank:
+
+      step k:  broadcast table k -> launch batch k (async on the GPU)
+               -> gather the results of step k-1 (done or finishing while batch k
+                  computes) -> rank 0 completes step k-1.
+
+    so the coordinator's bookkeeping, the descriptor broadcast and the result
+    gather hide under the next batch's forward. Any CollectiveFailure requeues
+    both in-flight steps and re-forms the communicator over the survivors."""
+
     def __init__(self, eg: ElasticGroup, backend: RankBackend, coord: Optional[CollectiveCoordinator] = None,
                  kill_rank: int = -1, kill_at_step: int = -1, on_device: bool = False):
         self.eg, self.be, self.coord = eg, backend, coord
@@ -219,6 +265,8 @@ class CollectiveService:
         self.dev = backend.device if on_device else torch.device("cpu")
         self.steps = 0
         self.rebuilds = 0
+        self.pending = None  # (step, result tensor, event) of the step awaiting its gather
+        self._idle = torch.zeros((2, self.be.max_batch, 5), dtype=torch.int32, device=self.dev)
 
     def _bufs(self) -> Optional[List[torch.Tensor]]:
         if self.eg.rank != 0:
@@ -226,29 +274,43 @@ class CollectiveService:
         return [torch.zeros((2, self.be.max_batch, 5), dtype=torch.int32, device=self.dev)
                 for _ in range(self.eg.world)]
 
+    def _collect(self) -> None:
+        """Gather + complete the pending step (all ranks call this in lockstep)."""
+        if self.pending is None:
+            return
+        k, res, ev = self.pending
+        if ev is not None:
+            if self.dev.type == "cuda":
+                torch.cuda.current_stream(self.dev).wait_event(ev)  # RCCL waits on the GPU, not the host
+            else:
+                ev.synchronize()
+        res = res.to(self.dev)
+        bufs = self._bufs()
+        self.eg.gather(res, bufs)
+        self.pending = None
+        if self.eg.rank == 0:
+            self.coord.complete(self.eg.members, bufs, step=k)
+
     def step(self) -> bool:
         eg = self.eg
         desc = torch.zeros((eg.world, DESC_FIELDS), dtype=torch.int64, device=self.dev)
-        table = None
         if eg.rank == 0:
-            table = self.coord.next_table(eg.members)
-            desc.copy_(torch.from_numpy(table))
+            desc.copy_(torch.from_numpy(self.coord.next_table(eg.members)))
         eg.broadcast(desc, 0)
         row = desc[eg.rank].cpu().numpy()
         if row[F_MODEL] == STOP:
+            self._collect()
             return False
         if self.steps == self.kill_at_step and eg.grank == self.kill_rank:
             log.warning("rank %d: injected kill at step %d", eg.grank, self.steps)
             os._exit(17)
         if row[F_MODEL] >= 0:
-            res = self.be.run(MODELS[int(row[F_MODEL])], int(row[F_START]), int(row[F_COUNT]))
+            launched = self.be.launch(MODELS[int(row[F_MODEL])], int(row[F_START]), int(row[F_COUNT]),
+                                      self.steps % 2)
         else:
-            res = torch.zeros((2, self.be.max_batch, 5), dtype=torch.int32, device=self.dev)
-        res = res.to(self.dev)
-        bufs = self._bufs()
-        eg.gather(res, bufs)
-        if eg.rank == 0:
-            self.coord.complete(eg.members, table, bufs)
+            launched = (self._idle, None)
+        self._collect()  # step k-1, overlapping batch k
+        self.pending = (self.steps, launched[0], launched[1])
         self.steps += 1
         return True
 
@@ -259,6 +321,7 @@ class CollectiveService:
                     break
             except CollectiveFailure as e:
                 log.warning("rank %d: collective failed (%s); rebuilding", self.eg.grank, e)
+                self.pending = None
                 if self.eg.rank == 0 and self.eg.grank == 0:
                     self.coord.requeue_inflight()
                 deadline = time.monotonic() + 10
@@ -266,4 +329,9 @@ class CollectiveService:
                     time.sleep(0.01)  # let SWIM confirm who died
                 self.eg.rebuild(set(self.eg.dead), decide=(self.eg.grank == 0))
                 self.rebuilds += 1
+        else:
+            try:
+                self._collect()
+            except CollectiveFailure:
+                pass
         return self.steps

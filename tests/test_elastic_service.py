@@ -81,3 +81,25 @@ def test_worker_kill_mid_job_recovers(tmp_path):
     assert res["requeued"] >= 1
     # at-least-once: every image of both jobs was served
     assert res["c1"]["ResNet50"]["query_count"] >= 96 and res["c1"]["InceptionV3"]["query_count"] >= 96
+
+
+def test_coordinator_two_steps_in_flight_requeue_order():
+    """Pipelined service: steps k-1 and k are both in flight; a failure requeues
+    both at the queue front in their original order; completion is per step."""
+    from distributed_machine_learning_amd.parallel.dataplane import F_BATCH
+    from distributed_machine_learning_amd.parallel.service import CollectiveCoordinator
+
+    c = CollectiveCoordinator({"ResNet50": 4, "InceptionV3": 4}, {"ResNet50": 64, "InceptionV3": 64})
+    c.submit("ResNet50", 16)                       # 4 batches of 4
+    t0 = c.next_table([0])
+    t1 = c.next_table([0])
+    assert sorted(c.inflight) == [0, 1] and c.steps == 2
+    first = [int(t0[0, F_BATCH]), int(t1[0, F_BATCH])]
+    assert c.requeue_inflight() == 2 and not c.inflight
+    t2 = c.next_table([0])
+    t3 = c.next_table([0])
+    assert [int(t2[0, F_BATCH]), int(t3[0, F_BATCH])] == first
+    c.complete([0], None, step=2)                  # out-of-order completion is per step
+    assert sorted(c.inflight) == [3]
+    c.complete([0], None)
+    assert not c.inflight and c.metrics.c1()["ResNet50"]["query_count"] == 8

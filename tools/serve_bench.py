@@ -66,9 +66,10 @@ def main():
         if a.inception_images:
             jobs.append(coord.submit("InceptionV3", a.inception_images))
     svc = CollectiveService(eg, backend, coord, kill_rank=kr, kill_at_step=ks, on_device=True)
-    # warm both engines (graph capture) outside the timed region
+    # warm both engines and both source slots (graph capture) outside the timed region
     for m in ("ResNet50", "InceptionV3"):
-        backend.run(m, 0, bs[m])
+        for slot in (0, 1):
+            backend.launch(m, 0, bs[m], slot)[1].synchronize()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     steps = svc.serve()
