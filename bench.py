@@ -44,6 +44,8 @@ def main() -> int:
     ap.add_argument("--model", default="ResNet50")
     ap.add_argument("--batch", type=int, default=0, help="per-worker batch (default 256 ResNet50 / 128 InceptionV3)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--splits", type=int, default=2,
+                    help="sub-batches of the per-worker batch, each on its own HIP stream (1 = one engine)")
     ap.add_argument("--op-times", default="", help="write per-op times (ms) of one forward to this JSON file")
     args = ap.parse_args()
 
@@ -51,7 +53,7 @@ def main() -> int:
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from distributed_machine_learning_amd.models import build_model, canonical_name
-    from distributed_machine_learning_amd.models.engine import Engine
+    from distributed_machine_learning_amd.models.engine import Engine, SplitEngine
     from distributed_machine_learning_amd.parallel.dataplane import DESC_FIELDS, DataPlane, init_process_group
     from distributed_machine_learning_amd.parallel.pipeline import ServingPipeline
     from distributed_machine_learning_amd.parallel.staging import PinnedImageStore
@@ -65,7 +67,10 @@ def main() -> int:
     torch.cuda.set_device(device)
 
     g, w = build_model(model, seed=0, calibrate=True)
-    eng = Engine(g, w, batch=B, device=str(device), src_slots=2)
+    if args.splits > 1:
+        eng = SplitEngine(g, w, batch=B, device=str(device), src_slots=2, splits=args.splits)
+    else:
+        eng = Engine(g, w, batch=B, device=str(device), src_slots=2)
     store = PinnedImageStore(capacity=4 * B, hw=g.input_hw)
     store.fill_synthetic(seed=rank)
     dp = DataPlane(device, result_shape=(2, B, 5))
@@ -97,7 +102,7 @@ def main() -> int:
     if args.op_times and rank == 0:
         times = eng.time_ops(torch.cuda.current_stream())
         with open(args.op_times, "w") as f:
-            json.dump({"model": model, "batch": B, "ops": times,
+            json.dump({"model": model, "batch": B // max(args.splits, 1), "ops": times,
                        "cfg": eng.op_cfg, "total_ms": sum(t for _, t in times)}, f, indent=1)
 
     if rank == 0:
@@ -119,7 +124,7 @@ def main() -> int:
             "data": "synthetic uint8 RGB images, random-init weights (Keras architecture)",
             "config": {"model": model, "global_batch": B * world, "seq_len": None,
                        "image_hw": list(g.input_hw), "parallelism": f"dp{world}",
-                       "per_worker_batch": B, "graph": not args.no_graph},
+                       "per_worker_batch": B, "graph": not args.no_graph, "stream_splits": args.splits},
             "p50_latency_ms": round(pct.get("p50_ms", 0.0), 3),
             "p90_latency_ms": round(pct.get("p90_ms", 0.0), 3),
             "p99_latency_ms": round(pct.get("p99_ms", 0.0), 3),

@@ -49,7 +49,7 @@ def save_cache(table: Dict[str, int], path: str = CACHE_PATH) -> None:
         os.makedirs(os.path.dirname(path), exist_ok=True)
         cur = load_cache(path)
         cur.update(table)
-        tmp = path + ".tmp"
+        tmp = f"{path}.{os.getpid()}.tmp"  # ranks of one node may tune concurrently
         with open(tmp, "w") as f:
             json.dump(dict(sorted(cur.items())), f, indent=0)
         os.replace(tmp, path)

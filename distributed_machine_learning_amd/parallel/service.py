@@ -89,9 +89,9 @@ class GpuRankBackend(RankBackend):
     stream); results land in one of two output slots."""
 
     def __init__(self, device: torch.device, batch_sizes: Dict[str, int], arena_images: int = 512, seed: int = 0,
-                 models: Sequence[str] = MODELS):
+                 models: Sequence[str] = MODELS, splits: int = 2):
         from ..models import build_model
-        from ..models.engine import Engine
+        from ..models.engine import Engine, SplitEngine
         from .staging import PinnedImageStore
 
         self.device = device
@@ -101,7 +101,11 @@ class GpuRankBackend(RankBackend):
         self.copy_stream = torch.cuda.Stream(device)
         for m in models:
             g, w = build_model(m, seed=seed, calibrate=True)
-            self.engines[m] = Engine(g, w, batch=batch_sizes[m], device=str(device), src_slots=2)
+            b = batch_sizes[m]
+            if splits > 1 and b % splits == 0:
+                self.engines[m] = SplitEngine(g, w, batch=b, device=str(device), src_slots=2, splits=splits)
+            else:
+                self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=2)
             st = PinnedImageStore(arena_images, g.input_hw)
             st.fill_synthetic(seed=1000 + MODEL_IDS[m])
             self.stores[m] = st

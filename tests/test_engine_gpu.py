@@ -117,3 +117,26 @@ def test_batch_rows_independent():
         outs.append(e1.buf[g.logits].clone())
     torch.cuda.synchronize()
     assert torch.allclose(torch.cat(outs), e4.buf[g.logits], atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_split_engine_matches_engine(use_graph):
+    """SplitEngine (2 sub-batches on 2 streams, shared weights) == plain Engine runs of each half."""
+    from distributed_machine_learning_amd.models.engine import SplitEngine
+
+    g, w = build_model("ResNet50", seed=3, calibrate=False)
+    imgs = torch.randint(0, 256, (8, 224, 224, 3), dtype=torch.uint8, device="cuda")
+    se = SplitEngine(g, w, batch=8, splits=2, src_slots=2)
+    assert se.engines[1].wdev is se.engines[0].wdev  # weights resident once
+    e4 = Engine(g, w, batch=4)
+    s = torch.cuda.Stream()
+    se.srcs[1].copy_(imgs)
+    with torch.cuda.stream(s):
+        se.run(s, use_graph=use_graph, slot=1)
+    s.synchronize()
+    ref = []
+    for h in range(2):
+        e4.infer(imgs[4 * h: 4 * h + 4])
+        torch.cuda.synchronize()
+        ref.append(e4.result.clone())
+    assert torch.equal(se.result, torch.cat(ref, dim=1))
