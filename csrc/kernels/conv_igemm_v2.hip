@@ -32,7 +32,7 @@ using convk::lds_swz;
 using convk::lds_void;
 using convk::wait_vmcnt;
 
-template <int BM, int BN, int WM, int WN, int STAGES>
+template <int BM, int BN, int WM, int WN, int STAGES, int BK_ = 64>
 struct Cfg {
   static constexpr int NW = WM * WN;          // waves
   static constexpr int NT = NW * 64;          // threads
@@ -40,24 +40,26 @@ struct Cfg {
   static constexpr int WTC = BN / WN;         // channels per wave
   static constexpr int FJ = WTP / 16;         // fragments along pixels
   static constexpr int FI = WTC / 16;         // fragments along channels
-  static constexpr int BK = 64;
-  static constexpr int ROWB = BK * 2;         // 128 B per tile row
-  static constexpr int XI = BM / 8 / NW;      // X DMA instructions per wave per K tile
-  static constexpr int WI = BN / 8 / NW;      // W DMA instructions per wave per K tile
+  static constexpr int BK = BK_;
+  using R = convk::Rows<BK>;
+  static constexpr int ROWB = R::ROWB;        // 128 B (BK 64) or 64 B (BK 32) per tile row
+  static constexpr int XI = BM / R::RP / NW;  // X DMA instructions per wave per K tile
+  static constexpr int WI = BN / R::RP / NW;  // W DMA instructions per wave per K tile
   static constexpr int L = XI + WI;           // vm ops per thread per K tile
   static constexpr int STAGE_BYTES = (BM + BN) * ROWB;
   static constexpr int PIPE_BYTES = STAGES * STAGE_BYTES;
   static constexpr int EPI_BYTES = BM * (BN * 4 + 16);  // = convk::Epilogue<BM, BN, NT, *>::BYTES
   static constexpr int LDS = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
   static_assert(XI >= 1 && WI >= 1, "each wave needs >=1 DMA instruction per operand");
-  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split evenly across waves");
+  static_assert(BM % (R::RP * NW) == 0 && BN % (R::RP * NW) == 0, "tile rows must split evenly across waves");
   static_assert(FI >= 1 && FJ >= 1, "wave tile too small");
   static_assert((STAGES - 2) * L < 64, "vmcnt overflow");
 };
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool RES>
+template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK = 64>
 __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
-  using T = Cfg<BM, BN, WM, WN, STAGES>;
+  using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
+  using RW = typename T::R;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int M = a.N * a.Ho * a.Wo;
@@ -71,9 +73,9 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   // ---- per-lane DMA bookkeeping ----
-  const int lrow = lane >> 3;                  // row within an 8-row DMA piece
-  const int lchunk = (lane & 7) ^ lrow;        // logical K chunk this lane always fetches
-  // X rows of this lane: piece q = wid*XI + j -> row 8q + lrow
+  const int lrow = RW::lane_row(lane);         // row within an RP-row DMA piece
+  const int lchunk = RW::lane_chunk(lane);     // logical K chunk this lane always fetches
+  // X rows of this lane: piece q = wid*XI + j -> row RP*q + lrow
   // Element offset of (row, k) = base[row] + koff(k) with
   //   base[row] = (pix0 + ih0*W + iw0) * ldx          (per row, fixed)
   //   koff(k)   = (rr*dh*W + ss*dw) * ldx + cc        (per lane, row-independent)
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   const int HoWo = a.Ho * a.Wo;
 #pragma unroll
   for (int j = 0; j < T::XI; ++j) {
-    const int m = m0 + (wid * T::XI + j) * 8 + lrow;
+    const int m = m0 + (wid * T::XI + j) * RW::RP + lrow;
     if (m < M) {
       const int n = m / HoWo;
       const int rem = m - n * HoWo;
@@ -123,8 +125,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   // buffer descriptor over the activations (range check -> zero fill)
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, 0x7ffffff0, 0x00020000);
   const unsigned OOB = 0x80000000u;
-  const char* wbase = (const char*)a.w + ((long)(c0 + wid * T::WI * 8 + lrow) * a.Kpad + lchunk * 8) * 2;
-  const long wstep_row = (long)8 * a.Kpad * 2;  // next 8-row piece
+  const char* wbase = (const char*)a.w + ((long)(c0 + wid * T::WI * RW::RP + lrow) * a.Kpad + lchunk * 8) * 2;
+  const long wstep_row = (long)RW::RP * a.Kpad * 2;  // next RP-row piece
 
   const int nk = a.Kpad / T::BK;
 
@@ -180,18 +182,18 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
     // Both 32-deep k-steps' fragments are read up front (separate registers), so
     // the second step's ds_reads are in flight while the first step's MFMAs run;
     // hipcc emits a counted lgkmcnt before each MFMA group.
-    bf16x8 fa[2][T::FI], fb[2][T::FJ];
+    bf16x8 fa[RW::KS][T::FI], fb[RW::KS][T::FJ];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < RW::KS; ++ks) {
       const int ch = ks * 4 + fq;
 #pragma unroll
-      for (int i = 0; i < T::FI; ++i) fa[ks][i] = *(const bf16x8*)(sw + lds_swz(wc * T::WTC + i * 16 + frow, ch));
+      for (int i = 0; i < T::FI; ++i) fa[ks][i] = *(const bf16x8*)(sw + RW::off(wc * T::WTC + i * 16 + frow, ch));
 #pragma unroll
-      for (int j = 0; j < T::FJ; ++j) fb[ks][j] = *(const bf16x8*)(sx + lds_swz(wp * T::WTP + j * 16 + frow, ch));
+      for (int j = 0; j < T::FJ; ++j) fb[ks][j] = *(const bf16x8*)(sx + RW::off(wp * T::WTP + j * 16 + frow, ch));
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < RW::KS; ++ks)
 #pragma unroll
       for (int i = 0; i < T::FI; ++i)
 #pragma unroll
@@ -204,27 +206,27 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   epi.template store<T::FI, T::FJ, T::WTP, T::WTC>(a, smem, acc, wp, wc, lane, tid);
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES>
+template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
 static int launch(const DmlConvArgs* a, hipStream_t s) {
-  using T = Cfg<BM, BN, WM, WN, STAGES>;
+  using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
   const long M = (long)a->N * a->Ho * a->Wo;
   const long tiles = ((M + BM - 1) / BM) * ((a->Cout + BN - 1) / BN);
   if (a->res)
-    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, true>), dim3((unsigned)tiles), dim3(T::NT), T::LDS, s,
-                       *a);
-  else
-    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, false>), dim3((unsigned)tiles), dim3(T::NT), T::LDS,
+    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK>), dim3((unsigned)tiles), dim3(T::NT), T::LDS,
                        s, *a);
+  else
+    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK>), dim3((unsigned)tiles), dim3(T::NT),
+                       T::LDS, s, *a);
   DML_CHECK_LAUNCH();
   return 0;
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES>
+template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
 static int set_attr() {
-  using T = Cfg<BM, BN, WM, WN, STAGES>;
-  return (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, true>,
+  using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
+  return (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS) |
-         (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, false>,
+         (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
@@ -249,6 +251,12 @@ extern "C" int dml_conv_v2_init(void) {
   rc |= set_attr<128, 128, 4, 2, 3>();
   rc |= set_attr<128, 256, 2, 4, 2>();
   rc |= set_attr<64, 256, 1, 4, 2>();
+  rc |= set_attr<64, 128, 1, 4, 2, 32>();
+  rc |= set_attr<128, 64, 2, 2, 2, 32>();
+  rc |= set_attr<128, 128, 2, 2, 2, 32>();
+  rc |= set_attr<64, 128, 1, 4, 3, 32>();
+  rc |= set_attr<128, 64, 2, 2, 3, 32>();
+  rc |= set_attr<128, 128, 2, 2, 3, 32>();
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   return rc ? -1 : 0;
 }
@@ -270,6 +278,13 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
     case 20: return launch<128, 128, 4, 2, 3>(a, s);  // 8 waves, 32px x 64ch per wave, 3-stage
     case 21: return launch<128, 256, 2, 4, 2>(a, s);  // 8 waves, 64x64 per wave, 2-stage
     case 22: return launch<64, 256, 1, 4, 2>(a, s);   // 4 waves, 64px x 64ch per wave
+    // BK = 32 (64-B tile rows): half-size stages -> more workgroups per CU
+    case 23: return launch<64, 128, 1, 4, 2, 32>(a, s);
+    case 24: return launch<128, 64, 2, 2, 2, 32>(a, s);
+    case 25: return launch<128, 128, 2, 2, 2, 32>(a, s);
+    case 26: return launch<64, 128, 1, 4, 3, 32>(a, s);
+    case 27: return launch<128, 64, 2, 2, 3, 32>(a, s);
+    case 28: return launch<128, 128, 2, 2, 3, 32>(a, s);
     default: dml_set_error("dml_conv_v2: bad cfg"); return -1;
   }
 }

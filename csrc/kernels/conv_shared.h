@@ -25,6 +25,33 @@ __device__ __forceinline__ void wait_vmcnt() {
 // byte offset of 16-B chunk `chunk` (0..7) of 128-B tile row `row`
 __device__ __forceinline__ int lds_swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
+// 64-B tile rows (BK = 32): a ds_read_b128 lane group reads 16 rows; four rows
+// share each 256-B bank window, so the chunk is XORed with a per-row-quad key.
+// s(q) = {0, 2, 3, 1}[q], q = (row >> 2) & 3, makes all 4 lane groups of an MFMA
+// fragment read (16 rows x chunk fq = lane >> 4) hit 64 distinct banks.
+__device__ __forceinline__ int swz64_key(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
+__device__ __forceinline__ int lds_swz64(int row, int chunk) { return row * 64 + ((chunk ^ swz64_key(row)) << 4); }
+
+// tile-row geometry for BK = 64 (128-B rows) or BK = 32 (64-B rows)
+template <int BK>
+struct Rows {
+  static_assert(BK == 64 || BK == 32, "BK");
+  static constexpr int ROWB = BK * 2;            // bytes per tile row
+  static constexpr int CPR = ROWB / 16;          // 16-B chunks per row
+  static constexpr int RP = 1024 / ROWB;         // rows per 1-KiB DMA wave-instruction
+  static constexpr int KS = BK / 32;             // MFMA k-steps per tile
+  __device__ static __forceinline__ int off(int row, int chunk) {
+    return BK == 64 ? lds_swz(row, chunk) : lds_swz64(row, chunk);
+  }
+  // DMA: lane writes physical chunk (lane % CPR) of row (lane / CPR); it must
+  // fetch the logical chunk that the read side expects there
+  __device__ static __forceinline__ int lane_row(int lane) { return lane / CPR; }
+  __device__ static __forceinline__ int lane_chunk(int lane) {
+    const int r = lane / CPR;  // row within the piece; pieces start at multiples of RP (>= 8, aligned)
+    return BK == 64 ? ((lane & 7) ^ (r & 7)) : ((lane & 3) ^ swz64_key(r));
+  }
+};
+
 // Epilogue of a BM(pixels) x BN(channels) tile computed by NT threads.
 template <int BM, int BN, int NT, bool RES>
 struct Epilogue {

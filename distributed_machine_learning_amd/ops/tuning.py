@@ -18,7 +18,7 @@ from typing import Dict, Iterable, List, Optional, Tuple
 
 from .. import _native as N
 
-V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22)
+V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27)  # 23..28: BK = 32 tile rows
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))
@@ -26,6 +26,8 @@ _lock = threading.Lock()
 
 
 HALO_CFGS = (40, 41, 42, 43, 44, 45, 46, 47)  # conv_halo.hip (stride-1, chunk-major weights)
+# cache entries are only valid for the candidate set they were timed against
+CAND_TAG = "c" + format(sum((i + 1) * c for i, c in enumerate(V2_CFGS + HALO_CFGS)) % 4096, "03x")
 
 
 def shape_key(a: N.ConvArgs, halo: bool = False) -> str:
@@ -33,7 +35,7 @@ def shape_key(a: N.ConvArgs, halo: bool = False) -> str:
     configs as candidates (so entries tuned before they existed are re-timed)."""
     return (f"n{a.N}_h{a.H}_w{a.W}_c{a.Cin}_ld{a.ldx}_k{a.kh}x{a.kw}_s{a.sh}x{a.sw}_p{a.ph}x{a.pw}"
             f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}_d{max(a.dh, 1)}x{max(a.dw, 1)}"
-            + ("_halo" if halo else ""))
+            + ("_halo" if halo else "") + "_" + CAND_TAG)
 
 
 def load_cache(path: str = CACHE_PATH) -> Dict[str, int]:
@@ -47,7 +49,7 @@ def load_cache(path: str = CACHE_PATH) -> Dict[str, int]:
 def save_cache(table: Dict[str, int], path: str = CACHE_PATH) -> None:
     with _lock:
         os.makedirs(os.path.dirname(path), exist_ok=True)
-        cur = load_cache(path)
+        cur = {k: v for k, v in load_cache(path).items() if k.endswith("_" + CAND_TAG)}  # drop stale tags
         cur.update(table)
         tmp = f"{path}.{os.getpid()}.tmp"  # ranks of one node may tune concurrently
         with open(tmp, "w") as f:
