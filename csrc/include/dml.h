@@ -93,6 +93,9 @@ int dml_plan_run(void* plan, hipStream_t s);
 int dml_plan_run_range(void* plan, int begin, int end, hipStream_t s);
 int dml_plan_capture(void* plan, hipStream_t s);   // capture the whole plan into a hipGraph
 int dml_plan_replay(void* plan, hipStream_t s);    // launch the captured graph
+// capture op ranges [bounds[i], bounds[i+1]) as separate graphs / launch graph i
+int dml_plan_capture_parts(void* plan, const int* bounds, int nparts, hipStream_t s);
+int dml_plan_replay_part(void* plan, int i, hipStream_t s);
 int dml_plan_time_ops(void* plan, hipStream_t s, float* ms_out, int n);  // per-op hipEvent timing
 
 // ---- pinned-host staging ring (csrc/runtime/staging.cpp) ----

@@ -58,9 +58,18 @@ struct Plan {
   std::vector<Op> ops;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
+  std::vector<hipGraph_t> part_graphs;      // dml_plan_capture_parts: one graph per op range
+  std::vector<hipGraphExec_t> part_execs;
+  void clear_parts() {
+    for (auto e : part_execs) (void)hipGraphExecDestroy(e);
+    for (auto g : part_graphs) (void)hipGraphDestroy(g);
+    part_execs.clear();
+    part_graphs.clear();
+  }
   ~Plan() {
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);
+    clear_parts();
   }
 };
 
@@ -139,6 +148,35 @@ extern "C" int dml_plan_capture(void* p, hipStream_t s) {
   if (e != hipSuccess) { g_err = hipGetErrorString(e); return -1; }
   pl->graph = g;
   HIP_OK(hipGraphInstantiate(&pl->exec, g, nullptr, nullptr, 0));
+  return 0;
+}
+// Capture ops [bounds[i], bounds[i+1]) as graph i (i < nparts): the forward can
+// then be replayed in pieces, e.g. to stagger sub-batches on two streams.
+extern "C" int dml_plan_capture_parts(void* p, const int* bounds, int nparts, hipStream_t s) {
+  Plan* pl = (Plan*)p;
+  pl->clear_parts();
+  for (int i = 0; i < nparts; ++i) {
+    if (bounds[i] < 0 || bounds[i] > bounds[i + 1] || bounds[i + 1] > (int)pl->ops.size()) {
+      g_err = "dml_plan_capture_parts: bad bounds";
+      return -1;
+    }
+    HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    int rc = dml_plan_run_range(p, bounds[i], bounds[i + 1], s);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(s, &g);
+    if (rc) return rc;
+    if (e != hipSuccess) { g_err = hipGetErrorString(e); return -1; }
+    hipGraphExec_t x = nullptr;
+    HIP_OK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+    pl->part_graphs.push_back(g);
+    pl->part_execs.push_back(x);
+  }
+  return 0;
+}
+extern "C" int dml_plan_replay_part(void* p, int i, hipStream_t s) {
+  Plan* pl = (Plan*)p;
+  if (i < 0 || i >= (int)pl->part_execs.size()) { g_err = "dml_plan_replay_part: not captured"; return -1; }
+  HIP_OK(hipGraphLaunch(pl->part_execs[i], s));
   return 0;
 }
 extern "C" int dml_plan_replay(void* p, hipStream_t s) {

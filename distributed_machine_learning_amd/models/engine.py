@@ -318,6 +318,16 @@ class Engine:
         else:
             N.check(self.lib.dml_plan_run(plan, s), "plan run")
 
+    def capture_parts(self, bounds: List[int], stream=None, slot: int = 0) -> None:
+        """Capture the forward of source slot ``slot`` as len(bounds)-1 graphs over
+        op ranges [bounds[i], bounds[i+1]) (op indices as in ``op_names``)."""
+        arr = (C.c_int * len(bounds))(*bounds)
+        N.check(self.lib.dml_plan_capture_parts(self.plans[slot], arr, len(bounds) - 1, N.stream_ptr(stream)),
+                "plan capture_parts")
+
+    def run_part(self, i: int, stream=None, slot: int = 0) -> None:
+        N.check(self.lib.dml_plan_replay_part(self.plans[slot], i, N.stream_ptr(stream)), "plan replay_part")
+
     def run_from_preprocessed(self, stream=None) -> None:
         N.check(self.lib.dml_plan_run_range(self.plan, 1, -1, N.stream_ptr(stream)), "plan run_range")
 

@@ -140,3 +140,21 @@ def test_split_engine_matches_engine(use_graph):
         torch.cuda.synchronize()
         ref.append(e4.result.clone())
     assert torch.equal(se.result, torch.cat(ref, dim=1))
+
+
+def test_capture_parts_matches_full_graph():
+    """Forward captured as 3 op-range graphs (dml_plan_capture_parts) == one full graph."""
+    g, w = build_model("ResNet50", seed=4, calibrate=False)
+    eng = Engine(g, w, batch=2)
+    eng.src.copy_(torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda"))
+    s = torch.cuda.Stream()
+    eng.run(s, use_graph=True)
+    s.synchronize()
+    full = eng.result.clone()
+    eng.result.zero_()
+    n = len(eng.op_names)
+    eng.capture_parts([0, n // 3, 2 * n // 3, n], s)
+    for i in range(3):
+        eng.run_part(i, s)
+    s.synchronize()
+    assert torch.equal(full, eng.result)
