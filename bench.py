@@ -47,6 +47,7 @@ def main() -> int:
     ap.add_argument("--splits", type=int, default=2,
                     help="sub-batches of the per-worker batch, each on its own HIP stream (1 = one engine)")
     ap.add_argument("--op-times", default="", help="write per-op times (ms) of one forward to this JSON file")
+    ap.add_argument("--trace", default="", help="Chrome-trace JSON of the timed steps ('{rank}' -> rank id)")
     args = ap.parse_args()
 
     import torch
@@ -57,6 +58,8 @@ def main() -> int:
     from distributed_machine_learning_amd.parallel.dataplane import DESC_FIELDS, DataPlane, init_process_group
     from distributed_machine_learning_amd.parallel.pipeline import ServingPipeline
     from distributed_machine_learning_amd.parallel.staging import PinnedImageStore
+
+    from distributed_machine_learning_amd.utils import trace as _trace
 
     model = canonical_name(args.model)
     B = args.batch or DEFAULT_BATCH[model]
@@ -90,6 +93,8 @@ def main() -> int:
     pipe.run(max(args.warmup, 1), table, record=False)
     pipe.stats.latencies_s.clear()
     pipe.stats.images = 0
+    if args.trace:
+        _trace.set_tracer(_trace.Tracer(process_name=f"bench rank {rank}", pid=rank))
 
     dp.barrier()
     torch.cuda.synchronize()
@@ -99,6 +104,10 @@ def main() -> int:
     dp.barrier()
     elapsed = dp.max_over_ranks(time.perf_counter() - t0)
 
+    if args.trace:
+        tr = _trace.get_tracer()
+        tr.add_gpu_ops(eng.time_ops(torch.cuda.current_stream()), lane="one sub-batch forward, per op")
+        tr.export_chrome(args.trace.replace("{rank}", str(rank)))
     if args.op_times and rank == 0:
         times = eng.time_ops(torch.cuda.current_stream())
         with open(args.op_times, "w") as f:

@@ -20,6 +20,7 @@ from typing import Callable, List, Optional
 import numpy as np
 import torch
 
+from ..utils import trace as _trace
 from .dataplane import DataPlane, F_COUNT, F_START
 from .staging import PinnedImageStore
 
@@ -67,31 +68,39 @@ class ServingPipeline:
         cs = self.copy_stream
         cs.wait_event(self.ev_consumed[slot])  # WAR: compute(step-2) finished reading this slot
         count = int(row[F_COUNT])
-        self.store.h2d(self.eng.srcs[slot], int(row[F_START]), count, cs)
+        with _trace.get_tracer().gpu_span("h2d", cs, lane="copy stream", step=step, images=count):
+            self.store.h2d(self.eng.srcs[slot], int(row[F_START]), count, cs)
         self.ev_copied[slot].record(cs)
 
     def run(self, steps: int, table_fn: Callable[[int], np.ndarray], record: bool = True) -> PipelineStats:
         """Serve `steps` batches; table_fn(k) -> descriptor table (used on rank 0)."""
         dp, eng = self.dp, self.eng
+        tr = _trace.get_tracer()
         is0 = dp.rank == 0
         recs: List[BatchRecord] = []
         t0 = time.perf_counter()
         recs.append(BatchRecord(0, t0))
-        row = dp.dispatch(table_fn(0) if is0 else None)
+        if is0:
+            tr.begin_async("batch", 0, step=0)
+        with tr.span("dispatch", step=0):
+            row = dp.dispatch(table_fn(0) if is0 else None)
         self._stage(0, row)
         prev: Optional[BatchRecord] = None
         for k in range(steps):
             slot = k % 2
             cs = self.compute_stream
             cs.wait_event(self.ev_copied[slot])
-            with torch.cuda.stream(cs):
+            with torch.cuda.stream(cs), tr.gpu_span("forward", cs, lane="compute stream", step=k):
                 eng.run(cs, use_graph=self.use_graph, slot=slot)
             self.ev_consumed[slot].record(cs)
             if k + 1 < steps:  # dispatch + stage the next batch while this one computes
                 recs.append(BatchRecord(k + 1, time.perf_counter()))
-                row = dp.dispatch(table_fn(k + 1) if is0 else None)
+                if is0:
+                    tr.begin_async("batch", k + 1, step=k + 1)
+                with tr.span("dispatch", step=k + 1):
+                    row = dp.dispatch(table_fn(k + 1) if is0 else None)
                 self._stage(k + 1, row)
-            with torch.cuda.stream(cs):
+            with torch.cuda.stream(cs), tr.gpu_span("gather", cs, lane="compute stream", step=k):
                 bufs = dp.gather(eng.result)
                 if is0:
                     hr = self.host_res[slot]
@@ -108,9 +117,12 @@ class ServingPipeline:
 
     def _finish(self, rec: BatchRecord, record: bool) -> None:
         slot = rec.step % 2
+        tr = _trace.get_tracer()
         if self.dp.rank == 0:
-            self.ev_res[slot].synchronize()
+            with tr.span("wait results", step=rec.step):
+                self.ev_res[slot].synchronize()
             rec.t_done = time.perf_counter()
+            tr.end_async("batch", rec.step, latency_ms=(rec.t_done - rec.t_dispatch) * 1e3)
             if record:
                 self.stats.latencies_s.append(rec.t_done - rec.t_dispatch)
                 self.stats.images += self.dp.world * self.eng.batch

@@ -23,8 +23,10 @@ from typing import Callable, Dict, List, Optional, Tuple
 from ..cluster.frames import Frame, MsgType
 from ..cluster.membership import MembershipList
 from ..cluster.transport import Endpoint
+from ..utils import trace as _trace
 from .cost_model import CostModel
 from .jobs import MODELS, Batch, Job, JobManager
+from .journal import JobJournal
 from .metrics import Metrics
 from .scheduler import plan
 
@@ -35,7 +37,7 @@ class Coordinator:
     def __init__(self, ep: Endpoint, ml: MembershipList, list_images: Callable[[str], List[str]],
                  locate: Callable[[str], Dict[str, List[int]]], batch_sizes: Optional[Dict[str, int]] = None,
                  is_active: Callable[[], bool] = lambda: True, worker_filter: Optional[Callable[[str], bool]] = None,
-                 clock=time.monotonic):
+                 clock=time.monotonic, journal: Optional[JobJournal] = None):
         self.ep, self.ml = ep, ml
         self.list_images = list_images    # pattern -> sorted image names in the store
         self.locate = locate              # image -> {node: [versions]}
@@ -61,6 +63,19 @@ class Coordinator:
         on(MsgType.JOB_STATUS, self._on_job_status)
         self.mirror = StandbyMirror(self)
         on(MsgType.STANDBY_SYNC, self.mirror.on_sync)
+        self.journal = journal
+        self.recovered = self._recover() if journal is not None else 0
+
+    def _recover(self) -> int:
+        """Replay the journal (same apply path as the standby mirror); batches
+        in flight at the crash go back to the front of their queues."""
+        n = self.journal.replay(self.mirror.apply)
+        for w in list(self.running):
+            self._requeue_worker(w, relay=False)
+        if n:
+            log.info("coordinator recovered %d journal entries: %d queued batches", n, self.jobs.pending())
+            self.journal.compact(self.jobs.snapshot())
+        return n
 
     # ------------------------------------------------------------ helpers --
     def workers(self) -> List[str]:
@@ -71,6 +86,9 @@ class Coordinator:
                 if self.ml.get(n).meta.get("role") == "standby"]
 
     async def relay(self, op: str, **kw) -> None:
+        if self.journal is not None:
+            self.journal.append(op, **kw)
+            self.journal.maybe_compact(self.jobs.snapshot)
         for s in self.standbys():
             await self.ep.send(s, MsgType.STANDBY_SYNC, {"op": op, **kw})
 
@@ -78,6 +96,8 @@ class Coordinator:
     async def submit(self, model: str, n_images: int, requester: str) -> Job:
         images = self.list_images("*.jpeg")
         job = self.jobs.submit(model, n_images, images, requester, now=self.clock())
+        _trace.get_tracer().instant("submit", cat="job", job=job.job_id, model=model, images=n_images,
+                                    batches=job.batches_total)
         batches = [b.to_dict() for b in self.jobs.queues[model] if b.job_id == job.job_id]
         await self.relay("submit", job={"job_id": job.job_id, "model": model, "n_images": n_images,
                                         "requester": requester, "batches_total": job.batches_total,
@@ -115,6 +135,7 @@ class Coordinator:
                     self.jobs.requeue_front(pkey)
                     self.running.pop(a.worker, None)
                     self.preemptions += 1
+                    _trace.get_tracer().end_async("batch", f"{pkey[0]}:{pkey[1]}", cat="job", outcome="preempted")
                     await self.relay("requeue", key=list(pkey))
                 b = self.jobs.pop_next(a.model)
                 if b is None:
@@ -127,6 +148,8 @@ class Coordinator:
         images = {img: self.locate(img) for img in b.images}
         self.running[worker] = (b.model, b.key, self.clock())
         self.dispatched += 1
+        _trace.get_tracer().begin_async("batch", f"{b.job_id}:{b.batch_id}", cat="job", worker=worker,
+                                        model=b.model, images=len(b.images), attempt=b.attempts)
         await self.relay("dispatch", worker=worker, batch=b.to_dict())
         r = await self.ep.request(worker, MsgType.WORKER_TASK_REQUEST,
                                   {"jobid": b.job_id, "batchid": b.batch_id, "model": b.model, "images": images},
@@ -134,13 +157,15 @@ class Coordinator:
         if r is None and not self.ml.is_alive(worker):
             self._requeue_worker(worker)
 
-    def _requeue_worker(self, worker: str) -> Optional[Batch]:
+    def _requeue_worker(self, worker: str, relay: bool = True) -> Optional[Batch]:
         ent = self.running.pop(worker, None)
         if ent is None:
             return None
         self.requeues += 1
         b = self.jobs.requeue_front(ent[1])
-        asyncio.get_running_loop().create_task(self.relay("requeue", key=list(ent[1])))
+        _trace.get_tracer().end_async("batch", f"{ent[1][0]}:{ent[1][1]}", cat="job", outcome="requeued")
+        if relay:
+            asyncio.get_running_loop().create_task(self.relay("requeue", key=list(ent[1])))
         return b
 
     def worker_failed(self, worker: str) -> None:
@@ -166,6 +191,8 @@ class Coordinator:
         job = self.jobs.complete(key, now=self.clock())
         if job is not None:
             n = int(p.get("image_count", 0))
+            _trace.get_tracer().end_async("batch", f"{key[0]}:{key[1]}", cat="job", outcome="done",
+                                          latency_ms=latency * 1e3)
             self.metrics.record(p["model"], latency, float(p.get("service_time", latency)), n)
             self.cost.observe(p["model"], n, float(p.get("service_time", latency)))
             await self.relay("complete", key=list(key), model=p["model"], latency=latency,
@@ -219,12 +246,19 @@ class StandbyMirror:
         self.applied = 0
 
     async def on_sync(self, fr: Frame) -> None:
-        c, p = self.c, fr.payload
-        if c.is_active():
+        if self.c.is_active():
             return
+        self.apply(fr.payload)
+
+    def apply(self, p: dict) -> None:
+        """Apply one relayed / journaled transition to the local state."""
+        c = self.c
         op = p.get("op")
         jm = c.jobs
-        if op == "submit":
+        if op == "snapshot":
+            jm.restore(p["state"], requeue_inprogress=True)
+            c.running.clear()
+        elif op == "submit":
             j = p["job"]
             jm.jobs[j["job_id"]] = Job(j["job_id"], j["model"], j["n_images"], j["requester"], j["batches_total"],
                                        0, j.get("submitted_at", 0.0))

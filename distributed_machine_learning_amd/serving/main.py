@@ -5,6 +5,13 @@
       --role coordinator --introducer 127.0.0.1:8888 [--backend gpu|cpu|fake] [-t] \
       [--cmd "5 /path/to/testfiles" --cmd "submit-job ResNet50 100" ...]
 
+  python -m distributed_machine_learning_amd.serving.main --config configs/local10.toml --node H3
+
+With ``--config`` the node takes its role, address, backend and every cluster
+setting from the file's entry for ``--node`` (utils/config.py); flags given
+explicitly on the command line still override the file. ``--trace out.json``
+writes a Chrome trace of the node's job / batch lifecycle at exit.
+
 With no ``--cmd`` the node runs the interactive stdin menu (cli.py); with
 ``--cmd`` it executes the commands in order and keeps serving until
 ``--exit-after`` seconds (or forever).
@@ -24,7 +31,11 @@ from .node import Node, NodeConfig
 def parse(argv=None) -> argparse.Namespace:
     ap = argparse.ArgumentParser(description="distributed inference node")
     ap.add_argument("-H", "--hostname", default="127.0.0.1")
-    ap.add_argument("-p", "--port", type=int, required=True)
+    ap.add_argument("-p", "--port", type=int, default=None)
+    ap.add_argument("--config", default="", help="cluster config file (TOML/JSON), utils/config.py")
+    ap.add_argument("--node", default="", help="this node's name / host:port / index in --config")
+    ap.add_argument("--journal", default=None, help="coordinator job journal (restart recovery)")
+    ap.add_argument("--trace", default="", help="write a Chrome trace of this node at exit")
     ap.add_argument("-t", "--testing", action="store_true", help="3%% send drop + bps/false-positive meters")
     ap.add_argument("--role", default="worker", choices=["coordinator", "standby", "worker", "client"])
     ap.add_argument("--introducer", default="127.0.0.1:8888")
@@ -42,18 +53,60 @@ def parse(argv=None) -> argparse.Namespace:
     ap.add_argument("--cmd", action="append", default=[])
     ap.add_argument("--exit-after", type=float, default=0.0)
     ap.add_argument("--log", default="debug.log")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    a.explicit = {k for k, v in vars(a).items() if v != ap.get_default(k)}
+    if a.port is None and not (a.config and a.node):
+        ap.error("--port is required (or --config with --node)")
+    return a
 
 
-async def amain(a: argparse.Namespace) -> int:
+def node_config(a: argparse.Namespace) -> NodeConfig:
+    """Build this node's NodeConfig from the flags, or from --config/--node
+    with explicitly given flags layered on top."""
     kw = {}
     if a.backend == "gpu":
         kw = {"device": f"cuda:{a.gpu}"}
-    cfg = NodeConfig(host=a.hostname, port=a.port, role=a.role, introducer=a.introducer or None,
-                     seeds=a.seed_node, store_dir=a.store_dir, out_dir=None, backend=a.backend, backend_kw=kw,
-                     testing=a.testing, period=a.period, ping_timeout=a.ping_timeout,
-                     suspect_timeout=a.suspect_timeout, cleanup_time=a.cleanup,
-                     batch_sizes={"ResNet50": a.batch_size, "InceptionV3": a.batch_size})
+    if not a.config:
+        return NodeConfig(host=a.hostname, port=a.port, role=a.role, introducer=a.introducer or None,
+                          seeds=a.seed_node, store_dir=a.store_dir, out_dir=None, backend=a.backend, backend_kw=kw,
+                          testing=a.testing, period=a.period, ping_timeout=a.ping_timeout,
+                          suspect_timeout=a.suspect_timeout, cleanup_time=a.cleanup,
+                          batch_sizes={"ResNet50": a.batch_size, "InceptionV3": a.batch_size}, journal=a.journal)
+    from ..utils import config as _config
+
+    cluster = _config.load(a.config)
+    ex = a.explicit
+    ov = {"period": a.period if "period" in ex else None,
+          "ping_timeout": a.ping_timeout if "ping_timeout" in ex else None,
+          "suspect_timeout": a.suspect_timeout if "suspect_timeout" in ex else None,
+          "cleanup_time": a.cleanup if "cleanup" in ex else None,
+          "store_dir": a.store_dir if "store_dir" in ex else None,
+          "testing": True if "testing" in ex else None,
+          "journal": a.journal if "journal" in ex else None,
+          "introducer": a.introducer if "introducer" in ex else None}
+    if "batch_size" in ex:
+        ov["batch_sizes"] = {"ResNet50": a.batch_size, "InceptionV3": a.batch_size}
+    cfg = cluster.node_config(a.node or str(a.port), **ov)
+    for flag, attr in (("hostname", "host"), ("port", "port"), ("role", "role"), ("backend", "backend")):
+        if flag in ex:
+            setattr(cfg, attr, getattr(a, flag))
+    if "backend" in ex or "gpu" in ex:
+        cfg.backend_kw = kw
+    if "seed_node" in ex:
+        cfg.seeds = a.seed_node
+    if not a.testfiles and cluster.testfiles:
+        a.testfiles = cluster.testfiles
+    if "download_dir" not in ex:
+        a.download_dir = cluster.download_dir
+    return cfg
+
+
+async def amain(a: argparse.Namespace) -> int:
+    cfg = node_config(a)
+    if a.trace:
+        from ..utils import trace as _trace
+
+        tr = _trace.set_tracer(_trace.Tracer(process_name=f"node {cfg.host}:{cfg.port} ({cfg.role})"))
     node = await Node(cfg).start()
     await node.join()
     cli = Cli(node, testfiles=a.testfiles, download_dir=a.download_dir)
@@ -73,6 +126,8 @@ async def amain(a: argparse.Namespace) -> int:
             except asyncio.TimeoutError:
                 pass
             await node.stop()
+            if a.trace:
+                tr.export_chrome(a.trace)
             return 0
     else:
         print(MENU, flush=True)
@@ -90,6 +145,8 @@ async def amain(a: argparse.Namespace) -> int:
         loop.create_task(reader())
     await stop.wait()
     await node.stop()
+    if a.trace:
+        tr.export_chrome(a.trace)
     return 0
 
 

@@ -30,6 +30,7 @@ from ..store.blob import BlobServer, BlobSource, InProcBlobNetwork, TcpBlobClien
 from ..store.local_store import LocalFileStore
 from ..store.service import StoreService
 from .coordinator import Coordinator
+from .journal import open_journal
 from .inference import Backend, make_backend
 from .worker import WorkerRole
 
@@ -56,6 +57,7 @@ class NodeConfig:
     replication: int = 4
     batch_sizes: Dict[str, int] = field(default_factory=lambda: {"ResNet50": 10, "InceptionV3": 10})
     store_timeout: float = 10.0
+    journal: Optional[str] = None        # coordinator job journal (restart recovery), serving/journal.py
 
 
 class Node:
@@ -103,7 +105,7 @@ class Node:
         if meta["eligible"]:
             self.coordinator = Coordinator(self.ep, self.ml, list_images=self.store.meta.matching,
                                            locate=self.store.meta.holders, batch_sizes=dict(cfg.batch_sizes),
-                                           is_active=lambda: self.is_leader())
+                                           is_active=lambda: self.is_leader(), journal=open_journal(cfg.journal))
         self.worker: Optional[WorkerRole] = None
         if cfg.role == "worker":
             be = self._backend or make_backend(cfg.backend, **cfg.backend_kw)

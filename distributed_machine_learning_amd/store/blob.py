@@ -102,8 +102,9 @@ class TcpBlobClient:
         self.resolve = resolve  # node name -> "host:port" of its blob server
         self.bytes_fetched = 0
 
-    async def fetch(self, node: str, req: dict, timeout: float = 30.0) -> List[Tuple[int, bytes]]:
-        addr = self.resolve(node)
+    async def fetch(self, node: str, req: dict, timeout: float = 30.0, addr: Optional[str] = None
+                    ) -> List[Tuple[int, bytes]]:
+        addr = self.resolve(node) or addr
         if addr is None:
             raise ConnectionError(f"no blob address for {node}")
         host, port = addr.rsplit(":", 1)
@@ -133,7 +134,8 @@ class InProcBlobNetwork:
     def register(self, node: str, source: BlobSource) -> None:
         self.sources[node] = source
 
-    async def fetch(self, node: str, req: dict, timeout: float = 30.0) -> List[Tuple[int, bytes]]:
+    async def fetch(self, node: str, req: dict, timeout: float = 30.0, addr: Optional[str] = None
+                    ) -> List[Tuple[int, bytes]]:
         if node in self.dead or node not in self.sources:
             raise ConnectionError(node)
         await asyncio.sleep(0)

@@ -70,8 +70,12 @@ class StoreService:
     # ========================================================== client API ==
     async def put(self, data: bytes, name: str) -> Tuple[bool, str]:
         tok = self.source.stage(data)
+        me = self.ml.get(self.me)
+        # our blob address rides along: replicas may not have our membership
+        # metadata yet right after we joined
+        blob = me.meta.get("blob") if me is not None else None
         try:
-            r = await self._leader_request(MsgType.PUT_REQUEST, {"filename": name, "token": tok},
+            r = await self._leader_request(MsgType.PUT_REQUEST, {"filename": name, "token": tok, "blob": blob},
                                            timeout=self.timeout * 3)
         finally:
             self.source.unstage(tok)
@@ -153,7 +157,8 @@ class StoreService:
             return
         version = self.meta.latest_version(name) + 1
         self.meta.begin(name, targets)
-        req = {"filename": name, "version": version, "source": fr.sender, "token": fr.payload.get("token")}
+        req = {"filename": name, "version": version, "source": fr.sender, "token": fr.payload.get("token"),
+               "source_blob": fr.payload.get("blob")}
         outcome = await self._fan_out(name, targets, req)
         self.meta.finish(name)
         if outcome == SUCCESS:
@@ -253,7 +258,8 @@ class StoreService:
     async def _r_download(self, fr: Frame) -> None:
         p = fr.payload
         try:
-            items = await self.blobs.fetch(p["source"], {"op": "outbox", "token": p.get("token")})
+            items = await self.blobs.fetch(p["source"], {"op": "outbox", "token": p.get("token")},
+                                           addr=p.get("source_blob"))
             if not items:
                 raise FileNotFoundError("outbox empty")
             self.local.put_bytes(p["filename"], items[0][1], version=p.get("version"))
