@@ -46,6 +46,8 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--splits", type=int, default=2,
                     help="sub-batches of the per-worker batch, each on its own HIP stream (1 = one engine)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="concurrent streams for the sub-batches (default = --splits); sub-batch i on stream i %% S")
     ap.add_argument("--op-times", default="", help="write per-op times (ms) of one forward to this JSON file")
     ap.add_argument("--trace", default="", help="Chrome-trace JSON of the timed steps ('{rank}' -> rank id)")
     args = ap.parse_args()
@@ -71,7 +73,7 @@ def main() -> int:
 
     g, w = build_model(model, seed=0, calibrate=True)
     if args.splits > 1:
-        eng = SplitEngine(g, w, batch=B, device=str(device), src_slots=2, splits=args.splits)
+        eng = SplitEngine(g, w, batch=B, device=str(device), src_slots=2, splits=args.splits, streams=args.streams)
     else:
         eng = Engine(g, w, batch=B, device=str(device), src_slots=2)
     store = PinnedImageStore(capacity=4 * B, hw=g.input_hw)
@@ -133,7 +135,8 @@ def main() -> int:
             "data": "synthetic uint8 RGB images, random-init weights (Keras architecture)",
             "config": {"model": model, "global_batch": B * world, "seq_len": None,
                        "image_hw": list(g.input_hw), "parallelism": f"dp{world}",
-                       "per_worker_batch": B, "graph": not args.no_graph, "stream_splits": args.splits},
+                       "per_worker_batch": B, "graph": not args.no_graph, "stream_splits": args.splits,
+                       "streams": eng.nstreams if args.splits > 1 else 1},
             "p50_latency_ms": round(pct.get("p50_ms", 0.0), 3),
             "p90_latency_ms": round(pct.get("p90_ms", 0.0), 3),
             "p99_latency_ms": round(pct.get("p99_ms", 0.0), 3),

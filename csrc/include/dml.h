@@ -42,6 +42,12 @@ typedef struct {
   int seg_ldy[4];
   int seg_relu[4];
   void* seg_y[4];
+  // Split-K (v2 kernels only; 0/1 = off): the K loop is cut into `ksplit`
+  // contiguous ranges, one per workgroup slice; slice s writes its fp32 partial
+  // sum to y + s * split_ld (elements) and only slice 0 adds the bias. The
+  // consumer sums the slices (dml_softmax_top5_split does, for the classifier).
+  int ksplit;
+  int split_ld;
 } DmlConvArgs;
 
 typedef struct {
@@ -77,6 +83,11 @@ int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);
 int dml_softmax_top5(const float* logits, int B, int classes, int ld, float* probs_out,
                      int* top_idx, float* top_p, hipStream_t s);
+// logits given as `nsplit` fp32 partial slices (split-K classifier): row r of
+// slice s at logits + s*split_ld + r*ld; the summed logits are written back to
+// slice 0 before the softmax.
+int dml_softmax_top5_split(float* logits, int B, int classes, int ld, int nsplit, int split_ld,
+                           float* probs_out, int* top_idx, float* top_p, hipStream_t s);
 int dml_preprocess(const DmlPreprocArgs* a, hipStream_t s);
 
 // ---- plan executor (C++ runtime, csrc/runtime/plan.cpp) ----
@@ -87,6 +98,8 @@ int dml_plan_add_pool(void* plan, const DmlPoolArgs* a);
 int dml_plan_add_gap(void* plan, const void* x, void* y, int N, int HW, int C, int ldx);
 int dml_plan_add_softmax_top5(void* plan, const float* logits, int B, int classes, int ld,
                               float* probs, int* idx, float* p);
+int dml_plan_add_softmax_top5_split(void* plan, float* logits, int B, int classes, int ld, int nsplit,
+                                    int split_ld, float* probs, int* idx, float* p);
 int dml_plan_add_preprocess(void* plan, const DmlPreprocArgs* a);
 int dml_plan_size(void* plan);
 int dml_plan_run(void* plan, hipStream_t s);

@@ -32,6 +32,9 @@ using convk::lds_swz;
 using convk::lds_void;
 using convk::wait_vmcnt;
 
+// workgroups per CU that the larger of two LDS regions allows (160 KiB per CU)
+constexpr int lds_occupancy(int a, int b) { return 163840 / (a > b ? a : b); }
+
 template <int BM, int BN, int WM, int WN, int STAGES, int BK_ = 64>
 struct Cfg {
   static constexpr int NW = WM * WN;          // waves
@@ -48,7 +51,17 @@ struct Cfg {
   static constexpr int L = XI + WI;           // vm ops per thread per K tile
   static constexpr int STAGE_BYTES = (BM + BN) * ROWB;
   static constexpr int PIPE_BYTES = STAGES * STAGE_BYTES;
-  static constexpr int EPI_BYTES = BM * (BN * 4 + 16);  // = convk::Epilogue<BM, BN, NT, *>::BYTES
+  // Epilogue staging passes: the fewest (1, 2, 4) whose fp32 staging rows fit in
+  // the operand ring, so the epilogue never raises the LDS size (occupancy).
+  static constexpr int CROW = BN * 4 + 16;
+  static constexpr bool EP_OK2 = (BM / 2) % 16 == 0 && ((BM * BN / 8) / NT) % 2 == 0;
+  static constexpr bool EP_OK4 = (BM / 4) % 16 == 0 && ((BM * BN / 8) / NT) % 4 == 0;
+  // most passes allowed, then back off to the fewest passes that keep that occupancy
+  static constexpr int EP_MAX = EP_OK4 ? 4 : (EP_OK2 ? 2 : 1);
+  static constexpr int OCC_BEST = lds_occupancy(PIPE_BYTES, (BM / EP_MAX) * CROW);
+  static constexpr int EP = lds_occupancy(PIPE_BYTES, BM * CROW) >= OCC_BEST ? 1
+                          : (EP_OK2 && lds_occupancy(PIPE_BYTES, (BM / 2) * CROW) >= OCC_BEST) ? 2 : EP_MAX;
+  static constexpr int EPI_BYTES = (BM / EP) * CROW;  // = convk::Epilogue<BM, BN, NT, *, EP>::BYTES
   static constexpr int LDS = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
   static_assert(XI >= 1 && WI >= 1, "each wave needs >=1 DMA instruction per operand");
   static_assert(BM % (R::RP * NW) == 0 && BN % (R::RP * NW) == 0, "tile rows must split evenly across waves");
@@ -64,7 +77,15 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
 
   const int M = a.N * a.Ho * a.Wo;
   const int ntc = (a.Cout + BN - 1) / BN;
-  const int Lb = xcd_remap(blockIdx.x, gridDim.x);
+  // split-K: the grid is ksplit slices of the tile grid; slice `split` runs K
+  // tiles [kbeg, kbeg + nk) and writes its own fp32 partial output
+  const int ksplit = a.ksplit > 1 ? a.ksplit : 1;
+  int Lb = xcd_remap(blockIdx.x, gridDim.x), split = 0;
+  if (ksplit > 1) {  // wave-uniform; the common path skips the division
+    const int ntiles = gridDim.x / ksplit;
+    split = Lb / ntiles;
+    Lb -= split * ntiles;
+  }
   const int tc = Lb % ntc, tm = Lb / ntc;
   const int m0 = tm * BM, c0 = tc * BN;
 
@@ -121,14 +142,20 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
     }
   };
   advance(0);
+  int nk = a.Kpad / T::BK, kbeg = 0;
+  if (ksplit > 1) {
+    const int nk_slice = (nk + ksplit - 1) / ksplit;
+    kbeg = split * nk_slice;
+    nk = max(0, min(nk_slice, nk - kbeg));
+    if (kbeg > 0) advance(kbeg * T::BK);
+  }
 
   // buffer descriptor over the activations (range check -> zero fill)
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, 0x7ffffff0, 0x00020000);
   const unsigned OOB = 0x80000000u;
-  const char* wbase = (const char*)a.w + ((long)(c0 + wid * T::WI * RW::RP + lrow) * a.Kpad + lchunk * 8) * 2;
+  const char* wbase =
+      (const char*)a.w + ((long)(c0 + wid * T::WI * RW::RP + lrow) * a.Kpad + (long)kbeg * T::BK + lchunk * 8) * 2;
   const long wstep_row = (long)RW::RP * a.Kpad * 2;  // next RP-row piece
-
-  const int nk = a.Kpad / T::BK;
 
   auto issue = [&](int kt, int stage) {
     char* sx = smem + stage * T::STAGE_BYTES;
@@ -164,8 +191,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
     if (s < nk) issue(s, s);
 
   // epilogue operands (bias, residual) prefetched behind the first DMA tiles
-  convk::Epilogue<BM, BN, T::NT, RES> epi;
-  epi.prefetch(a, m0, c0, M, tid);
+  convk::Epilogue<BM, BN, T::NT, RES, T::EP> epi;
+  epi.prefetch(a, m0, c0, M, tid, split);
 
   for (int kt = 0; kt < nk; ++kt) {
     // retire tile kt (leave the younger STAGES-2 tiles in flight), then barrier
@@ -210,7 +237,7 @@ template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
 static int launch(const DmlConvArgs* a, hipStream_t s) {
   using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
   const long M = (long)a->N * a->Ho * a->Wo;
-  const long tiles = ((M + BM - 1) / BM) * ((a->Cout + BN - 1) / BN);
+  const long tiles = ((M + BM - 1) / BM) * ((a->Cout + BN - 1) / BN) * (a->ksplit > 1 ? a->ksplit : 1);
   if (a->res)
     hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK>), dim3((unsigned)tiles), dim3(T::NT), T::LDS,
                        s, *a);
@@ -257,6 +284,11 @@ extern "C" int dml_conv_v2_init(void) {
   rc |= set_attr<64, 128, 1, 4, 3, 32>();
   rc |= set_attr<128, 64, 2, 2, 3, 32>();
   rc |= set_attr<128, 128, 2, 2, 3, 32>();
+  rc |= set_attr<128, 128, 2, 2, 4, 32>();
+  rc |= set_attr<256, 128, 4, 2, 3, 32>();
+  rc |= set_attr<128, 256, 2, 4, 3, 32>();
+  rc |= set_attr<64, 128, 1, 4, 3>();
+  rc |= set_attr<64, 128, 1, 4, 4, 32>();
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   return rc ? -1 : 0;
 }
@@ -285,6 +317,12 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
     case 26: return launch<64, 128, 1, 4, 3, 32>(a, s);
     case 27: return launch<128, 64, 2, 2, 3, 32>(a, s);
     case 28: return launch<128, 128, 2, 2, 3, 32>(a, s);
+    // deeper rings (the epilogue no longer sets the LDS size: Cfg::EP passes)
+    case 29: return launch<128, 128, 2, 2, 4, 32>(a, s);  // 64 KiB: 2 blocks/CU
+    case 30: return launch<256, 128, 4, 2, 3, 32>(a, s);  // 8 waves, 72 KiB
+    case 31: return launch<128, 256, 2, 4, 3, 32>(a, s);  // 8 waves, 72 KiB
+    case 32: return launch<64, 128, 1, 4, 3>(a, s);       // 72 KiB: 2 blocks/CU
+    case 33: return launch<64, 128, 1, 4, 4, 32>(a, s);   // 48 KiB: 3 blocks/CU
     default: dml_set_error("dml_conv_v2: bad cfg"); return -1;
   }
 }

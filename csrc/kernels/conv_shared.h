@@ -52,31 +52,39 @@ struct Rows {
   }
 };
 
-// Epilogue of a BM(pixels) x BN(channels) tile computed by NT threads.
-template <int BM, int BN, int NT, bool RES>
+// Epilogue of a BM(pixels) x BN(channels) tile computed by NT threads, staged
+// through LDS in P passes of BM/P pixels each (P > 1 keeps the fp32 staging
+// buffer within the operand ring's LDS, so the epilogue does not set the
+// kernel's LDS size and occupancy).
+template <int BM, int BN, int NT, bool RES, int P = 1>
 struct Epilogue {
   static constexpr int CG = BN / 8;            // 8-channel groups per pixel
   static constexpr int EIT = BM * CG / NT;     // pixels handled per thread
   static constexpr int CROW = BN * 4 + 16;     // fp32 staging row stride (+16 B pad)
-  static constexpr int BYTES = BM * CROW;
+  static constexpr int PB = BM / P;            // pixels per pass
+  static constexpr int BYTES = PB * CROW;
   static_assert(NT % CG == 0 && (BM * CG) % NT == 0, "epilogue mapping");
+  static_assert(PB % 16 == 0 && EIT % P == 0, "epilogue passes");
 
   int cg_t, ch_t, m0, M;
+  long yoff;                                    // split-K slice offset (elements, fp32 output)
   bool ch_ok;
   float4 bias0, bias1;
   uint4 rpre[RES ? EIT : 1];
 
   // Issue the bias / residual loads early: on memory-bound layers the residual
   // read then hides under the operand DMA instead of following the last MFMA.
-  __device__ __forceinline__ void prefetch(const DmlConvArgs& a, int m0_, int c0, int M_, int tid) {
+  // Split-K slice `split` > 0 adds no bias (slice 0 does).
+  __device__ __forceinline__ void prefetch(const DmlConvArgs& a, int m0_, int c0, int M_, int tid, int split = 0) {
     m0 = m0_;
     M = M_;
     cg_t = tid % CG;
     ch_t = c0 + cg_t * 8;
     ch_ok = ch_t < a.Cout;
+    yoff = (long)split * a.split_ld;
     bias0 = make_float4(0.f, 0.f, 0.f, 0.f);
     bias1 = bias0;
-    if (ch_ok) {
+    if (ch_ok && split == 0) {
       bias0 = *(const float4*)(a.bias + ch_t);
       bias1 = *(const float4*)(a.bias + ch_t + 4);
     }
@@ -96,16 +104,6 @@ struct Epilogue {
   __device__ __forceinline__ void store(const DmlConvArgs& a, char* smem, f32x4 (&acc)[FI][FJ], int wp, int wc,
                                         int lane, int tid) {
     const int frow = lane & 15, fq = lane >> 4;
-    __syncthreads();  // every wave is done reading the operand tiles
-#pragma unroll
-    for (int i = 0; i < FI; ++i)
-#pragma unroll
-      for (int j = 0; j < FJ; ++j) {
-        const int px = wp * WTP + j * 16 + frow;
-        const int ch = wc * WTC + i * 16 + fq * 4;
-        *(f32x4*)(smem + px * CROW + ch * 4) = acc[i][j];
-      }
-    __syncthreads();
     // destination of this thread's channel group: the plain output, or the
     // segment (fused sibling conv) that owns channel ch_t
     void* ybase = a.y;
@@ -121,32 +119,48 @@ struct Epilogue {
       choff = ch_t - a.seg_c0[sgi];
     }
 #pragma unroll
-    for (int it = 0; it < EIT; ++it) {
-      const int px = (tid + it * NT) / CG;
-      const int m = m0 + px;
-      if (m >= M || !ch_ok) continue;
-      const float4 v0 = *(const float4*)(smem + px * CROW + cg_t * 32);
-      const float4 v1 = *(const float4*)(smem + px * CROW + cg_t * 32 + 16);
-      float f[8] = {v0.x + bias0.x, v0.y + bias0.y, v0.z + bias0.z, v0.w + bias0.w,
-                    v1.x + bias1.x, v1.y + bias1.y, v1.z + bias1.z, v1.w + bias1.w};
-      if constexpr (RES) {
-        const uint4 r = rpre[it];
-        f[0] += bf2f(r.x & 0xffff); f[1] += bf2f(r.x >> 16);
-        f[2] += bf2f(r.y & 0xffff); f[3] += bf2f(r.y >> 16);
-        f[4] += bf2f(r.z & 0xffff); f[5] += bf2f(r.z >> 16);
-        f[6] += bf2f(r.w & 0xffff); f[7] += bf2f(r.w >> 16);
-      }
-      if (relu) {
+    for (int pass = 0; pass < P; ++pass) {
+      __syncthreads();  // operand tiles (pass 0) / the previous pass's staging rows are free
 #pragma unroll
-        for (int q = 0; q < 8; ++q) f[q] = fmaxf(f[q], 0.f);
+      for (int j = 0; j < FJ; ++j) {
+        if (P > 1 && (wp * WTP + j * 16) / PB != pass) continue;  // wave-uniform
+        const int px = wp * WTP + j * 16 + frow - pass * PB;
+#pragma unroll
+        for (int i = 0; i < FI; ++i) {
+          const int ch = wc * WTC + i * 16 + fq * 4;
+          *(f32x4*)(smem + px * CROW + ch * 4) = acc[i][j];
+        }
       }
-      if (a.out_f32) {
-        float* yp = (float*)ybase + (long)m * ldy + choff;
-        *(float4*)yp = make_float4(f[0], f[1], f[2], f[3]);
-        *(float4*)(yp + 4) = make_float4(f[4], f[5], f[6], f[7]);
-      } else {
-        *(uint4*)((unsigned short*)ybase + (long)m * ldy + choff) =
-            make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+      __syncthreads();
+#pragma unroll
+      for (int it = pass * (EIT / P); it < (pass + 1) * (EIT / P); ++it) {
+        const int px = (tid + it * NT) / CG;
+        const int m = m0 + px;
+        if (m >= M || !ch_ok) continue;
+        const int lp = px - pass * PB;
+        const float4 v0 = *(const float4*)(smem + lp * CROW + cg_t * 32);
+        const float4 v1 = *(const float4*)(smem + lp * CROW + cg_t * 32 + 16);
+        float f[8] = {v0.x + bias0.x, v0.y + bias0.y, v0.z + bias0.z, v0.w + bias0.w,
+                      v1.x + bias1.x, v1.y + bias1.y, v1.z + bias1.z, v1.w + bias1.w};
+        if constexpr (RES) {
+          const uint4 r = rpre[it];
+          f[0] += bf2f(r.x & 0xffff); f[1] += bf2f(r.x >> 16);
+          f[2] += bf2f(r.y & 0xffff); f[3] += bf2f(r.y >> 16);
+          f[4] += bf2f(r.z & 0xffff); f[5] += bf2f(r.z >> 16);
+          f[6] += bf2f(r.w & 0xffff); f[7] += bf2f(r.w >> 16);
+        }
+        if (relu) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] = fmaxf(f[q], 0.f);
+        }
+        if (a.out_f32) {
+          float* yp = (float*)ybase + yoff + (long)m * ldy + choff;
+          *(float4*)yp = make_float4(f[0], f[1], f[2], f[3]);
+          *(float4*)(yp + 4) = make_float4(f[4], f[5], f[6], f[7]);
+        } else {
+          *(uint4*)((unsigned short*)ybase + (long)m * ldy + choff) =
+              make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+        }
       }
     }
   }

@@ -82,84 +82,141 @@ __global__ __launch_bounds__(256) void pool3x3_kernel(DmlPoolArgs a) {
   }
 }
 
+// Global average pool. One workgroup per (image, 256-channel slab): 8 pixel
+// lanes x 32 channel groups, each thread sums every 8th pixel of its 16-B
+// channel group, then the 8 partial sums meet in LDS. N*ceil(C/256) workgroups
+// (ResNet50 b128: 1024) and 8 independent 16-B loads in flight per lane-column,
+// instead of one thread walking all HW pixels of a channel group.
 __global__ __launch_bounds__(256) void gap_kernel(const bf16* x, bf16* y, int N, int HW, int C, int ldx) {
-  const int C8 = C / 8;
-  const long total = (long)N * C8;
-  const float inv = 1.f / (float)HW;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int cg = (int)(t % C8);
-    const int n = (int)(t / C8);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __shared__ float part[8][32][9];  // +1 pad: the 8 partial rows of a group land in different banks
+  const int n = blockIdx.x / ((C + 255) / 256);
+  const int slab = blockIdx.x - n * ((C + 255) / 256);
+  const int cgl = threadIdx.x & 31, py = threadIdx.x >> 5;
+  const int cg = slab * 32 + cgl;
+  const bool ok = cg * 8 < C;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (ok) {
     const bf16* base = x + (long)n * HW * ldx + cg * 8;
-    for (int p = 0; p < HW; ++p) {
+    for (int p = py; p < HW; p += 8) {
       float f[8];
       unpack8(*(const uint4*)(base + (long)p * ldx), f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += f[j];
     }
+  }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] *= inv;
+  for (int j = 0; j < 8; ++j) part[py][cgl][j] = acc[j];
+  __syncthreads();
+  if (py == 0 && ok) {
+    const float inv = 1.f / (float)HW;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t += part[q][cgl][j];
+      acc[j] = t * inv;
+    }
     *(uint4*)(y + (long)n * C + cg * 8) = pack8(acc);
   }
 }
 
-// One wave (64 lanes) per row. Lane l owns classes l, l+64, ... (coalesced).
-template <int PER_LANE>
-__global__ __launch_bounds__(256) void softmax_top5_kernel(const float* logits, int B, int classes, int ld,
-                                                           float* probs, int* top_idx, float* top_p) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+// One 256-thread workgroup per row (4 waves): thread t owns classes t, t+256, ...
+// With nsplit > 1 the logits arrive as split-K partial slices (the classifier
+// GEMM's K range cut over workgroups): they are summed here, in slice order
+// (deterministic), and the summed row is written back to slice 0. Max / sum /
+// 5 rounds of argmax (ties -> lower class id) reduce per wave with shuffles,
+// then across the 4 waves through LDS.
+__device__ __forceinline__ void argmax_merge(float& v, int& i, float ov, int oi) {
+  if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+}
+
+template <int PER_T>
+__global__ __launch_bounds__(256) void softmax_top5_kernel(float* logits, int B, int classes, int ld, int nsplit,
+                                                           int split_ld, float* probs, int* top_idx, float* top_p) {
+  __shared__ float red_v[4];
+  __shared__ int red_i[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int row = blockIdx.x;
   if (row >= B) return;
-  const float* lr = logits + (long)row * ld;
-  float v[PER_LANE];
+  float* lr = logits + (long)row * ld;
+  float v[PER_T];
+#pragma unroll
+  for (int i = 0; i < PER_T; ++i) {
+    const int c = tid + i * 256;
+    v[i] = c < classes ? lr[c] : -3.0e38f;
+  }
+  if (nsplit > 1) {
+#pragma unroll 4
+    for (int sp = 1; sp < nsplit; ++sp) {
+      const float* ls = lr + (long)sp * split_ld;
+#pragma unroll
+      for (int i = 0; i < PER_T; ++i) {
+        const int c = tid + i * 256;
+        if (c < classes) v[i] += ls[c];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int c = tid + i * 256;
+      if (c < classes) lr[c] = v[i];
+    }
+  }
+  // row max
   float mx = -3.0e38f;
 #pragma unroll
-  for (int i = 0; i < PER_LANE; ++i) {
-    const int c = lane + i * 64;
-    v[i] = c < classes ? lr[c] : -3.0e38f;
-    mx = fmaxf(mx, v[i]);
-  }
+  for (int i = 0; i < PER_T; ++i) mx = fmaxf(mx, v[i]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) red_v[w] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red_v[0], red_v[1]), fmaxf(red_v[2], red_v[3]));
+  __syncthreads();
+  // row sum of exp
   float sum = 0.f;
 #pragma unroll
-  for (int i = 0; i < PER_LANE; ++i) {
-    const int c = lane + i * 64;
-    const float e = c < classes ? __expf(v[i] - mx) : 0.f;
-    sum += e;
+  for (int i = 0; i < PER_T; ++i) {
+    const int c = tid + i * 256;
+    if (c < classes) sum += __expf(v[i] - mx);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  if (lane == 0) red_v[w] = sum;
+  __syncthreads();
+  sum = (red_v[0] + red_v[1]) + (red_v[2] + red_v[3]);
+  __syncthreads();
   const float inv = 1.f / sum;
   if (probs) {
 #pragma unroll
-    for (int i = 0; i < PER_LANE; ++i) {
-      const int c = lane + i * 64;
+    for (int i = 0; i < PER_T; ++i) {
+      const int c = tid + i * 256;
       if (c < classes) probs[(long)row * classes + c] = __expf(v[i] - mx) * inv;
     }
   }
-  // top-5: 5 rounds of (lane-local argmax -> wave argmax, ties to the lower class id)
+  // top-5: 5 rounds of (thread-local argmax -> wave -> workgroup)
   unsigned taken = 0;
   for (int k = 0; k < 5; ++k) {
     float bv = -3.0e38f;
     int bi = 0x7fffffff, bslot = -1;
 #pragma unroll
-    for (int i = 0; i < PER_LANE; ++i) {
-      const int c = lane + i * 64;
+    for (int i = 0; i < PER_T; ++i) {
+      const int c = tid + i * 256;
       if (c < classes && !(taken >> i & 1u) && v[i] > bv) { bv = v[i]; bi = c; bslot = i; }
     }
     float wv = bv;
     int wi = bi;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(wv, o);
-      const int oi = __shfl_xor(wi, o);
-      if (ov > wv || (ov == wv && oi < wi)) { wv = ov; wi = oi; }
-    }
-    if (wi == bi && bslot >= 0) taken |= 1u << bslot;
-    if (lane == 0) {
-      top_idx[row * 5 + k] = wi;
-      top_p[row * 5 + k] = __expf(wv - mx) * inv;
+    for (int o = 32; o > 0; o >>= 1) argmax_merge(wv, wi, __shfl_xor(wv, o), __shfl_xor(wi, o));
+    if (lane == 0) { red_v[w] = wv; red_i[w] = wi; }
+    __syncthreads();
+    float gv = red_v[0];
+    int gi = red_i[0];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) argmax_merge(gv, gi, red_v[q], red_i[q]);
+    __syncthreads();
+    if (gi == bi && bslot >= 0) taken |= 1u << bslot;
+    if (tid == 0) {
+      top_idx[row * 5 + k] = gi;
+      top_p[row * 5 + k] = __expf(gv - mx) * inv;
     }
   }
 }
@@ -212,26 +269,33 @@ extern "C" int dml_pool(const DmlPoolArgs* a, hipStream_t s) {
 
 extern "C" int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s) {
   if (C % 8 || ldx % 8) { dml_set_error("dml_global_avgpool: channels must be %8"); return -1; }
-  const long work = (long)N * (C / 8);
-  hipLaunchKernelGGL(dml::gap_kernel, dim3(dml::grid_for(work, 256)), dim3(256), 0, s, (const bf16*)x,
+  hipLaunchKernelGGL(dml::gap_kernel, dim3((unsigned)(N * ((C + 255) / 256))), dim3(256), 0, s, (const bf16*)x,
                      (bf16*)y, N, HW, C, ldx);
   DML_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int dml_softmax_top5(const float* logits, int B, int classes, int ld, float* probs, int* top_idx,
-                                float* top_p, hipStream_t s) {
-  const dim3 grid((B + 3) / 4), block(256);
-  if (classes <= 16 * 64) {
-    hipLaunchKernelGGL(dml::softmax_top5_kernel<16>, grid, block, 0, s, logits, B, classes, ld, probs, top_idx, top_p);
-  } else if (classes <= 32 * 64) {
-    hipLaunchKernelGGL(dml::softmax_top5_kernel<32>, grid, block, 0, s, logits, B, classes, ld, probs, top_idx, top_p);
+extern "C" int dml_softmax_top5_split(float* logits, int B, int classes, int ld, int nsplit, int split_ld,
+                                      float* probs, int* top_idx, float* top_p, hipStream_t s) {
+  const dim3 grid(B), block(256);
+  if (nsplit < 1) nsplit = 1;
+  if (classes <= 4 * 256) {
+    hipLaunchKernelGGL(dml::softmax_top5_kernel<4>, grid, block, 0, s, logits, B, classes, ld, nsplit, split_ld,
+                       probs, top_idx, top_p);
+  } else if (classes <= 8 * 256) {
+    hipLaunchKernelGGL(dml::softmax_top5_kernel<8>, grid, block, 0, s, logits, B, classes, ld, nsplit, split_ld,
+                       probs, top_idx, top_p);
   } else {
     dml_set_error("dml_softmax_top5: classes > 2048");
     return -1;
   }
   DML_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int dml_softmax_top5(const float* logits, int B, int classes, int ld, float* probs, int* top_idx,
+                                float* top_p, hipStream_t s) {
+  return dml_softmax_top5_split((float*)logits, B, classes, ld, 1, 0, probs, top_idx, top_p, s);
 }
 
 extern "C" int dml_preprocess(const DmlPreprocArgs* a, hipStream_t s) {

@@ -44,7 +44,7 @@ extern "C" int dml_device_info(int* cus, int* arch_major, int* arch_minor) {
 namespace {
 enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC };
 struct GapArgs { const void* x; void* y; int N, HW, C, ldx; };
-struct SmArgs { const float* logits; int B, classes, ld; float* probs; int* idx; float* p; };
+struct SmArgs { float* logits; int B, classes, ld, nsplit, split_ld; float* probs; int* idx; float* p; };
 struct Op {
   OpKind kind;
   int cfg;
@@ -78,7 +78,9 @@ int run_op(const Op& o, hipStream_t s) {
     case OP_CONV: return dml_conv(&o.conv, o.cfg, s);
     case OP_POOL: return dml_pool(&o.pool, s);
     case OP_GAP: return dml_global_avgpool(o.gap.x, o.gap.y, o.gap.N, o.gap.HW, o.gap.C, o.gap.ldx, s);
-    case OP_SMTOP5: return dml_softmax_top5(o.sm.logits, o.sm.B, o.sm.classes, o.sm.ld, o.sm.probs, o.sm.idx, o.sm.p, s);
+    case OP_SMTOP5:
+      return dml_softmax_top5_split(o.sm.logits, o.sm.B, o.sm.classes, o.sm.ld, o.sm.nsplit, o.sm.split_ld,
+                                    o.sm.probs, o.sm.idx, o.sm.p, s);
     case OP_PREPROC: return dml_preprocess(&o.pre, s);
   }
   return -1;
@@ -111,13 +113,17 @@ extern "C" int dml_plan_add_gap(void* p, const void* x, void* y, int N, int HW, 
   ((Plan*)p)->ops.push_back(o);
   return 0;
 }
-extern "C" int dml_plan_add_softmax_top5(void* p, const float* logits, int B, int classes, int ld, float* probs,
-                                         int* idx, float* pr) {
+extern "C" int dml_plan_add_softmax_top5_split(void* p, float* logits, int B, int classes, int ld, int nsplit,
+                                               int split_ld, float* probs, int* idx, float* pr) {
   Op o{};
   o.kind = OP_SMTOP5;
-  o.sm = SmArgs{logits, B, classes, ld, probs, idx, pr};
+  o.sm = SmArgs{logits, B, classes, ld, nsplit, split_ld, probs, idx, pr};
   ((Plan*)p)->ops.push_back(o);
   return 0;
+}
+extern "C" int dml_plan_add_softmax_top5(void* p, const float* logits, int B, int classes, int ld, float* probs,
+                                         int* idx, float* pr) {
+  return dml_plan_add_softmax_top5_split(p, (float*)logits, B, classes, ld, 1, 0, probs, idx, pr);
 }
 extern "C" int dml_plan_add_preprocess(void* p, const DmlPreprocArgs* a) {
   Op o{};

@@ -28,6 +28,7 @@ class ConvArgs(C.Structure):
         ("dh", C.c_int), ("dw", C.c_int),
         ("nseg", C.c_int), ("seg_c0", C.c_int * 4), ("seg_ldy", C.c_int * 4), ("seg_relu", C.c_int * 4),
         ("seg_y", C.c_void_p * 4),
+        ("ksplit", C.c_int), ("split_ld", C.c_int),
     ]
 
 
@@ -58,6 +59,8 @@ _SIGS = {
     "dml_global_avgpool": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "dml_softmax_top5": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                    C.c_void_p]),
+    "dml_softmax_top5_split": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_void_p]),
     "dml_preprocess": (C.c_int, [C.POINTER(PreprocArgs), C.c_void_p]),
     "dml_plan_create": (C.c_void_p, []),
     "dml_plan_destroy": (None, [C.c_void_p]),
@@ -66,6 +69,8 @@ _SIGS = {
     "dml_plan_add_gap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
     "dml_plan_add_softmax_top5": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                             C.c_void_p, C.c_void_p]),
+    "dml_plan_add_softmax_top5_split": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                  C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "dml_plan_add_preprocess": (C.c_int, [C.c_void_p, C.POINTER(PreprocArgs)]),
     "dml_plan_size": (C.c_int, [C.c_void_p]),
     "dml_plan_run": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -119,7 +124,11 @@ def lib():
             raise NativeError(f"{path} missing; run python -m distributed_machine_learning_amd._build")
         L = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
         for name, (res, args) in _SIGS.items():
-            f = getattr(L, name)
+            f = getattr(L, name, None)
+            if f is None and os.environ.get("DML_LIB"):  # an older variant library: bind what it has
+                continue
+            if f is None:
+                raise NativeError(f"{path} lacks {name}; rebuild")
             f.restype = res
             f.argtypes = args
         _lib = L

@@ -15,6 +15,7 @@ Lowering (SURVEY §7.1 "C++/HIP graph executor"):
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -149,8 +150,21 @@ class Engine:
                 and self.device.type == "cuda")
 
     # ------------------------------------------------------------ buffers ----
+    def _fc_split(self) -> int:
+        """Split-K slices of the classifier GEMM: M = batch rows and N = 1000
+        classes give only a few dozen output tiles on 256 CUs, so the K = 2048
+        loop is cut into slices (fp32 partials, summed by the softmax kernel)."""
+        env = os.environ.get("DML_FC_KSPLIT")
+        dense = [n for n in self.g.nodes if isinstance(n, Dense)]
+        if not dense or self.device.type != "cuda":
+            return 1
+        nk = self.wdev[dense[0].name][3] // 64
+        ks = int(env) if env else (8 if nk >= 16 else max(1, nk // 2))
+        return max(1, min(ks, nk))
+
     def _alloc_buffers(self) -> None:
         g, B = self.g, self.batch
+        self.fc_ksplit = self._fc_split()
         nodes = g.nodes
         first_def, last_use = {g.input: -1}, {}
         for i, n in enumerate(nodes):
@@ -184,7 +198,10 @@ class Engine:
                 if name == g.input and self.stem is not None:
                     numel = B * t.h * (t.w + self.stem_lpad) * 8
                 if name in (g.logits,):
-                    self.buf[name] = torch.empty((B, t.c), device=self.device, dtype=torch.float32)
+                    # [ksplit][B][classes]: split-K partials; slice 0 holds the summed logits
+                    self.logit_parts = torch.empty((self.fc_ksplit, B, t.c), device=self.device,
+                                                   dtype=torch.float32)
+                    self.buf[name] = self.logit_parts[0]
                     continue
                 lst = free.get(numel)
                 buf = lst.pop() if lst else torch.empty(numel, device=self.device, dtype=torch.bfloat16)
@@ -260,8 +277,9 @@ class Engine:
                 N.check(L.dml_plan_add_gap(plan, self.buf[n.inp].data_ptr(), self.buf[n.out].data_ptr(),
                                            B, h * w, c, self.cbuf[n.inp]), "plan gap")
             self.op_names.append(n.name)
-        N.check(L.dml_plan_add_softmax_top5(plan, self.buf[g.logits].data_ptr(), B, g.classes, g.classes,
-                                            self.probs.data_ptr(), self.top_idx.data_ptr(), self.top_p.data_ptr()),
+        N.check(L.dml_plan_add_softmax_top5_split(plan, self.buf[g.logits].data_ptr(), B, g.classes, g.classes,
+                                                  self.fc_ksplit, B * g.classes, self.probs.data_ptr(),
+                                                  self.top_idx.data_ptr(), self.top_p.data_ptr()),
                 "plan softmax_top5")
         self.op_names.append("softmax_top5")
         return plan
@@ -273,9 +291,12 @@ class Engine:
             wk, kpad = self.whalo[n.name]
         if isinstance(n, Dense):
             x = self.buf[n.inp]
-            return N.ConvArgs(x.data_ptr(), wk.data_ptr(), bias.data_ptr(), None, self.buf[n.out].data_ptr(),
-                              B, 1, 1, cin_eff, self.cbuf[n.inp], 1, 1, 1, 1, 0, 0, 1, 1, n.cout, K, kpad,
-                              n.cout, 0, 0, 1, 1, 1)
+            a = N.ConvArgs(x.data_ptr(), wk.data_ptr(), bias.data_ptr(), None, self.buf[n.out].data_ptr(),
+                           B, 1, 1, cin_eff, self.cbuf[n.inp], 1, 1, 1, 1, 0, 0, 1, 1, n.cout, K, kpad,
+                           n.cout, 0, 0, 1, 1, 1)
+            if n.out == g.logits and self.fc_ksplit > 1:
+                a.ksplit, a.split_ld = self.fc_ksplit, B * n.cout
+            return a
         if isinstance(n, FusedConv):
             m0 = n.members[0]
             h, w, _ = g.shape(n.inp)
@@ -364,11 +385,16 @@ class SplitEngine:
     the serving pipeline: srcs, result, batch, src_slots, device, run."""
 
     def __init__(self, graph: Graph, weights: Weights, batch: int, device: str = "cuda", splits: int = 2,
-                 src_slots: int = 1, src_hw: Optional[Tuple[int, int]] = None, **kw):
+                 src_slots: int = 1, src_hw: Optional[Tuple[int, int]] = None, streams: int = 0, **kw):
+        """``streams``: concurrent streams (default = splits); sub-batch i runs on
+        stream i % streams, so splits=4, streams=2 runs two half-size sub-batches
+        back to back on each of two streams (smaller per-layer working sets that
+        stay in the 256 MiB Infinity Cache between producer and consumer)."""
         if batch % splits:
             raise ValueError(f"batch {batch} not divisible by splits {splits}")
         sub = batch // splits
         self.batch, self.splits, self.src_slots = batch, splits, src_slots
+        self.nstreams = max(1, min(streams or splits, splits))
         self.device = torch.device(device)
         hw = src_hw or graph.input_hw
         self.srcs = [torch.zeros((batch, hw[0], hw[1], 3), device=self.device, dtype=torch.uint8)
@@ -385,12 +411,12 @@ class SplitEngine:
                                        src_tensors=[t[rows] for t in self.srcs], result_view=self.result[:, rows],
                                        **kw))
         self.g = self.engines[0].g
-        # sub-batch 0 runs on the caller's stream: only splits-1 extra streams.
+        # stream 0 is the caller's stream: only nstreams-1 extra streams.
         # Measured in the serving pipeline (copy / compute / dispatch / RCCL
         # streams already live): 2 extra streams 49.1k img/s, 1 extra 58.3k.
-        self.streams = [torch.cuda.Stream(self.device) for _ in range(splits - 1)]
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(self.nstreams - 1)]
         self._fork = torch.cuda.Event()
-        self._join = [torch.cuda.Event() for _ in range(splits - 1)]
+        self._join = [torch.cuda.Event() for _ in range(self.nstreams - 1)]
 
     @property
     def op_cfg(self) -> Dict[str, int]:
@@ -399,12 +425,16 @@ class SplitEngine:
     def run(self, stream=None, use_graph: bool = False, slot: int = 0) -> None:
         main = stream if stream is not None else torch.cuda.current_stream(self.device)
         self._fork.record(main)
-        for e, s, ev in zip(self.engines[1:], self.streams, self._join):
+        lanes = [main] + self.streams
+        for s in self.streams:
             s.wait_event(self._fork)
-            e.run(s, use_graph=use_graph, slot=slot)
+        for i in range(1, self.splits):  # extra streams' sub-batches first, then the caller's
+            if i % self.nstreams:
+                self.engines[i].run(lanes[i % self.nstreams], use_graph=use_graph, slot=slot)
+        for i in range(0, self.splits, self.nstreams):
+            self.engines[i].run(main, use_graph=use_graph, slot=slot)
+        for s, ev in zip(self.streams, self._join):
             ev.record(s)
-        self.engines[0].run(main, use_graph=use_graph, slot=slot)
-        for ev in self._join:
             main.wait_event(ev)
 
     def infer(self, images_u8: torch.Tensor, stream=None):

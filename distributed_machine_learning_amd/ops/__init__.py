@@ -69,14 +69,21 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
                 stride=(1, 1), pad=(0, 0), relu: bool = False, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, out_coff: int = 0, in_coff: int = 0, cin: Optional[int] = None,
                 out_f32: bool = False, cfg: int = -1, K: Optional[int] = None, dilation=(1, 1),
-                out_hw: Optional[Tuple[int, int]] = None) -> torch.Tensor:
-    """x: NHWC bf16 [N,H,W,Cbuf] (Cbuf % 8 == 0). Returns/updates NHWC output."""
+                out_hw: Optional[Tuple[int, int]] = None, ksplit: int = 1) -> torch.Tensor:
+    """x: NHWC bf16 [N,H,W,Cbuf] (Cbuf % 8 == 0). Returns/updates NHWC output.
+    ksplit > 1 (fp32 output, v2 cfg): returns the [ksplit, N, Ho, Wo, C] split-K
+    partial sums (slice 0 carries the bias); their sum is the convolution."""
     n, h, w_, cbuf = x.shape
     cin = cin if cin is not None else cbuf - in_coff
     ho = (h + 2 * pad[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
     wo = (w_ + 2 * pad[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
     if out_hw is not None:
         ho, wo = out_hw
+    parts = None
+    if ksplit > 1:
+        assert out_f32 and out is None, "split-K writes fp32 partial slices into its own buffer"
+        parts = torch.empty((ksplit, n, ho, wo, _r(cout, 8)), device=x.device, dtype=torch.float32)
+        out = parts[0]
     if out is None:
         out = torch.empty((n, ho, wo, _r(cout, 8)), device=x.device,
                           dtype=torch.float32 if out_f32 else torch.bfloat16)
@@ -91,10 +98,15 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
                    n, h, w_, cin, cbuf, kh, kw, stride[0], stride[1], pad[0], pad[1], ho, wo, cout, K, kpad,
                    out.shape[-1], residual.shape[-1] if residual is not None else 0, int(relu), int(out_f32),
                    dilation[0], dilation[1])
+    if parts is not None:
+        a.ksplit, a.split_ld = ksplit, out.numel()
     L = N.lib()
     if cfg < 0:
         cfg = L.dml_conv_pick_cfg(C.byref(a))
     N.check(L.dml_conv(C.byref(a), cfg, N.stream_ptr()), "dml_conv")
+    if parts is not None:
+        parts._keep = bias_p
+        return parts
     out._keep = bias_p  # keep alive until the kernel ran (caller syncs)
     return out
 
@@ -120,14 +132,18 @@ def global_avgpool(x: torch.Tensor) -> torch.Tensor:
 
 
 def softmax_top5(logits: torch.Tensor, want_probs: bool = True):
-    b, classes = logits.shape
-    logits = logits.contiguous().float()
-    probs = torch.empty_like(logits) if want_probs else None
-    idx = torch.empty((b, 5), device=logits.device, dtype=torch.int32)
-    p = torch.empty((b, 5), device=logits.device, dtype=torch.float32)
-    N.check(N.lib().dml_softmax_top5(logits.data_ptr(), b, classes, classes,
-                                     probs.data_ptr() if probs is not None else None, idx.data_ptr(), p.data_ptr(),
-                                     N.stream_ptr()), "softmax_top5")
+    """logits [B, classes], or [S, B, classes] split-K partial slices (summed
+    in the kernel; the sum is written back into slice 0)."""
+    parts = logits.contiguous().float()
+    if parts.dim() == 2:
+        parts = parts[None]
+    s, b, classes = parts.shape
+    probs = torch.empty((b, classes), device=parts.device, dtype=torch.float32) if want_probs else None
+    idx = torch.empty((b, 5), device=parts.device, dtype=torch.int32)
+    p = torch.empty((b, 5), device=parts.device, dtype=torch.float32)
+    N.check(N.lib().dml_softmax_top5_split(parts.data_ptr(), b, classes, classes, s, b * classes,
+                                           probs.data_ptr() if probs is not None else None, idx.data_ptr(),
+                                           p.data_ptr(), N.stream_ptr()), "softmax_top5")
     return probs, idx, p
 
 

@@ -18,7 +18,7 @@ from typing import Dict, Iterable, List, Optional, Tuple
 
 from .. import _native as N
 
-V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27)  # 23..28: BK = 32 tile rows
+V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33)  # 23..: BK = 32 rows
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))
@@ -35,6 +35,7 @@ def shape_key(a: N.ConvArgs, halo: bool = False) -> str:
     configs as candidates (so entries tuned before they existed are re-timed)."""
     return (f"n{a.N}_h{a.H}_w{a.W}_c{a.Cin}_ld{a.ldx}_k{a.kh}x{a.kw}_s{a.sh}x{a.sw}_p{a.ph}x{a.pw}"
             f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}_d{max(a.dh, 1)}x{max(a.dw, 1)}"
+            + (f"_ks{a.ksplit}" if a.ksplit > 1 else "")
             + ("_halo" if halo else "") + "_" + CAND_TAG)
 
 

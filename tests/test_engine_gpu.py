@@ -28,6 +28,10 @@ def _rel(a, b):
     return ((a - b).abs().max() / (b.abs().max() + 1e-9)).item()
 
 
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
 @pytest.mark.parametrize("name", ["ResNet50", "InceptionV3"])
 def test_every_conv_layer_isolated(name):
     g, w = build_model(name, seed=0, calibrate=True)
@@ -117,6 +121,44 @@ def test_batch_rows_independent():
         outs.append(e1.buf[g.logits].clone())
     torch.cuda.synchronize()
     assert torch.allclose(torch.cat(outs), e4.buf[g.logits], atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_split_engine_round_robin_streams(use_graph):
+    """4 sub-batches on 2 streams (two back to back per stream) == Engine runs of each quarter."""
+    from distributed_machine_learning_amd.models.engine import SplitEngine
+
+    g, w = build_model("ResNet50", seed=5, calibrate=False)
+    imgs = torch.randint(0, 256, (8, 224, 224, 3), dtype=torch.uint8, device="cuda")
+    se = SplitEngine(g, w, batch=8, splits=4, streams=2, src_slots=2)
+    assert se.nstreams == 2 and len(se.streams) == 1
+    e2 = Engine(g, w, batch=2)
+    s = torch.cuda.Stream()
+    se.srcs[0].copy_(imgs)
+    with torch.cuda.stream(s):
+        se.run(s, use_graph=use_graph, slot=0)
+    s.synchronize()
+    ref = []
+    for q in range(4):
+        e2.infer(imgs[2 * q: 2 * q + 2])
+        torch.cuda.synchronize()
+        ref.append(e2.result.clone())
+    assert torch.equal(se.result, torch.cat(ref, dim=1))
+
+
+def test_engine_classifier_split_k():
+    """The engine's classifier runs split-K (fp32 slices summed in the softmax
+    kernel); slice 0 of the logits buffer ends up holding the summed logits."""
+    g, w = build_model("ResNet50", seed=6, calibrate=False)
+    eng = Engine(g, w, batch=4)
+    assert eng.fc_ksplit > 1 and eng.logit_parts.shape[0] == eng.fc_ksplit
+    eng.infer(torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8, device="cuda"))
+    torch.cuda.synchronize()
+    pooled = eng.buf["avg_pool"].float().view(4, -1).cpu()
+    dense = [n for n in eng.g.nodes if n.out == g.logits][0]
+    ref = pooled @ _bf(torch.from_numpy(w[f"{dense.name}/kernel"])) + torch.from_numpy(w[f"{dense.name}/bias"])
+    assert _rel(eng.buf[g.logits].cpu(), ref) < 1e-2
+    assert torch.equal(eng.top_idx.cpu().long(), eng.buf[g.logits].cpu().topk(5, -1).indices)
 
 
 @pytest.mark.parametrize("use_graph", [False, True])

@@ -43,7 +43,8 @@ def _pads(kh, kw, pad):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 15, 16, 17, 18, 23, 24, 25, 26, 27, 28])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 15, 16, 17, 18, 23, 24, 25, 26, 27, 28, 29,
+                                 30, 31, 32, 33])
 def test_conv_matches_fp32(case, cfg):
     n, h, w, cin, cout, kh, kw, s, pad, relu, has_res = case
     ph, pw = (kh // 2, kw // 2) if pad else (0, 0)
@@ -121,6 +122,31 @@ def test_fc_fp32_out():
     assert _rel(y.view(5, -1)[:, :1000].cpu(), ref) < 5e-3
 
 
+@pytest.mark.parametrize("ksplit,cfg", [(2, 14), (4, 11), (8, 14), (8, 23), (16, 22), (5, 15)])
+def test_fc_split_k(ksplit, cfg):
+    """Classifier GEMM with the K loop cut over workgroup slices: the fp32
+    partial slices sum to x @ W^T + b (bias in slice 0 only), and the split
+    softmax/top-5 over the slices equals softmax/top-5 of the summed logits."""
+    torch.manual_seed(7)
+    b_ = 37
+    x = _bf(torch.randn(b_, 2048))
+    wt = _bf(torch.randn(1000, 2048) * 0.02)
+    b = torch.randn(1000) * 0.1
+    ref = x @ wt.t() + b
+    wp, K, _ = ops.pack_weight(wt[:, :, None, None])
+    parts = ops.conv2d_nhwc(x.view(b_, 1, 1, 2048).cuda().to(torch.bfloat16), wp.cuda(), b.cuda(), 1000, 1, 1,
+                            out_f32=True, cfg=cfg, ksplit=ksplit)
+    torch.cuda.synchronize()
+    assert parts.shape[0] == ksplit
+    tot = parts.sum(0).view(b_, -1)[:, :1000].cpu()
+    assert _rel(tot, ref) < 5e-3
+    probs, idx, p = ops.softmax_top5(parts.view(ksplit, b_, -1)[..., :1000].contiguous())
+    torch.cuda.synchronize()
+    refp = torch.softmax(tot, -1)
+    assert torch.allclose(probs.cpu(), refp, atol=1e-5, rtol=1e-3)
+    assert torch.equal(idx.cpu().long(), refp.topk(5, dim=-1).indices)
+
+
 @pytest.mark.parametrize("mode,k,s,pad", [("max", 3, 2, 0), ("max", 3, 2, 1), ("avg", 3, 1, 1)])
 def test_pool(mode, k, s, pad):
     torch.manual_seed(4)
@@ -134,8 +160,9 @@ def test_pool(mode, k, s, pad):
     assert _rel(y.float().cpu().permute(0, 3, 1, 2), ref) < 1e-2
 
 
-def test_global_avgpool():
-    x = _bf(torch.randn(3, 7, 7, 2048))
+@pytest.mark.parametrize("shape", [(3, 7, 7, 2048), (2, 8, 8, 2048), (5, 3, 5, 200), (1, 1, 1, 8)])
+def test_global_avgpool(shape):
+    x = _bf(torch.randn(*shape))
     y = ops.global_avgpool(x.cuda().to(torch.bfloat16))
     torch.cuda.synchronize()
     assert _rel(y.float().cpu(), x.mean(dim=(1, 2))) < 1e-2
