@@ -289,6 +289,9 @@ extern "C" int dml_conv_v2_init(void) {
   rc |= set_attr<128, 256, 2, 4, 3, 32>();
   rc |= set_attr<64, 128, 1, 4, 3>();
   rc |= set_attr<64, 128, 1, 4, 4, 32>();
+  rc |= set_attr<256, 256, 2, 4, 3, 32>();
+  rc |= set_attr<128, 32, 2, 1, 3, 32>();
+  rc |= set_attr<256, 32, 4, 1, 3, 64>();
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   return rc ? -1 : 0;
 }
@@ -323,6 +326,12 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
     case 31: return launch<128, 256, 2, 4, 3, 32>(a, s);  // 8 waves, 72 KiB
     case 32: return launch<64, 128, 1, 4, 3>(a, s);       // 72 KiB: 2 blocks/CU
     case 33: return launch<64, 128, 1, 4, 4, 32>(a, s);   // 48 KiB: 3 blocks/CU
+    // 256x256: half the L2->LDS bytes per MFMA of 128x128 (the 3x3 layers are L2-bound)
+    case 34: return launch<256, 256, 2, 4, 3, 32>(a, s);  // 8 waves, 128px x 64ch per wave, 96 KiB
+    // (256x256 BK64 and the residual form of 34 spill at 2 waves/SIMD: not tuner candidates for residual layers)
+    // Cout = 32 layers (InceptionV3 stem)
+    case 36: return launch<128, 32, 2, 1, 3, 32>(a, s);   // 2 waves, 30 KiB
+    case 37: return launch<256, 32, 4, 1, 3, 64>(a, s);   // 4 waves, 3-stage
     default: dml_set_error("dml_conv_v2: bad cfg"); return -1;
   }
 }

@@ -1,0 +1,106 @@
+// host_checks.cpp — host-side checks of the native runtime, built with
+// AddressSanitizer + UndefinedBehaviorSanitizer on the host code only
+// (-Xarch_host -fsanitize=...; GPU sanitizers are not available on this
+// pool) and run on a CPU-only machine: every path exercised here is host code
+// (plan recording / teardown, argument validation, error plumbing) that must
+// not touch the device. tests/test_native_host.py builds and runs it.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include "dml.h"
+
+extern "C" void dml_set_error(const char* msg);
+
+static int failures = 0;
+#define CHECK(cond)                                                   \
+  do {                                                                \
+    if (!(cond)) {                                                    \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s (last error: %s)\n", __FILE__, __LINE__, #cond, \
+                   dml_last_error());                                 \
+      ++failures;                                                     \
+    }                                                                 \
+  } while (0)
+
+static DmlConvArgs conv_args(int cin, int cout, int kh, int kw) {
+  DmlConvArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.x = (const void*)0x1000; a.w = (const void*)0x2000; a.bias = (const float*)0x3000; a.y = (void*)0x4000;
+  a.N = 2; a.H = 14; a.W = 14; a.Cin = cin; a.ldx = cin;
+  a.kh = kh; a.kw = kw; a.sh = 1; a.sw = 1; a.ph = kh / 2; a.pw = kw / 2;
+  a.Ho = 14; a.Wo = 14; a.Cout = cout; a.K = kh * kw * cin; a.Kpad = (a.K + 63) / 64 * 64;
+  a.ldy = cout; a.dh = 1; a.dw = 1;
+  return a;
+}
+
+int main() {
+  // ---- plan recording and teardown (no launches) ----
+  for (int rep = 0; rep < 3; ++rep) {
+    void* plan = dml_plan_create();
+    CHECK(plan != nullptr);
+    int n = 0;
+    for (int i = 0; i < 500; ++i) {
+      DmlConvArgs a = conv_args(64 + 8 * (i % 7), 64 + 64 * (i % 5), 1 + 2 * (i % 2), 1 + 2 * (i % 2));
+      const int cfg = dml_plan_add_conv(plan, &a, -1);  // heuristic pick: pure host code
+      CHECK(cfg >= 0);
+      ++n;
+      DmlPoolArgs p;
+      std::memset(&p, 0, sizeof p);
+      p.N = 2; p.H = 14; p.W = 14; p.C = 64; p.ldx = 64; p.Ho = 7; p.Wo = 7; p.ldy = 64; p.k = 3; p.stride = 2;
+      CHECK(dml_plan_add_pool(plan, &p) == 0);
+      ++n;
+    }
+    CHECK(dml_plan_add_gap(plan, (void*)0x10, (void*)0x20, 2, 49, 2048, 2048) == 0);
+    CHECK(dml_plan_add_softmax_top5_split(plan, (float*)0x30, 2, 1000, 1000, 8, 2000, nullptr, (int*)0x40,
+                                          (float*)0x50) == 0);
+    DmlPreprocArgs pr;
+    std::memset(&pr, 0, sizeof pr);
+    CHECK(dml_plan_add_preprocess(plan, &pr) == 0);
+    n += 3;
+    CHECK(dml_plan_size(plan) == n);
+    // error paths that must return before any device call
+    CHECK(dml_plan_replay(plan, nullptr) != 0);
+    CHECK(std::string(dml_last_error()).find("not captured") != std::string::npos);
+    CHECK(dml_plan_replay_part(plan, 0, nullptr) != 0);
+    CHECK(dml_plan_replay_part(plan, -1, nullptr) != 0);
+    int bad[2] = {5, 2};
+    CHECK(dml_plan_capture_parts(plan, bad, 1, nullptr) != 0);
+    int oob[2] = {0, n + 1};
+    CHECK(dml_plan_capture_parts(plan, oob, 1, nullptr) != 0);
+    dml_plan_destroy(plan);
+  }
+
+  // ---- launch-argument validation (rejected on the host) ----
+  DmlConvArgs a = conv_args(3, 64, 3, 3);  // Cin % 8 != 0 is illegal for every config
+  CHECK(dml_conv(&a, 11, nullptr) != 0);
+  CHECK(dml_conv(&a, 0, nullptr) != 0);
+  a = conv_args(64, 64, 3, 3);
+  CHECK(dml_conv(&a, 99, nullptr) != 0);        // unknown config
+  CHECK(std::string(dml_last_error()).find("bad cfg") != std::string::npos);
+  a.nseg = 5;
+  CHECK(dml_conv(&a, 11, nullptr) != 0);        // too many output segments
+  a.nseg = 2;
+  CHECK(dml_conv(&a, 0, nullptr) != 0);         // segments need a v2 config
+  a = conv_args(64, 64, 1, 1);
+  a.ksplit = 4; a.split_ld = 1 << 20;
+  CHECK(dml_conv(&a, 14, nullptr) != 0);        // split-K needs fp32 output
+  a.out_f32 = 1; a.relu = 1;
+  CHECK(dml_conv(&a, 14, nullptr) != 0);        // ... and no ReLU
+  a.relu = 0;
+  CHECK(dml_conv(&a, 40, nullptr) != 0);        // ... and a v2 (non-halo) config
+  CHECK(dml_conv(&a, 2, nullptr) != 0);         // ... not a v1 config
+  DmlPoolArgs p;
+  std::memset(&p, 0, sizeof p);
+  p.C = 12; p.ldx = 12; p.ldy = 12;
+  CHECK(dml_pool(&p, nullptr) != 0);
+  CHECK(dml_global_avgpool(nullptr, nullptr, 1, 1, 12, 12, nullptr) != 0);
+  CHECK(dml_softmax_top5_split(nullptr, 1, 4096, 4096, 1, 0, nullptr, nullptr, nullptr, nullptr) != 0);
+  dml_set_error(nullptr);
+  CHECK(std::string(dml_last_error()).empty());
+
+  if (failures) {
+    std::fprintf(stderr, "%d host check(s) failed\n", failures);
+    return 1;
+  }
+  std::printf("host checks passed\n");
+  return 0;
+}

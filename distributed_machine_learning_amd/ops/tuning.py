@@ -18,7 +18,7 @@ from typing import Dict, Iterable, List, Optional, Tuple
 
 from .. import _native as N
 
-V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33)  # 23..: BK = 32 rows
+V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33, 34, 36, 37)  # 23..: BK32
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))
@@ -58,10 +58,13 @@ def save_cache(table: Dict[str, int], path: str = CACHE_PATH) -> None:
         os.replace(tmp, path)
 
 
+NO_RES_CFGS = (34,)  # the residual-epilogue instantiation spills (256x256 tile)
+
+
 def valid_cfgs(a: N.ConvArgs) -> List[int]:
     if a.Cout % 8 or a.Cin % 8 or a.ldx % 8 or a.ldy % 8:
         return [0]
-    return list(V2_CFGS)
+    return [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)]
 
 
 def time_cfg(a: N.ConvArgs, cfg: int, iters: int = 3) -> float:

@@ -73,6 +73,7 @@ def test_gpu_span_resolves_on_device():
     t = trace.Tracer()
     s = torch.cuda.Stream()
     x = torch.randn(2048, 2048, device="cuda")
+    s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s), t.gpu_span("matmul", s, lane="compute"):
         for _ in range(4):
             x = x @ x.T / 2048
@@ -294,3 +295,37 @@ def test_launch_cluster_from_config(tmp_path):
     assert "loaded 6/6 files" in r.stdout and "submitted job 31" in r.stdout
     ops = [e["op"] for e in JobJournal(str(tmp_path / "journal.jsonl")).entries()]
     assert ops[0] == "submit" and "dispatch" in ops
+
+
+# ------------------------------------------------- asyncio debug-mode run --
+def test_cluster_job_clean_under_asyncio_debug(tmp_path, caplog):
+    """The in-process cluster (coordinator + standby + workers + client) serves
+    a job with asyncio debug mode on: no coroutine is left un-awaited and no
+    task dies with an exception nobody retrieved (the reference's fire-and-
+    forget create_task pattern, worker.py:1188, loses both silently)."""
+    import gc
+    import logging
+    import warnings
+
+    from test_serving import _cluster, _load_images, _stop
+
+    async def main():
+        asyncio.get_running_loop().slow_callback_duration = 5.0  # only correctness, not timing
+        net, blobs, nodes = await _cluster(tmp_path, n_workers=3)
+        cli = nodes["cli"]
+        await _load_images(cli, 6)
+        jid = await cli.submit_job("ResNet50", 20)
+        assert await cli.wait_job(jid, timeout=20)
+        net.kill("w1")  # a failure mid-run exercises the requeue / FD paths too
+        jid2 = await cli.submit_job("InceptionV3", 12)
+        assert await cli.wait_job(jid2, timeout=30)
+        await _stop(nodes)
+
+    with warnings.catch_warnings(record=True) as rec, caplog.at_level(logging.ERROR, logger="asyncio"):
+        warnings.simplefilter("always")
+        asyncio.run(main(), debug=True)
+        gc.collect()
+    never_awaited = [str(w.message) for w in rec if "was never awaited" in str(w.message)]
+    assert not never_awaited, never_awaited
+    bad = [r.getMessage() for r in caplog.records if "never retrieved" in r.getMessage()]
+    assert not bad, bad

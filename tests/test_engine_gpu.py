@@ -97,6 +97,7 @@ def test_graph_replay_matches_eager():
     imgs = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8, device="cuda")
     eng.src.copy_(imgs)
     s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())  # the copy ran on the default stream
     with torch.cuda.stream(s):
         eng.run(s)
         s.synchronize()
@@ -135,6 +136,7 @@ def test_split_engine_round_robin_streams(use_graph):
     e2 = Engine(g, w, batch=2)
     s = torch.cuda.Stream()
     se.srcs[0].copy_(imgs)
+    s.wait_stream(torch.cuda.current_stream())  # the copy ran on the default stream
     with torch.cuda.stream(s):
         se.run(s, use_graph=use_graph, slot=0)
     s.synchronize()
@@ -173,6 +175,7 @@ def test_split_engine_matches_engine(use_graph):
     e4 = Engine(g, w, batch=4)
     s = torch.cuda.Stream()
     se.srcs[1].copy_(imgs)
+    s.wait_stream(torch.cuda.current_stream())  # the copy ran on the default stream
     with torch.cuda.stream(s):
         se.run(s, use_graph=use_graph, slot=1)
     s.synchronize()
@@ -190,6 +193,7 @@ def test_capture_parts_matches_full_graph():
     eng = Engine(g, w, batch=2)
     eng.src.copy_(torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda"))
     s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())  # the copy ran on the default stream
     eng.run(s, use_graph=True)
     s.synchronize()
     full = eng.result.clone()

@@ -44,7 +44,7 @@ def _pads(kh, kw, pad):
 
 @pytest.mark.parametrize("case", CONV_CASES)
 @pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 15, 16, 17, 18, 23, 24, 25, 26, 27, 28, 29,
-                                 30, 31, 32, 33])
+                                 30, 31, 32, 33, 34, 36, 37])
 def test_conv_matches_fp32(case, cfg):
     n, h, w, cin, cout, kh, kw, s, pad, relu, has_res = case
     ph, pw = (kh // 2, kw // 2) if pad else (0, 0)
