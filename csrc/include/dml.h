@@ -69,7 +69,23 @@ typedef struct {
   int lpad;         // pair mode: zero columns on the left; output width = Wo + lpad
 } DmlPreprocArgs;
 
+// Fused ResNet50 stem (csrc/kernels/stem_fused.hip): uint8 image -> preprocess ->
+// conv 7x7/2 pad 3 (64 ch, folded BN) + ReLU -> max pool 3x3/2 pad 1, one kernel.
+typedef struct {
+  const void* src;    // uint8 [N][Hs][Ws][3] RGB
+  const void* w;      // bf16 [>=64][ldw]: pair-packed 7x7 kernel, K = (row r, pair tap s', 8 ch), 224 used
+  const float* bias;  // fp32 [64]
+  void* y;            // bf16 NHWC [N][Ho][Wo][ldy] (pooled)
+  int N, Hs, Ws;      // source images
+  int H, W;           // network input size (nearest resize target)
+  int mode;           // 0 = caffe, 1 = tf
+  int ldw;
+  int Hc, Wc;         // conv output size
+  int Ho, Wo, ldy;    // pool output size / channel stride
+} DmlStemArgs;
+
 // ---- single-op launches (used by tests and by the plan executor) ----
+int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s);
 int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2_init(void);
@@ -101,6 +117,7 @@ int dml_plan_add_softmax_top5(void* plan, const float* logits, int B, int classe
 int dml_plan_add_softmax_top5_split(void* plan, float* logits, int B, int classes, int ld, int nsplit,
                                     int split_ld, float* probs, int* idx, float* p);
 int dml_plan_add_preprocess(void* plan, const DmlPreprocArgs* a);
+int dml_plan_add_stem(void* plan, const DmlStemArgs* a);
 int dml_plan_size(void* plan);
 int dml_plan_run(void* plan, hipStream_t s);
 int dml_plan_run_range(void* plan, int begin, int end, hipStream_t s);

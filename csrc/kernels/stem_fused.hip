@@ -1,0 +1,221 @@
+// stem_fused.hip — the whole ResNet50 stem as ONE kernel (gfx950):
+//
+//   uint8 RGB image -> nearest resize + caffe/tf normalisation (reference
+//   models.py:59-63) -> ZeroPad 3 + Conv 7x7/2, 64 ch (BN folded) + ReLU ->
+//   ZeroPad 1 + MaxPool 3x3/2  ->  bf16 NHWC [N][56][56][64]
+//
+// Unfused, these are three launches whose intermediates round-trip HBM: the
+// pair-packed bf16 input (B*224*227*16 B), the 112x112x64 conv output (written,
+// then re-read by the pool: 2 x 205 MB at batch 128). Here each workgroup owns a
+// 7 x 8 block of POOL outputs and computes, entirely on chip:
+//
+//  1. the input patch those need (35 rows x 20 pixel pairs) straight from the
+//     uint8 source into LDS, in the pair-packed layout of the unfused stem: one
+//     16-B chunk = two horizontally adjacent pixels x (3 channels + 1 zero), so
+//     the 7x7 kernel is 7 rows x 4 pair-taps x 8 = K 224 with no K padding;
+//  2. the 15 x 17 conv outputs under the pool windows (255 pixels + 1 dummy =
+//     16 MFMA pixel fragments) with v_mfma_f32_16x16x32_bf16: k-step r IS kernel
+//     row r and the lane's K quarter fq IS pair-tap s', so a pixel fragment is
+//     one ds_read_b128 at patch[2a + r][b + fq]. Weights (64 ch x 224) live in
+//     VGPRs for the whole workgroup (loaded once from L2). Channels sit on the
+//     MFMA rows as in conv_igemm_v2.hip: a lane's accumulator is 4 consecutive
+//     channels of one pixel;
+//  3. bias + ReLU -> bf16 (the unfused conv's rounding point) into an LDS tile;
+//     conv positions outside the conv image are stored as 0, which is exact for
+//     the max pool because every window holds a valid post-ReLU value >= 0;
+//  4. the 3x3/2 max pool from LDS -> one 16-B NHWC store per 8 channels.
+//
+// The 15x17 conv window of a 7x8 pool block overlaps its neighbours by one row /
+// column (14 % recomputed MACs) — traded for never writing the conv output.
+// Reference parity: Keras ResNet50 stem (models.py:48-51).
+#include "common.h"
+#include "dml.h"
+
+namespace dml {
+namespace stem {
+
+constexpr int PH = 7, PW = 8;                    // pool outputs per workgroup
+constexpr int CR = 2 * PH + 1, CC = 2 * PW + 1;  // conv window 15 x 17
+constexpr int NPIX = CR * CC;                    // 255 (+1 dummy MFMA column)
+constexpr int IR = 2 * (CR - 1) + 7;             // 35 input rows
+constexpr int PQ = CC + 3;                       // 20 pixel pairs per input row
+constexpr int PATCH_BYTES = IR * PQ * 16;        // 11200
+constexpr int SROW = 64 * 2 + 16;                // conv tile row: 64 bf16 + 16-B pad
+constexpr int TILE_BYTES = 256 * SROW;           // 36864
+constexpr int KROWS = 7;                         // k-steps (kernel rows)
+constexpr int NT = 256;                          // 4 waves: 2 (pixels) x 2 (channels)
+
+constexpr int FILL = (IR * PQ + NT - 1) / NT;  // patch chunks per thread (3)
+
+__device__ __forceinline__ float bf_at(const uint4& v, int q) {
+  const unsigned w = q < 2 ? v.x : q < 4 ? v.y : q < 6 ? v.z : v.w;
+  return bf2f((q & 1) ? (w >> 16) : (w & 0xffff));
+}
+
+__global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[PATCH_BYTES + TILE_BYTES];
+  char* patch = smem;
+  char* tile = smem + PATCH_BYTES;
+
+  const int bpr = (a.Wo + PW - 1) / PW, bpc = (a.Ho + PH - 1) / PH;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring blocks (shared patch rows) on one L2
+  const int n = blk / (bpr * bpc);
+  const int rem = blk - n * bpr * bpc;
+  const int by = rem / bpr, bx = rem - by * bpr;
+  const int py0 = by * PH, px0 = bx * PW;
+  const int cr0 = 2 * py0 - 1, cc0 = 2 * px0 - 1;  // conv window origin (pool pad 1)
+  const int ir0 = 2 * cr0 - 3, ic0 = 2 * cc0 - 3;  // input patch origin (conv pad 3, stride 2)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+  const int wc = wid & 1, wp = wid >> 1;  // 32 channels x 128 pixels per wave
+
+  // weights: A operand rows = channels; k-step r, quarter fq = W[c][r*32 + fq*8 .. +8]
+  bf16x8 wf[KROWS][2];
+#pragma unroll
+  for (int r = 0; r < KROWS; ++r)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      wf[r][i] = *(const bf16x8*)((const bf16*)a.w + (long)(wc * 32 + i * 16 + frow) * a.ldw + r * 32 + fq * 8);
+  float4 bias[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) bias[i] = *(const float4*)(a.bias + wc * 32 + i * 16 + fq * 4);
+
+  // 1. input patch: chunk (i, q) = input pixels (ir0 + i, ic0 + 2q) and (.., ic0 + 2q + 1).
+  // Every thread issues ALL its source byte loads before converting any: the
+  // addresses are clamped into the image (no branch around a load, which would
+  // make hipcc wait vmcnt(0) per pixel) and padding is zeroed afterwards.
+  {
+    const float sy = (float)a.Hs / (float)a.H, sx = (float)a.Ws / (float)a.W;
+    const unsigned char* img = (const unsigned char*)a.src + (long)n * a.Hs * a.Ws * 3;
+    unsigned char px[FILL][2][3];
+    unsigned okm[FILL];
+#pragma unroll
+    for (int it = 0; it < FILL; ++it) {
+      const int t = min(tid + it * NT, IR * PQ - 1);
+      const int i = t / PQ, q = t - i * PQ;
+      const int ih = ir0 + i, iw = ic0 + 2 * q;
+      const int iy = min((int)(((float)min(max(ih, 0), a.H - 1) + 0.5f) * sy), a.Hs - 1);  // Pillow NEAREST
+      okm[it] = ((unsigned)ih < (unsigned)a.H) ? ((unsigned)((unsigned)iw < (unsigned)a.W) |
+                                                  ((unsigned)((unsigned)(iw + 1) < (unsigned)a.W) << 1)) : 0u;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ix = min((int)(((float)min(max(iw + h, 0), a.W - 1) + 0.5f) * sx), a.Ws - 1);
+        const unsigned char* p = img + ((long)iy * a.Ws + ix) * 3;
+        px[it][h][0] = p[0];
+        px[it][h][1] = p[1];
+        px[it][h][2] = p[2];
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < FILL; ++it) {
+      const int t = tid + it * NT;
+      if (t >= IR * PQ) continue;
+      float f[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float r = px[it][h][0], g = px[it][h][1], b = px[it][h][2];
+        const bool ok = (okm[it] >> h) & 1u;
+        float* o = f + 4 * h;
+        if (a.mode == 0) {  // caffe: RGB -> BGR minus the ImageNet mean
+          o[0] = b - 103.939f; o[1] = g - 116.779f; o[2] = r - 123.68f;
+        } else {            // tf: [-1, 1]
+          o[0] = r / 127.5f - 1.f; o[1] = g / 127.5f - 1.f; o[2] = b / 127.5f - 1.f;
+        }
+        o[0] = ok ? o[0] : 0.f;
+        o[1] = ok ? o[1] : 0.f;
+        o[2] = ok ? o[2] : 0.f;
+        o[3] = 0.f;
+      }
+      *(uint4*)(patch + t * 16) =
+          make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+    }
+  }
+  __syncthreads();
+
+  // 2. conv: B operand = pixels; fragment j of this wave = window pixels wp*128 + j*16 + frow
+  int pb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int p = min(wp * 128 + j * 16 + frow, NPIX - 1);  // pixel 255 is a dummy (never pooled)
+    const int wa = p / CC, wb = p - wa * CC;
+    pb[j] = ((2 * wa) * PQ + wb + fq) * 16;
+  }
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < KROWS; ++r) {
+#pragma unroll
+    for (int jh = 0; jh < 8; jh += 4) {  // 4 pixel fragments live at a time (keeps VGPRs <= 168: 3 waves/SIMD)
+      bf16x8 pf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pf[j] = *(const bf16x8*)(patch + pb[jh + j] + r * PQ * 16);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][jh + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[r][i], pf[j], acc[i][jh + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  // 3. bias + ReLU -> bf16 conv tile in LDS (out-of-image conv positions -> 0)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int p = wp * 128 + j * 16 + frow;
+    if (p >= NPIX) continue;
+    const int wa = p / CC, wb = p - wa * CC;
+    const bool ok = (unsigned)(cr0 + wa) < (unsigned)a.Hc && (unsigned)(cc0 + wb) < (unsigned)a.Wc;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 v = acc[i][j];
+      const float4 b = bias[i];
+      const float f0 = ok ? fmaxf(v[0] + b.x, 0.f) : 0.f, f1 = ok ? fmaxf(v[1] + b.y, 0.f) : 0.f;
+      const float f2 = ok ? fmaxf(v[2] + b.z, 0.f) : 0.f, f3 = ok ? fmaxf(v[3] + b.w, 0.f) : 0.f;
+      *(uint2*)(tile + p * SROW + (wc * 32 + i * 16 + fq * 4) * 2) = make_uint2(pack2(f0, f1), pack2(f2, f3));
+    }
+  }
+  __syncthreads();
+
+  // 4. max pool 3x3/2 over the tile: item = (pool pixel, 8-channel group)
+  for (int t = tid; t < PH * PW * 8; t += NT) {
+    const int cg = t & 7, pp = t >> 3;
+    const int ly = pp / PW, lx = pp - ly * PW;
+    const int oy = py0 + ly, ox = px0 + lx;
+    if (oy >= a.Ho || ox >= a.Wo) continue;
+    float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const uint4 v = *(const uint4*)(tile + ((2 * ly + dy) * CC + 2 * lx + dx) * SROW + cg * 16);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], bf_at(v, q));
+      }
+    *(uint4*)((unsigned short*)a.y + ((long)(n * a.Ho + oy) * a.Wo + ox) * a.ldy + cg * 8) =
+        make_uint4(pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7]));
+  }
+}
+
+}  // namespace stem
+}  // namespace dml
+
+extern "C" int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s) {
+  // the kernel hard-codes conv 7x7/2 pad 3 -> 64 channels and max pool 3x3/2 pad 1
+  if (a->ldw % 8 || a->ldw < 224 || a->ldy % 8 || a->ldy < 64 || a->N < 1 || a->H < 1 || a->W < 1 ||
+      a->Hc != (a->H - 1) / 2 + 1 || a->Wc != (a->W - 1) / 2 + 1 || a->Ho != (a->Hc - 1) / 2 + 1 ||
+      a->Wo != (a->Wc - 1) / 2 + 1 || a->Hs < 1 || a->Ws < 1) {
+    dml_set_error("dml_stem_resnet: unsupported shape");
+    return -1;
+  }
+  using namespace dml::stem;
+  const long blocks = (long)a->N * ((a->Ho + PH - 1) / PH) * ((a->Wo + PW - 1) / PW);
+  hipLaunchKernelGGL(dml::stem::stem_kernel, dim3((unsigned)blocks), dim3(NT), 0, s, *a);
+  DML_CHECK_LAUNCH();
+  return 0;
+}

@@ -42,7 +42,7 @@ extern "C" int dml_device_info(int* cus, int* arch_major, int* arch_minor) {
 
 // ----------------------------------------------------------------- plan ----
 namespace {
-enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC };
+enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM };
 struct GapArgs { const void* x; void* y; int N, HW, C, ldx; };
 struct SmArgs { float* logits; int B, classes, ld, nsplit, split_ld; float* probs; int* idx; float* p; };
 struct Op {
@@ -53,6 +53,7 @@ struct Op {
   GapArgs gap;
   SmArgs sm;
   DmlPreprocArgs pre;
+  DmlStemArgs stem;
 };
 struct Plan {
   std::vector<Op> ops;
@@ -82,6 +83,7 @@ int run_op(const Op& o, hipStream_t s) {
       return dml_softmax_top5_split(o.sm.logits, o.sm.B, o.sm.classes, o.sm.ld, o.sm.nsplit, o.sm.split_ld,
                                     o.sm.probs, o.sm.idx, o.sm.p, s);
     case OP_PREPROC: return dml_preprocess(&o.pre, s);
+    case OP_STEM: return dml_stem_resnet(&o.stem, s);
   }
   return -1;
 }
@@ -129,6 +131,13 @@ extern "C" int dml_plan_add_preprocess(void* p, const DmlPreprocArgs* a) {
   Op o{};
   o.kind = OP_PREPROC;
   o.pre = *a;
+  ((Plan*)p)->ops.push_back(o);
+  return 0;
+}
+extern "C" int dml_plan_add_stem(void* p, const DmlStemArgs* a) {
+  Op o{};
+  o.kind = OP_STEM;
+  o.stem = *a;
   ((Plan*)p)->ops.push_back(o);
   return 0;
 }

@@ -55,7 +55,10 @@ int main() {
     DmlPreprocArgs pr;
     std::memset(&pr, 0, sizeof pr);
     CHECK(dml_plan_add_preprocess(plan, &pr) == 0);
-    n += 3;
+    DmlStemArgs st;
+    std::memset(&st, 0, sizeof st);
+    CHECK(dml_plan_add_stem(plan, &st) == 0);
+    n += 4;
     CHECK(dml_plan_size(plan) == n);
     // error paths that must return before any device call
     CHECK(dml_plan_replay(plan, nullptr) != 0);
@@ -94,6 +97,18 @@ int main() {
   CHECK(dml_pool(&p, nullptr) != 0);
   CHECK(dml_global_avgpool(nullptr, nullptr, 1, 1, 12, 12, nullptr) != 0);
   CHECK(dml_softmax_top5_split(nullptr, 1, 4096, 4096, 1, 0, nullptr, nullptr, nullptr, nullptr) != 0);
+  // fused stem: only conv 7x7/2 pad 3 + pool 3x3/2 pad 1 geometry, K >= 224, 64 channels
+  DmlStemArgs st;
+  std::memset(&st, 0, sizeof st);
+  st.N = 1; st.Hs = 224; st.Ws = 224; st.H = 224; st.W = 224; st.ldw = 256;
+  st.Hc = 112; st.Wc = 112; st.Ho = 56; st.Wo = 56; st.ldy = 64;
+  st.ldw = 128;
+  CHECK(dml_stem_resnet(&st, nullptr) != 0);    // weights shorter than K = 224
+  st.ldw = 256; st.Ho = 55;
+  CHECK(dml_stem_resnet(&st, nullptr) != 0);    // pool size not 3x3/2 pad 1 of the conv
+  st.Ho = 56; st.Hc = 111;
+  CHECK(dml_stem_resnet(&st, nullptr) != 0);    // conv size not 7x7/2 pad 3 of the input
+  CHECK(std::string(dml_last_error()).find("unsupported shape") != std::string::npos);
   dml_set_error(nullptr);
   CHECK(std::string(dml_last_error()).empty());
 

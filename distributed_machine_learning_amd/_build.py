@@ -27,6 +27,7 @@ SOURCES = [
     CSRC / "kernels" / "conv_igemm_v2.hip",
     CSRC / "kernels" / "conv_halo.hip",
     CSRC / "kernels" / "misc.hip",
+    CSRC / "kernels" / "stem_fused.hip",
     CSRC / "runtime" / "runtime.hip",
 ]
 HEADERS = [CSRC / "include" / "dml.h", CSRC / "kernels" / "common.h", CSRC / "kernels" / "conv_shared.h"]

@@ -49,7 +49,17 @@ class PreprocArgs(C.Structure):
     ]
 
 
+class StemArgs(C.Structure):
+    _fields_ = [
+        ("src", C.c_void_p), ("w", C.c_void_p), ("bias", C.c_void_p), ("y", C.c_void_p),
+        ("N", C.c_int), ("Hs", C.c_int), ("Ws", C.c_int), ("H", C.c_int), ("W", C.c_int), ("mode", C.c_int),
+        ("ldw", C.c_int), ("Hc", C.c_int), ("Wc", C.c_int), ("Ho", C.c_int), ("Wo", C.c_int), ("ldy", C.c_int),
+    ]
+
+
 _SIGS = {
+    "dml_stem_resnet": (C.c_int, [C.POINTER(StemArgs), C.c_void_p]),
+    "dml_plan_add_stem": (C.c_int, [C.c_void_p, C.POINTER(StemArgs)]),
     "dml_conv": (C.c_int, [C.POINTER(ConvArgs), C.c_int, C.c_void_p]),
     "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),
     "dml_conv_v2_init": (C.c_int, []),

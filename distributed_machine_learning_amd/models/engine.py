@@ -60,11 +60,12 @@ class Engine:
                  src_hw: Optional[Tuple[int, int]] = None, cfg_overrides: Optional[Dict[str, int]] = None,
                  src_slots: int = 1, reuse_buffers: bool = True, autotune: bool = True, optimize: bool = True,
                  share: Optional["Engine"] = None, src_tensors: Optional[List[torch.Tensor]] = None,
-                 result_view: Optional[torch.Tensor] = None):
+                 result_view: Optional[torch.Tensor] = None, fuse_stem: bool = True):
         """``share``: reuse another engine's (optimized) graph and resident weights
         (sub-batch engines of a SplitEngine); ``src_tensors`` / ``result_view``:
         external uint8 source slots / [2, batch, 5] result rows to use instead of
-        allocating them."""
+        allocating them. ``fuse_stem=False`` (or DML_FUSED_STEM=0) keeps the
+        ResNet stem as three launches (preprocess, conv, pool)."""
         if share is not None:
             graph = share.g
         elif optimize:  # graph rewrites: conv-before-avgpool, sibling 1x1 fusion (models/optimize.py)
@@ -87,6 +88,9 @@ class Engine:
         self.stem = readers[0] if (len(readers) == 1 and isinstance(readers[0], Conv) and readers[0].cin == 3
                                    and readers[0].in_coff == 0 and readers[0].kw > 1) else None
         self.stem_lpad = self.stem.pw if self.stem is not None else 0
+        # ResNet stem: preprocess + 7x7/2 conv + 3x3/2 max pool run as ONE kernel
+        # (csrc/kernels/stem_fused.hip) when the pool is the conv's only consumer.
+        self.stem_pool = self._fusable_stem_pool(fuse_stem)
         self._src_tensors, self._result_view = src_tensors, result_view
         if share is not None:
             self.wdev, self.whalo = share.wdev, share.whalo
@@ -144,6 +148,23 @@ class Engine:
                 torch.from_numpy(bias).to(self.device),
                 K, kpad, cin_eff,
             )
+
+    def _fusable_stem_pool(self, enabled: bool) -> Optional[Pool]:
+        """The max pool that the fused stem kernel can absorb together with the
+        stem conv (conv 7x7/2 pad 3 -> 64 ch + ReLU, then pool 3x3/2 pad 1), else None."""
+        s = self.stem
+        if not enabled or s is None or self.device.type != "cuda" or os.environ.get("DML_FUSED_STEM") == "0":
+            return None
+        if not (s.kh == s.kw == 7 and s.sh == s.sw == 2 and s.ph == s.pw == 3 and s.cout == 64 and s.relu
+                and s.residual is None and not s.out_f32 and s.out_coff == 0):
+            return None
+        users = [n for n in self.g.nodes if s.out in (getattr(n, "inp", None), getattr(n, "residual", None))]
+        if len(users) != 1 or not isinstance(users[0], Pool):
+            return None
+        p = users[0]
+        if (p.mode, p.k, p.stride, p.pad, p.out_coff, p.relu) != ("max", 3, 2, 1, 0, False):
+            return None
+        return p
 
     def _halo_eligible(self, n) -> bool:
         return (isinstance(n, Conv) and n is not self.stem and n.sh == 1 and n.sw == 1 and n.kh * n.kw > 1
@@ -253,12 +274,27 @@ class Engine:
         plan = L.dml_plan_create()
         self.op_names: List[str] = []
         self.op_cfg: Dict[str, int] = {}
-        pa = N.PreprocArgs(src.data_ptr(), self.buf[g.input].data_ptr(), B, self.src_hw[0], self.src_hw[1],
-                           g.input_hw[0], g.input_hw[1], 0 if g.preprocess == "caffe" else 1,
-                           int(self.stem is not None), self.stem_lpad)
-        N.check(L.dml_plan_add_preprocess(plan, C.byref(pa)), "plan preprocess")
-        self.op_names.append("preprocess")
+        mode = 0 if g.preprocess == "caffe" else 1
+        skip = set()
+        if self.stem_pool is not None:
+            s, p = self.stem, self.stem_pool
+            wk, bias, _, kpad, _ = self.wdev[s.name]
+            hc, wc, _ = g.shape(s.out)
+            ho, wo, _ = g.shape(p.out)
+            sa = N.StemArgs(src.data_ptr(), wk.data_ptr(), bias.data_ptr(), self.buf[p.out].data_ptr(), B,
+                            self.src_hw[0], self.src_hw[1], g.input_hw[0], g.input_hw[1], mode, kpad, hc, wc,
+                            ho, wo, self.cbuf[p.out])
+            N.check(L.dml_plan_add_stem(plan, C.byref(sa)), "plan stem")
+            self.op_names.append(f"preprocess+{s.name}+{p.name}")
+            skip = {s.name, p.name}
+        else:
+            pa = N.PreprocArgs(src.data_ptr(), self.buf[g.input].data_ptr(), B, self.src_hw[0], self.src_hw[1],
+                               g.input_hw[0], g.input_hw[1], mode, int(self.stem is not None), self.stem_lpad)
+            N.check(L.dml_plan_add_preprocess(plan, C.byref(pa)), "plan preprocess")
+            self.op_names.append("preprocess")
         for n in g.nodes:
+            if n.name in skip:
+                continue
             if isinstance(n, (Conv, Dense, FusedConv)):
                 cfg = self.cfg_overrides.get(n.name, self.tuned.get(n.name, -1))
                 a = self._conv_args(n, halo=cfg >= 40)
@@ -350,6 +386,8 @@ class Engine:
         N.check(self.lib.dml_plan_replay_part(self.plans[slot], i, N.stream_ptr(stream)), "plan replay_part")
 
     def run_from_preprocessed(self, stream=None) -> None:
+        if self.stem_pool is not None:
+            raise RuntimeError("the fused stem reads the uint8 source; build the Engine with fuse_stem=False")
         N.check(self.lib.dml_plan_run_range(self.plan, 1, -1, N.stream_ptr(stream)), "plan run_range")
 
     def infer(self, images_u8: torch.Tensor, stream=None):

@@ -16,7 +16,7 @@ import torch
 from .. import _native as N
 
 __all__ = ["conv2d_nhwc", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight",
-           "pack_weight_halo", "HALO_CFGS"]
+           "pack_weight_halo", "HALO_CFGS", "resnet_stem"]
 
 # stride-1 halo-tile conv configs (csrc/kernels/conv_halo.hip); they take
 # chunk-major weights from pack_weight_halo
@@ -156,6 +156,26 @@ def preprocess(images_u8: torch.Tensor, out_hw, mode: str, pair: bool = False, l
     a = N.PreprocArgs(images_u8.data_ptr(), out.data_ptr(), n, hs, ws, out_hw[0], out_hw[1],
                       0 if mode == "caffe" else 1, int(pair), lpad)
     N.check(N.lib().dml_preprocess(C.byref(a), N.stream_ptr()), "preprocess")
+    return out
+
+
+def resnet_stem(images_u8: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, out_hw=(224, 224),
+                mode: str = "caffe") -> torch.Tensor:
+    """Fused ResNet stem (csrc/kernels/stem_fused.hip): uint8 [N, Hs, Ws, 3] ->
+    nearest resize to out_hw + caffe/tf normalisation -> conv 7x7/2 pad 3 with the
+    pair-packed bf16 weights [>=64][>=224] (models.engine.pair_pack_kernel +
+    pack_conv_weight) + bias + ReLU -> max pool 3x3/2 pad 1 -> bf16 NHWC [N, Ho, Wo, 64]."""
+    n, hs, ws, _ = images_u8.shape
+    h, w = out_hw
+    hc, wc = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    ho, wo = (hc - 1) // 2 + 1, (wc - 1) // 2 + 1
+    out = torch.empty((n, ho, wo, 64), device=images_u8.device, dtype=torch.bfloat16)
+    bias_p = bias.to(images_u8.device, torch.float32).contiguous()
+    assert images_u8.is_contiguous() and w_packed.is_contiguous() and w_packed.shape[0] >= 64
+    a = N.StemArgs(images_u8.data_ptr(), w_packed.data_ptr(), bias_p.data_ptr(), out.data_ptr(), n, hs, ws, h, w,
+                   0 if mode == "caffe" else 1, w_packed.shape[1], hc, wc, ho, wo, 64)
+    N.check(N.lib().dml_stem_resnet(C.byref(a), N.stream_ptr()), "dml_stem_resnet")
+    out._keep = bias_p
     return out
 
 

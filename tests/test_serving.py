@@ -171,12 +171,15 @@ def test_cluster_job_end_to_end(tmp_path):
 
 def test_concurrent_jobs_fair_share(tmp_path):
     async def main():
-        net, blobs, nodes = await _cluster(tmp_path, n_workers=4, delay=0.05)
+        # batches long enough (0.3 s) that every worker is mid-batch when j2 arrives,
+        # so the fair-share split must preempt (a short delay left workers idle
+        # between batches on a loaded host and the test passed without stealing)
+        net, blobs, nodes = await _cluster(tmp_path, n_workers=4, delay=0.3)
         cli = nodes["cli"]
         await _load_images(cli, 8)
-        j1 = await cli.submit_job("ResNet50", 400)
+        j1 = await cli.submit_job("ResNet50", 160)
         await asyncio.sleep(0.2)
-        j2 = await cli.submit_job("InceptionV3", 400)
+        j2 = await cli.submit_job("InceptionV3", 160)
         await asyncio.sleep(0.25)
         models = [a["model"] for a in nodes["c0"].coordinator.assignments().values()]
         assert models.count("InceptionV3") >= 1 and models.count("ResNet50") >= 1
