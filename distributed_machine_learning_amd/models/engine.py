@@ -60,11 +60,11 @@ class Engine:
                  src_hw: Optional[Tuple[int, int]] = None, cfg_overrides: Optional[Dict[str, int]] = None,
                  src_slots: int = 1, reuse_buffers: bool = True, autotune: bool = True, optimize: bool = True,
                  share: Optional["Engine"] = None, src_tensors: Optional[List[torch.Tensor]] = None,
-                 result_view: Optional[torch.Tensor] = None, fuse_stem: bool = True):
+                 result_views: Optional[List[torch.Tensor]] = None, fuse_stem: bool = True):
         """``share``: reuse another engine's (optimized) graph and resident weights
-        (sub-batch engines of a SplitEngine); ``src_tensors`` / ``result_view``:
-        external uint8 source slots / [2, batch, 5] result rows to use instead of
-        allocating them. ``fuse_stem=False`` (or DML_FUSED_STEM=0) keeps the
+        (sub-batch engines of a SplitEngine); ``src_tensors`` / ``result_views``:
+        external uint8 source slots / per-slot [2, batch, 5] result rows to use
+        instead of allocating them. ``fuse_stem=False`` (or DML_FUSED_STEM=0) keeps the
         ResNet stem as three launches (preprocess, conv, pool)."""
         if share is not None:
             graph = share.g
@@ -91,7 +91,7 @@ class Engine:
         # ResNet stem: preprocess + 7x7/2 conv + 3x3/2 max pool run as ONE kernel
         # (csrc/kernels/stem_fused.hip) when the pool is the conv's only consumer.
         self.stem_pool = self._fusable_stem_pool(fuse_stem)
-        self._src_tensors, self._result_view = src_tensors, result_view
+        self._src_tensors, self._result_views = src_tensors, result_views
         if share is not None:
             self.wdev, self.whalo = share.wdev, share.whalo
         else:
@@ -236,13 +236,24 @@ class Engine:
             self.srcs = [torch.zeros((B, self.src_hw[0], self.src_hw[1], 3), device=self.device, dtype=torch.uint8)
                          for _ in range(self.src_slots)]
         self.src = self.srcs[0]
-        # one packed result tensor [2][B][5]: top-5 class ids (int32) and their
-        # probabilities (fp32 bits) -> a single RCCL gather per batch
-        self.result = (self._result_view if self._result_view is not None else
-                       torch.zeros((2, B, 5), device=self.device, dtype=torch.int32))
+        # one packed result tensor [2][B][5] per source slot: top-5 class ids
+        # (int32) and their probabilities (fp32 bits) -> a single RCCL gather per
+        # batch. Per slot, so the forward of batch k+1 may run while batch k's
+        # result is still being gathered.
+        if self._result_views is not None:
+            assert len(self._result_views) == self.src_slots
+            self.results = list(self._result_views)
+        else:
+            self.results = [torch.zeros((2, B, 5), device=self.device, dtype=torch.int32)
+                            for _ in range(self.src_slots)]
+        self._select_result(0)
+        self.probs = torch.zeros((B, g.classes), device=self.device, dtype=torch.float32)
+
+    def _select_result(self, slot: int) -> None:
+        """result / top_idx / top_p name the result rows of the last-run slot."""
+        self.result = self.results[slot]
         self.top_idx = self.result[0]
         self.top_p = self.result[1].view(torch.float32)
-        self.probs = torch.zeros((B, g.classes), device=self.device, dtype=torch.float32)
 
     def view(self, name: str) -> torch.Tensor:
         """NHWC view of a tensor buffer (for tests / debugging)."""
@@ -265,11 +276,11 @@ class Engine:
             table = tuning.autotune(convs, halo_args=halos)
             for n, a, ah in zip(cnodes, convs, halos):
                 self.tuned[n.name] = table.get(tuning.shape_key(a, ah is not None), -1)
-        self.plans = [self._build_one_plan(self.srcs[i]) for i in range(self.src_slots)]
+        self.plans = [self._build_one_plan(self.srcs[i], self.results[i]) for i in range(self.src_slots)]
         self.plan = self.plans[0]
         self.graph_captured = [False] * self.src_slots
 
-    def _build_one_plan(self, src: torch.Tensor):
+    def _build_one_plan(self, src: torch.Tensor, result: torch.Tensor):
         g, B, L = self.g, self.batch, self.lib
         plan = L.dml_plan_create()
         self.op_names: List[str] = []
@@ -315,7 +326,7 @@ class Engine:
             self.op_names.append(n.name)
         N.check(L.dml_plan_add_softmax_top5_split(plan, self.buf[g.logits].data_ptr(), B, g.classes, g.classes,
                                                   self.fc_ksplit, B * g.classes, self.probs.data_ptr(),
-                                                  self.top_idx.data_ptr(), self.top_p.data_ptr()),
+                                                  result[0].data_ptr(), result[1].data_ptr()),
                 "plan softmax_top5")
         self.op_names.append("softmax_top5")
         return plan
@@ -367,6 +378,7 @@ class Engine:
     def run(self, stream=None, use_graph: bool = False, slot: int = 0) -> None:
         s = N.stream_ptr(stream)
         plan = self.plans[slot]
+        self._select_result(slot)
         if use_graph:
             if not self.graph_captured[slot]:
                 N.check(self.lib.dml_plan_capture(plan, s), "plan capture")
@@ -438,15 +450,16 @@ class SplitEngine:
         self.srcs = [torch.zeros((batch, hw[0], hw[1], 3), device=self.device, dtype=torch.uint8)
                      for _ in range(src_slots)]
         self.src = self.srcs[0]
-        self.result = torch.zeros((2, batch, 5), device=self.device, dtype=torch.int32)
-        self.top_idx = self.result[0]
-        self.top_p = self.result[1].view(torch.float32)
+        self.results = [torch.zeros((2, batch, 5), device=self.device, dtype=torch.int32)
+                        for _ in range(src_slots)]
+        self._select_result(0)
         self.engines: List[Engine] = []
         for i in range(splits):
             rows = slice(i * sub, (i + 1) * sub)
             self.engines.append(Engine(graph, weights if i == 0 else None, batch=sub, device=device,
                                        src_slots=src_slots, src_hw=hw, share=self.engines[0] if i else None,
-                                       src_tensors=[t[rows] for t in self.srcs], result_view=self.result[:, rows],
+                                       src_tensors=[t[rows] for t in self.srcs],
+                                       result_views=[r[:, rows] for r in self.results],
                                        **kw))
         self.g = self.engines[0].g
         # stream 0 is the caller's stream: only nstreams-1 extra streams.
@@ -460,12 +473,32 @@ class SplitEngine:
     def op_cfg(self) -> Dict[str, int]:
         return self.engines[0].op_cfg
 
-    def run(self, stream=None, use_graph: bool = False, slot: int = 0) -> None:
+    def _select_result(self, slot: int) -> None:
+        self.result = self.results[slot]
+        self.top_idx = self.result[0]
+        self.top_p = self.result[1].view(torch.float32)
+
+    def run(self, stream=None, use_graph: bool = False, slot: int = 0,
+            deps: Optional[List[torch.cuda.Event]] = None) -> None:
+        """Forward of source slot ``slot``; returns with ``stream`` joined on
+        every sub-batch. ``deps=None``: the extra streams fork from ``stream``.
+        ``deps`` = the events this forward really depends on (source slot
+        filled, previous reader of this slot's result done): the extra streams
+        wait on those only, so the next batch's sub-batches start as soon as
+        their own inputs are ready instead of behind the caller stream's tail
+        (gather / host copies of the previous batch) — no drain bubble between
+        batches on the extra streams."""
         main = stream if stream is not None else torch.cuda.current_stream(self.device)
-        self._fork.record(main)
+        self._select_result(slot)
+        for e in self.engines:
+            e._select_result(slot)
         lanes = [main] + self.streams
+        if deps is None:
+            self._fork.record(main)
+            deps = [self._fork]
         for s in self.streams:
-            s.wait_event(self._fork)
+            for ev in deps:
+                s.wait_event(ev)
         for i in range(1, self.splits):  # extra streams' sub-batches first, then the caller's
             if i % self.nstreams:
                 self.engines[i].run(lanes[i % self.nstreams], use_graph=use_graph, slot=slot)

@@ -59,6 +59,10 @@ class ServingPipeline:
         self.ev_copied = [torch.cuda.Event() for _ in range(2)]
         self.ev_consumed = [torch.cuda.Event() for _ in range(2)]
         self.ev_res = [torch.cuda.Event() for _ in range(2)]
+        self.ev_gathered = [torch.cuda.Event() for _ in range(2)]  # WAR on the slot's result rows
+        # a SplitEngine's extra streams wait on these events only (not on the
+        # compute stream), so they never idle behind the previous batch's gather
+        self._split_deps = hasattr(engine, "engines")
         B = engine.batch
         self.host_res = [torch.empty((dp.world, 2, B, 5), dtype=torch.int32, pin_memory=True) for _ in range(2)]
         self.stats = PipelineStats()
@@ -91,7 +95,11 @@ class ServingPipeline:
             cs = self.compute_stream
             cs.wait_event(self.ev_copied[slot])
             with torch.cuda.stream(cs), tr.gpu_span("forward", cs, lane="compute stream", step=k):
-                eng.run(cs, use_graph=self.use_graph, slot=slot)
+                if self._split_deps:
+                    eng.run(cs, use_graph=self.use_graph, slot=slot,
+                            deps=[self.ev_copied[slot], self.ev_gathered[slot]])
+                else:
+                    eng.run(cs, use_graph=self.use_graph, slot=slot)
             self.ev_consumed[slot].record(cs)
             if k + 1 < steps:  # dispatch + stage the next batch while this one computes
                 recs.append(BatchRecord(k + 1, time.perf_counter()))
@@ -101,7 +109,8 @@ class ServingPipeline:
                     row = dp.dispatch(table_fn(k + 1) if is0 else None)
                 self._stage(k + 1, row)
             with torch.cuda.stream(cs), tr.gpu_span("gather", cs, lane="compute stream", step=k):
-                bufs = dp.gather(eng.result)
+                bufs = dp.gather(eng.results[slot])
+                self.ev_gathered[slot].record(cs)
                 if is0:
                     hr = self.host_res[slot]
                     for r, b in enumerate(bufs):

@@ -126,7 +126,7 @@ class GpuRankBackend(RankBackend):
             eng.run(s, use_graph=True, slot=slot)
             self.ev_consumed[(model, slot)].record(s)
             out.zero_()
-            out[:, : eng.batch].copy_(eng.result)
+            out[:, : eng.batch].copy_(eng.results[slot])
             self.ev_done[slot].record(s)
         return out, self.ev_done[slot]
 
