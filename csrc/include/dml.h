@@ -84,8 +84,24 @@ typedef struct {
   int Ho, Wo, ldy;    // pool output size / channel stride
 } DmlStemArgs;
 
+// Fused InceptionV3 stem (csrc/kernels/stem_fused.hip): uint8 image -> preprocess ->
+// conv 3x3/2 valid (3 -> 32) + ReLU -> conv 3x3/1 valid (32 -> 32) + ReLU, one kernel.
+typedef struct {
+  const void* src;     // uint8 [N][Hs][Ws][3] RGB
+  const void* w1;      // bf16 [>=32][ldw1]: pair-packed 3x3 kernel, K = (row r, pair tap s', 8 ch), 48 used
+  const float* b1;     // fp32 [32]
+  const void* w2;      // bf16 [>=32][ldw2]: K = (r, s, 32 ch), 288 used
+  const float* b2;     // fp32 [32]
+  void* y;             // bf16 NHWC [N][H2][W2][ldy]
+  int N, Hs, Ws, H, W, mode;
+  int ldw1, ldw2;
+  int H1, W1;          // conv1 output size
+  int H2, W2, ldy;     // conv2 output size / channel stride
+} DmlIncStemArgs;
+
 // ---- single-op launches (used by tests and by the plan executor) ----
 int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s);
+int dml_stem_inception(const DmlIncStemArgs* a, hipStream_t s);
 int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2_init(void);
@@ -118,6 +134,7 @@ int dml_plan_add_softmax_top5_split(void* plan, float* logits, int B, int classe
                                     int split_ld, float* probs, int* idx, float* p);
 int dml_plan_add_preprocess(void* plan, const DmlPreprocArgs* a);
 int dml_plan_add_stem(void* plan, const DmlStemArgs* a);
+int dml_plan_add_inc_stem(void* plan, const DmlIncStemArgs* a);
 int dml_plan_size(void* plan);
 int dml_plan_run(void* plan, hipStream_t s);
 int dml_plan_run_range(void* plan, int begin, int end, hipStream_t s);

@@ -203,6 +203,206 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
 }
 
 }  // namespace stem
+
+// ---------------------------------------------------------------------------
+// InceptionV3 stem: uint8 -> preprocess (tf) -> conv 3x3/2 valid 3->32 + ReLU ->
+// conv 3x3/1 valid 32->32 + ReLU, one launch (reference models.py:26-38; Keras
+// conv2d_1 / conv2d_2). A workgroup owns a 16x16 tile of conv2 outputs:
+//  1. the 37 x 19 pair-packed input patch, straight from the uint8 source (as the
+//     ResNet stem: all byte loads first, clamped addresses, padding zeroed after);
+//  2. conv1 over the 18x18 window under the tile (21 MFMA pixel fragments):
+//     K = 3 rows x 2 pair taps x 8 = 48 (two 32-deep k-steps; the 2 padding
+//     chunks carry zero weights), bias + ReLU -> bf16 into an LDS tile whose
+//     80-B rows keep the conv2 fragment reads bank-conflict free;
+//  3. conv2 from that tile: k-step t = tap (r, s) of 32 channels, a pixel
+//     fragment = one tile row of 16 outputs, one ds_read_b128 per fragment;
+//     weights (32 x 288) for both convs stay in VGPRs;
+//  4. bias + ReLU -> bf16 staged in LDS -> 16-B NHWC stores.
+// The 147x147x32 conv1 output and the 299x300x16-B pair-packed input never
+// touch HBM (the unfused path writes and re-reads both).
+namespace istem {
+
+constexpr int TH = 16, TW = 16;              // conv2 outputs per workgroup
+constexpr int R1H = TH + 2, R1W = TW + 2;    // conv1 window 18 x 18
+constexpr int NP1 = R1H * R1W;               // 324
+constexpr int F1 = (NP1 + 15) / 16;          // 21 conv1 pixel fragments
+constexpr int IR = 2 * (R1H - 1) + 3;        // 37 input rows
+constexpr int PQ = R1W + 1;                  // 19 pixel pairs per input row
+constexpr int PATCH_BYTES = IR * PQ * 16;    // 11248
+constexpr int C1ROW = 32 * 2 + 16;           // conv1 tile row (80 B)
+constexpr int C1_BYTES = NP1 * C1ROW;        // 25920
+constexpr int OROW = 32 * 2 + 16;            // output staging row (80 B)
+constexpr int OUT_BYTES = TH * TW * OROW;    // 20480
+constexpr int R0_BYTES = PATCH_BYTES > OUT_BYTES ? PATCH_BYTES : OUT_BYTES;
+constexpr int NT = 256;
+constexpr int FILL = (IR * PQ + NT - 1) / NT;  // 3
+
+__global__ __launch_bounds__(NT, 3) void inc_stem_kernel(DmlIncStemArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[R0_BYTES + C1_BYTES];
+  char* patch = smem;  // phase 1-2; reused as the output staging tile in phase 4
+  char* ostage = smem;
+  char* c1 = smem + R0_BYTES;
+
+  const int tpr = (a.W2 + TW - 1) / TW, tpc = (a.H2 + TH - 1) / TH;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = blk / (tpr * tpc);
+  const int rem = blk - n * tpr * tpc;
+  const int ty = rem / tpr, tx = rem - ty * tpr;
+  const int oy0 = ty * TH, ox0 = tx * TW;   // conv2 tile origin == conv1 window origin (valid 3x3)
+  const int ir0 = 2 * oy0, ic0 = 2 * ox0;   // input patch origin (conv1 3x3/2 valid)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+
+  // weights of both convs in VGPRs: A rows = output channel (2 fragments of 16)
+  bf16x8 w1f[2][2], w2f[9][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      w1f[ks][i] = *(const bf16x8*)((const bf16*)a.w1 + (long)(i * 16 + frow) * a.ldw1 + ks * 32 + fq * 8);
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      w2f[t][i] = *(const bf16x8*)((const bf16*)a.w2 + (long)(i * 16 + frow) * a.ldw2 + t * 32 + fq * 8);
+  float4 b1v[2], b2v[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    b1v[i] = *(const float4*)(a.b1 + i * 16 + fq * 4);
+    b2v[i] = *(const float4*)(a.b2 + i * 16 + fq * 4);
+  }
+
+  // 1. input patch (pair-packed; all loads issued before any conversion)
+  {
+    const float sy = (float)a.Hs / (float)a.H, sx = (float)a.Ws / (float)a.W;
+    const unsigned char* img = (const unsigned char*)a.src + (long)n * a.Hs * a.Ws * 3;
+    unsigned char px[FILL][2][3];
+    unsigned okm[FILL];
+#pragma unroll
+    for (int it = 0; it < FILL; ++it) {
+      const int t = min(tid + it * NT, IR * PQ - 1);
+      const int i = t / PQ, q = t - i * PQ;
+      const int ih = ir0 + i, iw = ic0 + 2 * q;
+      const int iy = min((int)(((float)min(max(ih, 0), a.H - 1) + 0.5f) * sy), a.Hs - 1);  // Pillow NEAREST
+      okm[it] = ((unsigned)ih < (unsigned)a.H) ? ((unsigned)((unsigned)iw < (unsigned)a.W) |
+                                                  ((unsigned)((unsigned)(iw + 1) < (unsigned)a.W) << 1)) : 0u;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ix = min((int)(((float)min(max(iw + h, 0), a.W - 1) + 0.5f) * sx), a.Ws - 1);
+        const unsigned char* p = img + ((long)iy * a.Ws + ix) * 3;
+        px[it][h][0] = p[0];
+        px[it][h][1] = p[1];
+        px[it][h][2] = p[2];
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < FILL; ++it) {
+      const int t = tid + it * NT;
+      if (t >= IR * PQ) continue;
+      float f[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float r = px[it][h][0], g = px[it][h][1], b = px[it][h][2];
+        const bool ok = (okm[it] >> h) & 1u;
+        float* o = f + 4 * h;
+        if (a.mode == 0) {
+          o[0] = b - 103.939f; o[1] = g - 116.779f; o[2] = r - 123.68f;
+        } else {
+          o[0] = r / 127.5f - 1.f; o[1] = g / 127.5f - 1.f; o[2] = b / 127.5f - 1.f;
+        }
+        o[0] = ok ? o[0] : 0.f;
+        o[1] = ok ? o[1] : 0.f;
+        o[2] = ok ? o[2] : 0.f;
+        o[3] = 0.f;
+      }
+      *(uint4*)(patch + t * 16) =
+          make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+    }
+  }
+  __syncthreads();
+
+  // 2. conv1: wave w owns window fragments j = w, w + 4, ... (< 21)
+#pragma unroll
+  for (int jj = 0; jj < (F1 + 3) / 4; ++jj) {
+    const int j = wid + 4 * jj;
+    if (j >= F1) break;  // wave-uniform
+    const int po = j * 16 + frow;
+    const int p = min(po, NP1 - 1);
+    const int wa = p / R1W, wb = p - wa * R1W;
+    f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + fq;                 // K chunk: (row r, pair tap s'); chunks 6, 7 are zero weights
+      const int r = min(c >> 1, 2), sp = c & 1;  // (clamped so the padding chunks read finite patch data)
+      const bf16x8 pf = *(const bf16x8*)(patch + ((2 * wa + r) * PQ + wb + sp) * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[ks][i], pf, acc[i], 0, 0, 0);
+    }
+    if (po < NP1) {
+      const bool ok = (oy0 + wa < a.H1) && (ox0 + wb < a.W1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const f32x4 v = acc[i];
+        const float4 b = b1v[i];
+        const float f0 = ok ? fmaxf(v[0] + b.x, 0.f) : 0.f, f1 = ok ? fmaxf(v[1] + b.y, 0.f) : 0.f;
+        const float f2 = ok ? fmaxf(v[2] + b.z, 0.f) : 0.f, f3 = ok ? fmaxf(v[3] + b.w, 0.f) : 0.f;
+        *(uint2*)(c1 + p * C1ROW + (i * 16 + fq * 4) * 2) = make_uint2(pack2(f0, f1), pack2(f2, f3));
+      }
+    }
+  }
+  __syncthreads();
+
+  // 3. conv2: wave w owns output rows 4w .. 4w+3 (one 16-pixel fragment each)
+  f32x4 acc2[4][2];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc2[jj][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int r = t / 3, s = t - 3 * (t / 3);
+    bf16x8 pf[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+      pf[jj] = *(const bf16x8*)(c1 + ((4 * wid + jj + r) * R1W + frow + s) * C1ROW + fq * 16);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        acc2[jj][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[t][i], pf[jj], acc2[jj][i], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+
+  // 4. bias + ReLU -> bf16 staging (the patch region: every patch read ended
+  //    before the conv1 -> conv2 barrier) -> 16-B NHWC stores
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int px = (4 * wid + jj) * TW + frow;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 v = acc2[jj][i];
+      const float4 b = b2v[i];
+      *(uint2*)(ostage + px * OROW + (i * 16 + fq * 4) * 2) =
+          make_uint2(pack2(fmaxf(v[0] + b.x, 0.f), fmaxf(v[1] + b.y, 0.f)),
+                     pack2(fmaxf(v[2] + b.z, 0.f), fmaxf(v[3] + b.w, 0.f)));
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < TH * TW * 4 / NT; ++it) {
+    const int t = tid + it * NT;
+    const int px = t >> 2, cg = t & 3;
+    const int oy = oy0 + px / TW, ox = ox0 + px % TW;
+    if (oy < a.H2 && ox < a.W2)
+      *(uint4*)((unsigned short*)a.y + ((long)(n * a.H2 + oy) * a.W2 + ox) * a.ldy + cg * 8) =
+          *(const uint4*)(ostage + px * OROW + cg * 16);
+  }
+}
+
+}  // namespace istem
 }  // namespace dml
 
 extern "C" int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s) {
@@ -216,6 +416,21 @@ extern "C" int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s) {
   using namespace dml::stem;
   const long blocks = (long)a->N * ((a->Ho + PH - 1) / PH) * ((a->Wo + PW - 1) / PW);
   hipLaunchKernelGGL(dml::stem::stem_kernel, dim3((unsigned)blocks), dim3(NT), 0, s, *a);
+  DML_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dml_stem_inception(const DmlIncStemArgs* a, hipStream_t s) {
+  // hard-coded: conv 3x3/2 valid 3 -> 32, conv 3x3/1 valid 32 -> 32
+  if (a->ldw1 % 8 || a->ldw1 < 64 || a->ldw2 % 8 || a->ldw2 < 288 || a->ldy % 8 || a->ldy < 32 || a->N < 1 ||
+      a->H < 7 || a->W < 7 || a->H1 != (a->H - 3) / 2 + 1 || a->W1 != (a->W - 3) / 2 + 1 || a->H2 != a->H1 - 2 ||
+      a->W2 != a->W1 - 2 || a->Hs < 1 || a->Ws < 1) {
+    dml_set_error("dml_stem_inception: unsupported shape");
+    return -1;
+  }
+  using namespace dml::istem;
+  const long blocks = (long)a->N * ((a->H2 + TH - 1) / TH) * ((a->W2 + TW - 1) / TW);
+  hipLaunchKernelGGL(dml::istem::inc_stem_kernel, dim3((unsigned)blocks), dim3(NT), 0, s, *a);
   DML_CHECK_LAUNCH();
   return 0;
 }

@@ -42,7 +42,7 @@ extern "C" int dml_device_info(int* cus, int* arch_major, int* arch_minor) {
 
 // ----------------------------------------------------------------- plan ----
 namespace {
-enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM };
+enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM, OP_INC_STEM };
 struct GapArgs { const void* x; void* y; int N, HW, C, ldx; };
 struct SmArgs { float* logits; int B, classes, ld, nsplit, split_ld; float* probs; int* idx; float* p; };
 struct Op {
@@ -54,6 +54,7 @@ struct Op {
   SmArgs sm;
   DmlPreprocArgs pre;
   DmlStemArgs stem;
+  DmlIncStemArgs istem;
 };
 struct Plan {
   std::vector<Op> ops;
@@ -84,6 +85,7 @@ int run_op(const Op& o, hipStream_t s) {
                                     o.sm.probs, o.sm.idx, o.sm.p, s);
     case OP_PREPROC: return dml_preprocess(&o.pre, s);
     case OP_STEM: return dml_stem_resnet(&o.stem, s);
+    case OP_INC_STEM: return dml_stem_inception(&o.istem, s);
   }
   return -1;
 }
@@ -138,6 +140,13 @@ extern "C" int dml_plan_add_stem(void* p, const DmlStemArgs* a) {
   Op o{};
   o.kind = OP_STEM;
   o.stem = *a;
+  ((Plan*)p)->ops.push_back(o);
+  return 0;
+}
+extern "C" int dml_plan_add_inc_stem(void* p, const DmlIncStemArgs* a) {
+  Op o{};
+  o.kind = OP_INC_STEM;
+  o.istem = *a;
   ((Plan*)p)->ops.push_back(o);
   return 0;
 }

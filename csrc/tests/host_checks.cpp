@@ -58,7 +58,10 @@ int main() {
     DmlStemArgs st;
     std::memset(&st, 0, sizeof st);
     CHECK(dml_plan_add_stem(plan, &st) == 0);
-    n += 4;
+    DmlIncStemArgs ist;
+    std::memset(&ist, 0, sizeof ist);
+    CHECK(dml_plan_add_inc_stem(plan, &ist) == 0);
+    n += 5;
     CHECK(dml_plan_size(plan) == n);
     // error paths that must return before any device call
     CHECK(dml_plan_replay(plan, nullptr) != 0);
@@ -109,6 +112,14 @@ int main() {
   st.Ho = 56; st.Hc = 111;
   CHECK(dml_stem_resnet(&st, nullptr) != 0);    // conv size not 7x7/2 pad 3 of the input
   CHECK(std::string(dml_last_error()).find("unsupported shape") != std::string::npos);
+  DmlIncStemArgs ist;
+  std::memset(&ist, 0, sizeof ist);
+  ist.N = 1; ist.Hs = 299; ist.Ws = 299; ist.H = 299; ist.W = 299; ist.ldw1 = 64; ist.ldw2 = 320;
+  ist.H1 = 149; ist.W1 = 149; ist.H2 = 147; ist.W2 = 147; ist.ldy = 32;
+  ist.ldw2 = 256;
+  CHECK(dml_stem_inception(&ist, nullptr) != 0);  // conv2 weights shorter than K = 288
+  ist.ldw2 = 320; ist.H2 = 149;
+  CHECK(dml_stem_inception(&ist, nullptr) != 0);  // conv2 size not 3x3 valid of conv1
   dml_set_error(nullptr);
   CHECK(std::string(dml_last_error()).empty());
 

@@ -57,8 +57,20 @@ class StemArgs(C.Structure):
     ]
 
 
+class IncStemArgs(C.Structure):
+    _fields_ = [
+        ("src", C.c_void_p), ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p),
+        ("y", C.c_void_p),
+        ("N", C.c_int), ("Hs", C.c_int), ("Ws", C.c_int), ("H", C.c_int), ("W", C.c_int), ("mode", C.c_int),
+        ("ldw1", C.c_int), ("ldw2", C.c_int), ("H1", C.c_int), ("W1", C.c_int), ("H2", C.c_int), ("W2", C.c_int),
+        ("ldy", C.c_int),
+    ]
+
+
 _SIGS = {
     "dml_stem_resnet": (C.c_int, [C.POINTER(StemArgs), C.c_void_p]),
+    "dml_stem_inception": (C.c_int, [C.POINTER(IncStemArgs), C.c_void_p]),
+    "dml_plan_add_inc_stem": (C.c_int, [C.c_void_p, C.POINTER(IncStemArgs)]),
     "dml_plan_add_stem": (C.c_int, [C.c_void_p, C.POINTER(StemArgs)]),
     "dml_conv": (C.c_int, [C.POINTER(ConvArgs), C.c_int, C.c_void_p]),
     "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),

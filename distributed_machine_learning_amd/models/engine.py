@@ -91,6 +91,8 @@ class Engine:
         # ResNet stem: preprocess + 7x7/2 conv + 3x3/2 max pool run as ONE kernel
         # (csrc/kernels/stem_fused.hip) when the pool is the conv's only consumer.
         self.stem_pool = self._fusable_stem_pool(fuse_stem)
+        # InceptionV3 stem: preprocess + conv 3x3/2 + conv 3x3 as ONE kernel
+        self.stem_conv2 = self._fusable_inception_stem(fuse_stem) if self.stem_pool is None else None
         self._src_tensors, self._result_views = src_tensors, result_views
         if share is not None:
             self.wdev, self.whalo = share.wdev, share.whalo
@@ -165,6 +167,25 @@ class Engine:
         if (p.mode, p.k, p.stride, p.pad, p.out_coff, p.relu) != ("max", 3, 2, 1, 0, False):
             return None
         return p
+
+    def _fusable_inception_stem(self, enabled: bool) -> Optional[Conv]:
+        """The second conv that the fused InceptionV3 stem kernel absorbs together
+        with the stem conv (conv 3x3/2 valid 3 -> 32, then conv 3x3 valid 32 -> 32,
+        both + ReLU), else None."""
+        s = self.stem
+        if not enabled or s is None or self.device.type != "cuda" or os.environ.get("DML_FUSED_STEM") == "0":
+            return None
+        if not (s.kh == s.kw == 3 and s.sh == s.sw == 2 and s.ph == s.pw == 0 and s.cout == 32 and s.relu
+                and s.residual is None and not s.out_f32 and s.out_coff == 0):
+            return None
+        users = [n for n in self.g.nodes if s.out in (getattr(n, "inp", None), getattr(n, "residual", None))]
+        if len(users) != 1 or not isinstance(users[0], Conv):
+            return None
+        c = users[0]
+        if not (c.kh == c.kw == 3 and c.sh == c.sw == 1 and c.ph == c.pw == 0 and c.cin == 32 and c.cout == 32
+                and c.relu and c.residual is None and not c.out_f32 and c.in_coff == 0):
+            return None
+        return c
 
     def _halo_eligible(self, n) -> bool:
         return (isinstance(n, Conv) and n is not self.stem and n.sh == 1 and n.sw == 1 and n.kh * n.kw > 1
@@ -298,6 +319,18 @@ class Engine:
             N.check(L.dml_plan_add_stem(plan, C.byref(sa)), "plan stem")
             self.op_names.append(f"preprocess+{s.name}+{p.name}")
             skip = {s.name, p.name}
+        elif self.stem_conv2 is not None:
+            s, c = self.stem, self.stem_conv2
+            w1, b1, _, kp1, _ = self.wdev[s.name]
+            w2, b2, _, kp2, _ = self.wdev[c.name]
+            h1, wd1, _ = g.shape(s.out)
+            h2, wd2, _ = g.shape(c.out)
+            ia = N.IncStemArgs(src.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+                               self.buf[c.out].data_ptr() + 2 * c.out_coff, B, self.src_hw[0], self.src_hw[1],
+                               g.input_hw[0], g.input_hw[1], mode, kp1, kp2, h1, wd1, h2, wd2, self.cbuf[c.out])
+            N.check(L.dml_plan_add_inc_stem(plan, C.byref(ia)), "plan inception stem")
+            self.op_names.append(f"preprocess+{s.name}+{c.name}")
+            skip = {s.name, c.name}
         else:
             pa = N.PreprocArgs(src.data_ptr(), self.buf[g.input].data_ptr(), B, self.src_hw[0], self.src_hw[1],
                                g.input_hw[0], g.input_hw[1], mode, int(self.stem is not None), self.stem_lpad)
@@ -398,7 +431,7 @@ class Engine:
         N.check(self.lib.dml_plan_replay_part(self.plans[slot], i, N.stream_ptr(stream)), "plan replay_part")
 
     def run_from_preprocessed(self, stream=None) -> None:
-        if self.stem_pool is not None:
+        if self.stem_pool is not None or self.stem_conv2 is not None:
             raise RuntimeError("the fused stem reads the uint8 source; build the Engine with fuse_stem=False")
         N.check(self.lib.dml_plan_run_range(self.plan, 1, -1, N.stream_ptr(stream)), "plan run_range")
 

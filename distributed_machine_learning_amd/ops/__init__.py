@@ -16,7 +16,7 @@ import torch
 from .. import _native as N
 
 __all__ = ["conv2d_nhwc", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight",
-           "pack_weight_halo", "HALO_CFGS", "resnet_stem"]
+           "pack_weight_halo", "HALO_CFGS", "resnet_stem", "inception_stem"]
 
 # stride-1 halo-tile conv configs (csrc/kernels/conv_halo.hip); they take
 # chunk-major weights from pack_weight_halo
@@ -176,6 +176,27 @@ def resnet_stem(images_u8: torch.Tensor, w_packed: torch.Tensor, bias: torch.Ten
                    0 if mode == "caffe" else 1, w_packed.shape[1], hc, wc, ho, wo, 64)
     N.check(N.lib().dml_stem_resnet(C.byref(a), N.stream_ptr()), "dml_stem_resnet")
     out._keep = bias_p
+    return out
+
+
+def inception_stem(images_u8: torch.Tensor, w1_packed: torch.Tensor, b1: torch.Tensor, w2_packed: torch.Tensor,
+                   b2: torch.Tensor, out_hw=(299, 299), mode: str = "tf") -> torch.Tensor:
+    """Fused InceptionV3 stem (csrc/kernels/stem_fused.hip): uint8 [N, Hs, Ws, 3] ->
+    nearest resize + normalisation -> conv 3x3/2 valid (pair-packed weights
+    [>=32][>=64]) + ReLU -> conv 3x3 valid (weights [>=32][>=288], K = (r, s, 32 ch))
+    + ReLU -> bf16 NHWC [N, H2, W2, 32]."""
+    n, hs, ws, _ = images_u8.shape
+    h, w = out_hw
+    h1, w1 = (h - 3) // 2 + 1, (w - 3) // 2 + 1
+    out = torch.empty((n, h1 - 2, w1 - 2, 32), device=images_u8.device, dtype=torch.bfloat16)
+    b1p = b1.to(images_u8.device, torch.float32).contiguous()
+    b2p = b2.to(images_u8.device, torch.float32).contiguous()
+    assert images_u8.is_contiguous() and w1_packed.is_contiguous() and w2_packed.is_contiguous()
+    a = N.IncStemArgs(images_u8.data_ptr(), w1_packed.data_ptr(), b1p.data_ptr(), w2_packed.data_ptr(),
+                      b2p.data_ptr(), out.data_ptr(), n, hs, ws, h, w, 0 if mode == "caffe" else 1,
+                      w1_packed.shape[1], w2_packed.shape[1], h1, w1, h1 - 2, w1 - 2, 32)
+    N.check(N.lib().dml_stem_inception(C.byref(a), N.stream_ptr()), "dml_stem_inception")
+    out._keep = (b1p, b2p)
     return out
 
 

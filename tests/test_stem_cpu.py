@@ -68,3 +68,71 @@ def test_stem_tiling_matches_conv_pool(shape):
     got = emulate_stem(x, k, b)
     assert got.shape == ref.shape
     np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4)
+
+
+# ------------------------------------------------------ InceptionV3 stem --
+TH = TW = 16
+R1H, R1W = TH + 2, TW + 2
+IR_I, PQ_I = 2 * (R1H - 1) + 3, R1W + 1
+
+
+def emulate_inception_stem(x_nhwc, k1_hwio, b1, k2_hwio, b2):
+    """Tile math of inc_stem_kernel: 16x16 conv2 tiles, 18x18 conv1 window,
+    37x19 pair-packed patch, conv1 K chunk c -> (row c >> 1 clamped to 2, pair
+    tap c & 1) with zero weights on chunks 6, 7, conv2 k-step = tap (r, s)."""
+    n_, h, w, _ = x_nhwc.shape
+    w1 = pack_conv_weight(pair_pack_kernel(k1_hwio), 8, 32, 64)  # [32][64]: K = (r, s', c8) + 16 zero
+    w2 = pack_conv_weight(k2_hwio, 32, 32, 320)[:, :288]          # [32][288]: K = (r, s, c)
+    h1, wd1 = (h - 3) // 2 + 1, (w - 3) // 2 + 1
+    h2, wd2 = h1 - 2, wd1 - 2
+    y = np.zeros((n_, h2, wd2, 32), np.float32)
+    p = np.arange(R1H * R1W)
+    wa, wb = p // R1W, p % R1W
+    for n in range(n_):
+        for ty in range((h2 + TH - 1) // TH):
+            for tx in range((wd2 + TW - 1) // TW):
+                oy0, ox0 = ty * TH, tx * TW
+                ir0, ic0 = 2 * oy0, 2 * ox0
+                patch = np.zeros((IR_I, PQ_I, 8), np.float32)
+                for i in range(IR_I):
+                    ih = ir0 + i
+                    if not 0 <= ih < h:
+                        continue
+                    for q in range(PQ_I):
+                        iw = ic0 + 2 * q
+                        if 0 <= iw < w:
+                            patch[i, q, 0:3] = x_nhwc[n, ih, iw]
+                        if 0 <= iw + 1 < w:
+                            patch[i, q, 4:7] = x_nhwc[n, ih, iw + 1]
+                chunks = []
+                for c in range(8):
+                    r, sp = min(c >> 1, 2), c & 1
+                    chunks.append(patch[2 * wa + r, wb + sp])
+                a1 = np.stack(chunks, 1).reshape(-1, 64)
+                c1 = np.maximum(a1 @ w1.T + b1, 0.0)
+                ok = (oy0 + wa < h1) & (ox0 + wb < wd1)
+                c1 = np.where(ok[:, None], c1, 0.0).reshape(R1H, R1W, 32)
+                taps = [c1[r:r + TH, s:s + TW] for r in range(3) for s in range(3)]
+                a2 = np.stack(taps, 2).reshape(TH * TW, 288)
+                out = np.maximum(a2 @ w2.T + b2, 0.0).reshape(TH, TW, 32)
+                hh, ww = min(TH, h2 - oy0), min(TW, wd2 - ox0)
+                y[n, oy0:oy0 + hh, ox0:ox0 + ww] = out[:hh, :ww]
+    return y
+
+
+@pytest.mark.parametrize("shape", [(1, 39, 41), (2, 35, 67)])
+def test_inception_stem_tiling_matches_two_convs(shape):
+    n, h, w = shape
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((n, h, w, 3)).astype(np.float32)
+    k1 = (rng.standard_normal((3, 3, 3, 32)) * 0.3).astype(np.float32)
+    b1 = (rng.standard_normal(32) * 0.1).astype(np.float32)
+    k2 = (rng.standard_normal((3, 3, 32, 32)) * 0.1).astype(np.float32)
+    b2 = (rng.standard_normal(32) * 0.1).astype(np.float32)
+    t = F.relu(F.conv2d(torch.from_numpy(x).permute(0, 3, 1, 2), torch.from_numpy(k1).permute(3, 2, 0, 1),
+                        torch.from_numpy(b1), stride=2))
+    ref = F.relu(F.conv2d(t, torch.from_numpy(k2).permute(3, 2, 0, 1), torch.from_numpy(b2)))
+    ref = ref.permute(0, 2, 3, 1).numpy()
+    got = emulate_inception_stem(x, k1, b1, k2, b2)
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4)

@@ -70,3 +70,44 @@ def test_engine_fused_stem_equals_unfused():
     pf, pu = ef.view("pool1").float(), eu.view("pool1").float()
     assert (pf - pu).abs().max().item() <= 1e-2 * pu.abs().max().item()
     assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 2e-2
+
+
+@pytest.mark.parametrize("n,hs,ws,out_hw,mode", [
+    (2, 299, 299, (299, 299), "tf"),      # the InceptionV3 shape (147x147 conv2 grid, partial edge tiles)
+    (2, 300, 169, (299, 299), "tf"),      # nearest resize from a reference testfiles/ JPEG size
+    (1, 50, 60, (41, 39), "caffe"),       # small odd image, several partial tiles
+])
+def test_fused_inception_stem_matches_fp32(n, hs, ws, out_hw, mode):
+    torch.manual_seed(1)
+    imgs = torch.randint(0, 256, (n, hs, ws, 3), dtype=torch.uint8)
+    k1 = _bf(torch.randn(3, 3, 3, 32) * (2.0 / 27) ** 0.5)
+    b1 = torch.randn(32) * 0.1
+    k2 = _bf(torch.randn(3, 3, 32, 32) * (2.0 / 288) ** 0.5)
+    b2 = torch.randn(32) * 0.1
+    x = _bf(preprocess_reference(imgs, out_hw, mode))
+    t = _bf(F.relu(F.conv2d(x, k1.permute(3, 2, 0, 1), b1, stride=2)))  # conv1 output rounded to bf16 (LDS tile)
+    ref = F.relu(F.conv2d(t, k2.permute(3, 2, 0, 1), b2)).permute(0, 2, 3, 1)
+    w1 = torch.from_numpy(pack_conv_weight(pair_pack_kernel(k1.numpy()), 8, 256, 64)).to(torch.bfloat16).cuda()
+    w2 = torch.from_numpy(pack_conv_weight(k2.numpy(), 32, 256, 320)).to(torch.bfloat16).cuda()
+    y = ops.inception_stem(imgs.cuda(), w1, b1.cuda(), w2, b2.cuda(), out_hw, mode)
+    torch.cuda.synchronize()
+    got = y.float().cpu()
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    rel = _rel(got, ref)
+    assert rel < 1e-2, rel
+
+
+def test_engine_fused_inception_stem_equals_unfused():
+    g, w = build_model("InceptionV3", seed=7, calibrate=True)
+    imgs = torch.randint(0, 256, (2, 299, 299, 3), dtype=torch.uint8, device="cuda")
+    ef = Engine(g, w, batch=2)
+    eu = Engine(g, w, batch=2, fuse_stem=False)
+    assert ef.stem_conv2 is not None and eu.stem_conv2 is None
+    assert ef.op_names[0].startswith("preprocess+") and len(ef.op_names) == len(eu.op_names) - 2
+    ef.infer(imgs)
+    eu.infer(imgs)
+    torch.cuda.synchronize()
+    name = ef.stem_conv2.out
+    pf, pu = ef.view(name).float(), eu.view(name).float()
+    assert (pf - pu).abs().max().item() <= 1e-2 * pu.abs().max().item()
+    assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 5e-2
