@@ -99,9 +99,21 @@ typedef struct {
   int H2, W2, ldy;     // conv2 output size / channel stride
 } DmlIncStemArgs;
 
+// Fused 3x3 'same' conv (32 -> 64 ch, folded BN) + ReLU + 3x3/2 'valid' max pool
+// (csrc/kernels/conv_pool.hip; InceptionV3 conv2d_3 + max_pooling2d_1).
+typedef struct {
+  const void* x;       // bf16 NHWC [N][H][W][ldx] (32 channels used)
+  const void* w;       // bf16 [>=64][ldw]: K = (r, s, 32 ch), 288 used
+  const float* bias;   // fp32 [64]
+  void* y;             // bf16 NHWC [N][Ho][Wo][ldy]
+  int N, H, W, ldx, ldw;
+  int Ho, Wo, ldy;     // pool output
+} DmlConvPoolArgs;
+
 // ---- single-op launches (used by tests and by the plan executor) ----
 int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s);
 int dml_stem_inception(const DmlIncStemArgs* a, hipStream_t s);
+int dml_conv3x3_pool(const DmlConvPoolArgs* a, hipStream_t s);
 int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2_init(void);
@@ -135,6 +147,7 @@ int dml_plan_add_softmax_top5_split(void* plan, float* logits, int B, int classe
 int dml_plan_add_preprocess(void* plan, const DmlPreprocArgs* a);
 int dml_plan_add_stem(void* plan, const DmlStemArgs* a);
 int dml_plan_add_inc_stem(void* plan, const DmlIncStemArgs* a);
+int dml_plan_add_conv_pool(void* plan, const DmlConvPoolArgs* a);
 int dml_plan_size(void* plan);
 int dml_plan_run(void* plan, hipStream_t s);
 int dml_plan_run_range(void* plan, int begin, int end, hipStream_t s);

@@ -1,0 +1,172 @@
+// conv_pool.hip — 3x3 'same' convolution (32 -> 64 channels) + ReLU fused with the
+// 3x3/2 'valid' max pool that consumes it (gfx950). InceptionV3 conv2d_3 +
+// max_pooling2d_1 (Keras; reference models.py:26): unfused, the 147x147x64 conv
+// output is written to HBM and read back by the pool (2 x 177 MB per 64 images).
+//
+// A workgroup owns an 8x8 block of pool outputs:
+//  1. the 19x19 x 32-channel input patch the conv window needs (conv pad 1 ->
+//     zeros), 16-B global loads into registers (all issued first, clamped
+//     addresses, padding zeroed after) -> LDS rows of 80 B (64 B + 16-B pad: the
+//     16 lanes of a fragment read hit distinct banks);
+//  2. the 17x17 conv window (289 pixels = 19 MFMA fragments) with
+//     v_mfma_f32_16x16x32_bf16: k-step t = tap (r, s) over 32 channels, one
+//     ds_read_b128 per pixel fragment; wave w owns output channels 16w..16w+15,
+//     its 16 x 288 weights in VGPRs;
+//  3. bias + ReLU -> bf16 (the unfused rounding point) into an LDS tile that
+//     reuses the patch region;
+//  4. 3x3/2 max pool from LDS -> one 16-B NHWC store per 8 channels.
+#include "common.h"
+#include "dml.h"
+
+namespace dml {
+namespace cpool {
+
+constexpr int PB = 8;                        // pool outputs per block side
+constexpr int CW = 2 * PB + 1;               // conv window 17 x 17
+constexpr int NPX = CW * CW;                 // 289
+constexpr int NF = (NPX + 15) / 16;          // 19 pixel fragments
+constexpr int PW = CW + 2;                   // patch 19 x 19 (conv pad 1)
+constexpr int PROW = 32 * 2 + 16;            // patch pixel row: 32 bf16 + 16-B pad
+constexpr int PATCH_BYTES = PW * PW * PROW;  // 28880
+constexpr int TROW = 64 * 2 + 16;            // conv tile row: 64 bf16 + 16-B pad
+constexpr int TILE_BYTES = NPX * TROW;       // 41616
+constexpr int LDS_BYTES = PATCH_BYTES > TILE_BYTES ? PATCH_BYTES : TILE_BYTES;
+constexpr int NT = 256;
+constexpr int CHUNKS = PW * PW * 4;          // 16-B input chunks of the patch (1444)
+constexpr int FILL = (CHUNKS + NT - 1) / NT; // 6
+
+__device__ __forceinline__ float bf_at(const uint4& v, int q) {
+  const unsigned w = q < 2 ? v.x : q < 4 ? v.y : q < 6 ? v.z : v.w;
+  return bf2f((q & 1) ? (w >> 16) : (w & 0xffff));
+}
+
+__global__ __launch_bounds__(NT, 3) void conv_pool_kernel(DmlConvPoolArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  char* patch = smem;
+  char* tile = smem;  // after the conv (barrier in between)
+
+  const int bpr = (a.Wo + PB - 1) / PB, bpc = (a.Ho + PB - 1) / PB;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = blk / (bpr * bpc);
+  const int rem = blk - n * bpr * bpc;
+  const int by = rem / bpr, bx = rem - by * bpr;
+  const int py0 = by * PB, px0 = bx * PB;
+  const int cy0 = 2 * py0, cx0 = 2 * px0;  // conv window origin (valid pool)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+
+  // weights: this wave's 16 output channels, k-step t = tap (r, s), quarter fq = 8 channels
+  bf16x8 wf[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+    wf[t] = *(const bf16x8*)((const bf16*)a.w + (long)(wid * 16 + frow) * a.ldw + t * 32 + fq * 8);
+  const float4 bias = *(const float4*)(a.bias + wid * 16 + fq * 4);
+
+  // 1. patch: pixel (i, j) = input (cy0 - 1 + i, cx0 - 1 + j), 4 chunks of 8 channels
+  {
+    const unsigned short* x = (const unsigned short*)a.x + (long)n * a.H * a.W * a.ldx;
+    uint4 v[FILL];
+    bool ok[FILL];
+#pragma unroll
+    for (int it = 0; it < FILL; ++it) {
+      const int t = min(tid + it * NT, CHUNKS - 1);
+      const int pix = t >> 2, c = t & 3;
+      const int i = pix / PW, j = pix - i * PW;
+      const int ih = cy0 - 1 + i, iw = cx0 - 1 + j;
+      ok[it] = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const int ihc = min(max(ih, 0), a.H - 1), iwc = min(max(iw, 0), a.W - 1);
+      v[it] = *(const uint4*)(x + ((long)ihc * a.W + iwc) * a.ldx + c * 8);
+    }
+#pragma unroll
+    for (int it = 0; it < FILL; ++it) {
+      const int t = tid + it * NT;
+      if (t >= CHUNKS) continue;
+      const int pix = t >> 2, c = t & 3;
+      *(uint4*)(patch + pix * PROW + c * 16) = ok[it] ? v[it] : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __syncthreads();
+
+  // 2. conv over the 17x17 window: fragment j = window pixels 16j .. 16j+15
+  int pb[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int p = min(j * 16 + frow, NPX - 1);  // pixels >= 289 are dummies (never pooled)
+    const int wa = p / CW, wb = p - wa * CW;
+    pb[j] = (wa * PW + wb) * PROW + fq * 16;
+  }
+  f32x4 acc[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int toff = ((t / 3) * PW + (t % 3)) * PROW;
+#pragma unroll
+    for (int j0 = 0; j0 < NF; j0 += 4) {  // 4 fragments in flight at a time
+      bf16x8 pf[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (j0 + q < NF) pf[q] = *(const bf16x8*)(patch + pb[j0 + q] + toff);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (j0 + q < NF) acc[j0 + q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t], pf[q], acc[j0 + q], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  __syncthreads();  // every wave done reading the patch: the conv tile reuses it
+
+  // 3. bias + ReLU -> bf16 conv tile (positions outside the conv image -> 0)
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int p = j * 16 + frow;
+    if (p >= NPX) continue;
+    const int wa = p / CW, wb = p - wa * CW;
+    const bool ok = (cy0 + wa < a.H) && (cx0 + wb < a.W);
+    const f32x4 v = acc[j];
+    const float f0 = ok ? fmaxf(v[0] + bias.x, 0.f) : 0.f, f1 = ok ? fmaxf(v[1] + bias.y, 0.f) : 0.f;
+    const float f2 = ok ? fmaxf(v[2] + bias.z, 0.f) : 0.f, f3 = ok ? fmaxf(v[3] + bias.w, 0.f) : 0.f;
+    *(uint2*)(tile + p * TROW + (wid * 16 + fq * 4) * 2) = make_uint2(pack2(f0, f1), pack2(f2, f3));
+  }
+  __syncthreads();
+
+  // 4. max pool 3x3/2 valid: item = (pool pixel, 8-channel group)
+#pragma unroll
+  for (int it = 0; it < PB * PB * 8 / NT; ++it) {
+    const int t = tid + it * NT;
+    const int cg = t & 7, pp = t >> 3;
+    const int ly = pp / PB, lx = pp - ly * PB;
+    const int oy = py0 + ly, ox = px0 + lx;
+    if (oy >= a.Ho || ox >= a.Wo) continue;
+    float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const uint4 v = *(const uint4*)(tile + ((2 * ly + dy) * CW + 2 * lx + dx) * TROW + cg * 16);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], bf_at(v, q));
+      }
+    *(uint4*)((unsigned short*)a.y + ((long)(n * a.Ho + oy) * a.Wo + ox) * a.ldy + cg * 8) =
+        make_uint4(pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7]));
+  }
+}
+
+}  // namespace cpool
+}  // namespace dml
+
+extern "C" int dml_conv3x3_pool(const DmlConvPoolArgs* a, hipStream_t s) {
+  // hard-coded: conv 3x3 stride 1 pad 1, 32 -> 64 channels; max pool 3x3/2 valid
+  if (a->ldx % 8 || a->ldx < 32 || a->ldw % 8 || a->ldw < 288 || a->ldy % 8 || a->ldy < 64 || a->N < 1 ||
+      a->H < 3 || a->W < 3 || a->Ho != (a->H - 3) / 2 + 1 || a->Wo != (a->W - 3) / 2 + 1) {
+    dml_set_error("dml_conv3x3_pool: unsupported shape");
+    return -1;
+  }
+  using namespace dml::cpool;
+  const long blocks = (long)a->N * ((a->Ho + PB - 1) / PB) * ((a->Wo + PB - 1) / PB);
+  hipLaunchKernelGGL(dml::cpool::conv_pool_kernel, dim3((unsigned)blocks), dim3(NT), 0, s, *a);
+  DML_CHECK_LAUNCH();
+  return 0;
+}

@@ -61,7 +61,10 @@ int main() {
     DmlIncStemArgs ist;
     std::memset(&ist, 0, sizeof ist);
     CHECK(dml_plan_add_inc_stem(plan, &ist) == 0);
-    n += 5;
+    DmlConvPoolArgs cp;
+    std::memset(&cp, 0, sizeof cp);
+    CHECK(dml_plan_add_conv_pool(plan, &cp) == 0);
+    n += 6;
     CHECK(dml_plan_size(plan) == n);
     // error paths that must return before any device call
     CHECK(dml_plan_replay(plan, nullptr) != 0);
@@ -120,6 +123,13 @@ int main() {
   CHECK(dml_stem_inception(&ist, nullptr) != 0);  // conv2 weights shorter than K = 288
   ist.ldw2 = 320; ist.H2 = 149;
   CHECK(dml_stem_inception(&ist, nullptr) != 0);  // conv2 size not 3x3 valid of conv1
+  DmlConvPoolArgs cp;
+  std::memset(&cp, 0, sizeof cp);
+  cp.N = 1; cp.H = 147; cp.W = 147; cp.ldx = 32; cp.ldw = 320; cp.Ho = 73; cp.Wo = 73; cp.ldy = 64;
+  cp.ldx = 16;
+  CHECK(dml_conv3x3_pool(&cp, nullptr) != 0);     // fewer than 32 input channels
+  cp.ldx = 32; cp.Wo = 74;
+  CHECK(dml_conv3x3_pool(&cp, nullptr) != 0);     // pool size not 3x3/2 valid of the conv
   dml_set_error(nullptr);
   CHECK(std::string(dml_last_error()).empty());
 

@@ -28,6 +28,7 @@ SOURCES = [
     CSRC / "kernels" / "conv_halo.hip",
     CSRC / "kernels" / "misc.hip",
     CSRC / "kernels" / "stem_fused.hip",
+    CSRC / "kernels" / "conv_pool.hip",
     CSRC / "runtime" / "runtime.hip",
 ]
 HEADERS = [CSRC / "include" / "dml.h", CSRC / "kernels" / "common.h", CSRC / "kernels" / "conv_shared.h"]

@@ -67,7 +67,17 @@ class IncStemArgs(C.Structure):
     ]
 
 
+class ConvPoolArgs(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p), ("w", C.c_void_p), ("bias", C.c_void_p), ("y", C.c_void_p),
+        ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("ldx", C.c_int), ("ldw", C.c_int),
+        ("Ho", C.c_int), ("Wo", C.c_int), ("ldy", C.c_int),
+    ]
+
+
 _SIGS = {
+    "dml_conv3x3_pool": (C.c_int, [C.POINTER(ConvPoolArgs), C.c_void_p]),
+    "dml_plan_add_conv_pool": (C.c_int, [C.c_void_p, C.POINTER(ConvPoolArgs)]),
     "dml_stem_resnet": (C.c_int, [C.POINTER(StemArgs), C.c_void_p]),
     "dml_stem_inception": (C.c_int, [C.POINTER(IncStemArgs), C.c_void_p]),
     "dml_plan_add_inc_stem": (C.c_int, [C.c_void_p, C.POINTER(IncStemArgs)]),

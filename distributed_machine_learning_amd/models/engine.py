@@ -93,6 +93,8 @@ class Engine:
         self.stem_pool = self._fusable_stem_pool(fuse_stem)
         # InceptionV3 stem: preprocess + conv 3x3/2 + conv 3x3 as ONE kernel
         self.stem_conv2 = self._fusable_inception_stem(fuse_stem) if self.stem_pool is None else None
+        # conv 3x3 (32 -> 64) + the 3x3/2 max pool reading it as ONE kernel (csrc/kernels/conv_pool.hip)
+        self.conv_pools = self._fusable_conv_pools(fuse_stem)
         self._src_tensors, self._result_views = src_tensors, result_views
         if share is not None:
             self.wdev, self.whalo = share.wdev, share.whalo
@@ -186,6 +188,24 @@ class Engine:
                 and c.relu and c.residual is None and not c.out_f32 and c.in_coff == 0):
             return None
         return c
+
+    def _fusable_conv_pools(self, enabled: bool) -> Dict[str, Pool]:
+        """{conv name: pool} for 3x3 stride-1 pad-1 convs (32 -> 64 channels, ReLU)
+        whose only consumer is a 3x3/2 valid max pool (InceptionV3 conv2d_3)."""
+        if not enabled or self.device.type != "cuda" or os.environ.get("DML_FUSED_STEM") == "0":
+            return {}
+        out: Dict[str, Pool] = {}
+        for c in self.g.nodes:
+            if not (isinstance(c, Conv) and c is not self.stem and c.kh == c.kw == 3 and c.sh == c.sw == 1
+                    and c.ph == c.pw == 1 and c.cin == 32 and c.cout == 64 and c.relu and c.residual is None
+                    and not c.out_f32 and c.in_coff == 0 and c.out_coff == 0):
+                continue
+            users = [n for n in self.g.nodes if c.out in (getattr(n, "inp", None), getattr(n, "residual", None))]
+            if len(users) == 1 and isinstance(users[0], Pool):
+                p = users[0]
+                if (p.mode, p.k, p.stride, p.pad, p.out_coff, p.relu) == ("max", 3, 2, 0, 0, False):
+                    out[c.name] = p
+        return out
 
     def _halo_eligible(self, n) -> bool:
         return (isinstance(n, Conv) and n is not self.stem and n.sh == 1 and n.sw == 1 and n.kh * n.kw > 1
@@ -336,8 +356,20 @@ class Engine:
                                g.input_hw[0], g.input_hw[1], mode, int(self.stem is not None), self.stem_lpad)
             N.check(L.dml_plan_add_preprocess(plan, C.byref(pa)), "plan preprocess")
             self.op_names.append("preprocess")
+        skip |= {p.name for p in self.conv_pools.values()}
         for n in g.nodes:
             if n.name in skip:
+                continue
+            if n.name in self.conv_pools:
+                p = self.conv_pools[n.name]
+                wk, bias, _, kpad, _ = self.wdev[n.name]
+                h, w, _ = g.shape(n.inp)
+                ho, wo, _ = g.shape(p.out)
+                ca = N.ConvPoolArgs(self.buf[n.inp].data_ptr(), wk.data_ptr(), bias.data_ptr(),
+                                    self.buf[p.out].data_ptr(), B, h, w, self.cbuf[n.inp], kpad, ho, wo,
+                                    self.cbuf[p.out])
+                N.check(L.dml_plan_add_conv_pool(plan, C.byref(ca)), "plan conv+pool")
+                self.op_names.append(f"{n.name}+{p.name}")
                 continue
             if isinstance(n, (Conv, Dense, FusedConv)):
                 cfg = self.cfg_overrides.get(n.name, self.tuned.get(n.name, -1))

@@ -16,7 +16,8 @@ import torch
 from .. import _native as N
 
 __all__ = ["conv2d_nhwc", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight",
-           "pack_weight_halo", "HALO_CFGS", "resnet_stem", "inception_stem"]
+           "pack_weight_halo", "HALO_CFGS", "resnet_stem", "inception_stem",
+           "conv3x3_pool"]
 
 # stride-1 halo-tile conv configs (csrc/kernels/conv_halo.hip); they take
 # chunk-major weights from pack_weight_halo
@@ -197,6 +198,22 @@ def inception_stem(images_u8: torch.Tensor, w1_packed: torch.Tensor, b1: torch.T
                       w1_packed.shape[1], w2_packed.shape[1], h1, w1, h1 - 2, w1 - 2, 32)
     N.check(N.lib().dml_stem_inception(C.byref(a), N.stream_ptr()), "dml_stem_inception")
     out._keep = (b1p, b2p)
+    return out
+
+
+def conv3x3_pool(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """Fused conv 3x3 'same' (32 -> 64 channels, weights [>=64][>=288], K = (r, s, c))
+    + bias + ReLU + max pool 3x3/2 'valid' (csrc/kernels/conv_pool.hip).
+    x: bf16 NHWC [N, H, W, Cbuf >= 32]; returns bf16 NHWC [N, Ho, Wo, 64]."""
+    n, h, w, cbuf = x.shape
+    ho, wo = (h - 3) // 2 + 1, (w - 3) // 2 + 1
+    out = torch.empty((n, ho, wo, 64), device=x.device, dtype=torch.bfloat16)
+    bias_p = bias.to(x.device, torch.float32).contiguous()
+    assert x.is_contiguous() and w_packed.is_contiguous()
+    a = N.ConvPoolArgs(x.data_ptr(), w_packed.data_ptr(), bias_p.data_ptr(), out.data_ptr(), n, h, w, cbuf,
+                       w_packed.shape[1], ho, wo, 64)
+    N.check(N.lib().dml_conv3x3_pool(C.byref(a), N.stream_ptr()), "dml_conv3x3_pool")
+    out._keep = bias_p
     return out
 
 

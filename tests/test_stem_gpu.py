@@ -103,11 +103,29 @@ def test_engine_fused_inception_stem_equals_unfused():
     ef = Engine(g, w, batch=2)
     eu = Engine(g, w, batch=2, fuse_stem=False)
     assert ef.stem_conv2 is not None and eu.stem_conv2 is None
-    assert ef.op_names[0].startswith("preprocess+") and len(ef.op_names) == len(eu.op_names) - 2
+    # the stem conv + conv2d_2 fold into op 0; conv2d_3 + max_pooling2d_1 into one conv+pool op
+    assert ef.op_names[0].startswith("preprocess+") and len(ef.op_names) == len(eu.op_names) - 3
+    assert list(ef.conv_pools.values())[0].out == "stem_pool1"
     ef.infer(imgs)
     eu.infer(imgs)
     torch.cuda.synchronize()
-    name = ef.stem_conv2.out
-    pf, pu = ef.view(name).float(), eu.view(name).float()
-    assert (pf - pu).abs().max().item() <= 1e-2 * pu.abs().max().item()
+    for name in (ef.stem_conv2.out, "stem_pool1"):
+        pf, pu = ef.view(name).float(), eu.view(name).float()
+        assert (pf - pu).abs().max().item() <= 1e-2 * pu.abs().max().item(), name
     assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 5e-2
+
+
+@pytest.mark.parametrize("n,h,w,cbuf", [(2, 147, 147, 32), (1, 20, 23, 32), (1, 9, 9, 40)])
+def test_conv3x3_pool_matches_fp32(n, h, w, cbuf):
+    torch.manual_seed(2)
+    x = _bf(torch.randn(n, cbuf, h, w).clamp(min=0))
+    k = _bf(torch.randn(3, 3, 32, 64) * (2.0 / 288) ** 0.5)
+    b = torch.randn(64) * 0.1
+    conv = _bf(F.relu(F.conv2d(x[:, :32], k.permute(3, 2, 0, 1), b, padding=1)))
+    ref = F.max_pool2d(conv, 3, 2).permute(0, 2, 3, 1)
+    wp = torch.from_numpy(pack_conv_weight(k.numpy(), 32, 256, 320)).to(torch.bfloat16).cuda()
+    y = ops.conv3x3_pool(x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda(), wp, b.cuda())
+    torch.cuda.synchronize()
+    got = y.float().cpu()
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    assert _rel(got, ref) < 1e-2
