@@ -6,8 +6,9 @@
 // A workgroup owns an 8x8 block of pool outputs:
 //  1. the 19x19 x 32-channel input patch the conv window needs (conv pad 1 ->
 //     zeros), 16-B global loads into registers (all issued first, clamped
-//     addresses, padding zeroed after) -> LDS rows of 80 B (64 B + 16-B pad: the
-//     16 lanes of a fragment read hit distinct banks);
+//     addresses, padding zeroed after) -> LDS rows of 96 B (64 B + 32-B pad: the
+//     16 lanes of each ds_read_b128 lane group hit distinct banks; 80-B rows
+//     measured 2-way conflicts, SQ_LDS_BANK_CONFLICT);
 //  2. the 17x17 conv window (289 pixels = 19 MFMA fragments) with
 //     v_mfma_f32_16x16x32_bf16: k-step t = tap (r, s) over 32 channels, one
 //     ds_read_b128 per pixel fragment; wave w owns output channels 16w..16w+15,
@@ -24,9 +25,17 @@ namespace cpool {
 constexpr int PB = 8;                        // pool outputs per block side
 constexpr int CW = 2 * PB + 1;               // conv window 17 x 17
 constexpr int NPX = CW * CW;                 // 289
-constexpr int NF = (NPX + 15) / 16;          // 19 pixel fragments
 constexpr int PW = CW + 2;                   // patch 19 x 19 (conv pad 1)
-constexpr int PROW = 32 * 2 + 16;            // patch pixel row: 32 bf16 + 16-B pad
+// The conv is computed over 17 rows x 19 columns in PATCH pitch (columns 17, 18
+// of each row are junk, never stored): output q' = a*19 + b reads patch pixel
+// q' + r*19 + s, so a fragment's 16 consecutive q' are 16 consecutive patch
+// pixels for every tap — linear addresses (one base register + immediate
+// offsets) and no row-wrap discontinuity, which made some 16-lane groups hit
+// the same banks. +2 fragments of MFMA work buy conflict-free reads.
+constexpr int NQ = CW * PW;                  // 323
+constexpr int NF = (NQ + 15) / 16;           // 21 pixel fragments
+constexpr int PROW = 32 * 2 + 32;            // patch pixel row: 32 bf16 + 32-B pad (96 B: the 16 lanes of
+                                             // every ds_read_b128 lane group hit 16 distinct 4-bank windows)
 constexpr int PATCH_BYTES = PW * PW * PROW;  // 28880
 constexpr int TROW = 64 * 2 + 16;            // conv tile row: 64 bf16 + 16-B pad
 constexpr int TILE_BYTES = NPX * TROW;       // 41616
@@ -89,14 +98,9 @@ __global__ __launch_bounds__(NT, 3) void conv_pool_kernel(DmlConvPoolArgs a) {
   }
   __syncthreads();
 
-  // 2. conv over the 17x17 window: fragment j = window pixels 16j .. 16j+15
-  int pb[NF];
-#pragma unroll
-  for (int j = 0; j < NF; ++j) {
-    const int p = min(j * 16 + frow, NPX - 1);  // pixels >= 289 are dummies (never pooled)
-    const int wa = p / CW, wb = p - wa * CW;
-    pb[j] = (wa * PW + wb) * PROW + fq * 16;
-  }
+  // 2. conv over the window in patch pitch: fragment j = outputs q' = 16j .. 16j+15
+  //    (q' >= 323 read past the patch into the same LDS allocation: junk, never stored)
+  const char* pbase = patch + frow * PROW + fq * 16;
   f32x4 acc[NF];
 #pragma unroll
   for (int j = 0; j < NF; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -108,7 +112,7 @@ __global__ __launch_bounds__(NT, 3) void conv_pool_kernel(DmlConvPoolArgs a) {
       bf16x8 pf[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (j0 + q < NF) pf[q] = *(const bf16x8*)(patch + pb[j0 + q] + toff);
+        if (j0 + q < NF) pf[q] = *(const bf16x8*)(pbase + (j0 + q) * 16 * PROW + toff);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -121,9 +125,10 @@ __global__ __launch_bounds__(NT, 3) void conv_pool_kernel(DmlConvPoolArgs a) {
   // 3. bias + ReLU -> bf16 conv tile (positions outside the conv image -> 0)
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
-    const int p = j * 16 + frow;
-    if (p >= NPX) continue;
-    const int wa = p / CW, wb = p - wa * CW;
+    const int qp = j * 16 + frow;
+    const int wa = qp / PW, wb = qp - wa * PW;
+    if (qp >= NQ || wb >= CW) continue;  // junk columns / dummy outputs
+    const int p = wa * CW + wb;          // conv tile (window) index
     const bool ok = (cy0 + wa < a.H) && (cx0 + wb < a.W);
     const f32x4 v = acc[j];
     const float f0 = ok ? fmaxf(v[0] + bias.x, 0.f) : 0.f, f1 = ok ? fmaxf(v[1] + bias.y, 0.f) : 0.f;
@@ -135,9 +140,12 @@ __global__ __launch_bounds__(NT, 3) void conv_pool_kernel(DmlConvPoolArgs a) {
   // 4. max pool 3x3/2 valid: item = (pool pixel, 8-channel group)
 #pragma unroll
   for (int it = 0; it < PB * PB * 8 / NT; ++it) {
+    // lanes 0-7 / 8-15 of a lane group read pool pixels lx and lx + 4: their conv
+    // pixels are 8 x 144 B apart = 128 B mod 256, so the two 128-B reads never
+    // share a bank (adjacent pool pixels, 288 B apart, overlapped: 2-way conflicts)
     const int t = tid + it * NT;
-    const int cg = t & 7, pp = t >> 3;
-    const int ly = pp / PB, lx = pp - ly * PB;
+    const int cg = t & 7, half = (t >> 3) & 1, pr = t >> 4;
+    const int ly = pr / (PB / 2), lx = pr - ly * (PB / 2) + half * (PB / 2);
     const int oy = py0 + ly, ox = px0 + lx;
     if (oy >= a.Ho || ox >= a.Wo) continue;
     float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};

@@ -184,8 +184,10 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
 
   // 4. max pool 3x3/2 over the tile: item = (pool pixel, 8-channel group)
   for (int t = tid; t < PH * PW * 8; t += NT) {
-    const int cg = t & 7, pp = t >> 3;
-    const int ly = pp / PW, lx = pp - ly * PW;
+    // lanes 0-7 / 8-15 of a lane group read pool pixels lx and lx + 4: conv pixels
+    // 8 x 144 B apart = 128 B mod 256, so their two 128-B reads never share a bank
+    const int cg = t & 7, half = (t >> 3) & 1, pr = t >> 4;
+    const int ly = pr / (PW / 2), lx = pr - ly * (PW / 2) + half * (PW / 2);
     const int oy = py0 + ly, ox = px0 + lx;
     if (oy >= a.Ho || ox >= a.Wo) continue;
     float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
 //  2. conv1 over the 18x18 window under the tile (21 MFMA pixel fragments):
 //     K = 3 rows x 2 pair taps x 8 = 48 (two 32-deep k-steps; the 2 padding
 //     chunks carry zero weights), bias + ReLU -> bf16 into an LDS tile whose
-//     80-B rows keep the conv2 fragment reads bank-conflict free;
+//     96-B rows keep the conv2 fragment reads bank-conflict free;
 //  3. conv2 from that tile: k-step t = tap (r, s) of 32 channels, a pixel
 //     fragment = one tile row of 16 outputs, one ds_read_b128 per fragment;
 //     weights (32 x 288) for both convs stay in VGPRs;
@@ -229,8 +231,8 @@ constexpr int F1 = (NP1 + 15) / 16;          // 21 conv1 pixel fragments
 constexpr int IR = 2 * (R1H - 1) + 3;        // 37 input rows
 constexpr int PQ = R1W + 1;                  // 19 pixel pairs per input row
 constexpr int PATCH_BYTES = IR * PQ * 16;    // 11248
-constexpr int C1ROW = 32 * 2 + 16;           // conv1 tile row (80 B)
-constexpr int C1_BYTES = NP1 * C1ROW;        // 25920
+constexpr int C1ROW = 32 * 2 + 32;           // conv1 tile row (96 B: conflict-free conv2 fragment reads)
+constexpr int C1_BYTES = NP1 * C1ROW;        // 31104
 constexpr int OROW = 32 * 2 + 16;            // output staging row (80 B)
 constexpr int OUT_BYTES = TH * TW * OROW;    // 20480
 constexpr int R0_BYTES = PATCH_BYTES > OUT_BYTES ? PATCH_BYTES : OUT_BYTES;
