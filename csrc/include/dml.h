@@ -157,6 +157,8 @@ int dml_plan_replay(void* plan, hipStream_t s);    // launch the captured graph
 int dml_plan_capture_parts(void* plan, const int* bounds, int nparts, hipStream_t s);
 int dml_plan_replay_part(void* plan, int i, hipStream_t s);
 int dml_plan_time_ops(void* plan, hipStream_t s, float* ms_out, int n);  // per-op hipEvent timing
+int dml_plan_set_cfg(void* plan, int i, int cfg);  // re-point conv op i at config cfg; returns the old one
+int dml_plan_get_cfg(void* plan, int i);
 
 // ---- pinned-host staging ring (csrc/runtime/staging.cpp) ----
 void* dml_ring_create(int slots, size_t slot_bytes);

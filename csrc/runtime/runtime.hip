@@ -219,6 +219,26 @@ extern "C" int dml_plan_replay(void* p, hipStream_t s) {
   return 0;
 }
 
+// Re-point conv op i at tile config cfg (joint tuning of co-scheduled
+// sub-batch plans). Returns the previous cfg, or -1 if op i is not a conv or
+// cfg cannot run it (halo and v2 configs take different weight layouts, so a
+// conv can only move within its family). A captured graph must be re-captured.
+extern "C" int dml_plan_set_cfg(void* p, int i, int cfg) {
+  Plan* pl = (Plan*)p;
+  if (i < 0 || i >= (int)pl->ops.size() || pl->ops[i].kind != OP_CONV) { g_err = "dml_plan_set_cfg: not a conv op"; return -1; }
+  Op& o = pl->ops[i];
+  if ((o.cfg >= 40) != (cfg >= 40) || cfg < 0) { g_err = "dml_plan_set_cfg: config family mismatch"; return -1; }
+  if (cfg >= 40 && dml_conv_halo_ok(&o.conv, cfg) != 0) { g_err = "dml_plan_set_cfg: halo config cannot run this conv"; return -1; }
+  const int prev = o.cfg;
+  o.cfg = cfg;
+  return prev;
+}
+extern "C" int dml_plan_get_cfg(void* p, int i) {
+  Plan* pl = (Plan*)p;
+  if (i < 0 || i >= (int)pl->ops.size() || pl->ops[i].kind != OP_CONV) return -1;
+  return pl->ops[i].cfg;
+}
+
 extern "C" int dml_plan_time_ops(void* p, hipStream_t s, float* ms_out, int n) {
   Plan* pl = (Plan*)p;
   const int cnt = (int)pl->ops.size() < n ? (int)pl->ops.size() : n;

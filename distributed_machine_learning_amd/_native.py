@@ -112,6 +112,8 @@ _SIGS = {
     "dml_plan_capture_parts": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_int, C.c_void_p]),
     "dml_plan_replay_part": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     "dml_plan_time_ops": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_float), C.c_int]),
+    "dml_plan_set_cfg": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "dml_plan_get_cfg": (C.c_int, [C.c_void_p, C.c_int]),
     "dml_ring_create": (C.c_void_p, [C.c_int, C.c_size_t]),
     "dml_ring_destroy": (None, [C.c_void_p]),
     "dml_ring_slot": (C.c_void_p, [C.c_void_p, C.c_int]),
