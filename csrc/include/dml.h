@@ -110,10 +110,26 @@ typedef struct {
   int Ho, Wo, ldy;     // pool output
 } DmlConvPoolArgs;
 
+// Fused ResNet50 stage-2 block boundary (csrc/kernels/bottleneck_fused.hip):
+//   y = relu(w3 . x + b3 + res)  (1x1 expand 64 -> 256 + shortcut)
+//   z = relu(w1 . y + b1)        (next block's 1x1 reduce 256 -> 64)
+typedef struct {
+  const void* x;     // bf16 [M][ldx] (64 channels)
+  const void* w3;    // bf16 [>=256][ldw3], K = 64 used
+  const float* b3;   // fp32 [256]
+  const void* res;   // bf16 [M][ldr] (256 channels)
+  void* y;           // bf16 [M][ldy] (256 channels)
+  const void* w1;    // bf16 [>=64][ldw1], K = 256 used
+  const float* b1;   // fp32 [64]
+  void* z;           // bf16 [M][ldz] (64 channels)
+  int M, ldx, ldw3, ldr, ldy, ldw1, ldz;
+} DmlExpandReduceArgs;
+
 // ---- single-op launches (used by tests and by the plan executor) ----
 int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s);
 int dml_stem_inception(const DmlIncStemArgs* a, hipStream_t s);
 int dml_conv3x3_pool(const DmlConvPoolArgs* a, hipStream_t s);
+int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s);
 int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2_init(void);
@@ -148,6 +164,7 @@ int dml_plan_add_preprocess(void* plan, const DmlPreprocArgs* a);
 int dml_plan_add_stem(void* plan, const DmlStemArgs* a);
 int dml_plan_add_inc_stem(void* plan, const DmlIncStemArgs* a);
 int dml_plan_add_conv_pool(void* plan, const DmlConvPoolArgs* a);
+int dml_plan_add_expand_reduce(void* plan, const DmlExpandReduceArgs* a);
 int dml_plan_size(void* plan);
 int dml_plan_run(void* plan, hipStream_t s);
 int dml_plan_run_range(void* plan, int begin, int end, hipStream_t s);

@@ -42,7 +42,7 @@ extern "C" int dml_device_info(int* cus, int* arch_major, int* arch_minor) {
 
 // ----------------------------------------------------------------- plan ----
 namespace {
-enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM, OP_INC_STEM, OP_CONV_POOL };
+enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM, OP_INC_STEM, OP_CONV_POOL, OP_EXP_RED };
 struct GapArgs { const void* x; void* y; int N, HW, C, ldx; };
 struct SmArgs { float* logits; int B, classes, ld, nsplit, split_ld; float* probs; int* idx; float* p; };
 struct Op {
@@ -56,6 +56,7 @@ struct Op {
   DmlStemArgs stem;
   DmlIncStemArgs istem;
   DmlConvPoolArgs cpool;
+  DmlExpandReduceArgs er;
 };
 struct Plan {
   std::vector<Op> ops;
@@ -88,6 +89,7 @@ int run_op(const Op& o, hipStream_t s) {
     case OP_STEM: return dml_stem_resnet(&o.stem, s);
     case OP_INC_STEM: return dml_stem_inception(&o.istem, s);
     case OP_CONV_POOL: return dml_conv3x3_pool(&o.cpool, s);
+    case OP_EXP_RED: return dml_expand_reduce(&o.er, s);
   }
   return -1;
 }
@@ -156,6 +158,13 @@ extern "C" int dml_plan_add_conv_pool(void* p, const DmlConvPoolArgs* a) {
   Op o{};
   o.kind = OP_CONV_POOL;
   o.cpool = *a;
+  ((Plan*)p)->ops.push_back(o);
+  return 0;
+}
+extern "C" int dml_plan_add_expand_reduce(void* p, const DmlExpandReduceArgs* a) {
+  Op o{};
+  o.kind = OP_EXP_RED;
+  o.er = *a;
   ((Plan*)p)->ops.push_back(o);
   return 0;
 }

@@ -64,7 +64,10 @@ int main() {
     DmlConvPoolArgs cp;
     std::memset(&cp, 0, sizeof cp);
     CHECK(dml_plan_add_conv_pool(plan, &cp) == 0);
-    n += 6;
+    DmlExpandReduceArgs er;
+    std::memset(&er, 0, sizeof er);
+    CHECK(dml_plan_add_expand_reduce(plan, &er) == 0);
+    n += 7;
     CHECK(dml_plan_size(plan) == n);
     // error paths that must return before any device call
     CHECK(dml_plan_replay(plan, nullptr) != 0);
@@ -130,6 +133,13 @@ int main() {
   CHECK(dml_conv3x3_pool(&cp, nullptr) != 0);     // fewer than 32 input channels
   cp.ldx = 32; cp.Wo = 74;
   CHECK(dml_conv3x3_pool(&cp, nullptr) != 0);     // pool size not 3x3/2 valid of the conv
+  DmlExpandReduceArgs er;
+  std::memset(&er, 0, sizeof er);
+  er.M = 100; er.ldx = 64; er.ldw3 = 64; er.ldr = 256; er.ldy = 256; er.ldw1 = 256; er.ldz = 64;
+  er.ldw1 = 128;
+  CHECK(dml_expand_reduce(&er, nullptr) != 0);    // reduce weights shorter than K = 256
+  er.ldw1 = 256; er.ldr = 64;
+  CHECK(dml_expand_reduce(&er, nullptr) != 0);    // shortcut narrower than 256 channels
   dml_set_error(nullptr);
   CHECK(std::string(dml_last_error()).empty());
 

@@ -29,6 +29,7 @@ SOURCES = [
     CSRC / "kernels" / "misc.hip",
     CSRC / "kernels" / "stem_fused.hip",
     CSRC / "kernels" / "conv_pool.hip",
+    CSRC / "kernels" / "bottleneck_fused.hip",
     CSRC / "runtime" / "runtime.hip",
 ]
 HEADERS = [CSRC / "include" / "dml.h", CSRC / "kernels" / "common.h", CSRC / "kernels" / "conv_shared.h"]

@@ -75,7 +75,18 @@ class ConvPoolArgs(C.Structure):
     ]
 
 
+class ExpandReduceArgs(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p), ("w3", C.c_void_p), ("b3", C.c_void_p), ("res", C.c_void_p), ("y", C.c_void_p),
+        ("w1", C.c_void_p), ("b1", C.c_void_p), ("z", C.c_void_p),
+        ("M", C.c_int), ("ldx", C.c_int), ("ldw3", C.c_int), ("ldr", C.c_int), ("ldy", C.c_int),
+        ("ldw1", C.c_int), ("ldz", C.c_int),
+    ]
+
+
 _SIGS = {
+    "dml_expand_reduce": (C.c_int, [C.POINTER(ExpandReduceArgs), C.c_void_p]),
+    "dml_plan_add_expand_reduce": (C.c_int, [C.c_void_p, C.POINTER(ExpandReduceArgs)]),
     "dml_conv3x3_pool": (C.c_int, [C.POINTER(ConvPoolArgs), C.c_void_p]),
     "dml_plan_add_conv_pool": (C.c_int, [C.c_void_p, C.POINTER(ConvPoolArgs)]),
     "dml_stem_resnet": (C.c_int, [C.POINTER(StemArgs), C.c_void_p]),

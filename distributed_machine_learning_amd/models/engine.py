@@ -60,12 +60,14 @@ class Engine:
                  src_hw: Optional[Tuple[int, int]] = None, cfg_overrides: Optional[Dict[str, int]] = None,
                  src_slots: int = 1, reuse_buffers: bool = True, autotune: bool = True, optimize: bool = True,
                  share: Optional["Engine"] = None, src_tensors: Optional[List[torch.Tensor]] = None,
-                 result_views: Optional[List[torch.Tensor]] = None, fuse_stem: bool = True):
+                 result_views: Optional[List[torch.Tensor]] = None, fuse_stem: bool = True,
+                 fuse_blocks: bool = True):
         """``share``: reuse another engine's (optimized) graph and resident weights
         (sub-batch engines of a SplitEngine); ``src_tensors`` / ``result_views``:
         external uint8 source slots / per-slot [2, batch, 5] result rows to use
         instead of allocating them. ``fuse_stem=False`` (or DML_FUSED_STEM=0) keeps the
-        ResNet stem as three launches (preprocess, conv, pool)."""
+        ResNet stem as three launches (preprocess, conv, pool); ``fuse_blocks=False``
+        (or DML_FUSED_BLOCKS=0) keeps every bottleneck 1x1 conv its own launch."""
         if share is not None:
             graph = share.g
         elif optimize:  # graph rewrites: conv-before-avgpool, sibling 1x1 fusion (models/optimize.py)
@@ -95,6 +97,9 @@ class Engine:
         self.stem_conv2 = self._fusable_inception_stem(fuse_stem) if self.stem_pool is None else None
         # conv 3x3 (32 -> 64) + the 3x3/2 max pool reading it as ONE kernel (csrc/kernels/conv_pool.hip)
         self.conv_pools = self._fusable_conv_pools(fuse_stem)
+        # ResNet stage-2 block boundaries: expand (64 -> 256, + shortcut) and the next
+        # block's reduce (256 -> 64) as ONE kernel (csrc/kernels/bottleneck_fused.hip)
+        self.exp_red = self._fusable_expand_reduce(fuse_blocks)
         self._src_tensors, self._result_views = src_tensors, result_views
         if share is not None:
             self.wdev, self.whalo = share.wdev, share.whalo
@@ -207,6 +212,26 @@ class Engine:
                     out[c.name] = p
         return out
 
+    def _fusable_expand_reduce(self, enabled: bool) -> Dict[str, Conv]:
+        """{expand conv name: reduce conv} for adjacent node pairs expand (1x1 s1,
+        64 -> 256, shortcut, ReLU) -> reduce (1x1 s1 reading the expand output,
+        256 -> 64, ReLU) — ResNet50's conv2_blockK_3 / conv2_blockK+1_1."""
+        if not enabled or self.device.type != "cuda" or os.environ.get("DML_FUSED_BLOCKS") == "0":
+            return {}
+        out: Dict[str, Conv] = {}
+        nodes = self.g.nodes
+        for e, r in zip(nodes, nodes[1:]):
+            if not (isinstance(e, Conv) and isinstance(r, Conv)):
+                continue
+            if not (e.kh == e.kw == 1 and e.sh == e.sw == 1 and e.cin == 64 and e.cout == 256 and e.residual
+                    and e.relu and e.in_coff == 0 and e.out_coff == 0 and not e.out_f32):
+                continue
+            if not (r.inp == e.out and r.kh == r.kw == 1 and r.sh == r.sw == 1 and r.cin == 256 and r.cout == 64
+                    and r.relu and r.residual is None and r.in_coff == 0 and r.out_coff == 0 and not r.out_f32):
+                continue
+            out[e.name] = r
+        return out
+
     def _halo_eligible(self, n) -> bool:
         return (isinstance(n, Conv) and n is not self.stem and n.sh == 1 and n.sw == 1 and n.kh * n.kw > 1
                 and self.device.type == "cuda")
@@ -236,6 +261,15 @@ class Engine:
                 if src:
                     last_use[src] = i
         last_use[g.logits] = len(nodes)
+        # A fused pair (first, second) runs as ONE kernel at the first node's
+        # position: the first node's inputs stay live through the second node, so
+        # the second's output can never be handed a buffer the kernel still reads.
+        index = {getattr(n, "name", None): i for i, n in enumerate(nodes)}
+        for first_name, second in {**self.conv_pools, **self.exp_red}.items():
+            first = nodes[index[first_name]]
+            for src in (first.inp, getattr(first, "residual", None)):
+                if src:
+                    last_use[src] = max(last_use[src], index[second.name])
         self.cbuf = {name: _r(t.c, 8) for name, t in g.tensors.items()}
         self.cbuf[g.input] = 8
         self.buf: Dict[str, torch.Tensor] = {}
@@ -357,8 +391,22 @@ class Engine:
             N.check(L.dml_plan_add_preprocess(plan, C.byref(pa)), "plan preprocess")
             self.op_names.append("preprocess")
         skip |= {p.name for p in self.conv_pools.values()}
+        skip |= {r.name for r in self.exp_red.values()}
         for n in g.nodes:
             if n.name in skip:
+                continue
+            if n.name in self.exp_red:
+                r = self.exp_red[n.name]
+                w3, b3, _, kp3, _ = self.wdev[n.name]
+                w1, b1, _, kp1, _ = self.wdev[r.name]
+                h, w, _ = g.shape(n.out)
+                ea = N.ExpandReduceArgs(self.buf[n.inp].data_ptr(), w3.data_ptr(), b3.data_ptr(),
+                                        self.buf[n.residual].data_ptr(), self.buf[n.out].data_ptr(),
+                                        w1.data_ptr(), b1.data_ptr(), self.buf[r.out].data_ptr(), B * h * w,
+                                        self.cbuf[n.inp], kp3, self.cbuf[n.residual], self.cbuf[n.out], kp1,
+                                        self.cbuf[r.out])
+                N.check(L.dml_plan_add_expand_reduce(plan, C.byref(ea)), "plan expand+reduce")
+                self.op_names.append(f"{n.name}+{r.name}")
                 continue
             if n.name in self.conv_pools:
                 p = self.conv_pools[n.name]

@@ -17,7 +17,7 @@ from .. import _native as N
 
 __all__ = ["conv2d_nhwc", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight",
            "pack_weight_halo", "HALO_CFGS", "resnet_stem", "inception_stem",
-           "conv3x3_pool"]
+           "conv3x3_pool", "expand_reduce"]
 
 # stride-1 halo-tile conv configs (csrc/kernels/conv_halo.hip); they take
 # chunk-major weights from pack_weight_halo
@@ -215,6 +215,27 @@ def conv3x3_pool(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor) ->
     N.check(N.lib().dml_conv3x3_pool(C.byref(a), N.stream_ptr()), "dml_conv3x3_pool")
     out._keep = bias_p
     return out
+
+
+def expand_reduce(x: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, res: torch.Tensor, w1: torch.Tensor,
+                  b1: torch.Tensor):
+    """Fused ResNet stage-2 block boundary (csrc/kernels/bottleneck_fused.hip):
+    y = relu(1x1 conv 64 -> 256 of x + b3 + res), z = relu(1x1 conv 256 -> 64 of y + b1).
+    x: bf16 [..., 64]; res: bf16 [..., 256]; w3 [>=256][>=64], w1 [>=64][>=256] packed
+    (pack_weight). Returns (y, z) with x's leading shape."""
+    lead = x.shape[:-1]
+    m = x.numel() // x.shape[-1]
+    y = torch.empty((*lead, 256), device=x.device, dtype=torch.bfloat16)
+    z = torch.empty((*lead, 64), device=x.device, dtype=torch.bfloat16)
+    b3p = b3.to(x.device, torch.float32).contiguous()
+    b1p = b1.to(x.device, torch.float32).contiguous()
+    assert x.is_contiguous() and res.is_contiguous() and w3.is_contiguous() and w1.is_contiguous()
+    a = N.ExpandReduceArgs(x.data_ptr(), w3.data_ptr(), b3p.data_ptr(), res.data_ptr(), y.data_ptr(), w1.data_ptr(),
+                           b1p.data_ptr(), z.data_ptr(), m, x.shape[-1], w3.shape[1], res.shape[-1], 256,
+                           w1.shape[1], 64)
+    N.check(N.lib().dml_expand_reduce(C.byref(a), N.stream_ptr()), "dml_expand_reduce")
+    y._keep = (b3p, b1p)
+    return y, z
 
 
 def fused_conv1x1(x: torch.Tensor, members, stride: int = 1, cfg: int = -1) -> None:

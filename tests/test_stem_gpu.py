@@ -60,8 +60,8 @@ def test_fused_stem_bad_shape_raises():
 def test_engine_fused_stem_equals_unfused():
     g, w = build_model("ResNet50", seed=7, calibrate=True)
     imgs = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda")
-    ef = Engine(g, w, batch=2)
-    eu = Engine(g, w, batch=2, fuse_stem=False)
+    ef = Engine(g, w, batch=2, reuse_buffers=False)
+    eu = Engine(g, w, batch=2, fuse_stem=False, reuse_buffers=False)
     assert ef.stem_pool is not None and eu.stem_pool is None
     assert ef.op_names[0] == "preprocess+conv1_conv+pool1_pool" and len(ef.op_names) == len(eu.op_names) - 2
     ef.infer(imgs)
@@ -100,8 +100,8 @@ def test_fused_inception_stem_matches_fp32(n, hs, ws, out_hw, mode):
 def test_engine_fused_inception_stem_equals_unfused():
     g, w = build_model("InceptionV3", seed=7, calibrate=True)
     imgs = torch.randint(0, 256, (2, 299, 299, 3), dtype=torch.uint8, device="cuda")
-    ef = Engine(g, w, batch=2)
-    eu = Engine(g, w, batch=2, fuse_stem=False)
+    ef = Engine(g, w, batch=2, reuse_buffers=False)
+    eu = Engine(g, w, batch=2, fuse_stem=False, reuse_buffers=False)
     assert ef.stem_conv2 is not None and eu.stem_conv2 is None
     # the stem conv + conv2d_2 fold into op 0; conv2d_3 + max_pooling2d_1 into one conv+pool op
     assert ef.op_names[0].startswith("preprocess+") and len(ef.op_names) == len(eu.op_names) - 3
@@ -129,3 +129,48 @@ def test_conv3x3_pool_matches_fp32(n, h, w, cbuf):
     got = y.float().cpu()
     assert got.shape == ref.shape, (got.shape, ref.shape)
     assert _rel(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("m", [64 * 7, 1000, 3 * 56 * 56])
+def test_expand_reduce_matches_fp32(m):
+    torch.manual_seed(3)
+    x = _bf(torch.randn(m, 64).clamp(min=0))
+    res = _bf(torch.randn(m, 256))
+    w3 = _bf(torch.randn(256, 64) * (2.0 / 64) ** 0.5)
+    b3 = torch.randn(256) * 0.1
+    w1 = _bf(torch.randn(64, 256) * (2.0 / 256) ** 0.5)
+    b1 = torch.randn(64) * 0.1
+    y_ref = _bf(F.relu(x @ w3.T + b3 + res))  # the engine's rounding point
+    z_ref = F.relu(y_ref @ w1.T + b1)
+    w3p = torch.zeros(256, 64)
+    w3p[:, :] = w3
+    w1p = torch.zeros(256, 256)
+    w1p[:64] = w1
+    y, z = ops.expand_reduce(x.to(torch.bfloat16).cuda(), w3p.to(torch.bfloat16).cuda(), b3.cuda(),
+                             res.to(torch.bfloat16).cuda(), w1p.to(torch.bfloat16).cuda(), b1.cuda())
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu(), y_ref) < 1e-2
+    assert _rel(z.float().cpu(), z_ref) < 1e-2
+
+
+def test_engine_fused_blocks_equal_unfused():
+    g, w = build_model("ResNet50", seed=8, calibrate=True)
+    imgs = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda")
+    # no buffer recycling: intermediate tensors are compared after the whole forward
+    ef = Engine(g, w, batch=2, reuse_buffers=False)
+    eu = Engine(g, w, batch=2, fuse_blocks=False, reuse_buffers=False)
+    assert sorted(ef.exp_red) == ["conv2_block1_3_conv", "conv2_block2_3_conv"] and not eu.exp_red
+    assert len(ef.op_names) == len(eu.op_names) - 2
+    # the fused kernel writes the reduce output while reading the expand inputs: never
+    # aliased, also under liveness-based buffer recycling
+    er = Engine(g, w, batch=2)
+    for e_name, r in er.exp_red.items():
+        e = next(n for n in er.g.nodes if n.name == e_name)
+        assert er.buf[r.out].data_ptr() not in (er.buf[e.inp].data_ptr(), er.buf[e.residual].data_ptr())
+    ef.infer(imgs)
+    eu.infer(imgs)
+    torch.cuda.synchronize()
+    for name in ("conv2_block1_out", "conv2_block2_1", "conv2_block3_1", "conv2_block3_out"):
+        pf, pu = ef.view(name).float(), eu.view(name).float()
+        assert (pf - pu).abs().max().item() <= 2e-2 * pu.abs().max().item(), name
+    assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 5e-2
