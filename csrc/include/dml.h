@@ -110,19 +110,20 @@ typedef struct {
   int Ho, Wo, ldy;     // pool output
 } DmlConvPoolArgs;
 
-// Fused ResNet50 stage-2 block boundary (csrc/kernels/bottleneck_fused.hip):
-//   y = relu(w3 . x + b3 + res)  (1x1 expand 64 -> 256 + shortcut)
-//   z = relu(w1 . y + b1)        (next block's 1x1 reduce 256 -> 64)
+// Fused ResNet50 block boundary (csrc/kernels/bottleneck_fused.hip), F = C / 4:
+//   y = relu(w3 . x + b3 + res)  (1x1 expand F -> C + shortcut)
+//   z = relu(w1 . y + b1)        (next block's 1x1 reduce C -> F)
 typedef struct {
-  const void* x;     // bf16 [M][ldx] (64 channels)
-  const void* w3;    // bf16 [>=256][ldw3], K = 64 used
-  const float* b3;   // fp32 [256]
-  const void* res;   // bf16 [M][ldr] (256 channels)
-  void* y;           // bf16 [M][ldy] (256 channels)
-  const void* w1;    // bf16 [>=64][ldw1], K = 256 used
-  const float* b1;   // fp32 [64]
-  void* z;           // bf16 [M][ldz] (64 channels)
+  const void* x;     // bf16 [M][ldx] (F channels)
+  const void* w3;    // bf16 [>=C][ldw3], K = F used
+  const float* b3;   // fp32 [C]
+  const void* res;   // bf16 [M][ldr] (C channels)
+  void* y;           // bf16 [M][ldy] (C channels)
+  const void* w1;    // bf16 [>=F][ldw1], K = C used
+  const float* b1;   // fp32 [F]
+  void* z;           // bf16 [M][ldz] (F channels)
   int M, ldx, ldw3, ldr, ldy, ldw1, ldz;
+  int C;             // expand width: 256, 512 or 1024 (reduce width F = C / 4)
 } DmlExpandReduceArgs;
 
 // ---- single-op launches (used by tests and by the plan executor) ----
@@ -130,6 +131,7 @@ int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s);
 int dml_stem_inception(const DmlIncStemArgs* a, hipStream_t s);
 int dml_conv3x3_pool(const DmlConvPoolArgs* a, hipStream_t s);
 int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s);
+int dml_expand_reduce_init(void);
 int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2_init(void);

@@ -293,6 +293,7 @@ extern "C" int dml_conv_v2_init(void) {
   rc |= set_attr<128, 32, 2, 1, 3, 32>();
   rc |= set_attr<256, 32, 4, 1, 3, 64>();
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  if (!rc && dml_expand_reduce_init() != 0) return -1;  // fused block-boundary kernels (bottleneck_fused.hip)
   return rc ? -1 : 0;
 }
 

@@ -135,6 +135,10 @@ int main() {
   CHECK(dml_conv3x3_pool(&cp, nullptr) != 0);     // pool size not 3x3/2 valid of the conv
   DmlExpandReduceArgs er;
   std::memset(&er, 0, sizeof er);
+  er.C = 128;
+  er.M = 100; er.ldx = 64; er.ldw3 = 64; er.ldr = 256; er.ldy = 256; er.ldw1 = 256; er.ldz = 64;
+  CHECK(dml_expand_reduce(&er, nullptr) != 0);    // expand width not 256 / 512 / 1024
+  er.C = 256;
   er.M = 100; er.ldx = 64; er.ldw3 = 64; er.ldr = 256; er.ldy = 256; er.ldw1 = 256; er.ldz = 64;
   er.ldw1 = 128;
   CHECK(dml_expand_reduce(&er, nullptr) != 0);    // reduce weights shorter than K = 256

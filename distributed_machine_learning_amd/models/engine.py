@@ -214,19 +214,24 @@ class Engine:
 
     def _fusable_expand_reduce(self, enabled: bool) -> Dict[str, Conv]:
         """{expand conv name: reduce conv} for adjacent node pairs expand (1x1 s1,
-        64 -> 256, shortcut, ReLU) -> reduce (1x1 s1 reading the expand output,
-        256 -> 64, ReLU) — ResNet50's conv2_blockK_3 / conv2_blockK+1_1."""
+        F -> C, shortcut, ReLU) -> reduce (1x1 s1 reading the expand output, C -> F,
+        ReLU), F = C / 4 — ResNet50's convN_blockK_3 / convN_blockK+1_1. The kernel
+        supports C in {256, 512, 1024}; only C = 256 (stage 2) beats the two separate
+        launches (bottleneck_fused.hip header), so DML_FUSED_BLOCKS_MAXC defaults to 256."""
         if not enabled or self.device.type != "cuda" or os.environ.get("DML_FUSED_BLOCKS") == "0":
             return {}
+        maxc = int(os.environ.get("DML_FUSED_BLOCKS_MAXC", "256"))
         out: Dict[str, Conv] = {}
         nodes = self.g.nodes
         for e, r in zip(nodes, nodes[1:]):
             if not (isinstance(e, Conv) and isinstance(r, Conv)):
                 continue
-            if not (e.kh == e.kw == 1 and e.sh == e.sw == 1 and e.cin == 64 and e.cout == 256 and e.residual
+            if not (e.kh == e.kw == 1 and e.sh == e.sw == 1 and e.cout in (256, 512, 1024) and e.cout <= maxc
+                    and e.cin * 4 == e.cout and e.residual
                     and e.relu and e.in_coff == 0 and e.out_coff == 0 and not e.out_f32):
                 continue
-            if not (r.inp == e.out and r.kh == r.kw == 1 and r.sh == r.sw == 1 and r.cin == 256 and r.cout == 64
+            if not (r.inp == e.out and r.kh == r.kw == 1 and r.sh == r.sw == 1 and r.cin == e.cout
+                    and r.cout == e.cin
                     and r.relu and r.residual is None and r.in_coff == 0 and r.out_coff == 0 and not r.out_f32):
                 continue
             out[e.name] = r
@@ -404,7 +409,7 @@ class Engine:
                                         self.buf[n.residual].data_ptr(), self.buf[n.out].data_ptr(),
                                         w1.data_ptr(), b1.data_ptr(), self.buf[r.out].data_ptr(), B * h * w,
                                         self.cbuf[n.inp], kp3, self.cbuf[n.residual], self.cbuf[n.out], kp1,
-                                        self.cbuf[r.out])
+                                        self.cbuf[r.out], n.cout)
                 N.check(L.dml_plan_add_expand_reduce(plan, C.byref(ea)), "plan expand+reduce")
                 self.op_names.append(f"{n.name}+{r.name}")
                 continue

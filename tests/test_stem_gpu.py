@@ -131,36 +131,40 @@ def test_conv3x3_pool_matches_fp32(n, h, w, cbuf):
     assert _rel(got, ref) < 1e-2
 
 
-@pytest.mark.parametrize("m", [64 * 7, 1000, 3 * 56 * 56])
-def test_expand_reduce_matches_fp32(m):
+@pytest.mark.parametrize("c,m", [(256, 64 * 7), (256, 1000), (256, 3 * 56 * 56), (512, 1000), (512, 2 * 28 * 28),
+                                 (1024, 999), (1024, 2 * 14 * 14)])
+def test_expand_reduce_matches_fp32(c, m):
     torch.manual_seed(3)
-    x = _bf(torch.randn(m, 64).clamp(min=0))
-    res = _bf(torch.randn(m, 256))
-    w3 = _bf(torch.randn(256, 64) * (2.0 / 64) ** 0.5)
-    b3 = torch.randn(256) * 0.1
-    w1 = _bf(torch.randn(64, 256) * (2.0 / 256) ** 0.5)
-    b1 = torch.randn(64) * 0.1
+    f = c // 4
+    x = _bf(torch.randn(m, f).clamp(min=0))
+    res = _bf(torch.randn(m, c))
+    w3 = _bf(torch.randn(c, f) * (2.0 / f) ** 0.5)
+    b3 = torch.randn(c) * 0.1
+    w1 = _bf(torch.randn(f, c) * (2.0 / c) ** 0.5)
+    b1 = torch.randn(f) * 0.1
     y_ref = _bf(F.relu(x @ w3.T + b3 + res))  # the engine's rounding point
     z_ref = F.relu(y_ref @ w1.T + b1)
-    w3p = torch.zeros(256, 64)
-    w3p[:, :] = w3
-    w1p = torch.zeros(256, 256)
-    w1p[:64] = w1
-    y, z = ops.expand_reduce(x.to(torch.bfloat16).cuda(), w3p.to(torch.bfloat16).cuda(), b3.cuda(),
+    w1p = torch.zeros(max(f, 64), c)  # packed weights: rows padded like pack_weight
+    w1p[:f] = w1
+    y, z = ops.expand_reduce(x.to(torch.bfloat16).cuda(), w3.to(torch.bfloat16).cuda(), b3.cuda(),
                              res.to(torch.bfloat16).cuda(), w1p.to(torch.bfloat16).cuda(), b1.cuda())
     torch.cuda.synchronize()
     assert _rel(y.float().cpu(), y_ref) < 1e-2
     assert _rel(z.float().cpu(), z_ref) < 1e-2
 
 
-def test_engine_fused_blocks_equal_unfused():
+@pytest.mark.parametrize("maxc,pairs", [(256, 2), (1024, 10)])
+def test_engine_fused_blocks_equal_unfused(maxc, pairs, monkeypatch):
+    monkeypatch.setenv("DML_FUSED_BLOCKS_MAXC", str(maxc))
     g, w = build_model("ResNet50", seed=8, calibrate=True)
     imgs = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda")
     # no buffer recycling: intermediate tensors are compared after the whole forward
     ef = Engine(g, w, batch=2, reuse_buffers=False)
     eu = Engine(g, w, batch=2, fuse_blocks=False, reuse_buffers=False)
-    assert sorted(ef.exp_red) == ["conv2_block1_3_conv", "conv2_block2_3_conv"] and not eu.exp_red
-    assert len(ef.op_names) == len(eu.op_names) - 2
+    # stage 2: 2 block boundaries, stage 3: 3, stage 4: 5 (stage 5, C = 2048, is not fused)
+    assert sorted(ef.exp_red) == sorted([f"conv{s}_block{k}_3_conv" for s, nb in ((2, 3), (3, 4), (4, 6))
+                                         for k in range(1, nb)][:pairs]) and not eu.exp_red
+    assert len(ef.op_names) == len(eu.op_names) - pairs
     # the fused kernel writes the reduce output while reading the expand inputs: never
     # aliased, also under liveness-based buffer recycling
     er = Engine(g, w, batch=2)
@@ -170,7 +174,8 @@ def test_engine_fused_blocks_equal_unfused():
     ef.infer(imgs)
     eu.infer(imgs)
     torch.cuda.synchronize()
-    for name in ("conv2_block1_out", "conv2_block2_1", "conv2_block3_1", "conv2_block3_out"):
+    for name in ("conv2_block1_out", "conv2_block2_1", "conv2_block3_1", "conv2_block3_out", "conv3_block2_1",
+                 "conv3_block4_out", "conv4_block2_1", "conv4_block6_1", "conv4_block6_out"):
         pf, pu = ef.view(name).float(), eu.view(name).float()
         assert (pf - pu).abs().max().item() <= 2e-2 * pu.abs().max().item(), name
     assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 5e-2
