@@ -15,7 +15,10 @@
 // 157 us vs 63 us — every workgroup re-reads both weight matrices (C^2 bytes,
 // 3-6x its activation bytes at BM = 32) and the phase-serialised workgroup runs
 // at 1-2 waves/SIMD, so those stay opt-in (DML_FUSED_BLOCKS_MAXC). BM = 32 / 128
-// for C = 256 measured 175 us.
+// for C = 256 measured 175 us. An epilogue straight from the MFMA layout (no fp32
+// staging tile, one barrier, 8-B residual loads / Y stores of 4 channels per lane)
+// measured 176-182 us vs 131-135 us: the 32-B-per-pixel access pattern costs more
+// than the staging round trip (profiles/r1_v11/op_times_direct_epilogue.json).
 //  1. expand: the wave's 64-channel x BM-pixel tile, K = F, W3 and T fragments
 //     loaded straight from global into VGPRs (no LDS ring: one pass over K); the
 //     shortcut rows are prefetched first (16-B loads, one 8-channel group per
