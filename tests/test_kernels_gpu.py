@@ -160,6 +160,25 @@ def test_pool(mode, k, s, pad):
     assert _rel(y.float().cpu().permute(0, 3, 1, 2), ref) < 1e-2
 
 
+@pytest.mark.parametrize("mode,k,s,pad,hw", [("max", 3, 2, 1, (9, 6)), ("max", 3, 1, 1, (5, 7)), ("max", 3, 2, 0, (71, 71)),
+                                             ("avg", 3, 2, 1, (9, 6)), ("avg", 3, 1, 1, (1, 2)),
+                                             ("max", 5, 2, 2, (9, 9)), ("avg", 5, 1, 2, (6, 5))])
+def test_pool_signed(mode, k, s, pad, hw):
+    """Signed inputs (padding must never win a max), edge windows, 1-pixel images; the
+    k = 3 / pad <= 1 cases run the all-taps-in-flight kernel, k = 5 the generic one."""
+    torch.manual_seed(5)
+    x = _bf(torch.randn(3, 48, *hw))
+    if mode == "max":
+        ref = F.max_pool2d(F.pad(x, (pad,) * 4, value=float("-inf")), k, s)
+    else:
+        ref = F.avg_pool2d(x, k, s, padding=pad, count_include_pad=False)
+    y = ops.pool3x3(x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16), mode, k, s, pad)
+    torch.cuda.synchronize()
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    assert got.shape == ref.shape
+    assert _rel(got, ref) < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(3, 7, 7, 2048), (2, 8, 8, 2048), (5, 3, 5, 200), (1, 1, 1, 8)])
 def test_global_avgpool(shape):
     x = _bf(torch.randn(*shape))
