@@ -48,6 +48,11 @@ typedef struct {
   // consumer sums the slices (dml_softmax_top5_split does, for the classifier).
   int ksplit;
   int split_ld;
+  // Subsampled residual (v2/halo kernels only; 0/1 = off): output pixel
+  // (n, ho, wo) adds res pixel n*rHW + (ho*rW + wo)*rsub — the shortcut read at
+  // stride rsub from its full-resolution grid (rW = its width, rHW = H*W), used
+  // when a stride-2 consumer has been pushed up into the block (models/optimize.py).
+  int rsub, rW, rHW;
 } DmlConvArgs;
 
 typedef struct {

@@ -246,14 +246,18 @@ extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
       dml_set_error("dml_conv(v2): nseg must be 0..4");
       return -1;
     }
+    if (a->rsub > 1 && (!a->res || a->rW < a->Wo * a->rsub || a->rHW < a->rW * a->Ho * a->rsub)) {
+      dml_set_error("dml_conv(v2): subsampled residual needs res and rW >= Wo*rsub, rHW >= rW*Ho*rsub");
+      return -1;
+    }
     if (a->ksplit > 1 && (cfg >= 40 || !a->out_f32 || a->res || a->nseg || a->relu || a->split_ld < 1)) {
       dml_set_error("dml_conv(v2): split-K needs a v2 config, fp32 output, no residual/segments/ReLU, split_ld");
       return -1;
     }
     return cfg >= 40 ? dml_conv_halo(a, cfg, s) : dml_conv_v2(a, cfg, s);
   }
-  if (a->nseg > 0 || a->ksplit > 1) {
-    dml_set_error("dml_conv: output segments / split-K need a v2 config (cfg >= 10)");
+  if (a->nseg > 0 || a->ksplit > 1 || a->rsub > 1) {
+    dml_set_error("dml_conv: output segments / split-K / subsampled residual need a v2 config (cfg >= 10)");
     return -1;
   }
   if (a->Cin % 8 || a->ldx % 8 || a->Cout % 4 || a->Kpad % 64) {

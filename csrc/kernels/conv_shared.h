@@ -93,7 +93,14 @@ struct Epilogue {
 #pragma unroll
       for (int it = 0; it < EIT; ++it) {
         const int m = m0 + (tid + it * NT) / CG;
-        rpre[it] = (ch_ok && m < M) ? *(const uint4*)(rg + (long)m * a.ldr + ch_t) : make_uint4(0, 0, 0, 0);
+        long rp = m;
+        if (a.rsub > 1) {  // shortcut read at stride rsub on its full-resolution grid
+          const int hw = a.Ho * a.Wo;
+          const int ni = m / hw, r = m - ni * hw;
+          const int ho = r / a.Wo, wo = r - ho * a.Wo;
+          rp = (long)ni * a.rHW + ((long)ho * a.rW + wo) * a.rsub;
+        }
+        rpre[it] = (ch_ok && m < M) ? *(const uint4*)(rg + rp * a.ldr + ch_t) : make_uint4(0, 0, 0, 0);
       }
     }
   }

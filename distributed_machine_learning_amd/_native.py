@@ -29,6 +29,7 @@ class ConvArgs(C.Structure):
         ("nseg", C.c_int), ("seg_c0", C.c_int * 4), ("seg_ldy", C.c_int * 4), ("seg_relu", C.c_int * 4),
         ("seg_y", C.c_void_p * 4),
         ("ksplit", C.c_int), ("split_ld", C.c_int),
+        ("rsub", C.c_int), ("rW", C.c_int), ("rHW", C.c_int),
     ]
 
 

@@ -73,7 +73,7 @@ class Engine:
         elif optimize:  # graph rewrites: conv-before-avgpool, sibling 1x1 fusion (models/optimize.py)
             from .optimize import optimize as _opt
 
-            graph = _opt(graph)
+            graph = _opt(graph, stride_push=os.environ.get("DML_STRIDE_PUSH") != "0")
         self.g, self.batch, self.device = graph, batch, torch.device(device)
         self.src_slots = src_slots
         self.reuse_buffers = reuse_buffers
@@ -227,7 +227,7 @@ class Engine:
             if not (isinstance(e, Conv) and isinstance(r, Conv)):
                 continue
             if not (e.kh == e.kw == 1 and e.sh == e.sw == 1 and e.cout in (256, 512, 1024) and e.cout <= maxc
-                    and e.cin * 4 == e.cout and e.residual
+                    and e.cin * 4 == e.cout and e.residual and e.res_sub == 1
                     and e.relu and e.in_coff == 0 and e.out_coff == 0 and not e.out_f32):
                 continue
             if not (r.inp == e.out and r.kh == r.kw == 1 and r.sh == r.sw == 1 and r.cin == e.cout
@@ -488,9 +488,13 @@ class Engine:
         kw, pw, dw, ldx = n.kw, n.pw, 1, self.cbuf[n.inp]
         if n is self.stem:  # pair-packed input: physical col = logical col + lpad, 2 taps per chunk
             kw, pw, dw, w, ldx = (n.kw + 1) // 2, n.pw - self.stem_lpad, 2, w + self.stem_lpad, 8
-        return N.ConvArgs(x, wk.data_ptr(), bias.data_ptr(), res, y, B, h, w, cin_eff, ldx,
-                          n.kh, kw, n.sh, n.sw, n.ph, pw, ho, wo, n.cout, K, kpad,
-                          self.cbuf[n.out], ldr, int(n.relu), int(n.out_f32), 1, dw)
+        a = N.ConvArgs(x, wk.data_ptr(), bias.data_ptr(), res, y, B, h, w, cin_eff, ldx,
+                       n.kh, kw, n.sh, n.sw, n.ph, pw, ho, wo, n.cout, K, kpad,
+                       self.cbuf[n.out], ldr, int(n.relu), int(n.out_f32), 1, dw)
+        if n.residual and n.res_sub > 1:  # shortcut read at stride res_sub (models/optimize.py)
+            rh, rw, _ = g.shape(n.residual)
+            a.rsub, a.rW, a.rHW = n.res_sub, rw, rh * rw
+        return a
 
     # ---------------------------------------------------------------- run ----
     def run(self, stream=None, use_graph: bool = False, slot: int = 0) -> None:

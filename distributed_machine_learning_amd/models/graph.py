@@ -52,6 +52,7 @@ class Conv:
     relu: bool = True
     residual: Optional[str] = None  # tensor added before the ReLU (ResNet shortcut)
     out_f32: bool = False
+    res_sub: int = 1           # residual read at this stride from its full-resolution grid
 
 
 @dataclass
@@ -172,7 +173,8 @@ class Graph:
                 ew = (w + 2 * n.pw - n.kw) // n.sw + 1
                 assert (eh, ew) == (ho, wo), f"{n.name}: spatial {(eh, ew)} != {(ho, wo)}"
                 if n.residual:
-                    assert n.residual in produced and self.shape(n.residual)[:2] == (ho, wo), n.name
+                    rs = n.res_sub
+                    assert n.residual in produced and self.shape(n.residual)[:2] == (ho * rs, wo * rs), n.name
             elif isinstance(n, Pool):
                 h, w, c = self.shape(n.inp)
                 ho, wo, co = self.shape(n.out)

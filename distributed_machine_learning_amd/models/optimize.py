@@ -14,7 +14,18 @@
    segment to its own destination (concat buffer at an offset, or a temporary).
    One read of the input, one launch, wider N.
 
-Both rewrites keep the weights dict unchanged (members keep their names); the
+3. ``push_stride_up`` — a tensor whose EVERY consumer is a 1x1 stride-2 conv
+   (ResNet50's stage-boundary shortcut + first reduce, conv{3,4,5}_block1_{0,1},
+   reading conv{2,3,4}_blockK_out) only ever has its even pixels read. The
+   producer then only computes those: a 1x1 s1 producer becomes 1x1 s2 (its own
+   input gets the same treatment next iteration) and a 'same'-padded k x k s1
+   producer becomes k x k s2 with the same top/left padding (output (i, j) reads
+   rows 2i-p..2i+p, exactly the s1 conv's even outputs). The consumers become s1
+   and the producer's shortcut is read at stride 2 (``Conv.res_sub``). For
+   ResNet50 this removes 3/4 of the work of each stage's last 1x1 expand and
+   3x3 conv (and 3/4 of their activation traffic) at three stage boundaries.
+
+All rewrites keep the weights dict unchanged (members keep their names); the
 fp32 oracle can execute the rewritten graph too (tests compare both forms).
 """
 from __future__ import annotations
@@ -23,7 +34,7 @@ import copy
 from dataclasses import replace
 from typing import Dict, List
 
-from .graph import Conv, FusedConv, Graph, Pool, node_outputs
+from .graph import Conv, FusedConv, Graph, Pool, Tensor, node_outputs
 
 
 def _consumers(g: Graph) -> Dict[str, List[object]]:
@@ -96,7 +107,39 @@ def fuse_sibling_1x1(g: Graph, max_members: int = 4) -> Graph:
     return g
 
 
-def optimize(g: Graph, pool_reorder: bool = True, fuse: bool = True) -> Graph:
+def push_stride_up(g: Graph) -> Graph:
+    g = copy.deepcopy(g)
+    while True:
+        cons = _consumers(g)
+        prod = {o: n for n in g.nodes for o in node_outputs(n)}
+        for tname, users in cons.items():
+            p = prod.get(tname)
+            if tname in (g.input, g.logits) or not isinstance(p, Conv) or p.out_coff or p.out_f32:
+                continue
+            h, w, c = g.shape(tname)
+            if h % 2 or w % 2 or c != p.cout or p.sh != 1 or p.sw != 1 or p.res_sub != 1:
+                continue
+            if not all(isinstance(u, Conv) and u.inp == tname and u.residual != tname and u.kh == u.kw == 1
+                       and u.sh == u.sw == 2 and u.ph == u.pw == 0 for u in users):
+                continue
+            if not (p.kh % 2 and p.kw % 2 and p.ph == p.kh // 2 and p.pw == p.kw // 2):
+                continue  # only 'same'-padded odd kernels keep the even outputs at stride 2
+            p.sh = p.sw = 2
+            if p.residual:
+                p.res_sub = 2
+            g.tensors[tname] = Tensor(tname, h // 2, w // 2, c)
+            for u in users:
+                u.sh = u.sw = 1
+            break
+        else:
+            break
+    g.validate()
+    return g
+
+
+def optimize(g: Graph, pool_reorder: bool = True, fuse: bool = True, stride_push: bool = True) -> Graph:
+    if stride_push:
+        g = push_stride_up(g)
     if pool_reorder:
         g = conv_before_avgpool(g)
     if fuse:

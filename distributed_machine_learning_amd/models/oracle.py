@@ -90,7 +90,7 @@ class OracleExecutor:
                     if c.bn:
                         y = self._bn(c, y)
                 if c.residual:
-                    y = y + t[c.residual]
+                    y = y + t[c.residual][:, :, ::c.res_sub, ::c.res_sub]
                 if c.relu:
                     y = F.relu(y)
                 self._write(t, c.out, rnd(y), c.out_coff, n_img)
@@ -149,7 +149,7 @@ def calibrate_bn(g: Graph, w: Weights, x: torch.Tensor) -> Weights:
                 p[f"{n.name}/mean"], p[f"{n.name}/var"] = mean, var
                 y = ex._bn(n, y)
             if n.residual:
-                y = y + t[n.residual]
+                y = y + t[n.residual][:, :, ::n.res_sub, ::n.res_sub]
             if n.relu:
                 y = F.relu(y)
             ex._write(t, n.out, y, n.out_coff, n_img)

@@ -101,6 +101,10 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
                    dilation[0], dilation[1])
     if parts is not None:
         a.ksplit, a.split_ld = ksplit, out.numel()
+    if residual is not None and residual.shape[1] != ho:  # shortcut read at stride rs (full-res grid)
+        rs = residual.shape[1] // ho
+        assert residual.shape[1] == ho * rs and residual.shape[2] == wo * rs and residual.is_contiguous()
+        a.rsub, a.rW, a.rHW = rs, residual.shape[2], residual.shape[1] * residual.shape[2]
     L = N.lib()
     if cfg < 0:
         cfg = L.dml_conv_pick_cfg(C.byref(a))

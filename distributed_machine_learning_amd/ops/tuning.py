@@ -36,6 +36,7 @@ def shape_key(a: N.ConvArgs, halo: bool = False) -> str:
     return (f"n{a.N}_h{a.H}_w{a.W}_c{a.Cin}_ld{a.ldx}_k{a.kh}x{a.kw}_s{a.sh}x{a.sw}_p{a.ph}x{a.pw}"
             f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}_d{max(a.dh, 1)}x{max(a.dw, 1)}"
             + (f"_ks{a.ksplit}" if a.ksplit > 1 else "")
+            + (f"_rs{a.rsub}" if a.rsub > 1 else "")
             + ("_halo" if halo else "") + "_" + CAND_TAG)
 
 

@@ -339,3 +339,34 @@ def test_halo_concat_offsets():
     ref = F.relu(F.conv2d(x[:, 32:96], wt, b, padding=1))
     assert _rel(got[:, 32:128], ref) < 1.5e-2
     assert torch.all(got[:, :32] == 7.0)
+
+
+@pytest.mark.parametrize("cfg", [10, 11, 12, 13, 14, 15, 16, 17, 18, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33,
+                                 34, 36, 37])
+@pytest.mark.parametrize("case", [(2, 28, 28, 64, 256, 1, 1), (2, 14, 10, 128, 512, 1, 1), (2, 7, 9, 64, 64, 3, 3)])
+def test_conv_subsampled_residual(case, cfg):
+    """Residual read at stride 2 from its full-resolution grid (rsub = 2: the
+    epilogue of a block whose stride-2 consumer was pushed up, models/optimize.py)."""
+    n, ho, wo, cin, cout, kh, kw = case
+    torch.manual_seed(1)
+    x = _bf(torch.randn(n, cin, ho, wo))
+    wt = _bf(torch.randn(cout, cin, kh, kw) * (2.0 / (cin * kh * kw)) ** 0.5)
+    b = torch.randn(cout) * 0.1
+    res = _bf(torch.randn(n, cout, 2 * ho, 2 * wo))
+    ref = F.relu(F.conv2d(x, wt, b, padding=(kh // 2, kw // 2)) + res[:, :, ::2, ::2])
+    wp, K, _ = ops.pack_weight(wt)
+    xd = x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
+    rd = res.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
+    y = ops.conv2d_nhwc(xd, wp.cuda(), b.cuda(), cout, kh, kw, (1, 1), (kh // 2, kw // 2), relu=True, residual=rd,
+                        cfg=cfg)
+    torch.cuda.synchronize()
+    got = y[..., :cout].float().cpu().permute(0, 3, 1, 2)
+    assert _rel(got, ref) < 1.5e-2, _rel(got, ref)
+
+
+def test_conv_subsampled_residual_v1_refused():
+    x = torch.zeros(1, 4, 4, 64, device="cuda", dtype=torch.bfloat16)
+    wp, _, _ = ops.pack_weight(torch.zeros(64, 64, 1, 1))
+    rd = torch.zeros(1, 8, 8, 64, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(Exception):
+        ops.conv2d_nhwc(x, wp.cuda(), torch.zeros(64), 64, 1, 1, residual=rd, cfg=0)

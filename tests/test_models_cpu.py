@@ -135,3 +135,29 @@ def test_graph_rewrites_exact_in_fp32():
         a = OracleExecutor(g, w).forward(x)["logits"]
         b = OracleExecutor(go, w).forward(x)["logits"]
         assert ((a - b).abs().max() / a.abs().max()).item() < 1e-4
+
+
+def test_stride_pushdown_resnet50():
+    """push_stride_up: the three stage boundaries' stride-2 1x1 consumers move up
+    into the previous block (its 3x3 becomes stride 2, its expand reads the shortcut
+    at stride 2); the logits are unchanged in fp32 and the FLOPs drop."""
+    from distributed_machine_learning_amd.models.optimize import push_stride_up
+
+    g, w = build_model("ResNet50", seed=0, calibrate=False)
+    go = push_stride_up(g)
+    by = {n.name: n for n in go.nodes}
+    for blk in ("conv2_block3", "conv3_block4", "conv4_block6"):
+        assert (by[f"{blk}_2_conv"].sh, by[f"{blk}_3_conv"].sh, by[f"{blk}_3_conv"].res_sub) == (2, 1, 2)
+    for st in ("conv3", "conv4", "conv5"):
+        assert by[f"{st}_block1_0_conv"].sh == by[f"{st}_block1_1_conv"].sh == 1
+    assert go.shape("conv2_block3_out")[:2] == (28, 28)
+    assert go.macs_per_image() < 0.95 * g.macs_per_image()
+    # nothing else qualifies (InceptionV3 has no 1x1 stride-2 consumers)
+    gi, _ = build_model("InceptionV3", seed=0, calibrate=False)
+    assert [(n.sh, n.sw) for n in push_stride_up(gi).nodes if hasattr(n, "sh")] == \
+        [(n.sh, n.sw) for n in gi.nodes if hasattr(n, "sh")]
+    imgs = torch.randint(0, 256, (2, *g.input_hw, 3), dtype=torch.uint8)
+    x = preprocess_reference(imgs, g.input_hw, g.preprocess)
+    a = OracleExecutor(g, w).forward(x)["logits"]
+    b = OracleExecutor(go, w).forward(x)["logits"]
+    assert ((a - b).abs().max() / a.abs().max()).item() < 1e-4
