@@ -73,7 +73,10 @@ class Engine:
         elif optimize:  # graph rewrites: conv-before-avgpool, sibling 1x1 fusion (models/optimize.py)
             from .optimize import optimize as _opt
 
-            graph = _opt(graph, stride_push=os.environ.get("DML_STRIDE_PUSH") != "0")
+            merge = os.environ.get("DML_SHORTCUT_MERGE", "1") != "0"
+            graph = _opt(graph, stride_push=os.environ.get("DML_STRIDE_PUSH") != "0",
+                         weights=weights if merge else None,
+                         shortcut_min_cout=int(os.environ.get("DML_SHORTCUT_MERGE_MINC", "0")))
         self.g, self.batch, self.device = graph, batch, torch.device(device)
         self.src_slots = src_slots
         self.reuse_buffers = reuse_buffers
@@ -171,7 +174,7 @@ class Engine:
         if len(users) != 1 or not isinstance(users[0], Pool):
             return None
         p = users[0]
-        if (p.mode, p.k, p.stride, p.pad, p.out_coff, p.relu) != ("max", 3, 2, 1, 0, False):
+        if (p.mode, p.k, p.stride, p.pad, p.relu) != ("max", 3, 2, 1, False) or p.out_coff % 8:
             return None
         return p
 
@@ -372,7 +375,8 @@ class Engine:
             wk, bias, _, kpad, _ = self.wdev[s.name]
             hc, wc, _ = g.shape(s.out)
             ho, wo, _ = g.shape(p.out)
-            sa = N.StemArgs(src.data_ptr(), wk.data_ptr(), bias.data_ptr(), self.buf[p.out].data_ptr(), B,
+            y = self.buf[p.out].data_ptr() + 2 * p.out_coff  # may be a channel slice (shortcut merge)
+            sa = N.StemArgs(src.data_ptr(), wk.data_ptr(), bias.data_ptr(), y, B,
                             self.src_hw[0], self.src_hw[1], g.input_hw[0], g.input_hw[1], mode, kpad, hc, wc,
                             ho, wo, self.cbuf[p.out])
             N.check(L.dml_plan_add_stem(plan, C.byref(sa)), "plan stem")

@@ -25,14 +25,27 @@
    ResNet50 this removes 3/4 of the work of each stage's last 1x1 expand and
    3x3 conv (and 3/4 of their activation traffic) at three stage boundaries.
 
-All rewrites keep the weights dict unchanged (members keep their names); the
+4. ``merge_projection_shortcut`` — a projection shortcut (1x1 conv + BN, no ReLU) is a
+   linear map whose output is only added into a block's last 1x1 expand, so
+       expand(x) + shortcut(s) == [W_e | W_s] . [x ; s] + (b_e + b_s)
+   — one GEMM over the channel concatenation of x and s (K = F + C_s) with no
+   residual. x's producer and s's producer write into one buffer at channel
+   offsets 0 and F (the Inception concat mechanism) and s's other readers read
+   the slice. Same MACs; the C_out-channel shortcut tensor is never written or
+   read back (ResNet50: 256/512/1024/2048 channels at the four stage entries).
+   Needs the folded weights: the merged conv's kernel/bias are ADDED to the
+   weights dict under "<expand>+<shortcut>" (BN folded, ``bn=False``).
+
+Rewrites 1-3 keep the weights dict unchanged (members keep their names); the
 fp32 oracle can execute the rewritten graph too (tests compare both forms).
 """
 from __future__ import annotations
 
 import copy
 from dataclasses import replace
-from typing import Dict, List
+from typing import Dict, List, Optional
+
+import numpy as np
 
 from .graph import Conv, FusedConv, Graph, Pool, Tensor, node_outputs
 
@@ -137,9 +150,60 @@ def push_stride_up(g: Graph) -> Graph:
     return g
 
 
-def optimize(g: Graph, pool_reorder: bool = True, fuse: bool = True, stride_push: bool = True) -> Graph:
+def merge_projection_shortcut(g: Graph, w: Dict[str, np.ndarray], min_cout: int = 0) -> Graph:
+    from .weights import fold_conv
+
+    g = copy.deepcopy(g)
+    while True:
+        cons = _consumers(g)
+        prod = {o: n for n in g.nodes for o in node_outputs(n)}
+        for e in g.nodes:
+            if not (isinstance(e, Conv) and e.residual and e.kh == e.kw == 1 and e.sh == e.sw == 1
+                    and e.ph == e.pw == 0 and e.res_sub == 1 and e.in_coff == 0 and not e.out_f32
+                    and e.cout >= min_cout):
+                continue
+            sc, q = prod.get(e.residual), prod.get(e.inp)
+            if not (isinstance(sc, Conv) and sc.kh == sc.kw == 1 and sc.sh == sc.sw == 1 and sc.ph == sc.pw == 0
+                    and not sc.relu and sc.residual is None and sc.in_coff == 0 and sc.out_coff == 0
+                    and not sc.out_f32 and cons.get(e.residual) == [e]):
+                continue
+            S, X = sc.inp, e.inp
+            pS = prod.get(S)
+            if not (isinstance(q, Conv) and q.out_coff == 0 and cons.get(X) == [e] and g.shape(X)[2] == e.cin
+                    and isinstance(pS, (Conv, Pool)) and pS.out_coff == 0 and S != g.input
+                    and g.shape(S)[:2] == g.shape(X)[:2] and g.shape(S)[2] == sc.cin
+                    and all(isinstance(u, Conv) and u.inp == S and u.residual != S and u.in_coff == 0
+                            for u in cons.get(S, []))):
+                continue
+            if e.cin % 8 or sc.cin % 8:
+                continue
+            ke, be = fold_conv(e, w)
+            ks, bs = fold_conv(sc, w)
+            name = f"{e.name}+{sc.name}"
+            w[f"{name}/kernel"] = np.concatenate([ke, ks], axis=2)
+            w[f"{name}/bias"] = (be + bs).astype(np.float32)
+            h, wd, _ = g.shape(X)
+            g.tensors[X] = Tensor(X, h, wd, e.cin + sc.cin)
+            pS.out, pS.out_coff = X, e.cin
+            for u in cons.get(S, []):
+                if u is not sc:
+                    u.inp, u.in_coff = X, e.cin
+            m = replace(e, name=name, cin=e.cin + sc.cin, residual=None, bias=True, bn=False)
+            g.nodes = [m if n is e else n for n in g.nodes if n is not sc]
+            del g.tensors[S], g.tensors[e.residual]
+            break
+        else:
+            break
+    g.validate()
+    return g
+
+
+def optimize(g: Graph, pool_reorder: bool = True, fuse: bool = True, stride_push: bool = True,
+             weights: Optional[Dict[str, np.ndarray]] = None, shortcut_min_cout: int = 0) -> Graph:
     if stride_push:
         g = push_stride_up(g)
+    if weights is not None:  # adds the merged convs' folded weights to `weights`
+        g = merge_projection_shortcut(g, weights, shortcut_min_cout)
     if pool_reorder:
         g = conv_before_avgpool(g)
     if fuse:

@@ -161,3 +161,27 @@ def test_stride_pushdown_resnet50():
     a = OracleExecutor(g, w).forward(x)["logits"]
     b = OracleExecutor(go, w).forward(x)["logits"]
     assert ((a - b).abs().max() / a.abs().max()).item() < 1e-4
+
+
+def test_projection_shortcut_merge_resnet50():
+    """merge_projection_shortcut: each stage's projection shortcut joins the block's
+    expand as one GEMM over the channel concat (exact in fp32; adds the folded
+    merged kernels to the weights dict; the shortcut tensors disappear)."""
+    from distributed_machine_learning_amd.models.optimize import optimize
+
+    g, w = build_model("ResNet50", seed=0, calibrate=False)
+    w2 = dict(w)
+    go = optimize(g, weights=w2)
+    merged = [n for n in go.nodes if getattr(n, "name", "").endswith("_block1_0_conv")]
+    assert [n.name for n in merged] == [f"conv{s}_block1_3_conv+conv{s}_block1_0_conv" for s in (2, 3, 4, 5)]
+    assert all(n.residual is None and not n.bn for n in merged)
+    assert [n.cin for n in merged] == [128, 384, 768, 1536]
+    assert "conv2_block1_0_conv" not in {t for t in go.tensors} and set(w) < set(w2)
+    assert optimize(g).nodes[0].name == go.nodes[0].name  # without weights: no merge, no error
+    imgs = torch.randint(0, 256, (2, *g.input_hw, 3), dtype=torch.uint8)
+    x = preprocess_reference(imgs, g.input_hw, g.preprocess)
+    a = OracleExecutor(g, w).forward(x)["logits"]
+    b = OracleExecutor(go, w2).forward(x)["logits"]
+    assert ((a - b).abs().max() / a.abs().max()).item() < 1e-4
+    # the bf16-emulating oracle runs the merged graph too (folded bias, no BN)
+    OracleExecutor(go, w2, emulate_bf16=True).forward(x)

@@ -67,7 +67,10 @@ def test_engine_fused_stem_equals_unfused():
     ef.infer(imgs)
     eu.infer(imgs)
     torch.cuda.synchronize()
-    pf, pu = ef.view("pool1").float(), eu.view("pool1").float()
+    # the pool output may live in a channel slice of a concat buffer (shortcut merge)
+    p = next(n for n in ef.g.nodes if getattr(n, "name", "") == "pool1_pool")
+    pf = ef.view(p.out)[..., p.out_coff:p.out_coff + 64].float()
+    pu = eu.view(p.out)[..., p.out_coff:p.out_coff + 64].float()
     assert (pf - pu).abs().max().item() <= 1e-2 * pu.abs().max().item()
     assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 2e-2
 
@@ -153,7 +156,7 @@ def test_expand_reduce_matches_fp32(c, m):
     assert _rel(z.float().cpu(), z_ref) < 1e-2
 
 
-@pytest.mark.parametrize("maxc,pairs", [(256, 2), (1024, 10)])
+@pytest.mark.parametrize("maxc,pairs", [(256, 1), (1024, 7)])
 def test_engine_fused_blocks_equal_unfused(maxc, pairs, monkeypatch):
     monkeypatch.setenv("DML_FUSED_BLOCKS_MAXC", str(maxc))
     g, w = build_model("ResNet50", seed=8, calibrate=True)
@@ -161,9 +164,10 @@ def test_engine_fused_blocks_equal_unfused(maxc, pairs, monkeypatch):
     # no buffer recycling: intermediate tensors are compared after the whole forward
     ef = Engine(g, w, batch=2, reuse_buffers=False)
     eu = Engine(g, w, batch=2, fuse_blocks=False, reuse_buffers=False)
-    # stage 2: 2 block boundaries, stage 3: 3, stage 4: 5 (stage 5, C = 2048, is not fused)
+    # block boundaries after each stage's first block (whose expand absorbed the projection
+    # shortcut, models/optimize.py): stage 2: 1, stage 3: 2, stage 4: 4 (stage 5, C = 2048, is not fused)
     assert sorted(ef.exp_red) == sorted([f"conv{s}_block{k}_3_conv" for s, nb in ((2, 3), (3, 4), (4, 6))
-                                         for k in range(1, nb)][:pairs]) and not eu.exp_red
+                                         for k in range(2, nb)][:pairs]) and not eu.exp_red
     assert len(ef.op_names) == len(eu.op_names) - pairs
     # the fused kernel writes the reduce output while reading the expand inputs: never
     # aliased, also under liveness-based buffer recycling
@@ -174,8 +178,9 @@ def test_engine_fused_blocks_equal_unfused(maxc, pairs, monkeypatch):
     ef.infer(imgs)
     eu.infer(imgs)
     torch.cuda.synchronize()
-    for name in ("conv2_block1_out", "conv2_block2_1", "conv2_block3_1", "conv2_block3_out", "conv3_block2_1",
-                 "conv3_block4_out", "conv4_block2_1", "conv4_block6_1", "conv4_block6_out"):
+    # (stage-final block outputs now live in the next stage's concat buffer, not under their own name)
+    for name in ("conv2_block1_out", "conv2_block2_1", "conv2_block2_out", "conv2_block3_1", "conv3_block2_1",
+                 "conv3_block3_out", "conv4_block2_1", "conv4_block6_1", "conv4_block5_out"):
         pf, pu = ef.view(name).float(), eu.view(name).float()
         assert (pf - pu).abs().max().item() <= 2e-2 * pu.abs().max().item(), name
     assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 5e-2
