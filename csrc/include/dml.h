@@ -129,6 +129,7 @@ typedef struct {
   void* z;           // bf16 [M][ldz] (F channels)
   int M, ldx, ldw3, ldr, ldy, ldw1, ldz;
   int C;             // expand width: 256, 512 or 1024 (reduce width F = C / 4)
+  int kx;            // expand K: 0/F with res, 2F with res == null (merged projection shortcut, C = 256)
 } DmlExpandReduceArgs;
 
 // ---- single-op launches (used by tests and by the plan executor) ----

@@ -27,6 +27,11 @@
 //     bias + shortcut + ReLU -> bf16 -> one coalesced 16-B store to Y AND a copy
 //     into an LDS Y tile (row pitch 2C + 32 B: the reduce's fragment reads are
 //     conflict-free);
+//  Merged-shortcut variant (RES = false, KX = 2F; C = 256): after the projection-
+//  shortcut merge (models/optimize.py) a stage's first expand reads the channel
+//  concat [x ; s] (K = 2F) with no residual; same kernel, longer K loop. Measured
+//  150 us vs 74 + 55 us for the two launches (profiles/r1_v15: the doubled expand K
+//  runs inside the phase-serialised workgroup), so the engine keeps it opt-in.
 //  3. reduce: the wave's 16 output channels for the BM pixels from the LDS Y
 //     tile (K = C), W1 fragments in VGPRs in chunks of 8 k-steps (the first
 //     chunk loaded during the epilogue), bias + ReLU -> 8-B stores.
@@ -36,9 +41,9 @@
 namespace dml {
 namespace bneck {
 
-template <int C_, int BM_>
+template <int C_, int BM_, int KX_ = C_ / 4>
 struct Cfg {
-  static constexpr int C = C_, BM = BM_, F = C / 4;
+  static constexpr int C = C_, BM = BM_, F = C / 4, KX = KX_;
   static constexpr int NW = C / 64, NT = NW * 64;
   static constexpr int SROW = C * 4 + 16;         // fp32 staging row
   static constexpr int STAGE_BYTES = 16 * SROW;   // one pass = 16 pixels
@@ -48,7 +53,7 @@ struct Cfg {
   static constexpr int PR = NT / CG;              // pixel rows per epilogue sweep (8)
   static constexpr int EIT = BM / PR;             // epilogue pixels per thread
   static constexpr int JN = BM / 16;              // pixel fragments
-  static constexpr int KS1 = F / 32, KS2 = C / 32;
+  static constexpr int KS1 = KX / 32, KS2 = C / 32;
   static constexpr int KC = 8;                    // reduce k-steps per weight chunk
   static_assert(PR == 8 && BM % 16 == 0 && KS2 % KC == 0, "tile shape");
 };
@@ -60,9 +65,9 @@ __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   f[6] = bf2f(v.w & 0xffff); f[7] = bf2f(v.w >> 16);
 }
 
-template <int C, int BM, int MINB>
+template <int C, int BM, int MINB, int KX = C / 4, bool RES = true>
 __global__ __launch_bounds__(C, MINB) void expand_reduce_kernel(DmlExpandReduceArgs a) {
-  using T = Cfg<C, BM>;
+  using T = Cfg<C, BM, KX>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* stage = smem;
   char* ytile = smem + T::STAGE_BYTES;
@@ -82,7 +87,7 @@ __global__ __launch_bounds__(C, MINB) void expand_reduce_kernel(DmlExpandReduceA
 #pragma unroll
   for (int it = 0; it < T::EIT; ++it) {
     const int m = min(m0 + prow + it * T::PR, a.M - 1);  // rows >= M are computed but never stored
-    rpre[it] = *(const uint4*)(rg + (long)m * a.ldr + ch_t);
+    rpre[it] = RES ? *(const uint4*)(rg + (long)m * a.ldr + ch_t) : make_uint4(0, 0, 0, 0);
   }
   const float4 bias0 = *(const float4*)(a.b3 + ch_t), bias1 = *(const float4*)(a.b3 + ch_t + 4);
 
@@ -131,8 +136,8 @@ __global__ __launch_bounds__(C, MINB) void expand_reduce_kernel(DmlExpandReduceA
       const int lp = px - 16 * p;
       const float4 v0 = *(const float4*)(stage + lp * T::SROW + cg_t * 32);
       const float4 v1 = *(const float4*)(stage + lp * T::SROW + cg_t * 32 + 16);
-      float r[8];
-      unpack8(rpre[it], r);
+      float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if constexpr (RES) unpack8(rpre[it], r);
       float f[8] = {v0.x + bias0.x + r[0], v0.y + bias0.y + r[1], v0.z + bias0.z + r[2], v0.w + bias0.w + r[3],
                     v1.x + bias1.x + r[4], v1.y + bias1.y + r[5], v1.z + bias1.z + r[6], v1.w + bias1.w + r[7]};
 #pragma unroll
@@ -177,19 +182,20 @@ __global__ __launch_bounds__(C, MINB) void expand_reduce_kernel(DmlExpandReduceA
   }
 }
 
-template <int C, int BM, int MINB>
+template <int C, int BM, int MINB, int KX = C / 4, bool RES = true>
 int launch(const DmlExpandReduceArgs* a, hipStream_t s) {
-  using T = Cfg<C, BM>;
+  using T = Cfg<C, BM, KX>;
   const long blocks = ((long)a->M + BM - 1) / BM;
-  hipLaunchKernelGGL((expand_reduce_kernel<C, BM, MINB>), dim3((unsigned)blocks), dim3(T::NT), T::LDS, s, *a);
+  hipLaunchKernelGGL((expand_reduce_kernel<C, BM, MINB, KX, RES>), dim3((unsigned)blocks), dim3(T::NT), T::LDS, s,
+                     *a);
   DML_CHECK_LAUNCH();
   return 0;
 }
 
-template <int C, int BM, int MINB>
+template <int C, int BM, int MINB, int KX = C / 4, bool RES = true>
 int set_attr() {
-  return (int)hipFuncSetAttribute((const void*)expand_reduce_kernel<C, BM, MINB>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, Cfg<C, BM>::LDS);
+  return (int)hipFuncSetAttribute((const void*)expand_reduce_kernel<C, BM, MINB, KX, RES>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, Cfg<C, BM, KX>::LDS);
 }
 
 }  // namespace bneck
@@ -199,21 +205,26 @@ int set_attr() {
 // capture); called from dml_conv_v2_init.
 extern "C" int dml_expand_reduce_init(void) {
   using namespace dml::bneck;
-  const int rc = set_attr<256, 64, 2>() | set_attr<512, 32, 2>() | set_attr<1024, 32, 1>();
+  const int rc = set_attr<256, 64, 2>() | set_attr<512, 32, 2>() | set_attr<1024, 32, 1>() |
+                 set_attr<256, 64, 2, 128, false>();
   if (rc) dml_set_error("dml_expand_reduce_init: hipFuncSetAttribute failed");
   return rc ? -1 : 0;
 }
 
 extern "C" int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s) {
-  // expand F -> C channels (+ shortcut), reduce C -> F, F = C / 4, C in {256, 512, 1024}
+  // expand KX -> C channels (+ shortcut), reduce C -> F, F = C / 4, C in {256, 512, 1024};
+  // KX = F with a shortcut, or KX = 2F without one (merged projection shortcut, C = 256)
   const int C = a->C, F = C / 4;
-  if ((C != 256 && C != 512 && C != 1024) || a->M < 1 || a->ldx % 8 || a->ldx < F || a->ldw3 % 8 ||
-      a->ldw3 < F || a->ldr % 8 || a->ldr < C || a->ldy % 8 || a->ldy < C || a->ldw1 % 8 || a->ldw1 < C ||
-      a->ldz % 4 || a->ldz < F) {
+  const int kx = a->kx > 0 ? a->kx : F;
+  const bool merged = a->res == nullptr;
+  if ((C != 256 && C != 512 && C != 1024) || a->M < 1 || a->ldx % 8 || a->ldx < kx || a->ldw3 % 8 ||
+      a->ldw3 < kx || (!merged && (a->ldr % 8 || a->ldr < C)) || a->ldy % 8 || a->ldy < C || a->ldw1 % 8 ||
+      a->ldw1 < C || a->ldz % 4 || a->ldz < F || (merged ? (C != 256 || kx != 2 * F) : kx != F)) {
     dml_set_error("dml_expand_reduce: unsupported shape");
     return -1;
   }
   using namespace dml::bneck;
+  if (merged) return launch<256, 64, 2, 128, false>(a, s);
   if (C == 256) return launch<256, 64, 2>(a, s);
   if (C == 512) return launch<512, 32, 2>(a, s);
   return launch<1024, 32, 1>(a, s);

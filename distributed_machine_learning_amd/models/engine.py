@@ -220,7 +220,9 @@ class Engine:
         F -> C, shortcut, ReLU) -> reduce (1x1 s1 reading the expand output, C -> F,
         ReLU), F = C / 4 — ResNet50's convN_blockK_3 / convN_blockK+1_1. The kernel
         supports C in {256, 512, 1024}; only C = 256 (stage 2) beats the two separate
-        launches (bottleneck_fused.hip header), so DML_FUSED_BLOCKS_MAXC defaults to 256."""
+        launches (bottleneck_fused.hip header), so DML_FUSED_BLOCKS_MAXC defaults to 256.
+        The merged-shortcut form (K = 2F, no residual) is opt-in (DML_FUSED_MERGED_BLOCK=1):
+        150 us vs 74 + 55 us for the two launches (profiles/r1_v15)."""
         if not enabled or self.device.type != "cuda" or os.environ.get("DML_FUSED_BLOCKS") == "0":
             return {}
         maxc = int(os.environ.get("DML_FUSED_BLOCKS_MAXC", "256"))
@@ -229,12 +231,16 @@ class Engine:
         for e, r in zip(nodes, nodes[1:]):
             if not (isinstance(e, Conv) and isinstance(r, Conv)):
                 continue
+            # with its shortcut (K = F), or a merged projection shortcut (K = 2F, no residual; C = 256)
+            shortcut = e.residual and e.res_sub == 1 and e.cin * 4 == e.cout
+            merged = (e.residual is None and e.cin * 2 == e.cout == 256
+                      and os.environ.get("DML_FUSED_MERGED_BLOCK", "0") == "1")  # opt-in: measured slower
             if not (e.kh == e.kw == 1 and e.sh == e.sw == 1 and e.cout in (256, 512, 1024) and e.cout <= maxc
-                    and e.cin * 4 == e.cout and e.residual and e.res_sub == 1
+                    and (shortcut or merged)
                     and e.relu and e.in_coff == 0 and e.out_coff == 0 and not e.out_f32):
                 continue
             if not (r.inp == e.out and r.kh == r.kw == 1 and r.sh == r.sw == 1 and r.cin == e.cout
-                    and r.cout == e.cin
+                    and r.cout * 4 == e.cout
                     and r.relu and r.residual is None and r.in_coff == 0 and r.out_coff == 0 and not r.out_f32):
                 continue
             out[e.name] = r
@@ -409,11 +415,13 @@ class Engine:
                 w3, b3, _, kp3, _ = self.wdev[n.name]
                 w1, b1, _, kp1, _ = self.wdev[r.name]
                 h, w, _ = g.shape(n.out)
+                res = self.buf[n.residual].data_ptr() if n.residual else None
+                ldr = self.cbuf[n.residual] if n.residual else 0
                 ea = N.ExpandReduceArgs(self.buf[n.inp].data_ptr(), w3.data_ptr(), b3.data_ptr(),
-                                        self.buf[n.residual].data_ptr(), self.buf[n.out].data_ptr(),
+                                        res, self.buf[n.out].data_ptr(),
                                         w1.data_ptr(), b1.data_ptr(), self.buf[r.out].data_ptr(), B * h * w,
-                                        self.cbuf[n.inp], kp3, self.cbuf[n.residual], self.cbuf[n.out], kp1,
-                                        self.cbuf[r.out], n.cout)
+                                        self.cbuf[n.inp], kp3, ldr, self.cbuf[n.out], kp1,
+                                        self.cbuf[r.out], n.cout, n.cin)
                 N.check(L.dml_plan_add_expand_reduce(plan, C.byref(ea)), "plan expand+reduce")
                 self.op_names.append(f"{n.name}+{r.name}")
                 continue

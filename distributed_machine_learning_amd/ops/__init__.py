@@ -221,13 +221,14 @@ def conv3x3_pool(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor) ->
     return out
 
 
-def expand_reduce(x: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, res: torch.Tensor, w1: torch.Tensor,
-                  b1: torch.Tensor):
+def expand_reduce(x: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, res: Optional[torch.Tensor],
+                  w1: torch.Tensor, b1: torch.Tensor, c: Optional[int] = None):
     """Fused ResNet block boundary (csrc/kernels/bottleneck_fused.hip), C = res channels,
     F = C / 4: y = relu(1x1 conv F -> C of x + b3 + res), z = relu(1x1 conv C -> F of y + b1).
     x: bf16 [..., F]; res: bf16 [..., C], C in {256, 512, 1024}; w3 [>=C][>=F], w1 [>=F][>=C]
-    packed (pack_weight). Returns (y, z) with x's leading shape."""
-    c = res.shape[-1]
+    packed (pack_weight). Returns (y, z) with x's leading shape.
+    res=None (merged projection shortcut): x is [..., 2F] (the [x ; s] concat), C = c = 256."""
+    c = res.shape[-1] if res is not None else c
     f = c // 4
     lead = x.shape[:-1]
     m = x.numel() // x.shape[-1]
@@ -235,11 +236,12 @@ def expand_reduce(x: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, res: torc
     z = torch.empty((*lead, f), device=x.device, dtype=torch.bfloat16)
     b3p = b3.to(x.device, torch.float32).contiguous()
     b1p = b1.to(x.device, torch.float32).contiguous()
-    assert x.is_contiguous() and res.is_contiguous() and w3.is_contiguous() and w1.is_contiguous()
+    assert x.is_contiguous() and (res is None or res.is_contiguous()) and w3.is_contiguous() and w1.is_contiguous()
     assert w3.shape[0] >= c and w1.shape[0] >= f and b3p.numel() >= c and b1p.numel() >= f
-    a = N.ExpandReduceArgs(x.data_ptr(), w3.data_ptr(), b3p.data_ptr(), res.data_ptr(), y.data_ptr(), w1.data_ptr(),
-                           b1p.data_ptr(), z.data_ptr(), m, x.shape[-1], w3.shape[1], res.shape[-1], c,
-                           w1.shape[1], f, c)
+    a = N.ExpandReduceArgs(x.data_ptr(), w3.data_ptr(), b3p.data_ptr(), res.data_ptr() if res is not None else None,
+                           y.data_ptr(), w1.data_ptr(), b1p.data_ptr(), z.data_ptr(), m, x.shape[-1], w3.shape[1],
+                           res.shape[-1] if res is not None else 0, c, w1.shape[1], f, c,
+                           f if res is not None else 2 * f)
     N.check(N.lib().dml_expand_reduce(C.byref(a), N.stream_ptr()), "dml_expand_reduce")
     y._keep = (b3p, b1p)
     return y, z

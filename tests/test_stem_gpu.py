@@ -156,25 +156,29 @@ def test_expand_reduce_matches_fp32(c, m):
     assert _rel(z.float().cpu(), z_ref) < 1e-2
 
 
-@pytest.mark.parametrize("maxc,pairs", [(256, 1), (1024, 7)])
+@pytest.mark.parametrize("maxc,pairs", [(256, 2), (1024, 8)])
 def test_engine_fused_blocks_equal_unfused(maxc, pairs, monkeypatch):
     monkeypatch.setenv("DML_FUSED_BLOCKS_MAXC", str(maxc))
+    monkeypatch.setenv("DML_FUSED_MERGED_BLOCK", "1")  # opt-in merged-shortcut form, covered here
     g, w = build_model("ResNet50", seed=8, calibrate=True)
     imgs = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda")
     # no buffer recycling: intermediate tensors are compared after the whole forward
     ef = Engine(g, w, batch=2, reuse_buffers=False)
     eu = Engine(g, w, batch=2, fuse_blocks=False, reuse_buffers=False)
-    # block boundaries after each stage's first block (whose expand absorbed the projection
-    # shortcut, models/optimize.py): stage 2: 1, stage 3: 2, stage 4: 4 (stage 5, C = 2048, is not fused)
-    assert sorted(ef.exp_red) == sorted([f"conv{s}_block{k}_3_conv" for s, nb in ((2, 3), (3, 4), (4, 6))
-                                         for k in range(2, nb)][:pairs]) and not eu.exp_red
+    # block boundaries: stage 2's first (its expand absorbed the projection shortcut,
+    # models/optimize.py: K = 2F, no residual) and second; stage 3: 2, stage 4: 4 (the merged
+    # first expands of stages 3-5 and stage 5, C = 2048, are not fused)
+    want = ["conv2_block1_3_conv+conv2_block1_0_conv"] + [
+        f"conv{s}_block{k}_3_conv" for s, nb in ((2, 3), (3, 4), (4, 6)) for k in range(2, nb)]
+    assert sorted(ef.exp_red) == sorted(want[:pairs]) and not eu.exp_red
     assert len(ef.op_names) == len(eu.op_names) - pairs
     # the fused kernel writes the reduce output while reading the expand inputs: never
     # aliased, also under liveness-based buffer recycling
     er = Engine(g, w, batch=2)
     for e_name, r in er.exp_red.items():
         e = next(n for n in er.g.nodes if n.name == e_name)
-        assert er.buf[r.out].data_ptr() not in (er.buf[e.inp].data_ptr(), er.buf[e.residual].data_ptr())
+        srcs = [er.buf[e.inp].data_ptr()] + ([er.buf[e.residual].data_ptr()] if e.residual else [])
+        assert er.buf[r.out].data_ptr() not in srcs
     ef.infer(imgs)
     eu.infer(imgs)
     torch.cuda.synchronize()
@@ -184,3 +188,24 @@ def test_engine_fused_blocks_equal_unfused(maxc, pairs, monkeypatch):
         pf, pu = ef.view(name).float(), eu.view(name).float()
         assert (pf - pu).abs().max().item() <= 2e-2 * pu.abs().max().item(), name
     assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 5e-2
+
+
+@pytest.mark.parametrize("m", [64 * 7, 1000, 3 * 56 * 56])
+def test_expand_reduce_merged_shortcut_matches_fp32(m):
+    """K = 2F, no residual: the stage-2 entry after the projection-shortcut merge."""
+    torch.manual_seed(4)
+    c, f = 256, 64
+    x = _bf(torch.randn(m, 2 * f))
+    w3 = _bf(torch.randn(c, 2 * f) * (2.0 / (2 * f)) ** 0.5)
+    b3 = torch.randn(c) * 0.1
+    w1 = _bf(torch.randn(f, c) * (2.0 / c) ** 0.5)
+    b1 = torch.randn(f) * 0.1
+    y_ref = _bf(F.relu(x @ w3.T + b3))
+    z_ref = F.relu(y_ref @ w1.T + b1)
+    w1p = torch.zeros(max(f, 64), c)
+    w1p[:f] = w1
+    y, z = ops.expand_reduce(x.to(torch.bfloat16).cuda(), w3.to(torch.bfloat16).cuda(), b3.cuda(), None,
+                             w1p.to(torch.bfloat16).cuda(), b1.cuda(), c=c)
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu(), y_ref) < 1e-2
+    assert _rel(z.float().cpu(), z_ref) < 1e-2
