@@ -130,6 +130,10 @@ typedef struct {
   int M, ldx, ldw3, ldr, ldy, ldw1, ldz;
   int C;             // expand width: 256, 512 or 1024 (reduce width F = C / 4)
   int kx;            // expand K: 0/F with res, 2F with res == null (merged projection shortcut, C = 256)
+  // Subsampled Y store (0/1 = off): when Y's only other reader takes every ysub-th
+  // pixel (a shortcut after the stride pushdown), pixel (n, h, w) of the yH x yW grid
+  // is stored only for h, w % ysub == 0, compactly at n*(yH/ysub)*(yW/ysub) + ...
+  int ysub, yH, yW;
 } DmlExpandReduceArgs;
 
 // ---- single-op launches (used by tests and by the plan executor) ----

@@ -144,7 +144,16 @@ __global__ __launch_bounds__(C, MINB) void expand_reduce_kernel(DmlExpandReduceA
       for (int q = 0; q < 8; ++q) f[q] = fmaxf(f[q], 0.f);
       const uint4 yv = make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
       const int m = m0 + px;
-      if (m < a.M) *(uint4*)((unsigned short*)a.y + (long)m * a.ldy + ch_t) = yv;
+      long ym = m;
+      bool keep = m < a.M;
+      if (a.ysub > 1) {  // only the pixels a strided reader takes, stored compactly
+        const int hw = a.yH * a.yW;
+        const int ni = m / hw, r = m - ni * hw;
+        const int hh = r / a.yW, ww = r - hh * a.yW;
+        keep = keep && hh % a.ysub == 0 && ww % a.ysub == 0;
+        ym = ((long)ni * (a.yH / a.ysub) + hh / a.ysub) * (a.yW / a.ysub) + ww / a.ysub;
+      }
+      if (keep) *(uint4*)((unsigned short*)a.y + ym * a.ldy + ch_t) = yv;
       *(uint4*)(ytile + px * T::YROW + cg_t * 16) = yv;
     }
   }
@@ -219,7 +228,9 @@ extern "C" int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s) {
   const bool merged = a->res == nullptr;
   if ((C != 256 && C != 512 && C != 1024) || a->M < 1 || a->ldx % 8 || a->ldx < kx || a->ldw3 % 8 ||
       a->ldw3 < kx || (!merged && (a->ldr % 8 || a->ldr < C)) || a->ldy % 8 || a->ldy < C || a->ldw1 % 8 ||
-      a->ldw1 < C || a->ldz % 4 || a->ldz < F || (merged ? (C != 256 || kx != 2 * F) : kx != F)) {
+      a->ldw1 < C || a->ldz % 4 || a->ldz < F || (merged ? (C != 256 || kx != 2 * F) : kx != F) ||
+      (a->ysub > 1 && (a->yH % a->ysub || a->yW % a->ysub || (long)a->yH * a->yW < 1 ||
+                       a->M % ((long)a->yH * a->yW)))) {
     dml_set_error("dml_expand_reduce: unsupported shape");
     return -1;
   }

@@ -82,6 +82,7 @@ class ExpandReduceArgs(C.Structure):
         ("w1", C.c_void_p), ("b1", C.c_void_p), ("z", C.c_void_p),
         ("M", C.c_int), ("ldx", C.c_int), ("ldw3", C.c_int), ("ldr", C.c_int), ("ldy", C.c_int),
         ("ldw1", C.c_int), ("ldz", C.c_int), ("C", C.c_int), ("kx", C.c_int),
+        ("ysub", C.c_int), ("yH", C.c_int), ("yW", C.c_int),
     ]
 
 

@@ -103,6 +103,8 @@ class Engine:
         # ResNet stage-2 block boundaries: expand (64 -> 256, + shortcut) and the next
         # block's reduce (256 -> 64) as ONE kernel (csrc/kernels/bottleneck_fused.hip)
         self.exp_red = self._fusable_expand_reduce(fuse_blocks)
+        # fused pairs whose Y is otherwise only read at stride 2 store just those pixels
+        self.ysub = self._subsampled_y()
         self._src_tensors, self._result_views = src_tensors, result_views
         if share is not None:
             self.wdev, self.whalo = share.wdev, share.whalo
@@ -244,6 +246,26 @@ class Engine:
                     and r.relu and r.residual is None and r.in_coff == 0 and r.out_coff == 0 and not r.out_f32):
                 continue
             out[e.name] = r
+        return out
+
+    def _subsampled_y(self) -> Dict[str, int]:
+        """{tensor: 2} for fused expand+reduce outputs Y whose readers besides the fused
+        reduce all take it as a stride-2 shortcut (``res_sub == 2``, left by the stride
+        pushdown): the kernel then stores only those pixels, compactly (a quarter of the
+        Y bytes), and the readers address it as a same-grid residual. The compact tensor
+        sits at the start of Y's full-size buffer (``view`` shows it in the first quarter)."""
+        if os.environ.get("DML_YSUB", "1") == "0":
+            return {}
+        out: Dict[str, int] = {}
+        for e_name, r in self.exp_red.items():
+            e = next(n for n in self.g.nodes if getattr(n, "name", None) == e_name)
+            h, w, _ = self.g.shape(e.out)
+            users = [n for n in self.g.nodes if n is not r and e.out in (getattr(n, "inp", None),
+                                                                          getattr(n, "residual", None))]
+            if (users and h % 2 == 0 and w % 2 == 0 and e.out != self.g.logits
+                    and all(isinstance(u, Conv) and u.inp != e.out and u.residual == e.out and u.res_sub == 2
+                            for u in users)):
+                out[e.out] = 2
         return out
 
     def _halo_eligible(self, n) -> bool:
@@ -422,6 +444,8 @@ class Engine:
                                         w1.data_ptr(), b1.data_ptr(), self.buf[r.out].data_ptr(), B * h * w,
                                         self.cbuf[n.inp], kp3, ldr, self.cbuf[n.out], kp1,
                                         self.cbuf[r.out], n.cout, n.cin)
+                if n.out in self.ysub:
+                    ea.ysub, ea.yH, ea.yW = self.ysub[n.out], h, w
                 N.check(L.dml_plan_add_expand_reduce(plan, C.byref(ea)), "plan expand+reduce")
                 self.op_names.append(f"{n.name}+{r.name}")
                 continue
@@ -503,7 +527,7 @@ class Engine:
         a = N.ConvArgs(x, wk.data_ptr(), bias.data_ptr(), res, y, B, h, w, cin_eff, ldx,
                        n.kh, kw, n.sh, n.sw, n.ph, pw, ho, wo, n.cout, K, kpad,
                        self.cbuf[n.out], ldr, int(n.relu), int(n.out_f32), 1, dw)
-        if n.residual and n.res_sub > 1:  # shortcut read at stride res_sub (models/optimize.py)
+        if n.residual and n.res_sub > 1 and n.residual not in self.ysub:  # strided shortcut (models/optimize.py)
             rh, rw, _ = g.shape(n.residual)
             a.rsub, a.rW, a.rHW = n.res_sub, rw, rh * rw
         return a

@@ -7,12 +7,15 @@ uint8 -> preprocess -> conv 7x7/2 + ReLU -> max pool 3x3/2 in one launch.
   both preprocess modes;
 * inside the engine: the fused plan's pool1 output and logits equal the
   unfused three-launch plan's (fuse_stem=False)."""
+import ctypes as C
+
 import pytest
 import torch
 import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
+from distributed_machine_learning_amd import _native as N  # noqa: E402
 from distributed_machine_learning_amd import ops  # noqa: E402
 from distributed_machine_learning_amd.models import build_model  # noqa: E402
 from distributed_machine_learning_amd.models.engine import Engine, pack_conv_weight, pair_pack_kernel  # noqa: E402
@@ -171,6 +174,8 @@ def test_engine_fused_blocks_equal_unfused(maxc, pairs, monkeypatch):
     want = ["conv2_block1_3_conv+conv2_block1_0_conv"] + [
         f"conv{s}_block{k}_3_conv" for s, nb in ((2, 3), (3, 4), (4, 6)) for k in range(2, nb)]
     assert sorted(ef.exp_red) == sorted(want[:pairs]) and not eu.exp_red
+    # the last fused boundary of each stage feeds only the stride-2 shortcut besides its reduce
+    assert "conv2_block2_out" in ef.ysub and not eu.ysub
     assert len(ef.op_names) == len(eu.op_names) - pairs
     # the fused kernel writes the reduce output while reading the expand inputs: never
     # aliased, also under liveness-based buffer recycling
@@ -186,6 +191,10 @@ def test_engine_fused_blocks_equal_unfused(maxc, pairs, monkeypatch):
     for name in ("conv2_block1_out", "conv2_block2_1", "conv2_block2_out", "conv2_block3_1", "conv3_block2_1",
                  "conv3_block3_out", "conv4_block2_1", "conv4_block6_1", "conv4_block5_out"):
         pf, pu = ef.view(name).float(), eu.view(name).float()
+        if name in ef.ysub:  # stored compactly: only the pixels the stride-2 shortcut reads
+            b, h, w, cb = pf.shape
+            pf = ef.buf[name].view(-1)[: b * (h // 2) * (w // 2) * cb].view(b, h // 2, w // 2, cb).float()
+            pu = pu[:, ::2, ::2]
         assert (pf - pu).abs().max().item() <= 2e-2 * pu.abs().max().item(), name
     assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 5e-2
 
@@ -208,4 +217,35 @@ def test_expand_reduce_merged_shortcut_matches_fp32(m):
                              w1p.to(torch.bfloat16).cuda(), b1.cuda(), c=c)
     torch.cuda.synchronize()
     assert _rel(y.float().cpu(), y_ref) < 1e-2
+    assert _rel(z.float().cpu(), z_ref) < 1e-2
+
+
+def test_expand_reduce_subsampled_y():
+    """ysub = 2: Y stored only at even (h, w), compactly; Z complete."""
+    torch.manual_seed(5)
+    n, h, w, c, f = 2, 10, 12, 256, 64
+    m = n * h * w
+    x = _bf(torch.randn(m, f).clamp(min=0))
+    res = _bf(torch.randn(m, c))
+    w3 = _bf(torch.randn(c, f) * (2.0 / f) ** 0.5)
+    b3 = torch.randn(c) * 0.1
+    w1 = _bf(torch.randn(f, c) * (2.0 / c) ** 0.5)
+    b1 = torch.randn(f) * 0.1
+    y_ref = _bf(F.relu(x @ w3.T + b3 + res))
+    z_ref = F.relu(y_ref @ w1.T + b1)
+    w1p = torch.zeros(64, c)
+    w1p[:f] = w1
+    xd, rd = x.to(torch.bfloat16).cuda(), res.to(torch.bfloat16).cuda()
+    y = torch.full((m, c), -7.0, device="cuda", dtype=torch.bfloat16)
+    z = torch.empty((m, f), device="cuda", dtype=torch.bfloat16)
+    w3d, w1d = w3.to(torch.bfloat16).cuda(), w1p.to(torch.bfloat16).cuda()
+    b3d, b1d = b3.cuda(), b1.cuda()
+    a = N.ExpandReduceArgs(xd.data_ptr(), w3d.data_ptr(), b3d.data_ptr(), rd.data_ptr(), y.data_ptr(), w1d.data_ptr(),
+                           b1d.data_ptr(), z.data_ptr(), m, f, f, c, c, c, f, c, f, 2, h, w)
+    N.check(N.lib().dml_expand_reduce(C.byref(a), N.stream_ptr()), "expand_reduce ysub")
+    torch.cuda.synchronize()
+    q = n * (h // 2) * (w // 2)
+    want = y_ref.view(n, h, w, c)[:, ::2, ::2].reshape(q, c)
+    assert _rel(y[:q].float().cpu(), want) < 1e-2
+    assert (y[q:].float() == -7.0).all()  # nothing stored past the compact tensor
     assert _rel(z.float().cpu(), z_ref) < 1e-2
