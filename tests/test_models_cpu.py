@@ -185,3 +185,68 @@ def test_projection_shortcut_merge_resnet50():
     assert ((a - b).abs().max() / a.abs().max()).item() < 1e-4
     # the bf16-emulating oracle runs the merged graph too (folded bias, no BN)
     OracleExecutor(go, w2, emulate_bf16=True).forward(x)
+
+
+def _tiny_graph(h=8, extra_reader=None, shortcut_relu=False):
+    """stem 3x3 -> [1x1 s2 shortcut, 1x1 s2 reduce] -> 3x3 -> 1x1 expand + shortcut -> GAP -> FC."""
+    from distributed_machine_learning_amd.models.graph import Conv, Dense, GlobalAvgPool, Graph
+
+    g = Graph(name="tiny", input_hw=(h, h), preprocess="tf", classes=10)
+    g.tensor("input", h, h, 3)
+    g.tensor("a", h, h, 16)
+    g.add(Conv("c0", "input", "a", 3, 16, 3, 3, 1, 1, 1, 1))
+    g.tensor("b", h, h, 32)
+    g.add(Conv("c1", "a", "b", 16, 32, 3, 3, 1, 1, 1, 1))
+    ho = (h - 1) // 2 + 1
+    g.tensor("s", ho, ho, 64)
+    g.add(Conv("sc", "b", "s", 32, 64, 1, 1, 2, 2, relu=shortcut_relu))
+    g.tensor("r", ho, ho, 16)
+    g.add(Conv("red", "b", "r", 32, 16, 1, 1, 2, 2))
+    g.tensor("m", ho, ho, 16)
+    g.add(Conv("mid", "r", "m", 16, 16, 3, 3, 1, 1, 1, 1))
+    g.tensor("o", ho, ho, 64)
+    g.add(Conv("exp", "m", "o", 16, 64, 1, 1, residual="s"))
+    last = "o"
+    if extra_reader == "3x3":  # a reader that needs every pixel of b
+        g.tensor("e", h, h, 64)
+        g.add(Conv("x3", "b", "e", 32, 64, 3, 3, 1, 1, 1, 1))
+        g.tensor("f", ho, ho, 64)
+        g.add(Conv("x3b", "e", "f", 64, 64, 1, 1, 2, 2, residual="o"))
+        last = "f"
+    g.tensor("gap", 1, 1, 64)
+    g.add(GlobalAvgPool("gap", last, "gap"))
+    g.tensor("logits", 1, 1, 10)
+    g.add(Dense("fc", "gap", "logits", 64, 10))
+    g.validate()
+    return g
+
+
+def test_rewrites_leave_ineligible_graphs_alone():
+    from distributed_machine_learning_amd.models.optimize import merge_projection_shortcut, push_stride_up
+    from distributed_machine_learning_amd.models.weights import init_weights
+
+    g = _tiny_graph()
+    go = push_stride_up(g)
+    assert [n.sh for n in go.nodes if hasattr(n, "sh")] == [1, 2, 1, 1, 1, 1]  # c1 now s2, readers s1
+    # a full-resolution reader of b blocks the pushdown into c1 (its own 1x1 s2 reader x3b
+    # still moves into x3); an odd grid blocks everything
+    by = {n.name: n for n in push_stride_up(_tiny_graph(extra_reader="3x3")).nodes}
+    assert (by["c1"].sh, by["sc"].sh, by["red"].sh, by["x3"].sh, by["x3b"].sh) == (1, 2, 2, 2, 1)
+    gg = _tiny_graph(h=7)
+    assert [n.sh for n in push_stride_up(gg).nodes if hasattr(n, "sh")] == \
+        [n.sh for n in gg.nodes if hasattr(n, "sh")]
+    # the merge needs a linear shortcut (no ReLU)
+    for relu, merged in ((False, True), (True, False)):
+        gg = push_stride_up(_tiny_graph(shortcut_relu=relu))
+        w = init_weights(gg, seed=0)
+        gm = merge_projection_shortcut(gg, w)
+        assert any(n.name == "exp+sc" for n in gm.nodes) == merged
+    # exactness on the tiny graph (pushdown + merge)
+    g = _tiny_graph()
+    w = init_weights(g, seed=1)
+    w2 = dict(w)
+    gm = merge_projection_shortcut(push_stride_up(g), w2)
+    x = torch.randn(2, 3, 8, 8)
+    a = OracleExecutor(g, w).forward(x)["logits"]
+    b = OracleExecutor(gm, w2).forward(x)["logits"]
+    assert ((a - b).abs().max() / a.abs().max()).item() < 1e-4
