@@ -63,6 +63,11 @@ struct Epilogue {
   static constexpr int CROW = BN * 4 + 16;     // fp32 staging row stride (+16 B pad)
   static constexpr int PB = BM / P;            // pixels per pass
   static constexpr int BYTES = PB * CROW;
+  // BN >= 256: the 32+ channel-group lanes of one staging row read 32 B apart, so
+  // lanes 16 apart hit the same banks (512 B = 128 dwords); the row's upper half is
+  // shifted into the row pad by 16 B (4 banks). Row pitch and writer pattern unchanged.
+  static constexpr int HALF = BN >= 256 ? BN * 2 : (1 << 30);
+  __device__ __forceinline__ static int sw(int b) { return b + (b >= HALF ? 16 : 0); }
   static_assert(NT % CG == 0 && (BM * CG) % NT == 0, "epilogue mapping");
   static_assert(PB % 16 == 0 && EIT % P == 0, "epilogue passes");
 
@@ -135,7 +140,7 @@ struct Epilogue {
 #pragma unroll
         for (int i = 0; i < FI; ++i) {
           const int ch = wc * WTC + i * 16 + fq * 4;
-          *(f32x4*)(smem + px * CROW + ch * 4) = acc[i][j];
+          *(f32x4*)(smem + px * CROW + sw(ch * 4)) = acc[i][j];
         }
       }
       __syncthreads();
@@ -145,8 +150,8 @@ struct Epilogue {
         const int m = m0 + px;
         if (m >= M || !ch_ok) continue;
         const int lp = px - pass * PB;
-        const float4 v0 = *(const float4*)(smem + lp * CROW + cg_t * 32);
-        const float4 v1 = *(const float4*)(smem + lp * CROW + cg_t * 32 + 16);
+        const float4 v0 = *(const float4*)(smem + lp * CROW + sw(cg_t * 32));
+        const float4 v1 = *(const float4*)(smem + lp * CROW + sw(cg_t * 32) + 16);
         float f[8] = {v0.x + bias0.x, v0.y + bias0.y, v0.z + bias0.z, v0.w + bias0.w,
                       v1.x + bias1.x, v1.y + bias1.y, v1.z + bias1.z, v1.w + bias1.w};
         if constexpr (RES) {
