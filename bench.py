@@ -12,16 +12,29 @@ the coordinator. Each step = one batch per worker served end to end:
   -> RCCL gather of the packed top-5 results to rank 0 -> host copy at rank 0.
 
 Weak scaling: the per-worker batch is fixed as N grows. ``value`` = total
-images/s over all workers. Data: synthetic uint8 RGB images of the model's input
-size, random-init weights of the exact Keras architecture (no network here).
+images/s over all workers of the headline model (ResNet50 b256, BASELINE config
+2); the same run also measures InceptionV3 b128 (config 3) as the
+``models.InceptionV3`` sub-record. Data: synthetic uint8 RGB images of the
+model's input size, random-init weights of the exact Keras architecture (no
+network here). After the timed steps every rank re-runs its last batch through
+``Engine.infer`` and rank 0 checks the pipeline's gathered top-5 against it.
 
-  python bench.py --gpus N --steps K --warmup W [--model ResNet50|InceptionV3]
+  python bench.py --gpus N --steps K --warmup W [--models ResNet50,InceptionV3]
+
+Launch: under torchrun (WORLD_SIZE set) each process is one rank. Without it and
+with ``--gpus N > 1`` this process becomes a launcher: it spawns N rank
+processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* env, 127.0.0.1 rendezvous) before
+touching the GPU, relays rank 0's JSON line and exits with the worst rank's
+status. ``--dry-run`` replaces the GPU step by the dispatch/gather skeleton on
+gloo (CPU test of the launcher and of the rank plumbing).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,62 +43,95 @@ import time
 # constants worker.py:57-84; BASELINE.md row "Scheduler-predicted query rate").
 REF_BATCH_TIME_S = {"ResNet50": 1 * 10 + 3.5 + 1 + 0.25 * 9, "InceptionV3": 1 * 10 + 5.6 + 2 + 0.325 * 9}
 DEFAULT_BATCH = {"ResNet50": 256, "InceptionV3": 128}
+METRIC = "queries/sec (images/s, whole job) + p50/p90 query latency"
 
 
 def ref_rate(model: str, n: int) -> float:
     return n * 10 / REF_BATCH_TIME_S[model]
 
 
-def main() -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="ResNet50")
-    ap.add_argument("--batch", type=int, default=0, help="per-worker batch (default 256 ResNet50 / 128 InceptionV3)")
+    ap.add_argument("--models", default="ResNet50,InceptionV3",
+                    help="comma list; the first is the headline `value`, the rest are sub-records")
+    ap.add_argument("--model", default="", help="alias: measure only this model")
+    ap.add_argument("--batch", type=int, default=0, help="per-worker batch of the headline model "
+                    "(default 256 ResNet50 / 128 InceptionV3)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--splits", type=int, default=2,
                     help="sub-batches of the per-worker batch, each on its own HIP stream (1 = one engine)")
     ap.add_argument("--streams", type=int, default=0,
                     help="concurrent streams for the sub-batches (default = --splits); sub-batch i on stream i %% S")
+    ap.add_argument("--no-verify", action="store_true", help="skip the post-run top-5 self-check")
     ap.add_argument("--op-times", default="", help="write per-op times (ms) of one forward to this JSON file")
     ap.add_argument("--trace", default="", help="Chrome-trace JSON of the timed steps ('{rank}' -> rank id)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: gloo dispatch/gather skeleton only (tests the launcher)")
+    return ap.parse_args(argv)
 
+
+# ------------------------------------------------------------------ launcher --
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n: int, argv) -> int:
+    """Spawn n rank processes of this script (no GPU call happens here)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+    out = procs[0].stdout
+    for line in iter(out.readline, b""):
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=120))
+        except subprocess.TimeoutExpired:
+            p.kill()  # exact child pid, never a pattern
+            rcs.append(p.wait())
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        print(f"bench launcher: rank exit codes {rcs}", file=sys.stderr)
+        return bad[0] if bad[0] > 0 else 1
+    return 0
+
+
+# ------------------------------------------------------------------ per model --
+def bench_model(model: str, B: int, args, rank: int, world: int, device, headline: bool) -> dict:
+    import numpy as np
     import torch
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from distributed_machine_learning_amd.models import build_model, canonical_name
+    from distributed_machine_learning_amd.models import build_model
     from distributed_machine_learning_amd.models.engine import Engine, SplitEngine
-    from distributed_machine_learning_amd.parallel.dataplane import DESC_FIELDS, DataPlane, init_process_group
+    from distributed_machine_learning_amd.parallel.dataplane import DESC_FIELDS, DataPlane
     from distributed_machine_learning_amd.parallel.pipeline import ServingPipeline
     from distributed_machine_learning_amd.parallel.staging import PinnedImageStore
-
     from distributed_machine_learning_amd.utils import trace as _trace
 
-    model = canonical_name(args.model)
-    B = args.batch or DEFAULT_BATCH[model]
-    rank, world, local = init_process_group()
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
-
     g, w = build_model(model, seed=0, calibrate=True)
-    if args.splits > 1:
-        eng = SplitEngine(g, w, batch=B, device=str(device), src_slots=2, splits=args.splits, streams=args.streams)
+    splits = args.splits if B % max(args.splits, 1) == 0 else 1
+    if splits > 1:
+        eng = SplitEngine(g, w, batch=B, device=str(device), src_slots=2, splits=splits, streams=args.streams)
     else:
         eng = Engine(g, w, batch=B, device=str(device), src_slots=2)
     store = PinnedImageStore(capacity=4 * B, hw=g.input_hw)
     store.fill_synthetic(seed=rank)
     dp = DataPlane(device, result_shape=(2, B, 5))
     pipe = ServingPipeline(eng, store, dp, use_graph=not args.no_graph)
-
     cap = store.capacity
 
     def table(k):
-        import numpy as np
-
         t = np.zeros((world, DESC_FIELDS), np.int64)
         for r in range(world):
             t[r] = (31, k * world + r, 0, (k * B) % cap, B, dp.epoch)
@@ -95,7 +141,7 @@ def main() -> int:
     pipe.run(max(args.warmup, 1), table, record=False)
     pipe.stats.latencies_s.clear()
     pipe.stats.images = 0
-    if args.trace:
+    if args.trace and headline:
         _trace.set_tracer(_trace.Tracer(process_name=f"bench rank {rank}", pid=rank))
 
     dp.barrier()
@@ -106,43 +152,142 @@ def main() -> int:
     dp.barrier()
     elapsed = dp.max_over_ranks(time.perf_counter() - t0)
 
-    if args.trace:
+    verified = None
+    if not args.no_verify:
+        # the last timed step's gathered rows vs a fresh Engine.infer of the same images
+        last = args.steps - 1
+        got = pipe.host_res[last % 2].clone() if rank == 0 else None
+        start = (last * B) % cap
+        idx = [(start + i) % cap for i in range(B)]
+        ti, tp = eng.infer(torch.from_numpy(store.array[idx]).to(device))
+        expect = torch.stack([ti.to(torch.int32), tp.contiguous().view(torch.int32)])
+        torch.cuda.synchronize()
+        bufs = dp.gather(expect.contiguous())
+        if rank == 0:
+            exp = torch.stack([b.cpu() for b in bufs])
+            verified = bool(torch.equal(exp, got))
+            if not verified:
+                bad_ids = (exp[:, 0] != got[:, 0]).sum().item()
+                print(f"bench: {model} pipeline top-5 differs from Engine.infer ({bad_ids} ids)", file=sys.stderr)
+
+    if args.trace and headline:
         tr = _trace.get_tracer()
         tr.add_gpu_ops(eng.time_ops(torch.cuda.current_stream()), lane="one sub-batch forward, per op")
         tr.export_chrome(args.trace.replace("{rank}", str(rank)))
+        _trace.set_tracer(_trace.Tracer(enabled=False))
     if args.op_times and rank == 0:
         times = eng.time_ops(torch.cuda.current_stream())
-        with open(args.op_times, "w") as f:
-            json.dump({"model": model, "batch": B // max(args.splits, 1), "ops": times,
+        path = args.op_times if headline else args.op_times.replace(".json", f"_{model}.json")
+        with open(path, "w") as f:
+            json.dump({"model": model, "batch": B // max(splits, 1), "ops": times,
                        "cfg": eng.op_cfg, "total_ms": sum(t for _, t in times)}, f, indent=1)
 
+    rec = None
     if rank == 0:
-        total_images = world * B * args.steps
-        value = total_images / elapsed
+        value = world * B * args.steps / elapsed
         pct = stats.percentiles()
-        out = {
-            "metric": "queries/sec (images/s, whole job) + p50/p90 query latency",
+        rec = {
             "value": round(value, 2),
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "vs_baseline": round(value / ref_rate(model, world), 1),
+            "p50_latency_ms": round(pct.get("p50_ms", 0.0), 3),
+            "p90_latency_ms": round(pct.get("p90_ms", 0.0), 3),
+            "p99_latency_ms": round(pct.get("p99_ms", 0.0), 3),
+            "verified_top5": verified,
+            "config": {"model": model, "global_batch": B * world, "seq_len": None,
+                       "image_hw": list(g.input_hw), "parallelism": f"dp{world}",
+                       "per_worker_batch": B, "graph": not args.no_graph, "stream_splits": splits,
+                       "streams": eng.nstreams if splits > 1 else 1},
+            "baseline": {"source": "BASELINE.md scheduler-predicted query rate (cost model, CS425 VMs, TF CPU)",
+                         "value": round(ref_rate(model, world), 3), "unit": "images/s"},
+        }
+    del pipe, eng, store, dp
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return rec
+
+
+def bench_dry(model: str, B: int, args, rank: int, world: int) -> dict:
+    """The rank plumbing without a GPU: gloo dispatch + gather per step."""
+    import numpy as np
+    import torch
+
+    from distributed_machine_learning_amd.parallel.dataplane import DESC_FIELDS, DataPlane
+
+    dp = DataPlane(torch.device("cpu"), result_shape=(2, B, 5))
+    res = torch.zeros((2, B, 5), dtype=torch.int32)
+    table = np.zeros((world, DESC_FIELDS), np.int64)
+    for _ in range(args.warmup):
+        dp.dispatch(table if rank == 0 else None)
+        dp.gather(res)
+    dp.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        row = dp.dispatch(table if rank == 0 else None)
+        res[0, 0, 0] = int(row[1])
+        dp.gather(res)
+    dp.barrier()
+    elapsed = dp.max_over_ranks(time.perf_counter() - t0)
+    if rank:
+        return None
+    return {"value": round(world * B * args.steps / elapsed, 2), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "vs_baseline": None, "verified_top5": None,
+            "config": {"model": model, "global_batch": B * world, "seq_len": None, "parallelism": f"dp{world}",
+                       "per_worker_batch": B}}
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch(args.gpus, argv)
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from distributed_machine_learning_amd.models import canonical_name
+    from distributed_machine_learning_amd.parallel.dataplane import init_process_group
+
+    models = [canonical_name(m) for m in (args.model or args.models).split(",") if m]
+    rank, world, local = init_process_group(backend="gloo" if args.dry_run else None)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    device = None
+    if not args.dry_run:
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(device)
+
+    recs = {}
+    for i, m in enumerate(models):
+        B = (args.batch if i == 0 and args.batch else 0) or DEFAULT_BATCH[m]
+        if args.dry_run:
+            recs[m] = bench_dry(m, B, args, rank, world)
+        else:
+            recs[m] = bench_model(m, B, args, rank, world, device, headline=(i == 0))
+
+    if rank == 0:
+        head = recs[models[0]]
+        out = {
+            "metric": METRIC,
+            "value": head["value"],
             "unit": "images/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / ref_rate(model, world), 1),
+            "vs_baseline": head["vs_baseline"],
             "dtype": "bf16",
-            "data": "synthetic uint8 RGB images, random-init weights (Keras architecture)",
-            "config": {"model": model, "global_batch": B * world, "seq_len": None,
-                       "image_hw": list(g.input_hw), "parallelism": f"dp{world}",
-                       "per_worker_batch": B, "graph": not args.no_graph, "stream_splits": args.splits,
-                       "streams": eng.nstreams if args.splits > 1 else 1},
-            "p50_latency_ms": round(pct.get("p50_ms", 0.0), 3),
-            "p90_latency_ms": round(pct.get("p90_ms", 0.0), 3),
-            "p99_latency_ms": round(pct.get("p99_ms", 0.0), 3),
-            "baseline": {"source": "BASELINE.md scheduler-predicted query rate (cost model, CS425 VMs, TF CPU)",
-                         "value": round(ref_rate(model, world), 3), "unit": "images/s"},
+            "data": ("dry-run: dispatch/gather skeleton only, no compute" if args.dry_run else
+                     "synthetic uint8 RGB images, random-init weights (Keras architecture)"),
+            "config": head["config"],
         }
+        for k in ("p50_latency_ms", "p90_latency_ms", "p99_latency_ms", "verified_top5", "baseline"):
+            if k in head:
+                out[k] = head[k]
+        if len(models) > 1:
+            out["models"] = {m: recs[m] for m in models[1:]}
         print(json.dumps(out), flush=True)
     import torch.distributed as dist
 
