@@ -254,10 +254,15 @@ extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
       dml_set_error("dml_conv(v2): split-K needs a v2 config, fp32 output, no residual/segments/ReLU, split_ld");
       return -1;
     }
+    if (a->kchunk && (cfg >= 40 || a->kchunk < 0 || a->kchunk % 64 || a->Cin % a->kchunk || a->dh > 1 ||
+                      a->dw > 1)) {
+      dml_set_error("dml_conv(v2): chunk-major K order needs a v2 config, kchunk%64==0, Cin%kchunk==0, no dilation");
+      return -1;
+    }
     return cfg >= 40 ? dml_conv_halo(a, cfg, s) : dml_conv_v2(a, cfg, s);
   }
-  if (a->nseg > 0 || a->ksplit > 1 || a->rsub > 1) {
-    dml_set_error("dml_conv: output segments / split-K / subsampled residual need a v2 config (cfg >= 10)");
+  if (a->nseg > 0 || a->ksplit > 1 || a->rsub > 1 || a->kchunk) {
+    dml_set_error("dml_conv: output segments / split-K / subsampled residual / chunk-major K need a v2 config (cfg >= 10)");
     return -1;
   }
   if (a->Cin % 8 || a->ldx % 8 || a->Cout % 4 || a->Kpad % 64) {

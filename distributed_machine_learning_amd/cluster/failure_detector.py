@@ -126,10 +126,10 @@ class FailureDetector:
 
     async def leave(self) -> None:
         """Graceful leave: tell the ring, then stop probing/acking."""
+        self.enabled = False  # before ml.leave(): a round() in between must not probe from a LEFT self
         self.ml.leave()
         for t in self.ml.alive(include_self=False):
             await self.ep.send(t, MsgType.LEAVE, {"members": self.ml.digest()})
-        self.enabled = False
 
     async def join(self, introducer: str, timeout: float = 1.0, retries: int = 3) -> bool:
         """INTRODUCE to a known member (the leader / introducer) and merge its list."""

@@ -86,7 +86,7 @@ class MembershipList:
     def ring_targets(self) -> List[str]:
         """Probe targets: [+1, -1, +4] neighbours of self over the sorted alive ring."""
         ring = self.alive(include_self=True)
-        if len(ring) <= 1:
+        if len(ring) <= 1 or self.self_name not in ring:  # self LEFT / not alive: nothing to probe
             return []
         i = ring.index(self.self_name)
         out: List[str] = []

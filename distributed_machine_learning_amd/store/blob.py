@@ -14,6 +14,7 @@ provides the same interface for in-process tests.
 from __future__ import annotations
 
 import asyncio
+import logging
 import json
 import struct
 import uuid
@@ -22,6 +23,8 @@ from typing import Dict, List, Optional, Tuple
 from .local_store import LocalFileStore
 
 _LEN = struct.Struct(">qI")  # length (-1 = not found), version
+
+log = logging.getLogger(__name__)
 
 
 class BlobSource:
@@ -78,7 +81,15 @@ class BlobServer:
                 line = await reader.readline()
                 if not line:
                     break
-                items = self.source.read(json.loads(line))
+                try:
+                    items = self.source.read(json.loads(line))
+                except (ConnectionError, asyncio.CancelledError):
+                    raise
+                except Exception as e:  # bad request / name / version evicted mid get_all
+                    log.warning("blob server: request failed (%s: %s)", type(e).__name__, e)
+                    writer.write(struct.pack(">i", -1))  # explicit error reply, connection stays usable
+                    await writer.drain()
+                    continue
                 writer.write(struct.pack(">i", len(items)))
                 for v, data in items:
                     writer.write(_LEN.pack(len(data), v))
@@ -113,6 +124,8 @@ class TcpBlobClient:
             writer.write((json.dumps(req) + "\n").encode())
             await writer.drain()
             (n,) = struct.unpack(">i", await asyncio.wait_for(reader.readexactly(4), timeout))
+            if n < 0:
+                raise ConnectionError(f"blob server {node} could not serve {req}")
             out = []
             for _ in range(n):
                 ln, v = _LEN.unpack(await asyncio.wait_for(reader.readexactly(_LEN.size), timeout))
@@ -120,6 +133,8 @@ class TcpBlobClient:
                 self.bytes_fetched += ln
                 out.append((v, data))
             return out
+        except asyncio.IncompleteReadError as e:  # peer closed mid-reply: an EOFError, not an OSError
+            raise ConnectionError(f"blob server {node} closed the connection mid-reply") from e
         finally:
             writer.close()
 

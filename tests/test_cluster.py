@@ -259,3 +259,13 @@ def test_udp_transport_request_reply():
         e2.stop()
 
     asyncio.run(main())
+
+
+def test_ring_targets_empty_after_leave():
+    """leave() marks self LEFT; a probe round afterwards must not raise (it used to
+    call ring.index(self) on an alive-list without self and kill the FD task)."""
+    ml = MembershipList("a:1")
+    ml.merge({"b:1": [0, 1, {}], "c:1": [0, 1, {}]})
+    assert ml.ring_targets()
+    ml.leave()
+    assert ml.ring_targets() == []

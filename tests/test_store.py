@@ -121,3 +121,30 @@ def test_tcp_blob_server(tmp_path):
         srv.close()
 
     asyncio.run(main())
+
+
+def test_tcp_blob_server_bad_request_replies_error(tmp_path):
+    """A request the source cannot serve (no "name" key, evicted version) gets an
+    explicit error reply (ConnectionError at the client, so callers try the next
+    holder) and the server keeps serving."""
+    async def main():
+        st = LocalFileStore(str(tmp_path / "a"))
+        st.put_bytes("f", b"v1")
+        src = BlobSource(st)
+        srv = await BlobServer(src).start()
+        cli = TcpBlobClient(lambda n: srv.addr)
+        with pytest.raises(ConnectionError):
+            await cli.fetch("a", {"op": "get"})  # KeyError in the source
+        orig = src.read
+
+        def evicted(req):
+            if req.get("op") == "get_all":
+                raise FileNotFoundError("version evicted mid get_all")
+            return orig(req)
+        src.read = evicted
+        with pytest.raises(ConnectionError):
+            await cli.fetch("a", {"op": "get_all", "name": "f"})
+        assert await cli.fetch("a", {"op": "get", "name": "f", "version": 1}) == [(1, b"v1")]
+        srv.close()
+
+    asyncio.run(main())
