@@ -52,10 +52,14 @@ class Election:
         m = self.ml.get(name)
         return m is not None and bool(m.meta.get("eligible"))
 
-    def priority(self, name: str) -> Tuple[int, str]:
+    def priority(self, name: str) -> Tuple[int, int, str]:
+        """(standby flag, numeric ``prio`` meta, name): the RCCL service's rank
+        nodes carry prio = global rank, so the highest alive rank leads — the
+        same rank the collective service picks as its coordinator."""
         m = self.ml.get(name)
         standby = 1 if (m is not None and m.meta.get("role") == "standby") else 0
-        return standby, name
+        prio = int(m.meta.get("prio", 0)) if m is not None else 0
+        return standby, prio, name
 
     def candidates(self) -> List[str]:
         return sorted((n for n in self.ml.alive() if self.eligible(n)), key=self.priority, reverse=True)

@@ -26,7 +26,7 @@ def build_graph(name: str) -> Graph:
     return MODELS[canonical_name(name)]()
 
 
-def build_model(name: str, seed: int = 0, calibrate: bool = True, calib_batch: int = 2) -> Tuple[Graph, Weights]:
+def build_model(name: str, seed: int = 0, calibrate: bool = True, calib_batch: int = 32) -> Tuple[Graph, Weights]:
     """Graph + deterministic random-init weights (optionally BN-calibrated on
     synthetic images so activations stay normalised through the depth)."""
     g = build_graph(name)

@@ -18,9 +18,26 @@ from .graph import Conv, Dense, Graph
 Weights = Dict[str, np.ndarray]
 
 
+# Numerically well-conditioned random init. A random-init deep ReLU net with
+# per-channel normalisation is chaotic: bf16 rounding at every layer is amplified
+# through the depth (fp32 vs bf16-emulated logits differed by 12 % / 20 % max-rel
+# on ResNet50 / InceptionV3 with the plain init, top-1 agreement 81 % / 63 %),
+# which made any whole-network numerics check loose. Two standard remedies:
+#  * residual nets: the BN gamma of each residual branch's last conv is scaled
+#    by RES_GAMMA (the "zero-gamma" residual init of Goyal et al., 2017): the
+#    identity path dominates -> ResNet50 gap 0.4 %, top-5 identical;
+#  * nets without residuals (InceptionV3, BN without scale): BN beta shifted by
+#    BETA_SHIFT before calibration, so ReLUs operate mostly in their linear
+#    region -> InceptionV3 gap 3.6 %, top-1 identical, top-5 overlap >= 4/5
+#    (32 images; /tmp experiment recorded in DESIGN.md §3 "Numerics").
+RES_GAMMA = 0.25
+BETA_SHIFT = 1.0
+
+
 def init_weights(g: Graph, seed: int = 0) -> Weights:
     rng = np.random.default_rng(seed)
     w: Weights = {}
+    residual_net = any(isinstance(n, Conv) and n.residual for n in g.nodes)
     for n in g.nodes:
         if isinstance(n, Conv):
             fan_in = n.kh * n.kw * n.cin
@@ -29,8 +46,14 @@ def init_weights(g: Graph, seed: int = 0) -> Weights:
                 w[f"{n.name}/bias"] = (rng.standard_normal(n.cout) * 0.05).astype(np.float32)
             if n.bn:
                 if n.bn_scale:
-                    w[f"{n.name}/gamma"] = rng.uniform(0.8, 1.2, n.cout).astype(np.float32)
-                w[f"{n.name}/beta"] = (rng.standard_normal(n.cout) * 0.1).astype(np.float32)
+                    gam = rng.uniform(0.8, 1.2, n.cout)
+                    if n.residual:  # last conv of a residual branch
+                        gam = gam * RES_GAMMA
+                    w[f"{n.name}/gamma"] = gam.astype(np.float32)
+                beta = rng.standard_normal(n.cout) * 0.1
+                if not residual_net:
+                    beta = beta + BETA_SHIFT
+                w[f"{n.name}/beta"] = beta.astype(np.float32)
                 w[f"{n.name}/mean"] = (rng.standard_normal(n.cout) * 0.1).astype(np.float32)
                 w[f"{n.name}/var"] = rng.uniform(0.5, 1.5, n.cout).astype(np.float32)
         elif isinstance(n, Dense):

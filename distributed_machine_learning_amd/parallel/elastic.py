@@ -3,15 +3,24 @@
 RCCL is not elastic — a rank that dies mid-collective hangs its peers (SURVEY
 §7.4 item 3). The recovery protocol here:
 
- * a persistent TCPStore hosted by global rank 0 (the coordinator) outlives
-   every communicator; communicator *epoch e* is initialised through
-   ``PrefixStore("epoch<e>", store)`` over the current member list;
+ * the rendezvous store is a ``FileStore`` on the node's local filesystem (one
+   node = one filesystem; 8 GPUs per MI355X node), so NO rank hosts it: any rank,
+   the coordinator included, can die without taking the rendezvous with it (the
+   previous TCPStore lived inside global rank 0). A TCPStore host can still be
+   given for multi-node runs (``store_host``), at the price of that single host;
+ * communicator *epoch e* is initialised through ``PrefixStore("epoch<e>")`` over
+   the epoch's member list;
  * liveness comes from the host-side SWIM detector (cluster/), never from the
-   collective library; collectives are issued ``async_op=True`` and polled, so
-   a rank declared dead while a collective is pending makes the survivors
-   ``abort()`` the communicator instead of hanging;
- * the coordinator publishes the survivor list for epoch e+1 in the store; every
-   survivor reads it, tears down epoch e and joins epoch e+1 with its new rank.
+   collective library; collectives are issued ``async_op=True`` and polled
+   (``Work.is_completed``), so a rank declared dead while a collective is pending
+   makes the survivors ABORT the communicator (``_abort_process_group``: on RCCL
+   this is ncclCommAbort, which also releases the collective kernels still queued
+   on RCCL's own stream) instead of hanging. The host never calls ``Work.wait``
+   before the poll has seen completion, so no compute stream is ever ordered
+   behind a collective that will not finish;
+ * agreement on the next member list: every survivor proposes its own survivor
+   view with ``compare_set(members<e+1>)`` — the first proposal wins, everyone
+   adopts it (a rank not in it leaves), then joins epoch e+1 with its new rank.
 
 Works identically on gloo (CPU tests) and nccl (= RCCL on ROCm).
 """
@@ -22,10 +31,11 @@ import json
 import logging
 import os
 import time
-from typing import Callable, List, Optional, Set
+from typing import List, Optional, Set
 
 import torch
 import torch.distributed as dist
+from torch.distributed import distributed_c10d as c10d
 
 log = logging.getLogger(__name__)
 
@@ -34,16 +44,29 @@ class CollectiveFailure(RuntimeError):
     """A collective could not complete (peer died / communicator aborted)."""
 
 
+def default_store_path(tag: str) -> str:
+    base = os.environ.get("DML_RDZV_DIR", "/tmp")
+    return os.path.join(base, f"dml_rdzv_{tag}")
+
+
 class ElasticGroup:
-    def __init__(self, global_rank: int, world: int, host: str = "127.0.0.1", port: int = 29555,
-                 backend: str = "gloo", device: Optional[torch.device] = None, timeout_s: float = 60.0):
+    def __init__(self, global_rank: int, world: int, store_path: Optional[str] = None, backend: str = "gloo",
+                 device: Optional[torch.device] = None, timeout_s: float = 60.0, store_host: Optional[str] = None,
+                 store_port: int = 0):
         self.grank, self.backend, self.device = global_rank, backend, device
         self.members: List[int] = list(range(world))
         self.epoch = 0
         self.timeout = datetime.timedelta(seconds=timeout_s)
-        self.store = dist.TCPStore(host, port, world_size=None, is_master=(global_rank == 0),
-                                   timeout=self.timeout, wait_for_workers=False)
+        if store_host is not None:  # multi-node: a TCPStore on one host (that host is then a SPOF)
+            self.store = dist.TCPStore(store_host, store_port, world_size=None, is_master=(global_rank == 0),
+                                       timeout=self.timeout, wait_for_workers=False)
+        else:
+            if store_path is None:
+                raise ValueError("ElasticGroup needs a store_path (FileStore) or a store_host")
+            self.store = dist.FileStore(store_path, -1)
+            self.store.set_timeout(self.timeout)
         self.dead: Set[int] = set()          # fed by the failure detector (thread-safe set ops)
+        self.aborts = 0
         self._init_pg()
 
     # --------------------------------------------------------------- group --
@@ -55,6 +78,9 @@ class ElasticGroup:
     def world(self) -> int:
         return len(self.members)
 
+    def group_rank_of(self, grank: int) -> int:
+        return self.members.index(grank)
+
     def _init_pg(self) -> None:
         prefix = dist.PrefixStore(f"epoch{self.epoch}", self.store)
         kw = {}
@@ -64,17 +90,20 @@ class ElasticGroup:
                                 timeout=self.timeout, **kw)
         log.info("rank %d joined epoch %d (%d members)", self.grank, self.epoch, self.world)
 
-    def _teardown(self) -> None:
-        try:
-            pg = dist.group.WORLD
-            if pg is not None and hasattr(pg, "abort"):
-                pg.abort()
-        except Exception:  # pragma: no cover - best effort
-            pass
+    def _teardown(self, abort: bool) -> None:
+        """End the current communicator. ``abort``: a collective may still be
+        pending (a peer died) — abort it explicitly (RCCL: ncclCommAbort) so
+        nothing waits on it, then destroy the group."""
+        if not dist.is_initialized():
+            return
+        if abort and self.backend == "nccl":
+            c10d._abort_process_group()   # NCCL/RCCL backend abort (no hasattr probing)
+            self.aborts += 1
+            return  # the abort destroyed the default group
         try:
             dist.destroy_process_group()
-        except Exception:  # pragma: no cover
-            pass
+        except Exception as e:  # gloo: a dead peer's socket may already be closed
+            log.debug("destroy_process_group: %s", e)
 
     # -------------------------------------------------------- collectives --
     def wait(self, work, poll_s: float = 0.0002) -> None:
@@ -91,39 +120,45 @@ class ElasticGroup:
         except Exception as e:  # gloo raises when a peer's socket closes
             raise CollectiveFailure(str(e)) from e
 
-    def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
+    def _run(self, fn, *args, **kw) -> None:
         try:
-            w = dist.broadcast(t, src=src, async_op=True)
+            w = fn(*args, async_op=True, **kw)
         except Exception as e:
             raise CollectiveFailure(str(e)) from e
         self.wait(w)
 
-    def gather(self, t: torch.Tensor, bufs: Optional[List[torch.Tensor]]) -> None:
-        try:
-            w = dist.gather(t, bufs if self.rank == 0 else None, dst=0, async_op=True)
-        except Exception as e:
-            raise CollectiveFailure(str(e)) from e
-        self.wait(w)
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
+        """``src`` is a GROUP rank."""
+        self._run(dist.broadcast, t, src=src)
+
+    def gather(self, t: torch.Tensor, bufs: Optional[List[torch.Tensor]], dst: int = 0) -> None:
+        self._run(dist.gather, t, bufs if self.rank == dst else None, dst=dst)
+
+    def all_gather(self, bufs: List[torch.Tensor], t: torch.Tensor) -> None:
+        self._run(dist.all_gather, bufs, t)
+
+    def barrier(self) -> None:
+        t = torch.zeros(1, device=self.device if self.backend == "nccl" else "cpu")
+        self._run(dist.all_reduce, t)
 
     # ------------------------------------------------------------ rebuild --
-    def rebuild(self, dead: Set[int], decide: bool) -> None:
-        """Move to epoch+1 over the survivors. The coordinator (``decide=True``)
-        publishes the member list; everyone else reads it from the store."""
+    def rebuild(self, dead: Set[int], decide: bool = True) -> List[int]:
+        """Move to epoch+1 over the survivors. Every survivor proposes its view
+        of the member list; the first proposal in the store wins (compare-set),
+        so all survivors adopt the same list without a designated decider."""
         nxt = self.epoch + 1
         key = f"members{nxt}"
-        if decide:
-            members = [m for m in self.members if m not in dead]
-            self.store.set(key, json.dumps(members))
-        else:
-            self.store.wait([key], self.timeout)
-            members = json.loads(self.store.get(key))
-        self._teardown()
+        mine = [m for m in self.members if m not in dead]
+        won = self.store.compare_set(key, "", json.dumps(mine))
+        members = json.loads(won)
+        self._teardown(abort=True)
         if self.grank not in members:
             raise CollectiveFailure("this rank was removed from the group")
         self.members = members
         self.epoch = nxt
         self.dead.intersection_update(self.members)  # forget the removed ranks
         self._init_pg()
+        return members
 
     def close(self) -> None:
-        self._teardown()
+        self._teardown(abort=False)

@@ -1,32 +1,58 @@
-"""Elastic multi-GPU serving: coordinator on rank 0, one worker per GPU, RCCL
-data plane, SWIM liveness, fair-share scheduling, failure re-dispatch.
+"""Elastic multi-GPU serving: one process per GPU, RCCL data plane, a
+REPLICATED coordinator, SWIM liveness, the reference's CLI and store.
 
-Bulk-synchronous steps (BASELINE configs 4 and 5):
+Reference: the leader (H1) owns all job state and relays submits/ACKs to one
+hard-coded standby (H2) over UDP (worker.py:176-495, 887-1037, 577-614); if both
+die nothing can take over (election.py:27). Here every rank holds the whole
+coordinator state as a replicated state machine driven by the step's
+collectives, so ANY survivor can continue as coordinator:
 
-  rank 0 (coordinator)  JobManager queues -> fair-share plan over the alive
-                        ranks -> descriptor table [world, 6]
-  all ranks             RCCL broadcast of the table (control: 48 B per rank)
-  each rank             stage its image range (pinned host -> HBM) and run its
-                        assigned model's engine (both models resident in HBM)
-  all ranks             RCCL gather of packed top-5 results to rank 0
-  rank 0                completes batches (C1/C2 metrics, job completion,
-                        output_<job>_<batch>_<host>.json via a writer thread)
+  step k (every rank, lockstep, lag-1 pipelined):
+    coordinator  drains its control inbox (client submits / C3 from the CLI) into
+                 log records, applies them, plans step k's dispatch table
+    broadcast    header [log length, step, table] from the coordinator (48 B per
+                 rank), then the log payload (JSON) if any
+    every rank   applies the same log records and the same table -> identical
+                 queues, in-flight sets and job-id counters on every rank
+    every rank   launches its own batch of step k (async on the GPU: arena slots
+                 -> H2D -> hipGraph forward), then ALL-GATHERS step k-1's packed
+                 top-5 results [2, cap, 5] int32 -> every rank completes step k-1
+                 identically (C1 counts, job completion); the coordinator also
+                 writes output_<job>_<batch>_<host>.json and PUTs it into the store
 
-A rank that dies is detected by SWIM; pending collectives abort, rank 0
-requeues the step's in-flight batches at the FRONT of their queues (at-least-
-once, like the reference's requeue, worker.py:1284-1306), survivors re-form
-the communicator at epoch+1 and serving continues over fewer workers.
-Both models' per-batch times are balanced by per-model batch sizes (C3).
+  The coordinator is the highest alive global rank — the same rank the
+  control plane's bully election (cluster/election.py, prio = rank) makes the
+  store leader, so the CLI's leader requests reach it.
+
+Failure: SWIM (host UDP, never RCCL) confirms a dead rank -> pending collectives
+are aborted (parallel/elastic.py) -> every survivor requeues all in-flight
+batches at the FRONT of their queues (identical replicas, so identical result)
+-> the communicator is rebuilt over the survivors (FileStore rendezvous: no rank
+hosts it) -> the new coordinator broadcasts its full job state (repairs any
+replica that completed one step more or less than it did) and re-PUTs the output
+files of the last completed steps (a dead coordinator may not have written them:
+at-least-once outputs). Batches may run twice; every job completes.
+
+Images: a job names store images (cyclic pick over the sorted ``*.jpeg``
+listing, reference worker.py:176-206) or synthetic arena images. Each rank
+decodes a store image ONCE into its per-model pinned arena (name -> slot, LRU);
+a batch is a list of arena slots, staged with coalesced hipMemcpyAsync. C3
+(per-model batch size) is a replicated log record, clamped to the result
+capacity; a batch larger than the engine's batch runs as several engine passes
+(never truncated).
 """
 from __future__ import annotations
 
+import asyncio
+import json
 import logging
 import os
 import queue
 import threading
 import time
-from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -36,69 +62,206 @@ from ..serving.jobs import MODELS, Batch, JobManager
 from ..serving.metrics import Metrics
 from ..serving.output import decode_top5, dumps, output_name
 from ..serving.scheduler import plan
-from .dataplane import DESC_FIELDS, F_BATCH, F_COUNT, F_EPOCH, F_JOB, F_MODEL, F_START
+from .dataplane import DESC_FIELDS, F_BATCH, F_JOB, F_MODEL
 from .elastic import CollectiveFailure, ElasticGroup
 
 log = logging.getLogger(__name__)
 MODEL_IDS = {m: i for i, m in enumerate(MODELS)}
 IDLE, STOP = -1, -2
+SYNTH = "synthetic:"          # synthetic arena image names: "synthetic:<index>"
+HDR = 3                       # header words before the table: log length, step, flags
+RESULT_HISTORY = 64           # completed steps whose results every rank keeps (output re-PUT on takeover)
 
 
-# ------------------------------------------------------------- backends ----
+def synthetic_names(n: int) -> List[str]:
+    return [f"{SYNTH}{i}" for i in range(n)]
+
+
+# ----------------------------------------------------------------- arenas ----
+class ImageArena:
+    """Per-model uint8 image arena with a name -> slot index (decode once).
+
+    Slots [0, n_synth) hold synthetic images (``synthetic:<i>`` -> slot
+    i % n_synth); the rest is an LRU cache of decoded store images. ``pinned``
+    arenas live in hipHostMalloc'ed memory (GPU backends stage from them with
+    hipMemcpyAsync); host backends use a numpy array."""
+
+    def __init__(self, capacity: int, hw: Tuple[int, int], pinned: bool = False, n_synth: int = 0, seed: int = 0):
+        if n_synth >= capacity:
+            raise ValueError("arena needs room beyond its synthetic images")
+        self.capacity, self.hw, self.n_synth = capacity, tuple(hw), n_synth
+        if pinned:
+            from .staging import PinnedImageStore
+
+            self.pinned = PinnedImageStore(capacity, self.hw)
+            self.array = self.pinned.array
+        else:
+            self.pinned = None
+            self.array = np.zeros((capacity, *self.hw, 3), np.uint8)
+        if n_synth:
+            rng = np.random.default_rng(seed)
+            for i in range(0, n_synth, 64):
+                j = min(n_synth, i + 64)
+                self.array[i:j] = rng.integers(0, 256, size=(j - i, *self.hw, 3), dtype=np.uint8)
+        self.index: "OrderedDict[str, int]" = OrderedDict()
+        self.free = list(range(capacity - 1, n_synth - 1, -1))
+        self.decoded = 0
+
+    def slots(self, names: Sequence[str], loader: Callable[[List[str]], Dict[str, Optional[np.ndarray]]]
+              ) -> Tuple[List[int], List[str]]:
+        """Arena slots of ``names`` (loading the missing ones through ``loader``);
+        returns (slots, failed names). A failed image gets slot 0 (its row is
+        computed but reported as failed)."""
+        synth = self.n_synth > 0
+        missing = []
+        for n in names:
+            if not (synth and n.startswith(SYNTH)) and n not in self.index and n not in missing:
+                missing.append(n)
+        failed = set()
+        if missing:
+            got = loader(missing)
+            keep = set(names)
+            for n in missing:
+                img = got.get(n)
+                if img is None:
+                    failed.add(n)
+                    continue
+                if not self.free:  # evict the least recently used image not needed now
+                    victim = next((k for k in self.index if k not in keep), None)
+                    if victim is None:
+                        raise RuntimeError("image arena too small for one batch")
+                    self.free.append(self.index.pop(victim))
+                s = self.free.pop()
+                self.array[s] = img
+                self.index[n] = s
+                self.decoded += 1
+        out = []
+        for n in names:
+            if synth and n.startswith(SYNTH):
+                out.append(int(n[len(SYNTH):]) % self.n_synth)
+            elif n in failed:
+                out.append(0)
+            else:
+                self.index.move_to_end(n)
+                out.append(self.index[n])
+        return out, sorted(failed)
+
+
+# --------------------------------------------------------------- backends ----
 class RankBackend:
-    """Runs one batch of images [start, start+count) of `model` on this rank.
+    """Runs one batch (a list of image names) of ``model`` on this rank.
 
     ``launch`` is asynchronous on GPU backends: it enqueues staging + forward and
-    returns (result [2, max_batch, 5] int32, completion event or None), so the
-    service can gather the previous step's results while this batch computes.
-    """
+    returns (result [2, cap, 5] int32, completion event or None) — rows of
+    images that could not be fetched or decoded carry class id -1 — so the
+    service gathers the previous step's results while this batch runs.
+    ``cap`` (result rows) bounds the batch size the coordinator may assign."""
 
-    max_batch: int = 256
+    cap: int = 256
     device = torch.device("cpu")
 
-    def launch(self, model: str, start: int, count: int, slot: int):
+    def launch(self, model: str, names: Sequence[str], slot: int):
         raise NotImplementedError
 
-    def run(self, model: str, start: int, count: int) -> torch.Tensor:
-        res, ev = self.launch(model, start, count, 0)
+    def run(self, model: str, names: Sequence[str]) -> torch.Tensor:
+        res, ev = self.launch(model, names, 0)
         if ev is not None:
             ev.synchronize()
         return res
 
 
-class FakeRankBackend(RankBackend):
-    """Deterministic results, optional per-image delay (CPU tests)."""
+class HostRankBackend(RankBackend):
+    """A serving.inference backend (fake / cpu) behind the rank interface:
+    decode-once per image name (LRU cache), synchronous predict. The same
+    backend classes as the host cluster's workers, so both serving modes produce
+    identical outputs for the same images. Synthetic names decode from their own
+    name bytes; failed images get class id -1 in their result row."""
 
-    def __init__(self, max_batch: int = 16, delay_per_image: float = 0.0):
-        self.max_batch, self.delay = max_batch, delay_per_image
+    def __init__(self, backend, loader: Optional[Callable] = None, cap: int = 256, delay_per_image: float = 0.0,
+                 cache_images: int = 4096):
+        self.be, self.loader, self.cap, self.delay = backend, loader, cap, delay_per_image
+        self.cache: "OrderedDict[Tuple[str, str], np.ndarray]" = OrderedDict()
+        self.cache_images = cache_images
 
-    def launch(self, model, start, count, slot):
+    def _blobs(self, names: List[str]) -> Dict[str, Optional[bytes]]:
+        out = {n: n.encode() for n in names if n.startswith(SYNTH)}
+        rest = [n for n in names if not n.startswith(SYNTH)]
+        if rest:
+            out.update(self.loader(rest) if self.loader else {n: None for n in rest})
+        return out
+
+    def launch(self, model, names, slot):
+        if len(names) > self.cap:
+            raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
         if self.delay:
-            time.sleep(self.delay * count)
-        out = torch.zeros((2, self.max_batch, 5), dtype=torch.int32)
-        i = torch.arange(count, dtype=torch.int32)[:, None] + start
-        out[0, :count] = (i * 7 + torch.arange(5, dtype=torch.int32)[None] + MODEL_IDS[model] * 100) % 1000
-        out[1, :count] = torch.tensor([0.5, 0.2, 0.1, 0.05, 0.01]).view(torch.int32)
+            time.sleep(self.delay * len(names))
+        missing = [n for n in dict.fromkeys(names) if (model, n) not in self.cache]
+        failed = set()
+        if missing:
+            blobs = self._blobs(missing)
+            for n in missing:
+                b = blobs.get(n)
+                try:
+                    self.cache[(model, n)] = self.be.decode_batch(model, [b])[0] if b is not None else None
+                except Exception as e:
+                    log.warning("decode of %s failed: %s", n, e)
+                    self.cache[(model, n)] = None
+            while len(self.cache) > self.cache_images:
+                self.cache.popitem(last=False)
+        imgs = []
+        for n in names:
+            im = self.cache.get((model, n))
+            if im is None:
+                failed.add(n)
+            else:
+                self.cache.move_to_end((model, n))
+                imgs.append(im)
+        out = torch.zeros((2, self.cap, 5), dtype=torch.int32)
+        ok = [i for i, n in enumerate(names) if n not in failed]
+        if ok:
+            idx, p = self.be.predict(model, np.stack(imgs))
+            rows = torch.tensor(ok, dtype=torch.long)
+            out[0, rows] = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32))
+            out[1, rows] = torch.from_numpy(np.ascontiguousarray(p, dtype=np.float32)).view(torch.int32)
+        for i, n in enumerate(names):
+            if n in failed:
+                out[0, i] = -1
         return out, None
+
+
+class FakeRankBackend(HostRankBackend):
+    """Deterministic pseudo-results (serving.inference.FakeBackend), optional
+    per-image delay (CPU tests)."""
+
+    def __init__(self, cap: int = 16, delay_per_image: float = 0.0, loader: Optional[Callable] = None):
+        from ..serving.inference import FakeBackend
+
+        super().__init__(FakeBackend(), loader=loader, cap=cap, delay_per_image=delay_per_image)
 
 
 class GpuRankBackend(RankBackend):
     """Native engines for both models resident in this GPU's HBM, fed from
-    per-model pinned host image arenas. Two source slots per engine: the H2D
-    copy of step k (copy stream) overlaps the forward of step k-1 (compute
-    stream); results land in one of two output slots."""
+    per-model pinned arenas (decode-once store images + synthetic images). Two
+    source slots per engine: the H2D copy of step k (copy stream) overlaps the
+    forward of step k-1 (compute stream); results land in one of two output
+    slots. A batch larger than the engine's batch runs as several engine passes
+    into consecutive result rows."""
 
-    def __init__(self, device: torch.device, batch_sizes: Dict[str, int], arena_images: int = 512, seed: int = 0,
-                 models: Sequence[str] = MODELS, splits: int = 2):
+    def __init__(self, device: torch.device, batch_sizes: Dict[str, int], cap: int = 0, arena_images: int = 1024,
+                 n_synth: int = 512, seed: int = 0, models: Sequence[str] = MODELS, splits: int = 2,
+                 loader: Optional[Callable] = None, decode_threads: int = 8):
+        from concurrent.futures import ThreadPoolExecutor
+
         from ..models import build_model
         from ..models.engine import Engine, SplitEngine
-        from .staging import PinnedImageStore
 
         self.device = device
-        self.max_batch = max(batch_sizes.values())
-        self.engines, self.stores = {}, {}
+        self.cap = cap or max(batch_sizes.values())
+        self.loader = loader
+        self.engines, self.arenas = {}, {}
         self.stream = torch.cuda.Stream(device)
         self.copy_stream = torch.cuda.Stream(device)
+        self.pool = ThreadPoolExecutor(max_workers=decode_threads)
         for m in models:
             g, w = build_model(m, seed=seed, calibrate=True)
             b = batch_sizes[m]
@@ -106,32 +269,57 @@ class GpuRankBackend(RankBackend):
                 self.engines[m] = SplitEngine(g, w, batch=b, device=str(device), src_slots=2, splits=splits)
             else:
                 self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=2)
-            st = PinnedImageStore(arena_images, g.input_hw)
-            st.fill_synthetic(seed=1000 + MODEL_IDS[m])
-            self.stores[m] = st
-        self.out = [torch.zeros((2, self.max_batch, 5), dtype=torch.int32, device=device) for _ in range(2)]
+            self.arenas[m] = ImageArena(max(arena_images, n_synth + 2 * self.cap), g.input_hw, pinned=True,
+                                        n_synth=n_synth, seed=1000 + MODEL_IDS[m])
+        self.out = [torch.zeros((2, self.cap, 5), dtype=torch.int32, device=device) for _ in range(2)]
         self.ev_copied = torch.cuda.Event()
         self.ev_consumed = {(m, k): torch.cuda.Event() for m in models for k in range(2)}
         self.ev_done = [torch.cuda.Event() for _ in range(2)]
 
-    def launch(self, model, start, count, slot):
-        eng = self.engines[model]
+    def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
+        from ..serving.inference import load_image
+
+        blobs = self.loader(names) if self.loader else {}
+        hw = self.arenas[model].hw
+
+        def dec(n):
+            b = blobs.get(n)
+            if b is None:
+                return n, None
+            try:
+                return n, load_image(b, hw)
+            except Exception as e:  # undecodable file -> reported as failed
+                log.warning("decode of %s failed: %s", n, e)
+                return n, None
+        return dict(self.pool.map(dec, names))
+
+    def launch(self, model, names, slot):
+        if len(names) > self.cap:
+            raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
+        eng, arena = self.engines[model], self.arenas[model]
+        slots, failed = arena.slots(list(names), lambda ns: self._load(model, ns))
         cs, s = self.copy_stream, self.stream
-        cs.wait_event(self.ev_consumed[(model, slot)])  # WAR: the forward that last read this source slot
-        self.stores[model].h2d(eng.srcs[slot], start, min(count, eng.batch), cs)
-        self.ev_copied.record(cs)
-        s.wait_event(self.ev_copied)
         out = self.out[slot]
-        with torch.cuda.stream(s):
-            eng.run(s, use_graph=True, slot=slot)
-            self.ev_consumed[(model, slot)].record(s)
-            out.zero_()
-            out[:, : eng.batch].copy_(eng.results[slot])
-            self.ev_done[slot].record(s)
+        B = eng.batch
+        for off in range(0, len(slots), B):  # one engine pass per B images: never truncated
+            chunk = slots[off:off + B]
+            cs.wait_event(self.ev_consumed[(model, slot)])  # WAR: the forward that last read this source slot
+            arena.pinned.h2d_indices(eng.srcs[slot], chunk, cs)
+            self.ev_copied.record(cs)
+            s.wait_event(self.ev_copied)
+            with torch.cuda.stream(s):
+                eng.run(s, use_graph=True, slot=slot)
+                self.ev_consumed[(model, slot)].record(s)
+                out[:, off:off + len(chunk)].copy_(eng.results[slot][:, :len(chunk)])
+        if failed:  # undecodable / unfetchable images: class id -1 marks the row failed
+            rows = torch.tensor([i for i, n in enumerate(names) if n in set(failed)], device=self.device)
+            with torch.cuda.stream(s):
+                out[0].index_fill_(0, rows, -1)
+        self.ev_done[slot].record(s)
         return out, self.ev_done[slot]
 
 
-# ---------------------------------------------------------- coordinator ----
+# ------------------------------------------------------------- coordinator ----
 @dataclass
 class Inflight:
     rank: int
@@ -139,47 +327,62 @@ class Inflight:
     t_dispatch: float
 
 
-class CollectiveCoordinator:
-    """Rank-0 scheduling state (the reference leader's job service). Batches are
-    tracked per dispatch step, so with the pipelined service two steps (the one
-    computing and the one being gathered) can be in flight."""
+class ReplicatedCoordinator:
+    """The job service's state machine (reference leader, worker.py:176-495,
+    989-1037), identical on every rank: log records and dispatch tables are
+    applied in broadcast order, results in all-gather order. Only the active
+    coordinator PLANS tables (its cost model is timing-dependent) and writes
+    outputs; replicas apply what it broadcast."""
 
-    def __init__(self, batch_sizes: Dict[str, int], arena_images: Dict[str, int], out_dir: Optional[str] = None,
-                 host_tag: str = "node"):
-        self.jobs = JobManager(dict(batch_sizes))
+    def __init__(self, batch_sizes: Dict[str, int], cap: int = 256, host_tag: str = "node"):
+        self.cap = cap
+        self.jobs = JobManager({m: min(int(b), cap) for m, b in batch_sizes.items()})
         self.cost = CostModel()
         self.metrics = Metrics()
-        self.arena = arena_images
-        self.inflight: Dict[int, Dict[int, Inflight]] = {}  # step -> global rank -> batch
+        self.inflight: Dict[int, Dict[int, Inflight]] = {}   # step -> global rank -> batch
         self.step_t0: Dict[int, float] = {}
         self.requeued = 0
-        self.steps = 0
-        self.out_dir = out_dir
         self.host_tag = host_tag
-        self._wq: "queue.Queue" = queue.Queue(maxsize=64)
-        self._writer = None
-        if out_dir:
-            os.makedirs(out_dir, exist_ok=True)
-            self._writer = threading.Thread(target=self._write_loop, daemon=True)
-            self._writer.start()
+        self.lock = threading.RLock()      # control-thread readers (C1/C2/C5/status) vs the serve loop
+        self.history: "OrderedDict[int, list]" = OrderedDict()  # step -> [(batch, idx, p, grank)]
 
-    def submit(self, model: str, n_images: int) -> int:
-        """Cyclic pick over the (replicated, synthetic) arena; image names are
-        arena indices so a batch is a contiguous range (one hipMemcpyAsync)."""
-        idx = [str(i % self.arena[model]) for i in range(n_images)]
-        return self.jobs.submit_images(model, idx, "client", now=time.monotonic()).job_id
+    # ------------------------------------------------------------- log ----
+    def apply(self, rec: dict) -> dict:
+        """Apply one replicated log record; returns what the requester is told."""
+        op = rec["op"]
+        if op == "submit":
+            jm = self.jobs
+            job = jm.submit_images(rec["model"], list(rec["images"]), rec.get("requester", "client"),
+                                   now=time.monotonic(), job_id=int(rec["job_id"]))
+            return {"jobid": job.job_id, "batches": job.batches_total}
+        if op == "batch_size":
+            bs = max(1, min(int(rec["batch_size"]), self.cap))
+            self.jobs.set_batch_size(rec["model"], bs)
+            return {"model": rec["model"], "batch_size": bs}
+        if op == "state":  # new coordinator's full state after a rebuild
+            self.jobs.restore(rec["jobs"], requeue_inprogress=True)
+            self.inflight.clear()
+            self.step_t0.clear()
+            return {}
+        raise ValueError(f"unknown log record {op}")
+
+    def next_job_id(self, pending: int = 0) -> int:
+        """Id the next submit will get once applied (records apply in order)."""
+        return max([30] + list(self.jobs.jobs)) + 1 + pending
 
     def idle(self) -> bool:
         return self.jobs.pending() == 0 and not self.jobs.inprogress
 
-    def next_table(self, members: List[int], stop_when_idle: bool = True) -> np.ndarray:
-        """Descriptor table of dispatch step ``self.steps`` (then increments it)."""
-        t = np.full((len(members), DESC_FIELDS), 0, np.int64)
+    # ---------------------------------------------------------- tables ----
+    def next_table(self, step: int, members: List[int]) -> np.ndarray:
+        """(active coordinator) plan step ``step``: fair-share split of the
+        members between the two models' queues (reference worker.py:255-495)."""
+        t = np.zeros((len(members), DESC_FIELDS), np.int64)
         t[:, F_MODEL] = IDLE
-        if stop_when_idle and self.idle():
-            t[:, F_MODEL] = STOP
-            return t
         queued = {m: len(self.jobs.queues[m]) for m in MODELS}
+        if not any(queued.values()):
+            self.inflight[step] = {}
+            return t
         workers = [f"rank{g}" for g in members]
         assigns = plan(queued, workers, {}, workers, self.cost, self.jobs.batch_sizes)
         now = time.monotonic()
@@ -189,43 +392,62 @@ class CollectiveCoordinator:
             b = self.jobs.pop_next(a.model)
             if b is None:
                 continue
-            r = members.index(g)
-            start = int(b.images[0])
-            t[r] = (b.job_id, b.batch_id, MODEL_IDS[b.model], start, len(b.images), 0)
+            t[members.index(g)] = (b.job_id, b.batch_id, MODEL_IDS[b.model], 0, len(b.images), 0)
             cur[g] = Inflight(g, b, now)
-        self.inflight[self.steps] = cur
-        self.step_t0[self.steps] = now
-        self.steps += 1
+        self.inflight[step] = cur
+        self.step_t0[step] = now
         return t
 
-    def complete(self, members: List[int], gathered: Optional[List[torch.Tensor]], step: Optional[int] = None
-                 ) -> None:
-        """Results of dispatch step ``step`` (default: the oldest in flight) arrived."""
-        if step is None:
-            if not self.inflight:
-                return
-            step = min(self.inflight)
+    def apply_table(self, step: int, table: np.ndarray, members: List[int]) -> None:
+        """(replica) take exactly the broadcast batches out of the local queues."""
+        now = time.monotonic()
+        cur: Dict[int, Inflight] = {}
+        for r, g in enumerate(members):
+            if int(table[r, F_MODEL]) < 0:
+                continue
+            model = MODELS[int(table[r, F_MODEL])]
+            b = self.jobs.pop_key(model, (int(table[r, F_JOB]), int(table[r, F_BATCH])))
+            if b is None:
+                raise RuntimeError(f"replica diverged: batch {table[r, F_JOB]}:{table[r, F_BATCH]} not queued")
+            cur[g] = Inflight(g, b, now)
+        self.inflight[step] = cur
+        self.step_t0[step] = now
+
+    def batch_of(self, step: int, grank: int) -> Optional[Batch]:
+        inf = self.inflight.get(step, {}).get(grank)
+        return None if inf is None else inf.batch
+
+    # -------------------------------------------------------- complete ----
+    def complete(self, step: int, gathered: Optional[Sequence[np.ndarray]], members: List[int]
+                 ) -> List[Tuple[Batch, np.ndarray, np.ndarray, int]]:
+        """Results of step ``step`` (all-gathered, group-rank order). Returns the
+        completed batches with their rows (for the output writer)."""
         now = time.monotonic()
         service = now - self.step_t0.pop(step, now)
+        done = []
         for g, inf in self.inflight.pop(step, {}).items():
             b = inf.batch
-            self.jobs.complete(b.key, now=now)
+            if self.jobs.complete(b.key, now=now) is None:
+                continue
             n = len(b.images)
             self.metrics.record(b.model, now - inf.t_dispatch, service, n)
             self.cost.observe(b.model, n, service)
-            if self._writer is not None and gathered is not None and g in members:
-                res = gathered[members.index(g)].cpu().numpy()
-                try:
-                    self._wq.put_nowait((b, res[0, :n].copy(), res[1, :n].view(np.float32).copy(), g))
-                except queue.Full:
-                    pass
+            if gathered is not None and g in members:
+                res = gathered[members.index(g)]
+                idx, p = res[0, :n].copy(), res[1, :n].view(np.float32).copy()
+                done.append((b, idx, p, g))
+        if done:
+            self.history[step] = done
+            while len(self.history) > RESULT_HISTORY:
+                self.history.popitem(last=False)
+        return done
 
     def requeue_inflight(self) -> int:
         """Failure: every batch of every in-flight step goes back to the FRONT
         of its queue (newest step first, so queue order is preserved)."""
         n = 0
         for step in sorted(self.inflight, reverse=True):
-            for g, inf in self.inflight[step].items():
+            for g, inf in sorted(self.inflight[step].items(), reverse=True):
                 if self.jobs.requeue_front(inf.batch.key) is not None:
                     n += 1
         self.inflight.clear()
@@ -233,53 +455,135 @@ class CollectiveCoordinator:
         self.requeued += n
         return n
 
-    def _write_loop(self) -> None:
+    def assignments(self) -> Dict[str, dict]:
+        """C5: {rank: {model, job_id, batch_id}} of the steps in flight."""
+        out = {}
+        for step in sorted(self.inflight):
+            for g, inf in self.inflight[step].items():
+                out[f"rank{g}"] = {"model": inf.batch.model, "job_id": inf.batch.job_id,
+                                   "batch_id": inf.batch.batch_id}
+        return out
+
+
+# ---------------------------------------------------------- output writer ----
+class OutputWriter:
+    """Writes output_<job>_<batch>_<host>.json off the serve loop (a blocking
+    queue: a file is never dropped) into ``out_dir`` and/or the store."""
+
+    def __init__(self, out_dir: Optional[str], put: Optional[Callable[[str, bytes], None]] = None,
+                 host_tag: str = "node"):
+        self.out_dir, self.put, self.host_tag = out_dir, put, host_tag
+        if out_dir:
+            os.makedirs(out_dir, exist_ok=True)
+        self.q: "queue.Queue" = queue.Queue()
+        self.written = 0
+        self.thread = threading.Thread(target=self._loop, daemon=True, name="output-writer")
+        self.thread.start()
+
+    def submit(self, b: Batch, idx: np.ndarray, p: np.ndarray, grank: int,
+               on_written: Optional[Callable[[Batch], None]] = None) -> None:
+        self.q.put((b, idx, p, grank, on_written))
+
+    def _loop(self) -> None:
         while True:
-            b, idx, p, g = self._wq.get()
-            if b is None:
+            item = self.q.get()
+            if item is None:
                 return
-            names = [f"synthetic_{b.model}_{i}.jpeg" for i in b.images]
-            doc = decode_top5(names, idx, p)
-            path = os.path.join(self.out_dir, output_name(b.job_id, b.batch_id, f"{self.host_tag}-rank{g}"))
-            with open(path, "w") as f:
-                f.write(dumps(doc))
+            b, idx, p, g, on_written = item
+            try:
+                failed = [n for i, n in enumerate(b.images) if idx[i, 0] < 0]
+                ok = [i for i in range(len(b.images)) if idx[i, 0] >= 0]
+                names = [b.images[i] for i in ok]
+                doc = decode_top5(names, idx[ok], p[ok], failed)
+                name = output_name(b.job_id, b.batch_id, f"{self.host_tag}-rank{g}")
+                text = dumps(doc)
+                if self.out_dir:
+                    with open(os.path.join(self.out_dir, name), "w") as f:
+                        f.write(text)
+                if self.put is not None:
+                    self.put(name, text.encode())
+                self.written += 1
+                if on_written is not None:
+                    on_written(b)
+            except Exception as e:  # a failed write is logged, never silently skipped
+                log.error("output %s:%s not written: %s", b.job_id, b.batch_id, e)
 
     def flush(self) -> None:
-        if self._writer is not None:
-            while not self._wq.empty():
-                time.sleep(0.01)
+        """Block until every queued file is written (sentinel + join), then restart."""
+        self.q.put(None)
+        self.thread.join()
+        self.thread = threading.Thread(target=self._loop, daemon=True, name="output-writer")
+        self.thread.start()
 
 
-# -------------------------------------------------------------- service ----
+# ---------------------------------------------------------------- service ----
 class CollectiveService:
-    """Lag-1 pipelined serving loop, identical on every rank:
+    """The per-rank serve loop (identical on every rank). See the module doc.
 
-      step k:  broadcast table k -> launch batch k (async on the GPU)
-               -> gather the results of step k-1 (done or finishing while batch k
-                  computes) -> rank 0 completes step k-1.
+    ``control``: optional RankControl (UDP control plane + store of this rank);
+    without it (tests, benches) jobs are submitted with ``submit_local`` on the
+    coordinator rank."""
 
-    so the coordinator's bookkeeping, the descriptor broadcast and the result
-    gather hide under the next batch's forward. Any CollectiveFailure requeues
-    both in-flight steps and re-forms the communicator over the survivors."""
-
-    def __init__(self, eg: ElasticGroup, backend: RankBackend, coord: Optional[CollectiveCoordinator] = None,
-                 kill_rank: int = -1, kill_at_step: int = -1, on_device: bool = False):
-        self.eg, self.be, self.coord = eg, backend, coord
+    def __init__(self, eg: ElasticGroup, backend: RankBackend, coord: ReplicatedCoordinator,
+                 control=None, writer: Optional[OutputWriter] = None, kill_rank: int = -1, kill_at_step: int = -1,
+                 on_device: bool = False, idle_sleep: float = 0.002, watchdog_s: float = 0.0):
+        self.eg, self.be, self.coord, self.control = eg, backend, coord, control
+        self.writer = writer
         self.kill_rank, self.kill_at_step = kill_rank, kill_at_step
         self.dev = backend.device if on_device else torch.device("cpu")
         self.steps = 0
         self.rebuilds = 0
-        self.pending = None  # (step, result tensor, event) of the step awaiting its gather
-        self._idle = torch.zeros((2, self.be.max_batch, 5), dtype=torch.int32, device=self.dev)
+        self.pending = None  # (step, result tensor, event) of the step awaiting its all-gather
+        self.cap = backend.cap
+        self._idle = torch.zeros((2, self.cap, 5), dtype=torch.int32, device=self.dev)
+        self.idle_sleep = idle_sleep
+        self._inbox: "queue.Queue" = queue.Queue()   # (record, reply callback or None)
+        self._written: Dict[int, set] = {}             # job id -> batch ids whose output is durable
+        self._stop = False
+        self.last_progress = time.monotonic()
+        self._watchdog = None
+        if watchdog_s > 0:
+            self._watchdog = threading.Thread(target=self._watch, args=(watchdog_s,), daemon=True)
+            self._watchdog.start()
+        if control is not None:
+            control.attach(self)
 
-    def _bufs(self) -> Optional[List[torch.Tensor]]:
-        if self.eg.rank != 0:
-            return None
-        return [torch.zeros((2, self.be.max_batch, 5), dtype=torch.int32, device=self.dev)
-                for _ in range(self.eg.world)]
+    # ------------------------------------------------------------- roles --
+    def coordinator_rank(self) -> int:
+        return max(self.eg.members)
 
+    def is_coordinator(self) -> bool:
+        return self.eg.grank == self.coordinator_rank()
+
+    # ------------------------------------------------------------ inputs --
+    def submit_local(self, model: str, n_images: int = 0, images: Optional[List[str]] = None,
+                     requester: str = "local", reply: Optional[Callable[[dict], None]] = None) -> None:
+        """Queue a submit on the coordinator (applied at the next step)."""
+        names = list(images) if images is not None else synthetic_names(n_images)
+        self._inbox.put(({"op": "submit", "model": model, "images": names, "requester": requester}, reply))
+
+    def set_batch_size(self, model: str, bs: int, reply: Optional[Callable[[dict], None]] = None) -> None:
+        self._inbox.put(({"op": "batch_size", "model": model, "batch_size": int(bs)}, reply))
+
+    def stop(self) -> None:
+        self._stop = True
+
+    def _drain(self) -> Tuple[List[dict], List[Optional[Callable]]]:
+        recs, replies = [], []
+        while True:
+            try:
+                rec, reply = self._inbox.get_nowait()
+            except queue.Empty:
+                break
+            if rec["op"] == "submit":
+                rec["job_id"] = self.coord.next_job_id(sum(r["op"] == "submit" for r in recs))
+            recs.append(rec)
+            replies.append(reply)
+        return recs, replies
+
+    # -------------------------------------------------------------- step --
     def _collect(self) -> None:
-        """Gather + complete the pending step (all ranks call this in lockstep)."""
+        """All-gather + complete the pending step (all ranks, lockstep)."""
         if self.pending is None:
             return
         k, res, ev = self.pending
@@ -289,53 +593,404 @@ class CollectiveService:
             else:
                 ev.synchronize()
         res = res.to(self.dev)
-        bufs = self._bufs()
-        self.eg.gather(res, bufs)
+        bufs = [torch.empty_like(res) for _ in range(self.eg.world)]
+        self.eg.all_gather(bufs, res)
         self.pending = None
-        if self.eg.rank == 0:
-            self.coord.complete(self.eg.members, bufs, step=k)
+        gathered = [b.cpu().numpy() for b in bufs]
+        with self.coord.lock:
+            done = self.coord.complete(k, gathered, self.eg.members)
+        if self.is_coordinator():
+            for b, idx, p, g in done:
+                if self.writer is not None:
+                    self.writer.submit(b, idx, p, g, on_written=self._output_written)
+            if self.control is not None and self.writer is None:
+                self.control.jobs_progress([b for b, *_ in done])
 
-    def step(self) -> bool:
-        eg = self.eg
-        desc = torch.zeros((eg.world, DESC_FIELDS), dtype=torch.int64, device=self.dev)
-        if eg.rank == 0:
-            desc.copy_(torch.from_numpy(self.coord.next_table(eg.members)))
-        eg.broadcast(desc, 0)
-        row = desc[eg.rank].cpu().numpy()
-        if row[F_MODEL] == STOP:
+    def _output_written(self, b: Batch) -> None:
+        """(writer thread) A job is reported finished to its requester only once
+        every batch's output file is durable — like the reference worker, which
+        PUT its output before ACKing (worker.py:518-537) — so get-output right
+        after the SUCCESS sees all of them."""
+        with self.coord.lock:
+            got = self._written.setdefault(b.job_id, set())
+            got.add(b.batch_id)
+            j = self.coord.jobs.jobs.get(b.job_id)
+            ready = j is not None and j.done and len(got) >= j.batches_total
+        if ready and self.control is not None:
+            self.control.jobs_progress([b])
+
+    def step(self, stop_when_idle: bool = False) -> bool:
+        eg, coord = self.eg, self.coord
+        k = self.steps
+        world = eg.world
+        hdr = torch.zeros(HDR + world * DESC_FIELDS, dtype=torch.int64, device=self.dev)
+        active = self.is_coordinator()
+        payload = b""
+        replies: List[Optional[Callable]] = []
+        results: List[dict] = []
+        if active:
+            recs, replies = self._drain()
+            with coord.lock:
+                results = [coord.apply(r) for r in recs]
+                stop = self._stop or (stop_when_idle and coord.idle() and not recs)
+                table = coord.next_table(k, eg.members) if not stop else None
+            if recs:
+                payload = json.dumps(recs).encode()
+            hdr[0] = len(payload)
+            hdr[1] = k
+            hdr[2] = 1 if stop else 0
+            if table is not None:
+                hdr[HDR:] = torch.from_numpy(table.reshape(-1))
+        eg.broadcast(hdr, src=eg.group_rank_of(self.coordinator_rank()))
+        h = hdr.cpu().numpy()
+        n = int(h[0])
+        if n:
+            buf = torch.zeros(n, dtype=torch.uint8, device=self.dev)
+            if active:
+                buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
+            eg.broadcast(buf, src=eg.group_rank_of(self.coordinator_rank()))
+            if not active:
+                with coord.lock:
+                    for r in json.loads(bytes(buf.cpu().numpy()).decode()):
+                        coord.apply(r)
+        if active and self.control is not None:
+            self.control.committed(replies, results)
+        elif active:
+            for cb, r in zip(replies, results):
+                if cb is not None:
+                    cb(r)
+        if int(h[2]) == 1:  # STOP
             self._collect()
             return False
-        if self.steps == self.kill_at_step and eg.grank == self.kill_rank:
-            log.warning("rank %d: injected kill at step %d", eg.grank, self.steps)
+        table = h[HDR:].reshape(world, DESC_FIELDS)
+        if not active:
+            with coord.lock:
+                coord.apply_table(k, table, eg.members)
+        if k == self.kill_at_step and eg.grank == self.kill_rank:
+            log.warning("rank %d: injected kill at step %d", eg.grank, k)
             os._exit(17)
-        if row[F_MODEL] >= 0:
-            launched = self.be.launch(MODELS[int(row[F_MODEL])], int(row[F_START]), int(row[F_COUNT]),
-                                      self.steps % 2)
-        else:
-            launched = (self._idle, None)
+        row = table[eg.rank]
+        launched = (self._idle, None)
+        if int(row[F_MODEL]) >= 0:
+            b = coord.batch_of(k, eg.grank)
+            launched = self.be.launch(b.model, b.images, k % 2)
+        idle_step = (table[:, F_MODEL] < 0).all() and self.pending is None
         self._collect()  # step k-1, overlapping batch k
-        self.pending = (self.steps, launched[0], launched[1])
+        self.pending = (k, launched[0], launched[1])
         self.steps += 1
+        self.last_progress = time.monotonic()
+        if idle_step and self.idle_sleep:
+            time.sleep(self.idle_sleep)
         return True
 
-    def serve(self, max_steps: int = 10 ** 9) -> int:
+    # -------------------------------------------------------------- serve --
+    def serve(self, max_steps: int = 10 ** 9, stop_when_idle: bool = False) -> int:
         while self.steps < max_steps:
             try:
-                if not self.step():
+                if not self.step(stop_when_idle):
                     break
             except CollectiveFailure as e:
-                log.warning("rank %d: collective failed (%s); rebuilding", self.eg.grank, e)
-                self.pending = None
-                if self.eg.rank == 0 and self.eg.grank == 0:
-                    self.coord.requeue_inflight()
-                deadline = time.monotonic() + 10
-                while not (self.eg.dead & set(self.eg.members)) and time.monotonic() < deadline:
-                    time.sleep(0.01)  # let SWIM confirm who died
-                self.eg.rebuild(set(self.eg.dead), decide=(self.eg.grank == 0))
-                self.rebuilds += 1
+                self._recover(e)
         else:
             try:
                 self._collect()
             except CollectiveFailure:
                 pass
+        if self.writer is not None:
+            self.writer.flush()
         return self.steps
+
+    def _recover(self, e: Exception) -> None:
+        eg = self.eg
+        log.warning("rank %d: collective failed (%s); rebuilding", eg.grank, e)
+        self.pending = None
+        with self.coord.lock:
+            self.coord.requeue_inflight()
+        deadline = time.monotonic() + 10
+        while not (eg.dead & set(eg.members)) and time.monotonic() < deadline:
+            time.sleep(0.01)  # let SWIM confirm who died
+        was = self.coordinator_rank()
+        eg.rebuild(set(eg.dead))
+        self.rebuilds += 1
+        # the new coordinator's state is authoritative: replicas that completed one
+        # step more or less than it did are repaired by a state record
+        if self.is_coordinator():
+            with self.coord.lock:
+                snap = self.coord.jobs.snapshot()
+            with self._inbox.mutex:
+                self._inbox.queue.appendleft(({"op": "state", "jobs": snap}, None))
+            if was != eg.grank and self.writer is not None:  # takeover: re-PUT recent outputs
+                for step, done in self.coord.history.items():
+                    for b, idx, p, g in done:
+                        self.writer.submit(b, idx, p, g, on_written=self._output_written)
+            if self.control is not None:
+                self.control.became_coordinator(was)
+        self.last_progress = time.monotonic()
+
+    def _watch(self, limit_s: float) -> None:
+        """Watchdog: a rank whose serve loop makes no progress for ``limit_s``
+        (e.g. stuck inside a collective the abort could not release) exits
+        non-zero; it is never re-exec'ed (the survivors rebuild without it)."""
+        while True:
+            time.sleep(min(1.0, limit_s / 4))
+            if time.monotonic() - self.last_progress > limit_s:
+                log.error("rank %d: no progress for %.0f s, exiting", self.eg.grank, limit_s)
+                os._exit(3)
+
+
+# ------------------------------------------------------------ control plane ----
+class RankControl:
+    """This rank's host control plane, in a daemon thread with its own asyncio
+    loop: a cluster Node with role "rank" (SWIM membership -> dead ranks for the
+    elastic group, bully election -> store leader = coordinator, the replicated
+    store with its TCP blob plane) plus the job-service request handlers the
+    reference leader served (SUBMIT_JOB_REQUEST, C1, C2, C3 = SET_BATCH_SIZE,
+    C5 = GET_ASSIGNMENTS, JOB_STATUS; worker.py:887-1059). Requests reach the
+    serve loop through its inbox; replies go out once the request's log record
+    has been broadcast (committed on every rank)."""
+
+    def __init__(self, grank: int, world: int, base_port: int, store_dir: str, host: str = "127.0.0.1",
+                 period: float = 0.1, ping_timeout: float = 0.1, suspect_timeout: float = 0.6,
+                 replication: int = 4, on_dead: Optional[Callable[[int], None]] = None):
+        self.grank, self.world, self.base, self.host = grank, world, base_port, host
+        self.store_dir, self.replication = store_dir, replication
+        self.period, self.ping_timeout, self.suspect_timeout = period, ping_timeout, suspect_timeout
+        self.on_dead = on_dead
+        self.svc: Optional[CollectiveService] = None
+        self.loop: Optional[asyncio.AbstractEventLoop] = None
+        self.node = None
+        self.ready = threading.Event()
+        self.dead: set = set()
+        self.thread = threading.Thread(target=self._main, daemon=True, name=f"rank-control-{grank}")
+
+    def addr(self, g: int) -> str:
+        return f"{self.host}:{self.base + g}"
+
+    def rank_of(self, name: str) -> Optional[int]:
+        try:
+            return int(name.rsplit(":", 1)[1]) - self.base
+        except (ValueError, IndexError):
+            return None
+
+    # ------------------------------------------------------------ thread --
+    def start(self, timeout: float = 30.0) -> "RankControl":
+        self.thread.start()
+        if not self.ready.wait(timeout):
+            raise RuntimeError("rank control plane did not start")
+        return self
+
+    def _main(self) -> None:
+        self.loop = asyncio.new_event_loop()
+        asyncio.set_event_loop(self.loop)
+        self.loop.create_task(self._run())
+        self.loop.run_forever()
+        pending = [t for t in asyncio.all_tasks(self.loop) if not t.done()]
+        for t in pending:
+            t.cancel()
+        if pending:
+            self.loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
+        self.loop.close()
+
+    async def _run(self) -> None:
+        from ..cluster.frames import MsgType
+        from ..serving.node import Node, NodeConfig
+
+        cfg = NodeConfig(host=self.host, port=self.base + self.grank, role="rank", seeds=[self.addr(0)],
+                         store_dir=self.store_dir, period=self.period, ping_timeout=self.ping_timeout,
+                         suspect_timeout=self.suspect_timeout, cleanup_time=30.0, replication=self.replication,
+                         meta={"prio": self.grank, "rank": self.grank})
+        self.node = n = await Node(cfg).start()
+        on = n.ep.on
+        on(MsgType.SUBMIT_JOB_REQUEST, self._on_submit)
+        on(MsgType.SET_BATCH_SIZE, self._on_batch_size)
+        on(MsgType.GET_C1_COMMAND, self._on_c1)
+        on(MsgType.GET_C2_COMMAND, self._on_c2)
+        on(MsgType.GET_ASSIGNMENTS, self._on_c5)
+        on(MsgType.JOB_STATUS, self._on_status)
+        on(MsgType.FETCH_INTRODUCER, self._on_fetch_leader)   # every rank is an introducer for clients
+        n.ml.on_fail.append(self._member_failed)
+        await n.join()
+        # every rank knows the static job membership: once all have joined, the
+        # bully election settles on the highest rank (= the collective
+        # coordinator); serving starts only then, so store requests of the first
+        # steps already reach the right leader
+        want = self.addr(self.world - 1)
+        for _ in range(400):
+            if len([m for m in n.ml.alive() if (n.ml.get(m).meta or {}).get("role") == "rank"]) >= self.world:
+                break
+            await asyncio.sleep(0.05)
+        for _ in range(400):
+            if n.leader() == want:
+                break
+            if not n.election.in_election:
+                n.election.trigger()
+            await asyncio.sleep(0.05)
+        self.ready.set()
+
+    def _member_failed(self, name: str) -> None:
+        g = self.rank_of(name)
+        if g is not None and 0 <= g < self.world and g not in self.dead:
+            self.dead.add(g)
+            log.warning("rank %d: SWIM confirmed rank %d dead", self.grank, g)
+            if self.on_dead is not None:
+                self.on_dead(g)
+
+    def stop(self) -> None:
+        if self.loop is None or not self.thread.is_alive():
+            return
+
+        async def _shutdown():
+            try:
+                await self.node.stop()
+            except Exception:
+                pass
+            tasks = [t for t in asyncio.all_tasks() if t is not asyncio.current_task()]
+            for t in tasks:
+                t.cancel()
+            await asyncio.gather(*tasks, return_exceptions=True)
+        try:
+            asyncio.run_coroutine_threadsafe(_shutdown(), self.loop).result(timeout=5)
+        except Exception:
+            pass
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self.thread.join(timeout=5)
+
+    # ------------------------------------------------------- serve hooks --
+    def attach(self, svc: CollectiveService) -> None:
+        self.svc = svc
+
+    def call(self, coro, timeout: float = 30.0):
+        """Run a coroutine on the control loop from the serve thread."""
+        return asyncio.run_coroutine_threadsafe(coro, self.loop).result(timeout)
+
+    def committed(self, replies: List[Optional[Callable]], results: List[dict]) -> None:
+        for cb, r in zip(replies, results):
+            if cb is not None:
+                self.loop.call_soon_threadsafe(cb, r)
+
+    def jobs_progress(self, batches: List[Batch]) -> None:
+        """Tell requesters whose job just finished (SUBMIT_JOB_REQUEST_SUCCESS)."""
+        from ..cluster.frames import MsgType
+
+        seen = set()
+        for b in batches:
+            j = self.svc.coord.jobs.jobs.get(b.job_id)
+            if j is not None and j.done and j.job_id not in seen and ":" in j.requester:  # a node, not "local"
+                seen.add(j.job_id)
+                self.loop.call_soon_threadsafe(
+                    lambda jj=j: self.loop.create_task(
+                        self.node.ep.send(jj.requester, MsgType.SUBMIT_JOB_REQUEST_SUCCESS, {"jobid": jj.job_id})))
+
+    def became_coordinator(self, previous: int) -> None:
+        log.warning("rank %d: now the coordinator (was rank %d)", self.grank, previous)
+        # requesters of jobs that finished while the old coordinator was dying are told again
+        done = [j for j in self.svc.coord.jobs.jobs.values() if j.done]
+        self.jobs_progress([Batch(j.job_id, 0, j.model, []) for j in done])
+
+    def store_put(self, name: str, data: bytes, deadline_s: float = 60.0) -> None:
+        """PUT into the store, retried across a store-leader change (the leader
+        is the coordinator rank, which is what fails over)."""
+        t0, err = time.monotonic(), ""
+        while time.monotonic() - t0 < deadline_s:
+            try:
+                ok, err = self.call(self.node.store.put(data, name), timeout=30)
+            except Exception as e:  # leader unreachable mid-failover
+                ok, err = False, str(e)
+            if ok:
+                return
+            time.sleep(0.1)
+        raise RuntimeError(f"store put {name}: {err}")
+
+    def store_loader(self, names: List[str]) -> Dict[str, Optional[bytes]]:
+        async def fetch_all():
+            sem = asyncio.Semaphore(16)
+
+            async def one(nm):
+                async with sem:
+                    if self.node.local.has(nm):
+                        return nm, self.node.local.get_bytes(nm)
+                    got = await self.node.store.get(nm)
+                    return nm, None if got is None else got[1]
+            return dict(await asyncio.gather(*(one(nm) for nm in names)))
+        return self.call(fetch_all(), timeout=120)
+
+    # ----------------------------------------------------------- handlers --
+    async def _on_fetch_leader(self, fr) -> None:
+        """Reference FETCH_INTRODUCER (introduce process/worker.py:55-58): any rank
+        tells a client who leads, once the election has settled."""
+        from ..cluster.frames import MsgType
+
+        if self.ready.is_set() and self.node.leader() is not None:
+            await self.node.ep.reply(fr, MsgType.FETCH_INTRODUCER_ACK, {"introducer": self.node.leader()})
+
+    def _active(self) -> bool:
+        return self.svc is not None and self.svc.is_coordinator()
+
+    async def _on_submit(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if not self._active():
+            return  # not the coordinator: the client retries at the elected leader
+        p = fr.payload
+        model = p["model"]
+        n = int(p["images_count"])
+        if p.get("synthetic"):
+            names = synthetic_names(n)
+        else:
+            from ..serving.jobs import pick_images
+
+            names = pick_images(sorted(self.node.store.meta.matching("*.jpeg")), n)
+
+        def reply(res, fr=fr):
+            self.loop.create_task(self.node.ep.reply(fr, MsgType.SUBMIT_JOB_REQUEST_ACK, res))
+            if res.get("batches") == 0:
+                self.loop.create_task(self.node.ep.send(fr.sender, MsgType.SUBMIT_JOB_REQUEST_SUCCESS,
+                                                        {"jobid": res["jobid"]}))
+        self.svc.submit_local(model, images=names, requester=fr.sender, reply=reply)
+
+    async def _on_batch_size(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if not self._active():
+            return
+
+        def reply(res, fr=fr):
+            if fr.seq:
+                self.loop.create_task(self.node.ep.reply(fr, MsgType.SET_BATCH_SIZE_ACK, res))
+        self.svc.set_batch_size(fr.payload["model"], int(fr.payload["batch_size"]), reply=reply)
+
+    async def _on_c1(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if self._active():
+            with self.svc.coord.lock:
+                c1 = self.svc.coord.metrics.c1()
+            await self.node.ep.reply(fr, MsgType.GET_C1_COMMAND_ACK, {"c1": c1})
+
+    async def _on_c2(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if self._active():
+            with self.svc.coord.lock:
+                p = self.svc.coord.metrics.c2_reference_payload()
+                p["detail"] = self.svc.coord.metrics.c2()
+            await self.node.ep.reply(fr, MsgType.GET_C2_COMMAND_ACK, p)
+
+    async def _on_c5(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if self._active():
+            with self.svc.coord.lock:
+                a = self.svc.coord.assignments()
+            await self.node.ep.reply(fr, MsgType.GET_ASSIGNMENTS_ACK, {"assignments": a})
+
+    async def _on_status(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if not self._active():
+            return
+        with self.svc.coord.lock:
+            j = self.svc.coord.jobs.jobs.get(int(fr.payload["jobid"]))
+            st = {"jobid": fr.payload["jobid"], "known": j is not None, "done": bool(j and j.done),
+                  "batches_done": j.batches_done if j else 0, "batches_total": j.batches_total if j else 0}
+        await self.node.ep.reply(fr, MsgType.JOB_STATUS_ACK, st)

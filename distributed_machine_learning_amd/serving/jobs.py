@@ -91,9 +91,17 @@ class JobManager:
         self.queues[model].extend(batches)
         return job
 
-    def submit_images(self, model: str, images: List[str], requester: str, now: float = 0.0) -> Job:
-        """Submit an explicit image list (already selected) as one job."""
-        jid = self.next_id()
+    def submit_images(self, model: str, images: List[str], requester: str, now: float = 0.0,
+                      job_id: Optional[int] = None) -> Job:
+        """Submit an explicit image list (already selected) as one job. An
+        explicit ``job_id`` (a replicated log record) also advances the counter."""
+        if model not in self.queues:
+            raise KeyError(f"unknown model {model}")
+        if job_id is None:
+            jid = self.next_id()
+        else:
+            jid = int(job_id)
+            self._ids = itertools.count(max([jid] + list(self.jobs)) + 1)
         batches = make_batches(jid, model, list(images), self.batch_sizes[model])
         job = Job(jid, model, len(images), requester, len(batches), 0, now)
         self.jobs[jid] = job
@@ -113,6 +121,17 @@ class JobManager:
         b.attempts += 1
         self.inprogress[b.key] = b
         return b
+
+    def pop_key(self, model: str, key: tuple) -> Optional[Batch]:
+        """Take a specific queued batch (a replica applying the coordinator's dispatch)."""
+        q = self.queues[model]
+        for i, b in enumerate(q):
+            if b.key == key:
+                del q[i]
+                b.attempts += 1
+                self.inprogress[b.key] = b
+                return b
+        return None
 
     def requeue_front(self, key: tuple) -> Optional[Batch]:
         """Preempted or failed batch goes back to the FRONT of its queue (worker.py:406-408, 1284-1306)."""

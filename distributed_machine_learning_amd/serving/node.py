@@ -41,7 +41,10 @@ log = logging.getLogger(__name__)
 class NodeConfig:
     host: str = "127.0.0.1"
     port: int = 0
-    role: str = "worker"                 # coordinator | standby | worker | client
+    role: str = "worker"                 # coordinator | standby | worker | client | rank
+    # "rank": one GPU process of the RCCL collective service (parallel/service.py):
+    # coordinator-eligible store node whose job service is the replicated
+    # collective coordinator, so no host Coordinator / WorkerRole is created here
     introducer: Optional[str] = None     # DNS "host:port" (reference config.py:25-26)
     seeds: List[str] = field(default_factory=list)
     store_dir: str = "/tmp/dml_store"
@@ -58,6 +61,7 @@ class NodeConfig:
     batch_sizes: Dict[str, int] = field(default_factory=lambda: {"ResNet50": 10, "InceptionV3": 10})
     store_timeout: float = 10.0
     journal: Optional[str] = None        # coordinator job journal (restart recovery), serving/journal.py
+    meta: Dict = field(default_factory=dict)  # extra membership metadata (e.g. the global rank)
 
 
 class Node:
@@ -83,7 +87,8 @@ class Node:
         self.ep = Endpoint(t)
         self.local = LocalFileStore(os.path.join(cfg.store_dir, self.name.replace(":", "_")))
         self.source = BlobSource(self.local)
-        meta = {"role": cfg.role, "eligible": cfg.role in ("coordinator", "standby")}
+        meta = {"role": cfg.role, "eligible": cfg.role in ("coordinator", "standby", "rank")}
+        meta.update(cfg.meta)
         if self.blob_net is not None:
             self.blob_net.register(self.name, self.source)
             self.blobs = self.blob_net
@@ -102,7 +107,7 @@ class Node:
         self.store = StoreService(self.ep, self.ml, self.local, self.source, self.blobs, self.leader,
                                   replication=cfg.replication, timeout=cfg.store_timeout, storage_role=storage)
         self.coordinator: Optional[Coordinator] = None
-        if meta["eligible"]:
+        if meta["eligible"] and cfg.role != "rank":
             self.coordinator = Coordinator(self.ep, self.ml, list_images=self.store.meta.matching,
                                            locate=self.store.meta.holders, batch_sizes=dict(cfg.batch_sizes),
                                            is_active=lambda: self.is_leader(), journal=open_journal(cfg.journal))
@@ -124,7 +129,7 @@ class Node:
         if self.cfg.introducer:
             leader = await fetch_leader(self.ep, self.cfg.introducer)
         if leader is None and self.cfg.seeds:
-            leader = self.cfg.seeds[0]
+            leader = next((sd for sd in self.cfg.seeds if sd != self.name), None)
         if leader is None or leader == self.name:
             if self.coordinator is not None:
                 self.election.set_leader(self.name)

@@ -232,11 +232,22 @@ class StoreService:
         self.meta.set_node_files(fr.sender, fr.payload.get("all_files", {}))
 
     def adopt(self, acks: Dict[str, dict]) -> None:
-        """New leader: rebuild the file map from COORDINATE_ACK payloads."""
-        self.meta.file_map.clear()
+        """New leader: rebuild the file map from COORDINATE_ACK payloads.
+
+        MERGED into what is already known, never cleared first: a follower's
+        ALL_LOCAL_FILES announce (sent when it learns the new leader) and replica
+        replies of PUTs this leader already coordinated can arrive while the
+        COORDINATE round is still collecting ACKs, and clearing the map here lost
+        them. Entries of nodes that are not alive are dropped."""
+        fm = self.meta.file_map
+        for node in [n for n in fm if n != self.me and not self.ml.is_alive(n)]:
+            fm.pop(node, None)
         self.meta.set_node_files(self.me, self.local.all_files())
         for node, p in acks.items():
-            self.meta.set_node_files(node, p.get("all_files", {}))
+            merged = {k: set(v) for k, v in fm.get(node, {}).items()}
+            for k, v in p.get("all_files", {}).items():
+                merged.setdefault(k, set()).update(int(x) for x in v)
+            self.meta.set_node_files(node, {k: sorted(v) for k, v in merged.items()})
 
     async def node_failed(self, node: str) -> int:
         """Leader: drop the node's files and restore the replication factor."""

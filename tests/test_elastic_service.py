@@ -1,9 +1,10 @@
-"""Elastic collective serving on CPU (gloo, world 3): concurrent ResNet50 +
-InceptionV3 jobs scheduled fair-share over the ranks, then an injected worker
-kill mid-job -> SWIM detects it -> rank 0 requeues the step's batches ->
-survivors re-form the communicator (epoch 1) -> every job still completes.
-(BASELINE configs 4/5 in miniature; the GPU version swaps gloo for RCCL and the
-fake backend for the native engines.)"""
+"""Elastic collective serving on CPU (gloo): concurrent ResNet50 + InceptionV3
+jobs scheduled fair-share over the ranks by the REPLICATED coordinator; an
+injected worker kill mid-job; an injected kill of the COORDINATOR rank mid-job
+(the next-highest survivor takes over from its replica of the job state); the
+replicated state machine itself. (BASELINE configs 4/5 in miniature; the GPU
+version swaps gloo for RCCL and the fake backend for the native engines.)"""
+import glob
 import json
 import os
 import socket
@@ -18,88 +19,161 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(grank, world, store_port, swim_base, out, kill_rank, kill_step):
+def _rank_main(grank, world, rdzv, swim_base, out, kill_rank, kill_step, control):
     import logging
 
     logging.basicConfig(level=logging.WARNING)
     from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
     from distributed_machine_learning_amd.parallel.fd_thread import RankFailureDetector
-    from distributed_machine_learning_amd.parallel.service import (CollectiveCoordinator, CollectiveService,
-                                                                   FakeRankBackend)
+    from distributed_machine_learning_amd.parallel.service import (CollectiveService, FakeRankBackend, OutputWriter,
+                                                                   RankControl, ReplicatedCoordinator)
 
-    eg = ElasticGroup(grank, world, port=store_port, backend="gloo", timeout_s=30)
-    fd = RankFailureDetector(grank, world, swim_base, on_dead=eg.dead.add).start()
-    coord = None
-    if grank == 0:
-        coord = CollectiveCoordinator({"ResNet50": 8, "InceptionV3": 8}, {"ResNet50": 64, "InceptionV3": 64},
-                                      out_dir=os.path.join(out, "outputs"), host_tag="test")
-        jobs = [coord.submit("ResNet50", 96), coord.submit("InceptionV3", 96)]
-    svc = CollectiveService(eg, FakeRankBackend(max_batch=8, delay_per_image=0.002), coord,
+    eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=30)
+    if control:
+        ctl = RankControl(grank, world, swim_base, store_dir=os.path.join(out, "sdfs"), replication=2,
+                          on_dead=eg.dead.add).start()
+        fd = None
+        put = ctl.store_put
+    else:
+        ctl, put = None, None
+        fd = RankFailureDetector(grank, world, swim_base, on_dead=eg.dead.add).start()
+    coord = ReplicatedCoordinator({"ResNet50": 8, "InceptionV3": 8}, cap=8, host_tag="test")
+    writer = OutputWriter(os.path.join(out, "outputs"), put=put, host_tag="test")
+    svc = CollectiveService(eg, FakeRankBackend(cap=8, delay_per_image=0.002), coord, control=ctl, writer=writer,
                             kill_rank=kill_rank, kill_at_step=kill_step)
-    steps = svc.serve(max_steps=500)
-    if grank == 0:
-        coord.flush()
+    if svc.is_coordinator():
+        svc.submit_local("ResNet50", 96)
+        svc.submit_local("InceptionV3", 96)
+    steps = svc.serve(max_steps=3000, stop_when_idle=True)
+    with coord.lock:
         res = {"steps": steps, "rebuilds": svc.rebuilds, "epoch": eg.epoch, "members": eg.members,
-               "done": [coord.jobs.jobs[j].done for j in jobs], "requeued": coord.requeued,
-               "c1": coord.metrics.c1(), "c2": coord.metrics.c2(),
-               "outputs": len(os.listdir(os.path.join(out, "outputs")))}
-        with open(os.path.join(out, "result.json"), "w") as f:
-            json.dump(res, f)
-    fd.stop()
+               "coordinator": svc.coordinator_rank(), "done": [coord.jobs.jobs[j].done for j in (31, 32)],
+               "requeued": coord.requeued, "c1": coord.metrics.c1(), "written": writer.written}
+    if ctl is not None and svc.is_coordinator():
+        res["store_outputs"] = sorted(ctl.call(ctl.node.store.ls_all("output_*.json")))
+    eg.barrier()  # replicas keep their store nodes up until the coordinator has listed the outputs
+    with open(os.path.join(out, f"result_{grank}.json"), "w") as f:
+        json.dump(res, f)
+    if fd is not None:
+        fd.stop()
+    if ctl is not None:
+        ctl.stop()
     eg.close()
 
 
-def _run(tmp_path, kill_rank=-1, kill_step=-1, world=3):
+def _run(tmp_path, kill_rank=-1, kill_step=-1, world=3, control=False):
     ctx = mp.get_context("spawn")
-    sp, swim = _free_port(), _free_port()
-    ps = [ctx.Process(target=_rank_main, args=(r, world, sp, swim, str(tmp_path), kill_rank, kill_step))
+    rdzv, swim = str(tmp_path / "rdzv"), _free_port() - world - 1
+    ps = [ctx.Process(target=_rank_main, args=(r, world, rdzv, swim, str(tmp_path), kill_rank, kill_step, control))
           for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
-        p.join(180)
+        p.join(240)
     for p in ps:
         if p.is_alive():
             p.kill()
-    with open(tmp_path / "result.json") as f:
-        return json.load(f), [p.exitcode for p in ps]
+    res = {}
+    for r in range(world):
+        f = tmp_path / f"result_{r}.json"
+        if f.exists():
+            res[r] = json.loads(f.read_text())
+    return res, [p.exitcode for p in ps]
 
 
 def test_concurrent_models_fair_share(tmp_path):
     res, codes = _run(tmp_path)
     assert codes == [0, 0, 0]
-    assert res["done"] == [True, True] and res["rebuilds"] == 0
-    assert res["c1"]["ResNet50"]["query_count"] == 96 and res["c1"]["InceptionV3"]["query_count"] == 96
-    assert res["outputs"] == 24  # 12 + 12 batches of 8
+    r = res[2]  # the coordinator: highest rank
+    assert r["coordinator"] == 2 and r["done"] == [True, True] and r["rebuilds"] == 0
+    assert r["c1"]["ResNet50"]["query_count"] == 96 and r["c1"]["InceptionV3"]["query_count"] == 96
+    assert r["written"] == 24  # 12 + 12 batches of 8, written by the coordinator only
+    assert len(os.listdir(tmp_path / "outputs")) == 24
+    # every replica completed exactly the same batches
+    for g in (0, 1):
+        assert res[g]["c1"]["ResNet50"]["query_count"] == 96 and res[g]["done"] == [True, True]
+        assert res[g]["written"] == 0
 
 
 def test_worker_kill_mid_job_recovers(tmp_path):
-    res, codes = _run(tmp_path, kill_rank=2, kill_step=3)
-    assert codes[2] == 17 and codes[0] == 0 and codes[1] == 0
-    assert res["rebuilds"] >= 1 and res["epoch"] >= 1 and res["members"] == [0, 1]
-    assert res["done"] == [True, True]
-    assert res["requeued"] >= 1
+    res, codes = _run(tmp_path, kill_rank=1, kill_step=3)
+    assert codes[1] == 17 and codes[0] == 0 and codes[2] == 0
+    r = res[2]
+    assert r["rebuilds"] >= 1 and r["epoch"] >= 1 and r["members"] == [0, 2]
+    assert r["done"] == [True, True] and r["requeued"] >= 1
     # at-least-once: every image of both jobs was served
-    assert res["c1"]["ResNet50"]["query_count"] >= 96 and res["c1"]["InceptionV3"]["query_count"] >= 96
+    assert r["c1"]["ResNet50"]["query_count"] >= 96 and r["c1"]["InceptionV3"]["query_count"] >= 96
 
 
-def test_coordinator_two_steps_in_flight_requeue_order():
-    """Pipelined service: steps k-1 and k are both in flight; a failure requeues
-    both at the queue front in their original order; completion is per step."""
+def test_coordinator_kill_mid_job_failover(tmp_path):
+    """World 4 with the per-rank control plane (SWIM + store): the coordinator
+    (rank 3) dies at step 4; rank 2 takes over from its replica, every job
+    completes, C1 >= submitted, and every batch's output file exists in the
+    store at least once (the new coordinator re-PUTs the recent ones)."""
+    res, codes = _run(tmp_path, kill_rank=3, kill_step=4, world=4, control=True)
+    assert codes[3] == 17 and codes[:3] == [0, 0, 0], codes
+    r = res[2]
+    assert r["coordinator"] == 2 and r["members"] == [0, 1, 2] and r["rebuilds"] >= 1
+    assert r["done"] == [True, True]
+    assert r["c1"]["ResNet50"]["query_count"] >= 96 and r["c1"]["InceptionV3"]["query_count"] >= 96
+    batches = {tuple(os.path.basename(f).split("_")[1:3]) for f in r["store_outputs"]}
+    assert batches == {(str(j), str(b)) for j in (31, 32) for b in range(1, 13)}
+    files = glob.glob(str(tmp_path / "outputs" / "output_*.json"))
+    assert {tuple(os.path.basename(f).split("_")[1:3]) for f in files} == batches
+
+
+def test_replicated_state_machine_two_steps_in_flight():
+    """Coordinator and replica apply the same records/tables -> same state; a
+    failure requeues both in-flight steps at the queue front in their original
+    order; completion is per step; C3 is clamped to the result capacity."""
+    import numpy as np
+
     from distributed_machine_learning_amd.parallel.dataplane import F_BATCH
-    from distributed_machine_learning_amd.parallel.service import CollectiveCoordinator
+    from distributed_machine_learning_amd.parallel.service import ReplicatedCoordinator, synthetic_names
 
-    c = CollectiveCoordinator({"ResNet50": 4, "InceptionV3": 4}, {"ResNet50": 64, "InceptionV3": 64})
-    c.submit("ResNet50", 16)                       # 4 batches of 4
-    t0 = c.next_table([0])
-    t1 = c.next_table([0])
-    assert sorted(c.inflight) == [0, 1] and c.steps == 2
+    c = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4)
+    rep = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4)
+    rec = {"op": "submit", "model": "ResNet50", "images": synthetic_names(16), "job_id": c.next_job_id()}
+    assert c.apply(rec) == rep.apply(rec) == {"jobid": 31, "batches": 4}
+    assert c.apply({"op": "batch_size", "model": "ResNet50", "batch_size": 64}) == {"model": "ResNet50",
+                                                                                      "batch_size": 4}
+    t0 = c.next_table(0, [0])
+    t1 = c.next_table(1, [0])
+    rep.apply_table(0, t0, [0])
+    rep.apply_table(1, t1, [0])
+    assert sorted(c.inflight) == sorted(rep.inflight) == [0, 1]
+    assert c.batch_of(1, 0).key == rep.batch_of(1, 0).key
     first = [int(t0[0, F_BATCH]), int(t1[0, F_BATCH])]
     assert c.requeue_inflight() == 2 and not c.inflight
-    t2 = c.next_table([0])
-    t3 = c.next_table([0])
+    t2 = c.next_table(2, [0])
+    t3 = c.next_table(3, [0])
     assert [int(t2[0, F_BATCH]), int(t3[0, F_BATCH])] == first
-    c.complete([0], None, step=2)                  # out-of-order completion is per step
-    assert sorted(c.inflight) == [3]
-    c.complete([0], None)
+    res = np.zeros((2, 4, 5), np.int32)
+    done = c.complete(3, [res], [0])                # out-of-order completion is per step
+    assert sorted(c.inflight) == [2] and len(done) == 1
+    c.complete(2, None, [0])
     assert not c.inflight and c.metrics.c1()["ResNet50"]["query_count"] == 8
+    # a new coordinator's state record repairs a diverged replica
+    rep.apply({"op": "state", "jobs": c.jobs.snapshot()})
+    assert [b.key for b in rep.jobs.queues["ResNet50"]] == [b.key for b in c.jobs.queues["ResNet50"]]
+
+
+def test_image_arena_decode_once_and_lru():
+    import numpy as np
+
+    from distributed_machine_learning_amd.parallel.service import ImageArena
+
+    calls = []
+
+    def loader(names):
+        calls.append(list(names))
+        return {n: (None if n == "bad" else np.full((4, 4, 3), len(n), np.uint8)) for n in names}
+
+    a = ImageArena(6, (4, 4), n_synth=2)
+    s, failed = a.slots(["synthetic:3", "a", "bb", "a", "bad"], loader)
+    assert s[0] == 1 and s[1] == s[3] and failed == ["bad"] and calls == [["a", "bb", "bad"]]
+    s2, _ = a.slots(["a", "bb"], loader)                    # cached: no second decode
+    assert s2 == s[1:3] and len(calls) == 1
+    a.slots(["c", "dd", "eee"], loader)                     # 4 free slots: evicts the LRU ("a")
+    a.slots(["ffff"], loader)
+    assert "a" not in a.index and a.array[a.index["eee"]][0, 0, 0] == 3

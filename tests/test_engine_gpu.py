@@ -1,14 +1,13 @@
 """Whole-network numerics of the native engine (BN folded, bf16, hand-written
 kernels).
 
-Random-init deep nets amplify bf16 rounding chaotically (fp32 oracle vs a
-bf16-emulating oracle already differ by ~0.12 / 0.21 max-rel on ResNet50 /
-InceptionV3 logits), so:
   * every conv layer is checked ISOLATED against the fp32 conv of the
     bf16-emulating oracle's own input (tight tolerance, all 147 shapes);
-  * the whole network is checked against the bf16-emulating oracle (same
-    rounding points, only accumulation order differs) and loosely against the
-    pure fp32 oracle.
+  * the whole network on 32 images against the fp32 oracle (max-rel <= 5e-2,
+    top-5 overlap >= 4/5 per image) and the bf16-emulating oracle (same
+    rounding points, only accumulation order differs: <= 2e-2). The random init
+    is numerically well-conditioned (models/weights.py: residual-branch gamma /
+    BN beta shift), so these bounds are real.
 """
 import pytest
 import torch
@@ -69,22 +68,32 @@ def test_every_conv_layer_isolated(name):
 
 @pytest.mark.parametrize("name", ["ResNet50", "InceptionV3"])
 def test_engine_matches_oracle(name):
+    """32 images through the whole engine vs the fp32 oracle: max-rel logits
+    error <= 5e-2 and top-5 overlap >= 4/5 on every image (the init is
+    numerically well-conditioned, models/weights.py, so this is a real bound;
+    the old init's chaos forced 0.35). Tighter against the bf16-emulating
+    oracle, which rounds where the engine rounds."""
     g, w = build_model(name, seed=0, calibrate=True)
-    torch.manual_seed(0)
     hw = g.input_hw
-    imgs = torch.randint(0, 256, (2, hw[0], hw[1], 3), dtype=torch.uint8)
-    eng = Engine(g, w, batch=2)
+    imgs = torch.randint(0, 256, (32, hw[0], hw[1], 3), dtype=torch.uint8,
+                         generator=torch.Generator().manual_seed(0))
+    eng = Engine(g, w, batch=32)
     eng.infer(imgs.cuda())
     torch.cuda.synchronize()
     x = preprocess_reference(imgs, hw, g.preprocess)
     got = eng.buf[g.logits].float().cpu()
     # the engine runs the rewritten graph (models/optimize.py); emulate ITS rounding points
     emu = OracleExecutor(eng.g, w, emulate_bf16=True).forward(x)["logits"]
-    ref = OracleExecutor(g, w).forward(x)
-    rel_emu, rel_fp32 = _rel(got, emu), _rel(got, ref["logits"])
-    print(name, "logits rel err vs bf16-emulating oracle", rel_emu, "vs fp32 oracle", rel_fp32)
-    assert rel_emu < 8e-2, rel_emu
-    assert rel_fp32 < 0.35, rel_fp32
+    ref = OracleExecutor(g, w).forward(x)["logits"]
+    rel_emu, rel_fp32 = _rel(got, emu), _rel(got, ref)
+    ov = [len(set(a.tolist()) & set(b.tolist())) for a, b in zip(eng.top_idx.cpu().long(), ref.topk(5, -1).indices)]
+    top1 = sum(int(a) == int(b) for a, b in zip(eng.top_idx.cpu()[:, 0], ref.argmax(-1))) / len(ov)
+    print(name, "logits rel err vs bf16-emulating oracle", rel_emu, "vs fp32 oracle", rel_fp32,
+          "top-5 overlap min", min(ov), "mean", sum(ov) / len(ov), "top-1 agreement", top1)
+    assert rel_emu < 2e-2, rel_emu
+    assert rel_fp32 < 5e-2, rel_fp32
+    assert min(ov) >= 4, ov
+    assert top1 >= 0.9, top1
     # softmax/top-5 outputs are consistent with the engine's own logits
     p = torch.softmax(got, -1)
     assert (eng.probs.cpu() - p).abs().max().item() < 1e-5

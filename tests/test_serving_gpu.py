@@ -1,0 +1,201 @@
+"""GPU tests of the serving paths the benches time (RCCL at world 1):
+
+* ServingPipeline (bench.py's timed loop: dispatch broadcast, double-buffered
+  H2D slots, SplitEngine hipGraph forward, RCCL gather) over 6 steps with
+  distinct images per step == Engine.infer of each batch, bit-exact;
+* the collective service (replicated coordinator + GpuRankBackend + output
+  writer) over RCCL: every output file present and equal to the engine; a C3
+  batch larger than the engine's batch runs as several passes (not truncated);
+* the host-mode GpuBackend.predict (bucketed engines, pinned staging);
+* PinnedImageStore.h2d_indices (coalesced runs);
+* RCCL failure semantics: explicit communicator abort, re-init of a new epoch
+  over the FileStore rendezvous, then a collective that succeeds.
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture
+def rccl_world1(monkeypatch):
+    import torch.distributed as dist
+
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(_free_port()))
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    yield
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def _split_ref(g, w, imgs, half):
+    """Engine(batch=half) on each half of imgs -> packed [2, 2*half, 5] (the
+    SplitEngine reference used by test_engine_gpu)."""
+    from distributed_machine_learning_amd.models.engine import Engine
+
+    e = Engine(g, w, batch=half)
+    out = []
+    for h in range(2):
+        e.infer(imgs[h * half:(h + 1) * half].cuda())
+        torch.cuda.synchronize()
+        out.append(e.result.clone().cpu())
+    return torch.cat(out, dim=1)
+
+
+def test_serving_pipeline_matches_engine(rccl_world1):
+    from distributed_machine_learning_amd.models import build_model
+    from distributed_machine_learning_amd.models.engine import SplitEngine
+    from distributed_machine_learning_amd.parallel.dataplane import DESC_FIELDS, DataPlane, init_process_group
+    from distributed_machine_learning_amd.parallel.pipeline import ServingPipeline
+    from distributed_machine_learning_amd.parallel.staging import PinnedImageStore
+
+    rank, world, local = init_process_group()
+    dev = torch.device("cuda", local)
+    B, steps = 16, 6
+    g, w = build_model("ResNet50", seed=0)
+    eng = SplitEngine(g, w, batch=B, device=str(dev), src_slots=2, splits=2)
+    store = PinnedImageStore(capacity=steps * B, hw=g.input_hw)
+    store.fill_synthetic(seed=3)
+    dp = DataPlane(dev, result_shape=(2, B, 5))
+    got = {}
+    pipe = ServingPipeline(eng, store, dp, use_graph=True, on_results=lambda rec: got.__setitem__(rec.step, rec.results[0]))
+
+    def table(k):
+        t = np.zeros((world, DESC_FIELDS), np.int64)
+        t[0] = (31, k, 0, k * B, B, 0)
+        return t
+
+    pipe.run(steps, table)
+    assert sorted(got) == list(range(steps))
+    for k in range(steps):
+        ref = _split_ref(g, w, torch.from_numpy(store.array[k * B:(k + 1) * B].copy()), B // 2)
+        assert torch.equal(got[k], ref), f"step {k} differs"
+
+
+def test_pinned_h2d_indices():
+    from distributed_machine_learning_amd.parallel.staging import PinnedImageStore
+
+    st = PinnedImageStore(capacity=12, hw=(8, 8))
+    st.fill_synthetic(seed=1)
+    idx = [3, 4, 5, 0, 9, 10, 2]
+    dst = torch.empty((len(idx), 8, 8, 3), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.Stream()
+    st.h2d_indices(dst, idx, s)
+    s.synchronize()
+    assert torch.equal(dst.cpu(), torch.from_numpy(st.array[idx]))
+    st.h2d(dst[:5], 10, 5, s)  # wrapping range
+    s.synchronize()
+    assert torch.equal(dst[:5].cpu(), torch.from_numpy(st.array[[10, 11, 0, 1, 2]]))
+
+
+def test_gpu_backend_predict_buckets():
+    from distributed_machine_learning_amd.models import build_model
+    from distributed_machine_learning_amd.models.engine import Engine
+    from distributed_machine_learning_amd.serving.inference import GpuBackend
+
+    be = GpuBackend(max_batch=64, quantum=32)
+    rng = np.random.default_rng(0)
+    imgs = rng.integers(0, 256, (70, 224, 224, 3), dtype=np.uint8)  # 64 + one 32-bucket pass of 6
+    idx, p = be.predict("ResNet50", imgs)
+    assert sorted(k[1] for k in be._engines) == [32, 64]
+    g, w = build_model("ResNet50", seed=0)
+    ref = Engine(g, w, batch=64)
+    ref.infer(torch.from_numpy(imgs[:64]).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(idx[:64], ref.top_idx.cpu().numpy())
+    assert np.array_equal(p[:64], ref.top_p.cpu().numpy())
+    r32 = Engine(g, w, batch=32)
+    src = np.zeros((32, 224, 224, 3), np.uint8)
+    src[:6] = imgs[64:]
+    r32.infer(torch.from_numpy(src).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(idx[64:], r32.top_idx.cpu().numpy()[:6])
+
+
+def test_collective_service_rccl_world1_outputs(tmp_path):
+    from distributed_machine_learning_amd.models import build_model
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+    from distributed_machine_learning_amd.parallel.service import (CollectiveService, GpuRankBackend, OutputWriter,
+                                                                   ReplicatedCoordinator)
+    from distributed_machine_learning_amd.utils.labels import load_class_index
+
+    dev = torch.device("cuda", 0)
+    eg = ElasticGroup(0, 1, store_path=str(tmp_path / "rdzv"), backend="nccl", device=dev, timeout_s=120)
+    try:
+        bs = {"ResNet50": 16, "InceptionV3": 8}
+        be = GpuRankBackend(dev, bs, cap=32, arena_images=256, n_synth=64)
+        coord = ReplicatedCoordinator(bs, cap=32, host_tag="gpu")
+        writer = OutputWriter(str(tmp_path / "out"), host_tag="gpu")
+        svc = CollectiveService(eg, be, coord, writer=writer, on_device=True)
+        svc.submit_local("ResNet50", 40)        # 16 + 16 + 8
+        svc.submit_local("InceptionV3", 20)     # 8 + 8 + 4
+        svc.set_batch_size("ResNet50", 32)      # applied after the first submit's batching
+        svc.submit_local("ResNet50", 32)        # one 32-image batch = 2 engine passes of 16
+        svc.serve(max_steps=200, stop_when_idle=True)
+        assert [coord.jobs.jobs[j].done for j in (31, 32, 33)] == [True, True, True]
+        files = sorted(os.listdir(tmp_path / "out"))
+        assert len(files) == 3 + 3 + 1, files
+        cls = {wnid: i for i, (wnid, _) in enumerate(load_class_index())}
+        for m, job, n_img, half in (("ResNet50", 31, 40, 8), ("InceptionV3", 32, 20, 4), ("ResNet50", 33, 32, 8)):
+            g, w = build_model(m, seed=0)
+            arena = be.arenas[m].array
+            doc = {}
+            for f in files:
+                if f.startswith(f"output_{job}_"):
+                    doc.update(json.load(open(tmp_path / "out" / f)))
+            assert len(doc) == n_img or job == 33  # job 33 reuses names synthetic:0..31
+            names = [f"{i}" for i in range(n_img)]
+            imgs = torch.from_numpy(arena[[i % 64 for i in range(n_img)]].copy())
+            bsz = 32 if job == 33 else bs[m]
+            for b0 in range(0, n_img, bsz):
+                rows = imgs[b0:b0 + bsz]
+                pad = torch.zeros((bsz, *rows.shape[1:]), dtype=torch.uint8)
+                pad[:len(rows)] = rows
+                if job == 33:  # two engine passes of 16 (SplitEngine halves of 8)
+                    ref = torch.cat([_split_ref(g, w, pad[:16], 8), _split_ref(g, w, pad[16:], 8)], dim=1)
+                else:
+                    ref = _split_ref(g, w, pad, half)
+                for i in range(len(rows)):
+                    ent = doc[f"synthetic:{names[b0 + i]}"][0]
+                    assert [cls[e[0]] for e in ent] == ref[0, i].tolist()
+                    assert np.allclose([e[2] for e in ent], ref[1, i].view(torch.float32).numpy(), rtol=0, atol=0)
+    finally:
+        eg.close()
+
+
+def test_rccl_abort_and_new_epoch(tmp_path):
+    """Explicit abort of the RCCL communicator (the path a dead peer triggers),
+    re-init of epoch 1 through the FileStore rendezvous, then collectives that
+    succeed on the new communicator."""
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+
+    dev = torch.device("cuda", 0)
+    eg = ElasticGroup(0, 1, store_path=str(tmp_path / "rdzv"), backend="nccl", device=dev, timeout_s=60)
+    try:
+        t = torch.arange(4, device=dev, dtype=torch.float32)
+        eg.broadcast(t, 0)
+        members = eg.rebuild(set())          # abort epoch 0, join epoch 1
+        assert members == [0] and eg.epoch == 1 and eg.aborts == 1
+        t2 = torch.ones(8, device=dev)
+        eg.broadcast(t2, 0)
+        bufs = [torch.empty_like(t2)]
+        eg.all_gather(bufs, t2)
+        torch.cuda.synchronize()
+        assert torch.equal(bufs[0], t2)
+        eg.barrier()
+    finally:
+        eg.close()
