@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
-timeout -k 10 600 $T tests/test_serving_gpu.py tests/test_engine_gpu.py -k "serving or pinned or backend or collective or rccl or matches_oracle" > gpurun_out/pytest_new.log 2>&1; rc=$?
+timeout -k 10 600 $T tests/test_serving_gpu.py tests/test_engine_gpu.py -k "matches_oracle" > gpurun_out/pytest_new.log 2>&1; rc=$?
 grep -E "PASSED|FAILED|ERROR|rel err" gpurun_out/pytest_new.log | tail -20; [ $rc -eq 0 ] || exit $rc
 if [ -z "$QUICK" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
