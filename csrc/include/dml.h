@@ -48,7 +48,7 @@ typedef struct {
   // consumer sums the slices (dml_softmax_top5_split does, for the classifier).
   int ksplit;
   int split_ld;
-  // Subsampled residual (v2/halo kernels only; 0/1 = off): output pixel
+  // Subsampled residual (0/1 = off): output pixel
   // (n, ho, wo) adds res pixel n*rHW + (ho*rW + wo)*rsub — the shortcut read at
   // stride rsub from its full-resolution grid (rW = its width, rHW = H*W), used
   // when a stride-2 consumer has been pushed up into the block (models/optimize.py).
@@ -150,11 +150,6 @@ int dml_expand_reduce_init(void);
 int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2_init(void);
-// Stride-1 halo-tile convolution (cfg ids 40..): weights packed chunk-major
-// W[cout][ceil(Cin/64)][kh*kw][64] with Kpad = ceil(Cin/64)*kh*kw*64.
-int dml_conv_halo(const DmlConvArgs* a, int cfg, hipStream_t s);
-int dml_conv_halo_ok(const DmlConvArgs* a, int cfg);  // 0 if cfg can run this shape
-int dml_conv_halo_init(void);
 int dml_conv_pick_cfg(const DmlConvArgs* a);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);

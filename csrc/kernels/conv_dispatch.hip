@@ -1,0 +1,54 @@
+// conv_dispatch.hip — argument validation, dispatch and default tile choice of
+// the MFMA implicit-GEMM convolution (the kernel: conv_igemm_v2.hip).
+//
+// Serves every convolution of ResNet50 / InceptionV3 and the FC layer
+// (SURVEY §2.7 "conv_igemm_bf16"; the reference runs these inside Keras,
+// models.py:26,51 — it has no kernel of its own). cfg ids 10..39 select a v2
+// tile configuration (dml_conv_v2); they are part of the ABI the plan builder
+// and the autotuner (ops/tuning.py) use.
+//
+// Removed in r2 (measured never faster, kept only as history in DESIGN.md and
+// profiles/): the register-staged v1 kernel (cfg 0..4, profiles/r1_v2) and the
+// stride-1 halo-tile kernel (cfg 40..47, profiles/r1_v5/halo_vs_v2_*.json: won
+// 0 of 217 tuned shapes).
+#include "common.h"
+#include "dml.h"
+
+extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
+  if (cfg < 10 || cfg >= 40) {
+    dml_set_error("dml_conv: cfg must be a v2 tile config (10..39)");
+    return -1;
+  }
+  if (a->Cin % 8 || a->ldx % 8 || a->Cout % 8 || a->Kpad % 64 || a->ldy % 8 || (a->res && a->ldr % 8)) {
+    dml_set_error("dml_conv: need Cin, ldx, Cout, ldy, ldr %8==0 and Kpad%64==0");
+    return -1;
+  }
+  if (a->nseg < 0 || a->nseg > 4) {
+    dml_set_error("dml_conv: nseg must be 0..4");
+    return -1;
+  }
+  if (a->rsub > 1 && (!a->res || a->rW < a->Wo * a->rsub || a->rHW < a->rW * a->Ho * a->rsub)) {
+    dml_set_error("dml_conv: subsampled residual needs res and rW >= Wo*rsub, rHW >= rW*Ho*rsub");
+    return -1;
+  }
+  if (a->ksplit > 1 && (!a->out_f32 || a->res || a->nseg || a->relu || a->split_ld < 1)) {
+    dml_set_error("dml_conv: split-K needs fp32 output, no residual/segments/ReLU, split_ld");
+    return -1;
+  }
+  if (a->kchunk && (a->kchunk < 0 || a->kchunk % 64 || a->Cin % a->kchunk || a->dh > 1 || a->dw > 1)) {
+    dml_set_error("dml_conv: chunk-major K order needs kchunk%64==0, Cin%kchunk==0, no dilation");
+    return -1;
+  }
+  return dml_conv_v2(a, cfg, s);
+}
+
+// Measured default tile per shape class (tools/conv_bench.py); the engine
+// autotunes every shape (ops/tuning.py). -1: no config can run this conv.
+extern "C" int dml_conv_pick_cfg(const DmlConvArgs* a) {
+  const long M = (long)a->N * a->Ho * a->Wo;
+  const int C = a->Cout;
+  if (a->Cin % 8 || a->ldx % 8 || C % 8 || a->ldy % 8 || (a->res && a->ldr % 8)) return -1;
+  if (C <= 64) return 15;
+  if (a->Kpad <= 512 || M < 16384) return 14;
+  return 11;
+}

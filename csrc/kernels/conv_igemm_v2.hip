@@ -1,7 +1,10 @@
 // conv_igemm_v2.hip — LDS-DMA pipelined MFMA implicit-GEMM convolution (gfx950).
 //
-// Same contract as conv_igemm.hip (DmlConvArgs, transposed GEMM D[c][m] with
-// v_mfma_f32_16x16x32_bf16, channels on MFMA rows), re-built around the CDNA4
+// Implicit-GEMM convolution over DmlConvArgs (validated and dispatched by
+// conv_dispatch.hip). GEMM view, computed TRANSPOSED: D[c][m] = sum_k W[c][k] X[k][m]
+// with c = output channel on the MFMA rows and m = output pixel on the columns:
+// the v_mfma_f32_16x16x32_bf16 accumulator of lane l then holds 4 CONSECUTIVE
+// output channels of one pixel (NHWC-friendly epilogue). Built around the CDNA4
 // memory path:
 //
 //  * Operand tiles go global -> LDS by LDS-DMA (no VGPR round trip):
@@ -320,7 +323,7 @@ extern "C" int dml_conv_v2_init(void) {
   return rc ? -1 : 0;
 }
 
-// v2 configurations (ids >= 10; see dml_conv in conv_igemm.hip for dispatch)
+// tile configurations (ids 10..39; validated by dml_conv in conv_dispatch.hip)
 extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
   using namespace dml::v2;
   switch (cfg) {

@@ -1,5 +1,5 @@
 // conv_shared.h — pieces shared by the LDS-DMA convolution kernels
-// (conv_igemm_v2.hip: generic implicit GEMM; conv_halo.hip: stride-1 halo tiles).
+// (conv_igemm_v2.hip: implicit GEMM; bottleneck_fused.hip: fused block boundary).
 //
 //  * counted vmcnt waits (LDS-DMA completes in issue order with other VMEM ops)
 //  * the 16-B-chunk XOR swizzle of a 128-B LDS tile row

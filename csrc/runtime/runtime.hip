@@ -104,6 +104,7 @@ extern "C" int dml_plan_add_conv(void* p, const DmlConvArgs* a, int cfg) {
   o.kind = OP_CONV;
   o.conv = *a;
   o.cfg = cfg < 0 ? dml_conv_pick_cfg(a) : cfg;
+  if (o.cfg < 10 || o.cfg >= 40) { g_err = "dml_plan_add_conv: no tile config for this conv"; return -1; }
   ((Plan*)p)->ops.push_back(o);
   return o.cfg;
 }
@@ -230,14 +231,12 @@ extern "C" int dml_plan_replay(void* p, hipStream_t s) {
 
 // Re-point conv op i at tile config cfg (joint tuning of co-scheduled
 // sub-batch plans). Returns the previous cfg, or -1 if op i is not a conv or
-// cfg cannot run it (halo and v2 configs take different weight layouts, so a
-// conv can only move within its family). A captured graph must be re-captured.
+// cfg is not a tile config. A captured graph must be re-captured.
 extern "C" int dml_plan_set_cfg(void* p, int i, int cfg) {
   Plan* pl = (Plan*)p;
   if (i < 0 || i >= (int)pl->ops.size() || pl->ops[i].kind != OP_CONV) { g_err = "dml_plan_set_cfg: not a conv op"; return -1; }
   Op& o = pl->ops[i];
-  if ((o.cfg >= 40) != (cfg >= 40) || cfg < 0) { g_err = "dml_plan_set_cfg: config family mismatch"; return -1; }
-  if (cfg >= 40 && dml_conv_halo_ok(&o.conv, cfg) != 0) { g_err = "dml_plan_set_cfg: halo config cannot run this conv"; return -1; }
+  if (cfg < 10 || cfg >= 40) { g_err = "dml_plan_set_cfg: not a tile config"; return -1; }
   const int prev = o.cfg;
   o.cfg = cfg;
   return prev;

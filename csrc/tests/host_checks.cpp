@@ -87,19 +87,26 @@ int main() {
   CHECK(dml_conv(&a, 0, nullptr) != 0);
   a = conv_args(64, 64, 3, 3);
   CHECK(dml_conv(&a, 99, nullptr) != 0);        // unknown config
-  CHECK(std::string(dml_last_error()).find("bad cfg") != std::string::npos);
+  CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
   a.nseg = 5;
   CHECK(dml_conv(&a, 11, nullptr) != 0);        // too many output segments
   a.nseg = 2;
-  CHECK(dml_conv(&a, 0, nullptr) != 0);         // segments need a v2 config
+  CHECK(dml_conv(&a, 0, nullptr) != 0);         // not a tile config
   a = conv_args(64, 64, 1, 1);
   a.ksplit = 4; a.split_ld = 1 << 20;
   CHECK(dml_conv(&a, 14, nullptr) != 0);        // split-K needs fp32 output
   a.out_f32 = 1; a.relu = 1;
   CHECK(dml_conv(&a, 14, nullptr) != 0);        // ... and no ReLU
   a.relu = 0;
-  CHECK(dml_conv(&a, 40, nullptr) != 0);        // ... and a v2 (non-halo) config
-  CHECK(dml_conv(&a, 2, nullptr) != 0);         // ... not a v1 config
+  CHECK(dml_conv(&a, 40, nullptr) != 0);        // ... and a tile config (10..39)
+  CHECK(dml_conv(&a, 2, nullptr) != 0);
+  a = conv_args(64, 64, 3, 3);
+  a.kchunk = 32;
+  CHECK(dml_conv(&a, 11, nullptr) != 0);        // chunk-major K order: kchunk % 64
+  a = conv_args(8, 64, 3, 3);
+  CHECK(dml_conv_pick_cfg(&a) == 15);
+  a = conv_args(3, 64, 3, 3);
+  CHECK(dml_conv_pick_cfg(&a) == -1);           // nothing can run Cin % 8 != 0
   DmlPoolArgs p;
   std::memset(&p, 0, sizeof p);
   p.C = 12; p.ldx = 12; p.ldy = 12;

@@ -23,9 +23,8 @@ BUILD_DIR = REPO / "build" / "hip"
 ARCH = os.environ.get("DML_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [
-    CSRC / "kernels" / "conv_igemm.hip",
+    CSRC / "kernels" / "conv_dispatch.hip",
     CSRC / "kernels" / "conv_igemm_v2.hip",
-    CSRC / "kernels" / "conv_halo.hip",
     CSRC / "kernels" / "misc.hip",
     CSRC / "kernels" / "stem_fused.hip",
     CSRC / "kernels" / "conv_pool.hip",

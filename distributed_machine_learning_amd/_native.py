@@ -99,8 +99,6 @@ _SIGS = {
     "dml_conv": (C.c_int, [C.POINTER(ConvArgs), C.c_int, C.c_void_p]),
     "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),
     "dml_conv_v2_init": (C.c_int, []),
-    "dml_conv_halo_init": (C.c_int, []),
-    "dml_conv_halo_ok": (C.c_int, [C.POINTER(ConvArgs), C.c_int]),
     "dml_pool": (C.c_int, [C.POINTER(PoolArgs), C.c_void_p]),
     "dml_global_avgpool": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "dml_softmax_top5": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -191,7 +189,6 @@ def ensure_device_init() -> None:
     global _inited
     if not _inited:
         check(lib().dml_conv_v2_init(), "dml_conv_v2_init")
-        check(lib().dml_conv_halo_init(), "dml_conv_halo_init")
         _inited = True
 
 

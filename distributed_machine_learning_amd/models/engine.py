@@ -24,7 +24,6 @@ import torch
 from .. import _native as N
 from .graph import Conv, Dense, FusedConv, Graph, GlobalAvgPool, Pool, node_outputs
 from .weights import Weights, fold_conv
-from ..ops import halo_layout
 
 
 def _r(x: int, m: int) -> int:
@@ -107,7 +106,7 @@ class Engine:
         self.ysub = self._subsampled_y()
         self._src_tensors, self._result_views = src_tensors, result_views
         if share is not None:
-            self.wdev, self.whalo = share.wdev, share.whalo
+            self.wdev = share.wdev
         else:
             self._upload_weights(weights)
         self._alloc_buffers()
@@ -116,7 +115,6 @@ class Engine:
     # ------------------------------------------------------------ weights ----
     def _upload_weights(self, w: Weights) -> None:
         self.wdev: Dict[str, Tuple[torch.Tensor, torch.Tensor, int, int, int]] = {}
-        self.whalo: Dict[str, Tuple[torch.Tensor, int]] = {}
         for n in self.g.nodes:
             if isinstance(n, Conv):
                 k, b = fold_conv(n, w)
@@ -130,13 +128,6 @@ class Engine:
                     K = n.kh * n.kw * cin_eff
                 coutp, kpad = _r(n.cout, 256), _r(K, 64)
                 wk = pack_conv_weight(k, cin_eff, coutp, kpad)
-                if self._halo_eligible(n):
-                    # chunk-major copy for the stride-1 halo-tile kernel (conv_halo.hip)
-                    kt = np.zeros((n.cout, n.kh * n.kw, cin_eff), np.float32)
-                    kt[..., : n.cin] = k.transpose(3, 0, 1, 2).reshape(n.cout, n.kh * n.kw, n.cin)
-                    wh = halo_layout(kt, coutp)
-                    self.whalo[n.name] = (torch.from_numpy(wh).to(self.device, torch.bfloat16).contiguous(),
-                                          wh.shape[1])
             elif isinstance(n, Dense):
                 k = w[f"{n.name}/kernel"][None, None]  # 1x1xCinxCout
                 b = w[f"{n.name}/bias"]
@@ -268,10 +259,6 @@ class Engine:
                 out[e.out] = 2
         return out
 
-    def _halo_eligible(self, n) -> bool:
-        return (isinstance(n, Conv) and n is not self.stem and n.sh == 1 and n.sw == 1 and n.kh * n.kw > 1
-                and self.device.type == "cuda")
-
     # ------------------------------------------------------------ buffers ----
     def _fc_split(self) -> int:
         """Split-K slices of the classifier GEMM: M = batch rows and N = 1000
@@ -383,10 +370,9 @@ class Engine:
 
             cnodes = [n for n in self.g.nodes if isinstance(n, (Conv, Dense, FusedConv))]
             convs = [self._conv_args(n) for n in cnodes]
-            halos = [self._conv_args(n, halo=True) if n.name in self.whalo else None for n in cnodes]
-            table = tuning.autotune(convs, halo_args=halos)
-            for n, a, ah in zip(cnodes, convs, halos):
-                self.tuned[n.name] = table.get(tuning.shape_key(a, ah is not None), -1)
+            table = tuning.autotune(convs)
+            for n, a in zip(cnodes, convs):
+                self.tuned[n.name] = table.get(tuning.shape_key(a), -1)
         self.plans = [self._build_one_plan(self.srcs[i], self.results[i]) for i in range(self.src_slots)]
         self.plan = self.plans[0]
         self.graph_captured = [False] * self.src_slots
@@ -462,8 +448,8 @@ class Engine:
                 continue
             if isinstance(n, (Conv, Dense, FusedConv)):
                 cfg = self.cfg_overrides.get(n.name, self.tuned.get(n.name, -1))
-                a = self._conv_args(n, halo=cfg >= 40)
-                used = L.dml_plan_add_conv(plan, C.byref(a), cfg)
+                a = self._conv_args(n)
+                used = N.check(L.dml_plan_add_conv(plan, C.byref(a), cfg), f"plan conv {n.name}")
                 self.op_cfg[n.name] = used
                 self._keep.append(a)
             elif isinstance(n, Pool):
@@ -485,11 +471,9 @@ class Engine:
         self.op_names.append("softmax_top5")
         return plan
 
-    def _conv_args(self, n, halo: bool = False) -> N.ConvArgs:
+    def _conv_args(self, n) -> N.ConvArgs:
         g, B = self.g, self.batch
         wk, bias, K, kpad, cin_eff = self.wdev[n.name]
-        if halo:  # same conv, chunk-major weights for the halo kernel
-            wk, kpad = self.whalo[n.name]
         if isinstance(n, Dense):
             x = self.buf[n.inp]
             a = N.ConvArgs(x.data_ptr(), wk.data_ptr(), bias.data_ptr(), None, self.buf[n.out].data_ptr(),

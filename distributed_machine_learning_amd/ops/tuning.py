@@ -25,19 +25,20 @@ CACHE_PATH = os.environ.get(
 _lock = threading.Lock()
 
 
-HALO_CFGS = (40, 41, 42, 43, 44, 45, 46, 47)  # conv_halo.hip (stride-1, chunk-major weights)
-# cache entries are only valid for the candidate set they were timed against
-CAND_TAG = "c" + format(sum((i + 1) * c for i, c in enumerate(V2_CFGS + HALO_CFGS)) % 4096, "03x")
+# Cache entries are only valid for the candidate set they were timed against.
+# The committed table was tuned with V2_CFGS plus the stride-1 halo configs
+# (40..47, removed in r2): a halo config never won a shape, so every winner is
+# a V2 config and the table stays valid — the tag keeps the value it had then.
+CAND_TAG = "c3ef"
 
 
-def shape_key(a: N.ConvArgs, halo: bool = False) -> str:
-    """Cache key of a conv shape; `halo` marks shapes that also had the halo
-    configs as candidates (so entries tuned before they existed are re-timed)."""
+def shape_key(a: N.ConvArgs) -> str:
+    """Cache key of a conv shape."""
     return (f"n{a.N}_h{a.H}_w{a.W}_c{a.Cin}_ld{a.ldx}_k{a.kh}x{a.kw}_s{a.sh}x{a.sw}_p{a.ph}x{a.pw}"
             f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}_d{max(a.dh, 1)}x{max(a.dw, 1)}"
             + (f"_ks{a.ksplit}" if a.ksplit > 1 else "")
             + (f"_rs{a.rsub}" if a.rsub > 1 else "")
-            + ("_halo" if halo else "") + "_" + CAND_TAG)
+            + "_" + CAND_TAG)
 
 
 def load_cache(path: str = CACHE_PATH) -> Dict[str, int]:
@@ -64,7 +65,7 @@ NO_RES_CFGS = (34,)  # the residual-epilogue instantiation spills (256x256 tile)
 
 def valid_cfgs(a: N.ConvArgs) -> List[int]:
     if a.Cout % 8 or a.Cin % 8 or a.ldx % 8 or a.ldy % 8:
-        return [0]
+        return []
     return [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)]
 
 
@@ -83,27 +84,20 @@ def time_cfg(a: N.ConvArgs, cfg: int, iters: int = 3) -> float:
     return e0.elapsed_time(e1) / iters
 
 
-def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None, persist: bool = True,
-             halo_args: Optional[Iterable[Optional[N.ConvArgs]]] = None) -> Dict[str, int]:
-    """Return {shape_key: best cfg} for every ConvArgs (timing the uncached ones).
-    halo_args[i], if not None, is the same conv with halo-packed weights: the
-    halo configs are timed on it and a winning id >= 40 means "use halo_args"."""
+def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None, persist: bool = True
+             ) -> Dict[str, int]:
+    """Return {shape_key: best cfg} for every ConvArgs (timing the uncached ones)."""
     args = list(args)
-    halo_args = list(halo_args) if halo_args is not None else [None] * len(args)
     cache = dict(load_cache() if cache is None else cache)
     new: Dict[str, int] = {}
-    L = N.lib()
-    for a, ah in zip(args, halo_args):
-        k = shape_key(a, ah is not None)
+    for a in args:
+        k = shape_key(a)
         if k in cache or k in new:
             continue
         best: Tuple[float, int] = (float("inf"), -1)
-        cands = [(cfg, a) for cfg in valid_cfgs(a)]
-        if ah is not None:
-            cands += [(cfg, ah) for cfg in HALO_CFGS if L.dml_conv_halo_ok(C.byref(ah), cfg) == 0]
-        for cfg, aa in cands:
+        for cfg in valid_cfgs(a):
             try:
-                t = time_cfg(aa, cfg)
+                t = time_cfg(a, cfg)
             except N.NativeError:
                 continue
             best = min(best, (t, cfg))

@@ -137,6 +137,13 @@ class ElasticGroup:
     def all_gather(self, bufs: List[torch.Tensor], t: torch.Tensor) -> None:
         self._run(dist.all_gather, bufs, t)
 
+    def all_gather_into(self, out: torch.Tensor, t: torch.Tensor) -> None:
+        """out[r] = rank r's t (out: [world, *t.shape])."""
+        if self.backend == "nccl":
+            self._run(dist.all_gather_into_tensor, out, t)
+        else:
+            self._run(dist.all_gather, list(out.unbind(0)), t)
+
     def barrier(self) -> None:
         t = torch.zeros(1, device=self.device if self.backend == "nccl" else "cpu")
         self._run(dist.all_reduce, t)

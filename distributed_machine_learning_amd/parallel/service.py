@@ -7,18 +7,25 @@ die nothing can take over (election.py:27). Here every rank holds the whole
 coordinator state as a replicated state machine driven by the step's
 collectives, so ANY survivor can continue as coordinator:
 
-  step k (every rank, lockstep, lag-1 pipelined):
+  step k (every rank; steps run at host speed, independent of GPU progress):
     coordinator  drains its control inbox (client submits / C3 from the CLI) into
-                 log records, applies them, plans step k's dispatch table
+                 log records, applies them, plans step k's dispatch table: at most
+                 one new batch for each rank whose work queue holds fewer than
+                 ``depth`` (2) batches, fair-share between the two models
     broadcast    header [log length, step, table] from the coordinator (48 B per
                  rank), then the log payload (JSON) if any
     every rank   applies the same log records and the same table -> identical
-                 queues, in-flight sets and job-id counters on every rank
-    every rank   launches its own batch of step k (async on the GPU: arena slots
-                 -> H2D -> hipGraph forward), then ALL-GATHERS step k-1's packed
-                 top-5 results [2, cap, 5] int32 -> every rank completes step k-1
-                 identically (C1 counts, job completion); the coordinator also
-                 writes output_<job>_<batch>_<host>.json and PUTs it into the store
+                 queues, in-flight sets and job-id counters on every rank, and
+                 enqueues its own new batch on its GPU (arena slots -> H2D ->
+                 hipGraph forward; the queue keeps the GPU busy)
+    all-gather   at most one COMPLETED batch per rank (its GPU event polled,
+                 never waited on): packed top-5 [2, cap, 5] int32 + batch key ->
+                 every rank completes those batches identically (C1 counts, job
+                 completion); the coordinator also writes
+                 output_<job>_<batch>_<host>.json and PUTs it into the store
+  No rank ever waits for another rank's compute: a ResNet50 rank and an
+  InceptionV3 rank run their own queues (the old lockstep step cost the slowest
+  rank's batch time on every rank).
 
   The coordinator is the highest alive global rank — the same rank the
   control plane's bully election (cluster/election.py, prio = rank) makes the
@@ -50,7 +57,7 @@ import os
 import queue
 import threading
 import time
-from collections import OrderedDict
+from collections import OrderedDict, deque
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -325,26 +332,28 @@ class Inflight:
     rank: int
     batch: Batch
     t_dispatch: float
+    seq: int            # dispatch order (requeue restores queue order)
 
 
 class ReplicatedCoordinator:
     """The job service's state machine (reference leader, worker.py:176-495,
     989-1037), identical on every rank: log records and dispatch tables are
-    applied in broadcast order, results in all-gather order. Only the active
+    applied in broadcast order, completions in all-gather order. Only the active
     coordinator PLANS tables (its cost model is timing-dependent) and writes
-    outputs; replicas apply what it broadcast."""
+    outputs; replicas apply what it broadcast. Each rank may hold up to
+    ``depth`` dispatched batches (its GPU work queue)."""
 
-    def __init__(self, batch_sizes: Dict[str, int], cap: int = 256, host_tag: str = "node"):
-        self.cap = cap
+    def __init__(self, batch_sizes: Dict[str, int], cap: int = 256, host_tag: str = "node", depth: int = 2):
+        self.cap, self.depth = cap, depth
         self.jobs = JobManager({m: min(int(b), cap) for m, b in batch_sizes.items()})
         self.cost = CostModel()
         self.metrics = Metrics()
-        self.inflight: Dict[int, Dict[int, Inflight]] = {}   # step -> global rank -> batch
-        self.step_t0: Dict[int, float] = {}
+        self.inflight: "OrderedDict[tuple, Inflight]" = OrderedDict()   # batch key -> assignment
+        self.seq = 0
         self.requeued = 0
         self.host_tag = host_tag
         self.lock = threading.RLock()      # control-thread readers (C1/C2/C5/status) vs the serve loop
-        self.history: "OrderedDict[int, list]" = OrderedDict()  # step -> [(batch, idx, p, grank)]
+        self.history: "OrderedDict[tuple, tuple]" = OrderedDict()  # key -> (batch, idx, p, grank), recent
 
     # ------------------------------------------------------------- log ----
     def apply(self, rec: dict) -> dict:
@@ -362,7 +371,6 @@ class ReplicatedCoordinator:
         if op == "state":  # new coordinator's full state after a rebuild
             self.jobs.restore(rec["jobs"], requeue_inprogress=True)
             self.inflight.clear()
-            self.step_t0.clear()
             return {}
         raise ValueError(f"unknown log record {op}")
 
@@ -373,35 +381,42 @@ class ReplicatedCoordinator:
     def idle(self) -> bool:
         return self.jobs.pending() == 0 and not self.jobs.inprogress
 
+    def outstanding(self, grank: int) -> int:
+        return sum(1 for inf in self.inflight.values() if inf.rank == grank)
+
     # ---------------------------------------------------------- tables ----
-    def next_table(self, step: int, members: List[int]) -> np.ndarray:
-        """(active coordinator) plan step ``step``: fair-share split of the
-        members between the two models' queues (reference worker.py:255-495)."""
+    def next_table(self, members: List[int]) -> np.ndarray:
+        """(active coordinator) at most one new batch per rank whose queue has
+        room: fair-share split of those ranks between the two models' queues
+        (reference worker.py:255-495)."""
         t = np.zeros((len(members), DESC_FIELDS), np.int64)
         t[:, F_MODEL] = IDLE
         queued = {m: len(self.jobs.queues[m]) for m in MODELS}
-        if not any(queued.values()):
-            self.inflight[step] = {}
+        free = [g for g in members if self.outstanding(g) < self.depth]
+        if not any(queued.values()) or not free:
             return t
-        workers = [f"rank{g}" for g in members]
-        assigns = plan(queued, workers, {}, workers, self.cost, self.jobs.batch_sizes)
-        now = time.monotonic()
-        cur: Dict[int, Inflight] = {}
+        workers = [f"rank{g}" for g in free]
+        online = [f"rank{g}" for g in members]
+        running = {}
+        for inf in self.inflight.values():  # what every rank is busy with (fair-share input)
+            running.setdefault(f"rank{inf.rank}", (inf.batch.model, inf.batch.key))
+        running = {w: v for w, v in running.items() if w not in workers}
+        assigns = plan(queued, workers, running, online, self.cost, self.jobs.batch_sizes, preempt=False)
+        taken = {m: 0 for m in MODELS}
         for a in assigns:
-            g = int(a.worker[4:])
-            b = self.jobs.pop_next(a.model)
-            if b is None:
+            q = self.jobs.queues[a.model]
+            if taken[a.model] >= len(q):
                 continue
+            b = q[taken[a.model]]   # popped for real by apply_table, on every rank
+            taken[a.model] += 1
+            g = int(a.worker[4:])
             t[members.index(g)] = (b.job_id, b.batch_id, MODEL_IDS[b.model], 0, len(b.images), 0)
-            cur[g] = Inflight(g, b, now)
-        self.inflight[step] = cur
-        self.step_t0[step] = now
         return t
 
-    def apply_table(self, step: int, table: np.ndarray, members: List[int]) -> None:
-        """(replica) take exactly the broadcast batches out of the local queues."""
+    def apply_table(self, table: np.ndarray, members: List[int]) -> None:
+        """Take exactly the broadcast batches out of the local queues (every
+        rank, the coordinator included)."""
         now = time.monotonic()
-        cur: Dict[int, Inflight] = {}
         for r, g in enumerate(members):
             if int(table[r, F_MODEL]) < 0:
                 continue
@@ -409,59 +424,54 @@ class ReplicatedCoordinator:
             b = self.jobs.pop_key(model, (int(table[r, F_JOB]), int(table[r, F_BATCH])))
             if b is None:
                 raise RuntimeError(f"replica diverged: batch {table[r, F_JOB]}:{table[r, F_BATCH]} not queued")
-            cur[g] = Inflight(g, b, now)
-        self.inflight[step] = cur
-        self.step_t0[step] = now
+            self.inflight[b.key] = Inflight(g, b, now, self.seq)
+            self.seq += 1
 
-    def batch_of(self, step: int, grank: int) -> Optional[Batch]:
-        inf = self.inflight.get(step, {}).get(grank)
+    def assigned(self, table: np.ndarray, members: List[int], grank: int) -> Optional[Batch]:
+        row = table[members.index(grank)]
+        if int(row[F_MODEL]) < 0:
+            return None
+        inf = self.inflight.get((int(row[F_JOB]), int(row[F_BATCH])))
         return None if inf is None else inf.batch
 
     # -------------------------------------------------------- complete ----
-    def complete(self, step: int, gathered: Optional[Sequence[np.ndarray]], members: List[int]
-                 ) -> List[Tuple[Batch, np.ndarray, np.ndarray, int]]:
-        """Results of step ``step`` (all-gathered, group-rank order). Returns the
-        completed batches with their rows (for the output writer)."""
+    def complete(self, key: tuple, rows: Optional[np.ndarray], service: float = 0.0
+                 ) -> Optional[Tuple[Batch, np.ndarray, np.ndarray, int]]:
+        """Batch ``key`` finished (its all-gathered result rows). Returns what
+        the output writer needs, or None for an unknown / duplicate key."""
+        inf = self.inflight.pop(key, None)
         now = time.monotonic()
-        service = now - self.step_t0.pop(step, now)
-        done = []
-        for g, inf in self.inflight.pop(step, {}).items():
-            b = inf.batch
-            if self.jobs.complete(b.key, now=now) is None:
-                continue
-            n = len(b.images)
-            self.metrics.record(b.model, now - inf.t_dispatch, service, n)
-            self.cost.observe(b.model, n, service)
-            if gathered is not None and g in members:
-                res = gathered[members.index(g)]
-                idx, p = res[0, :n].copy(), res[1, :n].view(np.float32).copy()
-                done.append((b, idx, p, g))
-        if done:
-            self.history[step] = done
-            while len(self.history) > RESULT_HISTORY:
-                self.history.popitem(last=False)
+        if inf is None or self.jobs.complete(key, now=now) is None:
+            return None
+        b = inf.batch
+        n = len(b.images)
+        self.metrics.record(b.model, now - inf.t_dispatch, service or now - inf.t_dispatch, n)
+        self.cost.observe(b.model, n, service or now - inf.t_dispatch)
+        if rows is None:
+            return None
+        done = (b, rows[0, :n].copy(), rows[1, :n].view(np.float32).copy(), inf.rank)
+        self.history[key] = done
+        while len(self.history) > RESULT_HISTORY:
+            self.history.popitem(last=False)
         return done
 
     def requeue_inflight(self) -> int:
-        """Failure: every batch of every in-flight step goes back to the FRONT
-        of its queue (newest step first, so queue order is preserved)."""
+        """Failure: every dispatched batch goes back to the FRONT of its queue
+        (newest dispatch first, so queue order is preserved)."""
         n = 0
-        for step in sorted(self.inflight, reverse=True):
-            for g, inf in sorted(self.inflight[step].items(), reverse=True):
-                if self.jobs.requeue_front(inf.batch.key) is not None:
-                    n += 1
+        for inf in sorted(self.inflight.values(), key=lambda i: -i.seq):
+            if self.jobs.requeue_front(inf.batch.key) is not None:
+                n += 1
         self.inflight.clear()
-        self.step_t0.clear()
         self.requeued += n
         return n
 
     def assignments(self) -> Dict[str, dict]:
-        """C5: {rank: {model, job_id, batch_id}} of the steps in flight."""
+        """C5: {rank: {model, job_id, batch_id}} — the oldest batch of each rank's queue."""
         out = {}
-        for step in sorted(self.inflight):
-            for g, inf in self.inflight[step].items():
-                out[f"rank{g}"] = {"model": inf.batch.model, "job_id": inf.batch.job_id,
-                                   "batch_id": inf.batch.batch_id}
+        for inf in self.inflight.values():
+            out.setdefault(f"rank{inf.rank}", {"model": inf.batch.model, "job_id": inf.batch.job_id,
+                                               "batch_id": inf.batch.batch_id})
         return out
 
 
@@ -520,27 +530,42 @@ class OutputWriter:
 class CollectiveService:
     """The per-rank serve loop (identical on every rank). See the module doc.
 
+    Per-rank work queues, no lockstep on compute: a step is one broadcast (log
+    + dispatch table: at most one new batch per rank whose queue holds fewer
+    than ``coord.depth`` batches) and one all-gather of at most one COMPLETED
+    batch per rank (a rank contributes a batch once its GPU event has fired —
+    polled, never waited on), so the collectives run at host speed while every
+    GPU works through its own queue; a ResNet50 rank and an InceptionV3 rank
+    never wait for each other. Collectives run on their own HIP stream.
+
     ``control``: optional RankControl (UDP control plane + store of this rank);
     without it (tests, benches) jobs are submitted with ``submit_local`` on the
     coordinator rank."""
 
     def __init__(self, eg: ElasticGroup, backend: RankBackend, coord: ReplicatedCoordinator,
                  control=None, writer: Optional[OutputWriter] = None, kill_rank: int = -1, kill_at_step: int = -1,
-                 on_device: bool = False, idle_sleep: float = 0.002, watchdog_s: float = 0.0):
+                 on_device: bool = False, idle_sleep: float = 0.002, poll_sleep: float = 0.0001,
+                 watchdog_s: float = 0.0):
+        if coord.depth > 2:
+            raise ValueError("rank queues deeper than the backends' 2 source/result slots")
         self.eg, self.be, self.coord, self.control = eg, backend, coord, control
         self.writer = writer
         self.kill_rank, self.kill_at_step = kill_rank, kill_at_step
         self.dev = backend.device if on_device else torch.device("cpu")
+        self.comm = torch.cuda.Stream(self.dev) if self.dev.type == "cuda" else None
         self.steps = 0
         self.rebuilds = 0
-        self.pending = None  # (step, result tensor, event) of the step awaiting its all-gather
         self.cap = backend.cap
-        self._idle = torch.zeros((2, self.cap, 5), dtype=torch.int32, device=self.dev)
-        self.idle_sleep = idle_sleep
+        self.local: "deque" = deque()   # (key, result, event) launched here, not yet reported
+        self.launched = 0
+        self.sbuf = torch.zeros((2, self.cap + 1, 5), dtype=torch.int32, device=self.dev)
+        self.idle_sleep, self.poll_sleep = idle_sleep, poll_sleep
         self._inbox: "queue.Queue" = queue.Queue()   # (record, reply callback or None)
         self._written: Dict[int, set] = {}             # job id -> batch ids whose output is durable
         self._stop = False
         self.last_progress = time.monotonic()
+        self.phase_s: Dict[str, float] = {"plan": 0.0, "broadcast": 0.0, "launch": 0.0, "exchange": 0.0,
+                                          "complete": 0.0, "sleep": 0.0}
         self._watchdog = None
         if watchdog_s > 0:
             self._watchdog = threading.Thread(target=self._watch, args=(watchdog_s,), daemon=True)
@@ -581,30 +606,44 @@ class CollectiveService:
             replies.append(reply)
         return recs, replies
 
-    # -------------------------------------------------------------- step --
-    def _collect(self) -> None:
-        """All-gather + complete the pending step (all ranks, lockstep)."""
-        if self.pending is None:
-            return
-        k, res, ev = self.pending
-        if ev is not None:
-            if self.dev.type == "cuda":
-                torch.cuda.current_stream(self.dev).wait_event(ev)  # RCCL waits on the GPU, not the host
-            else:
-                ev.synchronize()
-        res = res.to(self.dev)
-        bufs = [torch.empty_like(res) for _ in range(self.eg.world)]
-        self.eg.all_gather(bufs, res)
-        self.pending = None
-        gathered = [b.cpu().numpy() for b in bufs]
-        with self.coord.lock:
-            done = self.coord.complete(k, gathered, self.eg.members)
-        if self.is_coordinator():
-            for b, idx, p, g in done:
-                if self.writer is not None:
-                    self.writer.submit(b, idx, p, g, on_written=self._output_written)
-            if self.control is not None and self.writer is None:
-                self.control.jobs_progress([b for b, *_ in done])
+    # ----------------------------------------------------------- results --
+    def _completed_local(self):
+        """The oldest launched batch if its GPU work has finished (non-blocking)."""
+        if not self.local:
+            return None
+        key, res, ev = self.local[0]
+        if ev is not None and not ev.query():
+            return None
+        return self.local.popleft()
+
+    def _exchange(self) -> List[Tuple[tuple, np.ndarray]]:
+        """All-gather at most one completed batch per rank -> [(key, rows)]."""
+        done = self._completed_local()
+        sb = self.sbuf
+        world, cap = self.eg.world, self.cap
+        if self.comm is not None:
+            ctx = torch.cuda.stream(self.comm)
+        else:
+            import contextlib
+
+            ctx = contextlib.nullcontext()
+        with ctx:
+            sb[0, cap, :2] = -1
+            if done is not None:
+                key, res, ev = done
+                if ev is not None and self.comm is not None:
+                    self.comm.wait_event(ev)  # (already fired: ordering for the comm stream only)
+                sb[:, :cap].copy_(res.to(self.dev))
+                sb[0, cap, 0], sb[0, cap, 1] = int(key[0]), int(key[1])
+            out = torch.empty((world, *sb.shape), dtype=sb.dtype, device=self.dev)
+            self.eg.all_gather_into(out, sb)
+            host = out.cpu().numpy()
+        got = []
+        for r in range(world):
+            j, b = int(host[r, 0, cap, 0]), int(host[r, 0, cap, 1])
+            if j >= 0:
+                got.append(((j, b), host[r, :, :cap]))
+        return got
 
     def _output_written(self, b: Batch) -> None:
         """(writer thread) A job is reported finished to its requester only once
@@ -619,11 +658,14 @@ class CollectiveService:
         if ready and self.control is not None:
             self.control.jobs_progress([b])
 
+    # -------------------------------------------------------------- step --
     def step(self, stop_when_idle: bool = False) -> bool:
         eg, coord = self.eg, self.coord
         k = self.steps
         world = eg.world
-        hdr = torch.zeros(HDR + world * DESC_FIELDS, dtype=torch.int64, device=self.dev)
+        root = eg.group_rank_of(self.coordinator_rank())
+        ph, t0 = self.phase_s, time.perf_counter()
+        hcpu = np.zeros(HDR + world * DESC_FIELDS, np.int64)
         active = self.is_coordinator()
         payload = b""
         replies: List[Optional[Callable]] = []
@@ -633,54 +675,74 @@ class CollectiveService:
             with coord.lock:
                 results = [coord.apply(r) for r in recs]
                 stop = self._stop or (stop_when_idle and coord.idle() and not recs)
-                table = coord.next_table(k, eg.members) if not stop else None
+                table = coord.next_table(eg.members) if not stop else None
             if recs:
                 payload = json.dumps(recs).encode()
-            hdr[0] = len(payload)
-            hdr[1] = k
-            hdr[2] = 1 if stop else 0
+            hcpu[0] = len(payload)
+            hcpu[1] = k
+            hcpu[2] = 1 if stop else 0
             if table is not None:
-                hdr[HDR:] = torch.from_numpy(table.reshape(-1))
-        eg.broadcast(hdr, src=eg.group_rank_of(self.coordinator_rank()))
-        h = hdr.cpu().numpy()
-        n = int(h[0])
-        if n:
-            buf = torch.zeros(n, dtype=torch.uint8, device=self.dev)
-            if active:
-                buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
-            eg.broadcast(buf, src=eg.group_rank_of(self.coordinator_rank()))
-            if not active:
-                with coord.lock:
-                    for r in json.loads(bytes(buf.cpu().numpy()).decode()):
-                        coord.apply(r)
+                hcpu[HDR:] = table.reshape(-1)
+        t1 = time.perf_counter()
+        ph["plan"] += t1 - t0
+        with (torch.cuda.stream(self.comm) if self.comm is not None else _null()):
+            hdr = torch.from_numpy(hcpu).to(self.dev)  # staged on the comm stream itself
+            eg.broadcast(hdr, src=root)
+            h = hdr.cpu().numpy()
+            n = int(h[0])
+            if n:
+                buf = torch.zeros(n, dtype=torch.uint8, device=self.dev)
+                if active:
+                    buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
+                eg.broadcast(buf, src=root)
+                if not active:
+                    with coord.lock:
+                        for r in json.loads(bytes(buf.cpu().numpy()).decode()):
+                            coord.apply(r)
         if active and self.control is not None:
             self.control.committed(replies, results)
         elif active:
             for cb, r in zip(replies, results):
                 if cb is not None:
                     cb(r)
-        if int(h[2]) == 1:  # STOP
-            self._collect()
+        t2 = time.perf_counter()
+        ph["broadcast"] += t2 - t1
+        if int(h[2]) == 1:  # STOP (sent only when nothing is queued or in flight)
             return False
         table = h[HDR:].reshape(world, DESC_FIELDS)
-        if not active:
-            with coord.lock:
-                coord.apply_table(k, table, eg.members)
+        with coord.lock:
+            coord.apply_table(table, eg.members)
+            mine = coord.assigned(table, eg.members, eg.grank)
         if k == self.kill_at_step and eg.grank == self.kill_rank:
             log.warning("rank %d: injected kill at step %d", eg.grank, k)
             os._exit(17)
-        row = table[eg.rank]
-        launched = (self._idle, None)
-        if int(row[F_MODEL]) >= 0:
-            b = coord.batch_of(k, eg.grank)
-            launched = self.be.launch(b.model, b.images, k % 2)
-        idle_step = (table[:, F_MODEL] < 0).all() and self.pending is None
-        self._collect()  # step k-1, overlapping batch k
-        self.pending = (k, launched[0], launched[1])
+        if mine is not None:
+            res, ev = self.be.launch(mine.model, mine.images, self.launched % 2)
+            self.launched += 1
+            self.local.append((mine.key, res, ev))
+        t3 = time.perf_counter()
+        ph["launch"] += t3 - t2
+        got = self._exchange()
+        t4 = time.perf_counter()
+        ph["exchange"] += t4 - t3
+        if got:
+            with coord.lock:
+                finished = [coord.complete(key, rows) for key, rows in got]
+            if self.is_coordinator():
+                done = [d for d in finished if d is not None]
+                for b, idx, p, g in done:
+                    if self.writer is not None:
+                        self.writer.submit(b, idx, p, g, on_written=self._output_written)
+                if self.control is not None and self.writer is None:
+                    self.control.jobs_progress([d[0] for d in done])
         self.steps += 1
         self.last_progress = time.monotonic()
-        if idle_step and self.idle_sleep:
-            time.sleep(self.idle_sleep)
+        t5 = time.perf_counter()
+        ph["complete"] += t5 - t4
+        if not got and mine is None and not n:
+            # nothing moved: poll again soon while GPUs work, back off when idle
+            time.sleep(self.poll_sleep if coord.inflight else self.idle_sleep)
+            ph["sleep"] += time.perf_counter() - t5
         return True
 
     # -------------------------------------------------------------- serve --
@@ -691,11 +753,6 @@ class CollectiveService:
                     break
             except CollectiveFailure as e:
                 self._recover(e)
-        else:
-            try:
-                self._collect()
-            except CollectiveFailure:
-                pass
         if self.writer is not None:
             self.writer.flush()
         return self.steps
@@ -703,26 +760,30 @@ class CollectiveService:
     def _recover(self, e: Exception) -> None:
         eg = self.eg
         log.warning("rank %d: collective failed (%s); rebuilding", eg.grank, e)
-        self.pending = None
         with self.coord.lock:
             self.coord.requeue_inflight()
         deadline = time.monotonic() + 10
         while not (eg.dead & set(eg.members)) and time.monotonic() < deadline:
             time.sleep(0.01)  # let SWIM confirm who died
         was = self.coordinator_rank()
-        eg.rebuild(set(eg.dead))
+        eg.rebuild(set(eg.dead))  # aborts the communicator first (RCCL: ncclCommAbort)
+        # the requeued batches' GPU work may still be running: let it drain before
+        # their slots are reused (compute streams only; the aborted comm stream is not waited on)
+        for st in (getattr(self.be, "stream", None), getattr(self.be, "copy_stream", None)):
+            if st is not None:
+                st.synchronize()
+        self.local.clear()
         self.rebuilds += 1
         # the new coordinator's state is authoritative: replicas that completed one
-        # step more or less than it did are repaired by a state record
+        # exchange more or less than it did are repaired by a state record
         if self.is_coordinator():
             with self.coord.lock:
                 snap = self.coord.jobs.snapshot()
             with self._inbox.mutex:
                 self._inbox.queue.appendleft(({"op": "state", "jobs": snap}, None))
             if was != eg.grank and self.writer is not None:  # takeover: re-PUT recent outputs
-                for step, done in self.coord.history.items():
-                    for b, idx, p, g in done:
-                        self.writer.submit(b, idx, p, g, on_written=self._output_written)
+                for b, idx, p, g in list(self.coord.history.values()):
+                    self.writer.submit(b, idx, p, g, on_written=self._output_written)
             if self.control is not None:
                 self.control.became_coordinator(was)
         self.last_progress = time.monotonic()
@@ -736,6 +797,12 @@ class CollectiveService:
             if time.monotonic() - self.last_progress > limit_s:
                 log.error("rank %d: no progress for %.0f s, exiting", self.eg.grank, limit_s)
                 os._exit(3)
+
+
+def _null():
+    import contextlib
+
+    return contextlib.nullcontext()
 
 
 # ------------------------------------------------------------ control plane ----

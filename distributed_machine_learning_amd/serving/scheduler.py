@@ -40,13 +40,15 @@ def best_split(n: int, rate_a: float, rate_b: float) -> Tuple[int, int]:
 
 def plan(queued: Dict[str, int], free: Sequence[str], running: Dict[str, Tuple[str, tuple]],
          online: Sequence[str], cost: CostModel, batch_sizes: Dict[str, int],
-         models: Sequence[str] = ("InceptionV3", "ResNet50")) -> List[Assignment]:
+         models: Sequence[str] = ("InceptionV3", "ResNet50"), preempt: bool = True) -> List[Assignment]:
     """Decide which worker runs what next.
 
     queued:  model -> number of queued batches
     free:    idle alive workers
     running: worker -> (model, batch key) currently executing
     online:  all alive workers
+    preempt: steal workers running the other model (the reference's policy);
+             the collective service's per-rank queues only fill free slots
     """
     free = sorted(free)
     active = [m for m in models if queued.get(m, 0) > 0]
@@ -73,7 +75,7 @@ def plan(queued: Dict[str, int], free: Sequence[str], running: Dict[str, Tuple[s
             have += 1
             budget[m] -= 1
         # then steal from the other model's running workers beyond its own share
-        while have < want[m] and budget[m] > 0 and len(run_by[other]) > want[other]:
+        while preempt and have < want[m] and budget[m] > 0 and len(run_by[other]) > want[other]:
             w = run_by[other].pop()
             out.append(Assignment(w, m, preempt=(other, running[w][1])))
             have += 1

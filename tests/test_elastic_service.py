@@ -122,36 +122,40 @@ def test_coordinator_kill_mid_job_failover(tmp_path):
     assert {tuple(os.path.basename(f).split("_")[1:3]) for f in files} == batches
 
 
-def test_replicated_state_machine_two_steps_in_flight():
-    """Coordinator and replica apply the same records/tables -> same state; a
-    failure requeues both in-flight steps at the queue front in their original
-    order; completion is per step; C3 is clamped to the result capacity."""
+def test_replicated_state_machine_queues():
+    """Coordinator and replica apply the same records/tables -> same state; each
+    rank's queue holds at most ``depth`` batches; a failure requeues every
+    dispatched batch at the queue front in dispatch order; completion is per
+    batch (out of order is fine); C3 is clamped to the result capacity."""
     import numpy as np
 
-    from distributed_machine_learning_amd.parallel.dataplane import F_BATCH
+    from distributed_machine_learning_amd.parallel.dataplane import F_BATCH, F_MODEL
     from distributed_machine_learning_amd.parallel.service import ReplicatedCoordinator, synthetic_names
 
-    c = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4)
-    rep = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4)
+    c = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4, depth=2)
+    rep = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4, depth=2)
     rec = {"op": "submit", "model": "ResNet50", "images": synthetic_names(16), "job_id": c.next_job_id()}
     assert c.apply(rec) == rep.apply(rec) == {"jobid": 31, "batches": 4}
     assert c.apply({"op": "batch_size", "model": "ResNet50", "batch_size": 64}) == {"model": "ResNet50",
                                                                                       "batch_size": 4}
-    t0 = c.next_table(0, [0])
-    t1 = c.next_table(1, [0])
-    rep.apply_table(0, t0, [0])
-    rep.apply_table(1, t1, [0])
-    assert sorted(c.inflight) == sorted(rep.inflight) == [0, 1]
-    assert c.batch_of(1, 0).key == rep.batch_of(1, 0).key
-    first = [int(t0[0, F_BATCH]), int(t1[0, F_BATCH])]
+    tables = []
+    for _ in range(3):
+        t = c.next_table([0])
+        tables.append(t)
+        for x in (c, rep):
+            x.apply_table(t, [0])
+    assert int(tables[2][0, F_MODEL]) < 0            # queue depth 2 reached: nothing new for rank 0
+    assert list(c.inflight) == list(rep.inflight) == [(31, 1), (31, 2)] and c.outstanding(0) == 2
+    assert c.assigned(tables[1], [0], 0).key == (31, 2)
     assert c.requeue_inflight() == 2 and not c.inflight
-    t2 = c.next_table(2, [0])
-    t3 = c.next_table(3, [0])
-    assert [int(t2[0, F_BATCH]), int(t3[0, F_BATCH])] == first
-    res = np.zeros((2, 4, 5), np.int32)
-    done = c.complete(3, [res], [0])                # out-of-order completion is per step
-    assert sorted(c.inflight) == [2] and len(done) == 1
-    c.complete(2, None, [0])
+    assert [b.key for b in c.jobs.queues["ResNet50"]][:2] == [(31, 1), (31, 2)]
+    for _ in range(2):
+        c.apply_table(c.next_table([0]), [0])
+    rows = np.zeros((2, 4, 5), np.int32)
+    done = c.complete((31, 2), rows)                 # out-of-order completion is per batch
+    assert done is not None and list(c.inflight) == [(31, 1)]
+    assert c.complete((31, 2), rows) is None         # duplicate completion is ignored
+    c.complete((31, 1), None)
     assert not c.inflight and c.metrics.c1()["ResNet50"]["query_count"] == 8
     # a new coordinator's state record repairs a diverged replica
     rep.apply({"op": "state", "jobs": c.jobs.snapshot()})

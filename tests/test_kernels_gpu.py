@@ -43,7 +43,7 @@ def _pads(kh, kw, pad):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 15, 16, 17, 18, 23, 24, 25, 26, 27, 28, 29,
+@pytest.mark.parametrize("cfg", [-1, 10, 11, 12, 13, 14, 15, 16, 17, 18, 23, 24, 25, 26, 27, 28, 29,
                                  30, 31, 32, 33, 34, 36, 37])
 def test_conv_matches_fp32(case, cfg):
     n, h, w, cin, cout, kh, kw, s, pad, relu, has_res = case
@@ -214,7 +214,7 @@ def test_preprocess(mode, hw):
 
 
 @pytest.mark.parametrize("kh,kw,s,p,hw,mode", [(7, 7, 2, 3, (224, 224), "caffe"), (3, 3, 2, 0, (299, 299), "tf")])
-@pytest.mark.parametrize("cfg", [-1, 0, 15])
+@pytest.mark.parametrize("cfg", [-1, 11, 15])
 def test_pair_packed_stem(kh, kw, s, p, hw, mode, cfg):
     """preprocess(pair=True) + dilation-2 conv with pair-packed weights == the plain
     stem conv on the normal preprocess output."""
@@ -271,74 +271,42 @@ def test_avgpool_relu_flag():
     assert _rel(y.float().cpu().permute(0, 3, 1, 2), ref) < 1e-2
 
 
-HALO_CASES = [
-    # n, h, w, cin, cout, kh, kw, pad, relu, residual  (stride 1)
-    (3, 56, 56, 64, 64, 3, 3, 1, True, False),    # ResNet conv2 3x3; tiles cross images
-    (2, 28, 28, 128, 128, 3, 3, 1, True, False),  # 2 channel chunks (double-buffered halo)
-    (3, 14, 14, 256, 256, 3, 3, 1, True, True),   # 4 chunks + residual epilogue
-    (5, 7, 7, 512, 512, 3, 3, 1, True, False),    # 8 chunks, tiles span several images
-    (2, 9, 11, 64, 96, 3, 3, 1, True, False),
-    (1, 35, 35, 48, 64, 5, 5, 1, True, False),    # Cin % 64 != 0: zero channel tail
-    (2, 17, 17, 128, 192, 1, 7, 1, True, False),
-    (2, 17, 17, 160, 192, 7, 1, 1, True, False),
-    (2, 8, 8, 384, 384, 1, 3, 1, True, False),
-    (2, 8, 8, 448, 384, 3, 3, 1, True, False),
-    (1, 37, 37, 80, 192, 3, 3, 0, True, False),   # 'valid' padding (Inception stem)
-    (2, 35, 35, 96, 96, 3, 3, 1, False, False),
+CHUNK_CASES = [
+    # n, h, w, cin, cout, kh, kw, stride, pad, relu, residual
+    (3, 56, 56, 64, 64, 3, 3, 1, 1, True, False),     # ResNet conv2 3x3
+    (2, 28, 28, 128, 128, 3, 3, 1, 1, True, False),   # 2 channel chunks
+    (3, 14, 14, 256, 256, 3, 3, 2, 1, True, True),    # stride 2, 4 chunks, residual epilogue
+    (2, 17, 17, 128, 192, 1, 7, 1, 0, True, False),
+    (2, 8, 8, 448, 384, 3, 3, 1, 1, False, False),    # 7 chunks
 ]
 
 
-@pytest.mark.parametrize("case", HALO_CASES)
-@pytest.mark.parametrize("cfg", list(ops.HALO_CFGS))
-def test_halo_conv_matches_fp32(case, cfg):
-    """Stride-1 halo-tile conv (csrc/kernels/conv_halo.hip) vs fp32 F.conv2d."""
-    import ctypes as C
-    from distributed_machine_learning_amd import _native as N
-
-    n, h, w, cin, cout, kh, kw, pad, relu, has_res = case
-    ph, pw = (kh // 2, kw // 2) if pad else (0, 0)
+@pytest.mark.parametrize("case", CHUNK_CASES)
+@pytest.mark.parametrize("cfg", [11, 14, 15, 28, 30])
+def test_conv_chunk_major_k_order(case, cfg):
+    """K order (channel chunk, r, s, c) (DmlConvArgs.kchunk = 64) vs fp32 F.conv2d."""
+    n, h, w, cin, cout, kh, kw, s, pad, relu, has_res = case
+    ph, pw = _pads(kh, kw, pad)
     torch.manual_seed(0)
     x = _bf(torch.randn(n, cin, h, w))
     wt = _bf(torch.randn(cout, cin, kh, kw) * (2.0 / (cin * kh * kw)) ** 0.5)
     b = torch.randn(cout) * 0.1
-    ref = F.conv2d(x, wt, b, padding=(ph, pw))
+    ref = F.conv2d(x, wt, b, stride=s, padding=(ph, pw))
     res = None
     if has_res:
         res = _bf(torch.randn_like(ref))
         ref = ref + res
     if relu:
         ref = F.relu(ref)
-    wp, K, kpad = ops.pack_weight_halo(wt)
-    ho, wo = ref.shape[2], ref.shape[3]
-    probe = N.ConvArgs(None, None, None, 1 if has_res else None, None, n, h, w, cin, cin, kh, kw, 1, 1, ph, pw,
-                       ho, wo, cout, K, kpad, cout, cout, 0, 0, 1, 1)
-    if not ops.halo_ok(probe, cfg):
-        pytest.skip("shape outside this halo config's LDS budget")
+    wp, K, _ = ops.pack_weight_chunk_major(wt, 64)
     xd = x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
     rd = res.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16) if res is not None else None
-    y = ops.conv2d_nhwc(xd, wp.cuda(), b.cuda(), cout, kh, kw, (1, 1), (ph, pw), relu=relu, residual=rd, cfg=cfg)
+    y = ops.conv2d_nhwc(xd, wp.cuda(), b.cuda(), cout, kh, kw, (s, s), (ph, pw), relu=relu, residual=rd, cfg=cfg,
+                        kchunk=64)
     torch.cuda.synchronize()
     got = y[..., :cout].float().cpu().permute(0, 3, 1, 2)
     assert got.shape == ref.shape
     assert _rel(got, ref) < 1.5e-2, _rel(got, ref)
-
-
-def test_halo_concat_offsets():
-    """Halo conv reading a channel slice and writing at a channel offset."""
-    torch.manual_seed(4)
-    x = _bf(torch.randn(2, 160, 17, 17))
-    wt = _bf(torch.randn(96, 64, 3, 3) * 0.05)
-    b = torch.randn(96) * 0.1
-    xd = x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
-    out = torch.full((2, 17, 17, 128), 7.0, device="cuda", dtype=torch.bfloat16)
-    wp, _, _ = ops.pack_weight_halo(wt)
-    ops.conv2d_nhwc(xd, wp.cuda(), b.cuda(), 96, 3, 3, pad=(1, 1), in_coff=32, cin=64, out=out, out_coff=32,
-                    relu=True, cfg=40)
-    torch.cuda.synchronize()
-    got = out.float().cpu().permute(0, 3, 1, 2)
-    ref = F.relu(F.conv2d(x[:, 32:96], wt, b, padding=1))
-    assert _rel(got[:, 32:128], ref) < 1.5e-2
-    assert torch.all(got[:, :32] == 7.0)
 
 
 @pytest.mark.parametrize("cfg", [10, 11, 12, 13, 14, 15, 16, 17, 18, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33,
@@ -364,9 +332,11 @@ def test_conv_subsampled_residual(case, cfg):
     assert _rel(got, ref) < 1.5e-2, _rel(got, ref)
 
 
-def test_conv_subsampled_residual_v1_refused():
+def test_conv_non_tile_config_refused():
+    """cfg ids outside the v2 tile configs (the removed v1 / halo kernels) and
+    shapes no tile config can run fail loudly on the host."""
     x = torch.zeros(1, 4, 4, 64, device="cuda", dtype=torch.bfloat16)
     wp, _, _ = ops.pack_weight(torch.zeros(64, 64, 1, 1))
-    rd = torch.zeros(1, 8, 8, 64, device="cuda", dtype=torch.bfloat16)
-    with pytest.raises(Exception):
-        ops.conv2d_nhwc(x, wp.cuda(), torch.zeros(64), 64, 1, 1, residual=rd, cfg=0)
+    for cfg in (0, 4, 40):
+        with pytest.raises(Exception):
+            ops.conv2d_nhwc(x, wp.cuda(), torch.zeros(64), 64, 1, 1, cfg=cfg)

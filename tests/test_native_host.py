@@ -14,7 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = shutil.which("hipcc") or ("/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else None)
-SOURCES = ["kernels/conv_igemm.hip", "kernels/conv_igemm_v2.hip", "kernels/conv_halo.hip", "kernels/misc.hip",
+SOURCES = ["kernels/conv_dispatch.hip", "kernels/conv_igemm_v2.hip", "kernels/misc.hip",
            "kernels/stem_fused.hip", "kernels/conv_pool.hip",
            "kernels/bottleneck_fused.hip",
            "runtime/runtime.hip", "tests/host_checks.cpp"]

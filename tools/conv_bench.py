@@ -12,7 +12,7 @@ from distributed_machine_learning_amd.models.graph import Conv
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--model", default="ResNet50"); ap.add_argument("--batch", type=int, default=256)
-ap.add_argument("--cfgs", default="0,1,2,10,11,12,13,14,15,16,17"); ap.add_argument("--out", default="")
+ap.add_argument("--cfgs", default="10,11,12,13,14,15,16,17"); ap.add_argument("--out", default="")
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--only", default="", help="comma list of layer-name substrings to keep")
 ap.add_argument("--kchunk", type=int, default=0, help="also time the chunk-major K order (kchunk=64) on kxk shapes")
@@ -37,9 +37,6 @@ for key, names in shapes.items():
     x = torch.randn(B, h, w, cin, device="cuda").to(torch.bfloat16)
     w_oihw = torch.randn(cout, cin, kh, kw) * (2.0 / K) ** 0.5
     wt = ops.pack_weight(w_oihw)[0].cuda()
-    halo = st == 1 and kh * kw > 1
-    wh, _, Kh = ops.pack_weight_halo(w_oihw) if halo else (None, 0, 0)
-    wh = wh.cuda() if halo else None
     bias = torch.zeros(r(cout, 256), device="cuda")
     y = torch.empty(B, ho, wo, cout, device="cuda", dtype=torch.bfloat16)
     rs = torch.randn(B, ho, wo, cout, device="cuda").to(torch.bfloat16) if hasres else None
@@ -51,13 +48,9 @@ for key, names in shapes.items():
     row = {"layers": names, "M": B * ho * wo, "N": cout, "K": K, "kh": kh, "kw": kw, "stride": st,
            "gflop": flops / 1e9, "mb": nbytes / 1e6, "ms": {}}
     ref = None
-    ah = None
-    if halo:
-        ah = N.ConvArgs.from_buffer_copy(a)
-        ah.w, ah.Kpad = wh.data_ptr(), Kh
     ak = None
     if args.kchunk and kh * kw > 1 and cin % args.kchunk == 0 and st in (1, 2):
-        wk_, _, _ = ops.pack_weight_halo(w_oihw)  # [cout_pad][cin/64][taps][64] == chunk-major K, kchunk 64
+        wk_, _, _ = ops.pack_weight_chunk_major(w_oihw, args.kchunk)
         wk_ = wk_.cuda()
         ak = N.ConvArgs.from_buffer_copy(a)
         ak.w, ak.kchunk = wk_.data_ptr(), args.kchunk
@@ -65,11 +58,7 @@ for key, names in shapes.items():
     for cfg in variants:
         aa = a
         if cfg >= 1000:
-            aa, cfg_ = ak, cfg - 1000
-        if cfg >= 40 and cfg < 1000:
-            if ah is None or not ops.halo_ok(ah, cfg):
-                continue
-            aa = ah
+            aa = ak
         kc = cfg
         cfg = cfg - 1000 if cfg >= 1000 else cfg
         try:

@@ -30,7 +30,12 @@ def main():
     ap.add_argument("--out-dir", default="")
     ap.add_argument("--rdzv", default="", help="FileStore rendezvous path (default /tmp/dml_rdzv_<port>)")
     ap.add_argument("--swim-port", type=int, default=0)
+    ap.add_argument("--comm", default="nccl", choices=("nccl", "gloo"),
+                    help="backend of the service's control collectives (header, log, packed top-5)")
+    ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES for this process (0: HIP default)")
     a = ap.parse_args()
+    if a.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)  # before the HIP runtime initialises
 
     import torch
 
@@ -51,7 +56,8 @@ def main():
     bs = {"ResNet50": a.resnet_batch, "InceptionV3": a.inception_batch}
     cap = max(bs.values())
     backend = GpuRankBackend(dev, bs, cap=cap, arena_images=2 * cap + 64, n_synth=2 * cap)
-    eg = ElasticGroup(grank, world, store_path=rdzv, backend="nccl", device=dev, timeout_s=120)
+    eg = ElasticGroup(grank, world, store_path=rdzv, backend=a.comm, device=dev if a.comm == "nccl" else None,
+                      timeout_s=120)
     fd = RankFailureDetector(grank, world, swim_port, on_dead=eg.dead.add).start()
     kills = [tuple(int(x) for x in k.split(":")) for k in a.kill]
     kr, ks = (-1, -1)
@@ -60,40 +66,43 @@ def main():
             kr, ks = r, s
     coord = ReplicatedCoordinator(bs, cap=cap, host_tag="mi355x")
     writer = OutputWriter(a.out_dir) if a.out_dir else None
-    svc = CollectiveService(eg, backend, coord, writer=writer, kill_rank=kr, kill_at_step=ks, on_device=True,
-                            watchdog_s=300)
+    svc = CollectiveService(eg, backend, coord, writer=writer, kill_rank=kr, kill_at_step=ks,
+                            on_device=(a.comm == "nccl"), watchdog_s=300)
     if svc.is_coordinator():
         if a.resnet_images:
             svc.submit_local("ResNet50", a.resnet_images)
         if a.inception_images:
             svc.submit_local("InceptionV3", a.inception_images)
-    # warm both engines and both source slots (graph capture) outside the timed region
-    for m in ("ResNet50", "InceptionV3"):
-        for slot in (0, 1):
-            backend.launch(m, [f"synthetic:{i}" for i in range(bs[m])], slot)[1].synchronize()
-    torch.cuda.synchronize()
-    eg.barrier()
-    t0 = time.perf_counter()
-    steps = svc.serve(stop_when_idle=True)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if svc.is_coordinator():
-        c2 = coord.metrics.c2()
-        n_r = coord.metrics.query_count.get("ResNet50", 0)
-        n_i = coord.metrics.query_count.get("InceptionV3", 0)
-        out = {"metric": "concurrent ResNet50+InceptionV3 serving (images/s, whole job)",
-               "value": round((n_r + n_i) / el, 1), "unit": "images/s", "n_gpus": world,
-               "resnet50_images_per_s": round(n_r / el, 1), "inceptionv3_images_per_s": round(n_i / el, 1),
-               "elapsed_s": round(el, 3), "steps": steps, "rebuilds": svc.rebuilds, "final_members": eg.members,
-               "coordinator": svc.coordinator_rank(), "requeued_batches": coord.requeued,
-               "jobs_done": [j.done for j in coord.jobs.jobs.values()],
-               "p50_latency_ms": {m: round(v["query_latency_p50"] * 1e3, 3) for m, v in c2.items()},
-               "p90_latency_ms": {m: round(v["query_latency_p90"] * 1e3, 3) for m, v in c2.items()},
-               "batch_sizes": bs, "kills": a.kill, "dtype": "bf16", "data": "synthetic"}
-        print(json.dumps(out), flush=True)
-    fd.stop()
-    eg.close()
-
+    try:
+        # warm both engines and both source slots (graph capture) outside the timed region
+        for m in ("ResNet50", "InceptionV3"):
+            for slot in (0, 1):
+                backend.launch(m, [f"synthetic:{i}" for i in range(bs[m])], slot)[1].synchronize()
+        torch.cuda.synchronize()
+        eg.barrier()
+        t0 = time.perf_counter()
+        steps = svc.serve(stop_when_idle=True)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if svc.is_coordinator():
+            c2 = coord.metrics.c2()
+            n_r = coord.metrics.query_count.get("ResNet50", 0)
+            n_i = coord.metrics.query_count.get("InceptionV3", 0)
+            out = {"metric": "concurrent ResNet50+InceptionV3 serving (images/s, whole job)",
+                   "value": round((n_r + n_i) / el, 1), "unit": "images/s", "n_gpus": world,
+                   "resnet50_images_per_s": round(n_r / el, 1), "inceptionv3_images_per_s": round(n_i / el, 1),
+                   "elapsed_s": round(el, 3), "steps": steps, "rebuilds": svc.rebuilds,
+                   "final_members": eg.members, "coordinator": svc.coordinator_rank(),
+                   "requeued_batches": coord.requeued, "jobs_done": [j.done for j in coord.jobs.jobs.values()],
+                   "p50_latency_ms": {m: round(v["query_latency_p50"] * 1e3, 3) for m, v in c2.items()},
+                   "p90_latency_ms": {m: round(v["query_latency_p90"] * 1e3, 3) for m, v in c2.items()},
+                   "batch_sizes": bs, "kills": a.kill, "dtype": "bf16", "data": "synthetic",
+                   "comm": a.comm, "hw_queues": a.hw_queues,
+                   "loop_phase_s": {k: round(v, 4) for k, v in svc.phase_s.items()}}
+            print(json.dumps(out), flush=True)
+    finally:
+        fd.stop()
+        eg.close()
 
 if __name__ == "__main__":
     main()
