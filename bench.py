@@ -194,6 +194,7 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
             "p90_latency_ms": round(pct.get("p90_ms", 0.0), 3),
             "p99_latency_ms": round(pct.get("p99_ms", 0.0), 3),
             "verified_top5": verified,
+            "host_wait_s": {k: round(v, 4) for k, v in stats.wait_s.items()},
             "config": {"model": model, "global_batch": B * world, "seq_len": None,
                        "image_hw": list(g.input_hw), "parallelism": f"dp{world}",
                        "per_worker_batch": B, "graph": not args.no_graph, "stream_splits": splits,
@@ -283,7 +284,7 @@ def main(argv=None) -> int:
                      "synthetic uint8 RGB images, random-init weights (Keras architecture)"),
             "config": head["config"],
         }
-        for k in ("p50_latency_ms", "p90_latency_ms", "p99_latency_ms", "verified_top5", "baseline"):
+        for k in ("p50_latency_ms", "p90_latency_ms", "p99_latency_ms", "verified_top5", "host_wait_s", "baseline"):
             if k in head:
                 out[k] = head[k]
         if len(models) > 1:

@@ -63,6 +63,8 @@ def init_process_group(backend: Optional[str] = None, timeout_s: int = 600) -> t
 
 
 class DataPlane:
+    RING = 3  # descriptor buffers in flight (dispatch lookahead 2 + the one being read)
+
     def __init__(self, device: torch.device, result_shape=(2, 256, 5), group=None):
         self.group = group
         self.rank = dist.get_rank(group)
@@ -70,7 +72,14 @@ class DataPlane:
         self.device = device
         self.is_cuda = device.type == "cuda"
         self.dispatch_stream = torch.cuda.Stream(device) if self.is_cuda else None
-        self.desc = torch.zeros((self.world, DESC_FIELDS), dtype=torch.int64, device=device)
+        self.desc = [torch.zeros((self.world, DESC_FIELDS), dtype=torch.int64, device=device)
+                     for _ in range(self.RING)]
+        if self.is_cuda:  # pinned staging: table upload and row readback never block the host
+            self.host_table = [torch.zeros((self.world, DESC_FIELDS), dtype=torch.int64).pin_memory()
+                               for _ in range(self.RING)]
+            self.host_row = [torch.zeros(DESC_FIELDS, dtype=torch.int64).pin_memory() for _ in range(self.RING)]
+            self.row_ready = [torch.cuda.Event() for _ in range(self.RING)]
+        self._next = 0
         self.result_shape = tuple(result_shape)
         self.gather_bufs: List[torch.Tensor] = (
             [torch.empty(self.result_shape, dtype=torch.int32, device=device) for _ in range(self.world)]
@@ -79,25 +88,46 @@ class DataPlane:
         self.epoch = 0
 
     # ------------------------------------------------------------ dispatch --
-    def dispatch(self, table: Optional[np.ndarray]) -> np.ndarray:
-        """Broadcast the descriptor table from rank 0; return this rank's row (host)."""
+    def issue_dispatch(self, table: Optional[np.ndarray]) -> int:
+        """Enqueue the broadcast of rank 0's descriptor table and the readback
+        of this rank's row on the dispatch stream; returns a handle for
+        ``wait_dispatch``. Nothing here waits on the GPU: the serving pipeline
+        issues the table of step k+2 while step k computes, and reads it one step
+        later, so the host never blocks behind the forward it just enqueued
+        (a blocking read here cost a ~260 us GPU bubble per step,
+        profiles/r2_v1/resnet50_kernel_stats.csv trace analysis in DESIGN.md)."""
+        h = self._next
+        self._next = (self._next + 1) % self.RING
+        d = self.desc[h]
         if self.is_cuda:
             with torch.cuda.stream(self.dispatch_stream):
                 if self.rank == 0:
-                    self.desc.copy_(torch.as_tensor(table, dtype=torch.int64))
-                dist.broadcast(self.desc, src=0, group=self.group)
-                row = self.desc[self.rank].cpu()
+                    self.host_table[h].numpy()[...] = np.asarray(table, dtype=np.int64)
+                    d.copy_(self.host_table[h], non_blocking=True)
+                dist.broadcast(d, src=0, group=self.group)
+                self.host_row[h].copy_(d[self.rank], non_blocking=True)
+                self.row_ready[h].record(self.dispatch_stream)
         else:
             if self.rank == 0:
-                self.desc.copy_(torch.as_tensor(table, dtype=torch.int64))
-            dist.broadcast(self.desc, src=0, group=self.group)
-            row = self.desc[self.rank].clone()
-        return row.numpy()
+                d.copy_(torch.as_tensor(table, dtype=torch.int64))
+            dist.broadcast(d, src=0, group=self.group)
+        return h
+
+    def wait_dispatch(self, h: int) -> np.ndarray:
+        """This rank's row of the dispatch issued as ``h`` (host numpy copy)."""
+        if self.is_cuda:
+            self.row_ready[h].synchronize()
+            return self.host_row[h].numpy().copy()
+        return self.desc[h][self.rank].clone().numpy()
+
+    def dispatch(self, table: Optional[np.ndarray]) -> np.ndarray:
+        """Broadcast the descriptor table from rank 0; return this rank's row (host)."""
+        return self.wait_dispatch(self.issue_dispatch(table))
 
     # -------------------------------------------------------------- gather --
     def gather(self, result: torch.Tensor) -> Optional[List[torch.Tensor]]:
-        """Gather every rank's packed result to rank 0 (enqueued after the
-        compute that produced `result` on the current stream)."""
+        """Gather every rank's packed result to rank 0 (enqueued on the current
+        stream, after whatever produced `result` there)."""
         assert tuple(result.shape) == self.result_shape, (result.shape, self.result_shape)
         if self.rank == 0:
             dist.gather(result, self.gather_bufs, dst=0, group=self.group)

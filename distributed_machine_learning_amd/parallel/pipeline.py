@@ -37,6 +37,7 @@ class BatchRecord:
 class PipelineStats:
     latencies_s: List[float] = field(default_factory=list)
     images: int = 0
+    wait_s: dict = field(default_factory=lambda: {"dispatch": 0.0, "results": 0.0, "loop": 0.0})
 
     def percentiles(self):
         if not self.latencies_s:
@@ -77,23 +78,37 @@ class ServingPipeline:
         self.ev_copied[slot].record(cs)
 
     def run(self, steps: int, table_fn: Callable[[int], np.ndarray], record: bool = True) -> PipelineStats:
-        """Serve `steps` batches; table_fn(k) -> descriptor table (used on rank 0)."""
+        """Serve `steps` batches; table_fn(k) -> descriptor table (used on rank 0).
+
+        Dispatch runs two steps ahead: while batch k computes, the table of
+        step k+2 is broadcast (enqueued, not waited on) and the row of step k+1
+        (issued one step earlier, so already complete) is read and staged. The
+        host therefore never waits behind the forward it just enqueued and the
+        GPU always has the next forward queued."""
         dp, eng = self.dp, self.eng
         tr = _trace.get_tracer()
         is0 = dp.rank == 0
         recs: List[BatchRecord] = []
-        t0 = time.perf_counter()
-        recs.append(BatchRecord(0, t0))
-        if is0:
-            tr.begin_async("batch", 0, step=0)
-        with tr.span("dispatch", step=0):
-            row = dp.dispatch(table_fn(0) if is0 else None)
-        self._stage(0, row)
+        handles = {}
+
+        def issue(j):
+            recs.append(BatchRecord(j, time.perf_counter()))
+            if is0:
+                tr.begin_async("batch", j, step=j)
+            with tr.span("dispatch", step=j):
+                handles[j] = dp.issue_dispatch(table_fn(j) if is0 else None)
+
+        issue(0)
+        if steps > 1:
+            issue(1)
+        self._stage(0, dp.wait_dispatch(handles.pop(0)))
         prev: Optional[BatchRecord] = None
+        ds = dp.dispatch_stream
         for k in range(steps):
             slot = k % 2
             cs = self.compute_stream
             cs.wait_event(self.ev_copied[slot])
+            cs.wait_event(self.ev_gathered[slot])  # WAR: gather of step k-2 read this slot's result rows
             with torch.cuda.stream(cs), tr.gpu_span("forward", cs, lane="compute stream", step=k):
                 if self._split_deps:
                     eng.run(cs, use_graph=self.use_graph, slot=slot,
@@ -101,13 +116,18 @@ class ServingPipeline:
                 else:
                     eng.run(cs, use_graph=self.use_graph, slot=slot)
             self.ev_consumed[slot].record(cs)
-            if k + 1 < steps:  # dispatch + stage the next batch while this one computes
-                recs.append(BatchRecord(k + 1, time.perf_counter()))
-                if is0:
-                    tr.begin_async("batch", k + 1, step=k + 1)
-                with tr.span("dispatch", step=k + 1):
-                    row = dp.dispatch(table_fn(k + 1) if is0 else None)
+            if k + 1 < steps:  # stage the next batch (its row was broadcast one step ago)
+                tw = time.perf_counter()
+                row = dp.wait_dispatch(handles.pop(k + 1))
+                self.stats.wait_s["dispatch"] += time.perf_counter() - tw
                 self._stage(k + 1, row)
+            if k + 2 < steps:
+                issue(k + 2)
+            # result gather + host copy right behind forward k on the compute
+            # stream: work on another stream is starved while the forward's
+            # kernels fill every CU (measured r2: a gather on the dispatch stream
+            # ran only after the NEXT forward drained, and the host waiting for it
+            # left a ~270 us GPU bubble per step); in order here it takes ~10 us
             with torch.cuda.stream(cs), tr.gpu_span("gather", cs, lane="compute stream", step=k):
                 bufs = dp.gather(eng.results[slot])
                 self.ev_gathered[slot].record(cs)
@@ -122,14 +142,17 @@ class ServingPipeline:
         if prev is not None:
             self._finish(prev, record)
         self.compute_stream.synchronize()
+        ds.synchronize()
         return self.stats
 
     def _finish(self, rec: BatchRecord, record: bool) -> None:
         slot = rec.step % 2
         tr = _trace.get_tracer()
         if self.dp.rank == 0:
+            tw = time.perf_counter()
             with tr.span("wait results", step=rec.step):
                 self.ev_res[slot].synchronize()
+            self.stats.wait_s["results"] += time.perf_counter() - tw
             rec.t_done = time.perf_counter()
             tr.end_async("batch", rec.step, latency_ms=(rec.t_done - rec.t_dispatch) * 1e3)
             if record:
