@@ -52,8 +52,13 @@ def default_store_path(tag: str) -> str:
 class ElasticGroup:
     def __init__(self, global_rank: int, world: int, store_path: Optional[str] = None, backend: str = "gloo",
                  device: Optional[torch.device] = None, timeout_s: float = 60.0, store_host: Optional[str] = None,
-                 store_port: int = 0):
+                 store_port: int = 0, data_backend: Optional[str] = None):
+        """``backend``: the default group (control collectives); ``data_backend``:
+        a second group over the same members for bulk tensors (e.g. control on
+        host gloo, decoded images on RCCL), rebuilt with every epoch."""
         self.grank, self.backend, self.device = global_rank, backend, device
+        self.data_backend = data_backend or backend
+        self.data_group = None
         self.members: List[int] = list(range(world))
         self.epoch = 0
         self.timeout = datetime.timedelta(seconds=timeout_s)
@@ -88,6 +93,9 @@ class ElasticGroup:
             kw["device_id"] = self.device
         dist.init_process_group(self.backend, store=prefix, rank=self.rank, world_size=self.world,
                                 timeout=self.timeout, **kw)
+        self.data_group = None
+        if self.data_backend != self.backend:
+            self.data_group = dist.new_group(list(range(self.world)), backend=self.data_backend)
         log.info("rank %d joined epoch %d (%d members)", self.grank, self.epoch, self.world)
 
     def _teardown(self, abort: bool) -> None:
@@ -96,6 +104,10 @@ class ElasticGroup:
         nothing waits on it, then destroy the group."""
         if not dist.is_initialized():
             return
+        if abort and self.data_group is not None and self.data_backend == "nccl":
+            c10d._abort_process_group(self.data_group)   # RCCL data group: ncclCommAbort
+            self.aborts += 1
+        self.data_group = None
         if abort and self.backend == "nccl":
             c10d._abort_process_group()   # NCCL/RCCL backend abort (no hasattr probing)
             self.aborts += 1
@@ -138,11 +150,20 @@ class ElasticGroup:
         self._run(dist.all_gather, bufs, t)
 
     def all_gather_into(self, out: torch.Tensor, t: torch.Tensor) -> None:
-        """out[r] = rank r's t (out: [world, *t.shape])."""
+        """out = concat of every rank's t along dim 0 (out: [world * t.shape[0], ...]
+        or [world, *t.shape])."""
         if self.backend == "nccl":
             self._run(dist.all_gather_into_tensor, out, t)
         else:
-            self._run(dist.all_gather, list(out.unbind(0)), t)
+            self._run(dist.all_gather, list(out.view(self.world, *t.shape).unbind(0)), t)
+
+    def all_gather_data(self, out: torch.Tensor, t: torch.Tensor) -> None:
+        """all-gather on the data group (bulk tensors): out = concat of every
+        rank's t along dim 0 (all_gather_into_tensor semantics)."""
+        if self.data_backend == "nccl":
+            self._run(dist.all_gather_into_tensor, out, t, group=self.data_group)
+        else:
+            self._run(dist.all_gather, list(out.view(self.world, *t.shape).unbind(0)), t, group=self.data_group)
 
     def barrier(self) -> None:
         t = torch.zeros(1, device=self.device if self.backend == "nccl" else "cpu")

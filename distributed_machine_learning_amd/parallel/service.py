@@ -48,12 +48,14 @@ files of the last completed steps (a dead coordinator may not have written them:
 at-least-once outputs). Batches may run twice; every job completes.
 
 Images: a job names store images (cyclic pick over the sorted ``*.jpeg``
-listing, reference worker.py:176-206) or synthetic arena images. Each rank
-decodes a store image ONCE into its per-model pinned arena (name -> slot, LRU);
-a batch is a list of arena slots, staged with coalesced hipMemcpyAsync. C3
-(per-model batch size) is a replicated log record, clamped to the result
-capacity; a batch larger than the engine's batch runs as several engine passes
-(never truncated).
+listing, reference worker.py:176-206) or synthetic images. Applying a submit
+record, every rank fetches and decodes only ITS SHARE of the job's new images
+and one all-gather over the data group (RCCL over xGMI) replicates the decoded
+tensors into every rank's HBM image store (parallel/image_store.py): each
+image is decoded once per job, not once per rank. A batch is a list of store
+slots gathered on the GPU. C3 (per-model batch size) is a replicated log
+record, clamped to the result capacity; a batch larger than the engine's batch
+runs as several engine passes (never truncated).
 """
 from __future__ import annotations
 
@@ -89,76 +91,6 @@ RESULT_HISTORY = 64           # completed steps whose results every rank keeps (
 
 def synthetic_names(n: int) -> List[str]:
     return [f"{SYNTH}{i}" for i in range(n)]
-
-
-# ----------------------------------------------------------------- arenas ----
-class ImageArena:
-    """Per-model uint8 image arena with a name -> slot index (decode once).
-
-    Slots [0, n_synth) hold synthetic images (``synthetic:<i>`` -> slot
-    i % n_synth); the rest is an LRU cache of decoded store images. ``pinned``
-    arenas live in hipHostMalloc'ed memory (GPU backends stage from them with
-    hipMemcpyAsync); host backends use a numpy array."""
-
-    def __init__(self, capacity: int, hw: Tuple[int, int], pinned: bool = False, n_synth: int = 0, seed: int = 0):
-        if n_synth >= capacity:
-            raise ValueError("arena needs room beyond its synthetic images")
-        self.capacity, self.hw, self.n_synth = capacity, tuple(hw), n_synth
-        if pinned:
-            from .staging import PinnedImageStore
-
-            self.pinned = PinnedImageStore(capacity, self.hw)
-            self.array = self.pinned.array
-        else:
-            self.pinned = None
-            self.array = np.zeros((capacity, *self.hw, 3), np.uint8)
-        if n_synth:
-            rng = np.random.default_rng(seed)
-            for i in range(0, n_synth, 64):
-                j = min(n_synth, i + 64)
-                self.array[i:j] = rng.integers(0, 256, size=(j - i, *self.hw, 3), dtype=np.uint8)
-        self.index: "OrderedDict[str, int]" = OrderedDict()
-        self.free = list(range(capacity - 1, n_synth - 1, -1))
-        self.decoded = 0
-
-    def slots(self, names: Sequence[str], loader: Callable[[List[str]], Dict[str, Optional[np.ndarray]]]
-              ) -> Tuple[List[int], List[str]]:
-        """Arena slots of ``names`` (loading the missing ones through ``loader``);
-        returns (slots, failed names). A failed image gets slot 0 (its row is
-        computed but reported as failed)."""
-        synth = self.n_synth > 0
-        missing = []
-        for n in names:
-            if not (synth and n.startswith(SYNTH)) and n not in self.index and n not in missing:
-                missing.append(n)
-        failed = set()
-        if missing:
-            got = loader(missing)
-            keep = set(names)
-            for n in missing:
-                img = got.get(n)
-                if img is None:
-                    failed.add(n)
-                    continue
-                if not self.free:  # evict the least recently used image not needed now
-                    victim = next((k for k in self.index if k not in keep), None)
-                    if victim is None:
-                        raise RuntimeError("image arena too small for one batch")
-                    self.free.append(self.index.pop(victim))
-                s = self.free.pop()
-                self.array[s] = img
-                self.index[n] = s
-                self.decoded += 1
-        out = []
-        for n in names:
-            if synth and n.startswith(SYNTH):
-                out.append(int(n[len(SYNTH):]) % self.n_synth)
-            elif n in failed:
-                out.append(0)
-            else:
-                self.index.move_to_end(n)
-                out.append(self.index[n])
-        return out, sorted(failed)
 
 
 # --------------------------------------------------------------- backends ----
@@ -255,26 +187,28 @@ class FakeRankBackend(HostRankBackend):
 
 class GpuRankBackend(RankBackend):
     """Native engines for both models resident in this GPU's HBM, fed from
-    per-model pinned arenas (decode-once store images + synthetic images). Two
-    source slots per engine: the H2D copy of step k (copy stream) overlaps the
-    forward of step k-1 (compute stream); results land in one of two output
-    slots. A batch larger than the engine's batch runs as several engine passes
-    into consecutive result rows."""
+    per-model HBM image stores (parallel/image_store.py: store images decoded
+    once per job and replicated to every rank over the data group — RCCL —
+    plus seeded synthetic images). A batch is gathered from the store into the
+    engine's source slot on the compute stream, in order (no PCIe copy per
+    batch, nothing for another queue to starve); results land in one of two
+    output slots. A batch larger than the engine's batch runs as several engine
+    passes into consecutive result rows."""
 
-    def __init__(self, device: torch.device, batch_sizes: Dict[str, int], cap: int = 0, arena_images: int = 1024,
+    def __init__(self, device: torch.device, batch_sizes: Dict[str, int], cap: int = 0, arena_images: int = 8192,
                  n_synth: int = 512, seed: int = 0, models: Sequence[str] = MODELS, splits: int = 2,
                  loader: Optional[Callable] = None, decode_threads: int = 8):
         from concurrent.futures import ThreadPoolExecutor
 
         from ..models import build_model
         from ..models.engine import Engine, SplitEngine
+        from .image_store import HbmImageStore
 
         self.device = device
         self.cap = cap or max(batch_sizes.values())
         self.loader = loader
         self.engines, self.arenas = {}, {}
         self.stream = torch.cuda.Stream(device)
-        self.copy_stream = torch.cuda.Stream(device)
         self.pool = ThreadPoolExecutor(max_workers=decode_threads)
         for m in models:
             g, w = build_model(m, seed=seed, calibrate=True)
@@ -283,11 +217,9 @@ class GpuRankBackend(RankBackend):
                 self.engines[m] = SplitEngine(g, w, batch=b, device=str(device), src_slots=2, splits=splits)
             else:
                 self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=2)
-            self.arenas[m] = ImageArena(max(arena_images, n_synth + 2 * self.cap), g.input_hw, pinned=True,
-                                        n_synth=n_synth, seed=1000 + MODEL_IDS[m])
+            self.arenas[m] = HbmImageStore(max(arena_images, n_synth + 2 * self.cap), g.input_hw, device,
+                                           n_synth=n_synth, seed=1000 + MODEL_IDS[m])
         self.out = [torch.zeros((2, self.cap, 5), dtype=torch.int32, device=device) for _ in range(2)]
-        self.ev_copied = torch.cuda.Event()
-        self.ev_consumed = {(m, k): torch.cuda.Event() for m in models for k in range(2)}
         self.ev_done = [torch.cuda.Event() for _ in range(2)]
 
     def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
@@ -307,29 +239,33 @@ class GpuRankBackend(RankBackend):
                 return n, None
         return dict(self.pool.map(dec, names))
 
+    def on_submit(self, model: str, names: Sequence[str], eg: ElasticGroup) -> int:
+        """(collective, every rank) decode this rank's share of the job's new
+        images and all-gather all shares into every rank's HBM store."""
+        n = self.arenas[model].replicate(names, lambda ns: self._load(model, ns), rank=eg.rank, world=eg.world,
+                                         gather=eg.all_gather_data)
+        torch.cuda.current_stream(self.device).synchronize()  # store writes visible to the compute stream
+        return n
+
     def launch(self, model, names, slot):
         if len(names) > self.cap:
             raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
         eng, arena = self.engines[model], self.arenas[model]
         slots, failed = arena.slots(list(names), lambda ns: self._load(model, ns))
-        cs, s = self.copy_stream, self.stream
+        s = self.stream
         out = self.out[slot]
         B = eng.batch
-        for off in range(0, len(slots), B):  # one engine pass per B images: never truncated
-            chunk = slots[off:off + B]
-            cs.wait_event(self.ev_consumed[(model, slot)])  # WAR: the forward that last read this source slot
-            arena.pinned.h2d_indices(eng.srcs[slot], chunk, cs)
-            self.ev_copied.record(cs)
-            s.wait_event(self.ev_copied)
-            with torch.cuda.stream(s):
+        with torch.cuda.stream(s):
+            for off in range(0, len(slots), B):  # one engine pass per B images: never truncated
+                chunk = slots[off:off + B]
+                arena.gather_into(eng.srcs[slot], chunk)
                 eng.run(s, use_graph=True, slot=slot)
-                self.ev_consumed[(model, slot)].record(s)
                 out[:, off:off + len(chunk)].copy_(eng.results[slot][:, :len(chunk)])
-        if failed:  # undecodable / unfetchable images: class id -1 marks the row failed
-            rows = torch.tensor([i for i, n in enumerate(names) if n in set(failed)], device=self.device)
-            with torch.cuda.stream(s):
-                out[0].index_fill_(0, rows, -1)
-        self.ev_done[slot].record(s)
+            if failed:  # unfetchable / undecodable images: class id -1 marks the row failed
+                bad = set(failed)
+                rows = torch.tensor([i for i, n in enumerate(names) if n in bad], dtype=torch.long)
+                out[0].index_fill_(0, rows.pin_memory().to(self.device, non_blocking=True), -1)
+            self.ev_done[slot].record(s)
         return out, self.ev_done[slot]
 
 
@@ -675,6 +611,8 @@ class CollectiveService:
         hcpu = np.zeros(HDR + world * DESC_FIELDS, np.int64)
         active = self.is_coordinator()
         payload = b""
+        recs: List[dict] = []
+        applied_here: List[dict] = []
         replies: List[Optional[Callable]] = []
         results: List[dict] = []
         if active:
@@ -703,9 +641,14 @@ class CollectiveService:
                     buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
                 eg.broadcast(buf, src=root)
                 if not active:
+                    applied_here = json.loads(bytes(buf.cpu().numpy()).decode())
                     with coord.lock:
-                        for r in json.loads(bytes(buf.cpu().numpy()).decode()):
+                        for r in applied_here:
                             coord.apply(r)
+        applied = recs if active else applied_here
+        for r in applied:  # collective on every rank: decode-once + replicate the job's images
+            if r["op"] == "submit" and hasattr(self.be, "on_submit"):
+                self.be.on_submit(r["model"], r["images"], eg)
         if active and self.control is not None:
             self.control.committed(replies, results)
         elif active:

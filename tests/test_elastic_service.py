@@ -162,22 +162,50 @@ def test_replicated_state_machine_queues():
     assert [b.key for b in rep.jobs.queues["ResNet50"]] == [b.key for b in c.jobs.queues["ResNet50"]]
 
 
-def test_image_arena_decode_once_and_lru():
+def _replica_main(grank, world, rdzv, out):
     import numpy as np
+    import torch
 
-    from distributed_machine_learning_amd.parallel.service import ImageArena
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+    from distributed_machine_learning_amd.parallel.image_store import HbmImageStore
 
-    calls = []
+    eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=30)
+    decoded = []
 
-    def loader(names):
-        calls.append(list(names))
-        return {n: (None if n == "bad" else np.full((4, 4, 3), len(n), np.uint8)) for n in names}
+    def load(names):
+        decoded.extend(names)
+        return {n: (None if n == "bad.jpeg" else np.full((4, 4, 3), int(n.split(".")[0]) % 251, np.uint8))
+                for n in names}
 
-    a = ImageArena(6, (4, 4), n_synth=2)
-    s, failed = a.slots(["synthetic:3", "a", "bb", "a", "bad"], loader)
-    assert s[0] == 1 and s[1] == s[3] and failed == ["bad"] and calls == [["a", "bb", "bad"]]
-    s2, _ = a.slots(["a", "bb"], loader)                    # cached: no second decode
-    assert s2 == s[1:3] and len(calls) == 1
-    a.slots(["c", "dd", "eee"], loader)                     # 4 free slots: evicts the LRU ("a")
-    a.slots(["ffff"], loader)
-    assert "a" not in a.index and a.array[a.index["eee"]][0, 0, 0] == 3
+    st = HbmImageStore(16, (4, 4), torch.device("cpu"), n_synth=2, seed=0)
+    names = [f"{i}.jpeg" for i in range(10)] + ["bad.jpeg", "3.jpeg", "synthetic:5"]
+    n1 = st.replicate(names, load, rank=eg.rank, world=eg.world, gather=eg.all_gather_data)
+    n2 = st.replicate(names, load, rank=eg.rank, world=eg.world, gather=eg.all_gather_data)  # all known
+    slots, failed = st.slots(names)
+    got = st.arena[slots].numpy()[:, 0, 0, 0].tolist()
+    import json
+    json.dump({"decoded": decoded, "n1": n1, "n2": n2, "failed": failed, "vals": got},
+              open(os.path.join(out, f"rep_{grank}.json"), "w"))
+    eg.close()
+
+
+def test_hbm_image_store_decode_once_replicate_gloo(tmp_path):
+    """World 3: each rank decodes only ITS share of a job's new images (i % 3)
+    and one all-gather gives every rank every decoded image (the RCCL path on
+    GPUs; gloo here); a failed image is failed on every rank; known images are
+    never decoded again."""
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_replica_main, args=(r, 3, str(tmp_path / "rdzv"), str(tmp_path))) for r in range(3)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+    assert [p.exitcode for p in ps] == [0, 0, 0]
+    res = [json.loads((tmp_path / f"rep_{r}.json").read_text()) for r in range(3)]
+    new = [f"{i}.jpeg" for i in range(10)] + ["bad.jpeg"]
+    for r in range(3):
+        assert res[r]["decoded"] == new[r::3]                 # its share only, once
+        assert res[r]["n1"] == 10 and res[r]["n2"] == 0
+        assert res[r]["failed"] == ["bad.jpeg"]
+        assert res[r]["vals"][:10] == list(range(10)) and res[r]["vals"][11] == 3
+    assert res[0]["vals"] == res[1]["vals"] == res[2]["vals"]

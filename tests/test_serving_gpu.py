@@ -138,6 +138,7 @@ def test_collective_service_rccl_world1_outputs(tmp_path):
     try:
         bs = {"ResNet50": 16, "InceptionV3": 8}
         be = GpuRankBackend(dev, bs, cap=32, arena_images=256, n_synth=64)
+        assert be.arenas["ResNet50"].arena.device.type == "cuda"  # the image store lives in HBM
         coord = ReplicatedCoordinator(bs, cap=32, host_tag="gpu")
         writer = OutputWriter(str(tmp_path / "out"), host_tag="gpu")
         svc = CollectiveService(eg, be, coord, writer=writer, on_device=True)
@@ -152,7 +153,7 @@ def test_collective_service_rccl_world1_outputs(tmp_path):
         cls = {wnid: i for i, (wnid, _) in enumerate(load_class_index())}
         for m, job, n_img, half in (("ResNet50", 31, 40, 8), ("InceptionV3", 32, 20, 4), ("ResNet50", 33, 32, 8)):
             g, w = build_model(m, seed=0)
-            arena = be.arenas[m].array
+            arena = be.arenas[m].arena.cpu().numpy()
             doc = {}
             for f in files:
                 if f.startswith(f"output_{job}_"):
@@ -173,6 +174,64 @@ def test_collective_service_rccl_world1_outputs(tmp_path):
                     ent = doc[f"synthetic:{names[b0 + i]}"][0]
                     assert [cls[e[0]] for e in ent] == ref[0, i].tolist()
                     assert np.allclose([e[2] for e in ent], ref[1, i].view(torch.float32).numpy(), rtol=0, atol=0)
+    finally:
+        eg.close()
+
+
+def test_store_images_replicated_to_hbm_and_served(tmp_path):
+    """Store JPEGs -> decoded once into the HBM image store through the data
+    group (RCCL) at submit -> served from HBM; control collectives on host gloo
+    (the service default). Output rows == Engine.infer of the same decoded
+    images; an undecodable file is reported as failed."""
+    import io
+
+    from PIL import Image
+
+    from distributed_machine_learning_amd.models import build_model
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+    from distributed_machine_learning_amd.parallel.service import (CollectiveService, GpuRankBackend, OutputWriter,
+                                                                   ReplicatedCoordinator)
+    from distributed_machine_learning_amd.serving.inference import load_image
+    from distributed_machine_learning_amd.serving.output import FAILED_DOWNLOAD
+    from distributed_machine_learning_amd.utils.labels import load_class_index
+
+    rng = np.random.default_rng(0)
+    blobs = {}
+    for i in range(12):
+        buf = io.BytesIO()
+        Image.fromarray(rng.integers(0, 255, (300, 200 + 8 * i, 3), dtype=np.uint8)).save(buf, format="JPEG")
+        blobs[f"{i}.jpeg"] = buf.getvalue()
+    blobs["broken.jpeg"] = b"not a jpeg"
+    dev = torch.device("cuda", 0)
+    eg = ElasticGroup(0, 1, store_path=str(tmp_path / "rdzv"), backend="gloo", data_backend="nccl", timeout_s=120)
+    try:
+        bs = {"ResNet50": 8, "InceptionV3": 8}
+        be = GpuRankBackend(dev, bs, cap=8, arena_images=64, n_synth=8, loader=lambda ns: {n: blobs.get(n) for n in ns})
+        coord = ReplicatedCoordinator(bs, cap=8, host_tag="gpu")
+        writer = OutputWriter(str(tmp_path / "out"), host_tag="gpu")
+        svc = CollectiveService(eg, be, coord, writer=writer, on_device=False)
+        names = sorted(blobs)
+        svc.submit_local("ResNet50", images=names)
+        svc.serve(max_steps=100, stop_when_idle=True)
+        st = be.arenas["ResNet50"]
+        assert st.replicated == 12 and st.failed == {"broken.jpeg"}
+        doc = {}
+        for f in os.listdir(tmp_path / "out"):
+            doc.update(json.load(open(tmp_path / "out" / f)))
+        assert doc["broken.jpeg"] == FAILED_DOWNLOAD
+        g, w = build_model("ResNet50", seed=0)
+        good = [n for n in names if n != "broken.jpeg"]
+        imgs = torch.from_numpy(np.stack([load_image(blobs[n], (224, 224)) for n in good]))
+        cls = {wnid: i for i, (wnid, _) in enumerate(load_class_index())}
+        for b0 in range(0, len(names), 8):  # batches of 8 in submit order, failed rows computed on slot 0
+            batch = names[b0:b0 + 8]
+            pad = torch.zeros((8, 224, 224, 3), dtype=torch.uint8)
+            for i, n in enumerate(batch):
+                pad[i] = imgs[good.index(n)] if n in good else torch.from_numpy(st.arena[0].cpu().numpy())
+            ref = _split_ref(g, w, pad, 4)
+            for i, n in enumerate(batch):
+                if n in good:
+                    assert [cls[e[0]] for e in doc[n][0]] == ref[0, i].tolist(), n
     finally:
         eg.close()
 

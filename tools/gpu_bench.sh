@@ -5,7 +5,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_serving_gpu.py -k pipeline > gpurun_out/pytest_pipe.log 2>&1 || { tail -30 gpurun_out/pytest_pipe.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_serving_gpu.py > gpurun_out/pytest_pipe.log 2>&1 || { tail -30 gpurun_out/pytest_pipe.log; exit 1; }
 tail -1 gpurun_out/pytest_pipe.log
 timeout -k 10 600 python bench.py --steps 30 --warmup 5 ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 && tail -1 gpurun_out/bench.log || { tail -30 gpurun_out/bench.log; exit 1; }
 if [ -n "$PROFILE" ]; then

@@ -57,9 +57,9 @@ def main():
     torch.cuda.set_device(dev)
     bs = {"ResNet50": a.resnet_batch, "InceptionV3": a.inception_batch}
     cap = max(bs.values())
-    backend = GpuRankBackend(dev, bs, cap=cap, arena_images=2 * cap + 64, n_synth=2 * cap)
+    backend = GpuRankBackend(dev, bs, cap=cap, arena_images=4 * cap, n_synth=2 * cap)
     eg = ElasticGroup(grank, world, store_path=rdzv, backend=a.comm, device=dev if a.comm == "nccl" else None,
-                      timeout_s=120)
+                      timeout_s=120, data_backend="nccl")  # bulk (image replication) always over RCCL
     fd = RankFailureDetector(grank, world, swim_port, on_dead=eg.dead.add).start()
     kills = [tuple(int(x) for x in k.split(":")) for k in a.kill]
     kr, ks = (-1, -1)
