@@ -58,15 +58,6 @@ typedef struct {
   // the taps of one channel chunk, so a 3x3's shifted pixel rows are re-read
   // while still in the CU's L1 instead of once per tap from L2.
   int kchunk;
-  // In-kernel split-K reduction (``fixup`` = 1, ksplit > 1): the ksplit
-  // workgroups of one output tile each store their fp32 partial accumulators to
-  // ``ws`` and take a ticket (``tickets[tile]``, agent-scope atomic, zeroed once
-  // at allocation); the LAST arriver adds the other slices' partials to its own
-  // and runs the normal epilogue (bias, residual, ReLU, bf16 store), then resets
-  // the ticket for the next launch. ws: ntiles * ksplit * BM * BN floats.
-  int fixup;
-  float* ws;
-  int* tickets;
 } DmlConvArgs;
 
 typedef struct {

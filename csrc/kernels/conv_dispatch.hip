@@ -31,12 +31,7 @@ extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
     dml_set_error("dml_conv: subsampled residual needs res and rW >= Wo*rsub, rHW >= rW*Ho*rsub");
     return -1;
   }
-  if (a->ksplit > 1 && a->fixup) {
-    if (!a->ws || !a->tickets || a->ksplit > 16) {
-      dml_set_error("dml_conv: in-kernel split-K needs ws, zeroed tickets and ksplit <= 16");
-      return -1;
-    }
-  } else if (a->ksplit > 1 && (!a->out_f32 || a->res || a->nseg || a->relu || a->split_ld < 1)) {
+  if (a->ksplit > 1 && (!a->out_f32 || a->res || a->nseg || a->relu || a->split_ld < 1)) {
     dml_set_error("dml_conv: split-K needs fp32 output, no residual/segments/ReLU, split_ld");
     return -1;
   }

@@ -72,7 +72,7 @@ struct Cfg {
   static_assert((STAGES - 2) * L < 64, "vmcnt overflow");
 };
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK = 64, bool FIX = false>
+template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK = 64>
 __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
   using RW = typename T::R;
@@ -217,10 +217,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
     if (s < nk) issue(s, s);
 
   // epilogue operands (bias, residual) prefetched behind the first DMA tiles
-  // (with the in-kernel split-K fixup the one workgroup that finishes the tile
-  // adds the bias, whichever slice it is)
   convk::Epilogue<BM, BN, T::NT, RES, T::EP> epi;
-  epi.prefetch(a, m0, c0, M, tid, FIX ? 0 : split);
+  epi.prefetch(a, m0, c0, M, tid, split);
 
   for (int kt = 0; kt < nk; ++kt) {
     // retire tile kt (leave the younger STAGES-2 tiles in flight), then barrier
@@ -257,45 +255,6 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
     __builtin_amdgcn_s_setprio(0);
   }
 
-  if constexpr (FIX) {  // a separate instantiation: the plain kernels keep their register budget
-    // In-kernel split-K reduction, last arriver finishes the tile. Hand-off per
-    // MI355X_MICROARCH.md "Valid forms": every storing wave drains its stores,
-    // workgroup barrier, one lane releases (agent) and takes a ticket; the last
-    // arriver acquires (agent) before reading the others' partials. No wait on
-    // another workgroup ever happens: a slice that is not last just leaves.
-    constexpr int NF = T::FI * T::FJ;
-    float* wsl = a.ws + ((long)Lb * ksplit + split) * NF * 4 * T::NT;  // this slice's partial tile
-#pragma unroll
-    for (int i = 0; i < T::FI; ++i)
-#pragma unroll
-      for (int j = 0; j < T::FJ; ++j)  // fragment-major: a wave writes 1 KiB contiguous per fragment
-        *(f32x4*)(wsl + ((i * T::FJ + j) * T::NT + tid) * 4) = acc[i][j];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    __shared__ int ticket;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      ticket = __hip_atomic_fetch_add(a.tickets + Lb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (ticket != ksplit - 1) return;  // workgroup-uniform: another slice finishes this tile
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.tickets + Lb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-    }
-    __syncthreads();
-    for (int sl = 0; sl < ksplit; ++sl) {
-      if (sl == split) continue;
-      const float* o = a.ws + ((long)Lb * ksplit + sl) * NF * 4 * T::NT;
-#pragma unroll
-      for (int i = 0; i < T::FI; ++i)
-#pragma unroll
-        for (int j = 0; j < T::FJ; ++j) acc[i][j] += *(const f32x4*)(o + ((i * T::FJ + j) * T::NT + tid) * 4);
-    }
-  }
-
   // all DMA retired (vmcnt(0) on the last tile); epilogue through LDS
   epi.template store<T::FI, T::FJ, T::WTP, T::WTC>(a, smem, acc, wp, wc, lane, tid);
 }
@@ -305,14 +264,7 @@ static int launch(const DmlConvArgs* a, hipStream_t s) {
   using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
   const long M = (long)a->N * a->Ho * a->Wo;
   const long tiles = ((M + BM - 1) / BM) * ((a->Cout + BN - 1) / BN) * (a->ksplit > 1 ? a->ksplit : 1);
-  if (a->fixup && a->ksplit > 1) {  // in-kernel split-K reduction (residual-free layers)
-    if (a->res) {
-      dml_set_error("dml_conv: in-kernel split-K is instantiated for residual-free layers only");
-      return -1;
-    }
-    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK, true>), dim3((unsigned)tiles),
-                       dim3(T::NT), T::LDS, s, *a);
-  } else if (a->res)
+  if (a->res)
     hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK>), dim3((unsigned)tiles), dim3(T::NT), T::LDS,
                        s, *a);
   else
@@ -328,8 +280,6 @@ static int set_attr() {
   return (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS) |
          (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS) |
-         (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 

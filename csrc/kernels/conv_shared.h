@@ -86,7 +86,7 @@ struct Epilogue {
     cg_t = tid % CG;
     ch_t = c0 + cg_t * 8;
     ch_ok = ch_t < a.Cout;
-    yoff = a.fixup ? 0 : (long)split * a.split_ld;
+    yoff = (long)split * a.split_ld;
     bias0 = make_float4(0.f, 0.f, 0.f, 0.f);
     bias1 = bias0;
     if (ch_ok && split == 0) {

@@ -31,7 +31,6 @@ class ConvArgs(C.Structure):
         ("ksplit", C.c_int), ("split_ld", C.c_int),
         ("rsub", C.c_int), ("rW", C.c_int), ("rHW", C.c_int),
         ("kchunk", C.c_int),
-        ("fixup", C.c_int), ("ws", C.c_void_p), ("tickets", C.c_void_p),
     ]
 
 

@@ -373,33 +373,9 @@ class Engine:
             table = tuning.autotune(convs)
             for n, a in zip(cnodes, convs):
                 self.tuned[n.name] = table.get(tuning.shape_key(a), -1)
-        self._alloc_fixup()
         self.plans = [self._build_one_plan(self.srcs[i], self.results[i]) for i in range(self.src_slots)]
         self.plan = self.plans[0]
         self.graph_captured = [False] * self.src_slots
-
-    def _alloc_fixup(self) -> None:
-        """One workspace + ticket array per engine for the convs whose tuned
-        choice is the in-kernel split-K variant (ops of one engine run in
-        order on one stream, so they can share it; every ticket is back at 0
-        after each launch)."""
-        from ..ops import tuning
-
-        ws_n = tk_n = 0
-        self.fix_split: Dict[str, Tuple[int, int]] = {}
-        for n in self.g.nodes:
-            if not isinstance(n, (Conv, Dense, FusedConv)):
-                continue
-            v = self.cfg_overrides.get(n.name, self.tuned.get(n.name, -1))
-            cfg, ks = tuning.decode(v)
-            if ks > 1:
-                a = self._conv_args(n)
-                bm, bn = tuning.CFG_TILES[cfg]
-                nt = tuning.n_tiles(a, cfg)
-                ws_n, tk_n = max(ws_n, nt * ks * bm * bn), max(tk_n, nt)
-                self.fix_split[n.name] = (cfg, ks)
-        self.fix_ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=self.device)
-        self.fix_tickets = torch.zeros(max(tk_n, 1), dtype=torch.int32, device=self.device)
 
     def _build_one_plan(self, src: torch.Tensor, result: torch.Tensor):
         g, B, L = self.g, self.batch, self.lib
@@ -473,12 +449,8 @@ class Engine:
             if isinstance(n, (Conv, Dense, FusedConv)):
                 cfg = self.cfg_overrides.get(n.name, self.tuned.get(n.name, -1))
                 a = self._conv_args(n)
-                if n.name in self.fix_split:  # in-kernel split-K (last arriver finishes the tile)
-                    cfg, ks = self.fix_split[n.name]
-                    a.ksplit, a.fixup = ks, 1
-                    a.ws, a.tickets = self.fix_ws.data_ptr(), self.fix_tickets.data_ptr()
                 used = N.check(L.dml_plan_add_conv(plan, C.byref(a), cfg), f"plan conv {n.name}")
-                self.op_cfg[n.name] = used if n.name not in self.fix_split else used + 100 * a.ksplit
+                self.op_cfg[n.name] = used
                 self._keep.append(a)
             elif isinstance(n, Pool):
                 h, w, c = g.shape(n.inp)

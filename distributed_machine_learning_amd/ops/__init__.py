@@ -62,15 +62,11 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
                 stride=(1, 1), pad=(0, 0), relu: bool = False, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, out_coff: int = 0, in_coff: int = 0, cin: Optional[int] = None,
                 out_f32: bool = False, cfg: int = -1, K: Optional[int] = None, dilation=(1, 1),
-                out_hw: Optional[Tuple[int, int]] = None, ksplit: int = 1, kchunk: int = 0,
-                fixup: bool = False) -> torch.Tensor:
+                out_hw: Optional[Tuple[int, int]] = None, ksplit: int = 1, kchunk: int = 0) -> torch.Tensor:
     """x: NHWC bf16 [N,H,W,Cbuf] (Cbuf % 8 == 0). Returns/updates NHWC output.
     ksplit > 1 (fp32 output, v2 cfg): returns the [ksplit, N, Ho, Wo, C] split-K
     partial sums (slice 0 carries the bias); their sum is the convolution.
-    kchunk > 0: w_packed is in chunk-major K order (pack_weight_chunk_major).
-    fixup (with ksplit > 1): in-kernel split-K — the ksplit workgroups of a
-    tile reduce through a workspace and the last one runs the normal epilogue
-    (any output dtype, ReLU; residual-free)."""
+    kchunk > 0: w_packed is in chunk-major K order (pack_weight_chunk_major)."""
     n, h, w_, cbuf = x.shape
     cin = cin if cin is not None else cbuf - in_coff
     ho = (h + 2 * pad[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
@@ -78,7 +74,7 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
     if out_hw is not None:
         ho, wo = out_hw
     parts = None
-    if ksplit > 1 and not fixup:
+    if ksplit > 1:
         assert out_f32 and out is None, "split-K writes fp32 partial slices into its own buffer"
         parts = torch.empty((ksplit, n, ho, wo, _r(cout, 8)), device=x.device, dtype=torch.float32)
         out = parts[0]
@@ -99,14 +95,6 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
     if parts is not None:
         a.ksplit, a.split_ld = ksplit, out.numel()
     a.kchunk = kchunk
-    keep = None
-    if fixup and ksplit > 1:
-        from . import tuning
-
-        if cfg < 0:
-            cfg = N.lib().dml_conv_pick_cfg(C.byref(a))
-        keep = tuning.fixup_buffers(a, cfg, ksplit, device=x.device)
-        a.ksplit, a.fixup, a.ws, a.tickets = ksplit, 1, keep[0].data_ptr(), keep[1].data_ptr()
     if residual is not None and residual.shape[1] != ho:  # shortcut read at stride rs (full-res grid)
         rs = residual.shape[1] // ho
         assert residual.shape[1] == ho * rs and residual.shape[2] == wo * rs and residual.is_contiguous()
@@ -118,7 +106,7 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
     if parts is not None:
         parts._keep = bias_p
         return parts
-    out._keep = (bias_p, keep)  # keep alive until the kernel ran (caller syncs)
+    out._keep = bias_p  # keep alive until the kernel ran (caller syncs)
     return out
 
 

@@ -29,8 +29,7 @@ _lock = threading.Lock()
 # The committed table was tuned with V2_CFGS plus the stride-1 halo configs
 # (40..47, removed in r2): a halo config never won a shape, so every winner is
 # a V2 config and the table stays valid — the tag keeps the value it had then.
-CAND_TAG = "c3ef"  # unchanged by the split-K candidates: shapes they apply to are re-timed via KS_TAG
-KS_TAG = "ks1"
+CAND_TAG = "c3ef"
 
 
 def shape_key(a: N.ConvArgs) -> str:
@@ -39,7 +38,6 @@ def shape_key(a: N.ConvArgs) -> str:
             f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}_d{max(a.dh, 1)}x{max(a.dw, 1)}"
             + (f"_ks{a.ksplit}" if a.ksplit > 1 else "")
             + (f"_rs{a.rsub}" if a.rsub > 1 else "")
-            + ("_" + KS_TAG if (not a.res and a.ksplit <= 1 and not a.nseg) else "")
             + "_" + CAND_TAG)
 
 
@@ -63,49 +61,6 @@ def save_cache(table: Dict[str, int], path: str = CACHE_PATH) -> None:
 
 
 NO_RES_CFGS = (34,)  # the residual-epilogue instantiation spills (256x256 tile)
-
-# (BM pixels, BN channels) of every tile config (conv_igemm_v2.hip dml_conv_v2)
-CFG_TILES = {10: (256, 128), 11: (128, 128), 12: (256, 64), 13: (128, 256), 14: (64, 128), 15: (128, 64),
-             16: (256, 128), 17: (128, 128), 18: (256, 32), 19: (128, 128), 20: (128, 128), 21: (128, 256),
-             22: (64, 256), 23: (64, 128), 24: (128, 64), 25: (128, 128), 26: (64, 128), 27: (128, 64),
-             28: (128, 128), 29: (128, 128), 30: (256, 128), 31: (128, 256), 32: (64, 128), 33: (64, 128),
-             34: (256, 256), 36: (128, 32), 37: (256, 32)}
-BK_OF = {c: (32 if (23 <= c <= 31 or c in (33, 34, 36)) else 64) for c in CFG_TILES}
-SPLITS = (2, 3, 4)   # in-kernel split-K candidates (residual-free layers with few output tiles)
-
-
-def encode(cfg: int, ksplit: int = 1) -> int:
-    """Cache value: cfg, or cfg + 100 * ksplit for the in-kernel split-K variant."""
-    return cfg if ksplit <= 1 else cfg + 100 * ksplit
-
-
-def decode(v: int) -> Tuple[int, int]:
-    return (v % 100, max(1, v // 100)) if v >= 0 else (v, 1)
-
-
-def n_tiles(a: N.ConvArgs, cfg: int) -> int:
-    bm, bn = CFG_TILES[cfg]
-    return -(-a.N * a.Ho * a.Wo // bm) * -(-a.Cout // bn)
-
-
-def split_candidates(a: N.ConvArgs, cfg: int) -> List[int]:
-    """ksplit values worth timing: residual-free, no other split in use, fewer
-    tiles than two rounds of 256 CUs, at least 4 K tiles per slice."""
-    if a.res or a.ksplit > 1 or a.nseg or cfg not in CFG_TILES:
-        return []
-    nt = n_tiles(a, cfg)
-    ktiles = a.Kpad // BK_OF[cfg]
-    return [k for k in SPLITS if nt < 512 and nt * k <= 2048 and ktiles >= 4 * k]
-
-
-def fixup_buffers(a: N.ConvArgs, cfg: int, ksplit: int, device="cuda"):
-    """(workspace, tickets) tensors for the in-kernel split-K reduction."""
-    import torch
-
-    bm, bn = CFG_TILES[cfg]
-    nt = n_tiles(a, cfg)
-    return (torch.empty(nt * ksplit * bm * bn, dtype=torch.float32, device=device),
-            torch.zeros(nt, dtype=torch.int32, device=device))
 
 
 def valid_cfgs(a: N.ConvArgs) -> List[int]:
@@ -146,15 +101,6 @@ def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None,
             except N.NativeError:
                 continue
             best = min(best, (t, cfg))
-            for ks in split_candidates(a, cfg):
-                ws, tk = fixup_buffers(a, cfg, ks)
-                b = N.ConvArgs.from_buffer_copy(a)
-                b.ksplit, b.fixup, b.ws, b.tickets = ks, 1, ws.data_ptr(), tk.data_ptr()
-                try:
-                    t = time_cfg(b, cfg)
-                except N.NativeError:
-                    continue
-                best = min(best, (t, encode(cfg, ks)))
         new[k] = best[1]
     if new and persist:
         try:

@@ -340,47 +340,3 @@ def test_conv_non_tile_config_refused():
     for cfg in (0, 4, 40):
         with pytest.raises(Exception):
             ops.conv2d_nhwc(x, wp.cuda(), torch.zeros(64), 64, 1, 1, cfg=cfg)
-
-
-SPLITK_CASES = [
-    # n, h, w, cin, cout, kh, kw, stride, pad, relu
-    (8, 14, 14, 1024, 256, 1, 1, 1, 0, True),    # ResNet stage-4 reduce (K 1024)
-    (4, 7, 7, 2048, 512, 1, 1, 1, 0, True),      # stage-5 reduce (K 2048)
-    (4, 7, 7, 512, 512, 3, 3, 1, 1, True),       # stage-5 3x3 (K 4608)
-    (2, 8, 8, 448, 384, 3, 3, 1, 1, False),
-    (2, 17, 17, 160, 192, 1, 7, 1, 0, True),     # ragged K tail (K 1120)
-]
-
-
-@pytest.mark.parametrize("case", SPLITK_CASES)
-@pytest.mark.parametrize("cfg,ksplit", [(11, 2), (14, 2), (14, 3), (15, 4), (28, 2), (30, 3)])
-def test_conv_split_k_in_kernel_fixup(case, cfg, ksplit):
-    """In-kernel split-K (workspace + tickets, last arriver runs the epilogue)
-    vs fp32 F.conv2d, launched twice on the same buffers: the tickets are back
-    at zero after each launch (graph replays reuse them)."""
-    n, h, w, cin, cout, kh, kw, s, pad, relu = case
-    ph, pw = _pads(kh, kw, pad)
-    torch.manual_seed(3)
-    x = _bf(torch.randn(n, cin, h, w))
-    wt = _bf(torch.randn(cout, cin, kh, kw) * (2.0 / (cin * kh * kw)) ** 0.5)
-    b = torch.randn(cout) * 0.1
-    ref = F.conv2d(x, wt, b, stride=s, padding=(ph, pw))
-    if relu:
-        ref = F.relu(ref)
-    wp, K, _ = ops.pack_weight(wt)
-    xd = x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
-    for _ in range(2):
-        y = ops.conv2d_nhwc(xd, wp.cuda(), b.cuda(), cout, kh, kw, (s, s), (ph, pw), relu=relu, cfg=cfg,
-                            ksplit=ksplit, fixup=True)
-        torch.cuda.synchronize()
-        assert int(y._keep[1][1].abs().sum()) == 0  # every ticket reset by its last arriver
-        got = y[..., :cout].float().cpu().permute(0, 3, 1, 2)
-        assert _rel(got, ref) < 1.5e-2, _rel(got, ref)
-
-
-def test_conv_split_k_fixup_refuses_residual():
-    x = torch.zeros(1, 4, 4, 64, device="cuda", dtype=torch.bfloat16)
-    wp, _, _ = ops.pack_weight(torch.zeros(64, 64, 1, 1))
-    rd = torch.zeros(1, 4, 4, 64, device="cuda", dtype=torch.bfloat16)
-    with pytest.raises(Exception):
-        ops.conv2d_nhwc(x, wp.cuda(), torch.zeros(64), 64, 1, 1, residual=rd, cfg=11, ksplit=2, fixup=True)
