@@ -60,6 +60,16 @@ typedef struct {
   int kchunk;
 } DmlConvArgs;
 
+// Grouped launch of up to DML_CONV_GROUP_MAX independent convs in one grid
+// (dml_conv_group): residual-free, all on the same tile config. off[] is filled
+// by the launcher (prefix tile offsets, off[n] = grid size).
+#define DML_CONV_GROUP_MAX 4
+typedef struct {
+  int n;
+  int off[DML_CONV_GROUP_MAX + 1];
+  DmlConvArgs a[DML_CONV_GROUP_MAX];
+} DmlConvGroupArgs;
+
 typedef struct {
   const void* x;  // bf16 NHWC
   void* y;        // bf16 NHWC
@@ -151,6 +161,10 @@ int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2_init(void);
 int dml_conv_pick_cfg(const DmlConvArgs* a);
+int dml_conv_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s);
+int dml_conv_v2_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s);
+int dml_conv_v2_group_supported(int cfg);
+int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);
 int dml_softmax_top5(const float* logits, int B, int classes, int ld, float* probs_out,
@@ -162,10 +176,11 @@ int dml_softmax_top5_split(float* logits, int B, int classes, int ld, int nsplit
                            float* probs_out, int* top_idx, float* top_p, hipStream_t s);
 int dml_preprocess(const DmlPreprocArgs* a, hipStream_t s);
 
-// ---- plan executor (C++ runtime, csrc/runtime/plan.cpp) ----
+// ---- plan executor (C++ runtime, csrc/runtime/runtime.hip) ----
 void* dml_plan_create(void);
 void dml_plan_destroy(void* plan);
 int dml_plan_add_conv(void* plan, const DmlConvArgs* a, int cfg);
+int dml_plan_add_conv_group(void* plan, const DmlConvGroupArgs* g, int cfg);
 int dml_plan_add_pool(void* plan, const DmlPoolArgs* a);
 int dml_plan_add_gap(void* plan, const void* x, void* y, int N, int HW, int C, int ldx);
 int dml_plan_add_softmax_top5(void* plan, const float* logits, int B, int classes, int ld,

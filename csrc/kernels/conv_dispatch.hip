@@ -14,7 +14,7 @@
 #include "common.h"
 #include "dml.h"
 
-extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
+static int validate(const DmlConvArgs* a, int cfg) {
   if (cfg < 10 || cfg >= 40) {
     dml_set_error("dml_conv: cfg must be a v2 tile config (10..39)");
     return -1;
@@ -39,7 +39,36 @@ extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
     dml_set_error("dml_conv: chunk-major K order needs kchunk%64==0, Cin%kchunk==0, no dilation");
     return -1;
   }
+  return 0;
+}
+
+extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
+  if (validate(a, cfg) != 0) return -1;
   return dml_conv_v2(a, cfg, s);
+}
+
+extern "C" int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg) {
+  if (!g || g->n < 1 || g->n > DML_CONV_GROUP_MAX) {
+    dml_set_error("dml_conv_group: 1..4 members");
+    return -1;
+  }
+  if (!dml_conv_v2_group_supported(cfg)) {
+    dml_set_error("dml_conv_group: cfg has no grouped instantiation (11, 14, 15, 23, 32)");
+    return -1;
+  }
+  for (int i = 0; i < g->n; ++i) {
+    if (validate(&g->a[i], cfg) != 0) return -1;
+    if (g->a[i].res || g->a[i].ksplit > 1) {
+      dml_set_error("dml_conv_group: members must be residual-free and without split-K");
+      return -1;
+    }
+  }
+  return 0;
+}
+
+extern "C" int dml_conv_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s) {
+  if (dml_conv_group_validate(g, cfg) != 0) return -1;
+  return dml_conv_v2_group(g, cfg, s);
 }
 
 // Measured default tile per shape class (tools/conv_bench.py); the engine

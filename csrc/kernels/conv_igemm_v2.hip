@@ -72,8 +72,11 @@ struct Cfg {
   static_assert((STAGES - 2) * L < 64, "vmcnt overflow");
 };
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK = 64>
-__global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
+// One workgroup's tile: logical block Lb (already XCD-remapped) of a grid of
+// nblk blocks that runs conv `a` (the plain kernel's whole grid, or one member
+// of a grouped launch).
+template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK>
+__device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int nblk) {
   using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
   using RW = typename T::R;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -83,9 +86,9 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   // split-K: the grid is ksplit slices of the tile grid; slice `split` runs K
   // tiles [kbeg, kbeg + nk) and writes its own fp32 partial output
   const int ksplit = a.ksplit > 1 ? a.ksplit : 1;
-  int Lb = xcd_remap(blockIdx.x, gridDim.x), split = 0;
+  int split = 0;
   if (ksplit > 1) {  // wave-uniform; the common path skips the division
-    const int ntiles = gridDim.x / ksplit;
+    const int ntiles = nblk / ksplit;
     split = Lb / ntiles;
     Lb -= split * ntiles;
   }
@@ -259,6 +262,26 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
   epi.template store<T::FI, T::FJ, T::WTP, T::WTC>(a, smem, acc, wp, wc, lane, tid);
 }
 
+template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK = 64>
+__global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
+  conv_v2_tile<BM, BN, WM, WN, STAGES, RES, BK>(a, xcd_remap(blockIdx.x, gridDim.x), gridDim.x);
+}
+
+// Grouped launch: up to DML_CONV_GROUP_MAX independent convs (InceptionV3's
+// parallel branch convs: different kh x kw, inputs and outputs) share ONE grid;
+// block -> member by the prefix tile offsets, XCD remap over the whole grid.
+// Fills the 256 CUs where each member alone leaves them half idle.
+template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
+__global__ __launch_bounds__(WM* WN * 64) void conv_v2_group_kernel(DmlConvGroupArgs g) {
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  int i = 0;
+#pragma unroll
+  for (int q = 1; q < DML_CONV_GROUP_MAX; ++q)
+    if (q < g.n && L >= g.off[q]) i = q;
+  i = __builtin_amdgcn_readfirstlane(i);
+  conv_v2_tile<BM, BN, WM, WN, STAGES, false, BK>(g.a[i], L - g.off[i], g.off[i + 1] - g.off[i]);
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
 static int launch(const DmlConvArgs* a, hipStream_t s) {
   using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
@@ -272,6 +295,28 @@ static int launch(const DmlConvArgs* a, hipStream_t s) {
                        T::LDS, s, *a);
   DML_CHECK_LAUNCH();
   return 0;
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
+static int launch_group(const DmlConvGroupArgs* g, hipStream_t s) {
+  using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
+  DmlConvGroupArgs h = *g;
+  h.off[0] = 0;
+  for (int i = 0; i < h.n; ++i) {
+    const long M = (long)h.a[i].N * h.a[i].Ho * h.a[i].Wo;
+    h.off[i + 1] = h.off[i] + (int)(((M + BM - 1) / BM) * ((h.a[i].Cout + BN - 1) / BN));
+  }
+  hipLaunchKernelGGL((conv_v2_group_kernel<BM, BN, WM, WN, STAGES, BK>), dim3((unsigned)h.off[h.n]), dim3(T::NT),
+                     T::LDS, s, h);
+  DML_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
+static int set_attr_group() {
+  using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
+  return (int)hipFuncSetAttribute((const void*)conv_v2_group_kernel<BM, BN, WM, WN, STAGES, BK>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
 template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
@@ -318,6 +363,11 @@ extern "C" int dml_conv_v2_init(void) {
   rc |= set_attr<256, 256, 2, 4, 3, 32>();
   rc |= set_attr<128, 32, 2, 1, 3, 32>();
   rc |= set_attr<256, 32, 4, 1, 3, 64>();
+  rc |= set_attr_group<128, 128, 2, 2, 2>();
+  rc |= set_attr_group<64, 128, 1, 4, 2>();
+  rc |= set_attr_group<128, 64, 2, 2, 2>();
+  rc |= set_attr_group<64, 128, 1, 4, 3>();
+  rc |= set_attr_group<64, 128, 1, 4, 2, 32>();
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   if (!rc && dml_expand_reduce_init() != 0) return -1;  // fused block-boundary kernels (bottleneck_fused.hip)
   return rc ? -1 : 0;
@@ -361,4 +411,22 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
     case 37: return launch<256, 32, 4, 1, 3, 64>(a, s);   // 4 waves, 3-stage
     default: dml_set_error("dml_conv_v2: bad cfg"); return -1;
   }
+}
+
+// Grouped launch of independent convs (cfg: the tile config every member uses;
+// instantiated for the configs InceptionV3's branch convs tune to).
+extern "C" int dml_conv_v2_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s) {
+  using namespace dml::v2;
+  switch (cfg) {
+    case 11: return launch_group<128, 128, 2, 2, 2>(g, s);
+    case 14: return launch_group<64, 128, 1, 4, 2>(g, s);
+    case 15: return launch_group<128, 64, 2, 2, 2>(g, s);
+    case 32: return launch_group<64, 128, 1, 4, 3>(g, s);
+    case 23: return launch_group<64, 128, 1, 4, 2, 32>(g, s);
+    default: dml_set_error("dml_conv_group: cfg has no grouped instantiation (11, 14, 15, 23, 32)"); return -1;
+  }
+}
+
+extern "C" int dml_conv_v2_group_supported(int cfg) {
+  return cfg == 11 || cfg == 14 || cfg == 15 || cfg == 23 || cfg == 32;
 }

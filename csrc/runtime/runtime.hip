@@ -42,7 +42,8 @@ extern "C" int dml_device_info(int* cus, int* arch_major, int* arch_minor) {
 
 // ----------------------------------------------------------------- plan ----
 namespace {
-enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM, OP_INC_STEM, OP_CONV_POOL, OP_EXP_RED };
+enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM, OP_INC_STEM, OP_CONV_POOL, OP_EXP_RED,
+              OP_CONV_GROUP };
 struct GapArgs { const void* x; void* y; int N, HW, C, ldx; };
 struct SmArgs { float* logits; int B, classes, ld, nsplit, split_ld; float* probs; int* idx; float* p; };
 struct Op {
@@ -57,6 +58,7 @@ struct Op {
   DmlIncStemArgs istem;
   DmlConvPoolArgs cpool;
   DmlExpandReduceArgs er;
+  DmlConvGroupArgs grp;
 };
 struct Plan {
   std::vector<Op> ops;
@@ -90,6 +92,7 @@ int run_op(const Op& o, hipStream_t s) {
     case OP_INC_STEM: return dml_stem_inception(&o.istem, s);
     case OP_CONV_POOL: return dml_conv3x3_pool(&o.cpool, s);
     case OP_EXP_RED: return dml_expand_reduce(&o.er, s);
+    case OP_CONV_GROUP: return dml_conv_group(&o.grp, o.cfg, s);
   }
   return -1;
 }
@@ -161,6 +164,15 @@ extern "C" int dml_plan_add_conv_pool(void* p, const DmlConvPoolArgs* a) {
   o.cpool = *a;
   ((Plan*)p)->ops.push_back(o);
   return 0;
+}
+extern "C" int dml_plan_add_conv_group(void* p, const DmlConvGroupArgs* g, int cfg) {
+  if (dml_conv_group_validate(g, cfg) != 0) return -1;
+  Op o{};
+  o.kind = OP_CONV_GROUP;
+  o.grp = *g;
+  o.cfg = cfg;
+  ((Plan*)p)->ops.push_back(o);
+  return cfg;
 }
 extern "C" int dml_plan_add_expand_reduce(void* p, const DmlExpandReduceArgs* a) {
   Op o{};

@@ -67,7 +67,16 @@ int main() {
     DmlExpandReduceArgs er;
     std::memset(&er, 0, sizeof er);
     CHECK(dml_plan_add_expand_reduce(plan, &er) == 0);
-    n += 7;
+    DmlConvGroupArgs grp;
+    std::memset(&grp, 0, sizeof grp);
+    grp.n = 3;
+    grp.a[0] = conv_args(64, 96, 5, 5);
+    grp.a[1] = conv_args(64, 96, 3, 3);
+    grp.a[2] = conv_args(64, 64, 1, 1);
+    CHECK(dml_plan_add_conv_group(plan, &grp, 14) == 14);
+    CHECK(dml_plan_add_conv_group(plan, &grp, 10) != 0);   // no grouped instantiation of tile 10
+    CHECK(std::string(dml_last_error()).find("grouped") != std::string::npos);
+    n += 8;
     CHECK(dml_plan_size(plan) == n);
     // error paths that must return before any device call
     CHECK(dml_plan_replay(plan, nullptr) != 0);
@@ -103,6 +112,19 @@ int main() {
   a = conv_args(64, 64, 3, 3);
   a.kchunk = 32;
   CHECK(dml_conv(&a, 11, nullptr) != 0);        // chunk-major K order: kchunk % 64
+  DmlConvGroupArgs g;
+  std::memset(&g, 0, sizeof g);
+  CHECK(dml_conv_group(&g, 14, nullptr) != 0);  // no members
+  g.n = DML_CONV_GROUP_MAX + 1;
+  CHECK(dml_conv_group(&g, 14, nullptr) != 0);  // too many members
+  g.n = 2;
+  g.a[0] = conv_args(64, 64, 3, 3);
+  g.a[1] = conv_args(64, 64, 1, 1);
+  g.a[1].res = (const void*)0x100; g.a[1].ldr = 64;
+  CHECK(dml_conv_group(&g, 14, nullptr) != 0);  // members are residual-free
+  CHECK(std::string(dml_last_error()).find("residual-free") != std::string::npos);
+  g.a[1] = conv_args(12, 64, 1, 1);
+  CHECK(dml_conv_group(&g, 14, nullptr) != 0);  // every member passes dml_conv's validation
   a = conv_args(8, 64, 3, 3);
   CHECK(dml_conv_pick_cfg(&a) == 15);
   a = conv_args(3, 64, 3, 3);

@@ -34,6 +34,13 @@ class ConvArgs(C.Structure):
     ]
 
 
+GROUP_MAX = 4
+
+
+class ConvGroupArgs(C.Structure):
+    _fields_ = [("n", C.c_int), ("off", C.c_int * (GROUP_MAX + 1)), ("a", ConvArgs * GROUP_MAX)]
+
+
 class PoolArgs(C.Structure):
     _fields_ = [
         ("x", C.c_void_p), ("y", C.c_void_p),
@@ -97,6 +104,8 @@ _SIGS = {
     "dml_plan_add_inc_stem": (C.c_int, [C.c_void_p, C.POINTER(IncStemArgs)]),
     "dml_plan_add_stem": (C.c_int, [C.c_void_p, C.POINTER(StemArgs)]),
     "dml_conv": (C.c_int, [C.POINTER(ConvArgs), C.c_int, C.c_void_p]),
+    "dml_conv_group": (C.c_int, [C.POINTER(ConvGroupArgs), C.c_int, C.c_void_p]),
+    "dml_plan_add_conv_group": (C.c_int, [C.c_void_p, C.POINTER(ConvGroupArgs), C.c_int]),
     "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),
     "dml_conv_v2_init": (C.c_int, []),
     "dml_pool": (C.c_int, [C.POINTER(PoolArgs), C.c_void_p]),

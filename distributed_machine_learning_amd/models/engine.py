@@ -60,13 +60,17 @@ class Engine:
                  src_slots: int = 1, reuse_buffers: bool = True, autotune: bool = True, optimize: bool = True,
                  share: Optional["Engine"] = None, src_tensors: Optional[List[torch.Tensor]] = None,
                  result_views: Optional[List[torch.Tensor]] = None, fuse_stem: bool = True,
-                 fuse_blocks: bool = True):
+                 fuse_blocks: bool = True, conv_groups: Optional[bool] = None):
         """``share``: reuse another engine's (optimized) graph and resident weights
         (sub-batch engines of a SplitEngine); ``src_tensors`` / ``result_views``:
         external uint8 source slots / per-slot [2, batch, 5] result rows to use
         instead of allocating them. ``fuse_stem=False`` (or DML_FUSED_STEM=0) keeps the
         ResNet stem as three launches (preprocess, conv, pool); ``fuse_blocks=False``
-        (or DML_FUSED_BLOCKS=0) keeps every bottleneck 1x1 conv its own launch."""
+        (or DML_FUSED_BLOCKS=0) keeps every bottleneck 1x1 conv its own launch;
+        ``conv_groups=False`` (or DML_CONV_GROUPS=0) launches InceptionV3's
+        independent branch convs one by one instead of as grouped grids."""
+        if conv_groups is None:
+            conv_groups = os.environ.get("DML_CONV_GROUPS", "1") != "0"
         if share is not None:
             graph = share.g
         elif optimize:  # graph rewrites: conv-before-avgpool, sibling 1x1 fusion (models/optimize.py)
@@ -76,6 +80,10 @@ class Engine:
             graph = _opt(graph, stride_push=os.environ.get("DML_STRIDE_PUSH") != "0",
                          weights=weights if merge else None,
                          shortcut_min_cout=int(os.environ.get("DML_SHORTCUT_MERGE_MINC", "0")))
+            if conv_groups:  # independent convs side by side (models/optimize.py rewrite 5)
+                from .optimize import level_order
+
+                graph = level_order(graph)
         self.g, self.batch, self.device = graph, batch, torch.device(device)
         self.src_slots = src_slots
         self.reuse_buffers = reuse_buffers
@@ -104,6 +112,8 @@ class Engine:
         self.exp_red = self._fusable_expand_reduce(fuse_blocks)
         # fused pairs whose Y is otherwise only read at stride 2 store just those pixels
         self.ysub = self._subsampled_y()
+        # independent residual-free convs of one graph level -> one grouped grid each
+        self.conv_groups = self._conv_group_candidates() if conv_groups else []
         self._src_tensors, self._result_views = src_tensors, result_views
         if share is not None:
             self.wdev = share.wdev
@@ -239,6 +249,16 @@ class Engine:
             out[e.name] = r
         return out
 
+    def _conv_group_candidates(self) -> List[List[Conv]]:
+        """Runs of consecutive plain convs of one ASAP level (the level order puts
+        them side by side), at most GROUP_MAX per group. Whether a group really
+        launches as one grid is decided by timing at plan time (``_build_plan``)."""
+        from .optimize import conv_group_runs
+
+        taken = {t.name for t in (self.stem, self.stem_conv2) if t is not None}
+        taken |= set(self.conv_pools) | set(self.exp_red) | {r.name for r in self.exp_red.values()}
+        return conv_group_runs(self.g, taken, N.GROUP_MAX)
+
     def _subsampled_y(self) -> Dict[str, int]:
         """{tensor: 2} for fused expand+reduce outputs Y whose readers besides the fused
         reduce all take it as a stride-2 shortcut (``res_sub == 2``, left by the stride
@@ -293,6 +313,11 @@ class Engine:
             for src in (first.inp, getattr(first, "residual", None)):
                 if src:
                     last_use[src] = max(last_use[src], index[second.name])
+        # a conv group runs at its first member's position: every member's input
+        # stays live through the last member
+        for grp in self.conv_groups:
+            for m in grp:
+                last_use[m.inp] = max(last_use[m.inp], index[grp[-1].name])
         self.cbuf = {name: _r(t.c, 8) for name, t in g.tensors.items()}
         self.cbuf[g.input] = 8
         self.buf: Dict[str, torch.Tensor] = {}
@@ -364,15 +389,33 @@ class Engine:
 
     # --------------------------------------------------------------- plan ----
     def _build_plan(self) -> None:
+        from ..ops import tuning
+
         self.tuned: Dict[str, int] = {}
         if self.autotune and self.device.type == "cuda":
-            from ..ops import tuning
-
             cnodes = [n for n in self.g.nodes if isinstance(n, (Conv, Dense, FusedConv))]
             convs = [self._conv_args(n) for n in cnodes]
             table = tuning.autotune(convs)
             for n, a in zip(cnodes, convs):
                 self.tuned[n.name] = table.get(tuning.shape_key(a), -1)
+        # grouped launches: the timed best grouped tile, or -1 where the members
+        # run faster one by one on their own tuned tiles (no timing: group iff the
+        # largest member's default tile has a grouped instantiation)
+        self.group_cfg: Dict[str, int] = {}
+        for grp in self.conv_groups:
+            args = [self._conv_args(m) for m in grp]
+            cfgs = [self.cfg_overrides.get(m.name, self.tuned.get(m.name, -1)) for m in grp]
+            if any(m.name in self.cfg_overrides for m in grp):
+                cfg = -1
+            elif self.autotune and self.device.type == "cuda":
+                cfg = tuning.autotune_group(args, cfgs)
+            else:
+                big = max(range(len(grp)), key=lambda i: args[i].N * args[i].Ho * args[i].Wo * args[i].Cout
+                          * args[i].Kpad)
+                c = cfgs[big] if cfgs[big] >= 0 else self.lib.dml_conv_pick_cfg(C.byref(args[big]))
+                cfg = c if c in tuning.GROUP_CFGS else -1
+            if cfg >= 0:
+                self.group_cfg[grp[0].name] = cfg
         self.plans = [self._build_one_plan(self.srcs[i], self.results[i]) for i in range(self.src_slots)]
         self.plan = self.plans[0]
         self.graph_captured = [False] * self.src_slots
@@ -415,8 +458,23 @@ class Engine:
             self.op_names.append("preprocess")
         skip |= {p.name for p in self.conv_pools.values()}
         skip |= {r.name for r in self.exp_red.values()}
+        groups = {grp[0].name: grp for grp in self.conv_groups if grp[0].name in self.group_cfg}
+        for grp in groups.values():
+            skip |= {m.name for m in grp[1:]}
         for n in g.nodes:
             if n.name in skip:
+                continue
+            if n.name in groups:
+                grp, cfg = groups[n.name], self.group_cfg[n.name]
+                ga = N.ConvGroupArgs()
+                ga.n = len(grp)
+                for i, m in enumerate(grp):
+                    ga.a[i] = self._conv_args(m)
+                N.check(L.dml_plan_add_conv_group(plan, C.byref(ga), cfg), f"plan conv group {n.name}")
+                for m in grp:
+                    self.op_cfg[m.name] = cfg
+                self._keep.append(ga)
+                self.op_names.append("|".join(m.name for m in grp))
                 continue
             if n.name in self.exp_red:
                 r = self.exp_red[n.name]

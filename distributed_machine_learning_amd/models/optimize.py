@@ -36,6 +36,13 @@
    Needs the folded weights: the merged conv's kernel/bias are ADDED to the
    weights dict under "<expand>+<shortcut>" (BN folded, ``bn=False``).
 
+5. ``level_order`` — a topological re-order by ASAP level (level = 1 + the
+   deepest writer of any tensor the node reads; concat tensors have several
+   writers). Nodes of one level are mutually independent: InceptionV3's branch
+   convs (5x5 next to 3x3, 1x7 next to 7x1, 1x3 / 3x1 / 3x3) land side by side,
+   residual-free convs first, so the engine can launch each level's convs as
+   ONE grouped grid (dml_conv_group). Pure re-order: outputs are unchanged.
+
 Rewrites 1-3 keep the weights dict unchanged (members keep their names); the
 fp32 oracle can execute the rewritten graph too (tests compare both forms).
 """
@@ -196,6 +203,77 @@ def merge_projection_shortcut(g: Graph, w: Dict[str, np.ndarray], min_cout: int 
             break
     g.validate()
     return g
+
+
+def _writes(g: Graph, n) -> List[tuple]:
+    """(tensor, c0, c1) channel ranges node ``n`` writes."""
+    if isinstance(n, FusedConv):
+        return [(m.out, m.out_coff, m.out_coff + m.cout) for m in n.members]
+    if isinstance(n, Conv):
+        return [(n.out, n.out_coff, n.out_coff + n.cout)]
+    if isinstance(n, Pool):
+        return [(n.out, n.out_coff, n.out_coff + g.shape(n.inp)[2])]
+    return [(n.out, 0, g.shape(n.out)[2])]
+
+
+def _reads(g: Graph, n) -> List[tuple]:
+    out = []
+    if isinstance(n, Conv):
+        out.append((n.inp, n.in_coff, n.in_coff + n.cin))
+    else:
+        out.append((n.inp, 0, g.shape(n.inp)[2]))
+    if getattr(n, "residual", None):
+        out.append((n.residual, 0, g.shape(n.residual)[2]))
+    return out
+
+
+def levels(g: Graph) -> Dict[str, int]:
+    """{node name: ASAP level}; the graph input is level 0. Dependencies are
+    channel-range exact: a tensor written in slices (Inception concat, ResNet's
+    merged [x ; shortcut] buffer) makes a reader wait only for the writers of
+    the channels it reads."""
+    writers: Dict[str, List[tuple]] = {}
+    for n in g.nodes:
+        for t, c0, c1 in _writes(g, n):
+            writers.setdefault(t, []).append((n, c0, c1))
+    lv: Dict[str, int] = {}
+    for n in g.nodes:  # the node order is topological: producers come first
+        deps = [lv[w.name] for t, r0, r1 in _reads(g, n) for w, c0, c1 in writers.get(t, [])
+                if w is not n and c0 < r1 and r0 < c1]
+        lv[n.name] = 1 + max(deps, default=0)
+    return lv
+
+
+def groupable_conv(n) -> bool:
+    """A conv the grouped launch can run: plain (not fused), no residual, bf16 out."""
+    return isinstance(n, Conv) and n.residual is None and not n.out_f32
+
+
+def level_order(g: Graph) -> Graph:
+    lv = levels(g)
+    pos = {n.name: i for i, n in enumerate(g.nodes)}
+    g = copy.copy(g)
+    g.nodes = sorted(g.nodes, key=lambda n: (lv[n.name], not groupable_conv(n), pos[n.name]))
+    g.validate()
+    return g
+
+
+def conv_group_runs(g: Graph, exclude: set = frozenset(), max_members: int = 4) -> List[List[Conv]]:
+    """Runs of >= 2 consecutive groupable convs of one level (not in ``exclude``),
+    at most ``max_members`` each: the members of one grouped launch. Consecutive
+    + same level makes a run independent in any node order."""
+    lv = levels(g)
+    runs: List[List[Conv]] = []
+    run: List[Conv] = []
+    for n in list(g.nodes) + [None]:
+        ok = n is not None and groupable_conv(n) and n.name not in exclude
+        if run and not (ok and lv[n.name] == lv[run[0].name] and len(run) < max_members):
+            if len(run) > 1:
+                runs.append(run)
+            run = []
+        if ok:
+            run.append(n)
+    return runs
 
 
 def optimize(g: Graph, pool_reorder: bool = True, fuse: bool = True, stride_push: bool = True,

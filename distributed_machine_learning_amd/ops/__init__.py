@@ -62,8 +62,10 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
                 stride=(1, 1), pad=(0, 0), relu: bool = False, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, out_coff: int = 0, in_coff: int = 0, cin: Optional[int] = None,
                 out_f32: bool = False, cfg: int = -1, K: Optional[int] = None, dilation=(1, 1),
-                out_hw: Optional[Tuple[int, int]] = None, ksplit: int = 1, kchunk: int = 0) -> torch.Tensor:
+                out_hw: Optional[Tuple[int, int]] = None, ksplit: int = 1, kchunk: int = 0,
+                defer: Optional[list] = None) -> torch.Tensor:
     """x: NHWC bf16 [N,H,W,Cbuf] (Cbuf % 8 == 0). Returns/updates NHWC output.
+    defer: a list to append the ConvArgs to instead of launching (conv_group).
     ksplit > 1 (fp32 output, v2 cfg): returns the [ksplit, N, Ho, Wo, C] split-K
     partial sums (slice 0 carries the bias); their sum is the convolution.
     kchunk > 0: w_packed is in chunk-major K order (pack_weight_chunk_major)."""
@@ -100,6 +102,10 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
         assert residual.shape[1] == ho * rs and residual.shape[2] == wo * rs and residual.is_contiguous()
         a.rsub, a.rW, a.rHW = rs, residual.shape[2], residual.shape[1] * residual.shape[2]
     L = N.lib()
+    if defer is not None:
+        defer.append(a)
+        out._keep = bias_p
+        return out
     if cfg < 0:
         cfg = L.dml_conv_pick_cfg(C.byref(a))
     N.check(L.dml_conv(C.byref(a), cfg, N.stream_ptr()), "dml_conv")
@@ -108,6 +114,16 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
         return parts
     out._keep = bias_p  # keep alive until the kernel ran (caller syncs)
     return out
+
+
+def conv_group(args: list, cfg: int) -> None:
+    """Launch up to GROUP_MAX independent convs (ConvArgs from conv2d_nhwc(...,
+    defer=list)) as ONE grid on tile config ``cfg`` (dml_conv_group)."""
+    g = N.ConvGroupArgs()
+    g.n = len(args)
+    for i, a in enumerate(args):
+        g.a[i] = a
+    N.check(N.lib().dml_conv_group(C.byref(g), cfg, N.stream_ptr()), "dml_conv_group")
 
 
 def pool3x3(x: torch.Tensor, mode: str, k: int = 3, stride: int = 2, pad: int = 0,

@@ -109,3 +109,63 @@ def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None,
             pass
     cache.update(new)
     return cache
+
+
+# ---------------------------------------------------------- grouped convs --
+GROUP_CFGS = (11, 14, 15, 23, 32)  # tiles with a grouped instantiation (dml_conv_v2_group)
+
+
+def group_key(args: List[N.ConvArgs]) -> str:
+    return "grp_" + "|".join(shape_key(a)[:-len(CAND_TAG) - 1] for a in args) + "_" + CAND_TAG
+
+
+def group_args(args: List[N.ConvArgs]) -> N.ConvGroupArgs:
+    g = N.ConvGroupArgs()
+    g.n = len(args)
+    for i, a in enumerate(args):
+        g.a[i] = a
+    return g
+
+
+def _time(fn, iters: int) -> float:
+    import torch
+
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def autotune_group(args: List[N.ConvArgs], cfgs: List[int], cache: Optional[Dict[str, int]] = None,
+                   persist: bool = True, iters: int = 20) -> int:
+    """Best tile for launching ``args`` as ONE grouped grid, or -1 when running
+    them one after another, each on its own tuned tile ``cfgs``, is faster."""
+    k = group_key(args)
+    cache = load_cache() if cache is None else cache
+    if k in cache:
+        return cache[k]
+    L, s = N.lib(), N.stream_ptr()
+    best: Tuple[float, int] = (float("inf"), -1)
+    if all(c >= 0 for c in cfgs):
+        def seq():
+            for a, c in zip(args, cfgs):
+                N.check(L.dml_conv(C.byref(a), c, s), "conv")
+        best = (_time(seq, iters), -1)
+    g = group_args(args)
+    for cfg in GROUP_CFGS:
+        try:
+            t = _time(lambda: N.check(L.dml_conv_group(C.byref(g), cfg, s), "conv group"), iters)
+        except N.NativeError:
+            continue
+        best = min(best, (t, cfg))
+    cache[k] = best[1]
+    if persist:
+        try:
+            save_cache({k: best[1]})
+        except OSError:
+            pass
+    return best[1]

@@ -215,3 +215,34 @@ def test_capture_parts_matches_full_graph():
         eng.run_part(i, s)
     s.synchronize()
     assert torch.equal(full, eng.result)
+
+
+@pytest.mark.parametrize("autotune", [False, True])
+def test_inception_grouped_convs_match_ungrouped(autotune):
+    """InceptionV3 with its independent branch convs launched as grouped grids
+    (level-ordered graph, dml_conv_group) == the same network launched conv by
+    conv. Members may run on a different tile than alone, so only accumulation
+    order differs. autotune=False forces grouping (no timing decides against it)."""
+    g, w = build_model("InceptionV3", seed=0, calibrate=True)
+    imgs = torch.randint(0, 256, (8, *g.input_hw, 3), dtype=torch.uint8,
+                         generator=torch.Generator().manual_seed(1)).cuda()
+    eg = Engine(g, w, batch=8, conv_groups=True, autotune=autotune)
+    e1 = Engine(g, w, batch=8, conv_groups=False, autotune=autotune)
+    assert len(eg.conv_groups) == 17
+    if not autotune:
+        assert len(eg.group_cfg) >= 10 and any("|" in op for op in eg.op_names), eg.group_cfg
+    print("grouped launches", len(eg.group_cfg), "of", len(eg.conv_groups), eg.group_cfg)
+    eg.infer(imgs)
+    e1.infer(imgs)
+    torch.cuda.synchronize()
+    a, b = eg.buf[g.logits].float().cpu(), e1.buf[g.logits].float().cpu()
+    assert _rel(a, b) < 1e-2, _rel(a, b)
+    assert (eg.top_idx[:, 0] == e1.top_idx[:, 0]).float().mean().item() >= 0.875
+    # graph replay of the grouped plan == its eager run
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        eager = eg.buf[g.logits].clone()
+        eg.run(s, use_graph=True)
+        s.synchronize()
+    assert torch.equal(eager, eg.buf[g.logits])

@@ -250,3 +250,41 @@ def test_rewrites_leave_ineligible_graphs_alone():
     a = OracleExecutor(g, w).forward(x)["logits"]
     b = OracleExecutor(gm, w2).forward(x)["logits"]
     assert ((a - b).abs().max() / a.abs().max()).item() < 1e-4
+
+
+def test_level_order_and_conv_groups():
+    """level_order is a pure topological re-order (fp32 logits bit-identical) that
+    puts InceptionV3's independent branch convs side by side: 17 grouped launches
+    (5x5|3x3, 1x7|7x1, 1x3|3x1|3x3 ...); ResNet50 (a chain, shortcut merged into
+    sliced buffers) has none and keeps its order."""
+    from distributed_machine_learning_amd.models.optimize import (_reads, _writes, conv_group_runs, levels,
+                                                                  level_order, optimize)
+
+    for name, n_runs in (("InceptionV3", 17), ("ResNet50", 0)):
+        g, w = build_model(name, seed=0, calibrate=False)
+        w2 = dict(w)
+        go = optimize(g, weights=w2)
+        lo = level_order(go)
+        assert sorted(n.name for n in lo.nodes) == sorted(n.name for n in go.nodes)
+        # every writer of a channel range precedes every reader of it
+        pos = {n.name: i for i, n in enumerate(lo.nodes)}
+        for n in lo.nodes:
+            for t, r0, r1 in _reads(lo, n):
+                for m in lo.nodes:
+                    if m is not n and any(t2 == t and c0 < r1 and r0 < c1 for t2, c0, c1 in _writes(lo, m)):
+                        assert pos[m.name] < pos[n.name], (m.name, n.name)
+        runs = conv_group_runs(lo)
+        assert len(runs) == n_runs
+        lv = levels(lo)
+        for r in runs:
+            assert 2 <= len(r) <= 4 and len({lv[m.name] for m in r}) == 1
+            outs = {wr[0] for m in r for wr in _writes(lo, m)}
+            assert not any(m.inp in outs for m in r)  # members read nothing a member writes
+        assert conv_group_runs(lo) == conv_group_runs(level_order(lo))  # idempotent
+        if name == "ResNet50":
+            assert [n.name for n in lo.nodes] == [n.name for n in go.nodes]
+        imgs = torch.randint(0, 256, (1, *g.input_hw, 3), dtype=torch.uint8)
+        x = preprocess_reference(imgs, g.input_hw, g.preprocess)
+        a = OracleExecutor(go, w2).forward(x)["logits"]
+        b = OracleExecutor(lo, w2).forward(x)["logits"]
+        assert torch.equal(a, b)

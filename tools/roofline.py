@@ -56,7 +56,7 @@ def main():
                 if t:
                     readers.setdefault(t, set()).add(n.name)
     for name, ms in d["ops"]:
-        parts = [name] if name in by_name else [p for p in name.split("+") if p in by_name]
+        parts = [name] if name in by_name else [p for p in name.replace("|", "+").split("+") if p in by_name]
         fl = by = 0.0
         kinds = []
         for p in parts:
