@@ -60,15 +60,7 @@ typedef struct {
   int kchunk;
 } DmlConvArgs;
 
-// Grouped launch of up to DML_CONV_GROUP_MAX independent convs in one grid
-// (dml_conv_group): residual-free, all on the same tile config. off[] is filled
-// by the launcher (prefix tile offsets, off[n] = grid size).
-#define DML_CONV_GROUP_MAX 4
-typedef struct {
-  int n;
-  int off[DML_CONV_GROUP_MAX + 1];
-  DmlConvArgs a[DML_CONV_GROUP_MAX];
-} DmlConvGroupArgs;
+
 
 typedef struct {
   const void* x;  // bf16 NHWC
@@ -79,6 +71,20 @@ typedef struct {
   int mode;            // 0 = max (padding never wins), 1 = avg with padding excluded from the divisor
   int relu;            // apply ReLU to the pooled value (avg-pool after a pre-pool 1x1 conv)
 } DmlPoolArgs;
+
+// Grouped launch (dml_conv_group): up to DML_CONV_GROUP_MAX independent convs
+// (residual-free, all on one tile config) and up to DML_GROUP_POOL_MAX
+// independent 3x3 pools (pad <= 1) in ONE grid. off[] is filled by the launcher
+// (prefix block offsets: convs, then pools; off[n + npool] = grid size).
+#define DML_CONV_GROUP_MAX 4
+#define DML_GROUP_POOL_MAX 2
+typedef struct {
+  int n;      // convs (>= 1)
+  int npool;  // pools
+  int off[DML_CONV_GROUP_MAX + DML_GROUP_POOL_MAX + 1];
+  DmlConvArgs a[DML_CONV_GROUP_MAX];
+  DmlPoolArgs pool[DML_GROUP_POOL_MAX];
+} DmlConvGroupArgs;
 
 typedef struct {
   const void* src;  // uint8 [N][Hs][Ws][3] RGB
@@ -175,6 +181,8 @@ int dml_softmax_top5(const float* logits, int B, int classes, int ld, float* pro
 int dml_softmax_top5_split(float* logits, int B, int classes, int ld, int nsplit, int split_ld,
                            float* probs_out, int* top_idx, float* top_p, hipStream_t s);
 int dml_preprocess(const DmlPreprocArgs* a, hipStream_t s);
+
+int dml_abi_sizes(int* out, int n);
 
 // ---- plan executor (C++ runtime, csrc/runtime/runtime.hip) ----
 void* dml_plan_create(void);

@@ -13,6 +13,7 @@
 // 0 of 217 tuned shapes).
 #include "common.h"
 #include "dml.h"
+#include "pool_shared.h"
 
 static int validate(const DmlConvArgs* a, int cfg) {
   if (cfg < 10 || cfg >= 40) {
@@ -48,12 +49,18 @@ extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
 }
 
 extern "C" int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg) {
-  if (!g || g->n < 1 || g->n > DML_CONV_GROUP_MAX) {
-    dml_set_error("dml_conv_group: 1..4 members");
+  if (!g || g->n < 1 || g->n > DML_CONV_GROUP_MAX || g->npool < 0 || g->npool > DML_GROUP_POOL_MAX) {
+    dml_set_error("dml_conv_group: 1..4 convs and 0..2 pools");
     return -1;
   }
+  for (int j = 0; j < g->npool; ++j) {
+    if (!dml::poolk::pool3x3_fast_ok(g->pool[j])) {
+      dml_set_error("dml_conv_group: pool members must be 3x3, pad <= 1, channels %8");
+      return -1;
+    }
+  }
   if (!dml_conv_v2_group_supported(cfg)) {
-    dml_set_error("dml_conv_group: cfg has no grouped instantiation (11, 14, 15, 23, 32)");
+    dml_set_error("dml_conv_group: cfg has no grouped instantiation (the 4-wave tiles)");
     return -1;
   }
   for (int i = 0; i < g->n; ++i) {

@@ -27,6 +27,7 @@
 //  * XCD-aware bijective block remap; channel tiles fastest so the blocks on
 //    one XCD share the activation rows in its L2.
 #include "conv_shared.h"
+#include "pool_shared.h"
 
 namespace dml {
 namespace v2 {
@@ -268,12 +269,32 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
 }
 
 // Grouped launch: up to DML_CONV_GROUP_MAX independent convs (InceptionV3's
-// parallel branch convs: different kh x kw, inputs and outputs) share ONE grid;
-// block -> member by the prefix tile offsets, XCD remap over the whole grid.
-// Fills the 256 CUs where each member alone leaves them half idle.
+// parallel branch convs: different kh x kw, inputs and outputs) and up to
+// DML_GROUP_POOL_MAX independent 3x3 pools of the same graph level share ONE
+// grid; block -> member by the prefix block offsets. The conv tiles are
+// XCD-remapped over their own block range; the pools' blocks come last, so they
+// fill the conv tiles' tail instead of paying a launch and a drain of their own.
 template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
 __global__ __launch_bounds__(WM* WN * 64) void conv_v2_group_kernel(DmlConvGroupArgs g) {
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = blockIdx.x, nconv = g.off[g.n];
+  if (b >= nconv) {
+    // pool member: 256 work items per block, raw block order (dispatched last and
+    // round-robin over the XCDs; an XCD-remapped range would put them all on one)
+    const int nm = g.n + g.npool;
+    int i = g.n;
+#pragma unroll
+    for (int q = 1; q < DML_GROUP_POOL_MAX; ++q)
+      if (g.n + q < nm && b >= g.off[g.n + q]) i = g.n + q;
+    i = __builtin_amdgcn_readfirstlane(i);
+    const DmlPoolArgs& p = g.pool[i - g.n];
+    const unsigned t = (unsigned)(b - g.off[i]) * 256u + threadIdx.x;
+    if (t < (unsigned)poolk::pool_work(p)) {
+      if (p.mode == 0) poolk::pool3x3_item<0>(p, t);
+      else poolk::pool3x3_item<1>(p, t);
+    }
+    return;
+  }
+  const int L = xcd_remap(b, nconv);  // conv tiles: XCD-aware over their own range
   int i = 0;
 #pragma unroll
   for (int q = 1; q < DML_CONV_GROUP_MAX; ++q)
@@ -300,14 +321,17 @@ static int launch(const DmlConvArgs* a, hipStream_t s) {
 template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
 static int launch_group(const DmlConvGroupArgs* g, hipStream_t s) {
   using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
+  static_assert(T::NT == 256, "pool members run 256 work items per block");
   DmlConvGroupArgs h = *g;
   h.off[0] = 0;
   for (int i = 0; i < h.n; ++i) {
     const long M = (long)h.a[i].N * h.a[i].Ho * h.a[i].Wo;
     h.off[i + 1] = h.off[i] + (int)(((M + BM - 1) / BM) * ((h.a[i].Cout + BN - 1) / BN));
   }
-  hipLaunchKernelGGL((conv_v2_group_kernel<BM, BN, WM, WN, STAGES, BK>), dim3((unsigned)h.off[h.n]), dim3(T::NT),
-                     T::LDS, s, h);
+  for (int j = 0; j < h.npool; ++j)
+    h.off[h.n + j + 1] = h.off[h.n + j] + (int)((poolk::pool_work(h.pool[j]) + 255) / 256);
+  hipLaunchKernelGGL((conv_v2_group_kernel<BM, BN, WM, WN, STAGES, BK>), dim3((unsigned)h.off[h.n + h.npool]),
+                     dim3(T::NT), T::LDS, s, h);
   DML_CHECK_LAUNCH();
   return 0;
 }
@@ -364,10 +388,20 @@ extern "C" int dml_conv_v2_init(void) {
   rc |= set_attr<128, 32, 2, 1, 3, 32>();
   rc |= set_attr<256, 32, 4, 1, 3, 64>();
   rc |= set_attr_group<128, 128, 2, 2, 2>();
+  rc |= set_attr_group<256, 64, 4, 1, 2>();
   rc |= set_attr_group<64, 128, 1, 4, 2>();
   rc |= set_attr_group<128, 64, 2, 2, 2>();
-  rc |= set_attr_group<64, 128, 1, 4, 3>();
+  rc |= set_attr_group<128, 128, 2, 2, 3>();
+  rc |= set_attr_group<64, 256, 1, 4, 2>();
   rc |= set_attr_group<64, 128, 1, 4, 2, 32>();
+  rc |= set_attr_group<128, 64, 2, 2, 2, 32>();
+  rc |= set_attr_group<128, 128, 2, 2, 2, 32>();
+  rc |= set_attr_group<64, 128, 1, 4, 3, 32>();
+  rc |= set_attr_group<128, 64, 2, 2, 3, 32>();
+  rc |= set_attr_group<128, 128, 2, 2, 3, 32>();
+  rc |= set_attr_group<128, 128, 2, 2, 4, 32>();
+  rc |= set_attr_group<64, 128, 1, 4, 3>();
+  rc |= set_attr_group<64, 128, 1, 4, 4, 32>();
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   if (!rc && dml_expand_reduce_init() != 0) return -1;  // fused block-boundary kernels (bottleneck_fused.hip)
   return rc ? -1 : 0;
@@ -414,19 +448,48 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
 }
 
 // Grouped launch of independent convs (cfg: the tile config every member uses;
-// instantiated for the configs InceptionV3's branch convs tune to).
+// instantiated for every 4-wave tile, the block size the pool members assume).
 extern "C" int dml_conv_v2_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s) {
   using namespace dml::v2;
   switch (cfg) {
     case 11: return launch_group<128, 128, 2, 2, 2>(g, s);
+    case 12: return launch_group<256, 64, 4, 1, 2>(g, s);
     case 14: return launch_group<64, 128, 1, 4, 2>(g, s);
     case 15: return launch_group<128, 64, 2, 2, 2>(g, s);
-    case 32: return launch_group<64, 128, 1, 4, 3>(g, s);
+    case 17: return launch_group<128, 128, 2, 2, 3>(g, s);
+    case 22: return launch_group<64, 256, 1, 4, 2>(g, s);
     case 23: return launch_group<64, 128, 1, 4, 2, 32>(g, s);
-    default: dml_set_error("dml_conv_group: cfg has no grouped instantiation (11, 14, 15, 23, 32)"); return -1;
+    case 24: return launch_group<128, 64, 2, 2, 2, 32>(g, s);
+    case 25: return launch_group<128, 128, 2, 2, 2, 32>(g, s);
+    case 26: return launch_group<64, 128, 1, 4, 3, 32>(g, s);
+    case 27: return launch_group<128, 64, 2, 2, 3, 32>(g, s);
+    case 28: return launch_group<128, 128, 2, 2, 3, 32>(g, s);
+    case 29: return launch_group<128, 128, 2, 2, 4, 32>(g, s);
+    case 32: return launch_group<64, 128, 1, 4, 3>(g, s);
+    case 33: return launch_group<64, 128, 1, 4, 4, 32>(g, s);
+    default: dml_set_error("dml_conv_group: cfg has no grouped instantiation (the 4-wave tiles)"); return -1;
   }
 }
 
 extern "C" int dml_conv_v2_group_supported(int cfg) {
-  return cfg == 11 || cfg == 14 || cfg == 15 || cfg == 23 || cfg == 32;
+  switch (cfg) {
+    case 11:
+    case 12:
+    case 14:
+    case 15:
+    case 17:
+    case 22:
+    case 23:
+    case 24:
+    case 25:
+    case 26:
+    case 27:
+    case 28:
+    case 29:
+    case 32:
+    case 33:
+      return 1;
+    default:
+      return 0;
+  }
 }

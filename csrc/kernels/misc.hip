@@ -13,6 +13,7 @@
 // vectorisation rule; every kernel is a grid-stride loop capped near 8 blocks/CU.
 #include "common.h"
 #include "dml.h"
+#include "pool_shared.h"
 #include <cstdlib>
 
 namespace dml {
@@ -83,73 +84,11 @@ __global__ __launch_bounds__(256) void pool3x3_kernel(DmlPoolArgs a) {
   }
 }
 
-// 3x3 pool, pad <= 1: one thread per (pixel, 8-channel group), all nine 16-B
-// tap loads issued before any is consumed (the generic kernel's per-tap branches
-// serialise them: max_pooling2d_2 of InceptionV3 ran at 1.9 TB/s). Out-of-image
-// taps load the clamped edge pixel — for a 3-wide window with pad <= 1 that pixel
-// lies inside the window, so max needs no mask; avg weights it 0 and divides by
-// the in-image tap count (TF SAME semantics). 32-bit index math.
+// 3x3 pool, pad <= 1 (body: pool_shared.h, also run inside grouped conv grids)
 template <int MODE>
 __global__ __launch_bounds__(256) void pool3x3_fast_kernel(DmlPoolArgs a, unsigned total) {
   const unsigned t = blockIdx.x * 256u + threadIdx.x;
-  if (t >= total) return;
-  const unsigned C8 = (unsigned)a.C / 8;
-  const unsigned cg = t % C8;
-  unsigned p = t / C8;
-  const int ow = (int)(p % (unsigned)a.Wo); p /= (unsigned)a.Wo;
-  const int oh = (int)(p % (unsigned)a.Ho);
-  const int n = (int)(p / (unsigned)a.Ho);
-  const int h0 = oh * a.stride - a.pad, w0 = ow * a.stride - a.pad;
-  const bf16* xb = (const bf16*)a.x + (long)n * a.H * a.W * a.ldx + cg * 8;
-  uint4 v[9];
-  int rows[3], cols[3];
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    rows[r] = min(max(h0 + r, 0), a.H - 1);
-    cols[r] = min(max(w0 + r, 0), a.W - 1);
-  }
-#pragma unroll
-  for (int r = 0; r < 3; ++r)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) v[r * 3 + c] = *(const uint4*)(xb + (long)(rows[r] * a.W + cols[c]) * a.ldx);
-  float acc[8];
-  if (MODE == 0) {
-    unpack8(v[0], acc);
-#pragma unroll
-    for (int q = 1; q < 9; ++q) {
-      float f[8];
-      unpack8(v[q], f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = fmaxf(acc[j], f[j]);
-    }
-  } else {
-    float rw[3], cw[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      rw[r] = (unsigned)(h0 + r) < (unsigned)a.H ? 1.f : 0.f;
-      cw[r] = (unsigned)(w0 + r) < (unsigned)a.W ? 1.f : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        float f[8];
-        unpack8(v[r * 3 + c], f);
-        const float wgt = rw[r] * cw[c];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = fmaf(wgt, f[j], acc[j]);
-      }
-    const float inv = 1.f / fmaxf((rw[0] + rw[1] + rw[2]) * (cw[0] + cw[1] + cw[2]), 1.f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] *= inv;
-  }
-  if (a.relu) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = fmaxf(acc[j], 0.f);
-  }
-  *(uint4*)((bf16*)a.y + ((long)(n * a.Ho + oh) * a.Wo + ow) * a.ldy + cg * 8) = pack8(acc);
+  if (t < total) poolk::pool3x3_item<MODE>(a, t);
 }
 
 // Global average pool. One workgroup per (image, 256-channel slab): 8 pixel
@@ -332,8 +271,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(DmlPreprocArgs a) {
 extern "C" int dml_pool(const DmlPoolArgs* a, hipStream_t s) {
   static const bool generic = getenv("DML_POOL_GENERIC") != nullptr;  // A/B switch: the per-tap kernel
   if (a->C % 8 || a->ldx % 8 || a->ldy % 8) { dml_set_error("dml_pool: channels must be %8"); return -1; }
-  const long work = (long)a->N * a->Ho * a->Wo * (a->C / 8);
-  if (!generic && a->k == 3 && a->pad >= 0 && a->pad <= 1 && a->H >= 1 && a->W >= 1 && work < (1L << 31)) {
+  const long work = dml::poolk::pool_work(*a);
+  if (!generic && dml::poolk::pool3x3_fast_ok(*a)) {
     const unsigned blocks = (unsigned)((work + 255) / 256);
     if (a->mode == 0)
       hipLaunchKernelGGL(dml::pool3x3_fast_kernel<0>, dim3(blocks), dim3(256), 0, s, *a, (unsigned)work);

@@ -40,6 +40,17 @@ extern "C" int dml_device_info(int* cus, int* arch_major, int* arch_minor) {
   return 0;
 }
 
+// Argument-struct sizes, in the order of _native.ABI_STRUCTS: the Python
+// bindings refuse a library whose structs do not match their ctypes mirrors.
+extern "C" int dml_abi_sizes(int* out, int n) {
+  const int sz[] = {(int)sizeof(DmlConvArgs), (int)sizeof(DmlPoolArgs), (int)sizeof(DmlConvGroupArgs),
+                    (int)sizeof(DmlPreprocArgs), (int)sizeof(DmlStemArgs), (int)sizeof(DmlIncStemArgs),
+                    (int)sizeof(DmlConvPoolArgs), (int)sizeof(DmlExpandReduceArgs)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
+}
+
 // ----------------------------------------------------------------- plan ----
 namespace {
 enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM, OP_INC_STEM, OP_CONV_POOL, OP_EXP_RED,

@@ -125,6 +125,14 @@ int main() {
   CHECK(std::string(dml_last_error()).find("residual-free") != std::string::npos);
   g.a[1] = conv_args(12, 64, 1, 1);
   CHECK(dml_conv_group(&g, 14, nullptr) != 0);  // every member passes dml_conv's validation
+  g.a[1] = conv_args(64, 64, 1, 1);
+  g.npool = 3;
+  CHECK(dml_conv_group(&g, 14, nullptr) != 0);  // at most DML_GROUP_POOL_MAX pools
+  g.npool = 1;
+  g.pool[0].N = 2; g.pool[0].H = 14; g.pool[0].W = 14; g.pool[0].C = 64; g.pool[0].ldx = 64;
+  g.pool[0].Ho = 14; g.pool[0].Wo = 14; g.pool[0].ldy = 64; g.pool[0].k = 5; g.pool[0].stride = 1; g.pool[0].pad = 2;
+  CHECK(dml_conv_group(&g, 14, nullptr) != 0);  // pool members: 3x3, pad <= 1
+  CHECK(std::string(dml_last_error()).find("pool members") != std::string::npos);
   a = conv_args(8, 64, 3, 3);
   CHECK(dml_conv_pick_cfg(&a) == 15);
   a = conv_args(3, 64, 3, 3);

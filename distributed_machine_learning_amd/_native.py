@@ -34,13 +34,6 @@ class ConvArgs(C.Structure):
     ]
 
 
-GROUP_MAX = 4
-
-
-class ConvGroupArgs(C.Structure):
-    _fields_ = [("n", C.c_int), ("off", C.c_int * (GROUP_MAX + 1)), ("a", ConvArgs * GROUP_MAX)]
-
-
 class PoolArgs(C.Structure):
     _fields_ = [
         ("x", C.c_void_p), ("y", C.c_void_p),
@@ -48,6 +41,15 @@ class PoolArgs(C.Structure):
         ("Ho", C.c_int), ("Wo", C.c_int), ("ldy", C.c_int),
         ("k", C.c_int), ("stride", C.c_int), ("pad", C.c_int), ("mode", C.c_int), ("relu", C.c_int),
     ]
+
+
+GROUP_MAX = 4       # DML_CONV_GROUP_MAX
+GROUP_POOL_MAX = 2  # DML_GROUP_POOL_MAX
+
+
+class ConvGroupArgs(C.Structure):
+    _fields_ = [("n", C.c_int), ("npool", C.c_int), ("off", C.c_int * (GROUP_MAX + GROUP_POOL_MAX + 1)),
+                ("a", ConvArgs * GROUP_MAX), ("pool", PoolArgs * GROUP_POOL_MAX)]
 
 
 class PreprocArgs(C.Structure):
@@ -146,12 +148,31 @@ _SIGS = {
     "dml_memcpy_h2d_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "dml_memcpy_d2h_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "dml_last_error": (C.c_char_p, []),
+    "dml_abi_sizes": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
     "dml_device_info": (C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
 }
 
 
 class NativeError(RuntimeError):
     pass
+
+
+ABI_STRUCTS = ("ConvArgs", "PoolArgs", "ConvGroupArgs", "PreprocArgs", "StemArgs", "IncStemArgs", "ConvPoolArgs",
+               "ExpandReduceArgs")
+
+
+def _check_abi(L) -> None:
+    """The library's argument structs must match their ctypes mirrors byte for byte."""
+    f = getattr(L, "dml_abi_sizes", None)
+    if f is None:
+        return
+    n = len(ABI_STRUCTS)
+    out = (C.c_int * n)()
+    f(out, n)
+    for i, name in enumerate(ABI_STRUCTS):
+        want = C.sizeof(globals()[name])
+        if out[i] != want:
+            raise NativeError(f"ABI mismatch: sizeof(Dml{name}) = {out[i]} in the library, {want} in _native.py")
 
 
 def lib():
@@ -186,6 +207,7 @@ def lib():
                 raise NativeError(f"{path} lacks {name}; rebuild")
             f.restype = res
             f.argtypes = args
+        _check_abi(L)
         _lib = L
         return _lib
 

@@ -249,15 +249,17 @@ class Engine:
             out[e.name] = r
         return out
 
-    def _conv_group_candidates(self) -> List[List[Conv]]:
-        """Runs of consecutive plain convs of one ASAP level (the level order puts
-        them side by side), at most GROUP_MAX per group. Whether a group really
+    def _conv_group_candidates(self) -> List[list]:
+        """Runs of consecutive groupable convs / 3x3 pools of one ASAP level (the
+        level order puts them side by side), at most GROUP_MAX convs and
+        GROUP_POOL_MAX pools per group. Whether a group really
         launches as one grid is decided by timing at plan time (``_build_plan``)."""
         from .optimize import conv_group_runs
 
-        taken = {t.name for t in (self.stem, self.stem_conv2) if t is not None}
-        taken |= set(self.conv_pools) | set(self.exp_red) | {r.name for r in self.exp_red.values()}
-        return conv_group_runs(self.g, taken, N.GROUP_MAX)
+        taken = {t.name for t in (self.stem, self.stem_conv2, self.stem_pool) if t is not None}
+        taken |= set(self.conv_pools) | {p.name for p in self.conv_pools.values()}
+        taken |= set(self.exp_red) | {r.name for r in self.exp_red.values()}
+        return conv_group_runs(self.g, taken, N.GROUP_MAX, N.GROUP_POOL_MAX)
 
     def _subsampled_y(self) -> Dict[str, int]:
         """{tensor: 2} for fused expand+reduce outputs Y whose readers besides the fused
@@ -403,14 +405,16 @@ class Engine:
         # largest member's default tile has a grouped instantiation)
         self.group_cfg: Dict[str, int] = {}
         for grp in self.conv_groups:
-            args = [self._conv_args(m) for m in grp]
-            cfgs = [self.cfg_overrides.get(m.name, self.tuned.get(m.name, -1)) for m in grp]
+            convs = [m for m in grp if not isinstance(m, Pool)]
+            args = [self._conv_args(m) for m in convs]
+            pools = [self._pool_args(m) for m in grp if isinstance(m, Pool)]
+            cfgs = [self.cfg_overrides.get(m.name, self.tuned.get(m.name, -1)) for m in convs]
             if any(m.name in self.cfg_overrides for m in grp):
                 cfg = -1
             elif self.autotune and self.device.type == "cuda":
-                cfg = tuning.autotune_group(args, cfgs)
+                cfg = tuning.autotune_group(args, cfgs, pools)
             else:
-                big = max(range(len(grp)), key=lambda i: args[i].N * args[i].Ho * args[i].Wo * args[i].Cout
+                big = max(range(len(args)), key=lambda i: args[i].N * args[i].Ho * args[i].Wo * args[i].Cout
                           * args[i].Kpad)
                 c = cfgs[big] if cfgs[big] >= 0 else self.lib.dml_conv_pick_cfg(C.byref(args[big]))
                 cfg = c if c in tuning.GROUP_CFGS else -1
@@ -467,9 +471,13 @@ class Engine:
             if n.name in groups:
                 grp, cfg = groups[n.name], self.group_cfg[n.name]
                 ga = N.ConvGroupArgs()
-                ga.n = len(grp)
-                for i, m in enumerate(grp):
+                convs = [m for m in grp if not isinstance(m, Pool)]
+                pools = [m for m in grp if isinstance(m, Pool)]
+                ga.n, ga.npool = len(convs), len(pools)
+                for i, m in enumerate(convs):
                     ga.a[i] = self._conv_args(m)
+                for i, m in enumerate(pools):
+                    ga.pool[i] = self._pool_args(m)
                 N.check(L.dml_plan_add_conv_group(plan, C.byref(ga), cfg), f"plan conv group {n.name}")
                 for m in grp:
                     self.op_cfg[m.name] = cfg
@@ -511,12 +519,7 @@ class Engine:
                 self.op_cfg[n.name] = used
                 self._keep.append(a)
             elif isinstance(n, Pool):
-                h, w, c = g.shape(n.inp)
-                ho, wo, co = g.shape(n.out)
-                y = self.buf[n.out].data_ptr() + 2 * n.out_coff
-                a = N.PoolArgs(self.buf[n.inp].data_ptr(), y, B, h, w, c, self.cbuf[n.inp], ho, wo, self.cbuf[n.out],
-                               n.k, n.stride, n.pad, 0 if n.mode == "max" else 1, int(n.relu))
-                N.check(L.dml_plan_add_pool(plan, C.byref(a)), "plan pool")
+                N.check(L.dml_plan_add_pool(plan, C.byref(self._pool_args(n))), "plan pool")
             elif isinstance(n, GlobalAvgPool):
                 h, w, c = g.shape(n.inp)
                 N.check(L.dml_plan_add_gap(plan, self.buf[n.inp].data_ptr(), self.buf[n.out].data_ptr(),
@@ -528,6 +531,14 @@ class Engine:
                 "plan softmax_top5")
         self.op_names.append("softmax_top5")
         return plan
+
+    def _pool_args(self, n: Pool) -> N.PoolArgs:
+        g = self.g
+        h, w, c = g.shape(n.inp)
+        ho, wo, _ = g.shape(n.out)
+        y = self.buf[n.out].data_ptr() + 2 * n.out_coff
+        return N.PoolArgs(self.buf[n.inp].data_ptr(), y, self.batch, h, w, c, self.cbuf[n.inp], ho, wo,
+                          self.cbuf[n.out], n.k, n.stride, n.pad, 0 if n.mode == "max" else 1, int(n.relu))
 
     def _conv_args(self, n) -> N.ConvArgs:
         g, B = self.g, self.batch

@@ -37,11 +37,12 @@
    weights dict under "<expand>+<shortcut>" (BN folded, ``bn=False``).
 
 5. ``level_order`` — a topological re-order by ASAP level (level = 1 + the
-   deepest writer of any tensor the node reads; concat tensors have several
-   writers). Nodes of one level are mutually independent: InceptionV3's branch
-   convs (5x5 next to 3x3, 1x7 next to 7x1, 1x3 / 3x1 / 3x3) land side by side,
-   residual-free convs first, so the engine can launch each level's convs as
-   ONE grouped grid (dml_conv_group). Pure re-order: outputs are unchanged.
+   deepest writer of any channel range the node reads; concat tensors have
+   several writers). Nodes of one level are mutually independent: InceptionV3's
+   branch convs (5x5 next to 3x3, 1x7 next to 7x1, 1x3 / 3x1 / 3x3) and the
+   pool-branch avg pool / reduction max pool land side by side, groupable nodes
+   first, so the engine can launch each level's convs and 3x3 pools as ONE
+   grouped grid (dml_conv_group). Pure re-order: outputs are unchanged.
 
 Rewrites 1-3 keep the weights dict unchanged (members keep their names); the
 fp32 oracle can execute the rewritten graph too (tests compare both forms).
@@ -245,32 +246,52 @@ def levels(g: Graph) -> Dict[str, int]:
 
 
 def groupable_conv(n) -> bool:
-    """A conv the grouped launch can run: plain (not fused), no residual, bf16 out."""
-    return isinstance(n, Conv) and n.residual is None and not n.out_f32
+    """A conv the grouped launch can run: plain or sibling-fused, no residual, bf16 out."""
+    return isinstance(n, (Conv, FusedConv)) and getattr(n, "residual", None) is None and not getattr(n, "out_f32", False)
+
+
+def groupable_pool(n) -> bool:
+    """A pool the grouped launch can run beside its level's convs (3x3, pad <= 1)."""
+    return isinstance(n, Pool) and n.k == 3 and 0 <= n.pad <= 1
+
+
+def groupable(n) -> bool:
+    return groupable_conv(n) or groupable_pool(n)
 
 
 def level_order(g: Graph) -> Graph:
     lv = levels(g)
     pos = {n.name: i for i, n in enumerate(g.nodes)}
     g = copy.copy(g)
-    g.nodes = sorted(g.nodes, key=lambda n: (lv[n.name], not groupable_conv(n), pos[n.name]))
+    g.nodes = sorted(g.nodes, key=lambda n: (lv[n.name], not groupable(n), pos[n.name]))
     g.validate()
     return g
 
 
-def conv_group_runs(g: Graph, exclude: set = frozenset(), max_members: int = 4) -> List[List[Conv]]:
-    """Runs of >= 2 consecutive groupable convs of one level (not in ``exclude``),
-    at most ``max_members`` each: the members of one grouped launch. Consecutive
-    + same level makes a run independent in any node order."""
+def conv_group_runs(g: Graph, exclude: set = frozenset(), max_convs: int = 4, max_pools: int = 2
+                    ) -> List[List[object]]:
+    """Runs of consecutive groupable nodes of one level (not in ``exclude``): at
+    most ``max_convs`` convs and ``max_pools`` 3x3 pools, at least one conv and two
+    members — the members of one grouped launch. Consecutive + same level makes a
+    run independent in any node order."""
     lv = levels(g)
-    runs: List[List[Conv]] = []
-    run: List[Conv] = []
+    runs: List[List[object]] = []
+    run: List[object] = []
+
+    def flush():
+        if len(run) > 1 and any(groupable_conv(m) for m in run):
+            runs.append(list(run))
+        run.clear()
+
     for n in list(g.nodes) + [None]:
-        ok = n is not None and groupable_conv(n) and n.name not in exclude
-        if run and not (ok and lv[n.name] == lv[run[0].name] and len(run) < max_members):
-            if len(run) > 1:
-                runs.append(run)
-            run = []
+        ok = n is not None and groupable(n) and n.name not in exclude
+        if run and ok:
+            nc = sum(groupable_conv(m) for m in run) + groupable_conv(n)
+            npl = sum(groupable_pool(m) for m in run) + groupable_pool(n)
+            if lv[n.name] != lv[run[0].name] or nc > max_convs or npl > max_pools:
+                flush()
+        elif run:
+            flush()
         if ok:
             run.append(n)
     return runs

@@ -116,18 +116,19 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
     return out
 
 
-def conv_group(args: list, cfg: int) -> None:
+def conv_group(args: list, cfg: int, pools: Optional[list] = None) -> None:
     """Launch up to GROUP_MAX independent convs (ConvArgs from conv2d_nhwc(...,
+    defer=list)) and up to GROUP_POOL_MAX 3x3 pools (PoolArgs from pool3x3(...,
     defer=list)) as ONE grid on tile config ``cfg`` (dml_conv_group)."""
-    g = N.ConvGroupArgs()
-    g.n = len(args)
-    for i, a in enumerate(args):
-        g.a[i] = a
-    N.check(N.lib().dml_conv_group(C.byref(g), cfg, N.stream_ptr()), "dml_conv_group")
+    from .tuning import group_args
+
+    N.check(N.lib().dml_conv_group(C.byref(group_args(args, pools or [])), cfg, N.stream_ptr()), "dml_conv_group")
 
 
 def pool3x3(x: torch.Tensor, mode: str, k: int = 3, stride: int = 2, pad: int = 0,
-            out: Optional[torch.Tensor] = None, out_coff: int = 0, relu: bool = False) -> torch.Tensor:
+            out: Optional[torch.Tensor] = None, out_coff: int = 0, relu: bool = False,
+            defer: Optional[list] = None) -> torch.Tensor:
+    """defer: a list to append the PoolArgs to instead of launching (conv_group)."""
     n, h, w, c = x.shape
     ho = (h + 2 * pad - k) // stride + 1
     wo = (w + 2 * pad - k) // stride + 1
@@ -135,6 +136,9 @@ def pool3x3(x: torch.Tensor, mode: str, k: int = 3, stride: int = 2, pad: int = 
         out = torch.empty((n, ho, wo, c), device=x.device, dtype=torch.bfloat16)
     a = N.PoolArgs(x.data_ptr(), out.data_ptr() + 2 * out_coff, n, h, w, c, c, ho, wo, out.shape[-1], k, stride, pad,
                    0 if mode == "max" else 1, int(relu))
+    if defer is not None:
+        defer.append(a)
+        return out
     N.check(N.lib().dml_pool(C.byref(a), N.stream_ptr()), "dml_pool")
     return out
 

@@ -14,7 +14,7 @@ import ctypes as C
 import json
 import os
 import threading
-from typing import Dict, Iterable, List, Optional, Tuple
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 from .. import _native as N
 
@@ -112,18 +112,25 @@ def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None,
 
 
 # ---------------------------------------------------------- grouped convs --
-GROUP_CFGS = (11, 14, 15, 23, 32)  # tiles with a grouped instantiation (dml_conv_v2_group)
+GROUP_CFGS = (11, 12, 14, 15, 17, 22, 23, 24, 25, 26, 27, 28, 29, 32, 33)  # 4-wave tiles (dml_conv_v2_group)
 
 
-def group_key(args: List[N.ConvArgs]) -> str:
-    return "grp_" + "|".join(shape_key(a)[:-len(CAND_TAG) - 1] for a in args) + "_" + CAND_TAG
+def pool_key(p: N.PoolArgs) -> str:
+    return f"pool{p.mode}_n{p.N}_h{p.H}_w{p.W}_c{p.C}_o{p.Ho}x{p.Wo}_s{p.stride}_p{p.pad}"
 
 
-def group_args(args: List[N.ConvArgs]) -> N.ConvGroupArgs:
+def group_key(args: List[N.ConvArgs], pools: Sequence[N.PoolArgs] = ()) -> str:
+    return ("grp_" + "|".join([shape_key(a)[:-len(CAND_TAG) - 1] for a in args] + [pool_key(p) for p in pools])
+            + "_" + CAND_TAG)
+
+
+def group_args(args: List[N.ConvArgs], pools: Sequence[N.PoolArgs] = ()) -> N.ConvGroupArgs:
     g = N.ConvGroupArgs()
-    g.n = len(args)
+    g.n, g.npool = len(args), len(pools)
     for i, a in enumerate(args):
         g.a[i] = a
+    for i, p in enumerate(pools):
+        g.pool[i] = p
     return g
 
 
@@ -140,11 +147,12 @@ def _time(fn, iters: int) -> float:
     return e0.elapsed_time(e1) / iters
 
 
-def autotune_group(args: List[N.ConvArgs], cfgs: List[int], cache: Optional[Dict[str, int]] = None,
-                   persist: bool = True, iters: int = 20) -> int:
-    """Best tile for launching ``args`` as ONE grouped grid, or -1 when running
-    them one after another, each on its own tuned tile ``cfgs``, is faster."""
-    k = group_key(args)
+def autotune_group(args: List[N.ConvArgs], cfgs: List[int], pools: Sequence[N.PoolArgs] = (),
+                   cache: Optional[Dict[str, int]] = None, persist: bool = True, iters: int = 20) -> int:
+    """Best tile for launching ``args`` (and the 3x3 ``pools``) as ONE grouped
+    grid, or -1 when running them one after another, each conv on its own tuned
+    tile ``cfgs``, is faster."""
+    k = group_key(args, pools)
     cache = load_cache() if cache is None else cache
     if k in cache:
         return cache[k]
@@ -154,8 +162,10 @@ def autotune_group(args: List[N.ConvArgs], cfgs: List[int], cache: Optional[Dict
         def seq():
             for a, c in zip(args, cfgs):
                 N.check(L.dml_conv(C.byref(a), c, s), "conv")
+            for p in pools:
+                N.check(L.dml_pool(C.byref(p), s), "pool")
         best = (_time(seq, iters), -1)
-    g = group_args(args)
+    g = group_args(args, pools)
     for cfg in GROUP_CFGS:
         try:
             t = _time(lambda: N.check(L.dml_conv_group(C.byref(g), cfg, s), "conv group"), iters)

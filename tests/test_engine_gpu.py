@@ -228,7 +228,7 @@ def test_inception_grouped_convs_match_ungrouped(autotune):
                          generator=torch.Generator().manual_seed(1)).cuda()
     eg = Engine(g, w, batch=8, conv_groups=True, autotune=autotune)
     e1 = Engine(g, w, batch=8, conv_groups=False, autotune=autotune)
-    assert len(eg.conv_groups) == 17
+    assert len(eg.conv_groups) == 18
     if not autotune:
         assert len(eg.group_cfg) >= 10 and any("|" in op for op in eg.op_names), eg.group_cfg
     print("grouped launches", len(eg.group_cfg), "of", len(eg.conv_groups), eg.group_cfg)

@@ -352,7 +352,7 @@ GROUP_CASES = [
 
 
 @pytest.mark.parametrize("case", GROUP_CASES)
-@pytest.mark.parametrize("cfg", [11, 14, 15, 23, 32])
+@pytest.mark.parametrize("cfg", [11, 12, 14, 15, 17, 22, 23, 24, 25, 26, 27, 28, 29, 32, 33])
 def test_conv_group_matches_members(case, cfg):
     """dml_conv_group: independent convs (different kh x kw / Cin / Cout, input
     channel slices of one tensor, outputs at channel offsets of one concat
@@ -402,3 +402,39 @@ def test_conv_group_refuses_bad_members():
         ops.conv_group(d, 14)
     with pytest.raises(N.NativeError, match="grouped"):
         ops.conv_group(d[:1], 10)
+
+
+@pytest.mark.parametrize("cfg", [11, 14, 22, 29])
+def test_conv_group_with_pools(cfg):
+    """A grouped grid holding convs AND 3x3 pools (an Inception level: 5x5 + 3x3
+    branch convs + the pool branch's avg pool; a reduction block's 3x3/2 conv +
+    max pool) == the same ops launched one by one, bit-exact."""
+    torch.manual_seed(4)
+    n, h, w = 2, 17, 17
+    x = _bf(torch.randn(n, 64, h, w)).permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
+    pin = _bf(torch.randn(n, 32, h, w)).permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
+    wts = [(_bf(torch.randn(96, 64, k, k) * 0.05), k) for k in (5, 3)]
+    wps = [(ops.pack_weight(wt)[0].cuda(), k) for wt, k in wts]
+    b = torch.randn(96).cuda() * 0.1
+    outs = [torch.full((n, h, w, 96 * 2 + 32 + 8), 3.0, device="cuda", dtype=torch.bfloat16) for _ in range(2)]
+    mp = [torch.zeros(n, 8, 8, 64, device="cuda", dtype=torch.bfloat16) for _ in range(2)]
+    d, dp = [], []
+    for o, (wp, k) in zip((0, 96), wps):
+        ops.conv2d_nhwc(x, wp, b, 96, k, k, pad=(k // 2, k // 2), relu=True, out=outs[0], out_coff=o, cfg=cfg)
+        ops.conv2d_nhwc(x, wp, b, 96, k, k, pad=(k // 2, k // 2), relu=True, out=outs[1], out_coff=o, defer=d)
+    ops.pool3x3(pin, "avg", stride=1, pad=1, out=outs[0], out_coff=192, relu=True)
+    ops.pool3x3(pin, "avg", stride=1, pad=1, out=outs[1], out_coff=192, relu=True, defer=dp)
+    ops.pool3x3(x, "max", stride=2, pad=0, out=mp[0])
+    ops.pool3x3(x, "max", stride=2, pad=0, out=mp[1], defer=dp)
+    ops.conv_group(d, cfg, dp)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(mp[0], mp[1])
+    ref = F.avg_pool2d(pin.float().permute(0, 3, 1, 2), 3, 1, 1, count_include_pad=False).relu()
+    assert _rel(outs[1][..., 192:224].float().permute(0, 3, 1, 2).cpu(), ref.cpu()) < 1e-2
+    assert torch.all(outs[1][..., 224:] == 3.0)
+    from distributed_machine_learning_amd import _native as N
+    bad = list(dp)
+    bad[0].k = 5
+    with pytest.raises(N.NativeError, match="pool members"):
+        ops.conv_group(d, cfg, bad)

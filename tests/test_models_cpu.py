@@ -254,13 +254,16 @@ def test_rewrites_leave_ineligible_graphs_alone():
 
 def test_level_order_and_conv_groups():
     """level_order is a pure topological re-order (fp32 logits bit-identical) that
-    puts InceptionV3's independent branch convs side by side: 17 grouped launches
-    (5x5|3x3, 1x7|7x1, 1x3|3x1|3x3 ...); ResNet50 (a chain, shortcut merged into
-    sliced buffers) has none and keeps its order."""
-    from distributed_machine_learning_amd.models.optimize import (_reads, _writes, conv_group_runs, levels,
-                                                                  level_order, optimize)
+    puts InceptionV3's independent branch convs and 3x3 pools side by side: 18
+    grouped launches (5x5|3x3|avgpool, 1x7|7x1, 1x3|3x1|3x3|avgpool, the
+    reduction blocks' 3x3/2 + max pool ...) holding all 11 mixed-block pools;
+    ResNet50 (a chain, shortcut merged into sliced buffers) has none and keeps its
+    order."""
+    from distributed_machine_learning_amd.models.graph import Pool
+    from distributed_machine_learning_amd.models.optimize import (_reads, _writes, conv_group_runs, groupable_conv,
+                                                                  levels, level_order, optimize)
 
-    for name, n_runs in (("InceptionV3", 17), ("ResNet50", 0)):
+    for name, n_runs in (("InceptionV3", 18), ("ResNet50", 0)):
         g, w = build_model(name, seed=0, calibrate=False)
         w2 = dict(w)
         go = optimize(g, weights=w2)
@@ -277,14 +280,44 @@ def test_level_order_and_conv_groups():
         assert len(runs) == n_runs
         lv = levels(lo)
         for r in runs:
-            assert 2 <= len(r) <= 4 and len({lv[m.name] for m in r}) == 1
+            nc = sum(groupable_conv(m) for m in r)
+            assert 1 <= nc <= 4 and len(r) - nc <= 2 and len(r) >= 2 and len({lv[m.name] for m in r}) == 1
             outs = {wr[0] for m in r for wr in _writes(lo, m)}
             assert not any(m.inp in outs for m in r)  # members read nothing a member writes
         assert conv_group_runs(lo) == conv_group_runs(level_order(lo))  # idempotent
         if name == "ResNet50":
             assert [n.name for n in lo.nodes] == [n.name for n in go.nodes]
+        else:
+            pools = [m.name for r in runs for m in r if isinstance(m, Pool)]
+            assert len(pools) == 11 and all(p.startswith("mixed") for p in pools), pools
         imgs = torch.randint(0, 256, (1, *g.input_hw, 3), dtype=torch.uint8)
         x = preprocess_reference(imgs, g.input_hw, g.preprocess)
         a = OracleExecutor(go, w2).forward(x)["logits"]
         b = OracleExecutor(lo, w2).forward(x)["logits"]
         assert torch.equal(a, b)
+
+
+def test_engine_plan_records_grouped_launches_on_cpu():
+    """The plan builder (host-only: buffers on the CPU, nothing launched) records
+    InceptionV3's 18 grouped launches — 83 plan ops become 53 — and leaves
+    ResNet50's plan as it was."""
+    import pytest
+
+    from distributed_machine_learning_amd import _native as N
+    from distributed_machine_learning_amd.models.engine import Engine
+
+    try:
+        N.lib()
+    except N.NativeError as e:
+        pytest.skip(f"native library unavailable: {e}")
+    g, w = build_model("InceptionV3", seed=0, calibrate=False)
+    eg = Engine(g, w, batch=2, device="cpu", autotune=False)
+    e1 = Engine(g, w, batch=2, device="cpu", autotune=False, conv_groups=False)
+    assert len(eg.conv_groups) == 18 and len(eg.group_cfg) == 18
+    grouped = [o for o in eg.op_names if "|" in o]
+    assert len(grouped) == 18 and len(eg.op_names) == len(e1.op_names) - sum(o.count("|") for o in grouped)
+    assert len(e1.op_names) == 83 and len(eg.op_names) == 53
+    assert sorted(n for o in eg.op_names for n in o.split("|")) == sorted(e1.op_names)
+    g, w = build_model("ResNet50", seed=0, calibrate=False)
+    assert Engine(g, w, batch=2, device="cpu", autotune=False).op_names == \
+        Engine(g, w, batch=2, device="cpu", autotune=False, conv_groups=False).op_names

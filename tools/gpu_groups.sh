@@ -17,3 +17,4 @@ for G in 1 0; do
 done
 timeout -k 10 300 python tools/group_ops.py > gpurun_out/groups/ops.log 2>&1 && tail -25 gpurun_out/groups/ops.log \
   || { tail -30 gpurun_out/groups/ops.log; exit 1; }
+cp distributed_machine_learning_amd/tuning/conv_tuning.json gpurun_out/groups/conv_tuning.json
