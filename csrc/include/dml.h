@@ -170,6 +170,7 @@ int dml_conv_pick_cfg(const DmlConvArgs* a);
 int dml_conv_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s);
 int dml_conv_v2_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s);
 int dml_conv_v2_group_supported(int cfg);
+int dml_conv_v2_bn(int cfg);
 int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);

@@ -16,8 +16,15 @@
 #include "pool_shared.h"
 
 static int validate(const DmlConvArgs* a, int cfg) {
-  if (cfg < 10 || cfg >= 40) {
+  const int bn = (cfg >= 10 && cfg < 40) ? dml_conv_v2_bn(cfg) : 0;
+  if (bn <= 0) {
     dml_set_error("dml_conv: cfg must be a v2 tile config (10..39)");
+    return -1;
+  }
+  // weights are packed with Cout padded to a multiple of 256 rows; a 96- or
+  // 192-wide channel tile must not run past them
+  if ((a->Cout + bn - 1) / bn * bn > (a->Cout + 255) / 256 * 256) {
+    dml_set_error("dml_conv: the channel tiles of this cfg overrun the 256-row weight padding");
     return -1;
   }
   if (a->Cin % 8 || a->ldx % 8 || a->Cout % 8 || a->Kpad % 64 || a->ldy % 8 || (a->res && a->ldr % 8)) {

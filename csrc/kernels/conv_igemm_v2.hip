@@ -355,141 +355,110 @@ static int set_attr() {
 }  // namespace v2
 }  // namespace dml
 
+// Tile configurations: id, BM (pixels), BN (channels), WM x WN waves, ring
+// STAGES, BK. The ids are the ABI of the plan builder and the tuner
+// (ops/tuning.py); validated by dml_conv (conv_dispatch.hip).
+#define DML_V2_TILES(X)                                                                            \
+  X(10, 256, 128, 4, 2, 3, 64)   /* 8 waves, 64x64 per wave */                                     \
+  X(11, 128, 128, 2, 2, 2, 64)   /* 4 waves, 64x64 per wave, 2 blocks/CU */                        \
+  X(12, 256, 64, 4, 1, 2, 64)    /* 4 waves, 64x64 per wave */                                     \
+  X(13, 128, 256, 2, 4, 3, 64)   /* 8 waves, 64x64 per wave */                                     \
+  X(14, 64, 128, 1, 4, 2, 64)    /* 4 waves, 64px x 32ch per wave */                               \
+  X(15, 128, 64, 2, 2, 2, 64)    /* 4 waves, 64px x 32ch per wave */                               \
+  X(16, 256, 128, 4, 2, 2, 64)   /* 8 waves, 2-stage */                                            \
+  X(17, 128, 128, 2, 2, 3, 64)   /* 4 waves, 3-stage */                                            \
+  X(18, 256, 32, 4, 1, 2, 64)    /* 4 waves (Cout = 32 layers) */                                  \
+  X(19, 128, 128, 2, 4, 3, 64)   /* 8 waves, 64px x 32ch per wave, 3-stage */                      \
+  X(20, 128, 128, 4, 2, 3, 64)   /* 8 waves, 32px x 64ch per wave, 3-stage */                      \
+  X(21, 128, 256, 2, 4, 2, 64)   /* 8 waves, 64x64 per wave, 2-stage */                            \
+  X(22, 64, 256, 1, 4, 2, 64)    /* 4 waves, 64px x 64ch per wave */                               \
+  /* BK = 32 (64-B tile rows): half-size stages -> more workgroups per CU */                        \
+  X(23, 64, 128, 1, 4, 2, 32)                                                                      \
+  X(24, 128, 64, 2, 2, 2, 32)                                                                      \
+  X(25, 128, 128, 2, 2, 2, 32)                                                                     \
+  X(26, 64, 128, 1, 4, 3, 32)                                                                      \
+  X(27, 128, 64, 2, 2, 3, 32)                                                                      \
+  X(28, 128, 128, 2, 2, 3, 32)                                                                     \
+  /* deeper rings (the epilogue no longer sets the LDS size: Cfg::EP passes) */                    \
+  X(29, 128, 128, 2, 2, 4, 32)   /* 64 KiB: 2 blocks/CU */                                         \
+  X(30, 256, 128, 4, 2, 3, 32)   /* 8 waves, 72 KiB */                                             \
+  X(31, 128, 256, 2, 4, 3, 32)   /* 8 waves, 72 KiB */                                             \
+  X(32, 64, 128, 1, 4, 3, 64)    /* 72 KiB: 2 blocks/CU */                                         \
+  X(33, 64, 128, 1, 4, 4, 32)    /* 48 KiB: 3 blocks/CU */                                         \
+  /* 256x256: half the L2->LDS bytes per MFMA of 128x128 (the 3x3 layers are L2-bound); its */     \
+  /* residual form spills at 2 waves/SIMD (not a tuner candidate for residual layers) */           \
+  X(34, 256, 256, 2, 4, 3, 32)   /* 8 waves, 128px x 64ch per wave, 96 KiB */                      \
+  X(36, 128, 32, 2, 1, 3, 32)    /* Cout = 32 layers (InceptionV3 stem): 2 waves, 30 KiB */        \
+  X(37, 256, 32, 4, 1, 3, 64)    /* 4 waves, 3-stage */
+// (r2, measured and removed: 192x96 and 192x192 tiles with 64px x 96ch wave
+// tiles for InceptionV3's Cout = 96/160/192 layers won no shape; conv2d_5 156 us
+// vs 147 us on 128x64, profiles/r2_v8/cb_192.log)
+
+// the 4-wave tiles also instantiated as grouped launches (pool members run 256
+// work items per block)
+#define DML_V2_GROUP_TILES(X)                                                                      \
+  X(11, 128, 128, 2, 2, 2, 64) X(12, 256, 64, 4, 1, 2, 64) X(14, 64, 128, 1, 4, 2, 64)             \
+  X(15, 128, 64, 2, 2, 2, 64) X(17, 128, 128, 2, 2, 3, 64) X(22, 64, 256, 1, 4, 2, 64)             \
+  X(23, 64, 128, 1, 4, 2, 32) X(24, 128, 64, 2, 2, 2, 32) X(25, 128, 128, 2, 2, 2, 32)             \
+  X(26, 64, 128, 1, 4, 3, 32) X(27, 128, 64, 2, 2, 3, 32) X(28, 128, 128, 2, 2, 3, 32)             \
+  X(29, 128, 128, 2, 2, 4, 32) X(32, 64, 128, 1, 4, 3, 64) X(33, 64, 128, 1, 4, 4, 32)
+
 // Raise the dynamic-LDS limit of every v2 instantiation once (before any
 // launch or graph capture). Called by the Python loader.
 extern "C" int dml_conv_v2_init(void) {
   using namespace dml::v2;
   int rc = 0;
-  rc |= set_attr<256, 128, 4, 2, 3>();
-  rc |= set_attr<128, 128, 2, 2, 2>();
-  rc |= set_attr<256, 64, 4, 1, 2>();
-  rc |= set_attr<128, 256, 2, 4, 3>();
-  rc |= set_attr<64, 128, 1, 4, 2>();
-  rc |= set_attr<128, 64, 2, 2, 2>();
-  rc |= set_attr<256, 128, 4, 2, 2>();
-  rc |= set_attr<128, 128, 2, 2, 3>();
-  rc |= set_attr<256, 32, 4, 1, 2>();
-  rc |= set_attr<128, 128, 2, 4, 3>();
-  rc |= set_attr<128, 128, 4, 2, 3>();
-  rc |= set_attr<128, 256, 2, 4, 2>();
-  rc |= set_attr<64, 256, 1, 4, 2>();
-  rc |= set_attr<64, 128, 1, 4, 2, 32>();
-  rc |= set_attr<128, 64, 2, 2, 2, 32>();
-  rc |= set_attr<128, 128, 2, 2, 2, 32>();
-  rc |= set_attr<64, 128, 1, 4, 3, 32>();
-  rc |= set_attr<128, 64, 2, 2, 3, 32>();
-  rc |= set_attr<128, 128, 2, 2, 3, 32>();
-  rc |= set_attr<128, 128, 2, 2, 4, 32>();
-  rc |= set_attr<256, 128, 4, 2, 3, 32>();
-  rc |= set_attr<128, 256, 2, 4, 3, 32>();
-  rc |= set_attr<64, 128, 1, 4, 3>();
-  rc |= set_attr<64, 128, 1, 4, 4, 32>();
-  rc |= set_attr<256, 256, 2, 4, 3, 32>();
-  rc |= set_attr<128, 32, 2, 1, 3, 32>();
-  rc |= set_attr<256, 32, 4, 1, 3, 64>();
-  rc |= set_attr_group<128, 128, 2, 2, 2>();
-  rc |= set_attr_group<256, 64, 4, 1, 2>();
-  rc |= set_attr_group<64, 128, 1, 4, 2>();
-  rc |= set_attr_group<128, 64, 2, 2, 2>();
-  rc |= set_attr_group<128, 128, 2, 2, 3>();
-  rc |= set_attr_group<64, 256, 1, 4, 2>();
-  rc |= set_attr_group<64, 128, 1, 4, 2, 32>();
-  rc |= set_attr_group<128, 64, 2, 2, 2, 32>();
-  rc |= set_attr_group<128, 128, 2, 2, 2, 32>();
-  rc |= set_attr_group<64, 128, 1, 4, 3, 32>();
-  rc |= set_attr_group<128, 64, 2, 2, 3, 32>();
-  rc |= set_attr_group<128, 128, 2, 2, 3, 32>();
-  rc |= set_attr_group<128, 128, 2, 2, 4, 32>();
-  rc |= set_attr_group<64, 128, 1, 4, 3>();
-  rc |= set_attr_group<64, 128, 1, 4, 4, 32>();
+#define DML_SET(id, BM, BN, WM, WN, ST, BK) rc |= set_attr<BM, BN, WM, WN, ST, BK>();
+  DML_V2_TILES(DML_SET)
+#undef DML_SET
+#define DML_SET(id, BM, BN, WM, WN, ST, BK) rc |= set_attr_group<BM, BN, WM, WN, ST, BK>();
+  DML_V2_GROUP_TILES(DML_SET)
+#undef DML_SET
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   if (!rc && dml_expand_reduce_init() != 0) return -1;  // fused block-boundary kernels (bottleneck_fused.hip)
   return rc ? -1 : 0;
 }
 
-// tile configurations (ids 10..39; validated by dml_conv in conv_dispatch.hip)
 extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
   using namespace dml::v2;
   switch (cfg) {
-    case 10: return launch<256, 128, 4, 2, 3>(a, s);  // 8 waves, 64x64 per wave
-    case 11: return launch<128, 128, 2, 2, 2>(a, s);  // 4 waves, 64x64 per wave, 2 blocks/CU
-    case 12: return launch<256, 64, 4, 1, 2>(a, s);   // 4 waves, 64x64 per wave
-    case 13: return launch<128, 256, 2, 4, 3>(a, s);  // 8 waves, 64x64 per wave
-    case 14: return launch<64, 128, 1, 4, 2>(a, s);   // 4 waves, 64px x 32ch per wave
-    case 15: return launch<128, 64, 2, 2, 2>(a, s);   // 4 waves, 64px x 32ch per wave
-    case 16: return launch<256, 128, 4, 2, 2>(a, s);  // 8 waves, 2-stage
-    case 17: return launch<128, 128, 2, 2, 3>(a, s);  // 4 waves, 3-stage
-    case 18: return launch<256, 32, 4, 1, 2>(a, s);   // 4 waves, 64px x 32ch per wave (Cout = 32 layers)
-    case 19: return launch<128, 128, 2, 4, 3>(a, s);  // 8 waves, 64px x 32ch per wave, 3-stage
-    case 20: return launch<128, 128, 4, 2, 3>(a, s);  // 8 waves, 32px x 64ch per wave, 3-stage
-    case 21: return launch<128, 256, 2, 4, 2>(a, s);  // 8 waves, 64x64 per wave, 2-stage
-    case 22: return launch<64, 256, 1, 4, 2>(a, s);   // 4 waves, 64px x 64ch per wave
-    // BK = 32 (64-B tile rows): half-size stages -> more workgroups per CU
-    case 23: return launch<64, 128, 1, 4, 2, 32>(a, s);
-    case 24: return launch<128, 64, 2, 2, 2, 32>(a, s);
-    case 25: return launch<128, 128, 2, 2, 2, 32>(a, s);
-    case 26: return launch<64, 128, 1, 4, 3, 32>(a, s);
-    case 27: return launch<128, 64, 2, 2, 3, 32>(a, s);
-    case 28: return launch<128, 128, 2, 2, 3, 32>(a, s);
-    // deeper rings (the epilogue no longer sets the LDS size: Cfg::EP passes)
-    case 29: return launch<128, 128, 2, 2, 4, 32>(a, s);  // 64 KiB: 2 blocks/CU
-    case 30: return launch<256, 128, 4, 2, 3, 32>(a, s);  // 8 waves, 72 KiB
-    case 31: return launch<128, 256, 2, 4, 3, 32>(a, s);  // 8 waves, 72 KiB
-    case 32: return launch<64, 128, 1, 4, 3>(a, s);       // 72 KiB: 2 blocks/CU
-    case 33: return launch<64, 128, 1, 4, 4, 32>(a, s);   // 48 KiB: 3 blocks/CU
-    // 256x256: half the L2->LDS bytes per MFMA of 128x128 (the 3x3 layers are L2-bound)
-    case 34: return launch<256, 256, 2, 4, 3, 32>(a, s);  // 8 waves, 128px x 64ch per wave, 96 KiB
-    // (256x256 BK64 and the residual form of 34 spill at 2 waves/SIMD: not tuner candidates for residual layers)
-    // Cout = 32 layers (InceptionV3 stem)
-    case 36: return launch<128, 32, 2, 1, 3, 32>(a, s);   // 2 waves, 30 KiB
-    case 37: return launch<256, 32, 4, 1, 3, 64>(a, s);   // 4 waves, 3-stage
+#define DML_CASE(id, BM, BN, WM, WN, ST, BK) \
+  case id: return launch<BM, BN, WM, WN, ST, BK>(a, s);
+    DML_V2_TILES(DML_CASE)
+#undef DML_CASE
     default: dml_set_error("dml_conv_v2: bad cfg"); return -1;
   }
 }
 
-// Grouped launch of independent convs (cfg: the tile config every member uses;
-// instantiated for every 4-wave tile, the block size the pool members assume).
+// channel-tile width of a config (0: not a config)
+extern "C" int dml_conv_v2_bn(int cfg) {
+  switch (cfg) {
+#define DML_CASE(id, BM, BN, WM, WN, ST, BK) \
+  case id: return BN;
+    DML_V2_TILES(DML_CASE)
+#undef DML_CASE
+    default: return 0;
+  }
+}
+
+// Grouped launch of independent convs (cfg: the tile config every member uses).
 extern "C" int dml_conv_v2_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s) {
   using namespace dml::v2;
   switch (cfg) {
-    case 11: return launch_group<128, 128, 2, 2, 2>(g, s);
-    case 12: return launch_group<256, 64, 4, 1, 2>(g, s);
-    case 14: return launch_group<64, 128, 1, 4, 2>(g, s);
-    case 15: return launch_group<128, 64, 2, 2, 2>(g, s);
-    case 17: return launch_group<128, 128, 2, 2, 3>(g, s);
-    case 22: return launch_group<64, 256, 1, 4, 2>(g, s);
-    case 23: return launch_group<64, 128, 1, 4, 2, 32>(g, s);
-    case 24: return launch_group<128, 64, 2, 2, 2, 32>(g, s);
-    case 25: return launch_group<128, 128, 2, 2, 2, 32>(g, s);
-    case 26: return launch_group<64, 128, 1, 4, 3, 32>(g, s);
-    case 27: return launch_group<128, 64, 2, 2, 3, 32>(g, s);
-    case 28: return launch_group<128, 128, 2, 2, 3, 32>(g, s);
-    case 29: return launch_group<128, 128, 2, 2, 4, 32>(g, s);
-    case 32: return launch_group<64, 128, 1, 4, 3>(g, s);
-    case 33: return launch_group<64, 128, 1, 4, 4, 32>(g, s);
+#define DML_CASE(id, BM, BN, WM, WN, ST, BK) \
+  case id: return launch_group<BM, BN, WM, WN, ST, BK>(g, s);
+    DML_V2_GROUP_TILES(DML_CASE)
+#undef DML_CASE
     default: dml_set_error("dml_conv_group: cfg has no grouped instantiation (the 4-wave tiles)"); return -1;
   }
 }
 
 extern "C" int dml_conv_v2_group_supported(int cfg) {
   switch (cfg) {
-    case 11:
-    case 12:
-    case 14:
-    case 15:
-    case 17:
-    case 22:
-    case 23:
-    case 24:
-    case 25:
-    case 26:
-    case 27:
-    case 28:
-    case 29:
-    case 32:
-    case 33:
-      return 1;
-    default:
-      return 0;
+#define DML_CASE(id, BM, BN, WM, WN, ST, BK) \
+  case id: return 1;
+    DML_V2_GROUP_TILES(DML_CASE)
+#undef DML_CASE
+    default: return 0;
   }
 }

@@ -96,6 +96,7 @@ int main() {
   CHECK(dml_conv(&a, 0, nullptr) != 0);
   a = conv_args(64, 64, 3, 3);
   CHECK(dml_conv(&a, 99, nullptr) != 0);        // unknown config
+  CHECK(dml_conv(&a, 35, nullptr) != 0);        // an unassigned id inside 10..39
   CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
   a.nseg = 5;
   CHECK(dml_conv(&a, 11, nullptr) != 0);        // too many output segments

@@ -438,3 +438,4 @@ def test_conv_group_with_pools(cfg):
     bad[0].k = 5
     with pytest.raises(N.NativeError, match="pool members"):
         ops.conv_group(d, cfg, bad)
+
