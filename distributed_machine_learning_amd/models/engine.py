@@ -598,6 +598,22 @@ class Engine:
         else:
             N.check(self.lib.dml_plan_run(plan, s), "plan run")
 
+    def capture(self, stream=None) -> None:
+        """Capture every source slot's forward as a hipGraph NOW, on a private
+        stream with the device idle. Serving loops call this before their first
+        collective: a capture begun later, while RCCL work is in flight, can meet
+        the process-group watchdog querying an event on a capturing stream
+        (hipErrorCapturedEvent; seen with 8 sub-batch engines in the bench)."""
+        if all(self.graph_captured):
+            return
+        torch.cuda.synchronize(self.device)
+        s = stream if stream is not None else torch.cuda.Stream(self.device)
+        for slot in range(self.src_slots):
+            if not self.graph_captured[slot]:
+                N.check(self.lib.dml_plan_capture(self.plans[slot], N.stream_ptr(s)), "plan capture")
+                self.graph_captured[slot] = True
+        torch.cuda.synchronize(self.device)
+
     def capture_parts(self, bounds: List[int], stream=None, slot: int = 0) -> None:
         """Capture the forward of source slot ``slot`` as len(bounds)-1 graphs over
         op ranges [bounds[i], bounds[i+1]) (op indices as in ``op_names``)."""
@@ -683,6 +699,12 @@ class SplitEngine:
     @property
     def op_cfg(self) -> Dict[str, int]:
         return self.engines[0].op_cfg
+
+    def capture(self, stream=None) -> None:
+        """Capture every sub-batch engine's graphs now (Engine.capture)."""
+        s = stream if stream is not None else torch.cuda.Stream(self.device)
+        for e in self.engines:
+            e.capture(s)
 
     def _select_result(self, slot: int) -> None:
         self.result = self.results[slot]

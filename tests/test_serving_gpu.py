@@ -42,21 +42,25 @@ def rccl_world1(monkeypatch):
         dist.destroy_process_group()
 
 
-def _split_ref(g, w, imgs, half):
-    """Engine(batch=half) on each half of imgs -> packed [2, 2*half, 5] (the
-    SplitEngine reference used by test_engine_gpu)."""
+def _split_ref(g, w, imgs, half, parts=2):
+    """Engine(batch=half) on each of the ``parts`` slices of imgs -> packed
+    [2, parts*half, 5] (the SplitEngine reference used by test_engine_gpu)."""
     from distributed_machine_learning_amd.models.engine import Engine
 
     e = Engine(g, w, batch=half)
     out = []
-    for h in range(2):
+    for h in range(parts):
         e.infer(imgs[h * half:(h + 1) * half].cuda())
         torch.cuda.synchronize()
         out.append(e.result.clone().cpu())
     return torch.cat(out, dim=1)
 
 
-def test_serving_pipeline_matches_engine(rccl_world1):
+@pytest.mark.parametrize("splits,streams", [(2, 0), (8, 2)])
+def test_serving_pipeline_matches_engine(rccl_world1, splits, streams):
+    """splits 8 on 2 streams: eight graph captures; captured lazily inside the
+    loop they once met the RCCL watchdog querying an event on a capturing stream
+    (hipErrorCapturedEvent), hence Engine.capture() before the first collective."""
     from distributed_machine_learning_amd.models import build_model
     from distributed_machine_learning_amd.models.engine import SplitEngine
     from distributed_machine_learning_amd.parallel.dataplane import DESC_FIELDS, DataPlane, init_process_group
@@ -67,7 +71,7 @@ def test_serving_pipeline_matches_engine(rccl_world1):
     dev = torch.device("cuda", local)
     B, steps = 16, 6
     g, w = build_model("ResNet50", seed=0)
-    eng = SplitEngine(g, w, batch=B, device=str(dev), src_slots=2, splits=2)
+    eng = SplitEngine(g, w, batch=B, device=str(dev), src_slots=2, splits=splits, streams=streams)
     store = PinnedImageStore(capacity=steps * B, hw=g.input_hw)
     store.fill_synthetic(seed=3)
     dp = DataPlane(dev, result_shape=(2, B, 5))
@@ -82,7 +86,7 @@ def test_serving_pipeline_matches_engine(rccl_world1):
     pipe.run(steps, table)
     assert sorted(got) == list(range(steps))
     for k in range(steps):
-        ref = _split_ref(g, w, torch.from_numpy(store.array[k * B:(k + 1) * B].copy()), B // 2)
+        ref = _split_ref(g, w, torch.from_numpy(store.array[k * B:(k + 1) * B].copy()), B // splits, splits)
         assert torch.equal(got[k], ref), f"step {k} differs"
 
 
