@@ -38,6 +38,7 @@ def main():
         y = torch.empty(n, hw, hw, cout, device="cuda", dtype=torch.bfloat16)
         nbytes = x.numel() * 2 + y.numel() * 2 + (r.numel() * 2 if res else 0)
         best = None
+        per = {}
         for cfg in tuning.V2_CFGS:
             if res and cfg in tuning.NO_RES_CFGS:
                 continue
@@ -45,6 +46,7 @@ def main():
                 flush.zero_()
                 ops.conv2d_nhwc(x, wp, b, cout, 1, 1, residual=r, out=y, relu=True, cfg=cfg)
             t = timeit(run) - timeit(lambda: flush.zero_())
+            per[cfg] = round(t * 1e3, 1)
             best = min(best or (t, cfg), (t, cfg))
         src = torch.empty(nbytes // 4, dtype=torch.uint8, device="cuda")
         dst = torch.empty_like(src)
@@ -54,7 +56,7 @@ def main():
         tcopy = timeit(cp) - timeit(lambda: flush.zero_())  # copy of half the bytes read + written = nbytes/2 moved
         row = {"shape": f"{hw}x{hw} {cin}->{cout}{' +res' if res else ''}", "MB": round(nbytes / 1e6, 1),
                "conv_us": round(best[0] * 1e3, 1), "cfg": best[1], "conv_TBs": round(nbytes / best[0] / 1e9, 2),
-               "copy_TBs": round(nbytes / 2 / tcopy / 1e9, 2)}
+               "copy_TBs": round(nbytes / 2 / tcopy / 1e9, 2), "us_per_cfg": per}
         print(json.dumps(row), flush=True)
         rows.append(row)
     os.makedirs("gpurun_out", exist_ok=True)
