@@ -3,7 +3,7 @@
 //
 // Serves every convolution of ResNet50 / InceptionV3 and the FC layer
 // (SURVEY §2.7 "conv_igemm_bf16"; the reference runs these inside Keras,
-// models.py:26,51 — it has no kernel of its own). cfg ids 10..39 select a v2
+// models.py:26,51 — it has no kernel of its own). cfg ids 10..63 select a v2
 // tile configuration (dml_conv_v2); they are part of the ABI the plan builder
 // and the autotuner (ops/tuning.py) use.
 //
@@ -16,9 +16,9 @@
 #include "pool_shared.h"
 
 static int validate(const DmlConvArgs* a, int cfg) {
-  const int bn = (cfg >= 10 && cfg < 40) ? dml_conv_v2_bn(cfg) : 0;
+  const int bn = (cfg >= 10 && cfg < 64) ? dml_conv_v2_bn(cfg) : 0;
   if (bn <= 0) {
-    dml_set_error("dml_conv: cfg must be a v2 tile config (10..39)");
+    dml_set_error("dml_conv: cfg must be a v2 tile config (10..63)");
     return -1;
   }
   // weights are packed with Cout padded to a multiple of 256 rows; a 96- or

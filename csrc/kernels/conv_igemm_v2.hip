@@ -392,7 +392,10 @@ static int set_attr() {
   X(37, 256, 32, 4, 1, 3, 64)    /* 4 waves, 3-stage */
 // (r2, measured and removed: 192x96 and 192x192 tiles with 64px x 96ch wave
 // tiles for InceptionV3's Cout = 96/160/192 layers won no shape; conv2d_5 156 us
-// vs 147 us on 128x64, profiles/r2_v8/cb_192.log)
+// vs 147 us on 128x64, profiles/r2_v8/cb_192.log. Deep BK64 rings (4-5 stages,
+// 96-160 KiB, 1 workgroup/CU) for the long-K stage-4/5 layers were 1.3-1.9x
+// slower than the 2-3 workgroups/CU tiles: co-resident workgroups hide the L2
+// latency better than a deeper ring, profiles/r2_v11/cb_r50.log)
 
 // the 4-wave tiles also instantiated as grouped launches (pool members run 256
 // work items per block)
@@ -432,6 +435,7 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
 
 // channel-tile width of a config (0: not a config)
 extern "C" int dml_conv_v2_bn(int cfg) {
+  if (cfg < 10 || cfg > 63) return 0;
   switch (cfg) {
 #define DML_CASE(id, BM, BN, WM, WN, ST, BK) \
   case id: return BN;

@@ -118,7 +118,7 @@ extern "C" int dml_plan_add_conv(void* p, const DmlConvArgs* a, int cfg) {
   o.kind = OP_CONV;
   o.conv = *a;
   o.cfg = cfg < 0 ? dml_conv_pick_cfg(a) : cfg;
-  if (o.cfg < 10 || o.cfg >= 40) { g_err = "dml_plan_add_conv: no tile config for this conv"; return -1; }
+  if (dml_conv_v2_bn(o.cfg) <= 0) { g_err = "dml_plan_add_conv: no tile config for this conv"; return -1; }
   ((Plan*)p)->ops.push_back(o);
   return o.cfg;
 }
@@ -259,7 +259,7 @@ extern "C" int dml_plan_set_cfg(void* p, int i, int cfg) {
   Plan* pl = (Plan*)p;
   if (i < 0 || i >= (int)pl->ops.size() || pl->ops[i].kind != OP_CONV) { g_err = "dml_plan_set_cfg: not a conv op"; return -1; }
   Op& o = pl->ops[i];
-  if (cfg < 10 || cfg >= 40) { g_err = "dml_plan_set_cfg: not a tile config"; return -1; }
+  if (dml_conv_v2_bn(cfg) <= 0) { g_err = "dml_plan_set_cfg: not a tile config"; return -1; }
   const int prev = o.cfg;
   o.cfg = cfg;
   return prev;

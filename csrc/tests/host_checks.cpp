@@ -96,7 +96,8 @@ int main() {
   CHECK(dml_conv(&a, 0, nullptr) != 0);
   a = conv_args(64, 64, 3, 3);
   CHECK(dml_conv(&a, 99, nullptr) != 0);        // unknown config
-  CHECK(dml_conv(&a, 35, nullptr) != 0);        // an unassigned id inside 10..39
+  CHECK(dml_conv(&a, 35, nullptr) != 0);        // an unassigned id inside 10..63
+  CHECK(dml_conv(&a, 64, nullptr) != 0);        // past the table
   CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
   a.nseg = 5;
   CHECK(dml_conv(&a, 11, nullptr) != 0);        // too many output segments
@@ -108,7 +109,7 @@ int main() {
   a.out_f32 = 1; a.relu = 1;
   CHECK(dml_conv(&a, 14, nullptr) != 0);        // ... and no ReLU
   a.relu = 0;
-  CHECK(dml_conv(&a, 40, nullptr) != 0);        // ... and a tile config (10..39)
+  CHECK(dml_conv(&a, 40, nullptr) != 0);        // ... and a tile config
   CHECK(dml_conv(&a, 2, nullptr) != 0);
   a = conv_args(64, 64, 3, 3);
   a.kchunk = 32;

@@ -337,7 +337,7 @@ def test_conv_non_tile_config_refused():
     shapes no tile config can run fail loudly on the host."""
     x = torch.zeros(1, 4, 4, 64, device="cuda", dtype=torch.bfloat16)
     wp, _, _ = ops.pack_weight(torch.zeros(64, 64, 1, 1))
-    for cfg in (0, 4, 40):
+    for cfg in (0, 4, 35, 40, 64):
         with pytest.raises(Exception):
             ops.conv2d_nhwc(x, wp.cuda(), torch.zeros(64), 64, 1, 1, cfg=cfg)
 
