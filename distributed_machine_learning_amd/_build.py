@@ -31,7 +31,7 @@ SOURCES = [
     CSRC / "kernels" / "bottleneck_fused.hip",
     CSRC / "runtime" / "runtime.hip",
 ]
-HEADERS = [CSRC / "include" / "dml.h", CSRC / "kernels" / "common.h", CSRC / "kernels" / "conv_shared.h"]
+HEADERS = [CSRC / "include" / "dml.h"] + sorted((CSRC / "kernels").glob("*.h"))  # every header the stamp covers
 
 
 def _hipcc() -> str:
