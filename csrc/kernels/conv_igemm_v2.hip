@@ -294,13 +294,35 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_group_kernel(DmlConvGroup
     }
     return;
   }
-  const int L = xcd_remap(b, nconv);  // conv tiles: XCD-aware over their own range
-  int i = 0;
+  // Conv tiles: every member is cut into 8 contiguous chunks, one per XCD
+  // (block b runs on XCD b % 8), the members' remainder tiles rotating over the
+  // XCDs so each XCD gets exactly its share of blocks. On each XCD the members
+  // come in host order — longest K first (launch_group) — so the long tiles are
+  // dispatched first (longest-processing-time order) and no XCD is left with
+  // only the short member's tiles.
+  const int x = b & 7;
+  int j = b >> 3, i = 0, tile = 0, rot = 0;
+  bool found = false;
 #pragma unroll
-  for (int q = 1; q < DML_CONV_GROUP_MAX; ++q)
-    if (q < g.n && L >= g.off[q]) i = q;
+  for (int q = 0; q < DML_CONV_GROUP_MAX; ++q) {
+    if (q < g.n && !found) {
+      const int t = g.off[q + 1] - g.off[q], qd = t >> 3, r = t & 7;
+      const int cnt = qd + (((x - rot) & 7) < r ? 1 : 0);
+      if (j < cnt) {
+        int before = 0;  // XCDs before x holding one of this member's remainder tiles
+        for (int k = 0; k < x; ++k) before += (((k - rot) & 7) < r) ? 1 : 0;
+        i = q;
+        tile = x * qd + before + j;
+        found = true;
+      } else {
+        j -= cnt;
+      }
+      rot = (rot + r) & 7;
+    }
+  }
   i = __builtin_amdgcn_readfirstlane(i);
-  conv_v2_tile<BM, BN, WM, WN, STAGES, false, BK>(g.a[i], L - g.off[i], g.off[i + 1] - g.off[i]);
+  tile = __builtin_amdgcn_readfirstlane(tile);
+  conv_v2_tile<BM, BN, WM, WN, STAGES, false, BK>(g.a[i], tile, g.off[i + 1] - g.off[i]);
 }
 
 template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
@@ -323,6 +345,13 @@ static int launch_group(const DmlConvGroupArgs* g, hipStream_t s) {
   using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
   static_assert(T::NT == 256, "pool members run 256 work items per block");
   DmlConvGroupArgs h = *g;
+  // longest K first: the kernel dispatches each XCD's tiles in member order
+  for (int i = 1; i < h.n; ++i)
+    for (int k = i; k > 0 && h.a[k].Kpad > h.a[k - 1].Kpad; --k) {
+      const DmlConvArgs t = h.a[k];
+      h.a[k] = h.a[k - 1];
+      h.a[k - 1] = t;
+    }
   h.off[0] = 0;
   for (int i = 0; i < h.n; ++i) {
     const long M = (long)h.a[i].N * h.a[i].Ho * h.a[i].Wo;

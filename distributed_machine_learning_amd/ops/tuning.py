@@ -119,8 +119,11 @@ def pool_key(p: N.PoolArgs) -> str:
     return f"pool{p.mode}_n{p.N}_h{p.H}_w{p.W}_c{p.C}_o{p.Ho}x{p.Wo}_s{p.stride}_p{p.pad}"
 
 
+GROUP_TAG = "grp2"  # bumped when the grouped kernel's block schedule changes (r2: XCD-balanced LPT order)
+
+
 def group_key(args: List[N.ConvArgs], pools: Sequence[N.PoolArgs] = ()) -> str:
-    return ("grp_" + "|".join([shape_key(a)[:-len(CAND_TAG) - 1] for a in args] + [pool_key(p) for p in pools])
+    return (GROUP_TAG + "_" + "|".join([shape_key(a)[:-len(CAND_TAG) - 1] for a in args] + [pool_key(p) for p in pools])
             + "_" + CAND_TAG)
 
 
