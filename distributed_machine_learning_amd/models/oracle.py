@@ -8,7 +8,7 @@ reference models.py:34-38 / 59-63).
 """
 from __future__ import annotations
 
-from typing import Dict, Optional
+from typing import Dict
 
 import numpy as np
 import torch

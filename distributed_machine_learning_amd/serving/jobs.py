@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import itertools
 from collections import deque
-from dataclasses import asdict, dataclass, field
+from dataclasses import asdict, dataclass
 from typing import Deque, Dict, List, Optional
 
 MODELS = ("ResNet50", "InceptionV3")

@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import fnmatch
 import hashlib
-from typing import Dict, Iterable, List, Optional, Set, Tuple
+from typing import Dict, Iterable, List, Optional, Tuple
 
 REPLICATION_FACTOR = 4
 WAITING, SUCCESS, FAILED = "Waiting", "Success", "Failed"

@@ -18,7 +18,6 @@ pytestmark = pytest.mark.gpu
 from distributed_machine_learning_amd import ops  # noqa: E402
 from distributed_machine_learning_amd.models import build_model  # noqa: E402
 from distributed_machine_learning_amd.models.engine import Engine, _r, pack_conv_weight  # noqa: E402
-from distributed_machine_learning_amd.models.graph import Conv  # noqa: E402
 from distributed_machine_learning_amd.models.oracle import OracleExecutor, preprocess_reference  # noqa: E402
 from distributed_machine_learning_amd.models.weights import fold_conv  # noqa: E402
 
