@@ -67,7 +67,7 @@ class ServingPipeline:
         B = engine.batch
         self.host_res = [torch.empty((dp.world, 2, B, 5), dtype=torch.int32, pin_memory=True) for _ in range(2)]
         if use_graph and hasattr(engine, "capture"):
-            engine.capture()  # every graph before the first collective (Engine.capture)
+            engine.capture(self.compute_stream)  # every graph before the first collective (Engine.capture)
         self.stats = PipelineStats()
 
     def _stage(self, step: int, row: np.ndarray) -> None:

@@ -219,7 +219,7 @@ class GpuRankBackend(RankBackend):
                 self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=2)
             self.arenas[m] = HbmImageStore(max(arena_images, n_synth + 2 * self.cap), g.input_hw, device,
                                            n_synth=n_synth, seed=1000 + MODEL_IDS[m])
-            self.engines[m].capture()  # graphs now, before the service's first collective
+            self.engines[m].capture(self.stream)  # graphs now, before the service's first collective
         self.out = [torch.zeros((2, self.cap, 5), dtype=torch.int32, device=device) for _ in range(2)]
         self.ev_done = [torch.cuda.Event() for _ in range(2)]
 

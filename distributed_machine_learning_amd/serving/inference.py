@@ -153,7 +153,7 @@ class GpuBackend(Backend):
                 g, w = self._models[model]
                 self._engines[key] = Engine(g, w, batch=b, device=self.device)
                 if self.use_graph:
-                    self._engines[key].capture()
+                    self._engines[key].capture(self.stream)
                 hw = g.input_hw
                 self._stage[key] = (torch.empty((b, hw[0], hw[1], 3), dtype=torch.uint8).pin_memory(),
                                     torch.empty((2, b, 5), dtype=torch.int32).pin_memory(), torch.cuda.Event())
