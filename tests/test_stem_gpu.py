@@ -34,6 +34,7 @@ def _rel(a, b):
     (2, 224, 224, (224, 224), "caffe"),   # the ResNet50 shape (56x56 pool grid = 8x7 full blocks)
     (3, 300, 169, (224, 224), "caffe"),   # reference testfiles/ JPEG sizes: nearest resize in the patch fill
     (2, 64, 80, (61, 47), "tf"),          # partial blocks at the bottom/right edges
+    (2, 61, 47, (61, 47), "tf"),          # identity resize (16-B pair loads) with partial edge blocks
     (1, 20, 20, (9, 9), "caffe"),         # image smaller than one block
 ])
 def test_fused_stem_matches_fp32(n, hs, ws, out_hw, mode):
@@ -82,6 +83,7 @@ def test_engine_fused_stem_equals_unfused():
     (2, 299, 299, (299, 299), "tf"),      # the InceptionV3 shape (147x147 conv2 grid, partial edge tiles)
     (2, 300, 169, (299, 299), "tf"),      # nearest resize from a reference testfiles/ JPEG size
     (1, 50, 60, (41, 39), "caffe"),       # small odd image, several partial tiles
+    (3, 41, 39, (41, 39), "caffe"),       # identity resize (16-B pair loads), odd width
 ])
 def test_fused_inception_stem_matches_fp32(n, hs, ws, out_hw, mode):
     torch.manual_seed(1)
