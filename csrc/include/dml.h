@@ -53,11 +53,6 @@ typedef struct {
   // stride rsub from its full-resolution grid (rW = its width, rHW = H*W), used
   // when a stride-2 consumer has been pushed up into the block (models/optimize.py).
   int rsub, rW, rHW;
-  // K order (v2 kernels only): 0 = (r, s, c); kchunk > 0 (Cin % kchunk == 0,
-  // kchunk % BK == 0) = (c / kchunk, r, s, c % kchunk) — consecutive K tiles are
-  // the taps of one channel chunk, so a 3x3's shifted pixel rows are re-read
-  // while still in the CU's L1 instead of once per tap from L2.
-  int kchunk;
 } DmlConvArgs;
 
 

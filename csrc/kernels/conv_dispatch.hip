@@ -43,10 +43,6 @@ static int validate(const DmlConvArgs* a, int cfg) {
     dml_set_error("dml_conv: split-K needs fp32 output, no residual/segments/ReLU, split_ld");
     return -1;
   }
-  if (a->kchunk && (a->kchunk < 0 || a->kchunk % 64 || a->Cin % a->kchunk || a->dh > 1 || a->dw > 1)) {
-    dml_set_error("dml_conv: chunk-major K order needs kchunk%64==0, Cin%kchunk==0, no dilation");
-    return -1;
-  }
   return 0;
 }
 

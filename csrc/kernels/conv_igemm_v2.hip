@@ -132,32 +132,9 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
   const int step_s = dw * a.ldx;                 // koff change for ss += 1
   const int step_r = dh * a.W * a.ldx;           // koff change for rr += 1
   int cc = lchunk * 8, ss = 0, rr = 0, dih = 0, diw = 0, koff = lchunk * 8;
-  const int kc = a.kchunk;  // launch-uniform
-  int cb = 0;               // chunk-major order: first channel of the current chunk
   auto advance = [&](int by) {
     cc += by;
     koff += by;
-    if (kc > 0) {  // (chunk, r, s, c): cc is the channel offset inside the chunk
-      while (cc >= kc) {
-        cc -= kc;
-        koff += step_s - kc;
-        diw += dw;
-        if (++ss == a.kw) {
-          ss = 0;
-          koff += step_r - a.kw * step_s;
-          diw = 0;
-          if (++rr == a.kh) {
-            rr = 0;
-            koff += kc - a.kh * step_r;
-            cb += kc;
-            dih = cb < a.Cin ? 0 : (1 << 28);  // K tail: zeros
-          } else {
-            dih += dh;
-          }
-        }
-      }
-      return;
-    }
     while (cc >= a.Cin) {
       cc -= a.Cin;
       koff += step_s - a.Cin;

@@ -112,8 +112,6 @@ int main() {
   CHECK(dml_conv(&a, 40, nullptr) != 0);        // ... and a tile config
   CHECK(dml_conv(&a, 2, nullptr) != 0);
   a = conv_args(64, 64, 3, 3);
-  a.kchunk = 32;
-  CHECK(dml_conv(&a, 11, nullptr) != 0);        // chunk-major K order: kchunk % 64
   DmlConvGroupArgs g;
   std::memset(&g, 0, sizeof g);
   CHECK(dml_conv_group(&g, 14, nullptr) != 0);  // no members

@@ -30,7 +30,6 @@ class ConvArgs(C.Structure):
         ("seg_y", C.c_void_p * 4),
         ("ksplit", C.c_int), ("split_ld", C.c_int),
         ("rsub", C.c_int), ("rW", C.c_int), ("rHW", C.c_int),
-        ("kchunk", C.c_int),
     ]
 
 

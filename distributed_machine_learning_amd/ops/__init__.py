@@ -10,13 +10,12 @@ from __future__ import annotations
 import ctypes as C
 from typing import Optional, Tuple
 
-import numpy as np
 import torch
 
 from .. import _native as N
 
-__all__ = ["conv2d_nhwc", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight",
-           "pack_weight_chunk_major", "resnet_stem", "inception_stem", "conv3x3_pool", "expand_reduce"]
+__all__ = ["conv2d_nhwc", "conv_group", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight",
+           "resnet_stem", "inception_stem", "conv3x3_pool", "expand_reduce"]
 
 
 def _r(x, m):
@@ -35,40 +34,16 @@ def pack_weight(w_oihw: torch.Tensor, cin_eff: Optional[int] = None) -> Tuple[to
     return out.to(torch.bfloat16), K, _r(K, 64)
 
 
-def chunk_major_layout(kernel_tco: np.ndarray, cout_pad: int, chunk: int = 64) -> np.ndarray:
-    """[cout][taps][cin] fp32 -> [cout_pad][ceil(cin/chunk)][taps][chunk]: the
-    chunk-major K order of DmlConvArgs.kchunk (the conv's K loop visits every
-    tap of one channel chunk before the next chunk)."""
-    co, taps, ci = kernel_tco.shape
-    nch = (ci + chunk - 1) // chunk
-    out = np.zeros((cout_pad, nch, taps, chunk), np.float32)
-    for c in range(nch):
-        w = min(chunk, ci - chunk * c)
-        out[:co, c, :, :w] = kernel_tco[:, :, chunk * c: chunk * c + w]
-    return out.reshape(cout_pad, nch * taps * chunk)
-
-
-def pack_weight_chunk_major(w_oihw: torch.Tensor, chunk: int = 64) -> Tuple[torch.Tensor, int, int]:
-    """OIHW fp32 -> bf16 chunk-major layout (kchunk = chunk). Returns (w, K, Kpad)."""
-    co, ci, kh, kw = w_oihw.shape
-    if ci % chunk:
-        raise ValueError("chunk-major K order needs Cin % chunk == 0")
-    k = w_oihw.permute(0, 2, 3, 1).reshape(co, kh * kw, ci).float().cpu().numpy()
-    out = chunk_major_layout(k, _r(co, 256), chunk)
-    return torch.from_numpy(out).to(torch.bfloat16), kh * kw * ci, out.shape[1]
-
-
 def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cout: int, kh: int, kw: int,
                 stride=(1, 1), pad=(0, 0), relu: bool = False, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, out_coff: int = 0, in_coff: int = 0, cin: Optional[int] = None,
                 out_f32: bool = False, cfg: int = -1, K: Optional[int] = None, dilation=(1, 1),
-                out_hw: Optional[Tuple[int, int]] = None, ksplit: int = 1, kchunk: int = 0,
+                out_hw: Optional[Tuple[int, int]] = None, ksplit: int = 1,
                 defer: Optional[list] = None) -> torch.Tensor:
     """x: NHWC bf16 [N,H,W,Cbuf] (Cbuf % 8 == 0). Returns/updates NHWC output.
     defer: a list to append the ConvArgs to instead of launching (conv_group).
     ksplit > 1 (fp32 output, v2 cfg): returns the [ksplit, N, Ho, Wo, C] split-K
-    partial sums (slice 0 carries the bias); their sum is the convolution.
-    kchunk > 0: w_packed is in chunk-major K order (pack_weight_chunk_major)."""
+    partial sums (slice 0 carries the bias); their sum is the convolution."""
     n, h, w_, cbuf = x.shape
     cin = cin if cin is not None else cbuf - in_coff
     ho = (h + 2 * pad[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
@@ -96,7 +71,6 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
                    dilation[0], dilation[1])
     if parts is not None:
         a.ksplit, a.split_ld = ksplit, out.numel()
-    a.kchunk = kchunk
     if residual is not None and residual.shape[1] != ho:  # shortcut read at stride rs (full-res grid)
         rs = residual.shape[1] // ho
         assert residual.shape[1] == ho * rs and residual.shape[2] == wo * rs and residual.is_contiguous()

@@ -271,44 +271,6 @@ def test_avgpool_relu_flag():
     assert _rel(y.float().cpu().permute(0, 3, 1, 2), ref) < 1e-2
 
 
-CHUNK_CASES = [
-    # n, h, w, cin, cout, kh, kw, stride, pad, relu, residual
-    (3, 56, 56, 64, 64, 3, 3, 1, 1, True, False),     # ResNet conv2 3x3
-    (2, 28, 28, 128, 128, 3, 3, 1, 1, True, False),   # 2 channel chunks
-    (3, 14, 14, 256, 256, 3, 3, 2, 1, True, True),    # stride 2, 4 chunks, residual epilogue
-    (2, 17, 17, 128, 192, 1, 7, 1, 0, True, False),
-    (2, 8, 8, 448, 384, 3, 3, 1, 1, False, False),    # 7 chunks
-]
-
-
-@pytest.mark.parametrize("case", CHUNK_CASES)
-@pytest.mark.parametrize("cfg", [11, 14, 15, 28, 30])
-def test_conv_chunk_major_k_order(case, cfg):
-    """K order (channel chunk, r, s, c) (DmlConvArgs.kchunk = 64) vs fp32 F.conv2d."""
-    n, h, w, cin, cout, kh, kw, s, pad, relu, has_res = case
-    ph, pw = _pads(kh, kw, pad)
-    torch.manual_seed(0)
-    x = _bf(torch.randn(n, cin, h, w))
-    wt = _bf(torch.randn(cout, cin, kh, kw) * (2.0 / (cin * kh * kw)) ** 0.5)
-    b = torch.randn(cout) * 0.1
-    ref = F.conv2d(x, wt, b, stride=s, padding=(ph, pw))
-    res = None
-    if has_res:
-        res = _bf(torch.randn_like(ref))
-        ref = ref + res
-    if relu:
-        ref = F.relu(ref)
-    wp, K, _ = ops.pack_weight_chunk_major(wt, 64)
-    xd = x.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16)
-    rd = res.permute(0, 2, 3, 1).contiguous().cuda().to(torch.bfloat16) if res is not None else None
-    y = ops.conv2d_nhwc(xd, wp.cuda(), b.cuda(), cout, kh, kw, (s, s), (ph, pw), relu=relu, residual=rd, cfg=cfg,
-                        kchunk=64)
-    torch.cuda.synchronize()
-    got = y[..., :cout].float().cpu().permute(0, 3, 1, 2)
-    assert got.shape == ref.shape
-    assert _rel(got, ref) < 1.5e-2, _rel(got, ref)
-
-
 @pytest.mark.parametrize("cfg", [10, 11, 12, 13, 14, 15, 16, 17, 18, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33,
                                  34, 36, 37])
 @pytest.mark.parametrize("case", [(2, 28, 28, 64, 256, 1, 1), (2, 14, 10, 128, 512, 1, 1), (2, 7, 9, 64, 64, 3, 3)])

@@ -15,7 +15,6 @@ ap.add_argument("--model", default="ResNet50"); ap.add_argument("--batch", type=
 ap.add_argument("--cfgs", default="10,11,12,13,14,15,16,17"); ap.add_argument("--out", default="")
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--only", default="", help="comma list of layer-name substrings to keep")
-ap.add_argument("--kchunk", type=int, default=0, help="also time the chunk-major K order (kchunk=64) on kxk shapes")
 args = ap.parse_args()
 g = build_graph(args.model); B = args.batch
 L = N.lib(); N.ensure_device_init()
@@ -48,19 +47,10 @@ for key, names in shapes.items():
     row = {"layers": names, "M": B * ho * wo, "N": cout, "K": K, "kh": kh, "kw": kw, "stride": st,
            "gflop": flops / 1e9, "mb": nbytes / 1e6, "ms": {}}
     ref = None
-    ak = None
-    if args.kchunk and kh * kw > 1 and cin % args.kchunk == 0 and st in (1, 2):
-        wk_, _, _ = ops.pack_weight_chunk_major(w_oihw, args.kchunk)
-        wk_ = wk_.cuda()
-        ak = N.ConvArgs.from_buffer_copy(a)
-        ak.w, ak.kchunk = wk_.data_ptr(), args.kchunk
-    variants = list(cfgs) + ([1000 + c for c in cfgs if 10 <= c < 40] if ak is not None else [])
+    variants = list(cfgs)
     for cfg in variants:
         aa = a
-        if cfg >= 1000:
-            aa = ak
         kc = cfg
-        cfg = cfg - 1000 if cfg >= 1000 else cfg
         try:
             N.check(L.dml_conv(C.byref(aa), cfg, N.stream_ptr()), "conv")
             torch.cuda.synchronize()
@@ -85,8 +75,7 @@ for key, names in shapes.items():
     print(f"{names[0]:22s} x{len(names)} M={row['M']:8d} N={cout:5d} K={K:5d} " +
           " ".join(f"{c}:{row['ms'][c]}" for c in row["ms"]) + f" best={best[1]} {row['best_tflops']}TF err={row.get('err')}",
           flush=True)
-tot = {c: sum((row["ms"].get(c) or row["ms"].get(c - 1000) or 1e9) * len(row["layers"]) for row in res)
-       for c in cfgs + ([1000 + c for c in cfgs] if args.kchunk else [])}
+tot = {c: sum((row["ms"].get(c) or 1e9) * len(row["layers"]) for row in res) for c in cfgs}
 best_tot = sum(min(v for v in row["ms"].values() if v) * len(row["layers"]) for row in res)
 print("total per cfg (ms):", {c: round(v, 3) for c, v in tot.items()}, "best-per-shape total:", round(best_tot, 3))
 if args.out:
