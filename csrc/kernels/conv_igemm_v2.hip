@@ -266,8 +266,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_group_kernel(DmlConvGroup
     const DmlPoolArgs& p = g.pool[i - g.n];
     const unsigned t = (unsigned)(b - g.off[i]) * 256u + threadIdx.x;
     if (t < (unsigned)poolk::pool_work(p)) {
-      if (p.mode == 0) poolk::pool3x3_item<0>(p, t);
-      else poolk::pool3x3_item<1>(p, t);
+      if (p.mode == 0) poolk::pool3x3_item<0, true>(p, t);
+      else poolk::pool3x3_item<1, true>(p, t);
     }
     return;
   }

@@ -28,7 +28,11 @@ __host__ __device__ inline long pool_work(const DmlPoolArgs& a) { return (long)a
 // load the clamped edge pixel — for a 3-wide window with pad <= 1 that pixel
 // lies inside the window, so max needs no mask; avg weights it 0 and divides by
 // the in-image tap count (TF SAME semantics). 32-bit index math.
-template <int MODE>
+// LOW_REGS: the window is read one row (3 loads in flight) at a time instead of
+// all nine loads up front — about half the live registers, for the pool path of
+// the grouped conv kernel, whose register count (and so its occupancy) is the
+// max over its conv and pool paths.
+template <int MODE, bool LOW_REGS = false>
 __device__ __forceinline__ void pool3x3_item(const DmlPoolArgs& a, unsigned t) {
   const unsigned C8 = (unsigned)a.C / 8;
   const unsigned cg = t % C8;
@@ -38,18 +42,53 @@ __device__ __forceinline__ void pool3x3_item(const DmlPoolArgs& a, unsigned t) {
   const int n = (int)(p / (unsigned)a.Ho);
   const int h0 = oh * a.stride - a.pad, w0 = ow * a.stride - a.pad;
   const bf16* xb = (const bf16*)a.x + (long)n * a.H * a.W * a.ldx + cg * 8;
-  uint4 v[9];
   int rows[3], cols[3];
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
     rows[r] = min(max(h0 + r, 0), a.H - 1);
     cols[r] = min(max(w0 + r, 0), a.W - 1);
   }
+  float acc[8];
+  if constexpr (LOW_REGS) {
+    float rw[3], cw[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      rw[r] = (unsigned)(h0 + r) < (unsigned)a.H ? 1.f : 0.f;
+      cw[r] = (unsigned)(w0 + r) < (unsigned)a.W ? 1.f : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = MODE == 0 ? -3.0e38f : 0.f;
+#pragma unroll 1
+    for (int r = 0; r < 3; ++r) {  // one window row (3 loads in flight) at a time
+      uint4 v[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c] = *(const uint4*)(xb + (long)(rows[r] * a.W + cols[c]) * a.ldx);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float f[8];
+        unpack8(v[c], f);
+        const float wgt = rw[r] * cw[c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = MODE == 0 ? fmaxf(acc[j], f[j]) : fmaf(wgt, f[j], acc[j]);
+      }
+    }
+    if (MODE != 0) {
+      const float inv = 1.f / fmaxf((rw[0] + rw[1] + rw[2]) * (cw[0] + cw[1] + cw[2]), 1.f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= inv;
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fmaxf(acc[j], 0.f);
+    }
+    *(uint4*)((bf16*)a.y + ((long)(n * a.Ho + oh) * a.Wo + ow) * a.ldy + cg * 8) = pack8(acc);
+    return;
+  }
+  uint4 v[9];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
     for (int c = 0; c < 3; ++c) v[r * 3 + c] = *(const uint4*)(xb + (long)(rows[r] * a.W + cols[c]) * a.ldx);
-  float acc[8];
   if (MODE == 0) {
     unpack8(v[0], acc);
 #pragma unroll

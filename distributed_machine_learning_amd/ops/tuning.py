@@ -119,7 +119,7 @@ def pool_key(p: N.PoolArgs) -> str:
     return f"pool{p.mode}_n{p.N}_h{p.H}_w{p.W}_c{p.C}_o{p.Ho}x{p.Wo}_s{p.stride}_p{p.pad}"
 
 
-GROUP_TAG = "grp2"  # bumped when the grouped kernel's block schedule changes (r2: XCD-balanced LPT order)
+GROUP_TAG = "grp3"  # bumped when the grouped kernel changes (r2: XCD-balanced LPT order; low-register pool path)
 
 
 def group_key(args: List[N.ConvArgs], pools: Sequence[N.PoolArgs] = ()) -> str:
