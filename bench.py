@@ -66,6 +66,10 @@ def parse_args(argv=None):
     ap.add_argument("--streams", type=int, default=0,
                     help="concurrent streams for the sub-batches (default = --splits); sub-batch i on stream i %% S")
     ap.add_argument("--no-verify", action="store_true", help="skip the post-run top-5 self-check")
+    ap.add_argument("--lookahead", type=int, default=0, choices=(0, 1, 2),
+                    help="dispatch broadcast runs this many steps ahead; 0 = auto: 1 on one GPU (a "
+                         "batch-time less query latency at equal throughput, measured), 2 on several "
+                         "(the RCCL broadcast kernel would wait behind the running forward)")
     ap.add_argument("--op-times", default="", help="write per-op times (ms) of one forward to this JSON file")
     ap.add_argument("--trace", default="", help="Chrome-trace JSON of the timed steps ('{rank}' -> rank id)")
     ap.add_argument("--dry-run", action="store_true",
@@ -128,7 +132,8 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
     store = PinnedImageStore(capacity=4 * B, hw=g.input_hw)
     store.fill_synthetic(seed=rank)
     dp = DataPlane(device, result_shape=(2, B, 5))
-    pipe = ServingPipeline(eng, store, dp, use_graph=not args.no_graph)
+    lookahead = args.lookahead or (1 if world == 1 else 2)
+    pipe = ServingPipeline(eng, store, dp, use_graph=not args.no_graph, lookahead=lookahead)
     cap = store.capacity
 
     def table(k):
@@ -198,7 +203,7 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
             "config": {"model": model, "global_batch": B * world, "seq_len": None,
                        "image_hw": list(g.input_hw), "parallelism": f"dp{world}",
                        "per_worker_batch": B, "graph": not args.no_graph, "stream_splits": splits,
-                       "streams": eng.nstreams if splits > 1 else 1},
+                       "streams": eng.nstreams if splits > 1 else 1, "dispatch_lookahead": pipe.lookahead},
             "baseline": {"source": "BASELINE.md scheduler-predicted query rate (cost model, CS425 VMs, TF CPU)",
                          "value": round(ref_rate(model, world), 3), "unit": "images/s"},
         }

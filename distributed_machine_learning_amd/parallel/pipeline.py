@@ -49,10 +49,17 @@ class PipelineStats:
 
 class ServingPipeline:
     def __init__(self, engine, store: PinnedImageStore, dp: DataPlane, use_graph: bool = True,
-                 on_results: Optional[Callable[[BatchRecord], None]] = None):
+                 on_results: Optional[Callable[[BatchRecord], None]] = None, lookahead: int = 2):
+        """``lookahead``: how many steps ahead the dispatch broadcast runs. 2 (the
+        default) never makes the host wait for a broadcast; 1 dispatches a batch
+        only while the previous forward runs — one batch-time less queueing
+        latency per query, the host waits for each (µs-scale) broadcast."""
         assert engine.src_slots >= 2, "engine needs 2 source slots for double buffering"
+        if lookahead not in (1, 2):
+            raise ValueError("lookahead must be 1 or 2")
         self.eng, self.store, self.dp = engine, store, dp
         self.use_graph = use_graph
+        self.lookahead = lookahead
         self.on_results = on_results
         dev = engine.device
         self.copy_stream = torch.cuda.Stream(dev)
@@ -101,7 +108,7 @@ class ServingPipeline:
                 handles[j] = dp.issue_dispatch(table_fn(j) if is0 else None)
 
         issue(0)
-        if steps > 1:
+        if steps > 1 and self.lookahead == 2:
             issue(1)
         self._stage(0, dp.wait_dispatch(handles.pop(0)))
         prev: Optional[BatchRecord] = None
@@ -119,11 +126,13 @@ class ServingPipeline:
                     eng.run(cs, use_graph=self.use_graph, slot=slot)
             self.ev_consumed[slot].record(cs)
             if k + 1 < steps:  # stage the next batch (its row was broadcast one step ago)
+                if self.lookahead == 1:
+                    issue(k + 1)  # dispatched while forward k runs
                 tw = time.perf_counter()
                 row = dp.wait_dispatch(handles.pop(k + 1))
                 self.stats.wait_s["dispatch"] += time.perf_counter() - tw
                 self._stage(k + 1, row)
-            if k + 2 < steps:
+            if self.lookahead == 2 and k + 2 < steps:
                 issue(k + 2)
             # result gather + host copy right behind forward k on the compute
             # stream: work on another stream is starved while the forward's

@@ -56,8 +56,8 @@ def _split_ref(g, w, imgs, half, parts=2):
     return torch.cat(out, dim=1)
 
 
-@pytest.mark.parametrize("splits,streams", [(2, 0), (8, 2)])
-def test_serving_pipeline_matches_engine(rccl_world1, splits, streams):
+@pytest.mark.parametrize("splits,streams,lookahead", [(2, 0, 2), (8, 2, 2), (2, 0, 1)])
+def test_serving_pipeline_matches_engine(rccl_world1, splits, streams, lookahead):
     """splits 8 on 2 streams: eight graph captures; captured lazily inside the
     loop they once met the RCCL watchdog querying an event on a capturing stream
     (hipErrorCapturedEvent), hence Engine.capture() before the first collective."""
@@ -76,7 +76,8 @@ def test_serving_pipeline_matches_engine(rccl_world1, splits, streams):
     store.fill_synthetic(seed=3)
     dp = DataPlane(dev, result_shape=(2, B, 5))
     got = {}
-    pipe = ServingPipeline(eng, store, dp, use_graph=True, on_results=lambda rec: got.__setitem__(rec.step, rec.results[0]))
+    pipe = ServingPipeline(eng, store, dp, use_graph=True, on_results=lambda rec: got.__setitem__(rec.step, rec.results[0]),
+                           lookahead=lookahead)
 
     def table(k):
         t = np.zeros((world, DESC_FIELDS), np.int64)
