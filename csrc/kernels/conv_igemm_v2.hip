@@ -39,14 +39,15 @@ using convk::wait_vmcnt;
 // workgroups per CU that the larger of two LDS regions allows (160 KiB per CU)
 constexpr int lds_occupancy(int a, int b) { return 163840 / (a > b ? a : b); }
 
-template <int BM, int BN, int WM, int WN, int STAGES, int BK_ = 64>
+template <int BM, int BN, int WM, int WN, int STAGES, int BK_ = 64, int MF_ = 16>
 struct Cfg {
   static constexpr int NW = WM * WN;          // waves
   static constexpr int NT = NW * 64;          // threads
   static constexpr int WTP = BM / WM;         // pixels per wave
   static constexpr int WTC = BN / WN;         // channels per wave
-  static constexpr int FJ = WTP / 16;         // fragments along pixels
-  static constexpr int FI = WTC / 16;         // fragments along channels
+  static constexpr int MF = MF_;              // MFMA fragment: 16 (16x16x32) or 32 (32x32x16)
+  static constexpr int FJ = WTP / MF;         // fragments along pixels
+  static constexpr int FI = WTC / MF;         // fragments along channels
   static constexpr int BK = BK_;
   using R = convk::Rows<BK>;
   static constexpr int ROWB = R::ROWB;        // 128 B (BK 64) or 64 B (BK 32) per tile row
@@ -58,8 +59,8 @@ struct Cfg {
   // Epilogue staging passes: the fewest (1, 2, 4) whose fp32 staging rows fit in
   // the operand ring, so the epilogue never raises the LDS size (occupancy).
   static constexpr int CROW = BN * 4 + 16;
-  static constexpr bool EP_OK2 = (BM / 2) % 16 == 0 && ((BM * BN / 8) / NT) % 2 == 0;
-  static constexpr bool EP_OK4 = (BM / 4) % 16 == 0 && ((BM * BN / 8) / NT) % 4 == 0;
+  static constexpr bool EP_OK2 = (BM / 2) % MF == 0 && ((BM * BN / 8) / NT) % 2 == 0;
+  static constexpr bool EP_OK4 = (BM / 4) % MF == 0 && ((BM * BN / 8) / NT) % 4 == 0;
   // most passes allowed, then back off to the fewest passes that keep that occupancy
   static constexpr int EP_MAX = EP_OK4 ? 4 : (EP_OK2 ? 2 : 1);
   static constexpr int OCC_BEST = lds_occupancy(PIPE_BYTES, (BM / EP_MAX) * CROW);
@@ -69,16 +70,16 @@ struct Cfg {
   static constexpr int LDS = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
   static_assert(XI >= 1 && WI >= 1, "each wave needs >=1 DMA instruction per operand");
   static_assert(BM % (R::RP * NW) == 0 && BN % (R::RP * NW) == 0, "tile rows must split evenly across waves");
-  static_assert(FI >= 1 && FJ >= 1, "wave tile too small");
+  static_assert(FI >= 1 && FJ >= 1 && WTP % MF == 0 && WTC % MF == 0, "wave tile too small");
   static_assert((STAGES - 2) * L < 64, "vmcnt overflow");
 };
 
 // One workgroup's tile: logical block Lb (already XCD-remapped) of a grid of
 // nblk blocks that runs conv `a` (the plain kernel's whole grid, or one member
 // of a grouped launch).
-template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK>
+template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK, int MF = 16>
 __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int nblk) {
-  using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
+  using T = Cfg<BM, BN, WM, WN, STAGES, BK, MF>;
   using RW = typename T::R;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -183,14 +184,17 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
     advance(T::BK);
   };
 
-  f32x4 acc[T::FI][T::FJ];
+  using Acc = typename std::conditional<MF == 32, f32x16, f32x4>::type;
+  Acc acc[T::FI][T::FJ];
 #pragma unroll
   for (int i = 0; i < T::FI; ++i)
 #pragma unroll
-    for (int j = 0; j < T::FJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < T::FJ; ++j) acc[i][j] = (Acc)(0.f);
 
   const int wc = wid % WN, wp = wid / WN;
-  const int frow = lane & 15, fq = lane >> 4;
+  // fragment lane map: row (lane & (MF-1)) of the fragment, 16-B K chunk
+  // (lane / MF) of each MFMA k-step (32 deep for MF 16, 16 deep for MF 32)
+  const int frow = lane & (MF - 1), fq = lane / MF;
 
   // prologue: tiles 0 .. STAGES-2 in flight
 #pragma unroll
@@ -216,33 +220,39 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
     // Both 32-deep k-steps' fragments are read up front (separate registers), so
     // the second step's ds_reads are in flight while the first step's MFMAs run;
     // hipcc emits a counted lgkmcnt before each MFMA group.
-    bf16x8 fa[RW::KS][T::FI], fb[RW::KS][T::FJ];
+    constexpr int KSM = BK / (512 / MF);  // MFMA k-steps per tile (32 or 16 deep)
+    constexpr int CPS = 64 / MF;          // 16-B chunks per k-step (4 or 2)
+    bf16x8 fa[KSM][T::FI], fb[KSM][T::FJ];
 #pragma unroll
-    for (int ks = 0; ks < RW::KS; ++ks) {
-      const int ch = ks * 4 + fq;
+    for (int ks = 0; ks < KSM; ++ks) {
+      const int ch = ks * CPS + fq;
 #pragma unroll
-      for (int i = 0; i < T::FI; ++i) fa[ks][i] = *(const bf16x8*)(sw + RW::off(wc * T::WTC + i * 16 + frow, ch));
+      for (int i = 0; i < T::FI; ++i) fa[ks][i] = *(const bf16x8*)(sw + RW::off(wc * T::WTC + i * MF + frow, ch));
 #pragma unroll
-      for (int j = 0; j < T::FJ; ++j) fb[ks][j] = *(const bf16x8*)(sx + RW::off(wp * T::WTP + j * 16 + frow, ch));
+      for (int j = 0; j < T::FJ; ++j) fb[ks][j] = *(const bf16x8*)(sx + RW::off(wp * T::WTP + j * MF + frow, ch));
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int ks = 0; ks < RW::KS; ++ks)
+    for (int ks = 0; ks < KSM; ++ks)
 #pragma unroll
       for (int i = 0; i < T::FI; ++i)
 #pragma unroll
-        for (int j = 0; j < T::FJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < T::FJ; ++j) {
+          if constexpr (MF == 16)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+        }
     __builtin_amdgcn_s_setprio(0);
   }
 
   // all DMA retired (vmcnt(0) on the last tile); epilogue through LDS
-  epi.template store<T::FI, T::FJ, T::WTP, T::WTC>(a, smem, acc, wp, wc, lane, tid);
+  epi.template store<MF, T::FI, T::FJ, T::WTP, T::WTC>(a, smem, acc, wp, wc, lane, tid);
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK = 64>
+template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK = 64, int MF = 16>
 __global__ __launch_bounds__(WM* WN * 64) void conv_v2_kernel(DmlConvArgs a) {
-  conv_v2_tile<BM, BN, WM, WN, STAGES, RES, BK>(a, xcd_remap(blockIdx.x, gridDim.x), gridDim.x);
+  conv_v2_tile<BM, BN, WM, WN, STAGES, RES, BK, MF>(a, xcd_remap(blockIdx.x, gridDim.x), gridDim.x);
 }
 
 // Grouped launch: up to DML_CONV_GROUP_MAX independent convs (InceptionV3's
@@ -302,16 +312,16 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_group_kernel(DmlConvGroup
   conv_v2_tile<BM, BN, WM, WN, STAGES, false, BK>(g.a[i], tile, g.off[i + 1] - g.off[i]);
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
+template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64, int MF = 16>
 static int launch(const DmlConvArgs* a, hipStream_t s) {
-  using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
+  using T = Cfg<BM, BN, WM, WN, STAGES, BK, MF>;
   const long M = (long)a->N * a->Ho * a->Wo;
   const long tiles = ((M + BM - 1) / BM) * ((a->Cout + BN - 1) / BN) * (a->ksplit > 1 ? a->ksplit : 1);
   if (a->res)
-    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK>), dim3((unsigned)tiles), dim3(T::NT), T::LDS,
-                       s, *a);
+    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK, MF>), dim3((unsigned)tiles), dim3(T::NT),
+                       T::LDS, s, *a);
   else
-    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK>), dim3((unsigned)tiles), dim3(T::NT),
+    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK, MF>), dim3((unsigned)tiles), dim3(T::NT),
                        T::LDS, s, *a);
   DML_CHECK_LAUNCH();
   return 0;
@@ -349,12 +359,12 @@ static int set_attr_group() {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
+template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64, int MF = 16>
 static int set_attr() {
-  using T = Cfg<BM, BN, WM, WN, STAGES, BK>;
-  return (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK>,
+  using T = Cfg<BM, BN, WM, WN, STAGES, BK, MF>;
+  return (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK, MF>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS) |
-         (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK>,
+         (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK, MF>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
@@ -362,40 +372,47 @@ static int set_attr() {
 }  // namespace dml
 
 // Tile configurations: id, BM (pixels), BN (channels), WM x WN waves, ring
-// STAGES, BK. The ids are the ABI of the plan builder and the tuner
+// STAGES, BK, MF (MFMA fragment: 16 = v_mfma_f32_16x16x32_bf16, 32 =
+// v_mfma_f32_32x32x16_bf16). The ids are the ABI of the plan builder and the tuner
 // (ops/tuning.py); validated by dml_conv (conv_dispatch.hip).
 #define DML_V2_TILES(X)                                                                            \
-  X(10, 256, 128, 4, 2, 3, 64)   /* 8 waves, 64x64 per wave */                                     \
-  X(11, 128, 128, 2, 2, 2, 64)   /* 4 waves, 64x64 per wave, 2 blocks/CU */                        \
-  X(12, 256, 64, 4, 1, 2, 64)    /* 4 waves, 64x64 per wave */                                     \
-  X(13, 128, 256, 2, 4, 3, 64)   /* 8 waves, 64x64 per wave */                                     \
-  X(14, 64, 128, 1, 4, 2, 64)    /* 4 waves, 64px x 32ch per wave */                               \
-  X(15, 128, 64, 2, 2, 2, 64)    /* 4 waves, 64px x 32ch per wave */                               \
-  X(16, 256, 128, 4, 2, 2, 64)   /* 8 waves, 2-stage */                                            \
-  X(17, 128, 128, 2, 2, 3, 64)   /* 4 waves, 3-stage */                                            \
-  X(18, 256, 32, 4, 1, 2, 64)    /* 4 waves (Cout = 32 layers) */                                  \
-  X(19, 128, 128, 2, 4, 3, 64)   /* 8 waves, 64px x 32ch per wave, 3-stage */                      \
-  X(20, 128, 128, 4, 2, 3, 64)   /* 8 waves, 32px x 64ch per wave, 3-stage */                      \
-  X(21, 128, 256, 2, 4, 2, 64)   /* 8 waves, 64x64 per wave, 2-stage */                            \
-  X(22, 64, 256, 1, 4, 2, 64)    /* 4 waves, 64px x 64ch per wave */                               \
+  X(10, 256, 128, 4, 2, 3, 64, 16)   /* 8 waves, 64x64 per wave */                                     \
+  X(11, 128, 128, 2, 2, 2, 64, 16)   /* 4 waves, 64x64 per wave, 2 blocks/CU */                        \
+  X(12, 256, 64, 4, 1, 2, 64, 16)    /* 4 waves, 64x64 per wave */                                     \
+  X(13, 128, 256, 2, 4, 3, 64, 16)   /* 8 waves, 64x64 per wave */                                     \
+  X(14, 64, 128, 1, 4, 2, 64, 16)    /* 4 waves, 64px x 32ch per wave */                               \
+  X(15, 128, 64, 2, 2, 2, 64, 16)    /* 4 waves, 64px x 32ch per wave */                               \
+  X(16, 256, 128, 4, 2, 2, 64, 16)   /* 8 waves, 2-stage */                                            \
+  X(17, 128, 128, 2, 2, 3, 64, 16)   /* 4 waves, 3-stage */                                            \
+  X(18, 256, 32, 4, 1, 2, 64, 16)    /* 4 waves (Cout = 32 layers) */                                  \
+  X(19, 128, 128, 2, 4, 3, 64, 16)   /* 8 waves, 64px x 32ch per wave, 3-stage */                      \
+  X(20, 128, 128, 4, 2, 3, 64, 16)   /* 8 waves, 32px x 64ch per wave, 3-stage */                      \
+  X(21, 128, 256, 2, 4, 2, 64, 16)   /* 8 waves, 64x64 per wave, 2-stage */                            \
+  X(22, 64, 256, 1, 4, 2, 64, 16)    /* 4 waves, 64px x 64ch per wave */                               \
   /* BK = 32 (64-B tile rows): half-size stages -> more workgroups per CU */                        \
-  X(23, 64, 128, 1, 4, 2, 32)                                                                      \
-  X(24, 128, 64, 2, 2, 2, 32)                                                                      \
-  X(25, 128, 128, 2, 2, 2, 32)                                                                     \
-  X(26, 64, 128, 1, 4, 3, 32)                                                                      \
-  X(27, 128, 64, 2, 2, 3, 32)                                                                      \
-  X(28, 128, 128, 2, 2, 3, 32)                                                                     \
+  X(23, 64, 128, 1, 4, 2, 32, 16)                                                                      \
+  X(24, 128, 64, 2, 2, 2, 32, 16)                                                                      \
+  X(25, 128, 128, 2, 2, 2, 32, 16)                                                                     \
+  X(26, 64, 128, 1, 4, 3, 32, 16)                                                                      \
+  X(27, 128, 64, 2, 2, 3, 32, 16)                                                                      \
+  X(28, 128, 128, 2, 2, 3, 32, 16)                                                                     \
   /* deeper rings (the epilogue no longer sets the LDS size: Cfg::EP passes) */                    \
-  X(29, 128, 128, 2, 2, 4, 32)   /* 64 KiB: 2 blocks/CU */                                         \
-  X(30, 256, 128, 4, 2, 3, 32)   /* 8 waves, 72 KiB */                                             \
-  X(31, 128, 256, 2, 4, 3, 32)   /* 8 waves, 72 KiB */                                             \
-  X(32, 64, 128, 1, 4, 3, 64)    /* 72 KiB: 2 blocks/CU */                                         \
-  X(33, 64, 128, 1, 4, 4, 32)    /* 48 KiB: 3 blocks/CU */                                         \
+  X(29, 128, 128, 2, 2, 4, 32, 16)   /* 64 KiB: 2 blocks/CU */                                         \
+  X(30, 256, 128, 4, 2, 3, 32, 16)   /* 8 waves, 72 KiB */                                             \
+  X(31, 128, 256, 2, 4, 3, 32, 16)   /* 8 waves, 72 KiB */                                             \
+  X(32, 64, 128, 1, 4, 3, 64, 16)    /* 72 KiB: 2 blocks/CU */                                         \
+  X(33, 64, 128, 1, 4, 4, 32, 16)    /* 48 KiB: 3 blocks/CU */                                         \
   /* 256x256: half the L2->LDS bytes per MFMA of 128x128 (the 3x3 layers are L2-bound); its */     \
   /* residual form spills at 2 waves/SIMD (not a tuner candidate for residual layers) */           \
-  X(34, 256, 256, 2, 4, 3, 32)   /* 8 waves, 128px x 64ch per wave, 96 KiB */                      \
-  X(36, 128, 32, 2, 1, 3, 32)    /* Cout = 32 layers (InceptionV3 stem): 2 waves, 30 KiB */        \
-  X(37, 256, 32, 4, 1, 3, 64)    /* 4 waves, 3-stage */
+  X(34, 256, 256, 2, 4, 3, 32, 16)   /* 8 waves, 128px x 64ch per wave, 96 KiB */                      \
+  X(36, 128, 32, 2, 1, 3, 32, 16)    /* Cout = 32 layers (InceptionV3 stem): 2 waves, 30 KiB */        \
+  X(37, 256, 32, 4, 1, 3, 64, 16)    /* 4 waves, 3-stage */                                     \
+  /* v_mfma_f32_32x32x16_bf16 twins (MF 32: 32x32 fragments, f32x16 accumulators) of the two */   \
+  /* most-picked tiles; kept as A/B probes, not tuner candidates: over all 64 ResNet50 / */        \
+  /* InceptionV3 shapes x 8 tile pairs the MF 32 form ran a median 4-6 % slower (best on 2 */      \
+  /* HBM-bound K=64 shapes, within noise; profiles/r2_v23/mf32_*.json) */                         \
+  X(48, 64, 128, 1, 4, 2, 64, 32)    /* = 14 */                                                    \
+  X(49, 128, 64, 2, 2, 2, 64, 32)    /* = 15 */
 // (r2, measured and removed: 192x96 and 192x192 tiles with 64px x 96ch wave
 // tiles for InceptionV3's Cout = 96/160/192 layers won no shape; conv2d_5 156 us
 // vs 147 us on 128x64, profiles/r2_v8/cb_192.log. Deep BK64 rings (4-5 stages,
@@ -417,7 +434,7 @@ static int set_attr() {
 extern "C" int dml_conv_v2_init(void) {
   using namespace dml::v2;
   int rc = 0;
-#define DML_SET(id, BM, BN, WM, WN, ST, BK) rc |= set_attr<BM, BN, WM, WN, ST, BK>();
+#define DML_SET(id, BM, BN, WM, WN, ST, BK, MF) rc |= set_attr<BM, BN, WM, WN, ST, BK, MF>();
   DML_V2_TILES(DML_SET)
 #undef DML_SET
 #define DML_SET(id, BM, BN, WM, WN, ST, BK) rc |= set_attr_group<BM, BN, WM, WN, ST, BK>();
@@ -431,8 +448,8 @@ extern "C" int dml_conv_v2_init(void) {
 extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
   using namespace dml::v2;
   switch (cfg) {
-#define DML_CASE(id, BM, BN, WM, WN, ST, BK) \
-  case id: return launch<BM, BN, WM, WN, ST, BK>(a, s);
+#define DML_CASE(id, BM, BN, WM, WN, ST, BK, MF) \
+  case id: return launch<BM, BN, WM, WN, ST, BK, MF>(a, s);
     DML_V2_TILES(DML_CASE)
 #undef DML_CASE
     default: dml_set_error("dml_conv_v2: bad cfg"); return -1;
@@ -443,7 +460,7 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
 extern "C" int dml_conv_v2_bn(int cfg) {
   if (cfg < 10 || cfg > 63) return 0;
   switch (cfg) {
-#define DML_CASE(id, BM, BN, WM, WN, ST, BK) \
+#define DML_CASE(id, BM, BN, WM, WN, ST, BK, MF) \
   case id: return BN;
     DML_V2_TILES(DML_CASE)
 #undef DML_CASE

@@ -110,12 +110,18 @@ struct Epilogue {
     }
   }
 
-  // acc[i][j]: channel fragment i (16 ch) x pixel fragment j (16 px) of this
-  // wave's (WTC x WTP) sub-tile at (wc, wp). Caller must have retired all DMA.
-  template <int FI, int FJ, int WTP, int WTC>
-  __device__ __forceinline__ void store(const DmlConvArgs& a, char* smem, f32x4 (&acc)[FI][FJ], int wp, int wc,
+  // acc[i][j]: channel fragment i (MF ch) x pixel fragment j (MF px) of this
+  // wave's (WTC x WTP) sub-tile at (wc, wp); MF = 16 (f32x4 accumulators of
+  // v_mfma_f32_16x16x32_bf16: lane holds channels 4*(lane>>4)+0..3 of pixel
+  // lane&15) or MF = 32 (f32x16 of v_mfma_f32_32x32x16_bf16: register group g
+  // holds channels 8g+4*(lane>>5)+0..3 of pixel lane&31). Caller must have
+  // retired all DMA.
+  template <int MF, int FI, int FJ, int WTP, int WTC, class Acc>
+  __device__ __forceinline__ void store(const DmlConvArgs& a, char* smem, Acc (&acc)[FI][FJ], int wp, int wc,
                                         int lane, int tid) {
-    const int frow = lane & 15, fq = lane >> 4;
+    static_assert(MF == 16 || MF == 32, "MFMA fragment size");
+    static_assert(PB % MF == 0, "an epilogue pass must hold whole pixel fragments");
+    const int frow = lane & (MF - 1), fq = lane / MF;
     // destination of this thread's channel group: the plain output, or the
     // segment (fused sibling conv) that owns channel ch_t
     void* ybase = a.y;
@@ -135,12 +141,21 @@ struct Epilogue {
       __syncthreads();  // operand tiles (pass 0) / the previous pass's staging rows are free
 #pragma unroll
       for (int j = 0; j < FJ; ++j) {
-        if (P > 1 && (wp * WTP + j * 16) / PB != pass) continue;  // wave-uniform
-        const int px = wp * WTP + j * 16 + frow - pass * PB;
+        if (P > 1 && (wp * WTP + j * MF) / PB != pass) continue;  // wave-uniform
+        const int px = wp * WTP + j * MF + frow - pass * PB;
 #pragma unroll
         for (int i = 0; i < FI; ++i) {
-          const int ch = wc * WTC + i * 16 + fq * 4;
-          *(f32x4*)(smem + px * CROW + sw(ch * 4)) = acc[i][j];
+          if constexpr (MF == 16) {
+            const int ch = wc * WTC + i * 16 + fq * 4;
+            *(f32x4*)(smem + px * CROW + sw(ch * 4)) = acc[i][j];
+          } else {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int ch = wc * WTC + i * 32 + g * 8 + fq * 4;
+              *(f32x4*)(smem + px * CROW + sw(ch * 4)) =
+                  (f32x4){acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+            }
+          }
         }
       }
       __syncthreads();

@@ -58,9 +58,9 @@ def test_conv_tile_occupancy_floors(tmp_path):
             occ[cur] = int(m.group(1))
     plain, group = {}, {}
     for name, w in occ.items():
-        m = re.search(r"conv_v2_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)E", name)
-        if m:
-            plain[tuple(int(x) for x in m.groups())] = w
+        m = re.search(r"conv_v2_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)ELi(\d+)E", name)
+        if m and m.group(8) == "16":  # MF = 16 (v_mfma_f32_16x16x32_bf16) tiles
+            plain[tuple(int(x) for x in m.groups()[:7])] = w
         m = re.search(r"conv_v2_group_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", name)
         if m:
             group[tuple(int(x) for x in m.groups())] = w
