@@ -55,8 +55,11 @@ struct Rows {
 // Epilogue of a BM(pixels) x BN(channels) tile computed by NT threads, staged
 // through LDS in P passes of BM/P pixels each (P > 1 keeps the fp32 staging
 // buffer within the operand ring's LDS, so the epilogue does not set the
-// kernel's LDS size and occupancy).
-template <int BM, int BN, int NT, bool RES, int P = 1>
+// kernel's LDS size and occupancy). LATE (RES only): the residual is loaded at
+// the start of each pass instead of before the main loop, so its EIT x 4 VGPRs
+// are not live across the K loop (the tiles whose residual prefetch costs a
+// workgroup per CU).
+template <int BM, int BN, int NT, bool RES, int P = 1, bool LATE = false>
 struct Epilogue {
   static constexpr int CG = BN / 8;            // 8-channel groups per pixel
   static constexpr int EIT = BM * CG / NT;     // pixels handled per thread
@@ -93,20 +96,24 @@ struct Epilogue {
       bias0 = *(const float4*)(a.bias + ch_t);
       bias1 = *(const float4*)(a.bias + ch_t + 4);
     }
-    if constexpr (RES) {
-      const unsigned short* __restrict__ rg = (const unsigned short*)a.res;
+    if constexpr (RES && !LATE) load_res(a, tid, 0, EIT);
+  }
+
+  // residual rows [it0, it1) of this thread's channel group -> rpre
+  __device__ __forceinline__ void load_res(const DmlConvArgs& a, int tid, int it0, int it1) {
+    const unsigned short* __restrict__ rg = (const unsigned short*)a.res;
 #pragma unroll
-      for (int it = 0; it < EIT; ++it) {
-        const int m = m0 + (tid + it * NT) / CG;
-        long rp = m;
-        if (a.rsub > 1) {  // shortcut read at stride rsub on its full-resolution grid
-          const int hw = a.Ho * a.Wo;
-          const int ni = m / hw, r = m - ni * hw;
-          const int ho = r / a.Wo, wo = r - ho * a.Wo;
-          rp = (long)ni * a.rHW + ((long)ho * a.rW + wo) * a.rsub;
-        }
-        rpre[it] = (ch_ok && m < M) ? *(const uint4*)(rg + rp * a.ldr + ch_t) : make_uint4(0, 0, 0, 0);
+    for (int it = 0; it < EIT; ++it) {
+      if (it < it0 || it >= it1) continue;  // compile-time after unrolling
+      const int m = m0 + (tid + it * NT) / CG;
+      long rp = m;
+      if (a.rsub > 1) {  // shortcut read at stride rsub on its full-resolution grid
+        const int hw = a.Ho * a.Wo;
+        const int ni = m / hw, r = m - ni * hw;
+        const int ho = r / a.Wo, wo = r - ho * a.Wo;
+        rp = (long)ni * a.rHW + ((long)ho * a.rW + wo) * a.rsub;
       }
+      rpre[it] = (ch_ok && m < M) ? *(const uint4*)(rg + rp * a.ldr + ch_t) : make_uint4(0, 0, 0, 0);
     }
   }
 
@@ -138,6 +145,8 @@ struct Epilogue {
     }
 #pragma unroll
     for (int pass = 0; pass < P; ++pass) {
+      // late residual: this pass's rows in flight while the accumulators are staged
+      if constexpr (RES && LATE) load_res(a, tid, pass * (EIT / P), (pass + 1) * (EIT / P));
       __syncthreads();  // operand tiles (pass 0) / the previous pass's staging rows are free
 #pragma unroll
       for (int j = 0; j < FJ; ++j) {

@@ -26,10 +26,10 @@ _lock = threading.Lock()
 
 
 # Cache entries are only valid for the candidate set they were timed against.
-# The committed table was tuned with V2_CFGS plus the stride-1 halo configs
-# (40..47, removed in r2): a halo config never won a shape, so every winner is
-# a V2 config and the table stays valid — the tag keeps the value it had then.
-CAND_TAG = "c3ef"
+# "c4la": the late-residual twins joined the candidates of residual convs; the
+# residual-free entries (their candidate set unchanged since "c3ef") were
+# re-tagged, the residual ones re-timed.
+CAND_TAG = "c4la"
 
 
 def shape_key(a: N.ConvArgs) -> str:
@@ -61,12 +61,15 @@ def save_cache(table: Dict[str, int], path: str = CACHE_PATH) -> None:
 
 
 NO_RES_CFGS = (34,)  # the residual-epilogue instantiation spills (256x256 tile)
+# late-residual twins (residual loaded in the epilogue; identical to their base
+# tile on residual-free convs, so timed on residual layers only)
+LATE_RES_CFGS = (56, 57, 58, 59, 60)
 
 
 def valid_cfgs(a: N.ConvArgs) -> List[int]:
     if a.Cout % 8 or a.Cin % 8 or a.ldx % 8 or a.ldy % 8:
         return []
-    return [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)]
+    return [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)] + (list(LATE_RES_CFGS) if a.res else [])
 
 
 def time_cfg(a: N.ConvArgs, cfg: int, iters: int = 3) -> float:
