@@ -32,6 +32,11 @@ PLAIN_FLOORS = {
     (128, 128, 2, 2, 2, 0, 64): 2,   # cfg 11 (64 KiB)
     (256, 64, 4, 1, 2, 0, 64): 2,    # cfg 12 (80 KiB)
 }
+LATE_FLOORS = {  # late-residual twins (residual form): the occupancy their non-residual base has
+    (256, 128, 4, 2, 3, 1, 32): 4,   # cfg 56 (min-waves hint 4: 128 VGPRs, no scratch)
+    (128, 256, 2, 4, 3, 1, 32): 4,   # cfg 57
+    (64, 128, 1, 4, 2, 1, 32): 5,    # cfg 60
+}
 GROUP_FLOORS = {  # (BM, BN, WM, WN, STAGES, BK): the grouped kernel must keep its conv path's occupancy
     (64, 128, 1, 4, 2, 32): 5,
     (128, 64, 2, 2, 2, 32): 5,
@@ -47,7 +52,7 @@ def test_conv_tile_occupancy_floors(tmp_path):
            "-Rpass-analysis=kernel-resource-usage"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
-    occ, cur = {}, None
+    occ, cur, spills = {}, None, []
     for line in r.stderr.splitlines():
         m = re.search(r"Function Name: (\S+)", line)
         if m:
@@ -56,15 +61,20 @@ def test_conv_tile_occupancy_floors(tmp_path):
         m = re.search(r"Occupancy \[waves/SIMD\]: (\d+)", line)
         if m and cur:
             occ[cur] = int(m.group(1))
-    plain, group = {}, {}
+        m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
+        if m and cur and int(m.group(1)) and "ILi256ELi256E" not in cur:  # the 256x256 residual form is known to spill
+            spills.append(cur)
+    plain, group, late = {}, {}, {}
     for name, w in occ.items():
-        m = re.search(r"conv_v2_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)ELi(\d+)E", name)
+        m = re.search(r"conv_v2_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d+)ELi(\d+)ELb(\d)E", name)
         if m and m.group(8) == "16":  # MF = 16 (v_mfma_f32_16x16x32_bf16) tiles
-            plain[tuple(int(x) for x in m.groups()[:7])] = w
+            (late if m.group(9) == "1" else plain)[tuple(int(x) for x in m.groups()[:7])] = w
         m = re.search(r"conv_v2_group_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", name)
         if m:
             group[tuple(int(x) for x in m.groups())] = w
-    assert plain and group, "no resource-usage remarks parsed"
+    assert plain and group and late, "no resource-usage remarks parsed"
+    assert not spills, f"conv kernels with scratch (register spills): {spills}"
     bad = [(k, plain.get(k), f) for k, f in PLAIN_FLOORS.items() if plain.get(k, 0) < f]
     bad += [(("group",) + k, group.get(k), f) for k, f in GROUP_FLOORS.items() if group.get(k, 0) < f]
+    bad += [(("late",) + k, late.get(k), f) for k, f in LATE_FLOORS.items() if late.get(k, 0) < f]
     assert not bad, f"occupancy below the LDS-limited floor (config, waves/SIMD, floor): {bad}"
