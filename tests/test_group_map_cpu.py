@@ -44,3 +44,24 @@ def test_group_block_map_member_order_within_xcd():
     for x in range(8):
         members = [block_map(tiles, b)[0] for b in range(x, sum(tiles), 8)]
         assert members == sorted(members), (x, members)
+
+
+def test_tuner_candidates_are_built_tile_configs():
+    """Every config the tuner may pick exists in the library's tile table (host
+    functions only, no GPU): plain candidates, late-residual twins (offered to
+    residual convs only) and grouped-launch tiles."""
+    from distributed_machine_learning_amd import _native as N
+    from distributed_machine_learning_amd.ops import tuning
+
+    L = N.lib()
+    for c in tuning.V2_CFGS + tuning.LATE_RES_CFGS:
+        assert L.dml_conv_v2_bn(c) > 0, c
+    for c in tuning.GROUP_CFGS:
+        assert L.dml_conv_v2_group_supported(c), c
+    a = N.ConvArgs()
+    a.Cin = a.ldx = a.Cout = a.ldy = 64
+    plain = tuning.valid_cfgs(a)
+    assert not set(tuning.LATE_RES_CFGS) & set(plain)
+    a.res = 1
+    withres = tuning.valid_cfgs(a)
+    assert set(tuning.LATE_RES_CFGS) <= set(withres) and not set(tuning.NO_RES_CFGS) & set(withres)
