@@ -220,9 +220,6 @@ void dml_host_free(void* p);
 int dml_memcpy_h2d_async(void* dst, const void* src, size_t bytes, hipStream_t s);
 int dml_memcpy_d2h_async(void* dst, const void* src, size_t bytes, hipStream_t s);
 
-int dml_stream_create_cu_mask(const unsigned* mask, int nwords, hipStream_t* out);  // hipExtStreamCreateWithCUMask
-int dml_stream_destroy(hipStream_t s);
-
 const char* dml_last_error(void);
 int dml_device_info(int* cus, int* arch_major, int* arch_minor);
 

@@ -295,21 +295,6 @@ struct Ring {
 };
 }  // namespace
 
-// ---------------------------------------------------------- CU-masked streams ----
-// A stream whose kernels may only occupy the CUs whose bits are set in `mask`
-// (nwords 32-bit words, bit i = logical CU i). Used to give each concurrent
-// sub-batch its own share of the chip (SplitEngine / ServingPipeline,
-// DML_CU_MASK) instead of letting both streams' kernels interleave on every CU.
-extern "C" int dml_stream_create_cu_mask(const unsigned* mask, int nwords, hipStream_t* out) {
-  if (!mask || nwords < 1 || !out) { g_err = "dml_stream_create_cu_mask: bad arguments"; return -1; }
-  HIP_OK(hipExtStreamCreateWithCUMask(out, (uint32_t)nwords, (const uint32_t*)mask));
-  return 0;
-}
-extern "C" int dml_stream_destroy(hipStream_t s) {
-  HIP_OK(hipStreamDestroy(s));
-  return 0;
-}
-
 extern "C" void* dml_host_alloc(size_t bytes) {
   void* p = nullptr;
   if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) { g_err = "hipHostMalloc failed"; return nullptr; }

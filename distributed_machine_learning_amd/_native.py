@@ -146,8 +146,6 @@ _SIGS = {
     "dml_host_free": (None, [C.c_void_p]),
     "dml_memcpy_h2d_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "dml_memcpy_d2h_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
-    "dml_stream_create_cu_mask": (C.c_int, [C.POINTER(C.c_uint), C.c_int, C.POINTER(C.c_void_p)]),
-    "dml_stream_destroy": (C.c_int, [C.c_void_p]),
     "dml_last_error": (C.c_char_p, []),
     "dml_abi_sizes": (C.c_int, [C.POINTER(C.c_int), C.c_int]),
     "dml_device_info": (C.c_int, [C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),

@@ -695,12 +695,7 @@ class SplitEngine:
         # stream 0 is the caller's stream: only nstreams-1 extra streams.
         # Measured in the serving pipeline (copy / compute / dispatch / RCCL
         # streams already live): 2 extra streams 49.1k img/s, 1 extra 58.3k.
-        # DML_CU_MASK (parallel/cu_mask.py): with two streams, the extra one runs
-        # on the other half of the CUs than the caller's masked compute stream
-        from ..parallel import cu_mask
-        self._masked = [cu_mask.from_env(self.device, 1 + k) if self.nstreams == cu_mask.PARTS else None
-                        for k in range(self.nstreams - 1)]
-        self.streams = [m.stream if m else torch.cuda.Stream(self.device) for m in self._masked]
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(self.nstreams - 1)]
         self._fork = torch.cuda.Event()
         self._join = [torch.cuda.Event() for _ in range(self.nstreams - 1)]
 

@@ -21,7 +21,6 @@ import numpy as np
 import torch
 
 from ..utils import trace as _trace
-from . import cu_mask
 from .dataplane import DataPlane, F_COUNT, F_START
 from .staging import PinnedImageStore
 
@@ -64,9 +63,7 @@ class ServingPipeline:
         self.on_results = on_results
         dev = engine.device
         self.copy_stream = torch.cuda.Stream(dev)
-        # DML_CU_MASK: the compute stream (sub-batch 0) on its own half of the CUs
-        self._masked = cu_mask.from_env(dev, 0) if getattr(engine, "nstreams", 1) == cu_mask.PARTS else None
-        self.compute_stream = self._masked.stream if self._masked else torch.cuda.Stream(dev)
+        self.compute_stream = torch.cuda.Stream(dev)
         self.ev_copied = [torch.cuda.Event() for _ in range(2)]
         self.ev_consumed = [torch.cuda.Event() for _ in range(2)]
         self.ev_res = [torch.cuda.Event() for _ in range(2)]

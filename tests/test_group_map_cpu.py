@@ -65,20 +65,3 @@ def test_tuner_candidates_are_built_tile_configs():
     a.res = 1
     withres = tuning.valid_cfgs(a)
     assert set(tuning.LATE_RES_CFGS) <= set(withres) and not set(tuning.NO_RES_CFGS) & set(withres)
-
-
-def test_cu_mask_patterns_split_the_chip():
-    """DML_CU_MASK patterns: the two parts are disjoint and together cover every CU."""
-    from distributed_machine_learning_amd.parallel import cu_mask
-
-    for ncu in (256, 304, 80):
-        for pat in ("lohi", "mod8", "evenodd"):
-            a, b = cu_mask.mask_words(pat, 0, ncu), cu_mask.mask_words(pat, 1, ncu)
-            assert len(a) == len(b) == (ncu + 31) // 32
-            assert all(x & y == 0 for x, y in zip(a, b))
-            full = [x | y for x, y in zip(a, b)]
-            assert sum(bin(w).count("1") for w in full) == ncu
-            assert sum(bin(w).count("1") for w in a) == ncu // 2
-    assert cu_mask.mask_words("lohi", 0, 256) == [0xFFFFFFFF] * 4 + [0] * 4
-    assert cu_mask.mask_words("mod8", 0, 256) == [0x0F0F0F0F] * 8
-    assert cu_mask.mask_words("0x1,0x2;0x4,0x8", 1, 64) == [4, 8]
