@@ -25,11 +25,11 @@ CACHE_PATH = os.environ.get(
 _lock = threading.Lock()
 
 
-# Cache entries are only valid for the candidate set they were timed against.
-# "c4la": the late-residual twins joined the candidates of residual convs; the
-# residual-free entries (their candidate set unchanged since "c3ef") were
-# re-tagged, the residual ones re-timed.
-CAND_TAG = "c4la"
+# Cache entries are only valid for the candidate set (and kernel build) they
+# were timed against. "c4la": the late-residual twins joined the candidates of
+# residual convs. "c5rt": every shape re-timed (10 launches per candidate) on
+# the current kernels. DML_TUNING_TAG selects another tag (A/B of tables).
+CAND_TAG = os.environ.get("DML_TUNING_TAG", "c5rt")
 
 
 def shape_key(a: N.ConvArgs) -> str:
@@ -52,7 +52,7 @@ def load_cache(path: str = CACHE_PATH) -> Dict[str, int]:
 def save_cache(table: Dict[str, int], path: str = CACHE_PATH) -> None:
     with _lock:
         os.makedirs(os.path.dirname(path), exist_ok=True)
-        cur = {k: v for k, v in load_cache(path).items() if k.endswith("_" + CAND_TAG)}  # drop stale tags
+        cur = load_cache(path)  # entries of other tags stay (A/B via DML_TUNING_TAG); lookups match the tag
         cur.update(table)
         tmp = f"{path}.{os.getpid()}.tmp"  # ranks of one node may tune concurrently
         with open(tmp, "w") as f:
@@ -72,7 +72,7 @@ def valid_cfgs(a: N.ConvArgs) -> List[int]:
     return [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)] + (list(LATE_RES_CFGS) if a.res else [])
 
 
-def time_cfg(a: N.ConvArgs, cfg: int, iters: int = 3) -> float:
+def time_cfg(a: N.ConvArgs, cfg: int, iters: int = 10) -> float:
     import torch
 
     L = N.lib()
