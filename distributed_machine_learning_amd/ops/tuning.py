@@ -25,11 +25,14 @@ CACHE_PATH = os.environ.get(
 _lock = threading.Lock()
 
 
-# Cache entries are only valid for the candidate set (and kernel build) they
-# were timed against. "c4la": the late-residual twins joined the candidates of
-# residual convs. "c5rt": every shape re-timed (10 launches per candidate) on
-# the current kernels. DML_TUNING_TAG selects another tag (A/B of tables).
-CAND_TAG = os.environ.get("DML_TUNING_TAG", "c5rt")
+# Cache entries are only valid for the candidate set, kernel build and timing
+# method they were timed with. "c4la": the late-residual twins joined the
+# candidates of residual convs. "c5rt": every shape re-timed warm (10 back-to-back
+# launches). "c5cold": every shape timed cold (time_cfg), the engine's situation:
+# a forward's weights and most activations are out of L2/MALL when their layer
+# runs; same-box A/B ResNet50 83.2-83.7k vs 81.9-82.1k img/s (profiles/r2_v31).
+# DML_TUNING_TAG selects another tag (A/B of tables).
+CAND_TAG = os.environ.get("DML_TUNING_TAG", "c5cold")
 
 
 def shape_key(a: N.ConvArgs) -> str:
@@ -72,12 +75,37 @@ def valid_cfgs(a: N.ConvArgs) -> List[int]:
     return [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)] + (list(LATE_RES_CFGS) if a.res else [])
 
 
+_scrub = None
+
+
+def _cold() -> bool:
+    return os.environ.get("DML_TUNE_COLD", "1") == "1"
+
+
 def time_cfg(a: N.ConvArgs, cfg: int, iters: int = 10) -> float:
+    """Mean time of one launch. Default (DML_TUNE_COLD=1): every launch timed
+    alone after overwriting a 512 MiB buffer (L2 and MALL evicted: weights and
+    activations come from HBM, as inside a forward). DML_TUNE_COLD=0:
+    back-to-back launches (L2/MALL warm)."""
     import torch
 
+    global _scrub
     L = N.lib()
     s = N.stream_ptr()
     N.check(L.dml_conv(C.byref(a), cfg, s), "conv warmup")
+    if _cold():
+        if _scrub is None:
+            _scrub = torch.zeros(128 << 20, device=torch.cuda.current_device())
+        ms = 0.0
+        for _ in range(iters):
+            _scrub.add_(1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            L.dml_conv(C.byref(a), cfg, s)
+            e1.record()
+            e1.synchronize()
+            ms += e0.elapsed_time(e1)
+        return ms / iters
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):

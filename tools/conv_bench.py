@@ -15,6 +15,8 @@ ap.add_argument("--model", default="ResNet50"); ap.add_argument("--batch", type=
 ap.add_argument("--cfgs", default="10,11,12,13,14,15,16,17"); ap.add_argument("--out", default="")
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--only", default="", help="comma list of layer-name substrings to keep")
+ap.add_argument("--flush", action="store_true",
+                help="cold caches: overwrite a 512 MiB buffer before each timed launch (L2 + MALL evicted)")
 args = ap.parse_args()
 g = build_graph(args.model); B = args.batch
 L = N.lib(); N.ensure_device_init()
@@ -27,6 +29,7 @@ for n in g.conv_nodes():
     shapes.setdefault(key, []).append(n.name)
 res = []
 s = torch.cuda.current_stream()
+scrub = torch.zeros(128 << 20, device="cuda") if args.flush else None  # 512 MiB
 for key, names in shapes.items():
     if args.only and not any(o in names[0] for o in args.only.split(",")):
         continue
@@ -57,12 +60,22 @@ for key, names in shapes.items():
             out = y.float()
             if ref is None: ref = out
             err = ((out - ref).abs().max() / (ref.abs().max() + 1e-6)).item()
-            e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
-            e0.record()
-            for _ in range(args.iters):
-                L.dml_conv(C.byref(aa), cfg, N.stream_ptr())
-            e1.record(); torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / args.iters
+            if args.flush:
+                ms = 0.0
+                for _ in range(args.iters):
+                    scrub.add_(1.0)
+                    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+                    e0.record()
+                    L.dml_conv(C.byref(aa), cfg, N.stream_ptr())
+                    e1.record(); torch.cuda.synchronize()
+                    ms += e0.elapsed_time(e1) / args.iters
+            else:
+                e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+                e0.record()
+                for _ in range(args.iters):
+                    L.dml_conv(C.byref(aa), cfg, N.stream_ptr())
+                e1.record(); torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / args.iters
             row["ms"][kc] = round(ms, 4)
             row.setdefault("err", {})[kc] = round(err, 4)
         except Exception as ex:
