@@ -77,8 +77,7 @@ struct Cfg {
 // One workgroup's tile: logical block Lb (already XCD-remapped) of a grid of
 // nblk blocks that runs conv `a` (the plain kernel's whole grid, or one member
 // of a grouped launch).
-template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK, int MF = 16, bool LATE = false,
-          int ORD = 0>
+template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK, int MF = 16, bool LATE = false>
 __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int nblk) {
   using T = Cfg<BM, BN, WM, WN, STAGES, BK, MF>;
   using RW = typename T::R;
@@ -95,18 +94,10 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
     split = Lb / ntiles;
     Lb -= split * ntiles;
   }
-  // ORD 0: channel tiles fastest (an XCD's blocks share activation rows);
-  // ORD 1: pixel tiles fastest (an XCD's blocks share a weight panel: K-heavy
-  // layers whose weights exceed one XCD's 4 MB L2)
-  int tc, tm;
-  if constexpr (ORD == 1) {
-    const int ntm = (M + BM - 1) / BM;
-    tm = Lb % ntm;
-    tc = Lb / ntm;
-  } else {
-    tc = Lb % ntc;
-    tm = Lb / ntc;
-  }
+  // channel tiles fastest: an XCD's blocks share activation rows (a
+  // pixel-fastest order, sharing weight panels instead, measured neutral warm
+  // and cold on the K-heavy stage-4/5 layers, profiles/r2_v31)
+  const int tc = Lb % ntc, tm = Lb / ntc;
   const int m0 = tm * BM, c0 = tc * BN;
 
   const int tid = threadIdx.x;
@@ -265,10 +256,9 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
 // W: minimum waves/SIMD asked of the register allocator (launch-bounds hint; 1 =
 // none). Set per tile only where it reaches the LDS-limited occupancy without
 // scratch (checked by tests/test_kernel_occupancy.py).
-template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK = 64, int MF = 16, bool LATE = false, int W = 1,
-          int ORD = 0>
+template <int BM, int BN, int WM, int WN, int STAGES, bool RES, int BK = 64, int MF = 16, bool LATE = false, int W = 1>
 __global__ __launch_bounds__(WM* WN * 64, W) void conv_v2_kernel(DmlConvArgs a) {
-  conv_v2_tile<BM, BN, WM, WN, STAGES, RES, BK, MF, LATE, ORD>(a, xcd_remap(blockIdx.x, gridDim.x), gridDim.x);
+  conv_v2_tile<BM, BN, WM, WN, STAGES, RES, BK, MF, LATE>(a, xcd_remap(blockIdx.x, gridDim.x), gridDim.x);
 }
 
 // Grouped launch: up to DML_CONV_GROUP_MAX independent convs (InceptionV3's
@@ -328,17 +318,16 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_v2_group_kernel(DmlConvGroup
   conv_v2_tile<BM, BN, WM, WN, STAGES, false, BK>(g.a[i], tile, g.off[i + 1] - g.off[i]);
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64, int MF = 16, bool LATE = false, int W = 1,
-          int ORD = 0>
+template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64, int MF = 16, bool LATE = false, int W = 1>
 static int launch(const DmlConvArgs* a, hipStream_t s) {
   using T = Cfg<BM, BN, WM, WN, STAGES, BK, MF>;
   const long M = (long)a->N * a->Ho * a->Wo;
   const long tiles = ((M + BM - 1) / BM) * ((a->Cout + BN - 1) / BN) * (a->ksplit > 1 ? a->ksplit : 1);
   if (a->res)
-    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK, MF, LATE, W, ORD>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK, MF, LATE, W>), dim3((unsigned)tiles),
                        dim3(T::NT), T::LDS, s, *a);
   else
-    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK, MF, false, LATE ? 1 : W, ORD>),
+    hipLaunchKernelGGL((conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK, MF, false, LATE ? 1 : W>),
                        dim3((unsigned)tiles), dim3(T::NT), T::LDS, s, *a);
   DML_CHECK_LAUNCH();
   return 0;
@@ -376,14 +365,13 @@ static int set_attr_group() {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64, int MF = 16, bool LATE = false, int W = 1,
-          int ORD = 0>
+template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64, int MF = 16, bool LATE = false, int W = 1>
 static int set_attr() {
   using T = Cfg<BM, BN, WM, WN, STAGES, BK, MF>;
-  return (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK, MF, LATE, W, ORD>,
+  return (int)hipFuncSetAttribute((const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, true, BK, MF, LATE, W>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS) |
          (int)hipFuncSetAttribute(
-             (const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK, MF, false, LATE ? 1 : W, ORD>,
+             (const void*)conv_v2_kernel<BM, BN, WM, WN, STAGES, false, BK, MF, false, LATE ? 1 : W>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
@@ -394,57 +382,53 @@ static int set_attr() {
 // STAGES, BK, MF (MFMA fragment: 16 = v_mfma_f32_16x16x32_bf16, 32 =
 // v_mfma_f32_32x32x16_bf16), RL (residual load: 0 = prefetched before the K
 // loop, 1 = in the epilogue), W (min waves/SIMD register hint; for an RL 1 twin
-// it applies to the residual form only), ORD (block order: 0 = channel tiles
-// fastest, 1 = pixel tiles fastest). The ids are the ABI of the plan builder and the tuner
+// it applies to the residual form only). The ids are the ABI of the plan builder and the tuner
 // (ops/tuning.py); validated by dml_conv (conv_dispatch.hip).
 #define DML_V2_TILES(X)                                                                            \
-  X(10, 256, 128, 4, 2, 3, 64, 16, 0, 1, 0)   /* 8 waves, 64x64 per wave */                                     \
-  X(11, 128, 128, 2, 2, 2, 64, 16, 0, 1, 0)   /* 4 waves, 64x64 per wave, 2 blocks/CU */                        \
-  X(12, 256, 64, 4, 1, 2, 64, 16, 0, 1, 0)    /* 4 waves, 64x64 per wave */                                     \
-  X(13, 128, 256, 2, 4, 3, 64, 16, 0, 1, 0)   /* 8 waves, 64x64 per wave */                                     \
-  X(14, 64, 128, 1, 4, 2, 64, 16, 0, 1, 0)    /* 4 waves, 64px x 32ch per wave */                               \
-  X(15, 128, 64, 2, 2, 2, 64, 16, 0, 1, 0)    /* 4 waves, 64px x 32ch per wave */                               \
-  X(16, 256, 128, 4, 2, 2, 64, 16, 0, 1, 0)   /* 8 waves, 2-stage */                                            \
-  X(17, 128, 128, 2, 2, 3, 64, 16, 0, 1, 0)   /* 4 waves, 3-stage */                                            \
-  X(18, 256, 32, 4, 1, 2, 64, 16, 0, 1, 0)    /* 4 waves (Cout = 32 layers) */                                  \
-  X(19, 128, 128, 2, 4, 3, 64, 16, 0, 1, 0)   /* 8 waves, 64px x 32ch per wave, 3-stage */                      \
-  X(20, 128, 128, 4, 2, 3, 64, 16, 0, 1, 0)   /* 8 waves, 32px x 64ch per wave, 3-stage */                      \
-  X(21, 128, 256, 2, 4, 2, 64, 16, 0, 1, 0)   /* 8 waves, 64x64 per wave, 2-stage */                            \
-  X(22, 64, 256, 1, 4, 2, 64, 16, 0, 1, 0)    /* 4 waves, 64px x 64ch per wave */                               \
+  X(10, 256, 128, 4, 2, 3, 64, 16, 0, 1)   /* 8 waves, 64x64 per wave */                                     \
+  X(11, 128, 128, 2, 2, 2, 64, 16, 0, 1)   /* 4 waves, 64x64 per wave, 2 blocks/CU */                        \
+  X(12, 256, 64, 4, 1, 2, 64, 16, 0, 1)    /* 4 waves, 64x64 per wave */                                     \
+  X(13, 128, 256, 2, 4, 3, 64, 16, 0, 1)   /* 8 waves, 64x64 per wave */                                     \
+  X(14, 64, 128, 1, 4, 2, 64, 16, 0, 1)    /* 4 waves, 64px x 32ch per wave */                               \
+  X(15, 128, 64, 2, 2, 2, 64, 16, 0, 1)    /* 4 waves, 64px x 32ch per wave */                               \
+  X(16, 256, 128, 4, 2, 2, 64, 16, 0, 1)   /* 8 waves, 2-stage */                                            \
+  X(17, 128, 128, 2, 2, 3, 64, 16, 0, 1)   /* 4 waves, 3-stage */                                            \
+  X(18, 256, 32, 4, 1, 2, 64, 16, 0, 1)    /* 4 waves (Cout = 32 layers) */                                  \
+  X(19, 128, 128, 2, 4, 3, 64, 16, 0, 1)   /* 8 waves, 64px x 32ch per wave, 3-stage */                      \
+  X(20, 128, 128, 4, 2, 3, 64, 16, 0, 1)   /* 8 waves, 32px x 64ch per wave, 3-stage */                      \
+  X(21, 128, 256, 2, 4, 2, 64, 16, 0, 1)   /* 8 waves, 64x64 per wave, 2-stage */                            \
+  X(22, 64, 256, 1, 4, 2, 64, 16, 0, 1)    /* 4 waves, 64px x 64ch per wave */                               \
   /* BK = 32 (64-B tile rows): half-size stages -> more workgroups per CU */                        \
-  X(23, 64, 128, 1, 4, 2, 32, 16, 0, 1, 0)                                                                      \
-  X(24, 128, 64, 2, 2, 2, 32, 16, 0, 1, 0)                                                                      \
-  X(25, 128, 128, 2, 2, 2, 32, 16, 0, 1, 0)                                                                     \
-  X(26, 64, 128, 1, 4, 3, 32, 16, 0, 1, 0)                                                                      \
-  X(27, 128, 64, 2, 2, 3, 32, 16, 0, 1, 0)                                                                      \
-  X(28, 128, 128, 2, 2, 3, 32, 16, 0, 1, 0)                                                                     \
+  X(23, 64, 128, 1, 4, 2, 32, 16, 0, 1)                                                                      \
+  X(24, 128, 64, 2, 2, 2, 32, 16, 0, 1)                                                                      \
+  X(25, 128, 128, 2, 2, 2, 32, 16, 0, 1)                                                                     \
+  X(26, 64, 128, 1, 4, 3, 32, 16, 0, 1)                                                                      \
+  X(27, 128, 64, 2, 2, 3, 32, 16, 0, 1)                                                                      \
+  X(28, 128, 128, 2, 2, 3, 32, 16, 0, 1)                                                                     \
   /* deeper rings (the epilogue no longer sets the LDS size: Cfg::EP passes) */                    \
-  X(29, 128, 128, 2, 2, 4, 32, 16, 0, 1, 0)   /* 64 KiB: 2 blocks/CU */                                         \
-  X(30, 256, 128, 4, 2, 3, 32, 16, 0, 1, 0)   /* 8 waves, 72 KiB */                                             \
-  X(31, 128, 256, 2, 4, 3, 32, 16, 0, 1, 0)   /* 8 waves, 72 KiB */                                             \
-  X(32, 64, 128, 1, 4, 3, 64, 16, 0, 1, 0)    /* 72 KiB: 2 blocks/CU */                                         \
-  X(33, 64, 128, 1, 4, 4, 32, 16, 0, 1, 0)    /* 48 KiB: 3 blocks/CU */                                         \
+  X(29, 128, 128, 2, 2, 4, 32, 16, 0, 1)   /* 64 KiB: 2 blocks/CU */                                         \
+  X(30, 256, 128, 4, 2, 3, 32, 16, 0, 1)   /* 8 waves, 72 KiB */                                             \
+  X(31, 128, 256, 2, 4, 3, 32, 16, 0, 1)   /* 8 waves, 72 KiB */                                             \
+  X(32, 64, 128, 1, 4, 3, 64, 16, 0, 1)    /* 72 KiB: 2 blocks/CU */                                         \
+  X(33, 64, 128, 1, 4, 4, 32, 16, 0, 1)    /* 48 KiB: 3 blocks/CU */                                         \
   /* 256x256: half the L2->LDS bytes per MFMA of 128x128 (the 3x3 layers are L2-bound); its */     \
   /* residual form spills at 2 waves/SIMD (not a tuner candidate for residual layers) */           \
-  X(34, 256, 256, 2, 4, 3, 32, 16, 0, 1, 0)   /* 8 waves, 128px x 64ch per wave, 96 KiB */                      \
-  X(36, 128, 32, 2, 1, 3, 32, 16, 0, 1, 0)    /* Cout = 32 layers (InceptionV3 stem): 2 waves, 30 KiB */        \
-  X(37, 256, 32, 4, 1, 3, 64, 16, 0, 1, 0)    /* 4 waves, 3-stage */                                     \
+  X(34, 256, 256, 2, 4, 3, 32, 16, 0, 1)   /* 8 waves, 128px x 64ch per wave, 96 KiB */                      \
+  X(36, 128, 32, 2, 1, 3, 32, 16, 0, 1)    /* Cout = 32 layers (InceptionV3 stem): 2 waves, 30 KiB */        \
+  X(37, 256, 32, 4, 1, 3, 64, 16, 0, 1)    /* 4 waves, 3-stage */                                     \
   /* v_mfma_f32_32x32x16_bf16 twins (MF 32: 32x32 fragments, f32x16 accumulators) of the two */   \
   /* most-picked tiles; kept as A/B probes, not tuner candidates: over all 64 ResNet50 / */        \
   /* InceptionV3 shapes x 8 tile pairs the MF 32 form ran a median 4-6 % slower (best on 2 */      \
   /* HBM-bound K=64 shapes, within noise; profiles/r2_v23/mf32_*.json) */                         \
-  X(48, 64, 128, 1, 4, 2, 64, 32, 0, 1, 0)    /* = 14 */                                                    \
-  X(49, 128, 64, 2, 2, 2, 64, 32, 0, 1, 0)    /* = 15 */                                                 \
+  X(48, 64, 128, 1, 4, 2, 64, 32, 0, 1)    /* = 14 */                                                    \
+  X(49, 128, 64, 2, 2, 2, 64, 32, 0, 1)    /* = 15 */                                                 \
   /* late-residual twins (RL 1: residual loaded in the epilogue, not across the K loop) of the */  \
   /* tiles whose residual prefetch costs occupancy; residual layers only (ops/tuning.py) */        \
-  X(56, 256, 128, 4, 2, 3, 32, 16, 1, 4, 0)  /* = 30 */                                                  \
-  X(57, 128, 256, 2, 4, 3, 32, 16, 1, 1, 0)  /* = 31 */                                                  \
-  X(58, 128, 128, 2, 2, 2, 32, 16, 1, 1, 0)  /* = 25 */                                                  \
-  X(59, 128, 128, 2, 2, 3, 32, 16, 1, 1, 0)  /* = 28 */                                                  \
-  X(60, 64, 128, 1, 4, 2, 32, 16, 1, 1, 0)   /* = 23 */                                             \
-  /* pixel-fastest block order twins (ORD 1) for the K-heavy stage-4/5 layers */                   \
-  X(62, 64, 128, 1, 4, 2, 64, 16, 0, 1, 1)   /* = 14 */                                             \
-  X(63, 128, 128, 2, 2, 2, 64, 16, 0, 1, 1)  /* = 11 */
+  X(56, 256, 128, 4, 2, 3, 32, 16, 1, 4)  /* = 30 */                                                  \
+  X(57, 128, 256, 2, 4, 3, 32, 16, 1, 1)  /* = 31 */                                                  \
+  X(58, 128, 128, 2, 2, 2, 32, 16, 1, 1)  /* = 25 */                                                  \
+  X(59, 128, 128, 2, 2, 3, 32, 16, 1, 1)  /* = 28 */                                                  \
+  X(60, 64, 128, 1, 4, 2, 32, 16, 1, 1)   /* = 23 */
 // (r2, measured and removed: 192x96 and 192x192 tiles with 64px x 96ch wave
 // tiles for InceptionV3's Cout = 96/160/192 layers won no shape; conv2d_5 156 us
 // vs 147 us on 128x64, profiles/r2_v8/cb_192.log. Deep BK64 rings (4-5 stages,
@@ -466,7 +450,7 @@ static int set_attr() {
 extern "C" int dml_conv_v2_init(void) {
   using namespace dml::v2;
   int rc = 0;
-#define DML_SET(id, BM, BN, WM, WN, ST, BK, MF, RL, W, ORD) rc |= set_attr<BM, BN, WM, WN, ST, BK, MF, RL, W, ORD>();
+#define DML_SET(id, BM, BN, WM, WN, ST, BK, MF, RL, W) rc |= set_attr<BM, BN, WM, WN, ST, BK, MF, RL, W>();
   DML_V2_TILES(DML_SET)
 #undef DML_SET
 #define DML_SET(id, BM, BN, WM, WN, ST, BK) rc |= set_attr_group<BM, BN, WM, WN, ST, BK>();
@@ -480,8 +464,8 @@ extern "C" int dml_conv_v2_init(void) {
 extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
   using namespace dml::v2;
   switch (cfg) {
-#define DML_CASE(id, BM, BN, WM, WN, ST, BK, MF, RL, W, ORD) \
-  case id: return launch<BM, BN, WM, WN, ST, BK, MF, RL, W, ORD>(a, s);
+#define DML_CASE(id, BM, BN, WM, WN, ST, BK, MF, RL, W) \
+  case id: return launch<BM, BN, WM, WN, ST, BK, MF, RL, W>(a, s);
     DML_V2_TILES(DML_CASE)
 #undef DML_CASE
     default: dml_set_error("dml_conv_v2: bad cfg"); return -1;
@@ -492,7 +476,7 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
 extern "C" int dml_conv_v2_bn(int cfg) {
   if (cfg < 10 || cfg > 63) return 0;
   switch (cfg) {
-#define DML_CASE(id, BM, BN, WM, WN, ST, BK, MF, RL, W, ORD) \
+#define DML_CASE(id, BM, BN, WM, WN, ST, BK, MF, RL, W) \
   case id: return BN;
     DML_V2_TILES(DML_CASE)
 #undef DML_CASE
