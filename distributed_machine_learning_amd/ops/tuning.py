@@ -150,7 +150,9 @@ def pool_key(p: N.PoolArgs) -> str:
     return f"pool{p.mode}_n{p.N}_h{p.H}_w{p.W}_c{p.C}_o{p.Ho}x{p.Wo}_s{p.stride}_p{p.pad}"
 
 
-GROUP_TAG = "grp3"  # bumped when the grouped kernel changes (r2: XCD-balanced LPT order; low-register pool path)
+# bumped when the grouped kernel or the timing changes (r2: XCD-balanced LPT
+# order; low-register pool path; grp4: cold-cache timing). DML_GROUP_TAG: A/B.
+GROUP_TAG = os.environ.get("DML_GROUP_TAG", "grp4")
 
 
 def group_key(args: List[N.ConvArgs], pools: Sequence[N.PoolArgs] = ()) -> str:
@@ -169,9 +171,25 @@ def group_args(args: List[N.ConvArgs], pools: Sequence[N.PoolArgs] = ()) -> N.Co
 
 
 def _time(fn, iters: int) -> float:
+    """Mean time of ``fn``'s launches: cold (each call timed alone after the
+    L2/MALL scrub, as time_cfg) unless DML_TUNE_COLD=0."""
     import torch
 
+    global _scrub
     fn()
+    if _cold():
+        if _scrub is None:
+            _scrub = torch.zeros(128 << 20, device=torch.cuda.current_device())
+        ms = 0.0
+        for _ in range(iters):
+            _scrub.add_(1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ms += e0.elapsed_time(e1)
+        return ms / iters
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):

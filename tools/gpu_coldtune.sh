@@ -18,9 +18,9 @@ run() {  # name, env...
     && echo "$n: $(tail -1 gpurun_out/ct_$n.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["models"]["InceptionV3"]["value"], d["verified_top5"])')" \
     || { tail -20 gpurun_out/ct_$n.log; exit 1; }
 }
-run old1 DML_TUNING_TAG=$OLD
+run old1 DML_TUNING_TAG=$OLD $OLDENV
 run tune DML_TUNING_TAG=$NEW
 run new1 DML_TUNING_TAG=$NEW
-run old2 DML_TUNING_TAG=$OLD
+run old2 DML_TUNING_TAG=$OLD $OLDENV
 run new2 DML_TUNING_TAG=$NEW
 cp distributed_machine_learning_amd/tuning/conv_tuning.json gpurun_out/conv_tuning_ct.json
