@@ -169,7 +169,6 @@ int dml_conv_v2_bn(int cfg);
 int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);
-int dml_prefetch(const void* p, long bytes, void* sink, hipStream_t s);  // read p once (weights -> MALL/L2)
 int dml_softmax_top5(const float* logits, int B, int classes, int ld, float* probs_out,
                      int* top_idx, float* top_p, hipStream_t s);
 // logits given as `nsplit` fp32 partial slices (split-K classifier): row r of
@@ -187,7 +186,6 @@ void dml_plan_destroy(void* plan);
 int dml_plan_add_conv(void* plan, const DmlConvArgs* a, int cfg);
 int dml_plan_add_conv_group(void* plan, const DmlConvGroupArgs* g, int cfg);
 int dml_plan_add_pool(void* plan, const DmlPoolArgs* a);
-int dml_plan_add_prefetch(void* plan, const void* ptr, long bytes, void* sink);
 int dml_plan_add_gap(void* plan, const void* x, void* y, int N, int HW, int C, int ldx);
 int dml_plan_add_softmax_top5(void* plan, const float* logits, int B, int classes, int ld,
                               float* probs, int* idx, float* p);

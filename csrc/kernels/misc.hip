@@ -285,33 +285,6 @@ extern "C" int dml_pool(const DmlPoolArgs* a, hipStream_t s) {
   return 0;
 }
 
-// Weight prefetch: read a buffer once (plain cached loads) so its lines sit in
-// the memory-side cache (MALL) and the reading XCDs' L2 when the conv that
-// consumes it starts: inside a forward the K-heavy convs otherwise wait on DRAM
-// latency at every ring stage (cold weights; DESIGN.md §3 cold-cache tuning).
-// Nothing is written unless the XOR of the data hits a magic value (keeps the
-// loads alive; a per-lane vector store).
-namespace dml {
-__global__ __launch_bounds__(256) void prefetch_kernel(const uint4* __restrict__ p, long n16, unsigned* sink) {
-  unsigned acc = 0;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) {
-    const uint4 v = p[i];
-    acc ^= v.x ^ v.y ^ v.z ^ v.w;
-  }
-  if (acc == 0x9e3779b9u) sink[threadIdx.x] = acc;
-}
-}  // namespace dml
-
-extern "C" int dml_prefetch(const void* p, long bytes, void* sink, hipStream_t s) {
-  if (!p || bytes < 16 || !sink) { dml_set_error("dml_prefetch: bad arguments"); return -1; }
-  const long n16 = bytes / 16;
-  const long blocks = (n16 + 255) / 256;
-  hipLaunchKernelGGL(dml::prefetch_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s,
-                     (const uint4*)p, n16, (unsigned*)sink);
-  DML_CHECK_LAUNCH();
-  return 0;
-}
-
 extern "C" int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s) {
   if (C % 8 || ldx % 8) { dml_set_error("dml_global_avgpool: channels must be %8"); return -1; }
   hipLaunchKernelGGL(dml::gap_kernel, dim3((unsigned)(N * ((C + 255) / 256))), dim3(256), 0, s, (const bf16*)x,

@@ -54,8 +54,7 @@ extern "C" int dml_abi_sizes(int* out, int n) {
 // ----------------------------------------------------------------- plan ----
 namespace {
 enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM, OP_INC_STEM, OP_CONV_POOL, OP_EXP_RED,
-              OP_CONV_GROUP, OP_PREFETCH };
-struct PrefetchArgs { const void* p; long bytes; void* sink; };
+              OP_CONV_GROUP };
 struct GapArgs { const void* x; void* y; int N, HW, C, ldx; };
 struct SmArgs { float* logits; int B, classes, ld, nsplit, split_ld; float* probs; int* idx; float* p; };
 struct Op {
@@ -71,7 +70,6 @@ struct Op {
   DmlConvPoolArgs cpool;
   DmlExpandReduceArgs er;
   DmlConvGroupArgs grp;
-  PrefetchArgs pf;
 };
 struct Plan {
   std::vector<Op> ops;
@@ -106,7 +104,6 @@ int run_op(const Op& o, hipStream_t s) {
     case OP_CONV_POOL: return dml_conv3x3_pool(&o.cpool, s);
     case OP_EXP_RED: return dml_expand_reduce(&o.er, s);
     case OP_CONV_GROUP: return dml_conv_group(&o.grp, o.cfg, s);
-    case OP_PREFETCH: return dml_prefetch(o.pf.p, o.pf.bytes, o.pf.sink, s);
   }
   return -1;
 }
@@ -132,15 +129,6 @@ extern "C" int dml_plan_add_pool(void* p, const DmlPoolArgs* a) {
   ((Plan*)p)->ops.push_back(o);
   return 0;
 }
-extern "C" int dml_plan_add_prefetch(void* p, const void* ptr, long bytes, void* sink) {
-  if (!ptr || bytes < 16 || !sink) { g_err = "dml_plan_add_prefetch: bad arguments"; return -1; }
-  Op o{};
-  o.kind = OP_PREFETCH;
-  o.pf = {ptr, bytes, sink};
-  ((Plan*)p)->ops.push_back(o);
-  return 0;
-}
-
 extern "C" int dml_plan_add_gap(void* p, const void* x, void* y, int N, int HW, int C, int ldx) {
   Op o{};
   o.kind = OP_GAP;

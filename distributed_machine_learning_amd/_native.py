@@ -121,7 +121,6 @@ _SIGS = {
     "dml_plan_add_conv": (C.c_int, [C.c_void_p, C.POINTER(ConvArgs), C.c_int]),
     "dml_plan_add_pool": (C.c_int, [C.c_void_p, C.POINTER(PoolArgs)]),
     "dml_plan_add_gap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
-    "dml_plan_add_prefetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_long, C.c_void_p]),
     "dml_plan_add_softmax_top5": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                             C.c_void_p, C.c_void_p]),
     "dml_plan_add_softmax_top5_split": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,

@@ -426,11 +426,6 @@ class Engine:
 
     def _build_one_plan(self, src: torch.Tensor, result: torch.Tensor):
         g, B, L = self.g, self.batch, self.lib
-        # DML_WPREFETCH=<bytes>: prefetch op before every plain conv whose packed
-        # weights are at least that large (0 = off)
-        self.wprefetch = int(os.environ.get("DML_WPREFETCH", "0"))
-        if self.wprefetch and getattr(self, "_sink", None) is None:
-            self._sink = torch.zeros(256, dtype=torch.int32, device=self.device)
         plan = L.dml_plan_create()
         self.op_names: List[str] = []
         self.op_cfg: Dict[str, int] = {}
@@ -520,12 +515,6 @@ class Engine:
             if isinstance(n, (Conv, Dense, FusedConv)):
                 cfg = self.cfg_overrides.get(n.name, self.tuned.get(n.name, -1))
                 a = self._conv_args(n)
-                wk = self.wdev[n.name][0]
-                if self.wprefetch and wk.numel() * 2 >= self.wprefetch:
-                    # weights read once into MALL / L2 right before the conv (cold K-heavy layers)
-                    N.check(L.dml_plan_add_prefetch(plan, wk.data_ptr(), wk.numel() * 2, self._sink.data_ptr()),
-                            f"plan prefetch {n.name}")
-                    self.op_names.append(f"prefetch:{n.name}")
                 used = N.check(L.dml_plan_add_conv(plan, C.byref(a), cfg), f"plan conv {n.name}")
                 self.op_cfg[n.name] = used
                 self._keep.append(a)
