@@ -6,7 +6,10 @@ the 3x3 convs of ResNet50 run best on 128x128 (2 blocks/CU), the memory-bound
 ``autotune`` times every candidate config on the engine's real buffers once
 per unique shape (a few hundred launches, well under a second) and caches the
 winners in a JSON table keyed by the shape signature, so later processes load
-it instead of re-timing.
+it instead of re-timing. Candidates are timed cold by default (each launch after
+overwriting 512 MiB, so weights and activations come from HBM as inside a
+forward): the warm back-to-back timing picked tiles that lose in the engine
+(DESIGN.md §3 "Cold-cache tuning").
 """
 from __future__ import annotations
 
@@ -78,6 +81,11 @@ def valid_cfgs(a: N.ConvArgs) -> List[int]:
 _scrub = None
 
 
+def _release_scrub() -> None:
+    global _scrub
+    _scrub = None  # the 512 MiB eviction buffer is only needed while timing
+
+
 def _cold() -> bool:
     return os.environ.get("DML_TUNE_COLD", "1") == "1"
 
@@ -139,6 +147,7 @@ def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None,
         except OSError:
             pass
     cache.update(new)
+    _release_scrub()
     return cache
 
 
@@ -225,6 +234,7 @@ def autotune_group(args: List[N.ConvArgs], cfgs: List[int], pools: Sequence[N.Po
             continue
         best = min(best, (t, cfg))
     cache[k] = best[1]
+    _release_scrub()
     if persist:
         try:
             save_cache({k: best[1]})
