@@ -1,0 +1,18 @@
+#!/bin/bash
+# Runtime-environment A/B of the headline bench (interleaved, two rounds).
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # name, env...
+  local n=$1; shift
+  env "$@" timeout -k 10 600 python bench.py --steps 30 --warmup 5 > gpurun_out/env_$n.log 2>&1 \
+    && echo "$n: $(tail -1 gpurun_out/env_$n.log | python -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["models"]["InceptionV3"]["value"], d["verified_top5"])')" \
+    || { tail -20 gpurun_out/env_$n.log; exit 1; }
+}
+for rnd in 1 2; do
+  run base$rnd DML_ENVAB=0
+  run kernarg$rnd HIP_FORCE_DEV_KERNARG=1
+  run nosdma$rnd HSA_ENABLE_SDMA=0
+  run hwq8_$rnd GPU_MAX_HW_QUEUES=8
+done
