@@ -75,13 +75,14 @@ base = forward_ms()
 cur = base
 print(f"baseline split forward {base:.3f} ms", flush=True)
 changes = {}
+table = {}  # the changes as tuning-table entries (shape key -> cfg; shared shapes: last change wins)
 for i, name in enumerate(e0.op_names):
     if time.time() - t_start > args.budget_s:
         print("time budget reached", flush=True)
         break
     c0 = L.dml_plan_get_cfg(plans[0], i)
     n = nodes.get(name)
-    if c0 < 0 or c0 >= 40 or not isinstance(n, (Conv, Dense, FusedConv)):
+    if c0 < 0 or not isinstance(n, (Conv, Dense, FusedConv)):
         continue
     a = e0._conv_args(n)
     alone = []
@@ -103,10 +104,12 @@ for i, name in enumerate(e0.op_names):
         L.dml_plan_set_cfg(p, i, best[1] if best[0] < cur * (1 - args.thresh) else c0)
     if best[0] < cur * (1 - args.thresh):
         changes[name] = best[1]
+        table[tuning.shape_key(a)] = best[1]
         print(f"{name}: cfg {c0} -> {best[1]}  {cur:.3f} -> {best[0]:.3f} ms", flush=True)
         cur = best[0]
 final = forward_ms()
-res = {"model": model, "batch": B, "baseline_ms": round(base, 4), "final_ms": round(final, 4), "changes": changes}
+res = {"model": model, "batch": B, "baseline_ms": round(base, 4), "final_ms": round(final, 4), "changes": changes,
+       "table": table}
 print(json.dumps(res), flush=True)
 if args.out:
     with open(args.out, "w") as f:
