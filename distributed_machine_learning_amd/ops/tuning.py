@@ -72,10 +72,18 @@ NO_RES_CFGS = (34,)  # the residual-epilogue instantiation spills (256x256 tile)
 LATE_RES_CFGS = (56, 57, 58, 59, 60)
 
 
+def _excluded() -> set:
+    """DML_TUNE_EXCLUDE=<cfg,cfg,...>: configs the tuner must not pick (A/B)."""
+    v = os.environ.get("DML_TUNE_EXCLUDE", "")
+    return {int(c) for c in v.split(",") if c.strip()}
+
+
 def valid_cfgs(a: N.ConvArgs) -> List[int]:
     if a.Cout % 8 or a.Cin % 8 or a.ldx % 8 or a.ldy % 8:
         return []
-    return [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)] + (list(LATE_RES_CFGS) if a.res else [])
+    ex = _excluded()
+    cands = [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)] + (list(LATE_RES_CFGS) if a.res else [])
+    return [c for c in cands if c not in ex]
 
 
 _scrub = None
