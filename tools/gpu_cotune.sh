@@ -8,14 +8,15 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 T=distributed_machine_learning_amd/tuning/conv_tuning.json
 cp $T /tmp/tuning_base.json
-for m in ResNet50 InceptionV3; do
-  timeout -k 10 600 python -u tools/cotune.py --model $m --budget_s 300 --out gpurun_out/cotune_$m.json > gpurun_out/cotune_$m.log 2>&1 \
+for m in ${MODELS:-ResNet50 InceptionV3}; do
+  timeout -k 10 600 python -u tools/cotune.py --model $m --budget_s 400 ${COTUNE_ARGS:-} --out gpurun_out/cotune_$m.json > gpurun_out/cotune_$m.log 2>&1 \
     && tail -1 gpurun_out/cotune_$m.log | cut -c1-300 || { tail -20 gpurun_out/cotune_$m.log; exit 1; }
 done
 python - <<'PY'
 import json
 t = json.load(open("/tmp/tuning_base.json"))
-for m in ("ResNet50", "InceptionV3"):
+import os
+for m in os.environ.get("MODELS", "ResNet50 InceptionV3").split():
     t.update(json.load(open(f"gpurun_out/cotune_{m}.json"))["table"])
 json.dump(dict(sorted(t.items())), open("/tmp/tuning_co.json", "w"), indent=0)
 json.dump(dict(sorted(t.items())), open("gpurun_out/conv_tuning_co.json", "w"), indent=0)
