@@ -255,18 +255,27 @@ extern "C" int dml_plan_replay(void* p, hipStream_t s) {
 // Re-point conv op i at tile config cfg (joint tuning of co-scheduled
 // sub-batch plans). Returns the previous cfg, or -1 if op i is not a conv or
 // cfg is not a tile config. A captured graph must be re-captured.
+// tile config of a conv or grouped-conv op (co-tuning: tools/cotune*.py)
 extern "C" int dml_plan_set_cfg(void* p, int i, int cfg) {
   Plan* pl = (Plan*)p;
-  if (i < 0 || i >= (int)pl->ops.size() || pl->ops[i].kind != OP_CONV) { g_err = "dml_plan_set_cfg: not a conv op"; return -1; }
+  if (i < 0 || i >= (int)pl->ops.size() || (pl->ops[i].kind != OP_CONV && pl->ops[i].kind != OP_CONV_GROUP)) {
+    g_err = "dml_plan_set_cfg: not a conv op";
+    return -1;
+  }
   Op& o = pl->ops[i];
-  if (dml_conv_v2_bn(cfg) <= 0) { g_err = "dml_plan_set_cfg: not a tile config"; return -1; }
+  if (o.kind == OP_CONV_GROUP) {
+    if (dml_conv_group_validate(&o.grp, cfg) != 0) return -1;
+  } else if (dml_conv_v2_bn(cfg) <= 0) {
+    g_err = "dml_plan_set_cfg: not a tile config";
+    return -1;
+  }
   const int prev = o.cfg;
   o.cfg = cfg;
   return prev;
 }
 extern "C" int dml_plan_get_cfg(void* p, int i) {
   Plan* pl = (Plan*)p;
-  if (i < 0 || i >= (int)pl->ops.size() || pl->ops[i].kind != OP_CONV) return -1;
+  if (i < 0 || i >= (int)pl->ops.size() || (pl->ops[i].kind != OP_CONV && pl->ops[i].kind != OP_CONV_GROUP)) return -1;
   return pl->ops[i].cfg;
 }
 

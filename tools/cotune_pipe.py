@@ -4,8 +4,8 @@ tools/cotune.py scores a tile change by the split forward alone; in the serving
 pipeline consecutive batches overlap (the next batch's sub-batch streams start
 on their own input events), so a tile that hogs LDS at the end of batch k also
 slows the head of batch k+1. This tool times ``ServingPipeline.run`` itself: for
-each conv op it tries the best-alone candidates (ops/tuning.time_cfg, cold) on
-every plan of both sub-batch engines, re-captures the graphs and keeps a change
+each conv op it tries the best-alone candidates (ops/tuning.time_cfg, cold) —
+for a grouped launch every other grouped tile — on every plan of both sub-batch engines, re-captures the graphs and keeps a change
 only if the pipeline's ms/step improves by more than --thresh. Prints one final
 JSON line whose "table" holds the changes as tuning-table entries.
 
@@ -24,7 +24,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_machine_learning_amd import _native as N  # noqa: E402
 from distributed_machine_learning_amd.models import build_model, canonical_name  # noqa: E402
 from distributed_machine_learning_amd.models.engine import SplitEngine  # noqa: E402
-from distributed_machine_learning_amd.models.graph import Conv, Dense, FusedConv  # noqa: E402
+from distributed_machine_learning_amd.models.graph import Conv, Dense, FusedConv, Pool  # noqa: E402
 from distributed_machine_learning_amd.ops import tuning  # noqa: E402
 from distributed_machine_learning_amd.parallel.dataplane import DESC_FIELDS, DataPlane, init_process_group  # noqa: E402
 from distributed_machine_learning_amd.parallel.pipeline import ServingPipeline  # noqa: E402
@@ -54,6 +54,7 @@ L = N.lib()
 e0 = se.engines[0]
 nodes = {n.name: n for n in e0.g.nodes}
 plans = [p for e in se.engines for p in e.plans]
+groups = {"|".join(m.name for m in grp): grp for grp in e0.conv_groups}  # grouped-launch ops by op name
 
 
 def table(k):
@@ -93,18 +94,29 @@ for i, name in enumerate(e0.op_names):
         break
     c0 = L.dml_plan_get_cfg(e0.plans[0], i)
     n = nodes.get(name)
-    if c0 < 0 or not isinstance(n, (Conv, Dense, FusedConv)):
+    if c0 < 0:
         continue
-    a = e0._conv_args(n)
-    alone = []
-    for c in tuning.valid_cfgs(a):
-        try:
-            alone.append((tuning.time_cfg(a, c), c))
-        except N.NativeError:
-            pass
-    alone.sort()
+    if name in groups:  # grouped launch: every other grouped tile, scored in the pipeline only
+        grp = groups[name]
+        gargs = [e0._conv_args(m) for m in grp if not isinstance(m, Pool)]
+        gpools = [e0._pool_args(m) for m in grp if isinstance(m, Pool)]
+        key = tuning.group_key(gargs, gpools)
+        cands = [c for c in tuning.GROUP_CFGS if c != c0]
+    elif isinstance(n, (Conv, Dense, FusedConv)):
+        a = e0._conv_args(n)
+        key = tuning.shape_key(a)
+        alone = []
+        for c in tuning.valid_cfgs(a):
+            try:
+                alone.append((tuning.time_cfg(a, c), c))
+            except N.NativeError:
+                pass
+        alone.sort()
+        cands = [c for _, c in alone if c != c0][: args.cands]
+    else:
+        continue
     best = (cur, c0)
-    for _, c in [x for x in alone if x[1] != c0][: args.cands]:
+    for c in cands:
         if any(L.dml_plan_set_cfg(p, i, c) < 0 for p in plans):
             continue
         recapture()
@@ -117,7 +129,7 @@ for i, name in enumerate(e0.op_names):
     recapture()
     if keep:
         changes[name] = best[1]
-        entries[tuning.shape_key(a)] = best[1]
+        entries[key] = best[1]
         print(f"{name}: cfg {c0} -> {best[1]}  {cur:.4f} -> {best[0]:.4f} ms/step", flush=True)
         cur = best[0]
 final = ms_per_step()
