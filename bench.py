@@ -53,7 +53,7 @@ def ref_rate(model: str, n: int) -> float:
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=120, help="timed steps (120: >= 100 latency samples for p99)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--models", default="ResNet50,InceptionV3",
                     help="comma list; the first is the headline `value`, the rest are sub-records")
@@ -74,6 +74,16 @@ def parse_args(argv=None):
     ap.add_argument("--trace", default="", help="Chrome-trace JSON of the timed steps ('{rank}' -> rank id)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: gloo dispatch/gather skeleton only (tests the launcher)")
+    ap.add_argument("--no-service", action="store_true",
+                    help="skip the `service` sub-record (BASELINE config 4: the elastic serving product, "
+                         "concurrent ResNet50 + InceptionV3, outputs on)")
+    ap.add_argument("--svc-resnet-images", type=int, default=51200, help="ResNet50 images per GPU (service run)")
+    ap.add_argument("--svc-inception-images", type=int, default=25600,
+                    help="InceptionV3 images per GPU (service run)")
+    ap.add_argument("--svc-outputs", default="/tmp",
+                    help="directory for the service run's output files ('' = outputs off); removed afterwards")
+    ap.add_argument("--kill", action="append", default=[],
+                    help="rank:step - inject a rank kill into the service run (BASELINE config 5; needs --gpus > 1)")
     return ap.parse_args(argv)
 
 
@@ -271,6 +281,10 @@ def main(argv=None) -> int:
         else:
             recs[m] = bench_model(m, B, args, rank, world, device, headline=(i == 0))
 
+    svc = None
+    if not args.dry_run and not args.no_service:
+        svc = bench_service(args, rank, world, device, recs)
+
     if rank == 0:
         head = recs[models[0]]
         out = {
@@ -294,11 +308,33 @@ def main(argv=None) -> int:
                 out[k] = head[k]
         if len(models) > 1:
             out["models"] = {m: recs[m] for m in models[1:]}
+        if svc is not None:
+            out["service"] = svc
         print(json.dumps(out), flush=True)
     import torch.distributed as dist
 
-    dist.destroy_process_group()
+    if dist.is_initialized():
+        dist.destroy_process_group()
     return 0
+
+
+def bench_service(args, rank: int, world: int, device, recs: dict):
+    """BASELINE config 4 (and 5 with --kill): the elastic serving product on
+    every rank - concurrent ResNet50 b256 + InceptionV3 b128 jobs, fair-share
+    with preemption, one control collective per step, outputs written by the
+    ranks (parallel/service_bench.py). Weak scaling: images per GPU fixed."""
+    import torch.distributed as dist
+
+    from distributed_machine_learning_amd.parallel import service_bench
+
+    rdzv, port = service_bench.agree(rank)
+    dist.destroy_process_group()  # the service builds its own epoch-versioned groups
+    rates = {m: r["value"] for m, r in recs.items() if r and "value" in r}
+    out_dir = (os.path.join(args.svc_outputs, os.path.basename(rdzv) + "_outputs") if args.svc_outputs else None)
+    rec = service_bench.run(rank, world, device, rdzv, port, args.svc_resnet_images * world,
+                            args.svc_inception_images * world, dict(DEFAULT_BATCH), out_dir,
+                            kills=service_bench.parse_kills(args.kill), single_rates=rates)
+    return rec
 
 
 if __name__ == "__main__":

@@ -152,12 +152,31 @@ typedef struct {
   int ysub, yH, yW;
 } DmlExpandReduceArgs;
 
+// Whole ResNet50 identity bottleneck block (csrc/kernels/block_fused.hip), C = 4F:
+//   t1 = relu(w1 . x + b1)  (1x1 C -> F),  t2 = relu(w2 * t1 + b2)  (3x3 'same' F -> F),
+//   y  = relu(w3 . t2 + b3 + x)  (1x1 F -> C + identity shortcut); T1/T2 stay on chip.
+typedef struct {
+  const void* x;     // bf16 NHWC [N][H][W][ldx] (C channels): block input and shortcut
+  const void* w1;    // bf16 [>=F][ldw1], K = C
+  const float* b1;   // fp32 [F]
+  const void* w2;    // bf16 [>=F][ldw2], K = 9F in (r, s, c) order
+  const float* b2;   // fp32 [F]
+  const void* w3;    // bf16 [>=C][ldw3], K = F
+  const float* b3;   // fp32 [C]
+  void* y;           // bf16 NHWC [N][H][W][ldy] (C channels), must not alias x
+  int N, H, W, F;
+  int ldx, ldy, ldw1, ldw2, ldw3;
+  long long* stamps;  // diagnostics only (null in the engine): per workgroup 8 x s_memrealtime / s_memtime
+} DmlBlockArgs;
+
 // ---- single-op launches (used by tests and by the plan executor) ----
 int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s);
 int dml_stem_inception(const DmlIncStemArgs* a, hipStream_t s);
 int dml_conv3x3_pool(const DmlConvPoolArgs* a, hipStream_t s);
 int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s);
 int dml_expand_reduce_init(void);
+int dml_block_fused(const DmlBlockArgs* a, hipStream_t s);
+int dml_block_fused_init(void);
 int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2_init(void);
@@ -196,6 +215,7 @@ int dml_plan_add_stem(void* plan, const DmlStemArgs* a);
 int dml_plan_add_inc_stem(void* plan, const DmlIncStemArgs* a);
 int dml_plan_add_conv_pool(void* plan, const DmlConvPoolArgs* a);
 int dml_plan_add_expand_reduce(void* plan, const DmlExpandReduceArgs* a);
+int dml_plan_add_block(void* plan, const DmlBlockArgs* a);
 int dml_plan_size(void* plan);
 int dml_plan_run(void* plan, hipStream_t s);
 int dml_plan_run_range(void* plan, int begin, int end, hipStream_t s);

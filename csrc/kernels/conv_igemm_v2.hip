@@ -458,6 +458,7 @@ extern "C" int dml_conv_v2_init(void) {
 #undef DML_SET
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   if (!rc && dml_expand_reduce_init() != 0) return -1;  // fused block-boundary kernels (bottleneck_fused.hip)
+  if (!rc && dml_block_fused_init() != 0) return -1;    // whole fused bottleneck blocks (block_fused.hip)
   return rc ? -1 : 0;
 }
 

@@ -181,6 +181,20 @@ int main() {
   CHECK(dml_expand_reduce(&er, nullptr) != 0);    // reduce weights shorter than K = 256
   er.ldw1 = 256; er.ldr = 64;
   CHECK(dml_expand_reduce(&er, nullptr) != 0);    // shortcut narrower than 256 channels
+  {  // whole fused bottleneck block: only F = 64, C = 4F, 8-aligned strides, y != x
+    DmlBlockArgs b{};
+    char buf[64];
+    b.x = buf; b.y = buf + 16; b.N = 1; b.H = b.W = 14; b.F = 64;
+    b.ldx = b.ldy = b.ldw1 = 256; b.ldw2 = 576; b.ldw3 = 64;
+    b.F = 128;
+    CHECK(dml_block_fused(&b, nullptr) != 0);      // F = 128 not instantiated
+    b.F = 64; b.ldw2 = 512;
+    CHECK(dml_block_fused(&b, nullptr) != 0);      // 3x3 weights shorter than K = 9F
+    b.ldw2 = 576; b.y = buf;
+    CHECK(dml_block_fused(&b, nullptr) != 0);      // in place: other tiles still read x
+    b.y = buf + 16; b.ldx = 260;
+    CHECK(dml_block_fused(&b, nullptr) != 0);      // unaligned channel stride
+  }
   dml_set_error(nullptr);
   CHECK(std::string(dml_last_error()).empty());
 

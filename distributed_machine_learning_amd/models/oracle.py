@@ -127,6 +127,52 @@ class OracleExecutor:
         t[name][:, coff:coff + y.shape[1]] = y
 
 
+def synthetic_images(n: int, hw, seed: int = 0, noise: float = 24.0) -> torch.Tensor:
+    """uint8 [n, H, W, 3] test images with image-level structure: a random base
+    colour, four random low-frequency colour gratings and pixel noise. IID
+    uniform noise images all have the same statistics, so a random-init
+    network's pooled features (and logits) barely depend on them; these differ
+    image to image the way natural photos do, which makes a numerics check
+    input-sensitive (models/weights.py 'head calibration')."""
+    rng = np.random.default_rng(seed)
+    H, W = hw
+    yy, xx = np.meshgrid(np.linspace(0.0, 1.0, H), np.linspace(0.0, 1.0, W), indexing="ij")
+    out = np.empty((n, H, W, 3), np.uint8)
+    for i in range(n):
+        img = np.zeros((H, W, 3)) + rng.uniform(40, 215, 3)
+        for _ in range(4):
+            fx, fy = rng.uniform(0.5, 6.0, 2)
+            ph = rng.uniform(0.0, 2 * np.pi)
+            amp = rng.uniform(10, 50, 3)
+            img += amp * np.sin(2 * np.pi * (fx * xx + fy * yy) + ph)[..., None]
+        img += rng.uniform(-noise, noise, (H, W, 3))
+        out[i] = np.clip(img, 0, 255).astype(np.uint8)
+    return torch.from_numpy(out)
+
+
+@torch.no_grad()
+def calibrate_head(g: Graph, w: Weights, x: torch.Tensor, scale: float = 3.0) -> Weights:
+    """Per-class standardisation of the classifier over the calibration batch:
+    logit_c <- (logit_c - mean_c) * scale / std_c (folded into the Dense kernel
+    and bias). A trained classifier's logits vary with the image by several
+    units per class; a random-init head's vary by a small fraction of a large
+    common offset, so top-1 would be the same class for every image."""
+    dense = [n for n in g.nodes if isinstance(n, Dense)]
+    if not dense:
+        return w
+    d = dense[-1]
+    out = OracleExecutor(g, w).forward(x, keep=True)
+    f = out[d.inp].flatten(1)
+    k = torch.from_numpy(w[f"{d.name}/kernel"]).float()
+    b = torch.from_numpy(w[f"{d.name}/bias"]).float()
+    z = f @ k + b
+    mu, sd = z.mean(0), z.std(0).clamp_min(1e-6)
+    w = dict(w)
+    w[f"{d.name}/kernel"] = (k * (scale / sd)).numpy().astype(np.float32)
+    w[f"{d.name}/bias"] = ((b - mu) * (scale / sd)).numpy().astype(np.float32)
+    return w
+
+
 @torch.no_grad()
 def calibrate_bn(g: Graph, w: Weights, x: torch.Tensor) -> Weights:
     """Set every BN's mean/var to the batch statistics of its conv output on x

@@ -15,7 +15,7 @@ import torch
 from .. import _native as N
 
 __all__ = ["conv2d_nhwc", "conv_group", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight",
-           "resnet_stem", "inception_stem", "conv3x3_pool", "expand_reduce"]
+           "resnet_stem", "inception_stem", "conv3x3_pool", "expand_reduce", "block_fused"]
 
 
 def _r(x, m):
@@ -233,6 +233,27 @@ def expand_reduce(x: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, res: Opti
     N.check(N.lib().dml_expand_reduce(C.byref(a), N.stream_ptr()), "dml_expand_reduce")
     y._keep = (b3p, b1p)
     return y, z
+
+
+def block_fused(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
+                w3: torch.Tensor, b3: torch.Tensor, out: Optional[torch.Tensor] = None,
+                stamps: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """A whole identity bottleneck block in one kernel (csrc/kernels/block_fused.hip):
+    y = relu(1x1(F -> C) of relu(3x3(F -> F) of relu(1x1(C -> F) of x)) + x), C = 4F.
+    x: bf16 NHWC [N, H, W, C]; w1 [>=F][>=C], w2 [>=F][>=9F] (r, s, c), w3 [>=C][>=F]
+    packed (pack_weight); biases fp32. Returns bf16 NHWC [N, H, W, C]."""
+    n, h, w, c = x.shape
+    f = c // 4
+    y = out if out is not None else torch.empty_like(x)
+    bs = [b.to(x.device, torch.float32).contiguous() for b in (b1, b2, b3)]
+    assert x.is_contiguous() and y.is_contiguous() and all(t.is_contiguous() for t in (w1, w2, w3))
+    assert w1.shape[0] >= f and w2.shape[0] >= f and w3.shape[0] >= c and bs[0].numel() >= f and bs[2].numel() >= c
+    a = N.BlockArgs(x.data_ptr(), w1.data_ptr(), bs[0].data_ptr(), w2.data_ptr(), bs[1].data_ptr(), w3.data_ptr(),
+                    bs[2].data_ptr(), y.data_ptr(), n, h, w, f, x.shape[-1], y.shape[-1], w1.shape[1], w2.shape[1],
+                    w3.shape[1], stamps.data_ptr() if stamps is not None else None)
+    N.check(N.lib().dml_block_fused(C.byref(a), N.stream_ptr()), "dml_block_fused")
+    y._keep = bs
+    return y
 
 
 def fused_conv1x1(x: torch.Tensor, members, stride: int = 1, cfg: int = -1) -> None:

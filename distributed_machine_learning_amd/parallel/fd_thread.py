@@ -23,9 +23,9 @@ log = logging.getLogger(__name__)
 class RankFailureDetector:
     def __init__(self, grank: int, world: int, base_port: int, on_dead: Callable[[int], None],
                  host: str = "127.0.0.1", period: float = 0.1, ping_timeout: float = 0.1,
-                 suspect_timeout: float = 0.5):
+                 suspect_timeout: float = 0.5, on_alive: Optional[Callable[[int], None]] = None):
         self.grank, self.world, self.base, self.host = grank, world, base_port, host
-        self.on_dead = on_dead
+        self.on_dead, self.on_alive = on_dead, on_alive
         self.period, self.ping_timeout, self.suspect_timeout = period, ping_timeout, suspect_timeout
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self.ready = threading.Event()
@@ -39,8 +39,13 @@ class RankFailureDetector:
         return int(name.rsplit(":", 1)[1]) - self.base
 
     def start(self) -> "RankFailureDetector":
+        import atexit
+
         self.thread.start()
         self.ready.wait(10)
+        # a process that leaves without stop() (an exception unwinding the rank)
+        # must not tear the daemon thread's loop down with its tasks pending
+        atexit.register(self.stop)
         return self
 
     def _main(self) -> None:
@@ -71,7 +76,16 @@ class RankFailureDetector:
                 log.warning("rank %d: SWIM confirmed rank %d dead", self.grank, r)
                 self.on_dead(r)
 
+        def joined(name: str) -> None:  # a dead rank's restarted process (higher incarnation)
+            r = self.rank_of(name)
+            if r in self.dead:
+                self.dead.discard(r)
+                log.warning("rank %d: SWIM saw rank %d rejoin", self.grank, r)
+                if self.on_alive is not None:
+                    self.on_alive(r)
+
         ml.on_fail.append(failed)
+        ml.on_join.append(joined)
         self.fd = FailureDetector(ep, ml, period=self.period, ping_timeout=self.ping_timeout)
         ep.start()
         self.fd.start()

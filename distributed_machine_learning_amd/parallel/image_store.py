@@ -125,6 +125,49 @@ class HbmImageStore:
         self.replicated += len(dst)
         return len(dst)
 
+    # ----------------------------------------------------------- backfill --
+    def backfill(self, names: Sequence[str], eg, root: int) -> int:
+        """(collective) Copy the decoded images of ``names`` that group rank
+        ``root`` holds into every other rank's arena with ONE broadcast over
+        the data group (RCCL over xGMI on a GPU node): a rank that re-joins the
+        job (new communicator epoch) gets the queued jobs' images from a
+        survivor's HBM instead of fetching and decoding them again. Ranks that
+        already hold an image keep it. Returns the images copied here."""
+        want = [n for n in dict.fromkeys(names) if not self._synthetic(n)]
+        if not want or eg.world == 1:
+            return 0
+        me = eg.rank
+        flags = torch.zeros(len(want), dtype=torch.int32)
+        if me == root:
+            flags = torch.tensor([1 if n in self.index else 0 for n in want], dtype=torch.int32)
+        fl = flags.to(self.device)
+        eg.broadcast_data(fl, root)
+        have = [n for n, f in zip(want, fl.cpu().tolist()) if f]
+        if not have:
+            return 0
+        rows = torch.empty((len(have), *self.hw, 3), dtype=torch.uint8, device=self.device)
+        if me == root:
+            src = torch.tensor([self.index[n] for n in have], device=self.device)
+            torch.index_select(self.arena, 0, src, out=rows)
+        eg.broadcast_data(rows, root)
+        if me == root:
+            return 0
+        keep = set(names)
+        dst, src = [], []
+        for i, n in enumerate(have):
+            if n in self.index:
+                continue
+            self.failed.discard(n)
+            s = self._alloc(keep)
+            self.index[n] = s
+            dst.append(s)
+            src.append(i)
+        if dst:
+            self.arena.index_copy_(0, torch.tensor(dst, device=self.device),
+                                   rows.index_select(0, torch.tensor(src, device=self.device)))
+        self.replicated += len(dst)
+        return len(dst)
+
     # -------------------------------------------------------------- slots --
     def slots(self, names: Sequence[str], load: Optional[Callable] = None) -> Tuple[List[int], List[str]]:
         """Arena slots of ``names``; images never replicated are loaded locally

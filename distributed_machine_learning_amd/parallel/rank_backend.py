@@ -1,0 +1,307 @@
+"""Per-rank inference backends of the collective service (parallel/service.py).
+
+A backend runs one batch (a list of image names) of one model on this rank:
+``launch(model, names, slot)`` returns ``(rows, event)`` where ``rows`` is a
+[2, cap, 5] int32 tensor (top-5 class ids; the fp32 probabilities bit-cast into
+the second plane) that is valid once ``event`` has fired (``None`` = already
+valid). Rows of images that could not be fetched or decoded carry class id -1.
+GPU backends launch asynchronously into one of ``SLOTS`` result slots and copy
+the rows into pinned host memory in stream order, so the service polls an
+event instead of waiting on the GPU.
+
+Image names: ``synthetic:<i>`` (seeded arena images), ``<name>`` or
+``<name>@<version>`` (a store image pinned to one version by the coordinator at
+submit time, so a later PUT of a new version never changes what a queued job
+reads; reference worker.py:1323-1366 fetched the latest version at task time).
+"""
+from __future__ import annotations
+
+import hashlib
+import logging
+import time
+from collections import OrderedDict
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..serving.jobs import MODELS
+from ..serving.output import VERSION_SEP
+
+log = logging.getLogger(__name__)
+MODEL_IDS = {m: i for i, m in enumerate(MODELS)}
+SYNTH = "synthetic:"
+SLOTS = 2   # batches a GPU rank has launched at once (engine source / result slots)
+
+
+def synthetic_names(n: int) -> List[str]:
+    return [f"{SYNTH}{i}" for i in range(n)]
+
+
+def split_version(name: str) -> Tuple[str, Optional[int]]:
+    """'3.jpeg@2' -> ('3.jpeg', 2); '3.jpeg' -> ('3.jpeg', None)."""
+    head, sep, tail = name.rpartition(VERSION_SEP)
+    if sep and tail.isdigit():
+        return head, int(tail)
+    return name, None
+
+
+class RankBackend:
+    cap: int = 256
+    device = torch.device("cpu")
+    slots: int = SLOTS      # batches launched at once (GPU: the engines' source / result slots)
+
+    def launch(self, model: str, names: Sequence[str], slot: int):
+        raise NotImplementedError
+
+    def run(self, model: str, names: Sequence[str]) -> torch.Tensor:
+        res, ev = self.launch(model, names, 0)
+        if ev is not None:
+            ev.synchronize()
+        return res
+
+    # collective hooks (every rank calls them in the same order)
+    def on_submit(self, model: str, names: Sequence[str], eg) -> int:
+        return 0
+
+    def backfill(self, model: str, names: Sequence[str], eg, root: int) -> int:
+        return 0
+
+    def drain(self) -> None:
+        """Wait for every launched batch (failure recovery reuses the slots)."""
+
+
+class HostRankBackend(RankBackend):
+    """A serving.inference backend (fake / cpu) behind the rank interface:
+    decode-once per image name (LRU cache), synchronous predict. The same
+    backend classes as the host cluster's workers, so both serving modes produce
+    identical outputs for the same images. Synthetic names decode from their own
+    name bytes; failed images get class id -1 in their result row."""
+
+    slots = 8   # synchronous: a launch has finished when it returns
+
+    def __init__(self, backend, loader: Optional[Callable] = None, cap: int = 256, delay_per_image: float = 0.0,
+                 cache_images: int = 4096):
+        self.be, self.loader, self.cap, self.delay = backend, loader, cap, delay_per_image
+        self.cache: "OrderedDict[Tuple[str, str], np.ndarray]" = OrderedDict()
+        self.cache_images = cache_images
+
+    def _blobs(self, names: List[str]) -> Dict[str, Optional[bytes]]:
+        out = {n: n.encode() for n in names if n.startswith(SYNTH)}
+        rest = [n for n in names if not n.startswith(SYNTH)]
+        if rest:
+            out.update(self.loader(rest) if self.loader else {n: None for n in rest})
+        return out
+
+    def launch(self, model, names, slot):
+        if len(names) > self.cap:
+            raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
+        if self.delay:
+            time.sleep(self.delay * len(names))
+        missing = [n for n in dict.fromkeys(names) if (model, n) not in self.cache]
+        if missing:
+            blobs = self._blobs(missing)
+            for n in missing:  # keyed by the full (versioned) name: a new version is a new entry
+                b = blobs.get(n)
+                try:
+                    self.cache[(model, n)] = self.be.decode_batch(model, [b])[0] if b is not None else None
+                except Exception as e:
+                    log.warning("decode of %s failed: %s", n, e)
+                    self.cache[(model, n)] = None
+            while len(self.cache) > self.cache_images:
+                self.cache.popitem(last=False)
+        imgs, ok = [], []
+        for i, n in enumerate(names):
+            im = self.cache.get((model, n))
+            if im is not None:
+                self.cache.move_to_end((model, n))
+                imgs.append(im)
+                ok.append(i)
+        out = torch.zeros((2, self.cap, 5), dtype=torch.int32)
+        out[0, :len(names)] = -1
+        if ok:
+            idx, p = self.be.predict(model, np.stack(imgs))
+            rows = torch.tensor(ok, dtype=torch.long)
+            out[0, rows] = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32))
+            out[1, rows] = torch.from_numpy(np.ascontiguousarray(p, dtype=np.float32)).view(torch.int32)
+        return out, None
+
+
+class FakeRankBackend(HostRankBackend):
+    """Deterministic pseudo-results (serving.inference.FakeBackend), optional
+    per-image delay (CPU tests)."""
+
+    def __init__(self, cap: int = 16, delay_per_image: float = 0.0, loader: Optional[Callable] = None):
+        from ..serving.inference import FakeBackend
+
+        super().__init__(FakeBackend(), loader=loader, cap=cap, delay_per_image=delay_per_image)
+
+
+class StoreRankBackend(RankBackend):
+    """CPU stand-in of GpuRankBackend's data path for multi-rank tests: the same
+    replicated image store (parallel/image_store.py, on a CPU device, all-gather
+    and backfill broadcast over the data group) feeding a deterministic
+    'classifier' of the image bytes (top-5 = a hash of the pixels). Exercises
+    decode-once replication, version pinning and rejoin backfill without a GPU."""
+
+    slots = 8   # synchronous
+
+    def __init__(self, loader: Optional[Callable] = None, cap: int = 16, hw=(8, 8), arena_images: int = 512,
+                 n_synth: int = 16, delay_per_image: float = 0.0):
+        from .image_store import HbmImageStore
+
+        self.cap, self.loader, self.delay = cap, loader, delay_per_image
+        self.arenas = {m: HbmImageStore(arena_images, hw, torch.device("cpu"), n_synth=n_synth,
+                                        seed=1000 + MODEL_IDS[m]) for m in MODELS}
+        self.launched = 0
+
+    def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
+        hw = self.arenas[model].hw
+        blobs = self.loader(names) if self.loader else {}
+        out: Dict[str, Optional[np.ndarray]] = {}
+        for n in names:
+            b = blobs.get(n)
+            if b is None:
+                out[n] = None
+                continue
+            h = hashlib.sha256(b).digest()
+            out[n] = np.frombuffer((h * (hw[0] * hw[1] * 3 // 32 + 1))[:hw[0] * hw[1] * 3],
+                                   np.uint8).reshape(*hw, 3).copy()
+        return out
+
+    def on_submit(self, model, names, eg) -> int:
+        return self.arenas[model].replicate(names, lambda ns: self._load(model, ns), rank=eg.rank, world=eg.world,
+                                            gather=eg.all_gather_data)
+
+    def backfill(self, model, names, eg, root) -> int:
+        return self.arenas[model].backfill(names, eg, root)
+
+    @staticmethod
+    def classify(img: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        h = hashlib.sha256(img.tobytes()).digest()
+        ids = np.frombuffer(h[:20], np.uint32) % 1000
+        p = np.sort(np.frombuffer(h[12:32], np.uint8).astype(np.float32) / 1275.0)[::-1][:5]
+        return ids[:5].astype(np.int32), p.copy()
+
+    def launch(self, model, names, slot):
+        if len(names) > self.cap:
+            raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
+        if self.delay:
+            time.sleep(self.delay * len(names))
+        arena = self.arenas[model]
+        slots, failed = arena.slots(list(names), lambda ns: self._load(model, ns))
+        bad = set(failed)
+        out = torch.zeros((2, self.cap, 5), dtype=torch.int32)
+        for i, (n, s) in enumerate(zip(names, slots)):
+            if n in bad:
+                out[0, i] = -1
+                continue
+            ids, p = self.classify(arena.arena[s].numpy())
+            out[0, i] = torch.from_numpy(ids)
+            out[1, i] = torch.from_numpy(p).view(torch.int32)
+        self.launched += 1
+        return out, None
+
+
+class GpuRankBackend(RankBackend):
+    """Native engines for both models resident in this GPU's HBM, fed from
+    per-model HBM image stores (parallel/image_store.py: store images decoded
+    once per job and replicated to every rank over the data group — RCCL —
+    plus seeded synthetic images). A batch is gathered from the store into the
+    engine's source slot on the compute stream, in order (no PCIe copy per
+    batch, nothing for another queue to starve); its top-5 rows are copied
+    into pinned host memory on the same stream, then an event is recorded. A
+    batch larger than the engine's batch runs as several engine passes into
+    consecutive result rows.
+
+    Stream order is the only synchronisation of the arena: replication
+    (``on_submit``), backfill, the local fallback decode in ``launch`` and every
+    batch gather run on ``self.stream``, so a gather always reads what the
+    writes before it left, and an eviction write never overtakes a gather
+    queued before it."""
+
+    def __init__(self, device: torch.device, batch_sizes: Dict[str, int], cap: int = 0, arena_images: int = 8192,
+                 n_synth: int = 512, seed: int = 0, models: Sequence[str] = MODELS, splits: int = 2,
+                 loader: Optional[Callable] = None, decode_threads: int = 8):
+        from concurrent.futures import ThreadPoolExecutor
+
+        from ..models import build_model
+        from ..models.engine import Engine, SplitEngine
+        from .image_store import HbmImageStore
+
+        self.device = device
+        self.cap = cap or max(batch_sizes.values())
+        self.loader = loader
+        self.engines, self.arenas = {}, {}
+        self.stream = torch.cuda.Stream(device)
+        self.pool = ThreadPoolExecutor(max_workers=decode_threads)
+        for m in models:
+            g, w = build_model(m, seed=seed, calibrate=True)
+            b = batch_sizes[m]
+            if splits > 1 and b % splits == 0:
+                self.engines[m] = SplitEngine(g, w, batch=b, device=str(device), src_slots=SLOTS, splits=splits)
+            else:
+                self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=SLOTS)
+            self.arenas[m] = HbmImageStore(max(arena_images, n_synth + 2 * self.cap), g.input_hw, device,
+                                           n_synth=n_synth, seed=1000 + MODEL_IDS[m])
+            self.engines[m].capture(self.stream)  # graphs now, before the service's first collective
+        self.out = [torch.zeros((2, self.cap, 5), dtype=torch.int32, device=device) for _ in range(SLOTS)]
+        self.host = [torch.zeros((2, self.cap, 5), dtype=torch.int32).pin_memory() for _ in range(SLOTS)]
+        self.ev_done = [torch.cuda.Event() for _ in range(SLOTS)]
+
+    def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
+        from ..serving.inference import load_image
+
+        blobs = self.loader(names) if self.loader else {}
+        hw = self.arenas[model].hw
+
+        def dec(n):
+            b = blobs.get(n)
+            if b is None:
+                return n, None
+            try:
+                return n, load_image(b, hw)
+            except Exception as e:  # undecodable file -> reported as failed
+                log.warning("decode of %s failed: %s", n, e)
+                return n, None
+        return dict(self.pool.map(dec, names))
+
+    def on_submit(self, model: str, names: Sequence[str], eg) -> int:
+        """(collective, every rank) decode this rank's share of the job's new
+        images and all-gather all shares into every rank's HBM store — on the
+        compute stream, ahead of every later batch gather."""
+        with torch.cuda.stream(self.stream):
+            return self.arenas[model].replicate(names, lambda ns: self._load(model, ns), rank=eg.rank,
+                                                world=eg.world, gather=eg.all_gather_data)
+
+    def backfill(self, model: str, names: Sequence[str], eg, root: int) -> int:
+        """(collective) a re-joined rank receives the survivors' decoded images."""
+        with torch.cuda.stream(self.stream):
+            return self.arenas[model].backfill(names, eg, root)
+
+    def launch(self, model, names, slot):
+        if len(names) > self.cap:
+            raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
+        eng, arena = self.engines[model], self.arenas[model]
+        s = self.stream
+        out = self.out[slot]
+        B = eng.batch
+        with torch.cuda.stream(s):
+            # images never replicated (standalone use, or evicted) are decoded
+            # here; their arena writes are ordered before the gathers below
+            slots, failed = arena.slots(list(names), lambda ns: self._load(model, ns))
+            for off in range(0, len(slots), B):  # one engine pass per B images: never truncated
+                chunk = slots[off:off + B]
+                arena.gather_into(eng.srcs[slot], chunk)
+                eng.run(s, use_graph=True, slot=slot)
+                out[:, off:off + len(chunk)].copy_(eng.results[slot][:, :len(chunk)])
+            if failed:  # unfetchable / undecodable images: class id -1 marks the row failed
+                bad = set(failed)
+                rows = torch.tensor([i for i, n in enumerate(names) if n in bad], dtype=torch.long)
+                out[0].index_fill_(0, rows.pin_memory().to(self.device, non_blocking=True), -1)
+            self.host[slot].copy_(out, non_blocking=True)
+            self.ev_done[slot].record(s)
+        return self.host[slot], self.ev_done[slot]
+
+    def drain(self) -> None:
+        self.stream.synchronize()

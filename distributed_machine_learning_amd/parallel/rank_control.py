@@ -1,0 +1,311 @@
+"""This rank's host control plane (UDP, never RCCL) for the collective service.
+
+Reference: every VM ran the failure detector, the SDFS replica, the leader's
+handlers and the CLI in one asyncio process (worker.py:2036-2044, 887-1059).
+Here each GPU rank runs a cluster Node with role "rank" in a daemon thread with
+its own event loop; the serve loop (parallel/service.py) talks to it through
+thread-safe hooks.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import threading
+import time
+from typing import Callable, Dict, List, Optional
+
+from ..serving.jobs import Batch
+from .rank_backend import split_version, synthetic_names
+
+log = logging.getLogger(__name__)
+
+
+class RankControl:
+    """This rank's host control plane, in a daemon thread with its own asyncio
+    loop: a cluster Node with role "rank" (SWIM membership -> dead ranks for the
+    elastic group, bully election -> store leader = coordinator, the replicated
+    store with its TCP blob plane) plus the job-service request handlers the
+    reference leader served (SUBMIT_JOB_REQUEST, C1, C2, C3 = SET_BATCH_SIZE,
+    C5 = GET_ASSIGNMENTS, JOB_STATUS; worker.py:887-1059). Requests reach the
+    serve loop through its inbox; replies go out once the request's log record
+    has been broadcast (committed on every rank)."""
+
+    def __init__(self, grank: int, world: int, base_port: int, store_dir: str, host: str = "127.0.0.1",
+                 period: float = 0.1, ping_timeout: float = 0.1, suspect_timeout: float = 0.6,
+                 replication: int = 4, on_dead: Optional[Callable[[int], None]] = None,
+                 on_alive: Optional[Callable[[int], None]] = None, rejoin: bool = False):
+        self.grank, self.world, self.base, self.host = grank, world, base_port, host
+        self.store_dir, self.replication = store_dir, replication
+        self.period, self.ping_timeout, self.suspect_timeout = period, ping_timeout, suspect_timeout
+        self.on_dead, self.on_alive, self.rejoin = on_dead, on_alive, rejoin
+        self.svc = None  # the CollectiveService it serves
+        self.loop: Optional[asyncio.AbstractEventLoop] = None
+        self.node = None
+        self.ready = threading.Event()
+        self.dead: set = set()
+        self.thread = threading.Thread(target=self._main, daemon=True, name=f"rank-control-{grank}")
+
+    def addr(self, g: int) -> str:
+        return f"{self.host}:{self.base + g}"
+
+    def rank_of(self, name: str) -> Optional[int]:
+        try:
+            return int(name.rsplit(":", 1)[1]) - self.base
+        except (ValueError, IndexError):
+            return None
+
+    # ------------------------------------------------------------ thread --
+    def start(self, timeout: float = 30.0) -> "RankControl":
+        import atexit
+
+        atexit.register(self.stop)  # never tear the loop down with its tasks pending (see fd_thread)
+        self.thread.start()
+        if not self.ready.wait(timeout):
+            raise RuntimeError("rank control plane did not start")
+        return self
+
+    def _main(self) -> None:
+        self.loop = asyncio.new_event_loop()
+        asyncio.set_event_loop(self.loop)
+        self.loop.create_task(self._run())
+        self.loop.run_forever()
+        pending = [t for t in asyncio.all_tasks(self.loop) if not t.done()]
+        for t in pending:
+            t.cancel()
+        if pending:
+            self.loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
+        self.loop.close()
+
+    async def _run(self) -> None:
+        from ..cluster.frames import MsgType
+        from ..serving.node import Node, NodeConfig
+
+        cfg = NodeConfig(host=self.host, port=self.base + self.grank, role="rank", seeds=[self.addr(0)],
+                         store_dir=self.store_dir, period=self.period, ping_timeout=self.ping_timeout,
+                         suspect_timeout=self.suspect_timeout, cleanup_time=30.0, replication=self.replication,
+                         meta={"prio": self.grank, "rank": self.grank})
+        self.node = n = await Node(cfg).start()
+        on = n.ep.on
+        on(MsgType.SUBMIT_JOB_REQUEST, self._on_submit)
+        on(MsgType.SET_BATCH_SIZE, self._on_batch_size)
+        on(MsgType.GET_C1_COMMAND, self._on_c1)
+        on(MsgType.GET_C2_COMMAND, self._on_c2)
+        on(MsgType.GET_ASSIGNMENTS, self._on_c5)
+        on(MsgType.JOB_STATUS, self._on_status)
+        on(MsgType.FETCH_INTRODUCER, self._on_fetch_leader)   # every rank is an introducer for clients
+        n.ml.on_fail.append(self._member_failed)
+        n.ml.on_join.append(self._member_joined)
+        await n.join()
+        # every rank knows the static job membership: once all have joined, the
+        # bully election settles on the highest rank (= the collective
+        # coordinator); serving starts only then, so store requests of the first
+        # steps already reach the right leader
+        want = self.addr(self.world - 1)
+        if self.rejoin:  # a restarted rank: the running job's leader stays; learn it by joining
+            for _ in range(200):
+                if n.leader() is not None:
+                    break
+                await asyncio.sleep(0.05)
+            self.ready.set()
+            return
+        for _ in range(400):
+            if len([m for m in n.ml.alive() if (n.ml.get(m).meta or {}).get("role") == "rank"]) >= self.world:
+                break
+            await asyncio.sleep(0.05)
+        for _ in range(400):
+            if n.leader() == want:
+                break
+            if not n.election.in_election:
+                n.election.trigger()
+            await asyncio.sleep(0.05)
+        self.ready.set()
+
+    def _member_failed(self, name: str) -> None:
+        g = self.rank_of(name)
+        if g is not None and 0 <= g < self.world and g not in self.dead:
+            self.dead.add(g)
+            log.warning("rank %d: SWIM confirmed rank %d dead", self.grank, g)
+            if self.on_dead is not None:
+                self.on_dead(g)
+
+    def _member_joined(self, name: str) -> None:
+        """SWIM: a rank that had died is alive again (a restarted process)."""
+        g = self.rank_of(name)
+        if g is not None and 0 <= g < self.world and g in self.dead:
+            self.dead.discard(g)
+            log.warning("rank %d: SWIM saw rank %d rejoin", self.grank, g)
+            if self.on_alive is not None:
+                self.on_alive(g)
+
+    def stop(self) -> None:
+        if self.loop is None or not self.thread.is_alive():
+            return
+
+        async def _shutdown():
+            try:
+                await self.node.stop()
+            except Exception:
+                pass
+            tasks = [t for t in asyncio.all_tasks() if t is not asyncio.current_task()]
+            for t in tasks:
+                t.cancel()
+            await asyncio.gather(*tasks, return_exceptions=True)
+        try:
+            asyncio.run_coroutine_threadsafe(_shutdown(), self.loop).result(timeout=5)
+        except Exception:
+            pass
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self.thread.join(timeout=5)
+
+    # ------------------------------------------------------- serve hooks --
+    def attach(self, svc) -> None:
+        self.svc = svc
+
+    def call(self, coro, timeout: float = 30.0):
+        """Run a coroutine on the control loop from the serve thread."""
+        return asyncio.run_coroutine_threadsafe(coro, self.loop).result(timeout)
+
+    def committed(self, replies: List[Optional[Callable]], results: List[dict]) -> None:
+        for cb, r in zip(replies, results):
+            if cb is not None:
+                self.loop.call_soon_threadsafe(cb, r)
+
+    def jobs_progress(self, batches: List[Batch]) -> None:
+        """Tell requesters whose job just finished (SUBMIT_JOB_REQUEST_SUCCESS)."""
+        from ..cluster.frames import MsgType
+
+        seen = set()
+        for b in batches:
+            j = self.svc.coord.jobs.jobs.get(b.job_id)
+            if j is not None and j.done and j.job_id not in seen and ":" in j.requester:  # a node, not "local"
+                seen.add(j.job_id)
+                self.loop.call_soon_threadsafe(
+                    lambda jj=j: self.loop.create_task(
+                        self.node.ep.send(jj.requester, MsgType.SUBMIT_JOB_REQUEST_SUCCESS, {"jobid": jj.job_id})))
+
+    def became_coordinator(self, previous: int) -> None:
+        log.warning("rank %d: now the coordinator (was rank %d)", self.grank, previous)
+        # requesters of jobs that finished while the old coordinator was dying are told again
+        done = [j for j in self.svc.coord.jobs.jobs.values() if j.done]
+        self.jobs_progress([Batch(j.job_id, 0, j.model, []) for j in done])
+
+    def store_put(self, name: str, data: bytes, deadline_s: float = 60.0) -> None:
+        """PUT into the store, retried across a store-leader change (the leader
+        is the coordinator rank, which is what fails over)."""
+        t0, err = time.monotonic(), ""
+        while time.monotonic() - t0 < deadline_s:
+            try:
+                ok, err = self.call(self.node.store.put(data, name), timeout=30)
+            except Exception as e:  # leader unreachable mid-failover
+                ok, err = False, str(e)
+            if ok:
+                return
+            time.sleep(0.1)
+        raise RuntimeError(f"store put {name}: {err}")
+
+    def store_loader(self, names: List[str]) -> Dict[str, Optional[bytes]]:
+        """Fetch store images; ``name@v`` is that version exactly (pinned at submit)."""
+        async def fetch_all():
+            sem = asyncio.Semaphore(16)
+
+            async def one(nm):
+                base, ver = split_version(nm)
+                async with sem:
+                    if self.node.local.has(base, ver):
+                        return nm, self.node.local.get_bytes(base, ver)
+                    got = await self.node.store.get(base, ver)
+                    return nm, None if got is None else got[1]
+            return dict(await asyncio.gather(*(one(nm) for nm in names)))
+        return self.call(fetch_all(), timeout=120)
+
+    def pin_versions(self, names: List[str]) -> List[str]:
+        """(coordinator, control thread) name -> name@latest-version from the
+        store metadata, so every rank reads the same bytes for the whole job
+        (reference: the latest version at task time, worker.py:1323-1366)."""
+        meta = self.node.store.meta
+        out = []
+        for nm in names:
+            v = meta.latest_version(nm)
+            out.append(f"{nm}@{v}" if v and v > 0 else nm)
+        return out
+
+    # ----------------------------------------------------------- handlers --
+    async def _on_fetch_leader(self, fr) -> None:
+        """Reference FETCH_INTRODUCER (introduce process/worker.py:55-58): any rank
+        tells a client who leads, once the election has settled."""
+        from ..cluster.frames import MsgType
+
+        if self.ready.is_set() and self.node.leader() is not None:
+            await self.node.ep.reply(fr, MsgType.FETCH_INTRODUCER_ACK, {"introducer": self.node.leader()})
+
+    def _active(self) -> bool:
+        return self.svc is not None and self.svc.is_coordinator()
+
+    async def _on_submit(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if not self._active():
+            return  # not the coordinator: the client retries at the elected leader
+        p = fr.payload
+        model = p["model"]
+        n = int(p["images_count"])
+        if p.get("synthetic"):
+            names = synthetic_names(n)
+        else:
+            from ..serving.jobs import pick_images
+
+            names = self.pin_versions(pick_images(sorted(self.node.store.meta.matching("*.jpeg")), n))
+
+        def reply(res, fr=fr):
+            self.loop.create_task(self.node.ep.reply(fr, MsgType.SUBMIT_JOB_REQUEST_ACK, res))
+            if res.get("batches") == 0:
+                self.loop.create_task(self.node.ep.send(fr.sender, MsgType.SUBMIT_JOB_REQUEST_SUCCESS,
+                                                        {"jobid": res["jobid"]}))
+        self.svc.submit_local(model, images=names, requester=fr.sender, reply=reply)
+
+    async def _on_batch_size(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if not self._active():
+            return
+
+        def reply(res, fr=fr):
+            if fr.seq:
+                self.loop.create_task(self.node.ep.reply(fr, MsgType.SET_BATCH_SIZE_ACK, res))
+        self.svc.set_batch_size(fr.payload["model"], int(fr.payload["batch_size"]), reply=reply)
+
+    async def _on_c1(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if self._active():
+            with self.svc.coord.lock:
+                c1 = self.svc.coord.metrics.c1()
+            await self.node.ep.reply(fr, MsgType.GET_C1_COMMAND_ACK, {"c1": c1})
+
+    async def _on_c2(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if self._active():
+            with self.svc.coord.lock:
+                p = self.svc.coord.metrics.c2_reference_payload()
+                p["detail"] = self.svc.coord.metrics.c2()
+            await self.node.ep.reply(fr, MsgType.GET_C2_COMMAND_ACK, p)
+
+    async def _on_c5(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if self._active():
+            with self.svc.coord.lock:
+                a = self.svc.coord.assignments()
+            await self.node.ep.reply(fr, MsgType.GET_ASSIGNMENTS_ACK, {"assignments": a})
+
+    async def _on_status(self, fr) -> None:
+        from ..cluster.frames import MsgType
+
+        if not self._active():
+            return
+        with self.svc.coord.lock:
+            j = self.svc.coord.jobs.jobs.get(int(fr.payload["jobid"]))
+            st = {"jobid": fr.payload["jobid"], "known": j is not None, "done": bool(j and j.done),
+                  "batches_done": j.batches_done if j else 0, "batches_total": j.batches_total if j else 0}
+        await self.node.ep.reply(fr, MsgType.JOB_STATUS_ACK, st)

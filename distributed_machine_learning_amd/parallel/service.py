@@ -1,65 +1,74 @@
-"""Elastic multi-GPU serving: one process per GPU, RCCL data plane, a
-REPLICATED coordinator, SWIM liveness, the reference's CLI and store.
+"""Elastic multi-GPU serving: one process per GPU, a REPLICATED coordinator, one
+control collective per step, per-rank output writing, SWIM liveness, the
+reference's CLI and store.
 
 Reference: the leader (H1) owns all job state and relays submits/ACKs to one
-hard-coded standby (H2) over UDP (worker.py:176-495, 887-1037, 577-614); if both
-die nothing can take over (election.py:27). Here every rank holds the whole
-coordinator state as a replicated state machine driven by the step's
-collectives, so ANY survivor can continue as coordinator:
+hard-coded standby (H2) over UDP (worker.py:176-495, 887-1037, 577-614); each
+worker downloads its images, runs the batch, PUTs its output file into SDFS and
+only then ACKs (worker.py:518-537, 1361-1386, 1573-1585); if H1 and H2 die
+nothing can take over (election.py:27). Here every rank holds the whole
+coordinator state as a replicated state machine driven by ONE all-gather per
+step, so ANY survivor can continue as coordinator:
 
-  step k (every rank; steps run at host speed, independent of GPU progress):
-    coordinator  drains its control inbox (client submits / C3 from the CLI) into
-                 log records, applies them, plans step k's dispatch table: at most
-                 one new batch for each rank whose work queue holds fewer than
-                 ``depth`` (2) batches, fair-share between the two models
-    broadcast    header [log length, step, table] from the coordinator (48 B per
-                 rank), then the log payload (JSON) if any
-    every rank   applies the same log records and the same table -> identical
-                 queues, in-flight sets and job-id counters on every rank, and
-                 enqueues its own new batch on its GPU (arena slots -> H2D ->
-                 hipGraph forward; the queue keeps the GPU busy)
-    all-gather   at most one COMPLETED batch per rank (its GPU event polled,
-                 never waited on): packed top-5 [2, cap, 5] int32 + batch key ->
-                 every rank completes those batches identically (C1 counts, job
-                 completion); the coordinator also writes
-                 output_<job>_<batch>_<host>.json and PUTs it into the store
-  No rank ever waits for another rank's compute: a ResNet50 rank and an
-  InceptionV3 rank run their own queues (the old lockstep step cost the slowest
-  rank's batch time on every rank).
+  step k (every rank, at host speed, independent of GPU progress):
+    every rank   contributes a fixed-size record: the batches it FINISHED since
+                 its last step (output file already written - the reference's
+                 PUT-before-ACK - plus the measured service time) and its answers
+                 to revoke requests
+    coordinator  additionally: the number of new log bytes (client submits / C3
+                 / state records, applied by itself before the collective), the
+                 step's dispatch table (up to ``depth`` batches per rank in
+                 flight: a rank may receive several batches in one step) and
+                 revoke requests (preemption of a rank's not-yet-launched
+                 batches when the fair-share split moves it to the other model)
+    all-gather   of those records (+ a broadcast of the log bytes when any)
+    every rank   applies, in this order on every rank: log records -> reports ->
+                 revoke answers -> the table; identical queues, in-flight sets,
+                 job counters and metrics everywhere
+    own work     new batches go to the rank's host queue; a batch is launched
+                 whenever one of its GPU slots (2) is free; a finished batch's
+                 rows go to the rank's output writer thread (native renderer,
+                 csrc/host/output_json.cpp), which writes
+                 output_<job>_<batch>_<host>.json (and PUTs it into the store)
+                 and hands the batch back for the next step's report.
+  No rank ever waits for another rank's compute, a step may move many batches
+  (the step rate need not match the batch rate), and the coordinator never
+  touches result rows.
 
-  These step collectives carry control-sized messages (48 B per rank + 10 KB of
-  packed top-5), so they run on a host (gloo) group by default: issued as RCCL
-  kernels they queue behind the forward's kernels on the GPU, and a step then
-  waits for a whole batch (1 GPU, concurrent ResNet50 + InceptionV3: 41.0k
-  img/s over RCCL vs 61.5k over gloo = 98 % of the time-weighted single-model
-  rates; profiles/r2_v3). The ``nccl`` backend stays supported (GPU-tested).
+  The control record is control-sized (~1.5 KB at world 8), so the collective
+  runs on a host (gloo) group by default: issued as RCCL kernels they queue
+  behind the forward's kernels (profiles/r2_v3). The ``nccl`` backend stays
+  supported. Bulk tensors (decoded images) always go over the data group.
 
-  The coordinator is the highest alive global rank — the same rank the
-  control plane's bully election (cluster/election.py, prio = rank) makes the
-  store leader, so the CLI's leader requests reach it.
+Preemption (reference worker.py:389-408, 442-461): when both models have work,
+the fair-share split (serving/scheduler.best_split) assigns each rank a model;
+a rank moved to the other model gets that model's batches in its free slots at
+once, and its queued batches of the old model are revoked - the rank answers
+"revoked" for each one still in its host queue (never launched), and every rank
+requeues those at the FRONT of their queue. Launched batches finish.
 
-Failure: SWIM (host UDP, never RCCL) confirms a dead rank -> pending collectives
-are aborted (parallel/elastic.py) -> every survivor requeues all in-flight
-batches at the FRONT of their queues (identical replicas, so identical result)
--> the communicator is rebuilt over the survivors (FileStore rendezvous: no rank
-hosts it) -> the new coordinator broadcasts its full job state (repairs any
-replica that completed one step more or less than it did) and re-PUTs the output
-files of the last completed steps (a dead coordinator may not have written them:
-at-least-once outputs). Batches may run twice; every job completes.
+Failure: SWIM (host UDP) confirms a dead rank -> pending collectives abort
+(parallel/elastic.py) -> every survivor requeues all in-flight batches at the
+FRONT -> the communicator is rebuilt over the survivors -> the new coordinator
+broadcasts its full job state first. Outputs of batches that run twice are
+rewritten (at-least-once); every job completes.
+
+Rejoin: a restarted rank announces itself over SWIM; the coordinator admits it
+at a step boundary (``members<e+1>`` + ``admit<g>`` in the rendezvous store,
+GROW flag in the record); every rank requeues its in-flight batches and moves
+to epoch e+1 with it; the coordinator's state record then brings the joiner's
+replica up to date, and one broadcast over the data group backfills its HBM
+image store with the unfinished jobs' images (parallel/image_store.backfill).
 
 Images: a job names store images (cyclic pick over the sorted ``*.jpeg``
-listing, reference worker.py:176-206) or synthetic images. Applying a submit
-record, every rank fetches and decodes only ITS SHARE of the job's new images
-and one all-gather over the data group (RCCL over xGMI) replicates the decoded
-tensors into every rank's HBM image store (parallel/image_store.py): each
-image is decoded once per job, not once per rank. A batch is a list of store
-slots gathered on the GPU. C3 (per-model batch size) is a replicated log
-record, clamped to the result capacity; a batch larger than the engine's batch
-runs as several engine passes (never truncated).
+listing, reference worker.py:176-206), pinned to their latest version at submit
+time (``name@v``: a later PUT never changes what a queued job reads), or
+synthetic images. Applying a submit record, every rank decodes only ITS SHARE of
+the job's new images and one all-gather over the data group (RCCL over xGMI)
+replicates them into every rank's HBM image store (parallel/image_store.py).
 """
 from __future__ import annotations
 
-import asyncio
 import json
 import logging
 import os
@@ -68,7 +77,7 @@ import threading
 import time
 from collections import OrderedDict, deque
 from dataclasses import dataclass
-from typing import Callable, Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -76,198 +85,37 @@ import torch
 from ..serving.cost_model import CostModel
 from ..serving.jobs import MODELS, Batch, JobManager
 from ..serving.metrics import Metrics
-from ..serving.output import decode_top5, dumps, output_name
-from ..serving.scheduler import plan
-from .dataplane import DESC_FIELDS, F_BATCH, F_JOB, F_MODEL
+from ..serving.output import BatchRenderer, output_name
+from ..serving.scheduler import best_split
 from .elastic import CollectiveFailure, ElasticGroup
+from .rank_backend import (MODEL_IDS, SLOTS, SYNTH, FakeRankBackend, GpuRankBackend, HostRankBackend,  # noqa: F401
+                           RankBackend, StoreRankBackend, synthetic_names)
 
 log = logging.getLogger(__name__)
-MODEL_IDS = {m: i for i, m in enumerate(MODELS)}
-IDLE, STOP = -1, -2
-SYNTH = "synthetic:"          # synthetic arena image names: "synthetic:<index>"
-HDR = 3                       # header words before the table: log length, step, flags
-RESULT_HISTORY = 64           # completed steps whose results every rank keeps (output re-PUT on takeover)
+
+# ------------------------------------------------------------- the record ----
+# Every rank contributes one int64 record of rec_len(world, depth) words per step.
+H_VALID, H_LOGLEN, H_STEP, H_FLAGS, H_NREP, H_NACK, H_NREQ, H_GROW = range(8)
+HDR = 8
+F_STOP, F_GROW = 1, 2
+RP_MAX = 16          # reports per rank per step (more wait for the next step)
+RV_MAX = 8           # revoke requests per step / answers per rank per step
+REP_W = 4            # report: job, batch, service_us, attempts
+ACK_W = 3            # revoke answer: job, batch, revoked
+REQ_W = 3            # revoke request: global rank, job, batch
+TAB_W = 3            # table entry: job, batch, model id (-1 = empty)
 
 
-def synthetic_names(n: int) -> List[str]:
-    return [f"{SYNTH}{i}" for i in range(n)]
+def rec_len(world: int, depth: int) -> int:
+    return HDR + world * depth * TAB_W + RV_MAX * REQ_W + RP_MAX * REP_W + RV_MAX * ACK_W
 
 
-# --------------------------------------------------------------- backends ----
-class RankBackend:
-    """Runs one batch (a list of image names) of ``model`` on this rank.
-
-    ``launch`` is asynchronous on GPU backends: it enqueues staging + forward and
-    returns (result [2, cap, 5] int32, completion event or None) — rows of
-    images that could not be fetched or decoded carry class id -1 — so the
-    service gathers the previous step's results while this batch runs.
-    ``cap`` (result rows) bounds the batch size the coordinator may assign."""
-
-    cap: int = 256
-    device = torch.device("cpu")
-
-    def launch(self, model: str, names: Sequence[str], slot: int):
-        raise NotImplementedError
-
-    def run(self, model: str, names: Sequence[str]) -> torch.Tensor:
-        res, ev = self.launch(model, names, 0)
-        if ev is not None:
-            ev.synchronize()
-        return res
-
-
-class HostRankBackend(RankBackend):
-    """A serving.inference backend (fake / cpu) behind the rank interface:
-    decode-once per image name (LRU cache), synchronous predict. The same
-    backend classes as the host cluster's workers, so both serving modes produce
-    identical outputs for the same images. Synthetic names decode from their own
-    name bytes; failed images get class id -1 in their result row."""
-
-    def __init__(self, backend, loader: Optional[Callable] = None, cap: int = 256, delay_per_image: float = 0.0,
-                 cache_images: int = 4096):
-        self.be, self.loader, self.cap, self.delay = backend, loader, cap, delay_per_image
-        self.cache: "OrderedDict[Tuple[str, str], np.ndarray]" = OrderedDict()
-        self.cache_images = cache_images
-
-    def _blobs(self, names: List[str]) -> Dict[str, Optional[bytes]]:
-        out = {n: n.encode() for n in names if n.startswith(SYNTH)}
-        rest = [n for n in names if not n.startswith(SYNTH)]
-        if rest:
-            out.update(self.loader(rest) if self.loader else {n: None for n in rest})
-        return out
-
-    def launch(self, model, names, slot):
-        if len(names) > self.cap:
-            raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
-        if self.delay:
-            time.sleep(self.delay * len(names))
-        missing = [n for n in dict.fromkeys(names) if (model, n) not in self.cache]
-        failed = set()
-        if missing:
-            blobs = self._blobs(missing)
-            for n in missing:
-                b = blobs.get(n)
-                try:
-                    self.cache[(model, n)] = self.be.decode_batch(model, [b])[0] if b is not None else None
-                except Exception as e:
-                    log.warning("decode of %s failed: %s", n, e)
-                    self.cache[(model, n)] = None
-            while len(self.cache) > self.cache_images:
-                self.cache.popitem(last=False)
-        imgs = []
-        for n in names:
-            im = self.cache.get((model, n))
-            if im is None:
-                failed.add(n)
-            else:
-                self.cache.move_to_end((model, n))
-                imgs.append(im)
-        out = torch.zeros((2, self.cap, 5), dtype=torch.int32)
-        ok = [i for i, n in enumerate(names) if n not in failed]
-        if ok:
-            idx, p = self.be.predict(model, np.stack(imgs))
-            rows = torch.tensor(ok, dtype=torch.long)
-            out[0, rows] = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32))
-            out[1, rows] = torch.from_numpy(np.ascontiguousarray(p, dtype=np.float32)).view(torch.int32)
-        for i, n in enumerate(names):
-            if n in failed:
-                out[0, i] = -1
-        return out, None
-
-
-class FakeRankBackend(HostRankBackend):
-    """Deterministic pseudo-results (serving.inference.FakeBackend), optional
-    per-image delay (CPU tests)."""
-
-    def __init__(self, cap: int = 16, delay_per_image: float = 0.0, loader: Optional[Callable] = None):
-        from ..serving.inference import FakeBackend
-
-        super().__init__(FakeBackend(), loader=loader, cap=cap, delay_per_image=delay_per_image)
-
-
-class GpuRankBackend(RankBackend):
-    """Native engines for both models resident in this GPU's HBM, fed from
-    per-model HBM image stores (parallel/image_store.py: store images decoded
-    once per job and replicated to every rank over the data group — RCCL —
-    plus seeded synthetic images). A batch is gathered from the store into the
-    engine's source slot on the compute stream, in order (no PCIe copy per
-    batch, nothing for another queue to starve); results land in one of two
-    output slots. A batch larger than the engine's batch runs as several engine
-    passes into consecutive result rows."""
-
-    def __init__(self, device: torch.device, batch_sizes: Dict[str, int], cap: int = 0, arena_images: int = 8192,
-                 n_synth: int = 512, seed: int = 0, models: Sequence[str] = MODELS, splits: int = 2,
-                 loader: Optional[Callable] = None, decode_threads: int = 8):
-        from concurrent.futures import ThreadPoolExecutor
-
-        from ..models import build_model
-        from ..models.engine import Engine, SplitEngine
-        from .image_store import HbmImageStore
-
-        self.device = device
-        self.cap = cap or max(batch_sizes.values())
-        self.loader = loader
-        self.engines, self.arenas = {}, {}
-        self.stream = torch.cuda.Stream(device)
-        self.pool = ThreadPoolExecutor(max_workers=decode_threads)
-        for m in models:
-            g, w = build_model(m, seed=seed, calibrate=True)
-            b = batch_sizes[m]
-            if splits > 1 and b % splits == 0:
-                self.engines[m] = SplitEngine(g, w, batch=b, device=str(device), src_slots=2, splits=splits)
-            else:
-                self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=2)
-            self.arenas[m] = HbmImageStore(max(arena_images, n_synth + 2 * self.cap), g.input_hw, device,
-                                           n_synth=n_synth, seed=1000 + MODEL_IDS[m])
-            self.engines[m].capture(self.stream)  # graphs now, before the service's first collective
-        self.out = [torch.zeros((2, self.cap, 5), dtype=torch.int32, device=device) for _ in range(2)]
-        self.ev_done = [torch.cuda.Event() for _ in range(2)]
-
-    def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
-        from ..serving.inference import load_image
-
-        blobs = self.loader(names) if self.loader else {}
-        hw = self.arenas[model].hw
-
-        def dec(n):
-            b = blobs.get(n)
-            if b is None:
-                return n, None
-            try:
-                return n, load_image(b, hw)
-            except Exception as e:  # undecodable file -> reported as failed
-                log.warning("decode of %s failed: %s", n, e)
-                return n, None
-        return dict(self.pool.map(dec, names))
-
-    def on_submit(self, model: str, names: Sequence[str], eg: ElasticGroup) -> int:
-        """(collective, every rank) decode this rank's share of the job's new
-        images and all-gather all shares into every rank's HBM store."""
-        n = self.arenas[model].replicate(names, lambda ns: self._load(model, ns), rank=eg.rank, world=eg.world,
-                                         gather=eg.all_gather_data)
-        torch.cuda.current_stream(self.device).synchronize()  # store writes visible to the compute stream
-        return n
-
-    def launch(self, model, names, slot):
-        if len(names) > self.cap:
-            raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
-        eng, arena = self.engines[model], self.arenas[model]
-        slots, failed = arena.slots(list(names), lambda ns: self._load(model, ns))
-        s = self.stream
-        out = self.out[slot]
-        B = eng.batch
-        with torch.cuda.stream(s):
-            for off in range(0, len(slots), B):  # one engine pass per B images: never truncated
-                chunk = slots[off:off + B]
-                arena.gather_into(eng.srcs[slot], chunk)
-                eng.run(s, use_graph=True, slot=slot)
-                out[:, off:off + len(chunk)].copy_(eng.results[slot][:, :len(chunk)])
-            if failed:  # unfetchable / undecodable images: class id -1 marks the row failed
-                bad = set(failed)
-                rows = torch.tensor([i for i, n in enumerate(names) if n in bad], dtype=torch.long)
-                out[0].index_fill_(0, rows.pin_memory().to(self.device, non_blocking=True), -1)
-            self.ev_done[slot].record(s)
-        return out, self.ev_done[slot]
+def _offs(world: int, depth: int) -> Tuple[int, int, int, int]:
+    tab = HDR
+    req = tab + world * depth * TAB_W
+    rep = req + RV_MAX * REQ_W
+    ack = rep + RP_MAX * REP_W
+    return tab, req, rep, ack
 
 
 # ------------------------------------------------------------- coordinator ----
@@ -281,40 +129,43 @@ class Inflight:
 
 class ReplicatedCoordinator:
     """The job service's state machine (reference leader, worker.py:176-495,
-    989-1037), identical on every rank: log records and dispatch tables are
-    applied in broadcast order, completions in all-gather order. Only the active
-    coordinator PLANS tables (its cost model is timing-dependent) and writes
-    outputs; replicas apply what it broadcast. Each rank may hold up to
-    ``depth`` dispatched batches (its GPU work queue)."""
+    989-1037), identical on every rank: log records, reports, revoke answers
+    and dispatch tables are applied in the same order everywhere. Only the
+    active coordinator PLANS (its cost model is timing-dependent). Each rank
+    may hold up to ``depth`` dispatched, unfinished batches."""
 
-    def __init__(self, batch_sizes: Dict[str, int], cap: int = 256, host_tag: str = "node", depth: int = 2):
-        self.cap, self.depth = cap, depth
+    def __init__(self, batch_sizes: Dict[str, int], cap: int = 256, host_tag: str = "node", depth: int = 4,
+                 preempt: bool = True, gpu_slots: int = SLOTS):
+        self.cap, self.depth, self.preempt, self.gpu_slots = cap, depth, preempt, gpu_slots
         self.jobs = JobManager({m: min(int(b), cap) for m, b in batch_sizes.items()})
         self.cost = CostModel()
         self.metrics = Metrics()
         self.inflight: "OrderedDict[tuple, Inflight]" = OrderedDict()   # batch key -> assignment
+        self.revoking: set = set()          # keys with an unanswered revoke request
         self.seq = 0
         self.requeued = 0
+        self.preempted = 0
         self.host_tag = host_tag
         self.lock = threading.RLock()      # control-thread readers (C1/C2/C5/status) vs the serve loop
-        self.history: "OrderedDict[tuple, tuple]" = OrderedDict()  # key -> (batch, idx, p, grank), recent
+        self.split_log: List[Tuple[float, Dict[str, int]]] = []   # (t, ranks per model) when the split changes
+        self._last_split: Dict[str, int] = {}
 
     # ------------------------------------------------------------- log ----
     def apply(self, rec: dict) -> dict:
         """Apply one replicated log record; returns what the requester is told."""
         op = rec["op"]
         if op == "submit":
-            jm = self.jobs
-            job = jm.submit_images(rec["model"], list(rec["images"]), rec.get("requester", "client"),
-                                   now=time.monotonic(), job_id=int(rec["job_id"]))
+            job = self.jobs.submit_images(rec["model"], list(rec["images"]), rec.get("requester", "client"),
+                                          now=time.monotonic(), job_id=int(rec["job_id"]))
             return {"jobid": job.job_id, "batches": job.batches_total}
         if op == "batch_size":
             bs = max(1, min(int(rec["batch_size"]), self.cap))
             self.jobs.set_batch_size(rec["model"], bs)
             return {"model": rec["model"], "batch_size": bs}
-        if op == "state":  # new coordinator's full state after a rebuild
+        if op == "state":  # the coordinator's full state after a rebuild / growth
             self.jobs.restore(rec["jobs"], requeue_inprogress=True)
             self.inflight.clear()
+            self.revoking.clear()
             return {}
         raise ValueError(f"unknown log record {op}")
 
@@ -328,85 +179,148 @@ class ReplicatedCoordinator:
     def outstanding(self, grank: int) -> int:
         return sum(1 for inf in self.inflight.values() if inf.rank == grank)
 
-    # ---------------------------------------------------------- tables ----
-    def next_table(self, members: List[int]) -> np.ndarray:
-        """(active coordinator) at most one new batch per rank whose queue has
-        room: fair-share split of those ranks between the two models' queues
-        (reference worker.py:255-495)."""
-        t = np.zeros((len(members), DESC_FIELDS), np.int64)
-        t[:, F_MODEL] = IDLE
+    def unfinished_images(self) -> Dict[str, List[str]]:
+        """Images of every queued or in-flight batch, per model (rejoin backfill)."""
+        out: Dict[str, List[str]] = {m: [] for m in MODELS}
+        for m, q in self.jobs.queues.items():
+            for b in q:
+                out[m].extend(b.images)
+        for b in self.jobs.inprogress.values():
+            out[b.model].extend(b.images)
+        return {m: list(dict.fromkeys(v)) for m, v in out.items()}
+
+    # ---------------------------------------------------------- planning ----
+    def plan(self, members: List[int]) -> Tuple[Dict[int, List[Batch]], List[Tuple[int, tuple]]]:
+        """(active coordinator) This step's dispatches {rank: [batches]} and
+        revoke requests [(rank, key)]. One model with work: every rank gets its
+        batches. Both: the reference's fair-share split (worker.py:303-324) over
+        all ranks; ranks keep their current model while its share allows, and
+        a rank moved to the other model has its queued (not launched) batches
+        of the old model revoked (worker.py:389-408, 442-461)."""
         queued = {m: len(self.jobs.queues[m]) for m in MODELS}
-        free = [g for g in members if self.outstanding(g) < self.depth]
-        if not any(queued.values()) or not free:
-            return t
-        workers = [f"rank{g}" for g in free]
-        online = [f"rank{g}" for g in members]
-        running = {}
-        for inf in self.inflight.values():  # what every rank is busy with (fair-share input)
-            running.setdefault(f"rank{inf.rank}", (inf.batch.model, inf.batch.key))
-        running = {w: v for w, v in running.items() if w not in workers}
-        assigns = plan(queued, workers, running, online, self.cost, self.jobs.batch_sizes, preempt=False)
+        if not any(queued.values()) or not members:
+            return {}, []
+        mine: Dict[int, List[Inflight]] = {g: [] for g in members}
+        for inf in self.inflight.values():
+            if inf.rank in mine:
+                mine[inf.rank].append(inf)
+        cur = {g: (mine[g][-1].batch.model if mine[g] else None) for g in members}
+        active = [m for m in MODELS if queued[m] > 0]
+        target: Dict[int, str] = {}
+        if len(active) == 1:
+            target = {g: active[0] for g in members}
+        else:
+            a, b = "InceptionV3", "ResNet50"
+            bs = self.jobs.batch_sizes
+            ca, cb = best_split(len(members), self.cost.rate_per_worker(a, bs[a]),
+                                self.cost.rate_per_worker(b, bs[b]))
+            want = {a: ca, b: cb}
+            have = {a: 0, b: 0}
+            for g in members:  # ranks keep their model while its share allows (lowest ranks first)
+                m = cur[g]
+                if m in want and have[m] < want[m]:
+                    target[g] = m
+                    have[m] += 1
+            for g in members:  # idle / excess ranks fill the deficits
+                if g not in target:
+                    m = a if have[a] < want[a] else b
+                    target[g] = m
+                    have[m] += 1
+            if have != self._last_split:
+                self._last_split = dict(have)
+                self.split_log.append((time.monotonic(), dict(have)))
+        disp: Dict[int, List[Batch]] = {}
+        revokes: List[Tuple[int, tuple]] = []
         taken = {m: 0 for m in MODELS}
-        for a in assigns:
-            q = self.jobs.queues[a.model]
-            if taken[a.model] >= len(q):
-                continue
-            b = q[taken[a.model]]   # popped for real by apply_table, on every rank
-            taken[a.model] += 1
-            g = int(a.worker[4:])
-            t[members.index(g)] = (b.job_id, b.batch_id, MODEL_IDS[b.model], 0, len(b.images), 0)
+        for g in members:
+            m = target[g]
+            if self.preempt and cur[g] is not None and cur[g] != m:
+                # this rank's batches of the old model beyond its GPU slots are
+                # still in its host queue: revoke them
+                old = [inf for inf in mine[g] if inf.batch.model != m]
+                for inf in old[self.gpu_slots:]:
+                    if inf.batch.key not in self.revoking and len(revokes) < RV_MAX:
+                        revokes.append((g, inf.batch.key))
+            # batches being revoked do not hold a slot: the new model starts at once
+            # (a revoke that comes too late - the batch was launched - overfills the
+            # rank's queue by at most that batch)
+            gone = {k for gg, k in revokes if gg == g} | self.revoking
+            free = self.depth - sum(1 for inf in mine[g] if inf.batch.key not in gone)
+            q = self.jobs.queues[m]
+            while free > 0 and taken[m] < len(q):
+                disp.setdefault(g, []).append(q[taken[m]])   # popped for real by apply_table
+                taken[m] += 1
+                free -= 1
+        return disp, revokes
+
+    def table(self, members: List[int], disp: Dict[int, List[Batch]]) -> np.ndarray:
+        t = np.full((len(members), self.depth, TAB_W), -1, np.int64)
+        for g, bl in disp.items():
+            r = members.index(g)
+            for d, b in enumerate(bl[:self.depth]):
+                t[r, d] = (b.job_id, b.batch_id, MODEL_IDS[b.model])
         return t
 
-    def apply_table(self, table: np.ndarray, members: List[int]) -> None:
-        """Take exactly the broadcast batches out of the local queues (every
-        rank, the coordinator included)."""
+    def apply_table(self, table: np.ndarray, members: List[int]) -> Dict[int, List[Batch]]:
+        """Take exactly the dispatched batches out of the local queues (every
+        rank); returns {rank: [batches]}."""
         now = time.monotonic()
+        out: Dict[int, List[Batch]] = {}
         for r, g in enumerate(members):
-            if int(table[r, F_MODEL]) < 0:
-                continue
-            model = MODELS[int(table[r, F_MODEL])]
-            b = self.jobs.pop_key(model, (int(table[r, F_JOB]), int(table[r, F_BATCH])))
-            if b is None:
-                raise RuntimeError(f"replica diverged: batch {table[r, F_JOB]}:{table[r, F_BATCH]} not queued")
-            self.inflight[b.key] = Inflight(g, b, now, self.seq)
-            self.seq += 1
+            for d in range(table.shape[1]):
+                if int(table[r, d, 2]) < 0:
+                    continue
+                model = MODELS[int(table[r, d, 2])]
+                b = self.jobs.pop_key(model, (int(table[r, d, 0]), int(table[r, d, 1])))
+                if b is None:
+                    raise RuntimeError(f"replica diverged: batch {table[r, d, 0]}:{table[r, d, 1]} not queued")
+                self.inflight[b.key] = Inflight(g, b, now, self.seq)
+                self.seq += 1
+                out.setdefault(g, []).append(b)
+        return out
 
-    def assigned(self, table: np.ndarray, members: List[int], grank: int) -> Optional[Batch]:
-        row = table[members.index(grank)]
-        if int(row[F_MODEL]) < 0:
-            return None
-        inf = self.inflight.get((int(row[F_JOB]), int(row[F_BATCH])))
-        return None if inf is None else inf.batch
+    def apply_requests(self, reqs: List[Tuple[int, tuple]]) -> None:
+        for _, key in reqs:
+            self.revoking.add(key)
+
+    def apply_answers(self, answers: List[Tuple[tuple, bool]]) -> int:
+        """Revoke answers of this step: revoked batches go back to the queue
+        FRONT (newest dispatch first, so queue order is kept)."""
+        back = []
+        for key, revoked in answers:
+            self.revoking.discard(key)
+            if revoked and key in self.inflight:
+                back.append(self.inflight[key])
+        for inf in sorted(back, key=lambda i: -i.seq):
+            self.inflight.pop(inf.batch.key, None)
+            self.jobs.requeue_front(inf.batch.key)
+        self.preempted += len(back)
+        return len(back)
 
     # -------------------------------------------------------- complete ----
-    def complete(self, key: tuple, rows: Optional[np.ndarray], service: float = 0.0
-                 ) -> Optional[Tuple[Batch, np.ndarray, np.ndarray, int]]:
-        """Batch ``key`` finished (its all-gathered result rows). Returns what
-        the output writer needs, or None for an unknown / duplicate key."""
+    def complete(self, key: tuple, service: float = 0.0) -> Optional[Batch]:
+        """Batch ``key`` finished and its output is durable. Returns it, or None
+        for an unknown / duplicate key."""
         inf = self.inflight.pop(key, None)
         now = time.monotonic()
+        self.revoking.discard(key)
         if inf is None or self.jobs.complete(key, now=now) is None:
             return None
         b = inf.batch
         n = len(b.images)
         self.metrics.record(b.model, now - inf.t_dispatch, service or now - inf.t_dispatch, n)
         self.cost.observe(b.model, n, service or now - inf.t_dispatch)
-        if rows is None:
-            return None
-        done = (b, rows[0, :n].copy(), rows[1, :n].view(np.float32).copy(), inf.rank)
-        self.history[key] = done
-        while len(self.history) > RESULT_HISTORY:
-            self.history.popitem(last=False)
-        return done
+        return b
 
     def requeue_inflight(self) -> int:
-        """Failure: every dispatched batch goes back to the FRONT of its queue
-        (newest dispatch first, so queue order is preserved)."""
+        """Failure / growth: every dispatched batch goes back to the FRONT of its
+        queue (newest dispatch first, so queue order is preserved)."""
         n = 0
         for inf in sorted(self.inflight.values(), key=lambda i: -i.seq):
             if self.jobs.requeue_front(inf.batch.key) is not None:
                 n += 1
         self.inflight.clear()
+        self.revoking.clear()
         self.requeued += n
         return n
 
@@ -421,95 +335,124 @@ class ReplicatedCoordinator:
 
 # ---------------------------------------------------------- output writer ----
 class OutputWriter:
-    """Writes output_<job>_<batch>_<host>.json off the serve loop (a blocking
-    queue: a file is never dropped) into ``out_dir`` and/or the store."""
+    """This rank's result files, off the serve loop: a thread renders each
+    finished batch (native renderer, byte-identical to the reference's
+    indent-4 JSON), writes output_<job>_<batch>_<host>.json into ``out_dir``
+    and/or PUTs it into the store, then calls ``on_written(batch, tag)`` —
+    the service reports a batch only after that (reference: PUT, then ACK,
+    worker.py:518-537). A write that fails is logged and still reported (the
+    job must finish); the failure count is kept."""
 
     def __init__(self, out_dir: Optional[str], put: Optional[Callable[[str, bytes], None]] = None,
-                 host_tag: str = "node"):
+                 host_tag: str = "node", threads: int = 1):
         self.out_dir, self.put, self.host_tag = out_dir, put, host_tag
         if out_dir:
             os.makedirs(out_dir, exist_ok=True)
+        self.renderer = BatchRenderer()
         self.q: "queue.Queue" = queue.Queue()
         self.written = 0
-        self.thread = threading.Thread(target=self._loop, daemon=True, name="output-writer")
-        self.thread.start()
+        self.failed = 0
+        self.bytes = 0
+        self.busy_s = 0.0
+        self._threads = [threading.Thread(target=self._loop, daemon=True, name=f"output-writer-{i}")
+                         for i in range(threads)]
+        for t in self._threads:
+            t.start()
+
+    @property
+    def enabled(self) -> bool:
+        return bool(self.out_dir) or self.put is not None
 
     def submit(self, b: Batch, idx: np.ndarray, p: np.ndarray, grank: int,
-               on_written: Optional[Callable[[Batch], None]] = None) -> None:
-        self.q.put((b, idx, p, grank, on_written))
+               on_written: Optional[Callable[..., None]] = None, tag=None) -> None:
+        self.q.put((b, idx, p, grank, on_written, tag))
 
     def _loop(self) -> None:
         while True:
             item = self.q.get()
             if item is None:
+                self.q.task_done()
                 return
-            b, idx, p, g, on_written = item
+            b, idx, p, g, on_written, tag = item
+            t0 = time.perf_counter()
             try:
-                failed = [n for i, n in enumerate(b.images) if idx[i, 0] < 0]
-                ok = [i for i in range(len(b.images)) if idx[i, 0] >= 0]
-                names = [b.images[i] for i in ok]
-                doc = decode_top5(names, idx[ok], p[ok], failed)
+                data = self.renderer.render(b.images, idx, p)
                 name = output_name(b.job_id, b.batch_id, f"{self.host_tag}-rank{g}")
-                text = dumps(doc)
                 if self.out_dir:
-                    with open(os.path.join(self.out_dir, name), "w") as f:
-                        f.write(text)
+                    with open(os.path.join(self.out_dir, name), "wb") as f:
+                        f.write(data)
                 if self.put is not None:
-                    self.put(name, text.encode())
+                    self.put(name, data)
                 self.written += 1
-                if on_written is not None:
-                    on_written(b)
+                self.bytes += len(data)
             except Exception as e:  # a failed write is logged, never silently skipped
+                self.failed += 1
                 log.error("output %s:%s not written: %s", b.job_id, b.batch_id, e)
+            self.busy_s += time.perf_counter() - t0
+            if on_written is not None:
+                on_written(b, tag)
+            self.q.task_done()
 
     def flush(self) -> None:
-        """Block until every queued file is written (sentinel + join), then restart."""
-        self.q.put(None)
-        self.thread.join()
-        self.thread = threading.Thread(target=self._loop, daemon=True, name="output-writer")
-        self.thread.start()
+        """Block until every queued file is written."""
+        self.q.join()
+
+    def close(self) -> None:
+        for _ in self._threads:
+            self.q.put(None)
+        for t in self._threads:
+            t.join(timeout=10)
 
 
 # ---------------------------------------------------------------- service ----
+@dataclass
+class _Launched:
+    batch: Batch
+    rows: torch.Tensor
+    event: Optional[object]
+    slot: int
+    t0: float
+    epoch: int
+
+
 class CollectiveService:
     """The per-rank serve loop (identical on every rank). See the module doc.
 
-    Per-rank work queues, no lockstep on compute: a step is one broadcast (log
-    + dispatch table: at most one new batch per rank whose queue holds fewer
-    than ``coord.depth`` batches) and one all-gather of at most one COMPLETED
-    batch per rank (a rank contributes a batch once its GPU event has fired —
-    polled, never waited on), so the collectives run at host speed while every
-    GPU works through its own queue; a ResNet50 rank and an InceptionV3 rank
-    never wait for each other. Collectives run on their own HIP stream.
-
     ``control``: optional RankControl (UDP control plane + store of this rank);
     without it (tests, benches) jobs are submitted with ``submit_local`` on the
-    coordinator rank."""
+    coordinator rank. ``writer``: this rank's OutputWriter (None: batches are
+    reported as soon as their GPU work finishes, no files). ``rejoined``: this
+    process re-joined a running job (its replica is empty until the
+    coordinator's state record)."""
 
     def __init__(self, eg: ElasticGroup, backend: RankBackend, coord: ReplicatedCoordinator,
                  control=None, writer: Optional[OutputWriter] = None, kill_rank: int = -1, kill_at_step: int = -1,
-                 on_device: bool = False, idle_sleep: float = 0.002, poll_sleep: float = 0.0001,
-                 watchdog_s: float = 0.0):
-        if coord.depth > 2:
-            raise ValueError("rank queues deeper than the backends' 2 source/result slots")
+                 on_device: bool = False, idle_sleep: float = 0.002, poll_sleep: float = 0.0002,
+                 watchdog_s: float = 0.0, rejoined: bool = False):
         self.eg, self.be, self.coord, self.control = eg, backend, coord, control
         self.writer = writer
         self.kill_rank, self.kill_at_step = kill_rank, kill_at_step
         self.dev = backend.device if on_device else torch.device("cpu")
-        self.comm = torch.cuda.Stream(self.dev) if self.dev.type == "cuda" else None
         self.steps = 0
         self.rebuilds = 0
+        self.grows = 0
         self.cap = backend.cap
-        self.local: "deque" = deque()   # (key, result, event) launched here, not yet reported
+        self.slots = getattr(backend, "slots", SLOTS)
+        self.hostq: "deque[Batch]" = deque()             # dispatched to this rank, not launched
+        self.gpu: "deque[_Launched]" = deque()           # launched, not finished (launch order)
+        self.free_slots = list(range(self.slots))
+        self.done: "deque[Tuple[Batch, float, int]]" = deque()   # finished + written: (batch, service s, epoch)
+        self.answers: List[Tuple[tuple, bool]] = []       # revoke answers for the next record
         self.launched = 0
-        self.sbuf = torch.zeros((2, self.cap + 1, 5), dtype=torch.int32, device=self.dev)
+        self.served_here = 0
         self.idle_sleep, self.poll_sleep = idle_sleep, poll_sleep
         self._inbox: "queue.Queue" = queue.Queue()   # (record, reply callback or None)
-        self._written: Dict[int, set] = {}             # job id -> batch ids whose output is durable
         self._stop = False
+        self.rejoined = rejoined
         self.last_progress = time.monotonic()
-        self.phase_s: Dict[str, float] = {"plan": 0.0, "broadcast": 0.0, "launch": 0.0, "exchange": 0.0,
-                                          "complete": 0.0, "sleep": 0.0}
+        self.phase_s: Dict[str, float] = {"poll": 0.0, "plan": 0.0, "collective": 0.0, "apply": 0.0,
+                                          "launch": 0.0, "sleep": 0.0}
+        self.batches_per_step_max = 0
         self._watchdog = None
         if watchdog_s > 0:
             self._watchdog = threading.Thread(target=self._watch, args=(watchdog_s,), daemon=True)
@@ -550,92 +493,113 @@ class CollectiveService:
             replies.append(reply)
         return recs, replies
 
-    # ----------------------------------------------------------- results --
-    def _completed_local(self):
-        """The oldest launched batch if its GPU work has finished (non-blocking)."""
-        if not self.local:
-            return None
-        key, res, ev = self.local[0]
-        if ev is not None and not ev.query():
-            return None
-        return self.local.popleft()
+    # ----------------------------------------------------------- own work --
+    def _written(self, b: Batch, tag) -> None:
+        """(writer thread) output durable: reportable at the next step."""
+        self.done.append((b, tag[0], tag[1]))
 
-    def _exchange(self) -> List[Tuple[tuple, np.ndarray]]:
-        """All-gather at most one completed batch per rank -> [(key, rows)]."""
-        done = self._completed_local()
-        sb = self.sbuf
-        world, cap = self.eg.world, self.cap
-        if self.comm is not None:
-            ctx = torch.cuda.stream(self.comm)
-        else:
-            import contextlib
-
-            ctx = contextlib.nullcontext()
-        with ctx:
-            sb[0, cap, :2] = -1
-            if done is not None:
-                key, res, ev = done
-                if ev is not None and self.comm is not None:
-                    self.comm.wait_event(ev)  # (already fired: ordering for the comm stream only)
-                sb[:, :cap].copy_(res.to(self.dev))
-                sb[0, cap, 0], sb[0, cap, 1] = int(key[0]), int(key[1])
-            out = torch.empty((world, *sb.shape), dtype=sb.dtype, device=self.dev)
-            self.eg.all_gather_into(out, sb)
-            host = out.cpu().numpy()
-        got = []
-        for r in range(world):
-            j, b = int(host[r, 0, cap, 0]), int(host[r, 0, cap, 1])
-            if j >= 0:
-                got.append(((j, b), host[r, :, :cap]))
-        return got
-
-    def _output_written(self, b: Batch) -> None:
-        """(writer thread) A job is reported finished to its requester only once
-        every batch's output file is durable — like the reference worker, which
-        PUT its output before ACKing (worker.py:518-537) — so get-output right
-        after the SUCCESS sees all of them."""
-        with self.coord.lock:
-            got = self._written.setdefault(b.job_id, set())
-            got.add(b.batch_id)
-            j = self.coord.jobs.jobs.get(b.job_id)
-            ready = j is not None and j.done and len(got) >= j.batches_total
-        if ready and self.control is not None:
-            self.control.jobs_progress([b])
+    def _poll(self) -> int:
+        """Finished GPU batches -> writer (or straight to the report list);
+        launch host-queued batches into free slots. Never blocks."""
+        n = 0
+        while self.gpu:
+            L = self.gpu[0]
+            if L.event is not None and not L.event.query():
+                break
+            self.gpu.popleft()
+            svc = time.monotonic() - L.t0
+            k = len(L.batch.images)
+            rows = L.rows[:, :k].numpy()
+            idx = rows[0].copy()
+            p = rows[1].view(np.float32).copy()
+            self.free_slots.append(L.slot)
+            if self.writer is not None and self.writer.enabled:
+                self.writer.submit(L.batch, idx, p, self.eg.grank, on_written=self._written, tag=(svc, L.epoch))
+            else:
+                self.done.append((L.batch, svc, L.epoch))
+            self.served_here += 1
+            n += 1
+        while self.hostq and self.free_slots:
+            b = self.hostq.popleft()
+            slot = self.free_slots.pop(0)
+            rows, ev = self.be.launch(b.model, b.images, slot)
+            self.gpu.append(_Launched(b, rows, ev, slot, time.monotonic(), self.eg.epoch))
+            self.launched += 1
+            n += 1
+        return n
 
     # -------------------------------------------------------------- step --
+    def _record(self, L: int, depth: int, active: bool, loglen: int, stop: bool, grow: List[int],
+                table: Optional[np.ndarray], reqs: List[Tuple[int, tuple]]) -> Tuple[np.ndarray, list, list]:
+        world = self.eg.world
+        tab, req, rep, ack = _offs(world, depth)
+        r = np.zeros(L, np.int64)
+        r[H_VALID] = 1
+        reports = []
+        while self.done and len(reports) < RP_MAX:
+            b, svc, ep = self.done.popleft()
+            if ep != self.eg.epoch:
+                continue  # requeued by a rebuild since: it runs again
+            reports.append((b, svc))
+        answers, self.answers = self.answers[:RV_MAX], self.answers[RV_MAX:]
+        r[H_NREP] = len(reports)
+        for i, (b, svc) in enumerate(reports):
+            r[rep + i * REP_W: rep + (i + 1) * REP_W] = (b.job_id, b.batch_id, int(svc * 1e6), b.attempts)
+        r[H_NACK] = len(answers)
+        for i, (key, ok) in enumerate(answers):
+            r[ack + i * ACK_W: ack + (i + 1) * ACK_W] = (key[0], key[1], int(ok))
+        if active:
+            r[H_LOGLEN] = loglen
+            r[H_STEP] = self.steps
+            r[H_FLAGS] = (F_STOP if stop else 0) | (F_GROW if grow else 0)
+            r[H_GROW] = sum(1 << g for g in grow)
+            if table is not None:
+                r[tab:req] = table.reshape(-1)
+            else:
+                r[tab:req] = -1
+            r[H_NREQ] = len(reqs)
+            for i, (g, key) in enumerate(reqs):
+                r[req + i * REQ_W: req + (i + 1) * REQ_W] = (g, key[0], key[1])
+        return r, reports, answers
+
     def step(self, stop_when_idle: bool = False) -> bool:
         eg, coord = self.eg, self.coord
-        k = self.steps
-        world = eg.world
+        world, depth = eg.world, coord.depth
+        L = rec_len(world, depth)
+        tab, req, rep, ack = _offs(world, depth)
         root = eg.group_rank_of(self.coordinator_rank())
         ph, t0 = self.phase_s, time.perf_counter()
-        hcpu = np.zeros(HDR + world * DESC_FIELDS, np.int64)
+        self._poll()
+        t1 = time.perf_counter()
+        ph["poll"] += t1 - t0
         active = self.is_coordinator()
-        payload = b""
-        recs: List[dict] = []
-        applied_here: List[dict] = []
-        replies: List[Optional[Callable]] = []
-        results: List[dict] = []
+        payload, recs, replies, results = b"", [], [], []
+        table, reqs, grow, stop = None, [], [], False
         if active:
             recs, replies = self._drain()
             with coord.lock:
-                results = [coord.apply(r) for r in recs]
+                results = [coord.apply(r) for r in recs]  # the coordinator applies its log first, like everyone
                 stop = self._stop or (stop_when_idle and coord.idle() and not recs)
-                table = coord.next_table(eg.members) if not stop else None
+                if not stop:
+                    grow = sorted(g for g in set(eg.joiners) if g not in eg.members)
+                    if grow:
+                        grow = [g for g in eg.admit(set(grow)) if g not in eg.members]
+                    if not grow:
+                        disp, reqs = coord.plan(eg.members)
+                        table = coord.table(eg.members, disp)
             if recs:
                 payload = json.dumps(recs).encode()
-            hcpu[0] = len(payload)
-            hcpu[1] = k
-            hcpu[2] = 1 if stop else 0
-            if table is not None:
-                hcpu[HDR:] = table.reshape(-1)
-        t1 = time.perf_counter()
-        ph["plan"] += t1 - t0
-        with (torch.cuda.stream(self.comm) if self.comm is not None else _null()):
-            hdr = torch.from_numpy(hcpu).to(self.dev)  # staged on the comm stream itself
-            eg.broadcast(hdr, src=root)
-            h = hdr.cpu().numpy()
-            n = int(h[0])
+        rec, reports, answers = self._record(L, depth, active, len(payload), stop, grow, table, reqs)
+        t2 = time.perf_counter()
+        ph["plan"] += t2 - t1
+        # ---- the step's collective (+ the log bytes, rarely) ----
+        rec_t = torch.from_numpy(rec).to(self.dev)
+        out = torch.empty((world, L), dtype=torch.int64, device=self.dev)
+        applied_here: List[dict] = []
+        try:
+            eg.all_gather_into(out, rec_t)
+            h = out.cpu().numpy()
+            n = int(h[root, H_LOGLEN])
             if n:
                 buf = torch.zeros(n, dtype=torch.uint8, device=self.dev)
                 if active:
@@ -643,58 +607,97 @@ class CollectiveService:
                 eg.broadcast(buf, src=root)
                 if not active:
                     applied_here = json.loads(bytes(buf.cpu().numpy()).decode())
-                    with coord.lock:
-                        for r in applied_here:
-                            coord.apply(r)
+        except CollectiveFailure:
+            # nothing of this step was applied anywhere: its reports and answers go again
+            for b, svc in reversed(reports):
+                self.done.appendleft((b, svc, self.eg.epoch))
+            self.answers = answers + self.answers
+            raise
+        t3 = time.perf_counter()
+        ph["collective"] += t3 - t2
+        # ---- apply, in the same order on every rank: log, reports, answers, table ----
+        with coord.lock:
+            for r in applied_here:
+                coord.apply(r)
         applied = recs if active else applied_here
-        for r in applied:  # collective on every rank: decode-once + replicate the job's images
-            if r["op"] == "submit" and hasattr(self.be, "on_submit"):
+        for r in applied:  # collectives on every rank: replicate a job's images / backfill a joiner
+            if r["op"] == "submit":
                 self.be.on_submit(r["model"], r["images"], eg)
+            elif r["op"] == "state":
+                self.rejoined = False
+                self._backfill(root)
         if active and self.control is not None:
             self.control.committed(replies, results)
         elif active:
             for cb, r in zip(replies, results):
                 if cb is not None:
                     cb(r)
-        t2 = time.perf_counter()
-        ph["broadcast"] += t2 - t1
-        if int(h[2]) == 1:  # STOP (sent only when nothing is queued or in flight)
-            return False
-        table = h[HDR:].reshape(world, DESC_FIELDS)
+        flags = int(h[root, H_FLAGS])
+        finished: List[Batch] = []
+        moved = 0
+        rq: List[Tuple[int, tuple]] = []
+        mine: Optional[List[Batch]] = None
         with coord.lock:
-            coord.apply_table(table, eg.members)
-            mine = coord.assigned(table, eg.members, eg.grank)
-        if k == self.kill_at_step and eg.grank == self.kill_rank:
-            log.warning("rank %d: injected kill at step %d", eg.grank, k)
-            os._exit(17)
-        if mine is not None:
-            res, ev = self.be.launch(mine.model, mine.images, self.launched % 2)
-            self.launched += 1
-            self.local.append((mine.key, res, ev))
-        t3 = time.perf_counter()
-        ph["launch"] += t3 - t2
-        got = self._exchange()
+            for r in range(world):
+                for i in range(int(h[r, H_NREP])):
+                    j, bt, us, _ = h[r, rep + i * REP_W: rep + (i + 1) * REP_W]
+                    b = coord.complete((int(j), int(bt)), service=int(us) * 1e-6)
+                    if b is not None:
+                        finished.append(b)
+            ans = []
+            for r in range(world):
+                for i in range(int(h[r, H_NACK])):
+                    j, bt, ok = h[r, ack + i * ACK_W: ack + (i + 1) * ACK_W]
+                    ans.append(((int(j), int(bt)), bool(ok)))
+            coord.apply_answers(ans)
+            if not flags & F_STOP:
+                table = h[root, tab:req].reshape(world, depth, TAB_W)
+                disp = coord.apply_table(table, eg.members)
+                mine = disp.get(eg.grank, [])
+                moved = sum(len(v) for v in disp.values())
+                rq = [(int(h[root, req + i * REQ_W]), (int(h[root, req + i * REQ_W + 1]),
+                                                       int(h[root, req + i * REQ_W + 2])))
+                      for i in range(int(h[root, H_NREQ]))]
+                coord.apply_requests(rq)
+        if finished and active and self.control is not None:
+            self.control.jobs_progress(finished)
         t4 = time.perf_counter()
-        ph["exchange"] += t4 - t3
-        if got:
-            with coord.lock:
-                finished = [coord.complete(key, rows) for key, rows in got]
-            if self.is_coordinator():
-                done = [d for d in finished if d is not None]
-                for b, idx, p, g in done:
-                    if self.writer is not None:
-                        self.writer.submit(b, idx, p, g, on_written=self._output_written)
-                if self.control is not None and self.writer is None:
-                    self.control.jobs_progress([d[0] for d in done])
+        ph["apply"] += t4 - t3
+        if mine is None:  # STOP (sent only when nothing is queued or in flight)
+            return False
+        self.batches_per_step_max = max(self.batches_per_step_max, moved)
+        if self.steps == self.kill_at_step and eg.grank == self.kill_rank:
+            log.warning("rank %d: injected kill at step %d", eg.grank, self.steps)
+            os._exit(17)
+        # own new batches, then the revoke requests addressed to this rank (host queue only)
+        self.hostq.extend(mine)
+        for g, key in rq:
+            if g != eg.grank:
+                continue
+            hit = next((b for b in self.hostq if b.key == key), None)
+            if hit is not None:
+                self.hostq.remove(hit)
+            self.answers.append((key, hit is not None))
+        if flags & F_GROW:
+            self._grow([g for g in range(63) if (int(h[root, H_GROW]) >> g) & 1])
+        self._poll()
         self.steps += 1
         self.last_progress = time.monotonic()
         t5 = time.perf_counter()
-        ph["complete"] += t5 - t4
-        if not got and mine is None and not n:
-            # nothing moved: poll again soon while GPUs work, back off when idle
+        ph["launch"] += t5 - t4
+        if not (reports or answers or mine or n or self.done or self.answers or self.gpu or self.hostq):
             time.sleep(self.poll_sleep if coord.inflight else self.idle_sleep)
             ph["sleep"] += time.perf_counter() - t5
         return True
+
+    def _backfill(self, root: int) -> None:
+        """(collective, after a state record) the coordinator's HBM images of
+        every unfinished job to the ranks that lack them (a re-joined rank)."""
+        with self.coord.lock:
+            want = self.coord.unfinished_images()
+        for m in MODELS:
+            if want.get(m):
+                self.be.backfill(m, want[m], self.eg, root)
 
     # -------------------------------------------------------------- serve --
     def serve(self, max_steps: int = 10 ** 9, stop_when_idle: bool = False) -> int:
@@ -704,40 +707,55 @@ class CollectiveService:
                     break
             except CollectiveFailure as e:
                 self._recover(e)
+        self.be.drain()
         if self.writer is not None:
             self.writer.flush()
         return self.steps
 
-    def _recover(self, e: Exception) -> None:
-        eg = self.eg
-        log.warning("rank %d: collective failed (%s); rebuilding", eg.grank, e)
+    def _reset_local(self) -> None:
+        """Drop this rank's queue and in-flight work (requeued everywhere)."""
         with self.coord.lock:
             self.coord.requeue_inflight()
-        deadline = time.monotonic() + 10
-        while not (eg.dead & set(eg.members)) and time.monotonic() < deadline:
-            time.sleep(0.01)  # let SWIM confirm who died
-        was = self.coordinator_rank()
-        eg.rebuild(set(eg.dead))  # aborts the communicator first (RCCL: ncclCommAbort)
-        # the requeued batches' GPU work may still be running: let it drain before
-        # their slots are reused (compute streams only; the aborted comm stream is not waited on)
-        for st in (getattr(self.be, "stream", None), getattr(self.be, "copy_stream", None)):
-            if st is not None:
-                st.synchronize()
-        self.local.clear()
-        self.rebuilds += 1
+        self.be.drain()   # the requeued batches' GPU work may still run: let it finish before slots are reused
+        self.hostq.clear()
+        self.gpu.clear()
+        self.free_slots = list(range(self.slots))
+        self.answers = []
+
+    def _after_epoch(self, was: int) -> None:
         # the new coordinator's state is authoritative: replicas that completed one
-        # exchange more or less than it did are repaired by a state record
+        # step more or less than it did are repaired by a state record (and a
+        # joiner gets its first state); it is the first record of the next step
         if self.is_coordinator():
             with self.coord.lock:
                 snap = self.coord.jobs.snapshot()
             with self._inbox.mutex:
                 self._inbox.queue.appendleft(({"op": "state", "jobs": snap}, None))
-            if was != eg.grank and self.writer is not None:  # takeover: re-PUT recent outputs
-                for b, idx, p, g in list(self.coord.history.values()):
-                    self.writer.submit(b, idx, p, g, on_written=self._output_written)
-            if self.control is not None:
+            if self.control is not None and was != self.eg.grank:
                 self.control.became_coordinator(was)
         self.last_progress = time.monotonic()
+
+    def _recover(self, e: Exception) -> None:
+        eg = self.eg
+        log.warning("rank %d: collective failed (%s); rebuilding", eg.grank, e)
+        was = self.coordinator_rank()
+        self._reset_local()
+        deadline = time.monotonic() + 10
+        while not (eg.dead & set(eg.members)) and time.monotonic() < deadline:
+            time.sleep(0.01)  # let SWIM confirm who died
+        eg.rebuild(set(eg.dead))  # aborts the communicator first (RCCL: ncclCommAbort)
+        self.rebuilds += 1
+        self._after_epoch(was)
+
+    def _grow(self, joiners: List[int]) -> None:
+        """Admit re-joined ranks (every member, at the same step boundary)."""
+        eg = self.eg
+        was = self.coordinator_rank()
+        log.warning("rank %d: admitting ranks %s into epoch %d", eg.grank, joiners, eg.epoch + 1)
+        self._reset_local()
+        eg.grow(sorted(set(eg.members) | set(joiners)))
+        self.grows += 1
+        self._after_epoch(was)
 
     def _watch(self, limit_s: float) -> None:
         """Watchdog: a rank whose serve loop makes no progress for ``limit_s``
@@ -750,265 +768,5 @@ class CollectiveService:
                 os._exit(3)
 
 
-def _null():
-    import contextlib
-
-    return contextlib.nullcontext()
-
-
-# ------------------------------------------------------------ control plane ----
-class RankControl:
-    """This rank's host control plane, in a daemon thread with its own asyncio
-    loop: a cluster Node with role "rank" (SWIM membership -> dead ranks for the
-    elastic group, bully election -> store leader = coordinator, the replicated
-    store with its TCP blob plane) plus the job-service request handlers the
-    reference leader served (SUBMIT_JOB_REQUEST, C1, C2, C3 = SET_BATCH_SIZE,
-    C5 = GET_ASSIGNMENTS, JOB_STATUS; worker.py:887-1059). Requests reach the
-    serve loop through its inbox; replies go out once the request's log record
-    has been broadcast (committed on every rank)."""
-
-    def __init__(self, grank: int, world: int, base_port: int, store_dir: str, host: str = "127.0.0.1",
-                 period: float = 0.1, ping_timeout: float = 0.1, suspect_timeout: float = 0.6,
-                 replication: int = 4, on_dead: Optional[Callable[[int], None]] = None):
-        self.grank, self.world, self.base, self.host = grank, world, base_port, host
-        self.store_dir, self.replication = store_dir, replication
-        self.period, self.ping_timeout, self.suspect_timeout = period, ping_timeout, suspect_timeout
-        self.on_dead = on_dead
-        self.svc: Optional[CollectiveService] = None
-        self.loop: Optional[asyncio.AbstractEventLoop] = None
-        self.node = None
-        self.ready = threading.Event()
-        self.dead: set = set()
-        self.thread = threading.Thread(target=self._main, daemon=True, name=f"rank-control-{grank}")
-
-    def addr(self, g: int) -> str:
-        return f"{self.host}:{self.base + g}"
-
-    def rank_of(self, name: str) -> Optional[int]:
-        try:
-            return int(name.rsplit(":", 1)[1]) - self.base
-        except (ValueError, IndexError):
-            return None
-
-    # ------------------------------------------------------------ thread --
-    def start(self, timeout: float = 30.0) -> "RankControl":
-        self.thread.start()
-        if not self.ready.wait(timeout):
-            raise RuntimeError("rank control plane did not start")
-        return self
-
-    def _main(self) -> None:
-        self.loop = asyncio.new_event_loop()
-        asyncio.set_event_loop(self.loop)
-        self.loop.create_task(self._run())
-        self.loop.run_forever()
-        pending = [t for t in asyncio.all_tasks(self.loop) if not t.done()]
-        for t in pending:
-            t.cancel()
-        if pending:
-            self.loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
-        self.loop.close()
-
-    async def _run(self) -> None:
-        from ..cluster.frames import MsgType
-        from ..serving.node import Node, NodeConfig
-
-        cfg = NodeConfig(host=self.host, port=self.base + self.grank, role="rank", seeds=[self.addr(0)],
-                         store_dir=self.store_dir, period=self.period, ping_timeout=self.ping_timeout,
-                         suspect_timeout=self.suspect_timeout, cleanup_time=30.0, replication=self.replication,
-                         meta={"prio": self.grank, "rank": self.grank})
-        self.node = n = await Node(cfg).start()
-        on = n.ep.on
-        on(MsgType.SUBMIT_JOB_REQUEST, self._on_submit)
-        on(MsgType.SET_BATCH_SIZE, self._on_batch_size)
-        on(MsgType.GET_C1_COMMAND, self._on_c1)
-        on(MsgType.GET_C2_COMMAND, self._on_c2)
-        on(MsgType.GET_ASSIGNMENTS, self._on_c5)
-        on(MsgType.JOB_STATUS, self._on_status)
-        on(MsgType.FETCH_INTRODUCER, self._on_fetch_leader)   # every rank is an introducer for clients
-        n.ml.on_fail.append(self._member_failed)
-        await n.join()
-        # every rank knows the static job membership: once all have joined, the
-        # bully election settles on the highest rank (= the collective
-        # coordinator); serving starts only then, so store requests of the first
-        # steps already reach the right leader
-        want = self.addr(self.world - 1)
-        for _ in range(400):
-            if len([m for m in n.ml.alive() if (n.ml.get(m).meta or {}).get("role") == "rank"]) >= self.world:
-                break
-            await asyncio.sleep(0.05)
-        for _ in range(400):
-            if n.leader() == want:
-                break
-            if not n.election.in_election:
-                n.election.trigger()
-            await asyncio.sleep(0.05)
-        self.ready.set()
-
-    def _member_failed(self, name: str) -> None:
-        g = self.rank_of(name)
-        if g is not None and 0 <= g < self.world and g not in self.dead:
-            self.dead.add(g)
-            log.warning("rank %d: SWIM confirmed rank %d dead", self.grank, g)
-            if self.on_dead is not None:
-                self.on_dead(g)
-
-    def stop(self) -> None:
-        if self.loop is None or not self.thread.is_alive():
-            return
-
-        async def _shutdown():
-            try:
-                await self.node.stop()
-            except Exception:
-                pass
-            tasks = [t for t in asyncio.all_tasks() if t is not asyncio.current_task()]
-            for t in tasks:
-                t.cancel()
-            await asyncio.gather(*tasks, return_exceptions=True)
-        try:
-            asyncio.run_coroutine_threadsafe(_shutdown(), self.loop).result(timeout=5)
-        except Exception:
-            pass
-        self.loop.call_soon_threadsafe(self.loop.stop)
-        self.thread.join(timeout=5)
-
-    # ------------------------------------------------------- serve hooks --
-    def attach(self, svc: CollectiveService) -> None:
-        self.svc = svc
-
-    def call(self, coro, timeout: float = 30.0):
-        """Run a coroutine on the control loop from the serve thread."""
-        return asyncio.run_coroutine_threadsafe(coro, self.loop).result(timeout)
-
-    def committed(self, replies: List[Optional[Callable]], results: List[dict]) -> None:
-        for cb, r in zip(replies, results):
-            if cb is not None:
-                self.loop.call_soon_threadsafe(cb, r)
-
-    def jobs_progress(self, batches: List[Batch]) -> None:
-        """Tell requesters whose job just finished (SUBMIT_JOB_REQUEST_SUCCESS)."""
-        from ..cluster.frames import MsgType
-
-        seen = set()
-        for b in batches:
-            j = self.svc.coord.jobs.jobs.get(b.job_id)
-            if j is not None and j.done and j.job_id not in seen and ":" in j.requester:  # a node, not "local"
-                seen.add(j.job_id)
-                self.loop.call_soon_threadsafe(
-                    lambda jj=j: self.loop.create_task(
-                        self.node.ep.send(jj.requester, MsgType.SUBMIT_JOB_REQUEST_SUCCESS, {"jobid": jj.job_id})))
-
-    def became_coordinator(self, previous: int) -> None:
-        log.warning("rank %d: now the coordinator (was rank %d)", self.grank, previous)
-        # requesters of jobs that finished while the old coordinator was dying are told again
-        done = [j for j in self.svc.coord.jobs.jobs.values() if j.done]
-        self.jobs_progress([Batch(j.job_id, 0, j.model, []) for j in done])
-
-    def store_put(self, name: str, data: bytes, deadline_s: float = 60.0) -> None:
-        """PUT into the store, retried across a store-leader change (the leader
-        is the coordinator rank, which is what fails over)."""
-        t0, err = time.monotonic(), ""
-        while time.monotonic() - t0 < deadline_s:
-            try:
-                ok, err = self.call(self.node.store.put(data, name), timeout=30)
-            except Exception as e:  # leader unreachable mid-failover
-                ok, err = False, str(e)
-            if ok:
-                return
-            time.sleep(0.1)
-        raise RuntimeError(f"store put {name}: {err}")
-
-    def store_loader(self, names: List[str]) -> Dict[str, Optional[bytes]]:
-        async def fetch_all():
-            sem = asyncio.Semaphore(16)
-
-            async def one(nm):
-                async with sem:
-                    if self.node.local.has(nm):
-                        return nm, self.node.local.get_bytes(nm)
-                    got = await self.node.store.get(nm)
-                    return nm, None if got is None else got[1]
-            return dict(await asyncio.gather(*(one(nm) for nm in names)))
-        return self.call(fetch_all(), timeout=120)
-
-    # ----------------------------------------------------------- handlers --
-    async def _on_fetch_leader(self, fr) -> None:
-        """Reference FETCH_INTRODUCER (introduce process/worker.py:55-58): any rank
-        tells a client who leads, once the election has settled."""
-        from ..cluster.frames import MsgType
-
-        if self.ready.is_set() and self.node.leader() is not None:
-            await self.node.ep.reply(fr, MsgType.FETCH_INTRODUCER_ACK, {"introducer": self.node.leader()})
-
-    def _active(self) -> bool:
-        return self.svc is not None and self.svc.is_coordinator()
-
-    async def _on_submit(self, fr) -> None:
-        from ..cluster.frames import MsgType
-
-        if not self._active():
-            return  # not the coordinator: the client retries at the elected leader
-        p = fr.payload
-        model = p["model"]
-        n = int(p["images_count"])
-        if p.get("synthetic"):
-            names = synthetic_names(n)
-        else:
-            from ..serving.jobs import pick_images
-
-            names = pick_images(sorted(self.node.store.meta.matching("*.jpeg")), n)
-
-        def reply(res, fr=fr):
-            self.loop.create_task(self.node.ep.reply(fr, MsgType.SUBMIT_JOB_REQUEST_ACK, res))
-            if res.get("batches") == 0:
-                self.loop.create_task(self.node.ep.send(fr.sender, MsgType.SUBMIT_JOB_REQUEST_SUCCESS,
-                                                        {"jobid": res["jobid"]}))
-        self.svc.submit_local(model, images=names, requester=fr.sender, reply=reply)
-
-    async def _on_batch_size(self, fr) -> None:
-        from ..cluster.frames import MsgType
-
-        if not self._active():
-            return
-
-        def reply(res, fr=fr):
-            if fr.seq:
-                self.loop.create_task(self.node.ep.reply(fr, MsgType.SET_BATCH_SIZE_ACK, res))
-        self.svc.set_batch_size(fr.payload["model"], int(fr.payload["batch_size"]), reply=reply)
-
-    async def _on_c1(self, fr) -> None:
-        from ..cluster.frames import MsgType
-
-        if self._active():
-            with self.svc.coord.lock:
-                c1 = self.svc.coord.metrics.c1()
-            await self.node.ep.reply(fr, MsgType.GET_C1_COMMAND_ACK, {"c1": c1})
-
-    async def _on_c2(self, fr) -> None:
-        from ..cluster.frames import MsgType
-
-        if self._active():
-            with self.svc.coord.lock:
-                p = self.svc.coord.metrics.c2_reference_payload()
-                p["detail"] = self.svc.coord.metrics.c2()
-            await self.node.ep.reply(fr, MsgType.GET_C2_COMMAND_ACK, p)
-
-    async def _on_c5(self, fr) -> None:
-        from ..cluster.frames import MsgType
-
-        if self._active():
-            with self.svc.coord.lock:
-                a = self.svc.coord.assignments()
-            await self.node.ep.reply(fr, MsgType.GET_ASSIGNMENTS_ACK, {"assignments": a})
-
-    async def _on_status(self, fr) -> None:
-        from ..cluster.frames import MsgType
-
-        if not self._active():
-            return
-        with self.svc.coord.lock:
-            j = self.svc.coord.jobs.jobs.get(int(fr.payload["jobid"]))
-            st = {"jobid": fr.payload["jobid"], "known": j is not None, "done": bool(j and j.done),
-                  "batches_done": j.batches_done if j else 0, "batches_total": j.batches_total if j else 0}
-        await self.node.ep.reply(fr, MsgType.JOB_STATUS_ACK, st)
+# control plane of a rank (kept importable from here)
+from .rank_control import RankControl  # noqa: E402,F401

@@ -7,6 +7,9 @@
 
   python -m distributed_machine_learning_amd.serving.main --config configs/local10.toml --node H3
 
+  python -m distributed_machine_learning_amd.serving.main --role rank --gpus 8     # the MI355X service
+      (serving/rank_main.py: one rank process per GPU; the CLI connects with --role client)
+
 With ``--config`` the node takes its role, address, backend and every cluster
 setting from the file's entry for ``--node`` (utils/config.py); flags given
 explicitly on the command line still override the file. ``--trace out.json``
@@ -37,13 +40,13 @@ def parse(argv=None) -> argparse.Namespace:
     ap.add_argument("--journal", default=None, help="coordinator job journal (restart recovery)")
     ap.add_argument("--trace", default="", help="write a Chrome trace of this node at exit")
     ap.add_argument("-t", "--testing", action="store_true", help="3%% send drop + bps/false-positive meters")
-    ap.add_argument("--role", default="worker", choices=["coordinator", "standby", "worker", "client"])
+    ap.add_argument("--role", default="worker", choices=["coordinator", "standby", "worker", "client", "rank"])
     ap.add_argument("--introducer", default="127.0.0.1:8888")
     ap.add_argument("--seed-node", action="append", default=[])
     ap.add_argument("--store-dir", default="./sdfs")
     ap.add_argument("--download-dir", default="./download")
     ap.add_argument("--testfiles", default="")
-    ap.add_argument("--backend", default="cpu", choices=["gpu", "cpu", "fake"])
+    ap.add_argument("--backend", default="cpu", choices=["gpu", "cpu", "fake", "store"])
     ap.add_argument("--gpu", type=int, default=0)
     ap.add_argument("--period", type=float, default=0.5)
     ap.add_argument("--ping-timeout", type=float, default=0.25)
@@ -53,8 +56,13 @@ def parse(argv=None) -> argparse.Namespace:
     ap.add_argument("--cmd", action="append", default=[])
     ap.add_argument("--exit-after", type=float, default=0.0)
     ap.add_argument("--log", default="debug.log")
+    from .rank_main import add_args
+
+    add_args(ap)
     a = ap.parse_args(argv)
     a.explicit = {k for k, v in vars(a).items() if v != ap.get_default(k)}
+    if a.role == "rank":
+        return a
     if a.port is None and not (a.config and a.node):
         ap.error("--port is required (or --config with --node)")
     return a
@@ -151,7 +159,14 @@ async def amain(a: argparse.Namespace) -> int:
 
 
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
+    if a.role == "rank":
+        from . import rank_main
+
+        if a.rank < 0:
+            return rank_main.launch(a, argv)
+        return rank_main.rank_main(a)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s",
                         handlers=[logging.FileHandler(a.log), logging.StreamHandler(sys.stderr)])
     return asyncio.run(amain(a))

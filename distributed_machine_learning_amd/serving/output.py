@@ -9,15 +9,18 @@ merges every ``output_<job>_*.json`` into ``final_<job>.json`` (worker.py:1496-1
 """
 from __future__ import annotations
 
+import ctypes as C
 import json
 import os
-from typing import Dict, Iterable, Sequence
+import threading
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from ..utils.labels import load_class_index
 
 FAILED_DOWNLOAD = "Failed to download file from SDFS"
+VERSION_SEP = "@"   # a store image pinned to one version: "<name>@<version>" (parallel/service.py)
 
 
 class NpEncoder(json.JSONEncoder):
@@ -31,6 +34,13 @@ class NpEncoder(json.JSONEncoder):
         return super().default(o)
 
 
+def image_key(name: str) -> str:
+    """Output key of a batch image: its basename, without a pinned store version."""
+    base = os.path.basename(name)
+    head, sep, tail = base.rpartition(VERSION_SEP)
+    return head if sep and tail.isdigit() else base
+
+
 def output_name(job_id: int, batch_id: int, host: str) -> str:
     return f"output_{job_id}_{batch_id}_{host.split('.')[0].split(':')[0]}.json"
 
@@ -41,10 +51,10 @@ def decode_top5(names: Sequence[str], top_idx: np.ndarray, top_p: np.ndarray,
     idx = class_index or load_class_index()
     out: Dict[str, object] = {}
     for i, name in enumerate(names):
-        out[os.path.basename(name)] = [[[idx[int(c)][0], idx[int(c)][1], float(p)]
-                                        for c, p in zip(top_idx[i], top_p[i])]]
+        out[image_key(name)] = [[[idx[int(c)][0], idx[int(c)][1], float(p)]
+                                 for c, p in zip(top_idx[i], top_p[i])]]
     for name in failed:
-        out[os.path.basename(name)] = FAILED_DOWNLOAD
+        out[image_key(name)] = FAILED_DOWNLOAD
     return out
 
 
@@ -63,3 +73,97 @@ def merge_outputs(docs: Iterable[Dict[str, object]]) -> Dict[str, object]:
     for d in docs:
         merged.update(d)
     return merged
+
+
+# ----------------------------------------------------------- native renderer --
+class BatchRenderer:
+    """Renders a batch's output document byte-identically to
+    ``dumps(decode_top5(...))`` in native code (csrc/host/output_json.cpp): the
+    per-class text is pre-rendered once, image keys are cached, and the ctypes
+    call releases the GIL, so a rank's writer thread does not stall its serve
+    loop. Falls back to the Python encoder if the host library is unavailable."""
+
+    def __init__(self, class_index=None):
+        self.idx = class_index or load_class_index()
+        self._keys: Dict[str, bytes] = {}
+        self._lock = threading.Lock()
+        self.lib = _host_lib()
+        ind = " " * 16
+        parts = [(json.dumps(w) + ",\n" + ind + json.dumps(lab) + ",\n" + ind).encode() for w, lab in self.idx]
+        self.cls = b"".join(parts)
+        off = np.zeros(len(parts) + 1, np.int64)
+        np.cumsum([len(p) for p in parts], out=off[1:])
+        self.cls_off = off
+        self.buf = C.create_string_buffer(1 << 20)
+        self.native = self.lib is not None
+
+    def _key(self, name: str) -> bytes:
+        k = self._keys.get(name)
+        if k is None:
+            k = json.dumps(image_key(name)).encode()
+            with self._lock:
+                if len(self._keys) > 1 << 20:
+                    self._keys.clear()
+                self._keys[name] = k
+        return k
+
+    def render(self, images: Sequence[str], top_idx: np.ndarray, top_p: np.ndarray) -> bytes:
+        """images[i] <- row i of top_idx/top_p ([n, 5]); a row whose first class
+        id is negative is a failed image."""
+        top_idx = np.ascontiguousarray(top_idx, dtype=np.int32)
+        top_p = np.ascontiguousarray(top_p, dtype=np.float32)
+        failed = top_idx[:, 0] < 0 if len(images) else np.zeros(0, bool)
+        if not self.native:
+            ok = [i for i in range(len(images)) if not failed[i]]
+            doc = decode_top5([images[i] for i in ok], top_idx[ok], top_p[ok],
+                              [images[i] for i in range(len(images)) if failed[i]], self.idx)
+            return dumps(doc).encode()
+        ent: Dict[bytes, int] = {}  # decode_top5's dict: first-occurrence order, last assignment wins
+        for i, nm in enumerate(images):
+            if not failed[i]:
+                ent[self._key(nm)] = i
+        for i, nm in enumerate(images):
+            if failed[i]:
+                ent[self._key(nm)] = -1
+        keys = list(ent)
+        rows = np.fromiter(ent.values(), np.int32, len(keys))
+        koff = np.zeros(len(keys) + 1, np.int64)
+        np.cumsum([len(k) for k in keys], out=koff[1:])
+        blob = b"".join(keys)
+        k = top_idx.shape[1] if top_idx.ndim == 2 else 5
+        need = 256 + len(blob) + len(keys) * k * 160
+        buf = self.buf if C.sizeof(self.buf) >= need else C.create_string_buffer(need)
+        n = self.lib.dml_render_top5_json(len(keys), blob, koff.ctypes.data, rows.ctypes.data, top_idx.ctypes.data,
+                                          top_p.ctypes.data, k, self.cls, self.cls_off.ctypes.data, len(self.idx),
+                                          buf, C.sizeof(buf))
+        if n < 0:
+            raise RuntimeError("output render buffer too small")
+        return buf.raw[:n]
+
+
+_host = None
+_host_lock = threading.Lock()
+
+
+def _host_lib():
+    """libdml_host.so (built with g++ on first use; None if no compiler and no library)."""
+    global _host
+    if _host is not None:
+        return _host or None
+    with _host_lock:
+        if _host is None:
+            from .. import _build
+
+            try:
+                path = _build.build_host() if os.environ.get("DML_SKIP_BUILD") != "1" else _build.HOST_LIB_PATH
+                L = C.CDLL(str(path))
+                L.dml_render_top5_json.restype = C.c_long
+                L.dml_render_top5_json.argtypes = [C.c_int, C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                   C.c_void_p, C.c_int, C.c_char_p, C.c_void_p, C.c_int, C.c_void_p,
+                                                   C.c_long]
+                L.dml_py_repr.restype = C.c_int
+                L.dml_py_repr.argtypes = [C.c_double, C.c_char_p]
+                _host = L
+            except Exception:  # no compiler and no shipped library: Python encoder
+                _host = False
+    return _host or None

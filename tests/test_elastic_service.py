@@ -87,12 +87,13 @@ def test_concurrent_models_fair_share(tmp_path):
     r = res[2]  # the coordinator: highest rank
     assert r["coordinator"] == 2 and r["done"] == [True, True] and r["rebuilds"] == 0
     assert r["c1"]["ResNet50"]["query_count"] == 96 and r["c1"]["InceptionV3"]["query_count"] == 96
-    assert r["written"] == 24  # 12 + 12 batches of 8, written by the coordinator only
+    # 12 + 12 batches of 8: every rank wrote the outputs of the batches IT ran
+    assert sum(res[g]["written"] for g in range(3)) == 24
     assert len(os.listdir(tmp_path / "outputs")) == 24
+    assert all(res[g]["written"] > 0 for g in range(3))
     # every replica completed exactly the same batches
     for g in (0, 1):
         assert res[g]["c1"]["ResNet50"]["query_count"] == 96 and res[g]["done"] == [True, True]
-        assert res[g]["written"] == 0
 
 
 def test_worker_kill_mid_job_recovers(tmp_path):
@@ -123,43 +124,81 @@ def test_coordinator_kill_mid_job_failover(tmp_path):
 
 
 def test_replicated_state_machine_queues():
-    """Coordinator and replica apply the same records/tables -> same state; each
-    rank's queue holds at most ``depth`` batches; a failure requeues every
-    dispatched batch at the queue front in dispatch order; completion is per
-    batch (out of order is fine); C3 is clamped to the result capacity."""
-    import numpy as np
-
-    from distributed_machine_learning_amd.parallel.dataplane import F_BATCH, F_MODEL
+    """Coordinator and replica apply the same records/tables -> same state; a
+    rank holds at most ``depth`` batches and may receive several in one step; a
+    failure requeues every dispatched batch at the queue front in dispatch
+    order; completion is per batch (out of order is fine); C3 is clamped to the
+    result capacity."""
     from distributed_machine_learning_amd.parallel.service import ReplicatedCoordinator, synthetic_names
 
-    c = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4, depth=2)
-    rep = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4, depth=2)
-    rec = {"op": "submit", "model": "ResNet50", "images": synthetic_names(16), "job_id": c.next_job_id()}
-    assert c.apply(rec) == rep.apply(rec) == {"jobid": 31, "batches": 4}
+    c = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4, depth=3)
+    rep = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4, depth=3)
+    rec = {"op": "submit", "model": "ResNet50", "images": synthetic_names(24), "job_id": c.next_job_id()}
+    assert c.apply(rec) == rep.apply(rec) == {"jobid": 31, "batches": 6}
     assert c.apply({"op": "batch_size", "model": "ResNet50", "batch_size": 64}) == {"model": "ResNet50",
                                                                                       "batch_size": 4}
-    tables = []
-    for _ in range(3):
-        t = c.next_table([0])
-        tables.append(t)
+
+    def step():
+        disp, _ = c.plan([0, 1])
+        t = c.table([0, 1], disp)
         for x in (c, rep):
-            x.apply_table(t, [0])
-    assert int(tables[2][0, F_MODEL]) < 0            # queue depth 2 reached: nothing new for rank 0
-    assert list(c.inflight) == list(rep.inflight) == [(31, 1), (31, 2)] and c.outstanding(0) == 2
-    assert c.assigned(tables[1], [0], 0).key == (31, 2)
-    assert c.requeue_inflight() == 2 and not c.inflight
-    assert [b.key for b in c.jobs.queues["ResNet50"]][:2] == [(31, 1), (31, 2)]
-    for _ in range(2):
-        c.apply_table(c.next_table([0]), [0])
-    rows = np.zeros((2, 4, 5), np.int32)
-    done = c.complete((31, 2), rows)                 # out-of-order completion is per batch
-    assert done is not None and list(c.inflight) == [(31, 1)]
-    assert c.complete((31, 2), rows) is None         # duplicate completion is ignored
-    c.complete((31, 1), None)
-    assert not c.inflight and c.metrics.c1()["ResNet50"]["query_count"] == 8
-    # a new coordinator's state record repairs a diverged replica
+            got = x.apply_table(t, [0, 1])
+        return got
+    got = step()
+    assert [b.key for b in got[0]] == [(31, 1), (31, 2), (31, 3)]      # three batches in one step
+    assert [b.key for b in got[1]] == [(31, 4), (31, 5), (31, 6)]
+    assert step() == {}                                                   # depth 3 reached everywhere
+    assert list(c.inflight) == list(rep.inflight) and c.outstanding(0) == 3
+    assert c.requeue_inflight() == rep.requeue_inflight() == 6 and not c.inflight
+    assert [b.key for b in c.jobs.queues["ResNet50"]] == [(31, i) for i in range(1, 7)]
+    step()
+    assert c.complete((31, 5)) is not None                               # out-of-order completion
+    assert c.complete((31, 5)) is None                                   # duplicate completion is ignored
+    assert c.metrics.c1()["ResNet50"]["query_count"] == 4
+    # a new coordinator's state record (taken after its own requeue) repairs a diverged replica
+    c.requeue_inflight()
     rep.apply({"op": "state", "jobs": c.jobs.snapshot()})
     assert [b.key for b in rep.jobs.queues["ResNet50"]] == [b.key for b in c.jobs.queues["ResNet50"]]
+
+
+def test_preemption_reaches_fair_share_within_two_batch_times():
+    """A ResNet50 job saturates both ranks (depth 4: 2 launched + 2 queued per
+    rank); an InceptionV3 job arrives. The plan moves one rank to InceptionV3,
+    revokes that rank's QUEUED ResNet50 batches (they go back to the queue
+    front, in order) and fills its free slots with InceptionV3 batches at once:
+    the split is reached after the 2 launched batches, not 4 (reference
+    preemption, worker.py:389-408, 442-461)."""
+    from distributed_machine_learning_amd.parallel.service import ReplicatedCoordinator, synthetic_names
+
+    c = ReplicatedCoordinator({"ResNet50": 4, "InceptionV3": 4}, cap=4, depth=4)
+    c.apply({"op": "submit", "model": "ResNet50", "images": synthetic_names(64), "job_id": 31})
+    members = [0, 1]
+    launched = {0: [], 1: []}
+    disp, rq = c.plan(members)
+    assert not rq
+    got = c.apply_table(c.table(members, disp), members)
+    hostq = {g: list(got[g]) for g in members}
+    for g in members:  # each rank launches 2 (its GPU slots), 2 wait in its host queue
+        launched[g] = hostq[g][:2]
+        hostq[g] = hostq[g][2:]
+    c.apply({"op": "submit", "model": "InceptionV3", "images": synthetic_names(64), "job_id": 32})
+    disp, rq = c.plan(members)
+    moved = {g for g, _ in rq}
+    assert len(moved) == 1                                  # fair share: one rank per model
+    g = moved.pop()
+    assert sorted(k for _, k in rq) == sorted(b.key for b in hostq[g])   # exactly its queued batches
+    c.apply_requests(rq)
+    got = c.apply_table(c.table(members, disp), members)
+    # the rank answers: every requested batch was still queued -> revoked
+    assert c.apply_answers([(k, True) for _, k in rq]) == 2
+    assert [b.key for b in c.jobs.queues["ResNet50"]][:2] == sorted(k for _, k in rq)   # front, in order
+    # after its 2 launched ResNet50 batches the moved rank runs only InceptionV3
+    assert all(b.model == "InceptionV3" for b in got.get(g, [])) and got.get(g)
+    for b in launched[g]:
+        c.complete(b.key)
+    disp, rq = c.plan(members)
+    assert all(b.model == "InceptionV3" for b in disp.get(g, []))
+    assert c.preempted == 2
 
 
 def _replica_main(grank, world, rdzv, out):

