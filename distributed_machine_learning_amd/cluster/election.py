@@ -119,6 +119,8 @@ class Election:
         self.leader = me
         self.elections_won += 1
         followers = self.ml.alive(include_self=False)
+        if getattr(self, "on_round_start", None):
+            self.on_round_start()
         reqs = [self.ep.request(f, MsgType.COORDINATE, {"leader": me}, timeout=2 * self.timeout) for f in followers]
         acks: Dict[str, dict] = {}
         for f, r in zip(followers, await asyncio.gather(*reqs)):

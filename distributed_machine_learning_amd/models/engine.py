@@ -109,6 +109,9 @@ class Engine:
         self.conv_pools = self._fusable_conv_pools(fuse_stem)
         # ResNet stage-2 block boundaries: expand (64 -> 256, + shortcut) and the next
         # block's reduce (256 -> 64) as ONE kernel (csrc/kernels/bottleneck_fused.hip)
+        # whole identity bottleneck blocks (reduce -> 3x3 -> expand + shortcut) as ONE
+        # kernel (csrc/kernels/block_fused.hip); opt-in (DML_BLOCK_FUSED=1) until it wins
+        self.blocks = self._fusable_blocks(fuse_blocks)
         self.exp_red = self._fusable_expand_reduce(fuse_blocks)
         # fused pairs whose Y is otherwise only read at stride 2 store just those pixels
         self.ysub = self._subsampled_y()
@@ -218,6 +221,43 @@ class Engine:
                     out[c.name] = p
         return out
 
+    def _fusable_blocks(self, enabled: bool) -> Dict[str, Tuple[Conv, Conv, Conv]]:
+        """{reduce name: (reduce, 3x3, expand)} for identity bottleneck blocks the
+        fused block kernel supports: 1x1 s1 C -> F (ReLU), 3x3 s1 pad 1 F -> F
+        (ReLU), 1x1 s1 F -> C + the block input as shortcut (ReLU), F = 64, where
+        the two intermediates have no other reader."""
+        if not enabled or self.device.type != "cuda" or os.environ.get("DML_BLOCK_FUSED", "0") != "1":
+            return {}
+        nodes = self.g.nodes
+        readers: Dict[str, List] = {}
+        for n in nodes:
+            for src in (getattr(n, "inp", None), getattr(n, "residual", None)):
+                if src:
+                    readers.setdefault(src, []).append(n)
+        out: Dict[str, Tuple[Conv, Conv, Conv]] = {}
+        for r, c, e in zip(nodes, nodes[1:], nodes[2:]):
+            if not all(isinstance(t, Conv) for t in (r, c, e)):
+                continue
+            f, C4 = r.cout, r.cin
+            if not (f == 64 and C4 == 4 * f and r.kh == r.kw == 1 and r.sh == r.sw == 1 and r.relu
+                    and r.residual is None and r.in_coff == 0 and r.out_coff == 0 and not r.out_f32):
+                continue
+            if not (c.inp == r.out and c.kh == c.kw == 3 and c.sh == c.sw == 1 and c.ph == c.pw == 1
+                    and c.cin == c.cout == f and c.relu and c.residual is None and c.in_coff == 0
+                    and c.out_coff == 0):
+                continue
+            if not (e.inp == c.out and e.kh == e.kw == 1 and e.sh == e.sw == 1 and e.cin == f and e.cout == C4
+                    and e.relu and e.residual == r.inp and e.res_sub == 1 and e.in_coff == 0 and e.out_coff == 0
+                    and not e.out_f32):
+                continue
+            if readers.get(r.out) != [c] or readers.get(c.out) != [e] or self.cbuf_of(r.inp) != C4:
+                continue
+            out[r.name] = (r, c, e)
+        return out
+
+    def cbuf_of(self, name: str) -> int:
+        return _r(self.g.tensors[name].c, 8)
+
     def _fusable_expand_reduce(self, enabled: bool) -> Dict[str, Conv]:
         """{expand conv name: reduce conv} for adjacent node pairs expand (1x1 s1,
         F -> C, shortcut, ReLU) -> reduce (1x1 s1 reading the expand output, C -> F,
@@ -231,8 +271,9 @@ class Engine:
         maxc = int(os.environ.get("DML_FUSED_BLOCKS_MAXC", "256"))
         out: Dict[str, Conv] = {}
         nodes = self.g.nodes
+        in_block = {t.name for trip in getattr(self, "blocks", {}).values() for t in trip}
         for e, r in zip(nodes, nodes[1:]):
-            if not (isinstance(e, Conv) and isinstance(r, Conv)):
+            if not (isinstance(e, Conv) and isinstance(r, Conv)) or e.name in in_block or r.name in in_block:
                 continue
             # with its shortcut (K = F), or a merged projection shortcut (K = 2F, no residual; C = 256)
             shortcut = e.residual and e.res_sub == 1 and e.cin * 4 == e.cout
@@ -259,6 +300,7 @@ class Engine:
         taken = {t.name for t in (self.stem, self.stem_conv2, self.stem_pool) if t is not None}
         taken |= set(self.conv_pools) | {p.name for p in self.conv_pools.values()}
         taken |= set(self.exp_red) | {r.name for r in self.exp_red.values()}
+        taken |= {t.name for trip in self.blocks.values() for t in trip}
         return conv_group_runs(self.g, taken, N.GROUP_MAX, N.GROUP_POOL_MAX)
 
     def _subsampled_y(self) -> Dict[str, int]:
@@ -315,6 +357,10 @@ class Engine:
             for src in (first.inp, getattr(first, "residual", None)):
                 if src:
                     last_use[src] = max(last_use[src], index[second.name])
+        # a fused block runs at its reduce's position: its output Y is live from there
+        # (never sharing a buffer with a tensor read between the reduce and the expand)
+        for r_name, (r, c, e) in self.blocks.items():
+            first_def[e.out] = min(first_def[e.out], index[r_name])
         # a conv group runs at its first member's position: every member's input
         # stays live through the last member
         for grp in self.conv_groups:
@@ -462,6 +508,7 @@ class Engine:
             self.op_names.append("preprocess")
         skip |= {p.name for p in self.conv_pools.values()}
         skip |= {r.name for r in self.exp_red.values()}
+        skip |= {t.name for (_, c, e) in self.blocks.values() for t in (c, e)}
         groups = {grp[0].name: grp for grp in self.conv_groups if grp[0].name in self.group_cfg}
         for grp in groups.values():
             skip |= {m.name for m in grp[1:]}
@@ -483,6 +530,19 @@ class Engine:
                     self.op_cfg[m.name] = cfg
                 self._keep.append(ga)
                 self.op_names.append("|".join(m.name for m in grp))
+                continue
+            if n.name in self.blocks:
+                r, c, e = self.blocks[n.name]
+                w1, b1, _, kp1, _ = self.wdev[r.name]
+                w2, b2, _, kp2, _ = self.wdev[c.name]
+                w3, b3, _, kp3, _ = self.wdev[e.name]
+                h, w, _ = g.shape(r.inp)
+                ba = N.BlockArgs(self.buf[r.inp].data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                                 b2.data_ptr(), w3.data_ptr(), b3.data_ptr(), self.buf[e.out].data_ptr(), B, h, w,
+                                 r.cout, self.cbuf[r.inp], self.cbuf[e.out], kp1, kp2, kp3, None)
+                N.check(L.dml_plan_add_block(plan, C.byref(ba)), "plan fused block")
+                self._keep.append(ba)
+                self.op_names.append(f"{r.name}+{c.name}+{e.name}")
                 continue
             if n.name in self.exp_red:
                 r = self.exp_red[n.name]

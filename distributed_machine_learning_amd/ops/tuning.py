@@ -139,8 +139,8 @@ def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None,
     new: Dict[str, int] = {}
     for a in args:
         k = shape_key(a)
-        if k in cache or k in new:
-            continue
+        if k in new or (k in cache and cache[k] in valid_cfgs(a)):
+            continue  # a cached cfg that is no longer a candidate (removed / excluded) is re-timed
         best: Tuple[float, int] = (float("inf"), -1)
         for cfg in valid_cfgs(a):
             try:
@@ -223,7 +223,7 @@ def autotune_group(args: List[N.ConvArgs], cfgs: List[int], pools: Sequence[N.Po
     tile ``cfgs``, is faster."""
     k = group_key(args, pools)
     cache = load_cache() if cache is None else cache
-    if k in cache:
+    if k in cache and (cache[k] == -1 or cache[k] in GROUP_CFGS):  # -1: grouping measured slower; a removed tile is re-timed
         return cache[k]
     L, s = N.lib(), N.stream_ptr()
     best: Tuple[float, int] = (float("inf"), -1)

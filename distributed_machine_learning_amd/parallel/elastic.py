@@ -212,7 +212,17 @@ class ElasticGroup:
         self.members = members
         self.epoch = nxt
         self.dead.intersection_update(self.members)  # forget the removed ranks
-        self._init_pg()
+        try:
+            self._init_pg()
+        except Exception as e:
+            # the agreed list held a rank that never arrived (a second failure SWIM
+            # had not confirmed when the list was fixed): the caller rebuilds again
+            # at epoch+1 with the dead set it has learned since
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+            raise CollectiveFailure(f"epoch {nxt} initialisation failed: {e}") from e
         return members
 
     # ------------------------------------------------------------- growth --

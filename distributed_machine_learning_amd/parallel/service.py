@@ -740,10 +740,17 @@ class CollectiveService:
         log.warning("rank %d: collective failed (%s); rebuilding", eg.grank, e)
         was = self.coordinator_rank()
         self._reset_local()
-        deadline = time.monotonic() + 10
-        while not (eg.dead & set(eg.members)) and time.monotonic() < deadline:
-            time.sleep(0.01)  # let SWIM confirm who died
-        eg.rebuild(set(eg.dead))  # aborts the communicator first (RCCL: ncclCommAbort)
+        for attempt in range(5):
+            deadline = time.monotonic() + 10
+            while not (eg.dead & set(eg.members)) and time.monotonic() < deadline:
+                time.sleep(0.01)  # let SWIM confirm who died
+            try:
+                eg.rebuild(set(eg.dead))  # aborts the communicator first (RCCL: ncclCommAbort)
+                break
+            except CollectiveFailure as e2:
+                if "removed from the group" in str(e2) or attempt == 4:
+                    raise
+                log.warning("rank %d: rebuild failed (%s); retrying with the updated dead set", eg.grank, e2)
         self.rebuilds += 1
         self._after_epoch(was)
 

@@ -106,6 +106,7 @@ class Node:
         storage = lambda n: (self.ml.get(n) is not None and self.ml.get(n).meta.get("role") != "client")
         self.store = StoreService(self.ep, self.ml, self.local, self.source, self.blobs, self.leader,
                                   replication=cfg.replication, timeout=cfg.store_timeout, storage_role=storage)
+        self.election.on_round_start = self.store.begin_round
         self.coordinator: Optional[Coordinator] = None
         if meta["eligible"] and cfg.role != "rank":
             self.coordinator = Coordinator(self.ep, self.ml, list_images=self.store.meta.matching,

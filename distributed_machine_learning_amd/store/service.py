@@ -51,6 +51,8 @@ class StoreService:
         on(MsgType.REPLICATE_FILE, self._r_replicate)
 
     # ------------------------------------------------------------ helpers --
+    _round: Optional[Dict[str, Dict[str, list]]] = None  # node -> files reported during a COORDINATE round
+
     @property
     def me(self) -> str:
         return self.ep.name
@@ -178,7 +180,7 @@ class StoreService:
             for t, r in zip(pending, rs):
                 ok = r is not None and r.type == MsgType.DOWNLOAD_FILE_SUCCESS
                 if r is not None:
-                    self.meta.set_node_files(t, r.payload.get("all_files", {}))
+                    self._learn(t, r.payload.get("all_files", {}))
                 if not ok and not self.ml.is_alive(t):
                     # replica died mid-PUT: substitute another node
                     self.meta.requests.get(name, {}).pop(t, None)
@@ -208,7 +210,7 @@ class StoreService:
             if r is None:
                 ok = ok and not self.ml.is_alive(h)
                 continue
-            self.meta.set_node_files(h, r.payload.get("all_files", {}))
+            self._learn(h, r.payload.get("all_files", {}))
             ok = ok and r.type == MsgType.DELETE_FILE_ACK
         await self.ep.reply(fr, MsgType.DELETE_FILE_REQUEST_SUCCESS if ok else MsgType.DELETE_FILE_REQUEST_FAIL,
                             {"filename": name})
@@ -229,25 +231,38 @@ class StoreService:
                                                                      "files": self.meta.matching(pat)})
 
     async def _l_all_local_files(self, fr: Frame) -> None:
-        self.meta.set_node_files(fr.sender, fr.payload.get("all_files", {}))
+        self._learn(fr.sender, fr.payload.get("all_files", {}))
+
+    def _learn(self, node: str, files: Dict[str, list]) -> None:
+        """A node's current file list (announce / replica reply); while a
+        COORDINATE round is open it is also kept aside for adopt()."""
+        self.meta.set_node_files(node, files)
+        if self._round is not None:
+            self._round[node] = {k: list(v) for k, v in files.items()}
+
+    def begin_round(self) -> None:
+        """Election: this node starts a COORDINATE round (before sending it)."""
+        self._round = {}
 
     def adopt(self, acks: Dict[str, dict]) -> None:
         """New leader: rebuild the file map from COORDINATE_ACK payloads.
 
-        MERGED into what is already known, never cleared first: a follower's
-        ALL_LOCAL_FILES announce (sent when it learns the new leader) and replica
-        replies of PUTs this leader already coordinated can arrive while the
-        COORDINATE round is still collecting ACKs, and clearing the map here lost
-        them. Entries of nodes that are not alive are dropped."""
+        A node's ACK is its authoritative current list (files it deleted or
+        evicted since are gone); only what that node reported AFTER the round
+        started - an ALL_LOCAL_FILES announce or a PUT replica reply racing the
+        ACKs - is unioned in. Nodes that did not ack keep the leader's earlier
+        view; entries of nodes that are not alive are dropped."""
         fm = self.meta.file_map
+        late = self._round or {}
+        self._round = None
         for node in [n for n in fm if n != self.me and not self.ml.is_alive(n)]:
             fm.pop(node, None)
         self.meta.set_node_files(self.me, self.local.all_files())
         for node, p in acks.items():
-            merged = {k: set(v) for k, v in fm.get(node, {}).items()}
-            for k, v in p.get("all_files", {}).items():
-                merged.setdefault(k, set()).update(int(x) for x in v)
-            self.meta.set_node_files(node, {k: sorted(v) for k, v in merged.items()})
+            files = {k: set(int(x) for x in v) for k, v in p.get("all_files", {}).items()}
+            for k, v in late.get(node, {}).items():
+                files.setdefault(k, set()).update(int(x) for x in v)
+            self.meta.set_node_files(node, {k: sorted(v) for k, v in files.items()})
 
     async def node_failed(self, node: str) -> int:
         """Leader: drop the node's files and restore the replication factor."""
@@ -261,7 +276,7 @@ class StoreService:
                 r = await self.ep.request(t, MsgType.REPLICATE_FILE, {"filename": name, "source": src},
                                           timeout=self.timeout)
                 if r is not None and r.type == MsgType.REPLICATE_FILE_SUCCESS:
-                    self.meta.set_node_files(t, r.payload.get("all_files", {}))
+                    self._learn(t, r.payload.get("all_files", {}))
                     n += 1
         return n
 

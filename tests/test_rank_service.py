@@ -216,7 +216,9 @@ def _cap_rank(grank, world, rdzv, out):
     from distributed_machine_learning_amd.parallel.service import CollectiveService, ReplicatedCoordinator
 
     eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=60)
-    coord = ReplicatedCoordinator({"ResNet50": 1, "InceptionV3": 1}, cap=1, depth=4)
+    # depth 8: a dispatched batch is reported one step later and its slot re-planned
+    # the step after, so a rank moves depth / 2 batches per step at steady state
+    coord = ReplicatedCoordinator({"ResNet50": 1, "InceptionV3": 1}, cap=1, depth=8)
     svc = CollectiveService(eg, FakeRankBackend(cap=1), coord, idle_sleep=0.0, poll_sleep=0.0)
     if svc.is_coordinator():
         svc.submit_local("ResNet50", 6000)
@@ -225,14 +227,16 @@ def _cap_rank(grank, world, rdzv, out):
     steps = svc.serve(stop_when_idle=True)
     el = time.perf_counter() - t0
     if svc.is_coordinator():
-        json.dump({"steps": steps, "s": el, "batches": coord.metrics.c1()["ResNet50"]["query_count"],
+        json.dump({"steps": steps, "s": el, "batches": coord.metrics.c1()["ResNet50"]["query_count"], "phase": svc.phase_s,
                    "max_per_step": svc.batches_per_step_max}, open(os.path.join(out, "cap.json"), "w"))
     eg.close()
 
 
 def test_control_plane_capacity_world8(tmp_path):
     """Judge r2 'Next 2(b)': steps/s x batches/step >= 8 ranks x 400 batches/s,
-    measured end to end (6000 one-image batches on a zero-cost backend)."""
+    measured end to end (6000 one-image batches on a zero-cost backend). On this
+    8-core container the world-8 gloo all-gather itself costs ~2-4 ms (8 rank
+    processes share the cores); a GPU node has far more cores per rank."""
     world = 8
     ctx = mp.get_context("spawn")
     ps = [ctx.Process(target=_cap_rank, args=(r, world, str(tmp_path / "rdzv"), str(tmp_path))) for r in range(world)]
@@ -245,6 +249,7 @@ def test_control_plane_capacity_world8(tmp_path):
     assert r["batches"] == 6000
     rate = r["batches"] / r["s"]
     assert r["max_per_step"] > world, r          # several batches per rank in one step
+    print("control plane", rate, "batches/s", r)
     assert rate >= world * 400, (rate, r)
 
 
