@@ -167,6 +167,7 @@ typedef struct {
   int N, H, W, F;
   int ldx, ldy, ldw1, ldw2, ldw3;
   long long* stamps;  // diagnostics only (null in the engine): per workgroup 8 x s_memrealtime / s_memtime
+  int kernel;         // 0: persistent warp-specialised (default), 1: phase-serialised (A/B, stamps)
 } DmlBlockArgs;
 
 // ---- single-op launches (used by tests and by the plan executor) ----

@@ -27,6 +27,8 @@
 //           64-channel chunks, fp32 staging (per-wave scratch, 32-pixel passes)
 //           -> each lane owns 8 channels of a pixel: bias + shortcut (16-B load)
 //           + ReLU -> one 16-B store. Phases 2-3 are wave-private (no barrier).
+#include <cstdlib>
+
 #include "conv_shared.h"
 
 namespace dml {
@@ -310,11 +312,354 @@ int set_attr() {
                                   Cfg<F>::LDS);
 }
 
+
+// ===================================================================================
+// Persistent, warp-specialised form (the default): phase 1 of tile t+1 runs beside
+// phases 2-3 of tile t in the SAME workgroup.
+//
+// The phase-serialised kernel above measured 283 us per 128 images (stage 2), every
+// phase latency-bound: all resident workgroups start in phase 1 together, so HBM is
+// read in bursts and idles while every CU sits in the 3x3 (profiles/r3_v1 stamps:
+// phase 1 16 us, 3x3 12 us, expand 26 us per workgroup). Here one 768-thread
+// workgroup per CU loops over tiles with two roles:
+//   producers (waves 0-4)  reduce the halo of tile t+1 into T1 buffer (t+1) & 1:
+//                          X straight from HBM into VGPRs (3-deep register ring)
+//   consumers (waves 5-11) 3x3 over T1 buffer t & 1 + expand + shortcut + store Y
+// and ONE s_barrier per tile (T1 is double-buffered), so the HBM read stream
+// (producers) overlaps the MFMA work and the store stream (consumers) of the
+// previous tile on every CU, all the time. Tile = 8 x 28 output pixels (14 pixel
+// fragments, two per consumer wave), halo 10 x 30 (19 fragments over 5 producers).
+// Tiles: each XCD owns a contiguous range, dealt round-robin to its workgroups, so
+// neighbouring tiles (which share halo rows) run at the same time in one L2.
+template <int F_>
+struct WsCfg {
+  static constexpr int F = F_, C = 4 * F_;
+  static constexpr int TH = 8, TW = 28;            // output tile
+  static constexpr int HH = TH + 2, HW = TW + 2;   // halo tile
+  static constexpr int HP = HH * HW;               // 300 halo pixels
+  static constexpr int HFR = (HP + 15) / 16;       // 19 halo fragments
+  static constexpr int OP = TH * TW;               // 224 output pixels
+  static constexpr int OF = OP / 16;               // 14 output fragments
+  static constexpr int NP = 5, NQ = 7, NW = NP + NQ, NT = NW * 64;
+  static constexpr int PF = (HFR + NP - 1) / NP;   // 4 halo fragments per producer wave
+  static constexpr int QF = OF / NQ;               // 2 output fragments per consumer wave
+  static constexpr int FCH = F / 16;
+  static constexpr int ROW = F * 2;
+  static constexpr int T1B = HFR * 16 * ROW;       // one T1 buffer (304 rows)
+  static constexpr int SROW = 64 * 4 + 16, EPX = QF * 16;
+  static constexpr int SCR_T2 = QF * 16 * ROW, SCR_EP = EPX * SROW;
+  static constexpr int SCR = SCR_T2 > SCR_EP ? SCR_T2 : SCR_EP;
+  static constexpr int LDS = 2 * T1B + NQ * SCR;
+  static constexpr int KS1 = C / 32, KS2 = 9 * F / 32, KS3 = F / 32;
+  static_assert(OP % 16 == 0 && OF % NQ == 0 && ROW >= 128, "tile / role split");
+  static_assert(LDS <= 163840, "one workgroup per CU");
+};
+
+__device__ __forceinline__ void lds_barrier() {
+  // producers' T1 writes (ds_write) done, then the rendezvous; global loads and
+  // stores stay in flight across it (no vmcnt wait)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int F>
+__global__ __launch_bounds__(WsCfg<F>::NT, 1) void block_ws_kernel(DmlBlockArgs a, int total) {
+  using T = WsCfg<F>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+  const bool producer = wid < T::NP;
+  const int tiles_w = (a.W + T::TW - 1) / T::TW, tiles_h = (a.H + T::TH - 1) / T::TH;
+  const int per_img = tiles_w * tiles_h;
+  // contiguous tile range per XCD (workgroup b runs on XCD b % 8), dealt round-robin
+  const int G = gridDim.x, x8 = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int gx = (G >> 3) + ((G & 7) > x8 ? 1 : 0);                  // workgroups on this XCD
+  const int t_lo = (int)((long)total * x8 / 8), t_hi = (int)((long)total * (x8 + 1) / 8);
+  const int my_tiles = slot < gx ? (t_hi - t_lo - slot + gx - 1) / gx : 0;
+  // every workgroup runs the same iteration count (the barrier count must match):
+  // the largest share; surplus iterations do no work
+  const int per_xcd_max = (total + 7) / 8;
+  const int iters = (per_xcd_max + (G >> 3) - 1) / max(G >> 3, 1);
+  auto tile_of = [&](int j) { return j < my_tiles ? t_lo + slot + j * gx : -1; };
+
+  const bf16* __restrict__ x = (const bf16*)a.x;
+  const unsigned short* __restrict__ xs = (const unsigned short*)a.x;
+  unsigned short* __restrict__ y = (unsigned short*)a.y;
+
+  // ---------------------------------------------------------- producer --
+  auto produce = [&](int t, char* t1) {
+    const int n = t / per_img, rem = t - n * per_img;
+    const int th = rem / tiles_w, tw = rem - th * tiles_w;
+    const long img = (long)n * a.H * a.W;
+    const bf16* __restrict__ w1p = (const bf16*)a.w1 + (long)frow * a.ldw1 + fq * 8;
+    // two passes of PF / 2 halo fragments: half the accumulators and X ring live at
+    // once (W1 is streamed from L2 twice), so the union with the consumer code fits
+    // the 168 VGPRs of 3 waves per SIMD without spilling
+    constexpr int PP = T::PF / 2;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+      const bf16* xp[PP];
+      float mk[PP];
+      int hps[PP];
+#pragma unroll
+      for (int k = 0; k < PP; ++k) {
+        const int hf = min(wid + T::NP * (PP * pass + k), T::HFR - 1);  // a duplicate when past the end: never stored
+        const int hp = 16 * hf + frow;
+        const int hr = hp / T::HW, hc = hp - hr * T::HW;
+        const int h = th * T::TH - 1 + hr, w = tw * T::TW - 1 + hc;
+        const bool ok = hp < T::HP && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+        mk[k] = ok ? 1.f : 0.f;
+        hps[k] = hp;
+        const int hcl = min(max(h, 0), a.H - 1), wcl = min(max(w, 0), a.W - 1);
+        xp[k] = x + (img + (long)hcl * a.W + wcl) * a.ldx + fq * 8;
+      }
+      f32x4 acc[T::FCH][PP];
+#pragma unroll
+      for (int i = 0; i < T::FCH; ++i)
+#pragma unroll
+        for (int k = 0; k < PP; ++k) acc[i][k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      // k-steps in a rolled loop with explicit register buffers (a fully unrolled
+      // ring lets the scheduler hoist every load: 129 VGPRs of spills measured);
+      // X two k-steps ahead (HBM latency), W1 one ahead (L2)
+      bf16x8 x0[PP], x1[PP], x2[PP], w0[T::FCH], w1[T::FCH];
+      auto ldx = [&](bf16x8 (&d)[PP], int ks) {
+#pragma unroll
+        for (int k = 0; k < PP; ++k) d[k] = *(const bf16x8*)(xp[k] + ks * 32);
+      };
+      auto ldw = [&](bf16x8 (&d)[T::FCH], int ks) {
+#pragma unroll
+        for (int i = 0; i < T::FCH; ++i) d[i] = *(const bf16x8*)(w1p + (long)i * 16 * a.ldw1 + ks * 32);
+      };
+      ldx(x0, 0);
+      ldx(x1, 1);
+      ldw(w0, 0);
+#pragma unroll 1
+      for (int ks = 0; ks < T::KS1; ++ks) {
+        if (ks + 2 < T::KS1) ldx(x2, ks + 2);
+        if (ks + 1 < T::KS1) ldw(w1, ks + 1);
+#pragma unroll
+        for (int i = 0; i < T::FCH; ++i)
+#pragma unroll
+          for (int k = 0; k < PP; ++k)
+            acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[i], x0[k], acc[i][k], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < PP; ++k) {
+          x0[k] = x1[k];
+          x1[k] = x2[k];
+        }
+#pragma unroll
+        for (int i = 0; i < T::FCH; ++i) w0[i] = w1[i];
+      }
+#pragma unroll
+      for (int i = 0; i < T::FCH; ++i) {
+        const float4 bb = *(const float4*)(a.b1 + 16 * i + 4 * fq);
+#pragma unroll
+        for (int k = 0; k < PP; ++k) {
+          if (wid + T::NP * (PP * pass + k) >= T::HFR) continue;  // wave-uniform
+          const f32x4 v = acc[i][k];
+          const float m = mk[k];
+          const uint2 o = make_uint2(pack2(fmaxf(v[0] + bb.x, 0.f) * m, fmaxf(v[1] + bb.y, 0.f) * m),
+                                     pack2(fmaxf(v[2] + bb.z, 0.f) * m, fmaxf(v[3] + bb.w, 0.f) * m));
+          const int ch = 16 * i + 4 * fq;
+          *(uint2*)(t1 + toff<T::ROW>(hps[k], ch >> 3) + (ch & 7) * 2) = o;
+        }
+      }
+    }
+  };
+
+  // ---------------------------------------------------------- consumer --
+  const int q = wid - T::NP;
+  char* scr = smem + 2 * T::T1B + (producer ? 0 : q) * T::SCR;
+  auto consume = [&](int t, const char* t1) {
+    const int n = t / per_img, rem = t - n * per_img;
+    const int th = rem / tiles_w, tw = rem - th * tiles_w;
+    const long img = (long)n * a.H * a.W;
+    const int oh0 = th * T::TH, ow0 = tw * T::TW;
+    int hb[T::QF];
+#pragma unroll
+    for (int k = 0; k < T::QF; ++k) {
+      const int op = 16 * (T::QF * q + k) + frow;
+      const int r = op / T::TW, c = op - r * T::TW;
+      hb[k] = r * T::HW + c;
+    }
+    // 3x3 from T1 (per-lane shifted rows: a tap is a uniform offset)
+    const bf16* __restrict__ w2p = (const bf16*)a.w2 + (long)frow * a.ldw2 + fq * 8;
+    f32x4 acc[T::FCH][T::QF];
+#pragma unroll
+    for (int i = 0; i < T::FCH; ++i)
+#pragma unroll
+      for (int k = 0; k < T::QF; ++k) acc[i][k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    {
+      // rolled over the 9 taps; a tap's weights (HF k-steps) are loaded one tap ahead
+      constexpr int HF = F / 32;
+      bf16x8 wc[HF][T::FCH], wn[HF][T::FCH];
+      auto ldw = [&](bf16x8 (&d)[HF][T::FCH], int tp) {
+#pragma unroll
+        for (int hf = 0; hf < HF; ++hf)
+#pragma unroll
+          for (int i = 0; i < T::FCH; ++i)
+            d[hf][i] = *(const bf16x8*)(w2p + (long)i * 16 * a.ldw2 + (tp * HF + hf) * 32);
+      };
+      ldw(wc, 0);
+#pragma unroll 1
+      for (int tp = 0; tp < 9; ++tp) {
+        if (tp + 1 < 9) ldw(wn, tp + 1);
+        const int tap = (tp / 3) * T::HW + (tp % 3);
+#pragma unroll
+        for (int hf = 0; hf < HF; ++hf) {
+          bf16x8 xb[T::QF];
+#pragma unroll
+          for (int k = 0; k < T::QF; ++k) xb[k] = *(const bf16x8*)(t1 + toff<T::ROW>(hb[k] + tap, hf * 4 + fq));
+#pragma unroll
+          for (int i = 0; i < T::FCH; ++i)
+#pragma unroll
+            for (int k = 0; k < T::QF; ++k)
+              acc[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc[hf][i], xb[k], acc[i][k], 0, 0, 0);
+        }
+#pragma unroll
+        for (int hf = 0; hf < HF; ++hf)
+#pragma unroll
+          for (int i = 0; i < T::FCH; ++i) wc[hf][i] = wn[hf][i];
+      }
+    }
+    // epilogue items: staging pixel (lane >> 3) + 8 it of the wave's 32, channel group lane & 7
+    const int cg = lane & 7;
+    long opix[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int pxl = (lane >> 3) + 8 * it;
+      const int op = 16 * T::QF * q + pxl;
+      const int r = op / T::TW, c = op - r * T::TW;
+      const int oh = oh0 + r, ow = ow0 + c;
+      opix[it] = (oh < a.H && ow < a.W) ? img + (long)oh * a.W + ow : -1;
+    }
+    // shortcut rows of chunk 0, issued now: in flight under the T2 round trip and chunk 0's MFMAs (loaded during the 3x3 they cost 24 VGPRs)
+    uint4 rr[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+      rr[it] = opix[it] >= 0 ? *(const uint4*)(xs + opix[it] * a.ldx + 8 * cg) : make_uint4(0, 0, 0, 0);
+    // T2 = bias + ReLU -> bf16 rows in this wave's scratch -> expand B fragments
+#pragma unroll
+    for (int i = 0; i < T::FCH; ++i) {
+      const float4 bb = *(const float4*)(a.b2 + 16 * i + 4 * fq);
+#pragma unroll
+      for (int k = 0; k < T::QF; ++k) {
+        const f32x4 v = acc[i][k];
+        const uint2 o = make_uint2(pack2(fmaxf(v[0] + bb.x, 0.f), fmaxf(v[1] + bb.y, 0.f)),
+                                   pack2(fmaxf(v[2] + bb.z, 0.f), fmaxf(v[3] + bb.w, 0.f)));
+        const int ch = 16 * i + 4 * fq;
+        *(uint2*)(scr + toff<T::ROW>(16 * k + frow, ch >> 3) + (ch & 7) * 2) = o;
+      }
+    }
+    wave_lds_sync();
+    bf16x8 tb[T::QF][T::KS3];
+#pragma unroll
+    for (int k = 0; k < T::QF; ++k)
+#pragma unroll
+      for (int s = 0; s < T::KS3; ++s) tb[k][s] = *(const bf16x8*)(scr + toff<T::ROW>(16 * k + frow, s * 4 + fq));
+    wave_lds_sync();
+    // expand in 64-channel chunks + shortcut + ReLU -> Y
+    const bf16* __restrict__ w3p = (const bf16*)a.w3 + (long)frow * a.ldw3 + fq * 8;
+#pragma unroll 1
+    for (int cc = 0; cc < T::C / 64; ++cc) {
+      f32x4 e[4][T::QF];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < T::QF; ++k) e[i][k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < T::KS3; ++s) {
+        bf16x8 wa[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wa[i] = *(const bf16x8*)(w3p + (long)(64 * cc + 16 * i) * a.ldw3 + s * 32);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int k = 0; k < T::QF; ++k) e[i][k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i], tb[k][s], e[i][k], 0, 0, 0);
+      }
+      const float4 bb0 = *(const float4*)(a.b3 + 64 * cc + 8 * cg);
+      const float4 bb1 = *(const float4*)(a.b3 + 64 * cc + 8 * cg + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < T::QF; ++k)
+          *(f32x4*)(scr + (16 * k + frow) * T::SROW + (16 * i + 4 * fq) * 4) = e[i][k];
+      wave_lds_sync();
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int pxl = (lane >> 3) + 8 * it;
+        const float4 v0 = *(const float4*)(scr + pxl * T::SROW + cg * 32);
+        const float4 v1 = *(const float4*)(scr + pxl * T::SROW + cg * 32 + 16);
+        const uint4 r = rr[it];
+        float f[8] = {v0.x + bb0.x + bf2f(r.x & 0xffff), v0.y + bb0.y + bf2f(r.x >> 16),
+                      v0.z + bb0.z + bf2f(r.y & 0xffff), v0.w + bb0.w + bf2f(r.y >> 16),
+                      v1.x + bb1.x + bf2f(r.z & 0xffff), v1.y + bb1.y + bf2f(r.z >> 16),
+                      v1.z + bb1.z + bf2f(r.w & 0xffff), v1.w + bb1.w + bf2f(r.w >> 16)};
+        if (opix[it] >= 0)
+          *(uint4*)(y + opix[it] * a.ldy + 64 * cc + 8 * cg) =
+              make_uint4(pack2(fmaxf(f[0], 0.f), fmaxf(f[1], 0.f)), pack2(fmaxf(f[2], 0.f), fmaxf(f[3], 0.f)),
+                         pack2(fmaxf(f[4], 0.f), fmaxf(f[5], 0.f)), pack2(fmaxf(f[6], 0.f), fmaxf(f[7], 0.f)));
+        if (cc + 1 < T::C / 64 && opix[it] >= 0)
+          rr[it] = *(const uint4*)(xs + opix[it] * a.ldx + 64 * (cc + 1) + 8 * cg);
+      }
+      wave_lds_sync();
+    }
+  };
+
+  // ---------------------------------------------------------- schedule --
+  // prologue: T1 of the first tile; then one barrier per tile. The two roles run
+  // separate loops with the same barrier count, so each role's loop-invariant
+  // values stay out of the other's register budget (one shared loop spilled 49
+  // VGPRs although either role alone fits the 168 of 3 waves per SIMD).
+  if (producer) {
+    if (tile_of(0) >= 0) produce(tile_of(0), smem);
+    lds_barrier();
+#pragma unroll 1
+    for (int j = 0; j < iters; ++j) {
+      const int tn = tile_of(j + 1);
+      if (tn >= 0) produce(tn, smem + ((j + 1) & 1) * T::T1B);
+      lds_barrier();
+    }
+  } else {
+    lds_barrier();
+#pragma unroll 1
+    for (int j = 0; j < iters; ++j) {
+      const int t = tile_of(j);
+      if (t >= 0) consume(t, smem + (j & 1) * T::T1B);
+      lds_barrier();
+    }
+  }
+}
+
+static int cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+template <int F>
+int launch_ws(const DmlBlockArgs* a, hipStream_t s) {
+  using T = WsCfg<F>;
+  const int total = a->N * ((a->H + T::TH - 1) / T::TH) * ((a->W + T::TW - 1) / T::TW);
+  const int grid = max(8, min(cu_count(), ((total + 7) / 8) * 8));
+  hipLaunchKernelGGL((block_ws_kernel<F>), dim3((unsigned)grid), dim3(T::NT), T::LDS, s, *a, total);
+  DML_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace blk
 }  // namespace dml
 
 extern "C" int dml_block_fused_init(void) {
-  const int rc = dml::blk::set_attr<64>();
+  const int rc = dml::blk::set_attr<64>() |
+                 (int)hipFuncSetAttribute((const void*)dml::blk::block_ws_kernel<64>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, dml::blk::WsCfg<64>::LDS);
   if (rc) dml_set_error("dml_block_fused_init: hipFuncSetAttribute failed");
   return rc ? -1 : 0;
 }
@@ -327,5 +672,5 @@ extern "C" int dml_block_fused(const DmlBlockArgs* a, hipStream_t s) {
     dml_set_error("dml_block_fused: unsupported shape (F = 64, C = 4F, 8-aligned strides, y != x)");
     return -1;
   }
-  return dml::blk::launch<64>(a, s);
+  return a->kernel == 1 ? dml::blk::launch<64>(a, s) : dml::blk::launch_ws<64>(a, s);
 }

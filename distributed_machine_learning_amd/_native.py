@@ -101,7 +101,7 @@ class BlockArgs(C.Structure):
         ("w3", C.c_void_p), ("b3", C.c_void_p), ("y", C.c_void_p),
         ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("F", C.c_int),
         ("ldx", C.c_int), ("ldy", C.c_int), ("ldw1", C.c_int), ("ldw2", C.c_int), ("ldw3", C.c_int),
-        ("stamps", C.c_void_p),
+        ("stamps", C.c_void_p), ("kernel", C.c_int),
     ]
 
 

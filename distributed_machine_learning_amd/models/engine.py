@@ -539,7 +539,8 @@ class Engine:
                 h, w, _ = g.shape(r.inp)
                 ba = N.BlockArgs(self.buf[r.inp].data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
                                  b2.data_ptr(), w3.data_ptr(), b3.data_ptr(), self.buf[e.out].data_ptr(), B, h, w,
-                                 r.cout, self.cbuf[r.inp], self.cbuf[e.out], kp1, kp2, kp3, None)
+                                 r.cout, self.cbuf[r.inp], self.cbuf[e.out], kp1, kp2, kp3, None,
+                                 int(os.environ.get("DML_BLOCK_KERNEL", "0")))
                 N.check(L.dml_plan_add_block(plan, C.byref(ba)), "plan fused block")
                 self._keep.append(ba)
                 self.op_names.append(f"{r.name}+{c.name}+{e.name}")

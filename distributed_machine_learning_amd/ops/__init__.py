@@ -237,11 +237,13 @@ def expand_reduce(x: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, res: Opti
 
 def block_fused(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
                 w3: torch.Tensor, b3: torch.Tensor, out: Optional[torch.Tensor] = None,
-                stamps: Optional[torch.Tensor] = None) -> torch.Tensor:
+                stamps: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
     """A whole identity bottleneck block in one kernel (csrc/kernels/block_fused.hip):
     y = relu(1x1(F -> C) of relu(3x3(F -> F) of relu(1x1(C -> F) of x)) + x), C = 4F.
     x: bf16 NHWC [N, H, W, C]; w1 [>=F][>=C], w2 [>=F][>=9F] (r, s, c), w3 [>=C][>=F]
-    packed (pack_weight); biases fp32. Returns bf16 NHWC [N, H, W, C]."""
+    packed (pack_weight); biases fp32. Returns bf16 NHWC [N, H, W, C].
+    kernel: 0 = persistent warp-specialised (default), 1 = phase-serialised
+    (``stamps``: per-workgroup phase timestamps, phase-serialised form only)."""
     n, h, w, c = x.shape
     f = c // 4
     y = out if out is not None else torch.empty_like(x)
@@ -250,7 +252,7 @@ def block_fused(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.T
     assert w1.shape[0] >= f and w2.shape[0] >= f and w3.shape[0] >= c and bs[0].numel() >= f and bs[2].numel() >= c
     a = N.BlockArgs(x.data_ptr(), w1.data_ptr(), bs[0].data_ptr(), w2.data_ptr(), bs[1].data_ptr(), w3.data_ptr(),
                     bs[2].data_ptr(), y.data_ptr(), n, h, w, f, x.shape[-1], y.shape[-1], w1.shape[1], w2.shape[1],
-                    w3.shape[1], stamps.data_ptr() if stamps is not None else None)
+                    w3.shape[1], stamps.data_ptr() if stamps is not None else None, kernel)
     N.check(N.lib().dml_block_fused(C.byref(a), N.stream_ptr()), "dml_block_fused")
     y._keep = bs
     return y

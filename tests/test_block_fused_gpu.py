@@ -35,15 +35,16 @@ def _reference(x, w1, w2, w3, b1, b2, b3):
     return y.permute(0, 2, 3, 1)
 
 
-@pytest.mark.parametrize("n,h,w", [(2, 56, 56), (1, 20, 20), (3, 30, 23), (1, 28, 28)])
-def test_block_fused_matches_unfused_and_fp32(n, h, w):
+@pytest.mark.parametrize("kernel", [0, 1])
+@pytest.mark.parametrize("n,h,w", [(2, 56, 56), (1, 20, 20), (3, 30, 23), (1, 28, 28), (5, 56, 56)])
+def test_block_fused_matches_unfused_and_fp32(n, h, w, kernel):
     f = 64
     c = 4 * f
     dev = "cuda"
     w1, w2, w3, b1, b2, b3 = _block_params(f, seed=n * 100 + h)
     x = torch.randn(n, h, w, c, generator=torch.Generator().manual_seed(7)).to(torch.bfloat16).to(dev)
     w1p, w2p, w3p = (ops.pack_weight(t)[0].to(dev) for t in (w1, w2, w3))
-    y = ops.block_fused(x, w1p, b1, w2p, b2, w3p, b3)
+    y = ops.block_fused(x, w1p, b1, w2p, b2, w3p, b3, kernel=kernel)
     # the three-launch path of the same block
     t1 = ops.conv2d_nhwc(x, w1p, b1, f, 1, 1, relu=True)
     t2 = ops.conv2d_nhwc(t1, w2p, b2, f, 3, 3, pad=(1, 1), relu=True)

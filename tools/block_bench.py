@@ -60,7 +60,9 @@ def main():
 
     y = torch.empty_like(x)
     fused = {"cold_us": timeit(lambda: ops.block_fused(x, w1p, b1, w2p, b2, w3p, b3, out=y), True),
-             "warm_us": timeit(lambda: ops.block_fused(x, w1p, b1, w2p, b2, w3p, b3, out=y), False)}
+             "warm_us": timeit(lambda: ops.block_fused(x, w1p, b1, w2p, b2, w3p, b3, out=y), False),
+             "phased_cold_us": timeit(lambda: ops.block_fused(x, w1p, b1, w2p, b2, w3p, b3, out=y, kernel=1), True),
+             "phased_warm_us": timeit(lambda: ops.block_fused(x, w1p, b1, w2p, b2, w3p, b3, out=y, kernel=1), False)}
     # unfused: each conv on its cold-tuned best cfg
     t1 = torch.empty(n, hw, hw, f, dtype=torch.bfloat16, device=dev)
     t2 = torch.empty_like(t1)
@@ -83,7 +85,7 @@ def main():
     nblk = n * ((hw + 13) // 14) ** 2
     st = torch.zeros(nblk * 8, dtype=torch.int64, device=dev)
     scrub.add_(1.0)
-    ops.block_fused(x, w1p, b1, w2p, b2, w3p, b3, out=y, stamps=st)
+    ops.block_fused(x, w1p, b1, w2p, b2, w3p, b3, out=y, stamps=st, kernel=1)
     torch.cuda.synchronize()
     s = st.view(nblk, 4, 2).cpu().double()
     rt = s[:, :, 0]  # 100 MHz real-time ticks
@@ -93,6 +95,7 @@ def main():
     ph["kernel_span_us"] = round(float(rt[:, 3].max() - t0) / 100.0, 2)
     ph["clock_ghz"] = round(float(((s[:, 3, 1] - s[:, 0, 1]) / (rt[:, 3] - rt[:, 0])).median()) / 10.0, 3)
     fused["stamps"] = ph
+    ops.block_fused(x, w1p, b1, w2p, b2, w3p, b3, out=y)  # the default (checked below)
     torch.cuda.synchronize()
     d = (y.float() - y3.float()).abs().max().item()
     res = {"n": n, "hw": hw, "F": f, "C": c, "fused": fused, "unfused": unf,
