@@ -21,7 +21,9 @@ step, so ANY survivor can continue as coordinator:
                  flight: a rank may receive several batches in one step) and
                  revoke requests (preemption of a rank's not-yet-launched
                  batches when the fair-share split moves it to the other model)
-    all-gather   of those records (+ a broadcast of the log bytes when any)
+    exchange     of those records: every rank gets all of them (gloo: gather to the
+                 coordinator + broadcast, two hops at any world size), plus a
+                 broadcast of the log bytes when there are any
     every rank   applies, in this order on every rank: log records -> reports ->
                  revoke answers -> the table; identical queues, in-flight sets,
                  job counters and metrics everywhere
@@ -597,7 +599,7 @@ class CollectiveService:
         out = torch.empty((world, L), dtype=torch.int64, device=self.dev)
         applied_here: List[dict] = []
         try:
-            eg.all_gather_into(out, rec_t)
+            (eg.all_gather_into(out, rec_t) if os.environ.get('DML_AG') else eg.exchange(out, rec_t, root))
             h = out.cpu().numpy()
             n = int(h[root, H_LOGLEN])
             if n:
@@ -682,6 +684,10 @@ class CollectiveService:
             self._grow([g for g in range(63) if (int(h[root, H_GROW]) >> g) & 1])
         self._poll()
         self.steps += 1
+        if os.environ.get("DML_SVC_DEBUG") and self.steps % 200 == 0:
+            log.warning("rank %d step %d epoch %d: queued %s inflight %d hostq %d gpu %d done %d root %d",
+                        eg.grank, self.steps, eg.epoch, {m: len(q) for m, q in coord.jobs.queues.items()},
+                        len(coord.inflight), len(self.hostq), len(self.gpu), len(self.done), root)
         self.last_progress = time.monotonic()
         t5 = time.perf_counter()
         ph["launch"] += t5 - t4

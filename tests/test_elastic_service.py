@@ -44,7 +44,7 @@ def _rank_main(grank, world, rdzv, swim_base, out, kill_rank, kill_step, control
     if svc.is_coordinator():
         svc.submit_local("ResNet50", 96)
         svc.submit_local("InceptionV3", 96)
-    steps = svc.serve(max_steps=3000, stop_when_idle=True)
+    steps = svc.serve(max_steps=10 ** 6, stop_when_idle=True)  # steps are ~1 ms: the budget is not the bound
     with coord.lock:
         res = {"steps": steps, "rebuilds": svc.rebuilds, "epoch": eg.epoch, "members": eg.members,
                "coordinator": svc.coordinator_rank(), "done": [coord.jobs.jobs[j].done for j in (31, 32)],
@@ -115,7 +115,7 @@ def test_coordinator_kill_mid_job_failover(tmp_path):
     assert codes[3] == 17 and codes[:3] == [0, 0, 0], codes
     r = res[2]
     assert r["coordinator"] == 2 and r["members"] == [0, 1, 2] and r["rebuilds"] >= 1
-    assert r["done"] == [True, True]
+    assert r["done"] == [True, True], (r["steps"], r["rebuilds"], r["requeued"], r["written"])
     assert r["c1"]["ResNet50"]["query_count"] >= 96 and r["c1"]["InceptionV3"]["query_count"] >= 96
     batches = {tuple(os.path.basename(f).split("_")[1:3]) for f in r["store_outputs"]}
     assert batches == {(str(j), str(b)) for j in (31, 32) for b in range(1, 13)}

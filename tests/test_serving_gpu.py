@@ -151,7 +151,7 @@ def test_collective_service_rccl_world1_outputs(tmp_path):
         svc.submit_local("InceptionV3", 20)     # 8 + 8 + 4
         svc.set_batch_size("ResNet50", 32)      # applied after the first submit's batching
         svc.submit_local("ResNet50", 32)        # one 32-image batch = 2 engine passes of 16
-        svc.serve(max_steps=200, stop_when_idle=True)
+        svc.serve(max_steps=10 ** 6, stop_when_idle=True)
         assert [coord.jobs.jobs[j].done for j in (31, 32, 33)] == [True, True, True]
         files = sorted(os.listdir(tmp_path / "out"))
         assert len(files) == 3 + 3 + 1, files
@@ -217,7 +217,7 @@ def test_store_images_replicated_to_hbm_and_served(tmp_path):
         svc = CollectiveService(eg, be, coord, writer=writer, on_device=False)
         names = sorted(blobs)
         svc.submit_local("ResNet50", images=names)
-        svc.serve(max_steps=100, stop_when_idle=True)
+        svc.serve(max_steps=10 ** 6, stop_when_idle=True)
         st = be.arenas["ResNet50"]
         assert st.replicated == 12 and st.failed == {"broken.jpeg"}
         doc = {}
