@@ -186,6 +186,11 @@ int dml_conv_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s);
 int dml_conv_v2_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s);
 int dml_conv_v2_group_supported(int cfg);
 int dml_conv_v2_bn(int cfg);
+// shifted-pixel stride-1 "same" conv (conv_shift.hip; cfg ids 64..)
+int dml_conv_shift(const DmlConvArgs* a, int cfg, hipStream_t s);
+int dml_conv_shift_bn(int cfg);
+const char* dml_conv_shift_check(const DmlConvArgs* a, int cfg);
+int dml_conv_shift_init(void);
 int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);

@@ -4,8 +4,9 @@
 // Serves every convolution of ResNet50 / InceptionV3 and the FC layer
 // (SURVEY §2.7 "conv_igemm_bf16"; the reference runs these inside Keras,
 // models.py:26,51 — it has no kernel of its own). cfg ids 10..63 select a v2
-// tile configuration (dml_conv_v2); they are part of the ABI the plan builder
-// and the autotuner (ops/tuning.py) use.
+// tile configuration (dml_conv_v2), ids 64.. a shifted-pixel configuration of
+// the stride-1 "same" conv kernel (conv_shift.hip); they are part of the ABI the
+// plan builder and the autotuner (ops/tuning.py) use.
 //
 // Removed in r2 (measured never faster, kept only as history in DESIGN.md and
 // profiles/): the register-staged v1 kernel (cfg 0..4, profiles/r1_v2) and the
@@ -16,10 +17,17 @@
 #include "pool_shared.h"
 
 static int validate(const DmlConvArgs* a, int cfg) {
-  const int bn = (cfg >= 10 && cfg < 64) ? dml_conv_v2_bn(cfg) : 0;
+  const int bn = dml_conv_v2_bn(cfg);
   if (bn <= 0) {
-    dml_set_error("dml_conv: cfg must be a v2 tile config (10..63)");
+    dml_set_error("dml_conv: cfg must be a v2 tile config (10..63) or a shifted-pixel config (64..)");
     return -1;
+  }
+  if (cfg >= 64) {  // shifted-pixel kernel (conv_shift.hip): stride-1 same convs only
+    const char* why = dml_conv_shift_check(a, cfg);
+    if (why) {
+      dml_set_error(why);
+      return -1;
+    }
   }
   // weights are packed with Cout padded to a multiple of 256 rows; a 96- or
   // 192-wide channel tile must not run past them
@@ -48,7 +56,7 @@ static int validate(const DmlConvArgs* a, int cfg) {
 
 extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
   if (validate(a, cfg) != 0) return -1;
-  return dml_conv_v2(a, cfg, s);
+  return cfg >= 64 ? dml_conv_shift(a, cfg, s) : dml_conv_v2(a, cfg, s);
 }
 
 extern "C" int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg) {

@@ -97,8 +97,25 @@ int main() {
   a = conv_args(64, 64, 3, 3);
   CHECK(dml_conv(&a, 99, nullptr) != 0);        // unknown config
   CHECK(dml_conv(&a, 35, nullptr) != 0);        // an unassigned id inside 10..63
-  CHECK(dml_conv(&a, 64, nullptr) != 0);        // past the table
+  CHECK(dml_conv(&a, 90, nullptr) != 0);        // past the table
   CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
+  // shifted-pixel configs (64..): stride-1 "same" convs only, halo within the config's LDS rows
+  CHECK(dml_conv_v2_bn(64) == 128 && dml_conv_v2_bn(68) == 64 && dml_conv_v2_bn(70) == 0);
+  a.ph = 0;
+  CHECK(dml_conv(&a, 64, nullptr) != 0);        // valid (not same) padding
+  CHECK(std::string(dml_last_error()).find("same padding") != std::string::npos);
+  a = conv_args(64, 64, 3, 3);
+  a.sh = a.sw = 2; a.Ho = a.Wo = 7;
+  CHECK(dml_conv(&a, 65, nullptr) != 0);        // stride 2
+  a = conv_args(48, 64, 3, 3);
+  CHECK(dml_conv(&a, 64, nullptr) != 0);        // Cin % BK
+  a = conv_args(64, 64, 1, 1);
+  CHECK(dml_conv(&a, 66, nullptr) != 0);        // 1 tap < STAGES
+  a = conv_args(64, 64, 5, 5);
+  a.H = a.W = a.Ho = a.Wo = 60;
+  CHECK(dml_conv(&a, 66, nullptr) != 0);        // 128 + 2*(2*60+2) halo rows > 256
+  CHECK(std::string(dml_last_error()).find("halo") != std::string::npos);
+  a = conv_args(64, 64, 3, 3);
   a.nseg = 5;
   CHECK(dml_conv(&a, 11, nullptr) != 0);        // too many output segments
   a.nseg = 2;

@@ -30,6 +30,7 @@ SOURCES = [
     CSRC / "kernels" / "conv_pool.hip",
     CSRC / "kernels" / "bottleneck_fused.hip",
     CSRC / "kernels" / "block_fused.hip",
+    CSRC / "kernels" / "conv_shift.hip",
     CSRC / "runtime" / "runtime.hip",
 ]
 HEADERS = [CSRC / "include" / "dml.h"] + sorted((CSRC / "kernels").glob("*.h"))  # every header the stamp covers

@@ -73,10 +73,12 @@ class HbmImageStore:
 
     # ---------------------------------------------------------- replicate --
     def replicate(self, names: Sequence[str], load: Callable[[List[str]], Dict[str, Optional[np.ndarray]]],
-                  group=None, rank: int = 0, world: int = 1, gather: Optional[Callable] = None) -> int:
+                  group=None, rank: int = 0, world: int = 1, gather: Optional[Callable] = None,
+                  keep: Optional[set] = None) -> int:
         """Decode this rank's share of the new images and all-gather every
         rank's share into every rank's arena. ``gather(out, t)`` is the
-        all-gather to use (default: torch.distributed over ``group``)."""
+        all-gather to use (default: torch.distributed over ``group``). FIFO
+        eviction never picks a name in ``names`` or ``keep``."""
         missing = self.missing(names)
         if not missing:
             return 0
@@ -108,7 +110,7 @@ class HbmImageStore:
             gather(allimg, send)
             gather(allok, okd)
         flags = allok.cpu().numpy()
-        keep = set(names)
+        keep = set(names) | (keep or set())
         src, dst = [], []
         for i, n in enumerate(missing):
             k = (i % world) * chunk + i // world
@@ -174,7 +176,8 @@ class HbmImageStore:
         (standalone use without a service). Failed images get slot 0."""
         rest = self.missing(names)
         if rest and load is not None:
-            self.replicate(rest, load)
+            # the batch's resident images must survive the eviction its missing ones cause
+            self.replicate(rest, load, keep=set(names))
         out, failed = [], []
         for n in names:
             if self._synthetic(n):

@@ -248,3 +248,28 @@ def test_hbm_image_store_decode_once_replicate_gloo(tmp_path):
         assert res[r]["failed"] == ["bad.jpeg"]
         assert res[r]["vals"][:10] == list(range(10)) and res[r]["vals"][11] == 3
     assert res[0]["vals"] == res[1]["vals"] == res[2]["vals"]
+
+
+def test_hbm_image_store_eviction_keeps_the_batch():
+    """A full arena evicts FIFO, but never an image of the batch being
+    resolved: a batch mixing resident and missing-at-launch images gets every
+    resident image from its slot and the missing ones decoded into evicted
+    slots of OTHER images (eviction vs in-flight gathers)."""
+    import numpy as np
+    import torch
+
+    from distributed_machine_learning_amd.parallel.image_store import HbmImageStore
+
+    def load(names):
+        return {n: np.full((2, 2, 3), int(n.split(".")[0]), np.uint8) for n in names}
+
+    st = HbmImageStore(6, (2, 2), torch.device("cpu"), n_synth=0)
+    st.replicate([f"{i}.jpeg" for i in range(6)], load)       # full: 0..5
+    batch = ["0.jpeg", "1.jpeg", "7.jpeg", "8.jpeg", "2.jpeg"]  # 0,1,2 resident (the oldest), 7,8 missing
+    slots, failed = st.slots(batch, load)
+    assert failed == []
+    assert st.arena[slots].numpy()[:, 0, 0, 0].tolist() == [0, 1, 7, 8, 2]
+    assert "3.jpeg" not in st.index and "4.jpeg" not in st.index   # the oldest NOT in the batch went
+    assert len(set(slots)) == 5
+    with pytest.raises(RuntimeError):                               # a batch larger than the arena
+        st.slots([f"{i}.jpeg" for i in range(10, 17)], load)

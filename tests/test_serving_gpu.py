@@ -263,3 +263,71 @@ def test_rccl_abort_and_new_epoch(tmp_path):
         eg.barrier()
     finally:
         eg.close()
+
+
+def test_small_arena_eviction_and_missing_at_launch(tmp_path):
+    """an HBM arena smaller than two jobs. Job B's
+    replication evicts job A's images before A's batches launch, so A's images
+    are missing at launch and decoded again by the fallback in launch(), whose
+    arena writes evict other images while gathers are still queued on the
+    compute stream. Every output row must still equal Engine.infer of the
+    right decoded images."""
+    import io
+
+    from PIL import Image
+
+    from distributed_machine_learning_amd.models import build_model
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+    from distributed_machine_learning_amd.parallel.service import (CollectiveService, GpuRankBackend, OutputWriter,
+                                                                   ReplicatedCoordinator)
+    from distributed_machine_learning_amd.serving.inference import load_image
+    from distributed_machine_learning_amd.utils.labels import load_class_index
+
+    rng = np.random.default_rng(1)
+    blobs = {}
+    for j in "ab":
+        for i in range(12):
+            buf = io.BytesIO()
+            Image.fromarray(rng.integers(0, 255, (256, 240 + 4 * i, 3), dtype=np.uint8)).save(buf, format="JPEG")
+            blobs[f"{j}{i}.jpeg"] = buf.getvalue()
+    loads = []
+
+    def loader(ns):
+        loads.append(list(ns))
+        return {n: blobs.get(n) for n in ns}
+    dev = torch.device("cuda", 0)
+    eg = ElasticGroup(0, 1, store_path=str(tmp_path / "rdzv"), backend="gloo", data_backend="nccl", timeout_s=120)
+    try:
+        bs = {"ResNet50": 8, "InceptionV3": 8}
+        be = GpuRankBackend(dev, bs, cap=8, arena_images=24, n_synth=8, loader=loader)
+        st = be.arenas["ResNet50"]
+        assert st.capacity == 24                      # 16 image slots for 24 job images
+        coord = ReplicatedCoordinator(bs, cap=8, host_tag="gpu")
+        writer = OutputWriter(str(tmp_path / "out"), host_tag="gpu")
+        svc = CollectiveService(eg, be, coord, writer=writer, on_device=False)
+        na = [f"a{i}.jpeg" for i in range(12)]
+        nb = [f"b{i}.jpeg" for i in range(12)]
+        svc.submit_local("ResNet50", images=na)
+        svc.submit_local("ResNet50", images=nb)
+        svc.serve(max_steps=10 ** 6, stop_when_idle=True)
+        assert st.replicated > 24                     # images were decoded again at launch
+        doc = {}
+        for f in os.listdir(tmp_path / "out"):
+            doc.update(json.load(open(tmp_path / "out" / f)))
+        assert sorted(doc) == sorted(na + nb)
+        g, w = build_model("ResNet50", seed=0)
+        cls = {wnid: i for i, (wnid, _) in enumerate(load_class_index())}
+        for names in (na, nb):
+            imgs = torch.from_numpy(np.stack([load_image(blobs[n], (224, 224)) for n in names]))
+            for b0 in range(0, 12, 8):
+                rows = imgs[b0:b0 + 8]
+                pad = torch.zeros((8, 224, 224, 3), dtype=torch.uint8)
+                pad[:len(rows)] = rows
+                ref = _split_ref(g, w, pad, 4)
+                for i in range(len(rows)):
+                    n = names[b0 + i]
+                    assert [cls[e[0]] for e in doc[n][0]] == ref[0, i].tolist(), n
+                    assert np.allclose([e[2] for e in doc[n][0]], ref[1, i].view(torch.float32).numpy(),
+                                       rtol=0, atol=0), n
+    finally:
+        eg.close()
