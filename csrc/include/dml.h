@@ -150,6 +150,7 @@ typedef struct {
   // pixel (a shortcut after the stride pushdown), pixel (n, h, w) of the yH x yW grid
   // is stored only for h, w % ysub == 0, compactly at n*(yH/ysub)*(yW/ysub) + ...
   int ysub, yH, yW;
+  long long* stamps;  // diagnostics only (null in the engine): chained kernel, per workgroup 40 x s_memtime
 } DmlExpandReduceArgs;
 
 // Whole ResNet50 identity bottleneck block (csrc/kernels/block_fused.hip), C = 4F:
@@ -175,6 +176,10 @@ int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s);
 int dml_stem_inception(const DmlIncStemArgs* a, hipStream_t s);
 int dml_conv3x3_pool(const DmlConvPoolArgs* a, hipStream_t s);
 int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s);
+// chained-GEMM block boundary, F = 128 / C = 512 (expand_reduce_chain.hip); dml_expand_reduce routes to it
+int dml_chain(const DmlExpandReduceArgs* a, hipStream_t s);
+int dml_chain_supported(const DmlExpandReduceArgs* a);
+int dml_chain_init(void);
 int dml_expand_reduce_init(void);
 int dml_block_fused(const DmlBlockArgs* a, hipStream_t s);
 int dml_block_fused_init(void);

@@ -35,6 +35,8 @@
 //  3. reduce: the wave's 16 output channels for the BM pixels from the LDS Y
 //     tile (K = C), W1 fragments in VGPRs in chunks of 8 k-steps (the first
 //     chunk loaded during the epilogue), bias + ReLU -> 8-B stores.
+#include <cstdlib>
+
 #include "common.h"
 #include "dml.h"
 
@@ -215,7 +217,7 @@ int set_attr() {
 extern "C" int dml_expand_reduce_init(void) {
   using namespace dml::bneck;
   const int rc = set_attr<256, 64, 2>() | set_attr<512, 32, 2>() | set_attr<1024, 32, 1>() |
-                 set_attr<256, 64, 2, 128, false>();
+                 set_attr<256, 64, 2, 128, false>() | dml_chain_init();
   if (rc) dml_set_error("dml_expand_reduce_init: hipFuncSetAttribute failed");
   return rc ? -1 : 0;
 }
@@ -235,6 +237,10 @@ extern "C" int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s) {
     return -1;
   }
   using namespace dml::bneck;
+  // C = 512 with a shortcut: the chained-GEMM kernel (expand_reduce_chain.hip); DML_CHAIN=0
+  // keeps the phase-serialised r1 kernel below (A/B)
+  static const bool chain = [] { const char* e = getenv("DML_CHAIN"); return !(e && e[0] == '0'); }();
+  if (chain && dml_chain_supported(a)) return dml_chain(a, s);
   if (merged) return launch<256, 64, 2, 128, false>(a, s);
   if (C == 256) return launch<256, 64, 2>(a, s);
   if (C == 512) return launch<512, 32, 2>(a, s);

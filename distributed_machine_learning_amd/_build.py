@@ -31,6 +31,7 @@ SOURCES = [
     CSRC / "kernels" / "bottleneck_fused.hip",
     CSRC / "kernels" / "block_fused.hip",
     CSRC / "kernels" / "conv_shift.hip",
+    CSRC / "kernels" / "expand_reduce_chain.hip",
     CSRC / "runtime" / "runtime.hip",
 ]
 HEADERS = [CSRC / "include" / "dml.h"] + sorted((CSRC / "kernels").glob("*.h"))  # every header the stamp covers

@@ -91,7 +91,7 @@ class ExpandReduceArgs(C.Structure):
         ("w1", C.c_void_p), ("b1", C.c_void_p), ("z", C.c_void_p),
         ("M", C.c_int), ("ldx", C.c_int), ("ldw3", C.c_int), ("ldr", C.c_int), ("ldy", C.c_int),
         ("ldw1", C.c_int), ("ldz", C.c_int), ("C", C.c_int), ("kx", C.c_int),
-        ("ysub", C.c_int), ("yH", C.c_int), ("yW", C.c_int),
+        ("ysub", C.c_int), ("yH", C.c_int), ("yW", C.c_int), ("stamps", C.c_void_p),
     ]
 
 
@@ -109,6 +109,7 @@ _SIGS = {
     "dml_block_fused": (C.c_int, [C.POINTER(BlockArgs), C.c_void_p]),
     "dml_plan_add_block": (C.c_int, [C.c_void_p, C.POINTER(BlockArgs)]),
     "dml_expand_reduce": (C.c_int, [C.POINTER(ExpandReduceArgs), C.c_void_p]),
+    "dml_chain_supported": (C.c_int, [C.POINTER(ExpandReduceArgs)]),
     "dml_plan_add_expand_reduce": (C.c_int, [C.c_void_p, C.POINTER(ExpandReduceArgs)]),
     "dml_conv3x3_pool": (C.c_int, [C.POINTER(ConvPoolArgs), C.c_void_p]),
     "dml_plan_add_conv_pool": (C.c_int, [C.c_void_p, C.POINTER(ConvPoolArgs)]),

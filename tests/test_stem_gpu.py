@@ -251,3 +251,56 @@ def test_expand_reduce_subsampled_y():
     assert _rel(y[:q].float().cpu(), want) < 1e-2
     assert (y[q:].float() == -7.0).all()  # nothing stored past the compact tensor
     assert _rel(z.float().cpu(), z_ref) < 1e-2
+
+
+@pytest.mark.parametrize("c,m", [(512, 256), (512, 300), (512, 2 * 28 * 28), (512, 7 * 28 * 28 + 13),
+                                 (1024, 64), (1024, 77), (1024, 3 * 14 * 14 + 5)])
+def test_expand_reduce_chain(c, m):
+    """C = 512 / 1024 go to the chained-GEMM kernel (expand_reduce_chain.hip): Y written
+    once, Z from Y in registers; workgroup tails and several workgroups."""
+    torch.manual_seed(6)
+    f = c // 4
+    x = _bf(torch.randn(m, f).clamp(min=0))
+    res = _bf(torch.randn(m, c))
+    w3 = _bf(torch.randn(c, f) * (2.0 / f) ** 0.5)
+    b3 = torch.randn(c) * 0.1
+    w1 = _bf(torch.randn(f, c) * (2.0 / c) ** 0.5)
+    b1 = torch.randn(f) * 0.1
+    y_ref = _bf(F.relu(x @ w3.T + b3 + res))
+    z_ref = F.relu(y_ref @ w1.T + b1)
+    y, z = ops.expand_reduce(x.to(torch.bfloat16).cuda(), w3.to(torch.bfloat16).cuda(), b3.cuda(),
+                             res.to(torch.bfloat16).cuda(), w1.to(torch.bfloat16).cuda(), b1.cuda())
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu(), y_ref) < 1e-2
+    assert _rel(z.float().cpu(), z_ref) < 1e-2
+
+
+@pytest.mark.parametrize("c", [512, 1024])
+def test_expand_reduce_chain_subsampled_y(c):
+    torch.manual_seed(7)
+    n, h, w = 3, 14, 10
+    f = c // 4
+    m = n * h * w
+    x = _bf(torch.randn(m, f).clamp(min=0))
+    res = _bf(torch.randn(m, c))
+    w3 = _bf(torch.randn(c, f) * (2.0 / f) ** 0.5)
+    b3 = torch.randn(c) * 0.1
+    w1 = _bf(torch.randn(f, c) * (2.0 / c) ** 0.5)
+    b1 = torch.randn(f) * 0.1
+    y_ref = _bf(F.relu(x @ w3.T + b3 + res))
+    z_ref = F.relu(y_ref @ w1.T + b1)
+    xd, rd = x.to(torch.bfloat16).cuda(), res.to(torch.bfloat16).cuda()
+    y = torch.full((m, c), -7.0, device="cuda", dtype=torch.bfloat16)
+    z = torch.empty((m, f), device="cuda", dtype=torch.bfloat16)
+    w3d, w1d = w3.to(torch.bfloat16).cuda(), w1.to(torch.bfloat16).cuda()
+    b3d, b1d = b3.cuda(), b1.cuda()
+    a = N.ExpandReduceArgs(xd.data_ptr(), w3d.data_ptr(), b3d.data_ptr(), rd.data_ptr(), y.data_ptr(), w1d.data_ptr(),
+                           b1d.data_ptr(), z.data_ptr(), m, f, f, c, c, c, f, c, f, 2, h, w)
+    assert N.lib().dml_chain_supported(C.byref(a)) == 1
+    N.check(N.lib().dml_expand_reduce(C.byref(a), N.stream_ptr()), "expand_reduce chain ysub")
+    torch.cuda.synchronize()
+    q = n * (h // 2) * (w // 2)
+    want = y_ref.view(n, h, w, c)[:, ::2, ::2].reshape(q, c)
+    assert _rel(y[:q].float().cpu(), want) < 1e-2
+    assert (y[q:].float() == -7.0).all()
+    assert _rel(z.float().cpu(), z_ref) < 1e-2
