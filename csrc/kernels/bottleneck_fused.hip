@@ -237,9 +237,9 @@ extern "C" int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s) {
     return -1;
   }
   using namespace dml::bneck;
-  // C = 512 with a shortcut: the chained-GEMM kernel (expand_reduce_chain.hip); DML_CHAIN=0
-  // keeps the phase-serialised r1 kernel below (A/B)
-  static const bool chain = [] { const char* e = getenv("DML_CHAIN"); return !(e && e[0] == '0'); }();
+  // C = 512 / 1024 with a shortcut: the chained-GEMM kernel (expand_reduce_chain.hip);
+  // DML_ER_R1=1 keeps the phase-serialised r1 kernels below (A/B)
+  static const bool chain = [] { const char* e = getenv("DML_ER_R1"); return !(e && e[0] == '1'); }();
   if (chain && dml_chain_supported(a)) return dml_chain(a, s);
   if (merged) return launch<256, 64, 2, 128, false>(a, s);
   if (C == 256) return launch<256, 64, 2>(a, s);

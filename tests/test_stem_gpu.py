@@ -161,9 +161,11 @@ def test_expand_reduce_matches_fp32(c, m):
     assert _rel(z.float().cpu(), z_ref) < 1e-2
 
 
-@pytest.mark.parametrize("maxc,pairs", [(256, 2), (1024, 8)])
-def test_engine_fused_blocks_equal_unfused(maxc, pairs, monkeypatch):
+@pytest.mark.parametrize("maxc,chain,pairs", [(256, "0", 2), (256, "1", 4), (256, "2", 8), (1024, "0", 8)])
+def test_engine_fused_blocks_equal_unfused(maxc, chain, pairs, monkeypatch):
+    """DML_CHAIN=1 (default) adds stage 3's boundaries (C = 512, chained kernel), 2 also stage 4's."""
     monkeypatch.setenv("DML_FUSED_BLOCKS_MAXC", str(maxc))
+    monkeypatch.setenv("DML_CHAIN", chain)
     monkeypatch.setenv("DML_FUSED_MERGED_BLOCK", "1")  # opt-in merged-shortcut form, covered here
     g, w = build_model("ResNet50", seed=8, calibrate=True)
     imgs = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda")
