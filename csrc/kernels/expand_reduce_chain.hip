@@ -43,8 +43,6 @@ using convk::lds_void;
 using convk::wait_vmcnt;
 
 constexpr int CC = 64;                                     // Y channels per chunk
-constexpr int NS = 5;                                      // weight panel ring slots
-constexpr int SLOT = 64 * 128;                             // panel: 64 rows x 64 k bf16
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // F: reduce width (C = 4F); NW waves per workgroup; FJ 16-pixel fragments per wave.
@@ -52,18 +50,26 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 //  workgroups per CU (one's epilogue VALU work overlaps the other's MFMAs);
 //  <256, 4, 1>: stage 4 (C = 1024) - T (256 k) and the Z accumulators (256 channels)
 //  of 16 pixels per wave fit in VGPRs.
-template <int F_, int NW_, int FJ_>
+//  BIG: one barrier per GEMM1 / GEMM2 of a chunk (panels of 16 KiB: W3 64 rows x F k, W1 F rows
+//  x 64 k; a 3-slot ring) instead of one per 64-deep k slice (8 KiB panels, 5 slots); the bias
+//  is read from global memory so <128, 4, 2, BIG> fits 80 KiB: two workgroups per CU.
+template <int F_, int NW_, int FJ_, bool BIG_ = false>
 struct Cfg {
   static constexpr int F = F_, NW = NW_, FJ = FJ_, NT = NW * 64, PXW = 16 * FJ, BM = NW * PXW;
+  static constexpr bool BIG = BIG_;
+  static constexpr int NS = BIG ? 3 : 5;               // weight panel ring slots
+  static constexpr int SLOT = BIG ? 16384 : 8192;      // panel bytes
+  static constexpr int KW3 = BIG ? F : 64;             // k columns of a W3 panel (64 rows)
+  static constexpr int RW1 = BIG ? F : 64;             // rows of a W1 panel (64 k columns)
   static constexpr int C_MAX = 4 * F;
   static constexpr int KS1 = F / 32;       // T fragments (k32 steps of GEMM1)
   static constexpr int FI1 = CC / 16;      // GEMM1 channel fragments
   static constexpr int KS2 = CC / 32;      // Y fragments per chunk (k32 steps of GEMM2)
   static constexpr int FI2 = F / 16;       // GEMM2 output-channel fragments
-  static constexpr int P1 = F / 64;        // W3 panels per chunk (CC = 64 rows x 64 k)
-  static constexpr int P2 = F / 64;        // W1 panels per chunk (64 output rows x 64 k each)
+  static constexpr int P1 = F / KW3;       // W3 panels per chunk
+  static constexpr int P2 = F / RW1;       // W1 panels per chunk
   static constexpr int PPC = P1 + P2;
-  static constexpr int PI = 64 / 8 / NW;   // DMA instructions per wave per panel
+  static constexpr int PI = SLOT / 1024 / NW;  // DMA instructions per wave per panel
   static constexpr int TROW = F * 2;       // T / Z row bytes in the wave buffer
   static constexpr int TPR = 1024 / TROW;  // T rows per 1-KiB DMA piece
   static constexpr int TPC = PXW / TPR;    // T DMA pieces per wave
@@ -71,9 +77,9 @@ struct Cfg {
   static constexpr int HPC = PXW / 8;      // R DMA pieces per wave (8 rows of 128 B each)
   static constexpr int WBUF = PXW * TROW > 2 * HALF ? PXW * TROW : 2 * HALF;  // per-wave buffer
   static constexpr int WBUF0 = NS * SLOT;
-  static constexpr int BIAS = WBUF0 + NW * WBUF;  // b3 [C] then b1 [F], fp32
-  static constexpr int STAMPS = BIAS + (C_MAX + F) * 4;  // diagnostics: 40 x 8 B
-  static constexpr int LDS = STAMPS + 40 * 8;
+  static constexpr int BIAS = WBUF0 + NW * WBUF;  // b3 [C] then b1 [F], fp32 (not BIG)
+  static constexpr int STAMPS = BIAS + (BIG ? 0 : (C_MAX + F) * 4);  // diagnostics: 40 x 8 B (not BIG)
+  static constexpr int LDS = STAMPS + (BIG ? 0 : 40 * 8);
   static_assert(PI >= 1 && CC == 64 && F % 64 == 0 && TPC >= 1 && HPC >= 1, "DMA split");
   static_assert(LDS <= 163840, "LDS");
 };
@@ -106,10 +112,10 @@ __device__ __forceinline__ uint2 relu_pack4(float f0, float f1, float f2, float 
 template <int ROWB>
 __device__ __forceinline__ int wswz(int row, int ch) { return row * ROWB + ((ch ^ (row & 15)) << 4); }
 
-template <int F, int NW, int FJ>
+template <int F, int NW, int FJ, bool BIG>
 __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a) {
-  using T = Cfg<F, NW, FJ>;
-  constexpr int NT = T::NT, BM = T::BM, PXW = T::PXW, HALF = T::HALF;
+  using T = Cfg<F, NW, FJ, BIG>;
+  constexpr int NT = T::NT, BM = T::BM, PXW = T::PXW, HALF = T::HALF, NS = T::NS, SLOT = T::SLOT;
   using RW = convk::Rows<64>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -123,16 +129,20 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
   float* b3s = (float*)(smem + T::BIAS);
   float* b1s = b3s + C;
 
-  // diagnostics (a.stamps != null): wave 0 records s_memtime at phase boundaries into LDS,
-  // written out at the end to a buffer nothing else reads
+  // diagnostics (a.stamps != null): wave 0 records s_memtime at phase boundaries into LDS
+  // (BIG: straight to the stamp buffer), written to a buffer nothing else reads
   long long* stl = (long long*)(smem + T::STAMPS);
   const bool stamping = a.stamps != nullptr;
   auto stamp = [&](int i) {
-    if (stamping && tid == 0) stl[i] = __builtin_amdgcn_s_memtime();
+    if (stamping && tid == 0) {
+      if constexpr (BIG) a.stamps[(long)blockIdx.x * 40 + i] = __builtin_amdgcn_s_memtime();
+      else stl[i] = __builtin_amdgcn_s_memtime();
+    }
   };
   stamp(0);
   // biases -> LDS (read in the MFMA layout by every wave; visible after the loop's first barrier)
-  for (int i = tid; i < C + F; i += NT) b3s[i] = i < C ? a.b3[i] : a.b1[i - C];
+  if constexpr (!BIG)
+    for (int i = tid; i < C + F; i += NT) b3s[i] = i < C ? a.b3[i] : a.b1[i - C];
 
   int issued = 0;  // VMEM ops this wave issued since here (LDS-DMA, buffer stores)
   const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, 0x7ffffff0, 0x00020000);
@@ -169,25 +179,23 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
 
   // weight panels (64 rows x 64 k): q -> (chunk c, part); part < P1: W3 rows [c*64, +64) x
   // k [64 part, +64); else W1 rows [64 (part - P1), +64) x k [c*64, +64)
-  int mk0 = 0, mk1 = 0, mk2 = 0, mk3 = 0;  // issue marks of the pending panels q .. q+3, oldest first
-  static_assert(NS == 5, "mark FIFO depth");
+  int mk0 = 0, mk1 = 0, mk2 = 0, mk3 = 0;  // issue marks of the pending panels q .. q+NS-2, oldest first
+  static_assert(NS == 5 || NS == 3, "mark FIFO depth");
   auto issue_panel = [&](int q) {
     const int c = q / T::PPC, part = q - c * T::PPC;
     char* dst = smem + (q % NS) * SLOT;
-    const char* src;
-    long ld;
-    if (part < T::P1) {
-      src = (const char*)a.w3 + ((long)(c * CC) * a.ldw3 + part * 64 + lchunk * 8) * 2;
-      ld = a.ldw3;
-    } else {
-      src = (const char*)a.w1 + ((long)((part - T::P1) * 64) * a.ldw1 + c * CC + lchunk * 8) * 2;
-      ld = a.ldw1;
-    }
 #pragma unroll
     for (int j = 0; j < T::PI; ++j) {
-      const int pc = wid * T::PI + j;
-      __builtin_amdgcn_global_load_lds((const void*)(src + (long)(pc * 8 + lrow) * ld * 2), (lds_void*)(dst + pc * 1024),
-                                       16, 0, 0);
+      const int pc = wid * T::PI + j;  // 1-KiB piece = 8 rows of one 64-k sub-panel
+      const char* src;
+      if (part < T::P1) {  // W3 rows [c*64, +64), k [part*KW3 + 64 sp, +64)
+        const int sp = pc / 8, r = (pc % 8) * 8 + lrow;
+        src = (const char*)a.w3 + ((long)(c * CC + r) * a.ldw3 + part * T::KW3 + sp * 64 + lchunk * 8) * 2;
+      } else {             // W1 rows [(part - P1) * RW1, +RW1), k [c*64, +64)
+        const int r = (part - T::P1) * T::RW1 + pc * 8 + lrow;
+        src = (const char*)a.w1 + ((long)r * a.ldw1 + c * CC + lchunk * 8) * 2;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + pc * 1024), 16, 0, 0);
     }
     issued += T::PI;
   };
@@ -197,10 +205,12 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
   mk0 = issued;
   issue_panel(1);
   mk1 = issued;
-  issue_panel(2);
-  mk2 = issued;
-  issue_panel(3);
-  mk3 = issued;
+  if constexpr (NS == 5) {
+    issue_panel(2);
+    mk2 = issued;
+    issue_panel(3);
+    mk3 = issued;
+  }
 
   // T -> B-operand fragments (lane: pixel 16j + frow, k 32ks + 8fq .. +7)
   wait_vm(issued - mark_t);
@@ -238,26 +248,32 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
   for (int part = 0; part < T::PPC; ++part) {  // compile-time part: register arrays stay statically indexed
     const int q = c * T::PPC + part;
     wait_vm(issued - mk0);
-    mk0 = mk1, mk1 = mk2, mk2 = mk3;
+    if constexpr (NS == 5) mk0 = mk1, mk1 = mk2, mk2 = mk3;
+    else mk0 = mk1;
     __builtin_amdgcn_s_barrier();  // every wave's pieces of panel q landed; slot (q-1) % NS is free
     if (q + NS - 1 < nq) {
       issue_panel(q + NS - 1);
-      mk3 = issued;
+      if constexpr (NS == 5) mk3 = issued;
+      else mk1 = issued;
     }
     const char* pan = smem + (q % NS) * SLOT;
     if (part < T::P1) {
-      // ---- GEMM1: acc1[ch][px] += W3 panel (64 ch x 64 k) . T (k 64 part ..) ----
+      // ---- GEMM1: acc1[ch][px] += W3 panel (64 ch x KW3 k, as 64-k sub-panels) . T ----
+#pragma unroll
+      for (int sp = 0; sp < T::KW3 / 64; ++sp)
 #pragma unroll
       for (int kl = 0; kl < 2; ++kl) {
         bf16x8 fa[T::FI1];
 #pragma unroll
-        for (int i = 0; i < T::FI1; ++i) fa[i] = *(const bf16x8*)(pan + lds_swz(16 * i + frow, 4 * kl + fq));
+        for (int i = 0; i < T::FI1; ++i)
+          fa[i] = *(const bf16x8*)(pan + sp * 8192 + lds_swz(16 * i + frow, 4 * kl + fq));
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < T::FI1; ++i)
 #pragma unroll
           for (int j = 0; j < FJ; ++j)
-            acc1[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], tf[2 * part + kl][j], acc1[i][j], 0, 0, 0);
+            acc1[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fa[i], tf[(part * (T::KW3 / 64) + sp) * 2 + kl][j], acc1[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
       if (part == T::P1 - 1) {
@@ -269,8 +285,9 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
         if (c < 8) stamp(3 + 4 * c);
 #pragma unroll
         for (int i = 0; i < T::FI1; ++i) {
-          // the next chunk's bias (an LDS read; the accumulators restart from it)
-          const float4 nb = *(const float4*)(b3s + (c + 1 < nch ? c + 1 : c) * CC + 16 * i + 4 * fq);
+          // the next chunk's bias (the accumulators restart from it): LDS, or global memory (BIG)
+          const float* bsrc = BIG ? a.b3 : b3s;
+          const float4 nb = *(const float4*)(bsrc + (c + 1 < nch ? c + 1 : c) * CC + 16 * i + 4 * fq);
 #pragma unroll
           for (int j = 0; j < FJ; ++j) {
             const int off = lds_swz(16 * j + frow, 2 * i + (fq >> 1)) + 8 * (fq & 1);
@@ -313,19 +330,22 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
         if (c < 8) stamp(4 + 4 * c);
       }
     } else {
-      // ---- GEMM2: acc2[f][px] += W1 panel (64 output rows 64h .. x 64 k) . Y chunk c ----
-      const int h = part - T::P1;  // compile-time after the unroll
+      // ---- GEMM2: acc2[f][px] += W1 panel (RW1 output rows from (part-P1)*RW1, 64 k) . Y chunk c ----
+      const int fb0 = (part - T::P1) * (T::RW1 / 16);  // compile-time after the unroll
 #pragma unroll
-      for (int kl = 0; kl < 2; ++kl) {
+      for (int kl = 0; kl < 2; ++kl)
+#pragma unroll
+      for (int g = 0; g < T::RW1 / 64; ++g) {  // 4 output-channel fragments at a time (VGPRs)
         bf16x8 fa[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = *(const bf16x8*)(pan + lds_swz(16 * i + frow, 4 * kl + fq));
+        for (int i = 0; i < 4; ++i) fa[i] = *(const bf16x8*)(pan + lds_swz(16 * (4 * g + i) + frow, 4 * kl + fq));
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < FJ; ++j)
-            acc2[4 * h + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], yb[kl][j], acc2[4 * h + i][j], 0, 0, 0);
+            acc2[fb0 + 4 * g + i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], yb[kl][j], acc2[fb0 + 4 * g + i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
       if (c < 8 && part == T::PPC - 1) stamp(5 + 4 * c);
@@ -354,7 +374,7 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
     if (m < a.M) *(uint4*)((unsigned short*)a.z + (long)m * a.ldz + ch * 8) = v;
   }
   stamp(34);
-  if (stamping && tid < 40) {
+  if (!BIG && stamping && tid < 40) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     a.stamps[(long)blockIdx.x * 40 + tid] = stl[tid];
   }
@@ -363,22 +383,24 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
 }  // namespace chain
 }  // namespace dml
 
-template <int F, int NW, int FJ>
+template <int F, int NW, int FJ, bool BIG = false>
 static int chain_attr() {
-  using T = dml::chain::Cfg<F, NW, FJ>;
-  return (int)hipFuncSetAttribute((const void*)dml::chain::chain_kernel<F, NW, FJ>,
+  using T = dml::chain::Cfg<F, NW, FJ, BIG>;
+  return (int)hipFuncSetAttribute((const void*)dml::chain::chain_kernel<F, NW, FJ, BIG>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
-template <int F, int NW, int FJ>
+template <int F, int NW, int FJ, bool BIG = false>
 static void chain_launch(const DmlExpandReduceArgs* a, hipStream_t s) {
-  using T = dml::chain::Cfg<F, NW, FJ>;
+  using T = dml::chain::Cfg<F, NW, FJ, BIG>;
   const long blocks = ((long)a->M + T::BM - 1) / T::BM;
-  hipLaunchKernelGGL((dml::chain::chain_kernel<F, NW, FJ>), dim3((unsigned)blocks), dim3(T::NT), T::LDS, s, *a);
+  hipLaunchKernelGGL((dml::chain::chain_kernel<F, NW, FJ, BIG>), dim3((unsigned)blocks), dim3(T::NT), T::LDS, s,
+                     *a);
 }
 
 extern "C" int dml_chain_init(void) {
-  const int rc = chain_attr<128, 8, 2>() | chain_attr<128, 4, 2>() | chain_attr<256, 4, 1>() | chain_attr<256, 8, 1>();
+  const int rc = chain_attr<128, 8, 2>() | chain_attr<128, 4, 2>() | chain_attr<128, 4, 2, true>() |
+                 chain_attr<256, 4, 1>() | chain_attr<256, 8, 1>();
   if (rc) dml_set_error("dml_chain_init: hipFuncSetAttribute failed");
   return rc ? -1 : 0;
 }
@@ -402,8 +424,10 @@ extern "C" int dml_chain(const DmlExpandReduceArgs* a, hipStream_t s) {
     return -1;
   }
   static const int nw = [] { const char* e = getenv("DML_CHAIN_WAVES"); return e && atoi(e) == 8 ? 8 : 4; }();
+  static const bool big = [] { const char* e = getenv("DML_CHAIN_BIG"); return e && e[0] == '1'; }();
   if (a->C == 512) {
     if (nw == 8) chain_launch<128, 8, 2>(a, s);
+    else if (big) chain_launch<128, 4, 2, true>(a, s);
     else chain_launch<128, 4, 2>(a, s);
   } else {
     if (nw == 8) chain_launch<256, 8, 1>(a, s);
