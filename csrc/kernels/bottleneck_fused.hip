@@ -223,6 +223,11 @@ extern "C" int dml_expand_reduce_init(void) {
 }
 
 extern "C" int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s) {
+  // the chained-GEMM kernel (expand_reduce_chain.hip) where it serves the shape (C = 512 / 1024
+  // with a shortcut, merged C = 256 / 512); DML_ER_R1=1 keeps the phase-serialised r1 kernels
+  // below (A/B)
+  static const bool chain = [] { const char* e = getenv("DML_ER_R1"); return !(e && e[0] == '1'); }();
+  if (chain && dml_chain_supported(a)) return dml_chain(a, s);
   // expand KX -> C channels (+ shortcut), reduce C -> F, F = C / 4, C in {256, 512, 1024};
   // KX = F with a shortcut, or KX = 2F without one (merged projection shortcut, C = 256)
   const int C = a->C, F = C / 4;
@@ -237,10 +242,6 @@ extern "C" int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s) {
     return -1;
   }
   using namespace dml::bneck;
-  // C = 512 / 1024 with a shortcut: the chained-GEMM kernel (expand_reduce_chain.hip);
-  // DML_ER_R1=1 keeps the phase-serialised r1 kernels below (A/B)
-  static const bool chain = [] { const char* e = getenv("DML_ER_R1"); return !(e && e[0] == '1'); }();
-  if (chain && dml_chain_supported(a)) return dml_chain(a, s);
   if (merged) return launch<256, 64, 2, 128, false>(a, s);
   if (C == 256) return launch<256, 64, 2>(a, s);
   if (C == 512) return launch<512, 32, 2>(a, s);

@@ -53,29 +53,34 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 //  BIG: one barrier per GEMM1 / GEMM2 of a chunk (panels of 16 KiB: W3 64 rows x F k, W1 F rows
 //  x 64 k; a 3-slot ring) instead of one per 64-deep k slice (8 KiB panels, 5 slots); the bias
 //  is read from global memory so <128, 4, 2, BIG> fits 80 KiB: two workgroups per CU.
-template <int F_, int NW_, int FJ_, bool BIG_ = false>
+//  KX: expand input width (F, or 2F for a stage's first block after the projection-shortcut
+//  merge: T = [x ; s], no residual); RES: the expand adds the shortcut R.
+template <int F_, int NW_, int FJ_, bool BIG_ = false, int KX_ = F_, bool RES_ = true>
 struct Cfg {
   static constexpr int F = F_, NW = NW_, FJ = FJ_, NT = NW * 64, PXW = 16 * FJ, BM = NW * PXW;
-  static constexpr bool BIG = BIG_;
+  static constexpr int KX = KX_;
+  static constexpr bool BIG = BIG_, RES = RES_;
   static constexpr int NS = BIG ? 3 : 5;               // weight panel ring slots
   static constexpr int SLOT = BIG ? 16384 : 8192;      // panel bytes
-  static constexpr int KW3 = BIG ? F : 64;             // k columns of a W3 panel (64 rows)
+  static constexpr int KW3 = BIG ? KX : 64;            // k columns of a W3 panel (64 rows)
   static constexpr int RW1 = BIG ? F : 64;             // rows of a W1 panel (64 k columns)
   static constexpr int C_MAX = 4 * F;
-  static constexpr int KS1 = F / 32;       // T fragments (k32 steps of GEMM1)
+  static constexpr int KS1 = KX / 32;      // T fragments (k32 steps of GEMM1)
   static constexpr int FI1 = CC / 16;      // GEMM1 channel fragments
   static constexpr int KS2 = CC / 32;      // Y fragments per chunk (k32 steps of GEMM2)
   static constexpr int FI2 = F / 16;       // GEMM2 output-channel fragments
-  static constexpr int P1 = F / KW3;       // W3 panels per chunk
+  static constexpr int P1 = KX / KW3;      // W3 panels per chunk
   static constexpr int P2 = F / RW1;       // W1 panels per chunk
   static constexpr int PPC = P1 + P2;
   static constexpr int PI = SLOT / 1024 / NW;  // DMA instructions per wave per panel
-  static constexpr int TROW = F * 2;       // T / Z row bytes in the wave buffer
+  static constexpr int TROW = KX * 2;      // T row bytes in the wave buffer
+  static constexpr int ZROW = F * 2;       // Z row bytes (the Z epilogue reuses the wave buffer)
   static constexpr int TPR = 1024 / TROW;  // T rows per 1-KiB DMA piece
   static constexpr int TPC = PXW / TPR;    // T DMA pieces per wave
   static constexpr int HALF = PXW * 128;   // R / Y half: [PXW px][64 ch] bf16
   static constexpr int HPC = PXW / 8;      // R DMA pieces per wave (8 rows of 128 B each)
-  static constexpr int WBUF = PXW * TROW > 2 * HALF ? PXW * TROW : 2 * HALF;  // per-wave buffer
+  static constexpr int WB1 = PXW * TROW > 2 * HALF ? PXW * TROW : 2 * HALF;
+  static constexpr int WBUF = WB1 > PXW * ZROW ? WB1 : PXW * ZROW;  // per-wave buffer
   static constexpr int WBUF0 = NS * SLOT;
   static constexpr int BIAS = WBUF0 + NW * WBUF;  // b3 [C] then b1 [F], fp32 (not BIG)
   static constexpr int STAMPS = BIAS + (BIG ? 0 : (C_MAX + F) * 4);  // diagnostics: 40 x 8 B (not BIG)
@@ -107,14 +112,17 @@ __device__ __forceinline__ uint2 relu_pack4(float f0, float f1, float f2, float 
   return make_uint2(__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi));
 }
 
-// T / Z rows of ROWB bytes (256 or 512): 16-B chunk ^= row & 15 (16 consecutive rows of one
-// logical chunk hit 16 distinct 4-bank groups)
+// T / Z rows of ROWB bytes: 16-B chunk ^= row & 15 (256- and 512-B rows: 16 consecutive rows of
+// one logical chunk hit 16 distinct 4-bank groups) or ^= row & 7 (128-B rows, = lds_swz)
 template <int ROWB>
-__device__ __forceinline__ int wswz(int row, int ch) { return row * ROWB + ((ch ^ (row & 15)) << 4); }
+__device__ __forceinline__ int wswz(int row, int ch) {
+  constexpr int K = ROWB / 16 >= 16 ? 15 : ROWB / 16 - 1;
+  return row * ROWB + ((ch ^ (row & K)) << 4);
+}
 
-template <int F, int NW, int FJ, bool BIG>
+template <int F, int NW, int FJ, bool BIG, int KX, bool RES>
 __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a) {
-  using T = Cfg<F, NW, FJ, BIG>;
+  using T = Cfg<F, NW, FJ, BIG, KX, RES>;
   constexpr int NT = T::NT, BM = T::BM, PXW = T::PXW, HALF = T::HALF, NS = T::NS, SLOT = T::SLOT;
   using RW = convk::Rows<64>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -158,7 +166,8 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
 #pragma unroll
     for (int p = 0; p < T::TPC; ++p) {
       const int row = p * T::TPR + prow, m = mw + row;
-      const unsigned off = m < a.M ? (unsigned)(((long)m * a.ldx + (pch ^ (row & 15)) * 8) * 2) : OOB;
+      constexpr int K = CPRW >= 16 ? 15 : CPRW - 1;
+      const unsigned off = m < a.M ? (unsigned)(((long)m * a.ldx + (pch ^ (row & K)) * 8) * 2) : OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void*)(wb + p * 1024), 16, off, 0, 0, 0);
     }
     issued += T::TPC;
@@ -221,11 +230,13 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
     for (int j = 0; j < FJ; ++j) tf[ks][j] = *(const bf16x8*)(wb + wswz<T::TROW>(16 * j + frow, 4 * ks + fq));
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // T read out before R[0], R[1] land on it
   stamp(1);
-  dma_res(0);
-  mark_r0 = issued;
-  if (nch > 1) {
-    dma_res(1);
-    mark_r1 = issued;
+  if constexpr (RES) {
+    dma_res(0);
+    mark_r0 = issued;
+    if (nch > 1) {
+      dma_res(1);
+      mark_r1 = issued;
+    }
   }
 
   f32x4 acc1[T::FI1][FJ], acc2[T::FI2][FJ];
@@ -277,11 +288,13 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
         __builtin_amdgcn_s_setprio(0);
       }
       if (part == T::P1 - 1) {
-        // ---- epilogue of chunk c (this wave only): Y = relu(acc1 + b3 + R[c]) in place ----
+        // ---- epilogue of chunk c (this wave only): Y = relu(acc1 + b3 (+ R[c])) in place ----
         char* hb = wb + (c & 1) * HALF;
         if (c < 8) stamp(2 + 4 * c);
-        wait_vm(issued - mark_r0);
-        mark_r0 = mark_r1;
+        if constexpr (RES) {
+          wait_vm(issued - mark_r0);
+          mark_r0 = mark_r1;
+        }
         if (c < 8) stamp(3 + 4 * c);
 #pragma unroll
         for (int i = 0; i < T::FI1; ++i) {
@@ -291,10 +304,15 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
 #pragma unroll
           for (int j = 0; j < FJ; ++j) {
             const int off = lds_swz(16 * j + frow, 2 * i + (fq >> 1)) + 8 * (fq & 1);
-            const uint2 r = *(const uint2*)(hb + off);
             const f32x4 v = acc1[i][j];
-            *(uint2*)(hb + off) = relu_pack4(v[0] + __uint_as_float(r.x << 16), v[1] + __uint_as_float(r.x & 0xffff0000u),
-                                             v[2] + __uint_as_float(r.y << 16), v[3] + __uint_as_float(r.y & 0xffff0000u));
+            if constexpr (RES) {
+              const uint2 r = *(const uint2*)(hb + off);
+              *(uint2*)(hb + off) =
+                  relu_pack4(v[0] + __uint_as_float(r.x << 16), v[1] + __uint_as_float(r.x & 0xffff0000u),
+                             v[2] + __uint_as_float(r.y << 16), v[3] + __uint_as_float(r.y & 0xffff0000u));
+            } else {
+              *(uint2*)(hb + off) = relu_pack4(v[0], v[1], v[2], v[3]);
+            }
             acc1[i][j] = (f32x4){nb.x, nb.y, nb.z, nb.w};
           }
         }
@@ -323,7 +341,7 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
         }
         issued += PXW / 8;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // half read out before R[c+2] lands on it
-        if (c + 2 < nch) {
+        if (RES && c + 2 < nch) {
           dma_res(c + 2);
           mark_r1 = issued;
         }
@@ -359,18 +377,18 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
   for (int i = 0; i < T::FI2; ++i) {
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
-      const int off = wswz<T::TROW>(16 * j + frow, 2 * i + (fq >> 1)) + 8 * (fq & 1);
+      const int off = wswz<T::ZROW>(16 * j + frow, 2 * i + (fq >> 1)) + 8 * (fq & 1);
       const f32x4 v = acc2[i][j];
       *(uint2*)(wb + off) = relu_pack4(v[0], v[1], v[2], v[3]);
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  constexpr int ZC = T::TROW / 16;  // 16-B chunks per Z row
+  constexpr int ZC = T::ZROW / 16;  // 16-B chunks per Z row
 #pragma unroll
   for (int u = 0; u < PXW * ZC / 64; ++u) {
     const int row = u * (64 / ZC) + lane / ZC, ch = lane % ZC, m = mw + row;
-    const uint4 v = *(const uint4*)(wb + wswz<T::TROW>(row, ch));
+    const uint4 v = *(const uint4*)(wb + wswz<T::ZROW>(row, ch));
     if (m < a.M) *(uint4*)((unsigned short*)a.z + (long)m * a.ldz + ch * 8) = v;
   }
   stamp(34);
@@ -383,49 +401,67 @@ __global__ __launch_bounds__(NW * 64, 2) void chain_kernel(DmlExpandReduceArgs a
 }  // namespace chain
 }  // namespace dml
 
-template <int F, int NW, int FJ, bool BIG = false>
+template <int F, int NW, int FJ, bool BIG = false, int KX = F, bool RES = true>
 static int chain_attr() {
-  using T = dml::chain::Cfg<F, NW, FJ, BIG>;
-  return (int)hipFuncSetAttribute((const void*)dml::chain::chain_kernel<F, NW, FJ, BIG>,
+  using T = dml::chain::Cfg<F, NW, FJ, BIG, KX, RES>;
+  return (int)hipFuncSetAttribute((const void*)dml::chain::chain_kernel<F, NW, FJ, BIG, KX, RES>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
-template <int F, int NW, int FJ, bool BIG = false>
+template <int F, int NW, int FJ, bool BIG = false, int KX = F, bool RES = true>
 static void chain_launch(const DmlExpandReduceArgs* a, hipStream_t s) {
-  using T = dml::chain::Cfg<F, NW, FJ, BIG>;
+  using T = dml::chain::Cfg<F, NW, FJ, BIG, KX, RES>;
   const long blocks = ((long)a->M + T::BM - 1) / T::BM;
-  hipLaunchKernelGGL((dml::chain::chain_kernel<F, NW, FJ, BIG>), dim3((unsigned)blocks), dim3(T::NT), T::LDS, s,
-                     *a);
+  hipLaunchKernelGGL((dml::chain::chain_kernel<F, NW, FJ, BIG, KX, RES>), dim3((unsigned)blocks), dim3(T::NT),
+                     T::LDS, s, *a);
 }
 
 extern "C" int dml_chain_init(void) {
   const int rc = chain_attr<128, 8, 2>() | chain_attr<128, 4, 2>() | chain_attr<128, 4, 2, true>() |
-                 chain_attr<256, 4, 1>() | chain_attr<256, 8, 1>();
+                 chain_attr<256, 4, 1>() | chain_attr<256, 8, 1>() | chain_attr<64, 4, 2>() |
+                 chain_attr<64, 4, 2, false, 128, false>() | chain_attr<128, 4, 2, false, 256, false>();
   if (rc) dml_set_error("dml_chain_init: hipFuncSetAttribute failed");
   return rc ? -1 : 0;
 }
 
-// 1 if the chained kernel serves this block boundary (F = 128 / C = 512 or F = 256 /
-// C = 1024, with a shortcut), else 0; the caller falls back to the phase-serialised kernel
-extern "C" int dml_chain_supported(const DmlExpandReduceArgs* a) {
-  const int C = a->C, F = C / 4;
-  const long ld = a->ldx > a->ldr ? (a->ldx > a->ldy ? a->ldx : a->ldy) : (a->ldr > a->ldy ? a->ldr : a->ldy);
-  return (F == 128 || F == 256) && a->res != nullptr && (a->kx == 0 || a->kx == F) && a->M >= 1 &&
-         a->ldx % 8 == 0 && a->ldx >= F && a->ldw3 % 8 == 0 && a->ldw3 >= F && a->ldr % 8 == 0 && a->ldr >= C &&
-         a->ldy % 8 == 0 && a->ldy >= C && a->ldw1 % 8 == 0 && a->ldw1 >= C && a->ldz % 8 == 0 && a->ldz >= F &&
-         (long)a->M * ld * 2 < 0x7ffffff0L;
+static bool env_on(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '1';
 }
 
-// workgroup shape: F = 128: 4 waves x 32 pixels (DML_CHAIN_WAVES=8: 8 waves, A/B);
-// F = 256: 4 waves x 16 pixels (DML_CHAIN_WAVES=8: 8 waves)
+// 1 if the chained kernel serves this block boundary, else 0 (the caller falls back to the
+// phase-serialised kernels): with a shortcut, F = 128 / C = 512 or F = 256 / C = 1024 (F = 64 /
+// C = 256 with DML_CHAIN_C256=1: the r1 kernel is near the HBM roofline there); merged
+// projection shortcut (T = [x ; s], K = 2F, no residual), F = 64 / C = 256 or F = 128 / C = 512
+extern "C" int dml_chain_supported(const DmlExpandReduceArgs* a) {
+  const int C = a->C, F = C / 4;
+  const bool merged = a->res == nullptr;
+  const int kx = merged ? a->kx : F;
+  const long ld = a->ldx > a->ldr ? (a->ldx > a->ldy ? a->ldx : a->ldy) : (a->ldr > a->ldy ? a->ldr : a->ldy);
+  static const bool c256 = env_on("DML_CHAIN_C256");
+  const bool shape = merged ? ((F == 64 || F == 128) && a->kx == 2 * F)
+                            : ((F == 128 || F == 256 || (F == 64 && c256)) && (a->kx == 0 || a->kx == F));
+  return shape && a->M >= 1 && a->ldx % 8 == 0 && a->ldx >= kx && a->ldw3 % 8 == 0 && a->ldw3 >= kx &&
+         (merged || (a->ldr % 8 == 0 && a->ldr >= C)) && a->ldy % 8 == 0 && a->ldy >= C && a->ldw1 % 8 == 0 &&
+         a->ldw1 >= C && a->ldz % 8 == 0 && a->ldz >= F && (long)a->M * ld * 2 < 0x7ffffff0L;
+}
+
+// workgroup shape: 4 waves (two workgroups per CU) by default; DML_CHAIN_WAVES=8 (8 waves) and
+// DML_CHAIN_BIG=1 (one barrier per GEMM of a chunk) are A/B variants of the C = 512 form
 extern "C" int dml_chain(const DmlExpandReduceArgs* a, hipStream_t s) {
   if (!dml_chain_supported(a)) {
-    dml_set_error("dml_chain: unsupported shape (C = 512 or 1024, shortcut, 8-aligned strides)");
+    dml_set_error("dml_chain: unsupported shape (C = 512 / 1024 with a shortcut, merged C = 256 / 512)");
     return -1;
   }
   static const int nw = [] { const char* e = getenv("DML_CHAIN_WAVES"); return e && atoi(e) == 8 ? 8 : 4; }();
-  static const bool big = [] { const char* e = getenv("DML_CHAIN_BIG"); return e && e[0] == '1'; }();
-  if (a->C == 512) {
+  static const bool big = env_on("DML_CHAIN_BIG");
+  const bool merged = a->res == nullptr;
+  if (merged) {
+    if (a->C == 256) chain_launch<64, 4, 2, false, 128, false>(a, s);
+    else chain_launch<128, 4, 2, false, 256, false>(a, s);
+  } else if (a->C == 256) {
+    chain_launch<64, 4, 2>(a, s);
+  } else if (a->C == 512) {
     if (nw == 8) chain_launch<128, 8, 2>(a, s);
     else if (big) chain_launch<128, 4, 2, true>(a, s);
     else chain_launch<128, 4, 2>(a, s);

@@ -277,13 +277,17 @@ class Engine:
                 continue
             # with its shortcut (K = F), or a merged projection shortcut (K = 2F, no residual; C = 256)
             shortcut = e.residual and e.res_sub == 1 and e.cin * 4 == e.cout
-            merged = (e.residual is None and e.cin * 2 == e.cout == 256
-                      and os.environ.get("DML_FUSED_MERGED_BLOCK", "0") == "1")  # opt-in: measured slower
+            # merged: the r1 kernel (C = 256, DML_FUSED_MERGED_BLOCK=1: measured slower) or the
+            # chained kernel (C = 256 / 512, DML_CHAIN_MERGED=1)
+            chain_m = os.environ.get("DML_CHAIN_MERGED", "0") == "1"
+            merged = (e.residual is None and e.cin * 2 == e.cout
+                      and ((e.cout == 256 and (chain_m or os.environ.get("DML_FUSED_MERGED_BLOCK", "0") == "1"))
+                           or (e.cout == 512 and chain_m)))
             # the chained-GEMM kernel (expand_reduce_chain.hip): the C = 512 boundaries (stage 3) by
             # default (ResNet50 b256 87.8-88.3k vs 85.4-86.1k img/s, profiles/r3_v3); DML_CHAIN=2 also
             # C = 1024 (stage 4: no faster than its two launches), DML_CHAIN=0 none
             ch = os.environ.get("DML_CHAIN", "1")
-            chain = shortcut and ((e.cout == 512 and ch in ("1", "2")) or (e.cout == 1024 and ch == "2"))
+            chain = merged or (shortcut and ((e.cout == 512 and ch in ("1", "2")) or (e.cout == 1024 and ch == "2")))
             if not (e.kh == e.kw == 1 and e.sh == e.sw == 1 and e.cout in (256, 512, 1024) and (e.cout <= maxc or chain)
                     and (shortcut or merged)
                     and e.relu and e.in_coff == 0 and e.out_coff == 0 and not e.out_f32):

@@ -161,11 +161,14 @@ def test_expand_reduce_matches_fp32(c, m):
     assert _rel(z.float().cpu(), z_ref) < 1e-2
 
 
-@pytest.mark.parametrize("maxc,chain,pairs", [(256, "0", 2), (256, "1", 4), (256, "2", 8), (1024, "0", 8)])
-def test_engine_fused_blocks_equal_unfused(maxc, chain, pairs, monkeypatch):
-    """DML_CHAIN=1 (default) adds stage 3's boundaries (C = 512, chained kernel), 2 also stage 4's."""
+@pytest.mark.parametrize("maxc,chain,merged,pairs", [(256, "0", "0", 2), (256, "1", "0", 4), (256, "2", "0", 8),
+                                                     (1024, "0", "0", 8), (256, "1", "1", 5)])
+def test_engine_fused_blocks_equal_unfused(maxc, chain, merged, pairs, monkeypatch):
+    """DML_CHAIN=1 (default) adds stage 3's boundaries (C = 512, chained kernel), 2 also stage 4's;
+    DML_CHAIN_MERGED=1 also stage 3's merged entry (conv3_block1_3 + _0 -> conv3_block2_1)."""
     monkeypatch.setenv("DML_FUSED_BLOCKS_MAXC", str(maxc))
     monkeypatch.setenv("DML_CHAIN", chain)
+    monkeypatch.setenv("DML_CHAIN_MERGED", merged)
     monkeypatch.setenv("DML_FUSED_MERGED_BLOCK", "1")  # opt-in merged-shortcut form, covered here
     g, w = build_model("ResNet50", seed=8, calibrate=True)
     imgs = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda")
@@ -177,6 +180,8 @@ def test_engine_fused_blocks_equal_unfused(maxc, chain, pairs, monkeypatch):
     # first expands of stages 3-5 and stage 5, C = 2048, are not fused)
     want = ["conv2_block1_3_conv+conv2_block1_0_conv"] + [
         f"conv{s}_block{k}_3_conv" for s, nb in ((2, 3), (3, 4), (4, 6)) for k in range(2, nb)]
+    if merged == "1":
+        want = want[:4] + ["conv3_block1_3_conv+conv3_block1_0_conv"]
     assert sorted(ef.exp_red) == sorted(want[:pairs]) and not eu.exp_red
     # the last fused boundary of each stage feeds only the stride-2 shortcut besides its reduce
     assert "conv2_block2_out" in ef.ysub and not eu.ysub
@@ -203,11 +208,12 @@ def test_engine_fused_blocks_equal_unfused(maxc, chain, pairs, monkeypatch):
     assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 5e-2
 
 
-@pytest.mark.parametrize("m", [64 * 7, 1000, 3 * 56 * 56])
-def test_expand_reduce_merged_shortcut_matches_fp32(m):
-    """K = 2F, no residual: the stage-2 entry after the projection-shortcut merge."""
+@pytest.mark.parametrize("c,m", [(256, 64 * 7), (256, 1000), (256, 3 * 56 * 56), (512, 300), (512, 2 * 28 * 28)])
+def test_expand_reduce_merged_shortcut_matches_fp32(c, m):
+    """K = 2F, no residual: a stage's entry after the projection-shortcut merge (chained
+    kernel: C = 256 and 512)."""
     torch.manual_seed(4)
-    c, f = 256, 64
+    f = c // 4
     x = _bf(torch.randn(m, 2 * f))
     w3 = _bf(torch.randn(c, 2 * f) * (2.0 / (2 * f)) ** 0.5)
     b3 = torch.randn(c) * 0.1
