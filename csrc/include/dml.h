@@ -128,7 +128,12 @@ typedef struct {
   const float* bias;   // fp32 [64]
   void* y;             // bf16 NHWC [N][Ho][Wo][ldy]
   int N, H, W, ldx, ldw;
-  int Ho, Wo, ldy;     // pool output
+  int Ho, Wo, ldy;     // pool output (or, with c4 > 0, the folded 1x1 conv's output)
+  // optional folded 1x1 conv on the pooled tile (InceptionV3 conv2d_4: 64 -> 80, ReLU):
+  // y = relu(w4 . pool + b4) with c4 output channels (c4 % 16 == 0, <= 128); c4 = 0: off
+  const void* w4;      // bf16 [>=c4][ldw4], K = 64 used
+  const float* b4;     // fp32 [c4]
+  int c4, ldw4;
 } DmlConvPoolArgs;
 
 // Fused ResNet50 block boundary (csrc/kernels/bottleneck_fused.hip), F = C / 4:

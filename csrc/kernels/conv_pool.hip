@@ -15,7 +15,12 @@
 //     its 16 x 288 weights in VGPRs;
 //  3. bias + ReLU -> bf16 (the unfused rounding point) into an LDS tile that
 //     reuses the patch region;
-//  4. 3x3/2 max pool from LDS -> one 16-B NHWC store per 8 channels.
+//  4. 3x3/2 max pool from LDS -> one 16-B NHWC store per 8 channels;
+//  or, with a folded 1x1 conv (c4 > 0: InceptionV3 conv2d_4, 64 -> 80 + ReLU, the pool's only
+//  reader), the pooled 64-pixel x 64-channel tile goes to LDS instead, and
+//  5. y = relu(w4 . tile + b4) per 16-pixel fragment (one wave each; 2 k-steps x c4/16
+//     MFMAs), staged through LDS for 16-B NHWC stores: the 64-channel pool output never
+//     reaches HBM (its write and the 1x1 conv's re-read, 2 x 44 MB per 64 images).
 #include "common.h"
 #include "dml.h"
 
@@ -39,10 +44,18 @@ constexpr int PROW = 32 * 2 + 32;            // patch pixel row: 32 bf16 + 32-B 
 constexpr int PATCH_BYTES = PW * PW * PROW;  // 28880
 constexpr int TROW = 64 * 2 + 16;            // conv tile row: 64 bf16 + 16-B pad
 constexpr int TILE_BYTES = NPX * TROW;       // 41616
-constexpr int LDS_BYTES = PATCH_BYTES > TILE_BYTES ? PATCH_BYTES : TILE_BYTES;
+constexpr int LDS_MAIN = PATCH_BYTES > TILE_BYTES ? PATCH_BYTES : TILE_BYTES;
+constexpr int POOLT = LDS_MAIN;                 // folded 1x1: pooled tile [64 px][64 ch] bf16, 128-B rows
+constexpr int LDS_BYTES = POOLT + PB * PB * 128;
+constexpr int C4_MAX = 128;
+constexpr int SROW4 = C4_MAX * 2 + 16;          // folded 1x1 output staging row (reuses the conv tile)
 constexpr int NT = 256;
 constexpr int CHUNKS = PW * PW * 4;          // 16-B input chunks of the patch (1444)
 constexpr int FILL = (CHUNKS + NT - 1) / NT; // 6
+
+// 16-B chunk `ch` of 128-B row `row` of the pooled tile, XOR-swizzled (conflict-free
+// fragment reads of 16 consecutive rows)
+__device__ __forceinline__ int convk_swz(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
 
 __device__ __forceinline__ float bf_at(const uint4& v, int q) {
   const unsigned w = q < 2 ? v.x : q < 4 ? v.y : q < 6 ? v.z : v.w;
@@ -157,8 +170,54 @@ __global__ __launch_bounds__(NT, 3) void conv_pool_kernel(DmlConvPoolArgs a) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], bf_at(v, q));
       }
+    const uint4 pv = make_uint4(pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7]));
+    if (a.c4 > 0)
+      *(uint4*)(smem + POOLT + convk_swz(ly * PB + lx, cg)) = pv;
+    else
+      *(uint4*)((unsigned short*)a.y + ((long)(n * a.Ho + oy) * a.Wo + ox) * a.ldy + cg * 8) = pv;
+  }
+  if (a.c4 <= 0) return;
+
+  // 5. folded 1x1 conv: wave w owns pool pixels 16w .. 16w+15 (pool tile row-major, 8 wide)
+  __syncthreads();  // pooled tile complete; pool rows outside the image hold junk, never stored
+  const int nf4 = a.c4 / 16;
+  f32x4 acc4[C4_MAX / 16];
+#pragma unroll
+  for (int o = 0; o < C4_MAX / 16; ++o) {
+    if (o < nf4) {
+      const float4 bb = *(const float4*)(a.b4 + 16 * o + 4 * fq);
+      acc4[o] = (f32x4){bb.x, bb.y, bb.z, bb.w};
+    }
+  }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const bf16x8 pb = *(const bf16x8*)(smem + POOLT + convk_swz(16 * wid + frow, 4 * ks + fq));
+#pragma unroll
+    for (int o = 0; o < C4_MAX / 16; ++o) {
+      if (o < nf4) {
+        const bf16x8 wa = *(const bf16x8*)((const bf16*)a.w4 + (long)(16 * o + frow) * a.ldw4 + 32 * ks + 8 * fq);
+        acc4[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, pb, acc4[o], 0, 0, 0);
+      }
+    }
+  }
+  // bias (in the accumulator start) + ReLU -> bf16 staging rows (the conv tile region is free:
+  // every wave passed the barrier above after its last pool read)
+#pragma unroll
+  for (int o = 0; o < C4_MAX / 16; ++o) {
+    if (o < nf4) {
+      const f32x4 v = acc4[o];
+      *(uint2*)(smem + (16 * wid + frow) * SROW4 + (16 * o + 4 * fq) * 2) =
+          make_uint2(pack2(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f)), pack2(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)));
+    }
+  }
+  __syncthreads();
+  const int cgs = a.c4 / 8;
+  for (int t = tid; t < PB * PB * cgs; t += NT) {
+    const int px = t / cgs, cg = t - px * cgs;
+    const int oy = py0 + px / PB, ox = px0 + px % PB;
+    if (oy >= a.Ho || ox >= a.Wo) continue;
     *(uint4*)((unsigned short*)a.y + ((long)(n * a.Ho + oy) * a.Wo + ox) * a.ldy + cg * 8) =
-        make_uint4(pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7]));
+        *(const uint4*)(smem + px * SROW4 + cg * 16);
   }
 }
 
@@ -167,8 +226,10 @@ __global__ __launch_bounds__(NT, 3) void conv_pool_kernel(DmlConvPoolArgs a) {
 
 extern "C" int dml_conv3x3_pool(const DmlConvPoolArgs* a, hipStream_t s) {
   // hard-coded: conv 3x3 stride 1 pad 1, 32 -> 64 channels; max pool 3x3/2 valid
-  if (a->ldx % 8 || a->ldx < 32 || a->ldw % 8 || a->ldw < 288 || a->ldy % 8 || a->ldy < 64 || a->N < 1 ||
-      a->H < 3 || a->W < 3 || a->Ho != (a->H - 3) / 2 + 1 || a->Wo != (a->W - 3) / 2 + 1) {
+  const int cy = a->c4 > 0 ? a->c4 : 64;
+  if (a->ldx % 8 || a->ldx < 32 || a->ldw % 8 || a->ldw < 288 || a->ldy % 8 || a->ldy < cy || a->N < 1 ||
+      a->H < 3 || a->W < 3 || a->Ho != (a->H - 3) / 2 + 1 || a->Wo != (a->W - 3) / 2 + 1 ||
+      (a->c4 > 0 && (a->c4 % 16 || a->c4 > dml::cpool::C4_MAX || !a->w4 || !a->b4 || a->ldw4 % 8 || a->ldw4 < 64))) {
     dml_set_error("dml_conv3x3_pool: unsupported shape");
     return -1;
   }

@@ -82,6 +82,7 @@ class ConvPoolArgs(C.Structure):
         ("x", C.c_void_p), ("w", C.c_void_p), ("bias", C.c_void_p), ("y", C.c_void_p),
         ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("ldx", C.c_int), ("ldw", C.c_int),
         ("Ho", C.c_int), ("Wo", C.c_int), ("ldy", C.c_int),
+        ("w4", C.c_void_p), ("b4", C.c_void_p), ("c4", C.c_int), ("ldw4", C.c_int),
     ]
 
 

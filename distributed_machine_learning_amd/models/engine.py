@@ -105,8 +105,10 @@ class Engine:
         self.stem_pool = self._fusable_stem_pool(fuse_stem)
         # InceptionV3 stem: preprocess + conv 3x3/2 + conv 3x3 as ONE kernel
         self.stem_conv2 = self._fusable_inception_stem(fuse_stem) if self.stem_pool is None else None
-        # conv 3x3 (32 -> 64) + the 3x3/2 max pool reading it as ONE kernel (csrc/kernels/conv_pool.hip)
+        # conv 3x3 (32 -> 64) + the 3x3/2 max pool reading it as ONE kernel (csrc/kernels/conv_pool.hip),
+        # with the 1x1 conv that is the pool's only reader folded in (InceptionV3 conv2d_4)
         self.conv_pools = self._fusable_conv_pools(fuse_stem)
+        self.conv_pool_1x1 = self._foldable_pool_1x1(fuse_stem)
         # ResNet stage-2 block boundaries: expand (64 -> 256, + shortcut) and the next
         # block's reduce (256 -> 64) as ONE kernel (csrc/kernels/bottleneck_fused.hip)
         # whole identity bottleneck blocks (reduce -> 3x3 -> expand + shortcut) as ONE
@@ -221,6 +223,24 @@ class Engine:
                     out[c.name] = p
         return out
 
+    def _foldable_pool_1x1(self, enabled: bool) -> Dict[str, Conv]:
+        """{conv name: 1x1 conv} for fused conv+pool pairs whose pool output is read only by
+        a 1x1 stride-1 conv (64 -> c4, c4 % 16 == 0, <= 128, ReLU, no residual): the conv_pool
+        kernel applies it to the pooled tile in LDS. DML_FOLD_POOL_1X1=0: off (A/B)."""
+        if not enabled or os.environ.get("DML_FOLD_POOL_1X1", "1") == "0":
+            return {}
+        out: Dict[str, Conv] = {}
+        for c_name, p in self.conv_pools.items():
+            users = [n for n in self.g.nodes if p.out in (getattr(n, "inp", None), getattr(n, "residual", None))]
+            if len(users) != 1 or not isinstance(users[0], Conv):
+                continue
+            k = users[0]
+            if (k.kh == k.kw == 1 and k.sh == k.sw == 1 and k.ph == k.pw == 0 and k.cin == 64 and k.relu
+                    and k.residual is None and not k.out_f32 and k.in_coff == 0 and k.out_coff == 0
+                    and k.cout % 16 == 0 and k.cout <= 128 and max(getattr(k, "dh", 1), 1) == 1):
+                out[c_name] = k
+        return out
+
     def _fusable_blocks(self, enabled: bool) -> Dict[str, Tuple[Conv, Conv, Conv]]:
         """{reduce name: (reduce, 3x3, expand)} for identity bottleneck blocks the
         fused block kernel supports: 1x1 s1 C -> F (ReLU), 3x3 s1 pad 1 F -> F
@@ -308,6 +328,7 @@ class Engine:
 
         taken = {t.name for t in (self.stem, self.stem_conv2, self.stem_pool) if t is not None}
         taken |= set(self.conv_pools) | {p.name for p in self.conv_pools.values()}
+        taken |= {k.name for k in self.conv_pool_1x1.values()}
         taken |= set(self.exp_red) | {r.name for r in self.exp_red.values()}
         taken |= {t.name for trip in self.blocks.values() for t in trip}
         return conv_group_runs(self.g, taken, N.GROUP_MAX, N.GROUP_POOL_MAX)
@@ -361,7 +382,11 @@ class Engine:
         # position: the first node's inputs stay live through the second node, so
         # the second's output can never be handed a buffer the kernel still reads.
         index = {getattr(n, "name", None): i for i, n in enumerate(nodes)}
-        for first_name, second in {**self.conv_pools, **self.exp_red}.items():
+        pairs = {**self.conv_pools, **self.exp_red}
+        for c_name, k in self.conv_pool_1x1.items():  # conv + pool + folded 1x1 end at the 1x1
+            pairs[c_name] = k
+            first_def[k.out] = min(first_def[k.out], index[c_name])
+        for first_name, second in pairs.items():
             first = nodes[index[first_name]]
             for src in (first.inp, getattr(first, "residual", None)):
                 if src:
@@ -516,6 +541,7 @@ class Engine:
             N.check(L.dml_plan_add_preprocess(plan, C.byref(pa)), "plan preprocess")
             self.op_names.append("preprocess")
         skip |= {p.name for p in self.conv_pools.values()}
+        skip |= {k.name for k in self.conv_pool_1x1.values()}
         skip |= {r.name for r in self.exp_red.values()}
         skip |= {t.name for (_, c, e) in self.blocks.values() for t in (c, e)}
         groups = {grp[0].name: grp for grp in self.conv_groups if grp[0].name in self.group_cfg}
@@ -576,11 +602,17 @@ class Engine:
                 wk, bias, _, kpad, _ = self.wdev[n.name]
                 h, w, _ = g.shape(n.inp)
                 ho, wo, _ = g.shape(p.out)
+                k = self.conv_pool_1x1.get(n.name)
+                out = k.out if k is not None else p.out
                 ca = N.ConvPoolArgs(self.buf[n.inp].data_ptr(), wk.data_ptr(), bias.data_ptr(),
-                                    self.buf[p.out].data_ptr(), B, h, w, self.cbuf[n.inp], kpad, ho, wo,
-                                    self.cbuf[p.out])
+                                    self.buf[out].data_ptr(), B, h, w, self.cbuf[n.inp], kpad, ho, wo,
+                                    self.cbuf[out])
+                if k is not None:
+                    w4, b4, _, kp4, _ = self.wdev[k.name]
+                    ca.w4, ca.b4, ca.c4, ca.ldw4 = w4.data_ptr(), b4.data_ptr(), k.cout, kp4
                 N.check(L.dml_plan_add_conv_pool(plan, C.byref(ca)), "plan conv+pool")
-                self.op_names.append(f"{n.name}+{p.name}")
+                self._keep.append(ca)
+                self.op_names.append(f"{n.name}+{p.name}" + (f"+{k.name}" if k is not None else ""))
                 continue
             if isinstance(n, (Conv, Dense, FusedConv)):
                 cfg = self.cfg_overrides.get(n.name, self.tuned.get(n.name, -1))

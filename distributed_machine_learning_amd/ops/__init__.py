@@ -193,19 +193,29 @@ def inception_stem(images_u8: torch.Tensor, w1_packed: torch.Tensor, b1: torch.T
     return out
 
 
-def conv3x3_pool(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+def conv3x3_pool(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor,
+                 w4: Optional[torch.Tensor] = None, b4: Optional[torch.Tensor] = None,
+                 c4: int = 0) -> torch.Tensor:
     """Fused conv 3x3 'same' (32 -> 64 channels, weights [>=64][>=288], K = (r, s, c))
-    + bias + ReLU + max pool 3x3/2 'valid' (csrc/kernels/conv_pool.hip).
-    x: bf16 NHWC [N, H, W, Cbuf >= 32]; returns bf16 NHWC [N, Ho, Wo, 64]."""
+    + bias + ReLU + max pool 3x3/2 'valid' (csrc/kernels/conv_pool.hip), optionally followed
+    by a folded 1x1 conv 64 -> c4 (+ b4, ReLU; w4 packed [>=c4][>=64]).
+    x: bf16 NHWC [N, H, W, Cbuf >= 32]; returns bf16 NHWC [N, Ho, Wo, 64 or c4]."""
     n, h, w, cbuf = x.shape
     ho, wo = (h - 3) // 2 + 1, (w - 3) // 2 + 1
-    out = torch.empty((n, ho, wo, 64), device=x.device, dtype=torch.bfloat16)
+    cy = c4 if c4 else 64
+    out = torch.empty((n, ho, wo, cy), device=x.device, dtype=torch.bfloat16)
     bias_p = bias.to(x.device, torch.float32).contiguous()
     assert x.is_contiguous() and w_packed.is_contiguous()
     a = N.ConvPoolArgs(x.data_ptr(), w_packed.data_ptr(), bias_p.data_ptr(), out.data_ptr(), n, h, w, cbuf,
-                       w_packed.shape[1], ho, wo, 64)
+                       w_packed.shape[1], ho, wo, cy)
+    keep = [bias_p]
+    if c4:
+        b4p = b4.to(x.device, torch.float32).contiguous()
+        assert w4.is_contiguous() and w4.shape[0] >= c4
+        a.w4, a.b4, a.c4, a.ldw4 = w4.data_ptr(), b4p.data_ptr(), c4, w4.shape[1]
+        keep.append(b4p)
     N.check(N.lib().dml_conv3x3_pool(C.byref(a), N.stream_ptr()), "dml_conv3x3_pool")
-    out._keep = bias_p
+    out._keep = keep
     return out
 
 

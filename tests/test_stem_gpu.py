@@ -139,6 +139,50 @@ def test_conv3x3_pool_matches_fp32(n, h, w, cbuf):
     assert _rel(got, ref) < 1e-2
 
 
+@pytest.mark.parametrize("n,h,w,c4", [(1, 147, 147, 80), (2, 20, 23, 80), (1, 9, 9, 32), (1, 35, 19, 128)])
+def test_conv3x3_pool_folded_1x1(n, h, w, c4):
+    """conv2d_3 + max_pooling2d_1 + conv2d_4 (1x1 64 -> c4 + ReLU) as ONE kernel: the pooled
+    tile never leaves LDS; edge blocks (partial pool tiles) included."""
+    torch.manual_seed(9)
+    x = _bf(torch.randn(n, 32, h, w).clamp(min=0))
+    k = _bf(torch.randn(3, 3, 32, 64) * (2.0 / 288) ** 0.5)
+    b = torch.randn(64) * 0.1
+    w4 = _bf(torch.randn(c4, 64) * (2.0 / 64) ** 0.5)
+    b4 = torch.randn(c4) * 0.1
+    pool = _bf(F.max_pool2d(_bf(F.relu(F.conv2d(x, k.permute(3, 2, 0, 1), b, padding=1))), 3, 2))
+    ref = F.relu(F.conv2d(pool, w4.view(c4, 64, 1, 1), b4)).permute(0, 2, 3, 1)
+    wp = torch.from_numpy(pack_conv_weight(k.numpy(), 32, 256, 320)).to(torch.bfloat16).cuda()
+    w4p = torch.zeros(max(c4, 64), 64)
+    w4p[:c4] = w4
+    y = ops.conv3x3_pool(x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda(), wp, b.cuda(),
+                         w4p.to(torch.bfloat16).cuda(), b4.cuda(), c4)
+    torch.cuda.synchronize()
+    got = y.float().cpu()
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    assert _rel(got, ref) < 1e-2
+
+
+def test_engine_folds_pool_1x1_into_conv_pool():
+    """InceptionV3: conv2d_3 + max_pooling2d_1 + conv2d_4 run as one plan op and the
+    forward matches the engine without the fold."""
+    import os
+
+    g, w = build_model("InceptionV3", seed=3, calibrate=True)
+    imgs = torch.randint(0, 256, (2, 299, 299, 3), dtype=torch.uint8, device="cuda")
+    ef = Engine(g, w, batch=2)
+    os.environ["DML_FOLD_POOL_1X1"] = "0"
+    try:
+        eu = Engine(g, w, batch=2)
+    finally:
+        del os.environ["DML_FOLD_POOL_1X1"]
+    assert ef.conv_pool_1x1 and not eu.conv_pool_1x1
+    assert any(name.endswith("+conv2d_4") for name in ef.op_names)
+    ef.infer(imgs)
+    eu.infer(imgs)
+    torch.cuda.synchronize()
+    assert torch.equal(ef.result.cpu(), eu.result.cpu()) or _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 2e-2
+
+
 @pytest.mark.parametrize("c,m", [(256, 64 * 7), (256, 1000), (256, 3 * 56 * 56), (512, 1000), (512, 2 * 28 * 28),
                                  (1024, 999), (1024, 2 * 14 * 14)])
 def test_expand_reduce_matches_fp32(c, m):

@@ -18,4 +18,10 @@ DML_CHAIN_MERGED=1 DML_CHAIN_C256=1 timeout -k 10 300 $B > gpurun_out/r3k_mc256_
 timeout -k 10 300 $B > gpurun_out/r3k_base_b.log 2>&1 && \
 DML_CHAIN_BIG=1 timeout -k 10 300 $B > gpurun_out/r3k_big_b.log 2>&1 && \
 DML_CHAIN_MERGED=1 timeout -k 10 300 $B > gpurun_out/r3k_merged_b.log 2>&1 && \
-DML_CHAIN_MERGED=1 DML_CHAIN_C256=1 timeout -k 10 300 $B > gpurun_out/r3k_mc256_b.log 2>&1
+DML_CHAIN_MERGED=1 DML_CHAIN_C256=1 timeout -k 10 300 $B > gpurun_out/r3k_mc256_b.log 2>&1 &&
+timeout -k 10 300 $T -k "folded or folds" > gpurun_out/r3k_test_fold.log 2>&1 && \
+BI="python -u bench.py --models InceptionV3 --no-service --steps 100" && \
+timeout -k 10 300 $BI > gpurun_out/r3k_inc_fold_a.log 2>&1 && \
+DML_FOLD_POOL_1X1=0 timeout -k 10 300 $BI > gpurun_out/r3k_inc_nofold_a.log 2>&1 && \
+timeout -k 10 300 $BI > gpurun_out/r3k_inc_fold_b.log 2>&1 && \
+DML_FOLD_POOL_1X1=0 timeout -k 10 300 $BI > gpurun_out/r3k_inc_nofold_b.log 2>&1
