@@ -50,9 +50,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 //  workgroups per CU (one's epilogue VALU work overlaps the other's MFMAs);
 //  <256, 4, 1>: stage 4 (C = 1024) - T (256 k) and the Z accumulators (256 channels)
 //  of 16 pixels per wave fit in VGPRs.
-//  BIG: one barrier per GEMM1 / GEMM2 of a chunk (panels of 16 KiB: W3 64 rows x F k, W1 F rows
-//  x 64 k; a 3-slot ring) instead of one per 64-deep k slice (8 KiB panels, 5 slots); the bias
-//  is read from global memory so <128, 4, 2, BIG> fits 80 KiB: two workgroups per CU.
+//  BIG: 16-KiB panels (W3 64 rows x 128 k, W1 128 rows x 64 k: one barrier per GEMM of a chunk
+//  at F = 128) in a 3-slot ring instead of 8-KiB ones (64 x 64) in 5 slots; the bias is read
+//  from global memory so the 4-wave forms fit 80 KiB: two workgroups per CU.
 //  KX: expand input width (F, or 2F for a stage's first block after the projection-shortcut
 //  merge: T = [x ; s], no residual); RES: the expand adds the shortcut R.
 template <int F_, int NW_, int FJ_, bool BIG_ = false, int KX_ = F_, bool RES_ = true>
@@ -62,8 +62,8 @@ struct Cfg {
   static constexpr bool BIG = BIG_, RES = RES_;
   static constexpr int NS = BIG ? 3 : 5;               // weight panel ring slots
   static constexpr int SLOT = BIG ? 16384 : 8192;      // panel bytes
-  static constexpr int KW3 = BIG ? KX : 64;            // k columns of a W3 panel (64 rows)
-  static constexpr int RW1 = BIG ? F : 64;             // rows of a W1 panel (64 k columns)
+  static constexpr int KW3 = BIG ? (KX < 128 ? KX : 128) : 64;  // k columns of a W3 panel (64 rows)
+  static constexpr int RW1 = BIG ? (F < 128 ? F : 128) : 64;     // rows of a W1 panel (64 k columns)
   static constexpr int C_MAX = 4 * F;
   static constexpr int KS1 = KX / 32;      // T fragments (k32 steps of GEMM1)
   static constexpr int FI1 = CC / 16;      // GEMM1 channel fragments
@@ -418,7 +418,8 @@ static void chain_launch(const DmlExpandReduceArgs* a, hipStream_t s) {
 
 extern "C" int dml_chain_init(void) {
   const int rc = chain_attr<128, 8, 2>() | chain_attr<128, 4, 2>() | chain_attr<128, 4, 2, true>() |
-                 chain_attr<256, 4, 1>() | chain_attr<256, 8, 1>() | chain_attr<64, 4, 2>() |
+                 chain_attr<256, 4, 1>() | chain_attr<256, 8, 1>() | chain_attr<256, 4, 1, true>() |
+                 chain_attr<64, 4, 2>() |
                  chain_attr<64, 4, 2, false, 128, false>() | chain_attr<128, 4, 2, false, 256, false>();
   if (rc) dml_set_error("dml_chain_init: hipFuncSetAttribute failed");
   return rc ? -1 : 0;
@@ -467,6 +468,7 @@ extern "C" int dml_chain(const DmlExpandReduceArgs* a, hipStream_t s) {
     else chain_launch<128, 4, 2>(a, s);
   } else {
     if (nw == 8) chain_launch<256, 8, 1>(a, s);
+    else if (big) chain_launch<256, 4, 1, true>(a, s);
     else chain_launch<256, 4, 1>(a, s);
   }
   DML_CHECK_LAUNCH();

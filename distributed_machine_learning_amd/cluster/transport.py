@@ -22,6 +22,7 @@ import time
 from typing import Awaitable, Callable, Dict, Optional, Set, Tuple
 
 from .frames import Frame, FrameError, MsgType, Reassembler, encode
+from .tasks import spawn
 
 log = logging.getLogger(__name__)
 Addr = Tuple[str, int]
@@ -182,7 +183,7 @@ class LoopbackTransport(Transport):
     async def send(self, dest: str, frame: Frame) -> None:
         self.bytes_sent += sum(len(d) for d in encode(frame))
         if self.net.latency:
-            asyncio.get_running_loop().create_task(self.net.deliver(self.name, dest, frame))
+            spawn(self.net.deliver(self.name, dest, frame))
         else:
             await self.net.deliver(self.name, dest, frame)
 
@@ -226,7 +227,7 @@ class Endpoint:
             if h is None:
                 log.debug("%s: no handler for %s", self.name, fr.type.name)
                 continue
-            asyncio.get_running_loop().create_task(self._safe(h, fr))
+            spawn(self._safe(h, fr))
 
     async def _safe(self, h: Handler, fr: Frame) -> None:
         try:

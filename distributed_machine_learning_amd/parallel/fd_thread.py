@@ -16,6 +16,7 @@ from typing import Callable, Optional, Set
 from ..cluster.failure_detector import FailureDetector
 from ..cluster.membership import MembershipList
 from ..cluster.transport import Endpoint, UdpTransport
+from ..cluster.tasks import spawn
 
 log = logging.getLogger(__name__)
 
@@ -51,7 +52,9 @@ class RankFailureDetector:
     def _main(self) -> None:
         self.loop = asyncio.new_event_loop()
         asyncio.set_event_loop(self.loop)
-        self.loop.create_task(self._run())
+        # the loop keeps only a weak reference to a task: without this one, the garbage
+        # collector destroys the pending detector task (and with it its objects) mid-run
+        self._task = spawn(self._run(), self.loop)
         self.loop.run_forever()
         # drain anything stop() did not reach (e.g. it timed out) before closing
         pending = [t for t in asyncio.all_tasks(self.loop) if not t.done()]
@@ -90,7 +93,8 @@ class RankFailureDetector:
         ep.start()
         self.fd.start()
         self.ready.set()
-        await asyncio.Event().wait()
+        self._idle = asyncio.Event()  # held by self: the parked task stays reachable
+        await self._idle.wait()
 
     async def _shutdown(self) -> None:
         for stop in (getattr(self.fd, "stop", None), getattr(getattr(self.fd, "ep", None), "stop", None)):

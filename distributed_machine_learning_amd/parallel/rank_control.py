@@ -16,6 +16,7 @@ from typing import Callable, Dict, List, Optional
 
 from ..serving.jobs import Batch
 from .rank_backend import split_version, synthetic_names
+from ..cluster.tasks import spawn
 
 log = logging.getLogger(__name__)
 
@@ -67,7 +68,7 @@ class RankControl:
     def _main(self) -> None:
         self.loop = asyncio.new_event_loop()
         asyncio.set_event_loop(self.loop)
-        self.loop.create_task(self._run())
+        self._task = spawn(self._run(), self.loop)
         self.loop.run_forever()
         pending = [t for t in asyncio.all_tasks(self.loop) if not t.done()]
         for t in pending:
@@ -180,8 +181,9 @@ class RankControl:
             if j is not None and j.done and j.job_id not in seen and ":" in j.requester:  # a node, not "local"
                 seen.add(j.job_id)
                 self.loop.call_soon_threadsafe(
-                    lambda jj=j: self.loop.create_task(
-                        self.node.ep.send(jj.requester, MsgType.SUBMIT_JOB_REQUEST_SUCCESS, {"jobid": jj.job_id})))
+                    lambda jj=j: spawn(
+                        self.node.ep.send(jj.requester, MsgType.SUBMIT_JOB_REQUEST_SUCCESS, {"jobid": jj.job_id}),
+                        self.loop))
 
     def became_coordinator(self, previous: int) -> None:
         log.warning("rank %d: now the coordinator (was rank %d)", self.grank, previous)
@@ -257,9 +259,9 @@ class RankControl:
             names = self.pin_versions(pick_images(sorted(self.node.store.meta.matching("*.jpeg")), n))
 
         def reply(res, fr=fr):
-            self.loop.create_task(self.node.ep.reply(fr, MsgType.SUBMIT_JOB_REQUEST_ACK, res))
+            spawn(self.node.ep.reply(fr, MsgType.SUBMIT_JOB_REQUEST_ACK, res), self.loop)
             if res.get("batches") == 0:
-                self.loop.create_task(self.node.ep.send(fr.sender, MsgType.SUBMIT_JOB_REQUEST_SUCCESS,
+                spawn(self.node.ep.send(fr.sender, MsgType.SUBMIT_JOB_REQUEST_SUCCESS,
                                                         {"jobid": res["jobid"]}))
         self.svc.submit_local(model, images=names, requester=fr.sender, reply=reply)
 
@@ -271,7 +273,7 @@ class RankControl:
 
         def reply(res, fr=fr):
             if fr.seq:
-                self.loop.create_task(self.node.ep.reply(fr, MsgType.SET_BATCH_SIZE_ACK, res))
+                spawn(self.node.ep.reply(fr, MsgType.SET_BATCH_SIZE_ACK, res), self.loop)
         self.svc.set_batch_size(fr.payload["model"], int(fr.payload["batch_size"]), reply=reply)
 
     async def _on_c1(self, fr) -> None:

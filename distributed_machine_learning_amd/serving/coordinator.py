@@ -29,6 +29,7 @@ from .jobs import MODELS, Batch, Job, JobManager
 from .journal import JobJournal
 from .metrics import Metrics
 from .scheduler import plan
+from ..cluster.tasks import spawn
 
 log = logging.getLogger(__name__)
 
@@ -165,7 +166,7 @@ class Coordinator:
         b = self.jobs.requeue_front(ent[1])
         _trace.get_tracer().end_async("batch", f"{ent[1][0]}:{ent[1][1]}", cat="job", outcome="requeued")
         if relay:
-            asyncio.get_running_loop().create_task(self.relay("requeue", key=list(ent[1])))
+            spawn(self.relay("requeue", key=list(ent[1])))
         return b
 
     def worker_failed(self, worker: str) -> None:
@@ -173,7 +174,7 @@ class Coordinator:
         if self._requeue_worker(worker) is not None:
             log.info("requeued batch of failed worker %s", worker)
         if self.is_active():
-            asyncio.get_running_loop().create_task(self.schedule())
+            spawn(self.schedule())
 
     # ---------------------------------------------------------------- acks --
     async def _on_worker_ack(self, fr: Frame) -> None:

@@ -29,6 +29,7 @@ import sys
 
 from .cli import MENU, Cli
 from .node import Node, NodeConfig
+from ..cluster.tasks import spawn
 
 
 def parse(argv=None) -> argparse.Namespace:
@@ -150,7 +151,7 @@ async def amain(a: argparse.Namespace) -> int:
                     return
                 print(await cli.run_line(line), flush=True)
 
-        loop.create_task(reader())
+        spawn(reader(), loop)
     await stop.wait()
     await node.stop()
     if a.trace:

@@ -33,6 +33,7 @@ from .coordinator import Coordinator
 from .journal import open_journal
 from .inference import Backend, make_backend
 from .worker import WorkerRole
+from ..cluster.tasks import spawn
 
 log = logging.getLogger(__name__)
 
@@ -162,11 +163,11 @@ class Node:
         if self.is_leader():
             if self.coordinator is not None:
                 self.coordinator.worker_failed(name)
-            asyncio.get_running_loop().create_task(self.store.node_failed(name))
+            spawn(self.store.node_failed(name))
 
     def _on_member_joined(self, name: str) -> None:
         if self.is_leader() and self.coordinator is not None:
-            asyncio.get_running_loop().create_task(self.coordinator.schedule())
+            spawn(self.coordinator.schedule())
 
     def _on_elected(self, acks: Dict[str, dict]) -> None:
         self.store.adopt(acks)
@@ -177,11 +178,11 @@ class Node:
         loop = asyncio.get_running_loop()
         if leader == self.name:
             if self.cfg.introducer:
-                loop.create_task(update_leader(self.ep, self.cfg.introducer, self.name))
+                spawn(update_leader(self.ep, self.cfg.introducer, self.name), loop)
             if self.coordinator is not None:
-                loop.create_task(self.coordinator.schedule())
+                spawn(self.coordinator.schedule(), loop)
         else:
-            loop.create_task(self.store.announce_files())
+            spawn(self.store.announce_files(), loop)
 
     async def _on_job_success(self, fr: Frame) -> None:
         jid = int(fr.payload["jobid"])

@@ -10,6 +10,7 @@ DML_CHAIN_BIG=1 timeout -k 10 300 $T -k "chain" > gpurun_out/r3k_test_big.log 2>
 DML_CHAIN_C256=1 timeout -k 10 300 $T -k "expand_reduce_matches or subsampled" > gpurun_out/r3k_test_c256.log 2>&1 && \
 DML_CHAIN_MERGED=1 timeout -k 10 300 $T -k "engine_fused" > gpurun_out/r3k_test_engine_merged.log 2>&1 && \
 DML_CHAIN_BIG=1 timeout -k 10 300 python -u tools/chain_bench.py --out gpurun_out/r3k_chain_big.json > gpurun_out/r3k_chain_big.log 2>&1 && \
+DML_CHAIN_BIG=1 timeout -k 10 300 python -u tools/chain_bench.py --c 1024 --out gpurun_out/r3k_chain_big1024.json > gpurun_out/r3k_chain_big1024.log 2>&1 && \
 B="python -u bench.py --models ResNet50 --no-service --steps 100" && \
 timeout -k 10 300 $B > gpurun_out/r3k_base_a.log 2>&1 && \
 DML_CHAIN_BIG=1 timeout -k 10 300 $B > gpurun_out/r3k_big_a.log 2>&1 && \
