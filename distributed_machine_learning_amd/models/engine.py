@@ -298,7 +298,7 @@ class Engine:
             # with its shortcut (K = F), or a merged projection shortcut (K = 2F, no residual; C = 256)
             shortcut = e.residual and e.res_sub == 1 and e.cin * 4 == e.cout
             # merged: the r1 kernel (C = 256, DML_FUSED_MERGED_BLOCK=1: measured slower) or the
-            # chained kernel (C = 256 / 512, DML_CHAIN_MERGED=1)
+            # chained kernel (DML_CHAIN_MERGED=1; C = 256 only: stage 3's entry has K = 3F)
             chain_m = os.environ.get("DML_CHAIN_MERGED", "0") == "1"
             merged = (e.residual is None and e.cin * 2 == e.cout
                       and ((e.cout == 256 and (chain_m or os.environ.get("DML_FUSED_MERGED_BLOCK", "0") == "1"))
