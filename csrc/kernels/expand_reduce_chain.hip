@@ -420,7 +420,8 @@ extern "C" int dml_chain_init(void) {
   const int rc = chain_attr<128, 8, 2>() | chain_attr<128, 4, 2>() | chain_attr<128, 4, 2, true>() |
                  chain_attr<256, 4, 1>() | chain_attr<256, 8, 1>() | chain_attr<256, 4, 1, true>() |
                  chain_attr<64, 4, 2>() |
-                 chain_attr<64, 4, 2, false, 128, false>() | chain_attr<128, 4, 2, false, 256, false>();
+                 chain_attr<64, 4, 2, false, 128, false>() | chain_attr<128, 4, 2, false, 256, false>() |
+                 chain_attr<128, 4, 2, false, 64, true>();
   if (rc) dml_set_error("dml_chain_init: hipFuncSetAttribute failed");
   return rc ? -1 : 0;
 }
@@ -431,15 +432,23 @@ static bool env_on(const char* name) {
 }
 
 // 1 if the chained kernel serves this block boundary, else 0 (the caller falls back to the
-// phase-serialised kernels): with a shortcut, F = 128 / C = 512 or F = 256 / C = 1024 (F = 64 /
-// C = 256 with DML_CHAIN_C256=1: the r1 kernel is near the HBM roofline there); merged
-// projection shortcut (T = [x ; s], K = 2F, no residual), F = 64 / C = 256 or F = 128 / C = 512
+// phase-serialised kernels): with a shortcut, F = 64 / C = 256 (stage 2: ResNet50 b256 90.3-90.9k
+// vs 88.1-88.7k img/s with the r1 kernel, interleaved on one box, profiles/r3_v6; DML_CHAIN_C256=0:
+// the r1 kernel), F = 128 / C = 512 or F = 256 / C = 1024; merged projection shortcut (T = [x ; s],
+// K = 2F, no residual), F = 64 / C = 256 or F = 128 / C = 512
 extern "C" int dml_chain_supported(const DmlExpandReduceArgs* a) {
-  const int C = a->C, F = C / 4;
+  const int C = a->C, F = C / 4, FZ = a->fz > 0 ? a->fz : F;
   const bool merged = a->res == nullptr;
   const int kx = merged ? a->kx : F;
+  // a stage's last boundary: expand F = 64 -> C = 256 (+ shortcut) feeding the next stage's
+  // first reduce 256 -> 128 (template F = reduce width 128, KX = 64; a.C = 256 chunks)
+  if (FZ != F)
+    return !merged && C == 256 && FZ == 128 && (a->kx == 0 || a->kx == F) && a->M >= 1 && a->ldx % 8 == 0 &&
+           a->ldx >= F && a->ldw3 % 8 == 0 && a->ldw3 >= F && a->ldr % 8 == 0 && a->ldr >= C &&
+           a->ldy % 8 == 0 && a->ldy >= C && a->ldw1 % 8 == 0 && a->ldw1 >= C && a->ldz % 8 == 0 &&
+           a->ldz >= FZ && (long)a->M * (a->ldr > a->ldy ? a->ldr : a->ldy) * 2 < 0x7ffffff0L;
   const long ld = a->ldx > a->ldr ? (a->ldx > a->ldy ? a->ldx : a->ldy) : (a->ldr > a->ldy ? a->ldr : a->ldy);
-  static const bool c256 = env_on("DML_CHAIN_C256");
+  static const bool c256 = [] { const char* e = getenv("DML_CHAIN_C256"); return !(e && e[0] == '0'); }();
   const bool shape = merged ? ((F == 64 || F == 128) && a->kx == 2 * F)
                             : ((F == 128 || F == 256 || (F == 64 && c256)) && (a->kx == 0 || a->kx == F));
   return shape && a->M >= 1 && a->ldx % 8 == 0 && a->ldx >= kx && a->ldw3 % 8 == 0 && a->ldw3 >= kx &&
@@ -451,13 +460,16 @@ extern "C" int dml_chain_supported(const DmlExpandReduceArgs* a) {
 // DML_CHAIN_BIG=1 (one barrier per GEMM of a chunk) are A/B variants of the C = 512 form
 extern "C" int dml_chain(const DmlExpandReduceArgs* a, hipStream_t s) {
   if (!dml_chain_supported(a)) {
-    dml_set_error("dml_chain: unsupported shape (C = 512 / 1024 with a shortcut, merged C = 256 / 512)");
+    dml_set_error("dml_chain: unsupported shape (C = 256 / 512 / 1024 with a shortcut, merged C = 256 / 512, "
+                  "stage end C = 256 -> 128)");
     return -1;
   }
   static const int nw = [] { const char* e = getenv("DML_CHAIN_WAVES"); return e && atoi(e) == 8 ? 8 : 4; }();
   static const bool big = env_on("DML_CHAIN_BIG");
   const bool merged = a->res == nullptr;
-  if (merged) {
+  if (a->fz > 0 && a->fz != a->C / 4) {
+    chain_launch<128, 4, 2, false, 64, true>(a, s);  // stage-end boundary (256 -> 128 reduce)
+  } else if (merged) {
     if (a->C == 256) chain_launch<64, 4, 2, false, 128, false>(a, s);
     else chain_launch<128, 4, 2, false, 256, false>(a, s);
   } else if (a->C == 256) {
