@@ -103,6 +103,13 @@ typedef struct {
   int ldw;
   int Hc, Wc;         // conv output size
   int Ho, Wo, ldy;    // pool output size / channel stride
+  // optional folded 1x1 conv on the pooled tile (ResNet50 conv2_block1_1: 64 -> 64 + ReLU, the
+  // next op reading exactly the pool output), z = relu(w4 . pool + b4); c4 = 0: off. The pooled
+  // tensor y is still written (the merged projection shortcut reads it).
+  const void* w4;     // bf16 [>=64][ldw4], K = 64 used
+  const float* b4;    // fp32 [64]
+  void* z;            // bf16 NHWC [N][Ho][Wo][ldz]
+  int c4, ldw4, ldz;
 } DmlStemArgs;
 
 // Fused InceptionV3 stem (csrc/kernels/stem_fused.hip): uint8 image -> preprocess ->
@@ -156,6 +163,10 @@ typedef struct {
   // is stored only for h, w % ysub == 0, compactly at n*(yH/ysub)*(yW/ysub) + ...
   int ysub, yH, yW;
   long long* stamps;  // diagnostics only (null in the engine): chained kernel, per workgroup 40 x s_memtime
+  // reduce width (0 = F = C / 4). 2F at a stage's last boundary, where the expand's output feeds
+  // the next stage's first reduce (ResNet50 conv2_block3_3 -> conv3_block1_1: 256 -> 128;
+  // chained kernel only)
+  int fz;
 } DmlExpandReduceArgs;
 
 // Whole ResNet50 identity bottleneck block (csrc/kernels/block_fused.hip), C = 4F:

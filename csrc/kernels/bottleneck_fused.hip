@@ -228,6 +228,10 @@ extern "C" int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s) {
   // below (A/B)
   static const bool chain = [] { const char* e = getenv("DML_ER_R1"); return !(e && e[0] == '1'); }();
   if (chain && dml_chain_supported(a)) return dml_chain(a, s);
+  if (a->fz > 0 && a->fz != a->C / 4) {  // a stage-end boundary: the chained kernel's form only
+    dml_set_error("dml_expand_reduce: reduce width != C / 4 needs the chained kernel (DML_ER_R1 unset)");
+    return -1;
+  }
   // expand KX -> C channels (+ shortcut), reduce C -> F, F = C / 4, C in {256, 512, 1024};
   // KX = F with a shortcut, or KX = 2F without one (merged projection shortcut, C = 256)
   const int C = a->C, F = C / 4;

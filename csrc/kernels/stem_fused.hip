@@ -23,7 +23,10 @@
 //  3. bias + ReLU -> bf16 (the unfused conv's rounding point) into an LDS tile;
 //     conv positions outside the conv image are stored as 0, which is exact for
 //     the max pool because every window holds a valid post-ReLU value >= 0;
-//  4. the 3x3/2 max pool from LDS -> one 16-B NHWC store per 8 channels.
+//  4. the 3x3/2 max pool from LDS -> one 16-B NHWC store per 8 channels;
+//  5. optionally (c4 = 64) the next 1x1 conv (ResNet50 conv2_block1_1, 64 -> 64 + ReLU) on the
+//     pooled tile, which then stays in LDS: its 56 pixels x 64 channels are one 16-pixel
+//     fragment per wave, K = 64 (8 MFMAs per wave), weights read as A fragments from L2.
 //
 // The 15x17 conv window of a 7x8 pool block overlaps its neighbours by one row /
 // column (14 % recomputed MACs) — traded for never writing the conv output.
@@ -46,6 +49,10 @@ constexpr int KROWS = 7;                         // k-steps (kernel rows)
 constexpr int NT = 256;                          // 4 waves: 2 (pixels) x 2 (channels)
 
 constexpr int FILL = (IR * PQ + NT - 1) / NT;  // patch chunks per thread (3)
+
+// pooled tile rows of 128 B (64 bf16), 16-B chunk ^= row & 7 (conflict-free fragment reads)
+__device__ __forceinline__ int pswz(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
+static_assert(PH * PW <= 64 && 64 * 128 <= PATCH_BYTES, "pooled tile: 4 fragments in the patch region");
 
 __device__ __forceinline__ float bf_at(const uint4& v, int q) {
   const unsigned w = q < 2 ? v.x : q < 4 ? v.y : q < 6 ? v.z : v.w;
@@ -199,8 +206,44 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], bf_at(v, q));
       }
-    *(uint4*)((unsigned short*)a.y + ((long)(n * a.Ho + oy) * a.Wo + ox) * a.ldy + cg * 8) =
-        make_uint4(pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7]));
+    const uint4 pv = make_uint4(pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7]));
+    *(uint4*)((unsigned short*)a.y + ((long)(n * a.Ho + oy) * a.Wo + ox) * a.ldy + cg * 8) = pv;
+    if (a.c4 > 0) *(uint4*)(patch + pswz(ly * PW + lx, cg)) = pv;  // the patch is dead since step 3
+  }
+  if (a.c4 <= 0) return;
+
+  // 5. folded 1x1 conv: wave w owns pooled pixels 16w .. 16w+15 (row-major 7 x 8; rows past 56 and
+  // pool pixels outside the image hold junk and are never stored), all 64 output channels
+  __syncthreads();  // pooled tile complete; every wave's last conv-tile read is behind this barrier
+  f32x4 acc4[4];
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const float4 bb = *(const float4*)(a.b4 + 16 * o + 4 * fq);
+    acc4[o] = (f32x4){bb.x, bb.y, bb.z, bb.w};
+  }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const bf16x8 pb = *(const bf16x8*)(patch + pswz(16 * wid + frow, 4 * ks + fq));
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const bf16x8 wa = *(const bf16x8*)((const bf16*)a.w4 + (long)(16 * o + frow) * a.ldw4 + 32 * ks + 8 * fq);
+      acc4[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, pb, acc4[o], 0, 0, 0);
+    }
+  }
+  // ReLU -> bf16 staging rows in the (free) conv tile region -> 16-B NHWC stores
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const f32x4 v = acc4[o];
+    *(uint2*)(tile + (16 * wid + frow) * SROW + (16 * o + 4 * fq) * 2) =
+        make_uint2(pack2(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f)), pack2(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)));
+  }
+  __syncthreads();
+  for (int t = tid; t < PH * PW * 8; t += NT) {
+    const int px = t >> 3, cg = t & 7;
+    const int oy = py0 + px / PW, ox = px0 + px % PW;
+    if (oy >= a.Ho || ox >= a.Wo) continue;
+    *(uint4*)((unsigned short*)a.z + ((long)(n * a.Ho + oy) * a.Wo + ox) * a.ldz + cg * 8) =
+        *(const uint4*)(tile + px * SROW + cg * 16);
   }
 }
 
@@ -411,8 +454,10 @@ extern "C" int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s) {
   // the kernel hard-codes conv 7x7/2 pad 3 -> 64 channels and max pool 3x3/2 pad 1
   if (a->ldw % 8 || a->ldw < 224 || a->ldy % 8 || a->ldy < 64 || a->N < 1 || a->H < 1 || a->W < 1 ||
       a->Hc != (a->H - 1) / 2 + 1 || a->Wc != (a->W - 1) / 2 + 1 || a->Ho != (a->Hc - 1) / 2 + 1 ||
-      a->Wo != (a->Wc - 1) / 2 + 1 || a->Hs < 1 || a->Ws < 1) {
-    dml_set_error("dml_stem_resnet: unsupported shape");
+      a->Wo != (a->Wc - 1) / 2 + 1 || a->Hs < 1 || a->Ws < 1 ||
+      (a->c4 != 0 && (a->c4 != 64 || !a->w4 || !a->b4 || !a->z || a->ldw4 % 8 || a->ldw4 < 64 || a->ldz % 8 ||
+                      a->ldz < 64))) {
+    dml_set_error("dml_stem_resnet: unsupported shape (folded 1x1: 64 -> 64 only)");
     return -1;
   }
   using namespace dml::stem;

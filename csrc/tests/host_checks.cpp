@@ -198,6 +198,15 @@ int main() {
   CHECK(dml_expand_reduce(&er, nullptr) != 0);    // reduce weights shorter than K = 256
   er.ldw1 = 256; er.ldr = 64;
   CHECK(dml_expand_reduce(&er, nullptr) != 0);    // shortcut narrower than 256 channels
+  er.ldr = 256; er.fz = 96; er.ldz = 128;
+  er.res = (const void*)&er;                       // a shortcut (never dereferenced by the checks)
+  CHECK(dml_chain_supported(&er) == 0);            // stage-end reduce width: 128 only
+  CHECK(dml_expand_reduce(&er, nullptr) != 0);    // ... and never the r1 kernel
+  er.fz = 128;
+  CHECK(dml_chain_supported(&er) == 1);            // 64 -> 256 (+ shortcut) -> 128
+  er.ldz = 64;
+  CHECK(dml_chain_supported(&er) == 0);            // Z rows narrower than the reduce width
+  er.fz = 0; er.ldz = 64; er.res = nullptr;
   {  // whole fused bottleneck block: only F = 64, C = 4F, 8-aligned strides, y != x
     DmlBlockArgs b{};
     char buf[64];

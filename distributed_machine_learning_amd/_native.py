@@ -64,6 +64,8 @@ class StemArgs(C.Structure):
         ("src", C.c_void_p), ("w", C.c_void_p), ("bias", C.c_void_p), ("y", C.c_void_p),
         ("N", C.c_int), ("Hs", C.c_int), ("Ws", C.c_int), ("H", C.c_int), ("W", C.c_int), ("mode", C.c_int),
         ("ldw", C.c_int), ("Hc", C.c_int), ("Wc", C.c_int), ("Ho", C.c_int), ("Wo", C.c_int), ("ldy", C.c_int),
+        ("w4", C.c_void_p), ("b4", C.c_void_p), ("z", C.c_void_p), ("c4", C.c_int), ("ldw4", C.c_int),
+        ("ldz", C.c_int),
     ]
 
 
@@ -92,7 +94,7 @@ class ExpandReduceArgs(C.Structure):
         ("w1", C.c_void_p), ("b1", C.c_void_p), ("z", C.c_void_p),
         ("M", C.c_int), ("ldx", C.c_int), ("ldw3", C.c_int), ("ldr", C.c_int), ("ldy", C.c_int),
         ("ldw1", C.c_int), ("ldz", C.c_int), ("C", C.c_int), ("kx", C.c_int),
-        ("ysub", C.c_int), ("yH", C.c_int), ("yW", C.c_int), ("stamps", C.c_void_p),
+        ("ysub", C.c_int), ("yH", C.c_int), ("yW", C.c_int), ("stamps", C.c_void_p), ("fz", C.c_int),
     ]
 
 

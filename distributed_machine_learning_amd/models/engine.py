@@ -103,6 +103,8 @@ class Engine:
         # ResNet stem: preprocess + 7x7/2 conv + 3x3/2 max pool run as ONE kernel
         # (csrc/kernels/stem_fused.hip) when the pool is the conv's only consumer.
         self.stem_pool = self._fusable_stem_pool(fuse_stem)
+        # ... with the 1x1 conv reading exactly the pooled tensor folded in (ResNet50 conv2_block1_1)
+        self.stem_1x1 = self._foldable_stem_1x1(fuse_stem)
         # InceptionV3 stem: preprocess + conv 3x3/2 + conv 3x3 as ONE kernel
         self.stem_conv2 = self._fusable_inception_stem(fuse_stem) if self.stem_pool is None else None
         # conv 3x3 (32 -> 64) + the 3x3/2 max pool reading it as ONE kernel (csrc/kernels/conv_pool.hip),
@@ -117,6 +119,9 @@ class Engine:
         self.exp_red = self._fusable_expand_reduce(fuse_blocks)
         # fused pairs whose Y is otherwise only read at stride 2 store just those pixels
         self.ysub = self._subsampled_y()
+        # a stage's last expand (its shortcut stored compactly by the pair above) chained with
+        # the next stage's first reduce
+        self.exp_red.update(self._fusable_stage_end(fuse_blocks))
         # independent residual-free convs of one graph level -> one grouped grid each
         self.conv_groups = self._conv_group_candidates() if conv_groups else []
         self._src_tensors, self._result_views = src_tensors, result_views
@@ -168,6 +173,24 @@ class Engine:
                 torch.from_numpy(bias).to(self.device),
                 K, kpad, cin_eff,
             )
+
+    def _foldable_stem_1x1(self, enabled: bool) -> Optional[Conv]:
+        """The 1x1 conv (64 -> 64, stride 1, ReLU, no residual) that reads exactly the fused stem's
+        pooled tensor — ResNet50's conv2_block1_1, which after the projection-shortcut merge reads
+        the s slice of stage 2's [x ; s] buffer — applied by the stem kernel to the pooled tile in
+        LDS (csrc/kernels/stem_fused.hip step 5). The pooled tensor is still written (the merged
+        expand reads it). DML_FOLD_STEM_1X1=0: off (A/B)."""
+        p = self.stem_pool
+        if not enabled or p is None or os.environ.get("DML_FOLD_STEM_1X1", "1") == "0":
+            return None
+        nodes = self.g.nodes
+        i = nodes.index(p)
+        k = nodes[i + 1] if i + 1 < len(nodes) else None
+        if not (isinstance(k, Conv) and k.inp == p.out and k.in_coff == p.out_coff and k.cin == 64
+                and k.cout == 64 and k.kh == k.kw == 1 and k.sh == k.sw == 1 and k.ph == k.pw == 0 and k.relu
+                and k.residual is None and not k.out_f32 and k.out_coff == 0 and max(getattr(k, "dh", 1), 1) == 1):
+            return None
+        return k
 
     def _fusable_stem_pool(self, enabled: bool) -> Optional[Pool]:
         """The max pool that the fused stem kernel can absorb together with the
@@ -319,6 +342,33 @@ class Engine:
             out[e.name] = r
         return out
 
+    def _fusable_stage_end(self, enabled: bool) -> Dict[str, Conv]:
+        """{expand name: reduce} for a stage's last block boundary, chained (expand_reduce_chain.hip):
+        the expand (1x1 F -> C = 4F, + the shortcut, which the previous fused boundary stored
+        compactly: ``ysub``) writes its C channels into the next stage's ``[x ; s]`` concat buffer,
+        and the next stage's first reduce (C -> 2F) reads exactly that slice. ResNet50:
+        conv2_block3_3 -> conv3_block1_1 (64 -> 256 -> 128 at 28x28; the stage-3/4 ends would need
+        2F = 256 / 512 reduce accumulators per wave). DML_CHAIN_STAGE_END=0: off."""
+        if (not enabled or self.device.type != "cuda" or os.environ.get("DML_FUSED_BLOCKS") == "0"
+                or os.environ.get("DML_CHAIN_STAGE_END", "1") == "0" or os.environ.get("DML_ER_R1") == "1"):
+            return {}
+        out: Dict[str, Conv] = {}
+        nodes = self.g.nodes
+        taken = set(self.exp_red) | {r.name for r in self.exp_red.values()}
+        taken |= {t.name for trip in getattr(self, "blocks", {}).values() for t in trip}
+        for e, r in zip(nodes, nodes[1:]):
+            if not (isinstance(e, Conv) and isinstance(r, Conv)) or e.name in taken or r.name in taken:
+                continue
+            if not (e.kh == e.kw == 1 and e.sh == e.sw == 1 and e.cin == 64 and e.cout == 256 and e.relu
+                    and e.residual in self.ysub and e.in_coff == 0 and not e.out_f32):
+                continue
+            if not (r.inp == e.out and r.in_coff == e.out_coff and r.cin == e.cout and r.cout == 2 * e.cin
+                    and r.kh == r.kw == 1 and r.sh == r.sw == 1 and r.relu and r.residual is None
+                    and r.out_coff == 0 and not r.out_f32):
+                continue
+            out[e.name] = r
+        return out
+
     def _conv_group_candidates(self) -> List[list]:
         """Runs of consecutive groupable convs / 3x3 pools of one ASAP level (the
         level order puts them side by side), at most GROUP_MAX convs and
@@ -326,7 +376,7 @@ class Engine:
         launches as one grid is decided by timing at plan time (``_build_plan``)."""
         from .optimize import conv_group_runs
 
-        taken = {t.name for t in (self.stem, self.stem_conv2, self.stem_pool) if t is not None}
+        taken = {t.name for t in (self.stem, self.stem_conv2, self.stem_pool, self.stem_1x1) if t is not None}
         taken |= set(self.conv_pools) | {p.name for p in self.conv_pools.values()}
         taken |= {k.name for k in self.conv_pool_1x1.values()}
         taken |= set(self.exp_red) | {r.name for r in self.exp_red.values()}
@@ -386,6 +436,9 @@ class Engine:
         for c_name, k in self.conv_pool_1x1.items():  # conv + pool + folded 1x1 end at the 1x1
             pairs[c_name] = k
             first_def[k.out] = min(first_def[k.out], index[c_name])
+        if self.stem_1x1 is not None:  # the fused stem writes the folded 1x1's output at its own position
+            first_def[self.stem_1x1.out] = min(first_def[self.stem_1x1.out], index[self.stem.name])
+            last_use[self.stem_pool.out] = max(last_use.get(self.stem_pool.out, 0), index[self.stem_1x1.name])
         for first_name, second in pairs.items():
             first = nodes[index[first_name]]
             for src in (first.inp, getattr(first, "residual", None)):
@@ -520,9 +573,15 @@ class Engine:
             sa = N.StemArgs(src.data_ptr(), wk.data_ptr(), bias.data_ptr(), y, B,
                             self.src_hw[0], self.src_hw[1], g.input_hw[0], g.input_hw[1], mode, kpad, hc, wc,
                             ho, wo, self.cbuf[p.out])
+            k = self.stem_1x1
+            if k is not None:
+                w4, b4, _, kp4, _ = self.wdev[k.name]
+                sa.w4, sa.b4, sa.z, sa.c4, sa.ldw4, sa.ldz = (w4.data_ptr(), b4.data_ptr(), self.buf[k.out].data_ptr(),
+                                                              k.cout, kp4, self.cbuf[k.out])
             N.check(L.dml_plan_add_stem(plan, C.byref(sa)), "plan stem")
-            self.op_names.append(f"preprocess+{s.name}+{p.name}")
-            skip = {s.name, p.name}
+            self._keep.append(sa)
+            self.op_names.append(f"preprocess+{s.name}+{p.name}" + (f"+{k.name}" if k is not None else ""))
+            skip = {s.name, p.name} | ({k.name} if k is not None else set())
         elif self.stem_conv2 is not None:
             s, c = self.stem, self.stem_conv2
             w1, b1, _, kp1, _ = self.wdev[s.name]
@@ -588,10 +647,11 @@ class Engine:
                 res = self.buf[n.residual].data_ptr() if n.residual else None
                 ldr = self.cbuf[n.residual] if n.residual else 0
                 ea = N.ExpandReduceArgs(self.buf[n.inp].data_ptr(), w3.data_ptr(), b3.data_ptr(),
-                                        res, self.buf[n.out].data_ptr(),
+                                        res, self.buf[n.out].data_ptr() + 2 * n.out_coff,
                                         w1.data_ptr(), b1.data_ptr(), self.buf[r.out].data_ptr(), B * h * w,
                                         self.cbuf[n.inp], kp3, ldr, self.cbuf[n.out], kp1,
                                         self.cbuf[r.out], n.cout, n.cin)
+                ea.fz = r.cout
                 if n.out in self.ysub:
                     ea.ysub, ea.yH, ea.yW = self.ysub[n.out], h, w
                 N.check(L.dml_plan_add_expand_reduce(plan, C.byref(ea)), "plan expand+reduce")

@@ -153,11 +153,13 @@ def preprocess(images_u8: torch.Tensor, out_hw, mode: str, pair: bool = False, l
 
 
 def resnet_stem(images_u8: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, out_hw=(224, 224),
-                mode: str = "caffe") -> torch.Tensor:
+                mode: str = "caffe", w4: Optional[torch.Tensor] = None, b4: Optional[torch.Tensor] = None):
     """Fused ResNet stem (csrc/kernels/stem_fused.hip): uint8 [N, Hs, Ws, 3] ->
     nearest resize to out_hw + caffe/tf normalisation -> conv 7x7/2 pad 3 with the
     pair-packed bf16 weights [>=64][>=224] (models.engine.pair_pack_kernel +
-    pack_conv_weight) + bias + ReLU -> max pool 3x3/2 pad 1 -> bf16 NHWC [N, Ho, Wo, 64]."""
+    pack_conv_weight) + bias + ReLU -> max pool 3x3/2 pad 1 -> bf16 NHWC [N, Ho, Wo, 64].
+    With w4 (bf16 [>=64][>=64], packed) and b4: also the folded 1x1 conv relu(w4 . pool + b4)
+    (ResNet50 conv2_block1_1); returns (pool, z) then."""
     n, hs, ws, _ = images_u8.shape
     h, w = out_hw
     hc, wc = (h - 1) // 2 + 1, (w - 1) // 2 + 1
@@ -167,8 +169,17 @@ def resnet_stem(images_u8: torch.Tensor, w_packed: torch.Tensor, bias: torch.Ten
     assert images_u8.is_contiguous() and w_packed.is_contiguous() and w_packed.shape[0] >= 64
     a = N.StemArgs(images_u8.data_ptr(), w_packed.data_ptr(), bias_p.data_ptr(), out.data_ptr(), n, hs, ws, h, w,
                    0 if mode == "caffe" else 1, w_packed.shape[1], hc, wc, ho, wo, 64)
+    z = None
+    if w4 is not None:
+        z = torch.empty((n, ho, wo, 64), device=images_u8.device, dtype=torch.bfloat16)
+        b4p = b4.to(images_u8.device, torch.float32).contiguous()
+        assert w4.is_contiguous() and w4.shape[0] >= 64
+        a.w4, a.b4, a.z, a.c4, a.ldw4, a.ldz = w4.data_ptr(), b4p.data_ptr(), z.data_ptr(), 64, w4.shape[1], 64
     N.check(N.lib().dml_stem_resnet(C.byref(a), N.stream_ptr()), "dml_stem_resnet")
     out._keep = bias_p
+    if z is not None:
+        z._keep = b4p
+        return out, z
     return out
 
 
@@ -220,14 +231,16 @@ def conv3x3_pool(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor,
 
 
 def expand_reduce(x: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, res: Optional[torch.Tensor],
-                  w1: torch.Tensor, b1: torch.Tensor, c: Optional[int] = None):
+                  w1: torch.Tensor, b1: torch.Tensor, c: Optional[int] = None, fz: int = 0):
     """Fused ResNet block boundary (csrc/kernels/bottleneck_fused.hip), C = res channels,
     F = C / 4: y = relu(1x1 conv F -> C of x + b3 + res), z = relu(1x1 conv C -> F of y + b1).
     x: bf16 [..., F]; res: bf16 [..., C], C in {256, 512, 1024}; w3 [>=C][>=F], w1 [>=F][>=C]
     packed (pack_weight). Returns (y, z) with x's leading shape.
-    res=None (merged projection shortcut): x is [..., 2F] (the [x ; s] concat), C = c = 256."""
+    res=None (merged projection shortcut): x is [..., 2F] (the [x ; s] concat), C = c = 256.
+    fz: reduce width when it is not F — a stage's last boundary (C = 256, fz = 128: the next
+    stage's first reduce; chained kernel)."""
     c = res.shape[-1] if res is not None else c
-    f = c // 4
+    f = fz or c // 4
     lead = x.shape[:-1]
     m = x.numel() // x.shape[-1]
     y = torch.empty((*lead, c), device=x.device, dtype=torch.bfloat16)
@@ -239,7 +252,8 @@ def expand_reduce(x: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, res: Opti
     a = N.ExpandReduceArgs(x.data_ptr(), w3.data_ptr(), b3p.data_ptr(), res.data_ptr() if res is not None else None,
                            y.data_ptr(), w1.data_ptr(), b1p.data_ptr(), z.data_ptr(), m, x.shape[-1], w3.shape[1],
                            res.shape[-1] if res is not None else 0, c, w1.shape[1], f, c,
-                           f if res is not None else 2 * f)
+                           c // 4 if res is not None else c // 2)
+    a.fz = f
     N.check(N.lib().dml_expand_reduce(C.byref(a), N.stream_ptr()), "dml_expand_reduce")
     y._keep = (b3p, b1p)
     return y, z

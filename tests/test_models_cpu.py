@@ -343,3 +343,60 @@ def test_oracle_is_input_sensitive(name):
     a, b = emu - emu.mean(0), ref - ref.mean(0)
     assert ((a - b).abs().max() / b.abs().max()).item() < 6e-2
     assert (ref.std(0).mean() / ref.std(1).mean()).item() > 0.5   # image-dependent part is not a sliver
+
+
+def test_block_boundary_fusion_plan_resnet50(monkeypatch):
+    """Which ResNet50 block boundaries the engine fuses (decided on the graph alone, as on the
+    GPU): stage-2 / stage-3 identity boundaries, their Y stored compactly where only the stride-2
+    shortcut reads it, and stage 2's last expand chained with stage 3's first reduce (the expand
+    writes the s slice of stage 3's [x ; s] concat buffer, the reduce reads exactly that slice)."""
+    from distributed_machine_learning_amd.models.engine import Engine
+    from distributed_machine_learning_amd.models.optimize import level_order, optimize
+
+    g, w = build_model("ResNet50", seed=0)
+    g2 = level_order(optimize(g, stride_push=True, weights=w))
+
+    def plan(**env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        e = Engine.__new__(Engine)
+        e.g, e.device, e.blocks = g2, torch.device("cuda"), {}
+        e.exp_red = e._fusable_expand_reduce(True)
+        e.ysub = e._subsampled_y()
+        e.exp_red.update(e._fusable_stage_end(True))
+        return e
+
+    e = plan()
+    assert sorted(e.exp_red) == ["conv2_block2_3_conv", "conv2_block3_3_conv", "conv3_block2_3_conv",
+                                 "conv3_block3_3_conv"]
+    assert e.ysub == {"conv2_block2_out": 2, "conv3_block3_out": 2}
+    x, r = next(n for n in g2.nodes if n.name == "conv2_block3_3_conv"), e.exp_red["conv2_block3_3_conv"]
+    assert r.name == "conv3_block1_1_conv" and r.cout == 2 * x.cin and r.in_coff == x.out_coff == 128
+    assert x.residual in e.ysub  # the shortcut is read compactly, at the expand's own grid
+    assert "conv2_block3_3_conv" not in plan(DML_CHAIN_STAGE_END="0").exp_red
+    assert "conv2_block3_3_conv" not in plan(DML_CHAIN_STAGE_END="1", DML_ER_R1="1").exp_red
+
+
+def test_stem_fold_plan_resnet50(monkeypatch):
+    """The fused ResNet50 stem absorbs conv2_block1_1 (the 1x1 reading exactly its pooled output,
+    the s slice of stage 2's [x ; s] buffer); InceptionV3 has no such pair."""
+    from distributed_machine_learning_amd.models.engine import Engine
+    from distributed_machine_learning_amd.models.optimize import level_order, optimize
+
+    def plan(name):
+        g, w = build_model(name, seed=0)
+        e = Engine.__new__(Engine)
+        e.g, e.device = level_order(optimize(g, stride_push=True, weights=w)), torch.device("cuda")
+        readers = [n for n in e.g.nodes if getattr(n, "inp", None) == e.g.input]
+        e.stem = readers[0]
+        e.stem_pool = e._fusable_stem_pool(True)
+        return e, e._foldable_stem_1x1(True)
+
+    e, k = plan("ResNet50")
+    assert e.stem_pool is not None and k is not None and k.name == "conv2_block1_1_conv"
+    assert k.in_coff == e.stem_pool.out_coff == 64 and k.inp == e.stem_pool.out
+    monkeypatch.setenv("DML_FOLD_STEM_1X1", "0")
+    assert plan("ResNet50")[1] is None
+    monkeypatch.delenv("DML_FOLD_STEM_1X1")
+    e, k = plan("InceptionV3")
+    assert e.stem_pool is None and k is None

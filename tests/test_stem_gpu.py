@@ -54,6 +54,27 @@ def test_fused_stem_matches_fp32(n, hs, ws, out_hw, mode):
     assert rel < 1e-2, rel
 
 
+@pytest.mark.parametrize("n,hs,ws,out_hw", [(2, 224, 224, (224, 224)), (2, 64, 80, (61, 47)), (1, 20, 20, (9, 9))])
+def test_fused_stem_folded_1x1_matches_fp32(n, hs, ws, out_hw):
+    """Step 5 of the stem kernel: the next 1x1 conv (ResNet50 conv2_block1_1, 64 -> 64 + ReLU)
+    on the pooled tile in LDS; the pooled tensor is still written."""
+    torch.manual_seed(1)
+    imgs = torch.randint(0, 256, (n, hs, ws, 3), dtype=torch.uint8)
+    k = _bf(torch.randn(7, 7, 3, 64) * (2.0 / 147) ** 0.5)
+    b = torch.randn(64) * 0.1
+    k4 = _bf(torch.randn(64, 64) * (2.0 / 64) ** 0.5)  # [cout][cin]
+    b4 = torch.randn(64) * 0.1
+    x = _bf(preprocess_reference(imgs, out_hw, "caffe"))
+    pool = F.max_pool2d(_bf(F.relu(F.conv2d(x, k.permute(3, 2, 0, 1), b, stride=2, padding=3))), 3, 2, 1)
+    pool = _bf(pool).permute(0, 2, 3, 1)
+    zref = F.relu(pool @ k4.T + b4)
+    wp = torch.from_numpy(pack_conv_weight(pair_pack_kernel(k.numpy()), 8, 256, 256)).to(torch.bfloat16).cuda()
+    y, z = ops.resnet_stem(imgs.cuda(), wp, b.cuda(), out_hw, "caffe", w4=k4.to(torch.bfloat16).cuda(), b4=b4.cuda())
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu(), pool) < 1e-2
+    assert _rel(z.float().cpu(), zref) < 1e-2, _rel(z.float().cpu(), zref)
+
+
 def test_fused_stem_bad_shape_raises():
     wp = torch.zeros(64, 128, dtype=torch.bfloat16, device="cuda")  # ldw < 224
     with pytest.raises(Exception):
@@ -61,13 +82,20 @@ def test_fused_stem_bad_shape_raises():
                         torch.zeros(64, device="cuda"), (32, 32))
 
 
-def test_engine_fused_stem_equals_unfused():
+@pytest.mark.parametrize("fold", ["1", "0"])
+def test_engine_fused_stem_equals_unfused(fold, monkeypatch):
+    monkeypatch.setenv("DML_FOLD_STEM_1X1", fold)
     g, w = build_model("ResNet50", seed=7, calibrate=True)
     imgs = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda")
     ef = Engine(g, w, batch=2, reuse_buffers=False)
     eu = Engine(g, w, batch=2, fuse_stem=False, reuse_buffers=False)
-    assert ef.stem_pool is not None and eu.stem_pool is None
-    assert ef.op_names[0] == "preprocess+conv1_conv+pool1_pool" and len(ef.op_names) == len(eu.op_names) - 2
+    assert ef.stem_pool is not None and eu.stem_pool is None and eu.stem_1x1 is None
+    assert (ef.stem_1x1 is not None) == (fold == "1")
+    want = "preprocess+conv1_conv+pool1_pool" + ("+conv2_block1_1_conv" if fold == "1" else "")
+    assert ef.op_names[0] == want and len(ef.op_names) == len(eu.op_names) - 2 - (fold == "1")
+    if fold == "1":  # the folded conv's output never shares a buffer with the pooled tensor it reads
+        er = Engine(g, w, batch=2)
+        assert er.buf[er.stem_1x1.out].data_ptr() != er.buf[er.stem_pool.out].data_ptr()
     ef.infer(imgs)
     eu.infer(imgs)
     torch.cuda.synchronize()
@@ -76,6 +104,8 @@ def test_engine_fused_stem_equals_unfused():
     pf = ef.view(p.out)[..., p.out_coff:p.out_coff + 64].float()
     pu = eu.view(p.out)[..., p.out_coff:p.out_coff + 64].float()
     assert (pf - pu).abs().max().item() <= 1e-2 * pu.abs().max().item()
+    zf, zu = ef.view("conv2_block1_1").float(), eu.view("conv2_block1_1").float()
+    assert (zf - zu).abs().max().item() <= 1e-2 * zu.abs().max().item()
     assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 2e-2
 
 
@@ -209,13 +239,15 @@ def test_expand_reduce_matches_fp32(c, m):
     assert _rel(z.float().cpu(), z_ref) < 1e-2
 
 
-@pytest.mark.parametrize("maxc,chain,merged,pairs", [(256, "0", "0", 2), (256, "1", "0", 4), (256, "2", "0", 8),
-                                                     (1024, "0", "0", 8), (256, "1", "1", 4)])
+@pytest.mark.parametrize("maxc,chain,merged,pairs", [(256, "0", "0", 3), (256, "1", "0", 5), (256, "2", "0", 9),
+                                                     (1024, "0", "0", 9), (256, "1", "1", 5)])
 def test_engine_fused_blocks_equal_unfused(maxc, chain, merged, pairs, monkeypatch):
     """DML_CHAIN=1 (default) adds stage 3's boundaries (C = 512, chained kernel), 2 also stage 4's;
     DML_CHAIN_MERGED=1 routes stage 2's merged entry (K = 2F) to the chained kernel; stage 3's merged
     entry (conv3_block1_3 + _0) reads [x ; s] with K = F + 256 = 3F, which the chained kernel's
-    merged form (K = 2F) does not take, so it stays two launches."""
+    merged form (K = 2F) does not take, so it stays two launches. Stage 2's last expand
+    (conv2_block3_3, its shortcut stored compactly by the boundary before) is chained with stage
+    3's first reduce (256 -> 128) in every case (DML_CHAIN_STAGE_END, default on)."""
     monkeypatch.setenv("DML_FUSED_BLOCKS_MAXC", str(maxc))
     monkeypatch.setenv("DML_CHAIN", chain)
     monkeypatch.setenv("DML_CHAIN_MERGED", merged)
@@ -230,7 +262,9 @@ def test_engine_fused_blocks_equal_unfused(maxc, chain, merged, pairs, monkeypat
     # first expands of stages 3-5 and stage 5, C = 2048, are not fused)
     want = ["conv2_block1_3_conv+conv2_block1_0_conv"] + [
         f"conv{s}_block{k}_3_conv" for s, nb in ((2, 3), (3, 4), (4, 6)) for k in range(2, nb)]
-    assert sorted(ef.exp_red) == sorted(want[:pairs]) and not eu.exp_red
+    want = want[:pairs - 1] + ["conv2_block3_3_conv"]
+    assert sorted(ef.exp_red) == sorted(want) and not eu.exp_red
+    assert ef.exp_red["conv2_block3_3_conv"].name == "conv3_block1_1_conv"
     # the last fused boundary of each stage feeds only the stride-2 shortcut besides its reduce
     assert "conv2_block2_out" in ef.ysub and not eu.ysub
     assert len(ef.op_names) == len(eu.op_names) - pairs
@@ -245,8 +279,9 @@ def test_engine_fused_blocks_equal_unfused(maxc, chain, merged, pairs, monkeypat
     eu.infer(imgs)
     torch.cuda.synchronize()
     # (stage-final block outputs now live in the next stage's concat buffer, not under their own name)
-    for name in ("conv2_block1_out", "conv2_block2_1", "conv2_block2_out", "conv2_block3_1", "conv3_block2_1",
-                 "conv3_block3_out", "conv4_block2_1", "conv4_block6_1", "conv4_block5_out"):
+    for name in ("conv2_block1_out", "conv2_block2_1", "conv2_block2_out", "conv2_block3_1", "conv3_block1_1",
+                 "conv3_block1_2", "conv3_block2_1", "conv3_block3_out", "conv4_block2_1", "conv4_block6_1",
+                 "conv4_block5_out"):
         pf, pu = ef.view(name).float(), eu.view(name).float()
         if name in ef.ysub:  # stored compactly: only the pixels the stride-2 shortcut reads
             b, h, w, cb = pf.shape
@@ -360,3 +395,36 @@ def test_expand_reduce_chain_subsampled_y(c):
     assert _rel(y[:q].float().cpu(), want) < 1e-2
     assert (y[q:].float() == -7.0).all()
     assert _rel(z.float().cpu(), z_ref) < 1e-2
+
+
+@pytest.mark.parametrize("m", [128, 300, 2 * 28 * 28, 5 * 28 * 28 + 7])
+def test_expand_reduce_chain_stage_end(m):
+    """A stage's last boundary (chained kernel, fz = 2F): y = relu(x W3 + b3 + res) (64 -> 256)
+    stored into channels [128, 384) of a 384-wide concat buffer, z = relu(y W1 + b1) (256 -> 128)."""
+    torch.manual_seed(9)
+    f, c, fz, ldy, coff = 64, 256, 128, 384, 128
+    x = _bf(torch.randn(m, f).clamp(min=0))
+    res = _bf(torch.randn(m, c))
+    w3 = _bf(torch.randn(c, f) * (2.0 / f) ** 0.5)
+    b3 = torch.randn(c) * 0.1
+    w1 = _bf(torch.randn(fz, c) * (2.0 / c) ** 0.5)
+    b1 = torch.randn(fz) * 0.1
+    y_ref = _bf(F.relu(x @ w3.T + b3 + res))
+    z_ref = F.relu(y_ref @ w1.T + b1)
+    xd, rd = x.to(torch.bfloat16).cuda(), res.to(torch.bfloat16).cuda()
+    y = torch.full((m, ldy), -7.0, device="cuda", dtype=torch.bfloat16)
+    z = torch.empty((m, fz), device="cuda", dtype=torch.bfloat16)
+    w3d, w1d = w3.to(torch.bfloat16).cuda(), w1.to(torch.bfloat16).cuda()
+    b3d, b1d = b3.cuda(), b1.cuda()
+    a = N.ExpandReduceArgs(xd.data_ptr(), w3d.data_ptr(), b3d.data_ptr(), rd.data_ptr(), y.data_ptr() + 2 * coff,
+                           w1d.data_ptr(), b1d.data_ptr(), z.data_ptr(), m, f, f, c, ldy, c, fz, c, f)
+    a.fz = fz
+    assert N.lib().dml_chain_supported(C.byref(a)) == 1
+    N.check(N.lib().dml_expand_reduce(C.byref(a), N.stream_ptr()), "expand_reduce stage end")
+    torch.cuda.synchronize()
+    assert _rel(y[:, coff:].float().cpu(), y_ref) < 1e-2
+    assert (y[:, :coff].float() == -7.0).all()  # the other slice of the concat is untouched
+    assert _rel(z.float().cpu(), z_ref) < 1e-2
+    y2, z2 = ops.expand_reduce(xd, w3d, b3d, rd, w1d, b1d, fz=fz)  # the torch-facing wrapper
+    torch.cuda.synchronize()
+    assert _rel(y2.float().cpu(), y_ref) < 1e-2 and _rel(z2.float().cpu(), z_ref) < 1e-2
