@@ -127,7 +127,7 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
     import torch
 
     from distributed_machine_learning_amd.models import build_model
-    from distributed_machine_learning_amd.models.engine import Engine, SplitEngine
+    from distributed_machine_learning_amd.models.engine import Engine, SplitEngine, merge_point
     from distributed_machine_learning_amd.parallel.dataplane import DESC_FIELDS, DataPlane
     from distributed_machine_learning_amd.parallel.pipeline import ServingPipeline
     from distributed_machine_learning_amd.parallel.staging import PinnedImageStore
@@ -136,7 +136,8 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
     g, w = build_model(model, seed=0, calibrate=True)
     splits = args.splits if B % max(args.splits, 1) == 0 else 1
     if splits > 1:
-        eng = SplitEngine(g, w, batch=B, device=str(device), src_slots=2, splits=splits, streams=args.streams)
+        eng = SplitEngine(g, w, batch=B, device=str(device), src_slots=2, splits=splits, streams=args.streams,
+                          merge_at=merge_point(model) if splits == 2 else None)
     else:
         eng = Engine(g, w, batch=B, device=str(device), src_slots=2)
     store = PinnedImageStore(capacity=4 * B, hw=g.input_hw)
@@ -213,7 +214,8 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
             "config": {"model": model, "global_batch": B * world, "seq_len": None,
                        "image_hw": list(g.input_hw), "parallelism": f"dp{world}",
                        "per_worker_batch": B, "graph": not args.no_graph, "stream_splits": splits,
-                       "streams": eng.nstreams if splits > 1 else 1, "dispatch_lookahead": pipe.lookahead},
+                       "streams": eng.nstreams if splits > 1 else 1, "dispatch_lookahead": pipe.lookahead,
+                       "merged_tail_from": getattr(eng, "merge_at", None)},
             "baseline": {"source": "BASELINE.md scheduler-predicted query rate (cost model, CS425 VMs, TF CPU)",
                          "value": round(ref_rate(model, world), 3), "unit": "images/s"},
         }

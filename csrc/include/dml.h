@@ -143,6 +143,14 @@ typedef struct {
   int c4, ldw4;
 } DmlConvPoolArgs;
 
+// Max pool 3x3/2 (valid) + the 1x1 GEMM that is the pooled tensor's only reader, ONE kernel
+// (csrc/kernels/pool_gemm.hip; InceptionV3 max_pooling2d_2 -> mixed0's sibling 1x1 GEMM). p: the
+// pool (its y is never written); g: the 1x1 conv over the pooled grid (g.x unused; segments ok).
+typedef struct {
+  DmlConvArgs g;
+  DmlPoolArgs p;
+} DmlPoolGemmArgs;
+
 // Fused ResNet50 block boundary (csrc/kernels/bottleneck_fused.hip), F = C / 4:
 //   y = relu(w3 . x + b3 + res)  (1x1 expand F -> C + shortcut)
 //   z = relu(w1 . y + b1)        (next block's 1x1 reduce C -> F)
@@ -195,6 +203,8 @@ int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s);
 // chained-GEMM block boundary, F = 128 / C = 512 (expand_reduce_chain.hip); dml_expand_reduce routes to it
 int dml_chain(const DmlExpandReduceArgs* a, hipStream_t s);
 int dml_chain_supported(const DmlExpandReduceArgs* a);
+int dml_pool_gemm(const DmlPoolGemmArgs* a, hipStream_t s);
+int dml_pool_gemm_supported(const DmlPoolGemmArgs* a);
 int dml_chain_init(void);
 int dml_expand_reduce_init(void);
 int dml_block_fused(const DmlBlockArgs* a, hipStream_t s);
@@ -242,6 +252,7 @@ int dml_plan_add_stem(void* plan, const DmlStemArgs* a);
 int dml_plan_add_inc_stem(void* plan, const DmlIncStemArgs* a);
 int dml_plan_add_conv_pool(void* plan, const DmlConvPoolArgs* a);
 int dml_plan_add_expand_reduce(void* plan, const DmlExpandReduceArgs* a);
+int dml_plan_add_pool_gemm(void* plan, const DmlPoolGemmArgs* a);
 int dml_plan_add_block(void* plan, const DmlBlockArgs* a);
 int dml_plan_size(void* plan);
 int dml_plan_run(void* plan, hipStream_t s);

@@ -46,7 +46,7 @@ extern "C" int dml_abi_sizes(int* out, int n) {
   const int sz[] = {(int)sizeof(DmlConvArgs), (int)sizeof(DmlPoolArgs), (int)sizeof(DmlConvGroupArgs),
                     (int)sizeof(DmlPreprocArgs), (int)sizeof(DmlStemArgs), (int)sizeof(DmlIncStemArgs),
                     (int)sizeof(DmlConvPoolArgs), (int)sizeof(DmlExpandReduceArgs),
-                    (int)sizeof(DmlBlockArgs)};
+                    (int)sizeof(DmlBlockArgs), (int)sizeof(DmlPoolGemmArgs)};
   const int m = (int)(sizeof(sz) / sizeof(sz[0]));
   for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
   return m;
@@ -55,7 +55,7 @@ extern "C" int dml_abi_sizes(int* out, int n) {
 // ----------------------------------------------------------------- plan ----
 namespace {
 enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM, OP_INC_STEM, OP_CONV_POOL, OP_EXP_RED,
-              OP_CONV_GROUP, OP_BLOCK };
+              OP_CONV_GROUP, OP_BLOCK, OP_POOL_GEMM };
 struct GapArgs { const void* x; void* y; int N, HW, C, ldx; };
 struct SmArgs { float* logits; int B, classes, ld, nsplit, split_ld; float* probs; int* idx; float* p; };
 struct Op {
@@ -72,6 +72,7 @@ struct Op {
   DmlExpandReduceArgs er;
   DmlBlockArgs blk;
   DmlConvGroupArgs grp;
+  DmlPoolGemmArgs pg;
 };
 struct Plan {
   std::vector<Op> ops;
@@ -107,6 +108,7 @@ int run_op(const Op& o, hipStream_t s) {
     case OP_EXP_RED: return dml_expand_reduce(&o.er, s);
     case OP_CONV_GROUP: return dml_conv_group(&o.grp, o.cfg, s);
     case OP_BLOCK: return dml_block_fused(&o.blk, s);
+    case OP_POOL_GEMM: return dml_pool_gemm(&o.pg, s);
   }
   return -1;
 }
@@ -188,6 +190,15 @@ extern "C" int dml_plan_add_conv_group(void* p, const DmlConvGroupArgs* g, int c
   ((Plan*)p)->ops.push_back(o);
   return cfg;
 }
+extern "C" int dml_plan_add_pool_gemm(void* p, const DmlPoolGemmArgs* a) {
+  if (!dml_pool_gemm_supported(a)) return -1;  // the error names the unsupported field
+  Op o{};
+  o.kind = OP_POOL_GEMM;
+  o.pg = *a;
+  ((Plan*)p)->ops.push_back(o);
+  return 0;
+}
+
 extern "C" int dml_plan_add_expand_reduce(void* p, const DmlExpandReduceArgs* a) {
   Op o{};
   o.kind = OP_EXP_RED;

@@ -207,6 +207,29 @@ int main() {
   er.ldz = 64;
   CHECK(dml_chain_supported(&er) == 0);            // Z rows narrower than the reduce width
   er.fz = 0; er.ldz = 64; er.res = nullptr;
+  {  // max pool 3x3/2 + 1x1 GEMM: shape gate names what it refuses, the plan refuses it too
+    DmlPoolGemmArgs pg{};
+    pg.p.N = 2; pg.p.H = 71; pg.p.W = 71; pg.p.C = 192; pg.p.ldx = 192; pg.p.Ho = 35; pg.p.Wo = 35;
+    pg.p.k = 3; pg.p.stride = 2;
+    pg.g.N = 2; pg.g.H = 35; pg.g.W = 35; pg.g.Ho = 35; pg.g.Wo = 35; pg.g.Cin = 192; pg.g.kh = pg.g.kw = 1;
+    pg.g.sh = pg.g.sw = 1; pg.g.Cout = 208; pg.g.Kpad = 192; pg.g.ldy = 208; pg.g.y = (void*)&pg;
+    CHECK(dml_pool_gemm_supported(&pg) == 1);
+    pg.p.pad = 1;
+    CHECK(dml_pool_gemm_supported(&pg) == 0);
+    CHECK(std::string(dml_last_error()).find("max 3x3/2") != std::string::npos);
+    pg.p.pad = 0; pg.g.Cout = 200;                    // not a multiple of 16
+    CHECK(dml_pool_gemm_supported(&pg) == 0);
+    pg.g.Cout = 208; pg.g.nseg = 2; pg.g.seg_c0[1] = 72; pg.g.seg_ldy[0] = pg.g.seg_ldy[1] = 208;
+    pg.g.seg_y[0] = pg.g.seg_y[1] = (void*)&pg;
+    CHECK(dml_pool_gemm_supported(&pg) == 0);          // segment boundary off the 16-channel grid
+    pg.g.seg_c0[1] = 64;
+    CHECK(dml_pool_gemm_supported(&pg) == 1);
+    void* plan = dml_plan_create();
+    pg.g.Cin = 128;                                     // not the pooled tensor
+    CHECK(dml_plan_add_pool_gemm(plan, &pg) != 0);
+    CHECK(dml_plan_size(plan) == 0);
+    dml_plan_destroy(plan);
+  }
   {  // whole fused bottleneck block: only F = 64, C = 4F, 8-aligned strides, y != x
     DmlBlockArgs b{};
     char buf[64];

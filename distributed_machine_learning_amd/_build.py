@@ -28,6 +28,7 @@ SOURCES = [
     CSRC / "kernels" / "misc.hip",
     CSRC / "kernels" / "stem_fused.hip",
     CSRC / "kernels" / "conv_pool.hip",
+    CSRC / "kernels" / "pool_gemm.hip",
     CSRC / "kernels" / "bottleneck_fused.hip",
     CSRC / "kernels" / "block_fused.hip",
     CSRC / "kernels" / "conv_shift.hip",

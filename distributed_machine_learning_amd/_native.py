@@ -108,7 +108,14 @@ class BlockArgs(C.Structure):
     ]
 
 
+class PoolGemmArgs(C.Structure):
+    _fields_ = [("g", ConvArgs), ("p", PoolArgs)]
+
+
 _SIGS = {
+    "dml_pool_gemm": (C.c_int, [C.POINTER(PoolGemmArgs), C.c_void_p]),
+    "dml_pool_gemm_supported": (C.c_int, [C.POINTER(PoolGemmArgs)]),
+    "dml_plan_add_pool_gemm": (C.c_int, [C.c_void_p, C.POINTER(PoolGemmArgs)]),
     "dml_block_fused": (C.c_int, [C.POINTER(BlockArgs), C.c_void_p]),
     "dml_plan_add_block": (C.c_int, [C.c_void_p, C.POINTER(BlockArgs)]),
     "dml_expand_reduce": (C.c_int, [C.POINTER(ExpandReduceArgs), C.c_void_p]),
@@ -175,7 +182,7 @@ class NativeError(RuntimeError):
 
 
 ABI_STRUCTS = ("ConvArgs", "PoolArgs", "ConvGroupArgs", "PreprocArgs", "StemArgs", "IncStemArgs", "ConvPoolArgs",
-               "ExpandReduceArgs", "BlockArgs")
+               "ExpandReduceArgs", "BlockArgs", "PoolGemmArgs")
 
 
 def _check_abi(L) -> None:

@@ -60,7 +60,9 @@ class Engine:
                  src_slots: int = 1, reuse_buffers: bool = True, autotune: bool = True, optimize: bool = True,
                  share: Optional["Engine"] = None, src_tensors: Optional[List[torch.Tensor]] = None,
                  result_views: Optional[List[torch.Tensor]] = None, fuse_stem: bool = True,
-                 fuse_blocks: bool = True, conv_groups: Optional[bool] = None):
+                 fuse_blocks: bool = True, conv_groups: Optional[bool] = None,
+                 ext_buffers: Optional[Dict[str, List[torch.Tensor]]] = None,
+                 tune_range: Optional[Tuple[Optional[str], Optional[str]]] = None):
         """``share``: reuse another engine's (optimized) graph and resident weights
         (sub-batch engines of a SplitEngine); ``src_tensors`` / ``result_views``:
         external uint8 source slots / per-slot [2, batch, 5] result rows to use
@@ -68,7 +70,13 @@ class Engine:
         ResNet stem as three launches (preprocess, conv, pool); ``fuse_blocks=False``
         (or DML_FUSED_BLOCKS=0) keeps every bottleneck 1x1 conv its own launch;
         ``conv_groups=False`` (or DML_CONV_GROUPS=0) launches InceptionV3's
-        independent branch convs one by one instead of as grouped grids."""
+        independent branch convs one by one instead of as grouped grids.
+        ``ext_buffers``: {tensor: [flat bf16 storage per source slot]} — tensors this engine
+        reads / writes in caller-owned memory instead of its own buffers (the merge tensors of
+        a split-head / merged-tail SplitEngine: each head writes its rows of the tail's
+        buffer), never recycled for another tensor. ``tune_range``: (first node, stop node) names
+        (None = graph start / end): only those convs are autotuned (the part of the graph this
+        engine will run); the others get the default tile."""
         if conv_groups is None:
             conv_groups = os.environ.get("DML_CONV_GROUPS", "1") != "0"
         if share is not None:
@@ -111,6 +119,8 @@ class Engine:
         # with the 1x1 conv that is the pool's only reader folded in (InceptionV3 conv2d_4)
         self.conv_pools = self._fusable_conv_pools(fuse_stem)
         self.conv_pool_1x1 = self._foldable_pool_1x1(fuse_stem)
+        # a max pool 3x3/2 whose only reader is the next 1x1 GEMM -> ONE kernel (csrc/kernels/pool_gemm.hip)
+        self.pool_gemm = self._fusable_pool_gemm(fuse_stem)
         # ResNet stage-2 block boundaries: expand (64 -> 256, + shortcut) and the next
         # block's reduce (256 -> 64) as ONE kernel (csrc/kernels/bottleneck_fused.hip)
         # whole identity bottleneck blocks (reduce -> 3x3 -> expand + shortcut) as ONE
@@ -125,6 +135,9 @@ class Engine:
         # independent residual-free convs of one graph level -> one grouped grid each
         self.conv_groups = self._conv_group_candidates() if conv_groups else []
         self._src_tensors, self._result_views = src_tensors, result_views
+        self._ext = ext_buffers or {}
+        self._tune_range = tune_range
+        self.op_range: Optional[Tuple[int, int]] = None
         if share is not None:
             self.wdev = share.wdev
         else:
@@ -244,6 +257,34 @@ class Engine:
                 p = users[0]
                 if (p.mode, p.k, p.stride, p.pad, p.out_coff, p.relu) == ("max", 3, 2, 0, 0, False):
                     out[c.name] = p
+        return out
+
+    def _fusable_pool_gemm(self, enabled: bool) -> Dict[str, object]:
+        """{pool name: 1x1 conv} for a max pool 3x3/2 (valid) whose output is read only by the
+        next node, a 1x1 stride-1 conv or sibling-fused 1x1 GEMM (InceptionV3 max_pooling2d_2 ->
+        conv2d_6+conv2d_7+conv2d_9+conv2d_12): the pooled tile goes from LDS straight into the GEMM
+        and the pooled tensor is never written. DML_POOL_GEMM=0: off (A/B)."""
+        if not enabled or self.device.type != "cuda" or os.environ.get("DML_POOL_GEMM", "1") == "0":
+            return {}
+        out: Dict[str, object] = {}
+        nodes = self.g.nodes
+        taken = set(self.conv_pools) | {p.name for p in self.conv_pools.values()}
+        for p, k in zip(nodes, nodes[1:]):
+            if not isinstance(p, Pool) or p.name in taken:
+                continue
+            if (p.mode, p.k, p.stride, p.pad, p.relu, p.out_coff) != ("max", 3, 2, 0, False, 0):
+                continue
+            users = [n for n in nodes if p.out in (getattr(n, "inp", None), getattr(n, "residual", None))]
+            if users != [k] or not isinstance(k, (Conv, FusedConv)) or k.inp != p.out:
+                continue
+            m0 = k.members[0] if isinstance(k, FusedConv) else k
+            if not (m0.kh == m0.kw == 1 and m0.sh == m0.sw == 1 and (getattr(k, "in_coff", 0) or 0) == 0
+                    and getattr(k, "residual", None) is None and not getattr(k, "out_f32", False)
+                    and k.cout % 16 == 0 and k.cout <= 256 and self.g.shape(p.out)[2] % 32 == 0):
+                continue
+            if isinstance(k, FusedConv) and any(m.cout % 16 for m in k.members):
+                continue
+            out[p.name] = k
         return out
 
     def _foldable_pool_1x1(self, enabled: bool) -> Dict[str, Conv]:
@@ -379,6 +420,7 @@ class Engine:
         taken = {t.name for t in (self.stem, self.stem_conv2, self.stem_pool, self.stem_1x1) if t is not None}
         taken |= set(self.conv_pools) | {p.name for p in self.conv_pools.values()}
         taken |= {k.name for k in self.conv_pool_1x1.values()}
+        taken |= set(self.pool_gemm) | {k.name for k in self.pool_gemm.values()}
         taken |= set(self.exp_red) | {r.name for r in self.exp_red.values()}
         taken |= {t.name for trip in self.blocks.values() for t in trip}
         return conv_group_runs(self.g, taken, N.GROUP_MAX, N.GROUP_POOL_MAX)
@@ -432,7 +474,7 @@ class Engine:
         # position: the first node's inputs stay live through the second node, so
         # the second's output can never be handed a buffer the kernel still reads.
         index = {getattr(n, "name", None): i for i, n in enumerate(nodes)}
-        pairs = {**self.conv_pools, **self.exp_red}
+        pairs = {**self.conv_pools, **self.exp_red, **self.pool_gemm}
         for c_name, k in self.conv_pool_1x1.items():  # conv + pool + folded 1x1 end at the 1x1
             pairs[c_name] = k
             first_def[k.out] = min(first_def[k.out], index[c_name])
@@ -466,6 +508,8 @@ class Engine:
         for step in range(-1, len(nodes) + 1):
             # tensors whose last use was before this step can be recycled
             for name in pending_release if self.reuse_buffers else []:
+                if name in self._ext:  # caller-owned storage is never recycled
+                    continue
                 t = self.buf[name]
                 free.setdefault(t.numel(), []).append(t)
             pending_release = release_at.get(step, [])
@@ -481,6 +525,10 @@ class Engine:
                     self.logit_parts = torch.empty((self.fc_ksplit, B, t.c), device=self.device,
                                                    dtype=torch.float32)
                     self.buf[name] = self.logit_parts[0]
+                    continue
+                if name in self._ext:
+                    assert all(t.numel() == numel and t.dtype == torch.bfloat16 for t in self._ext[name]), name
+                    self.buf[name] = self._ext[name][0]
                     continue
                 lst = free.get(numel)
                 buf = lst.pop() if lst else torch.empty(numel, device=self.device, dtype=torch.bfloat16)
@@ -527,8 +575,14 @@ class Engine:
         from ..ops import tuning
 
         self.tuned: Dict[str, int] = {}
+        lo, hi = 0, len(self.g.nodes)
+        if self._tune_range is not None:
+            idx = {n.name: i for i, n in enumerate(self.g.nodes)}
+            lo = idx[self._tune_range[0]] if self._tune_range[0] else 0
+            hi = idx[self._tune_range[1]] if self._tune_range[1] else len(self.g.nodes)
+        active = {n.name for n in self.g.nodes[lo:hi]}
         if self.autotune and self.device.type == "cuda":
-            cnodes = [n for n in self.g.nodes if isinstance(n, (Conv, Dense, FusedConv))]
+            cnodes = [n for n in self.g.nodes if isinstance(n, (Conv, Dense, FusedConv)) and n.name in active]
             convs = [self._conv_args(n) for n in cnodes]
             table = tuning.autotune(convs)
             for n, a in zip(cnodes, convs):
@@ -544,7 +598,7 @@ class Engine:
             cfgs = [self.cfg_overrides.get(m.name, self.tuned.get(m.name, -1)) for m in convs]
             if any(m.name in self.cfg_overrides for m in grp):
                 cfg = -1
-            elif self.autotune and self.device.type == "cuda":
+            elif self.autotune and self.device.type == "cuda" and grp[0].name in active:
                 cfg = tuning.autotune_group(args, cfgs, pools)
             else:
                 big = max(range(len(args)), key=lambda i: args[i].N * args[i].Ho * args[i].Wo * args[i].Cout
@@ -553,7 +607,13 @@ class Engine:
                 cfg = c if c in tuning.GROUP_CFGS else -1
             if cfg >= 0:
                 self.group_cfg[grp[0].name] = cfg
-        self.plans = [self._build_one_plan(self.srcs[i], self.results[i]) for i in range(self.src_slots)]
+        self.plans = []
+        for i in range(self.src_slots):
+            for name, ts in self._ext.items():
+                self.buf[name] = ts[i]
+            self.plans.append(self._build_one_plan(self.srcs[i], self.results[i]))
+        for name, ts in self._ext.items():
+            self.buf[name] = ts[0]
         self.plan = self.plans[0]
         self.graph_captured = [False] * self.src_slots
 
@@ -602,6 +662,7 @@ class Engine:
         skip |= {p.name for p in self.conv_pools.values()}
         skip |= {k.name for k in self.conv_pool_1x1.values()}
         skip |= {r.name for r in self.exp_red.values()}
+        skip |= {k.name for k in self.pool_gemm.values()}
         skip |= {t.name for (_, c, e) in self.blocks.values() for t in (c, e)}
         groups = {grp[0].name: grp for grp in self.conv_groups if grp[0].name in self.group_cfg}
         for grp in groups.values():
@@ -656,6 +717,14 @@ class Engine:
                     ea.ysub, ea.yH, ea.yW = self.ysub[n.out], h, w
                 N.check(L.dml_plan_add_expand_reduce(plan, C.byref(ea)), "plan expand+reduce")
                 self.op_names.append(f"{n.name}+{r.name}")
+                continue
+            if n.name in self.pool_gemm:
+                k = self.pool_gemm[n.name]
+                pg = N.PoolGemmArgs(self._conv_args(k), self._pool_args(n))
+                N.check(L.dml_plan_add_pool_gemm(plan, C.byref(pg)), f"plan pool+gemm {n.name}")
+                self._keep.append(pg)
+                self.op_cfg[k.name] = -1
+                self.op_names.append(f"{n.name}+{k.name}")
                 continue
             if n.name in self.conv_pools:
                 p = self.conv_pools[n.name]
@@ -748,10 +817,42 @@ class Engine:
         return a
 
     # ---------------------------------------------------------------- run ----
+    def op_node_span(self, i: int) -> Tuple[int, int]:
+        """(first, last) graph-node index that op ``i`` of the plan covers (op names join the
+        covered nodes' names with '+' / '|'; 'preprocess' covers node 0)."""
+        index: Dict[str, int] = {}
+        for k, n in enumerate(self.g.nodes):
+            index[n.name] = k
+            for m in getattr(n, "members", []):
+                index[m.name] = k
+        name = self.op_names[i]
+        if name in index:
+            return index[name], index[name]
+        ks = [index[x] for x in name.replace("|", "+").split("+") if x in index] or [0]
+        return min(ks), max(ks)
+
+    def set_op_range(self, begin: int, end: int) -> None:
+        """From now on ``run`` executes only plan ops [begin, end) (split-head / merged-tail
+        serving: the heads stop at the merge point, the tail starts there)."""
+        if not (0 <= begin <= end <= len(self.op_names)):
+            raise ValueError(f"bad op range {begin}..{end} of {len(self.op_names)}")
+        self.op_range = (begin, end)
+        self.graph_captured = [False] * self.src_slots
+
     def run(self, stream=None, use_graph: bool = False, slot: int = 0) -> None:
         s = N.stream_ptr(stream)
         plan = self.plans[slot]
         self._select_result(slot)
+        if self.op_range is not None:
+            b, e = self.op_range
+            if use_graph:
+                if not self.graph_captured[slot]:
+                    self.capture_parts([b, e], stream, slot)
+                    self.graph_captured[slot] = True
+                N.check(self.lib.dml_plan_replay_part(plan, 0, s), "plan replay_part")
+            else:
+                N.check(self.lib.dml_plan_run_range(plan, b, e, s), "plan run_range")
+            return
         if use_graph:
             if not self.graph_captured[slot]:
                 N.check(self.lib.dml_plan_capture(plan, s), "plan capture")
@@ -775,7 +876,10 @@ class Engine:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         for slot in range(self.src_slots):
             if not self.graph_captured[slot]:
-                N.check(self.lib.dml_plan_capture(self.plans[slot], N.stream_ptr(s)), "plan capture")
+                if self.op_range is not None:
+                    self.capture_parts(list(self.op_range), s, slot)
+                else:
+                    N.check(self.lib.dml_plan_capture(self.plans[slot], N.stream_ptr(s)), "plan capture")
                 self.graph_captured[slot] = True
         torch.cuda.synchronize(self.device)
 
@@ -816,6 +920,25 @@ class Engine:
             pass
 
 
+# Split-head / merged-tail serving (SplitEngine(merge_at=...)): the first node of the full-batch
+# tail per model (None: two half-batch engines end to end). DML_MERGE_AT overrides it:
+# "InceptionV3=<node>,ResNet50=<node>" (a model left out keeps its default), "0" = off for all.
+MERGE_AT: Dict[str, Optional[str]] = {"ResNet50": None, "InceptionV3": None}
+
+
+def merge_point(model: str) -> Optional[str]:
+    env = os.environ.get("DML_MERGE_AT")
+    if env is None:
+        return MERGE_AT.get(model)
+    if env.strip() in ("", "0"):
+        return None
+    for item in env.split(","):
+        k, _, v = item.partition("=")
+        if k.strip() == model:
+            return v.strip() or None
+    return MERGE_AT.get(model)
+
+
 class SplitEngine:
     """The per-worker batch served as ``splits`` sub-batches, each its own
     Engine (own activations, own hipGraph) on its own HIP stream, all sharing
@@ -827,11 +950,16 @@ class SplitEngine:
     the serving pipeline: srcs, result, batch, src_slots, device, run."""
 
     def __init__(self, graph: Graph, weights: Weights, batch: int, device: str = "cuda", splits: int = 2,
-                 src_slots: int = 1, src_hw: Optional[Tuple[int, int]] = None, streams: int = 0, **kw):
+                 src_slots: int = 1, src_hw: Optional[Tuple[int, int]] = None, streams: int = 0,
+                 merge_at: Optional[str] = None, **kw):
         """``streams``: concurrent streams (default = splits); sub-batch i runs on
         stream i % streams, so splits=4, streams=2 runs two half-size sub-batches
         back to back on each of two streams (smaller per-layer working sets that
-        stay in the 256 MiB Infinity Cache between producer and consumer)."""
+        stay in the 256 MiB Infinity Cache between producer and consumer).
+        ``merge_at`` (a node name of the optimized graph; splits = 2): split head, merged
+        tail — the two half-batch engines run the graph up to that node on two streams and
+        ONE full-batch engine runs the rest (the late, small-grid layers at twice the grid),
+        see ``_init_merged``."""
         if batch % splits:
             raise ValueError(f"batch {batch} not divisible by splits {splits}")
         sub = batch // splits
@@ -845,6 +973,10 @@ class SplitEngine:
         self.results = [torch.zeros((2, batch, 5), device=self.device, dtype=torch.int32)
                         for _ in range(src_slots)]
         self._select_result(0)
+        self.tails: List[Engine] = []
+        if merge_at:
+            self._init_merged(graph, weights, hw, merge_at, kw)
+            return
         self.engines: List[Engine] = []
         for i in range(splits):
             rows = slice(i * sub, (i + 1) * sub)
@@ -861,6 +993,82 @@ class SplitEngine:
         self._fork = torch.cuda.Event()
         self._join = [torch.cuda.Event() for _ in range(self.nstreams - 1)]
 
+    def _init_merged(self, graph: Graph, weights: Weights, hw, merge_at: str, kw) -> None:
+        """Split head, merged tail. Two half-batch HEAD engines run ops up to ``merge_at`` (the
+        first tail node), one on the caller's stream and one on the extra stream; a full-batch
+        TAIL engine runs the rest on the caller's stream. Every tensor live across the cut (the
+        merge tensors) is stored in the tail's buffers: head i writes rows [i*B/2, (i+1)*B/2) of
+        them (``Engine(ext_buffers=...)``). There is one tail engine per source slot, so the
+        extra stream can run the head of batch k+1 while the caller's stream still runs the
+        tail of batch k (the merge tensors are double-buffered; a head waits only for the tail
+        two batches back). Motivation (InceptionV3, serial per-op times, profiles/r3_v7): the
+        17x17 / 8x8 layers take 1454 us at 128 images vs 2 x 936 us at 64 — their grids are a
+        few hundred tiles for 256 CUs, so a 128-image grid costs 1.55x, not 2x, a 64-image one."""
+        if self.splits != 2:
+            raise ValueError("merge_at needs splits = 2")
+        B, sub = self.batch, self.batch // 2
+        for s in range(self.src_slots):
+            self.tails.append(Engine(graph, weights if s == 0 else None, batch=B, device=str(self.device),
+                                     src_slots=1, src_hw=hw, share=self.tails[0] if s else None,
+                                     src_tensors=[self.srcs[s]], result_views=[self.results[s]],
+                                     tune_range=(merge_at, None), **kw))
+        t0 = self.tails[0]
+        g = t0.g
+        names = [n.name for n in g.nodes]
+        if merge_at not in names:
+            raise ValueError(f"merge_at: no node {merge_at!r} in the optimized graph")
+        cut = names.index(merge_at)
+        self.merge_tensors = self.live_across(g, cut)
+
+        def rows(t: Engine, name: str, i: int) -> torch.Tensor:
+            per = t.buf[name].numel() // B
+            return t.buf[name][i * sub * per:(i + 1) * sub * per]
+
+        self.engines = []
+        for i in range(2):
+            ext = {name: [rows(self.tails[s], name, i) for s in range(self.src_slots)] for name in self.merge_tensors}
+            self.engines.append(Engine(graph, None, batch=sub, device=str(self.device), src_slots=self.src_slots,
+                                       src_hw=hw, share=t0, src_tensors=[t[i * sub:(i + 1) * sub] for t in self.srcs],
+                                       result_views=[r[:, i * sub:(i + 1) * sub] for r in self.results],
+                                       ext_buffers=ext, tune_range=(None, merge_at), **kw))
+        for e in self.engines:
+            e.set_op_range(0, self._op_cut(e, cut))
+        for t in self.tails:
+            t.set_op_range(self._op_cut(t, cut), len(t.op_names))
+        self.g = g
+        self.merge_at = merge_at
+        self.streams = [torch.cuda.Stream(self.device)]
+        self._fork = torch.cuda.Event()
+        self._join = [torch.cuda.Event()]
+        self._head_done = torch.cuda.Event()
+        self._tail_done = [torch.cuda.Event() for _ in range(self.src_slots)]
+        cur = torch.cuda.current_stream(self.device)
+        for ev in self._tail_done:  # recorded once, so the first waits are well defined
+            ev.record(cur)
+
+    @staticmethod
+    def live_across(g: Graph, cut: int) -> List[str]:
+        """Tensors written before node ``cut`` and read at or after it."""
+        first_def: Dict[str, int] = {}
+        last_use: Dict[str, int] = {}
+        for i, n in enumerate(g.nodes):
+            for o in node_outputs(n):
+                first_def.setdefault(o, i)
+            for src in (getattr(n, "inp", None), getattr(n, "residual", None)):
+                if src:
+                    last_use[src] = i
+        return sorted(t for t, d in first_def.items() if d < cut and last_use.get(t, -1) >= cut)
+
+    @staticmethod
+    def _op_cut(e: "Engine", cut: int) -> int:
+        """Index of the first op of ``e`` at or after graph node ``cut``; no op may straddle it."""
+        spans = [e.op_node_span(i) for i in range(len(e.op_names))]
+        p = next((i for i, (lo, _) in enumerate(spans) if lo >= cut), len(spans))
+        bad = [e.op_names[i] for i in range(len(spans)) if (i < p and spans[i][1] >= cut) or (i >= p and spans[i][0] < cut)]
+        if bad:
+            raise ValueError(f"merge point inside fused ops {bad}")
+        return p
+
     @property
     def op_cfg(self) -> Dict[str, int]:
         return self.engines[0].op_cfg
@@ -872,6 +1080,8 @@ class SplitEngine:
         lanes = [main] + self.streams
         for i, e in enumerate(self.engines):
             e.capture(lanes[i % self.nstreams])
+        for t in self.tails:
+            t.capture(main)
 
     def _select_result(self, slot: int) -> None:
         self.result = self.results[slot]
@@ -892,6 +1102,9 @@ class SplitEngine:
         self._select_result(slot)
         for e in self.engines:
             e._select_result(slot)
+        if self.tails:
+            self._run_merged(main, use_graph, slot, deps)
+            return
         lanes = [main] + self.streams
         if deps is None:
             self._fork.record(main)
@@ -907,6 +1120,23 @@ class SplitEngine:
         for s, ev in zip(self.streams, self._join):
             ev.record(s)
             main.wait_event(ev)
+
+    def _run_merged(self, main, use_graph: bool, slot: int, deps) -> None:
+        """Head 1 on the extra stream (after its inputs and the tail that last read this slot's
+        merge tensors), head 0 then the merged tail on the caller's stream."""
+        x = self.streams[0]
+        if deps is None:
+            self._fork.record(main)
+            deps = [self._fork]
+        for ev in deps:
+            x.wait_event(ev)
+        x.wait_event(self._tail_done[slot])
+        self.engines[1].run(x, use_graph=use_graph, slot=slot)
+        self._head_done.record(x)
+        self.engines[0].run(main, use_graph=use_graph, slot=slot)
+        main.wait_event(self._head_done)
+        self.tails[slot].run(main, use_graph=use_graph, slot=0)
+        self._tail_done[slot].record(main)
 
     def infer(self, images_u8: torch.Tensor, stream=None):
         self.src.copy_(images_u8, non_blocking=True)

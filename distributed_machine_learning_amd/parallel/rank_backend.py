@@ -226,7 +226,7 @@ class GpuRankBackend(RankBackend):
         from concurrent.futures import ThreadPoolExecutor
 
         from ..models import build_model
-        from ..models.engine import Engine, SplitEngine
+        from ..models.engine import Engine, SplitEngine, merge_point
         from .image_store import HbmImageStore
 
         self.device = device
@@ -239,7 +239,8 @@ class GpuRankBackend(RankBackend):
             g, w = build_model(m, seed=seed, calibrate=True)
             b = batch_sizes[m]
             if splits > 1 and b % splits == 0:
-                self.engines[m] = SplitEngine(g, w, batch=b, device=str(device), src_slots=SLOTS, splits=splits)
+                self.engines[m] = SplitEngine(g, w, batch=b, device=str(device), src_slots=SLOTS, splits=splits,
+                                              merge_at=merge_point(m) if splits == 2 else None)
             else:
                 self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=SLOTS)
             self.arenas[m] = HbmImageStore(max(arena_images, n_synth + 2 * self.cap), g.input_hw, device,

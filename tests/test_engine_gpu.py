@@ -209,6 +209,54 @@ def test_split_engine_matches_engine(use_graph):
     assert torch.equal(se.result, torch.cat(ref, dim=1))
 
 
+@pytest.mark.parametrize("model,merge_at,want", [
+    ("InceptionV3", "conv2d_31+conv2d_32+conv2d_35+conv2d_40", ["mixed3"]),
+    ("ResNet50", "conv4_block1_1_conv", ["conv4_block1_2"]),  # a [x ; s] concat written on both sides
+])
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_split_engine_merged_tail(model, merge_at, want, use_graph):
+    """Split head / merged tail (SplitEngine(merge_at=...)): two half-batch heads on two streams
+    write the merge tensor into the slot's full-batch tail engine, which runs the rest. Two
+    batches on the two source slots are enqueued back to back (the head of batch 2 may run on the
+    extra stream under the tail of batch 1), then checked against a plain full-batch Engine:
+    same top-5 rows, logits within bf16 accumulation-order noise."""
+    from distributed_machine_learning_amd.models.engine import SplitEngine
+    from distributed_machine_learning_amd.models.oracle import synthetic_images
+
+    g, w = build_model(model, seed=2, calibrate=True)
+    B = 8
+    se = SplitEngine(g, w, batch=B, splits=2, src_slots=2, merge_at=merge_at)
+    assert se.merge_tensors == want and len(se.tails) == 2
+    assert se.engines[0].wdev is se.tails[0].wdev and se.tails[1].wdev is se.tails[0].wdev
+    for e in se.engines:  # the heads' merge tensors are rows of the tails' buffers
+        for s_, t in enumerate(se.tails):
+            assert e._ext[want[0]][s_].data_ptr() in (t.buf[want[0]].data_ptr(),
+                                                      t.buf[want[0]].data_ptr() + t.buf[want[0]].numel())
+    ref = Engine(g, w, batch=B)
+    imgs = [synthetic_images(B, g.input_hw, seed=10 + k).cuda() for k in range(4)]
+    main = torch.cuda.Stream()
+    se.capture(main)
+    for pair in range(2):
+        for slot in range(2):
+            se.srcs[slot].copy_(imgs[2 * pair + slot])
+        main.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(main):
+            for slot in range(2):
+                se.run(main, use_graph=use_graph, slot=slot)
+        main.synchronize()
+        for slot in range(2):
+            ref.infer(imgs[2 * pair + slot])
+            torch.cuda.synchronize()
+            got, exp = se.results[slot][0].cpu(), ref.result[0].cpu()
+            top1 = (got[:, 0] == exp[:, 0]).float().mean().item()
+            ov = sum(len(set(a.tolist()) & set(b.tolist())) for a, b in zip(got, exp)) / B
+            assert top1 >= 0.85 and ov >= 4.0, (slot, top1, ov)
+            lt = se.tails[slot].buf[g.logits].float().cpu()
+            lr = ref.buf[g.logits].float().cpu()
+            lt, lr = lt - lt.mean(0), lr - lr.mean(0)
+            assert _rel(lt, lr) < 3e-2, _rel(lt, lr)
+
+
 def test_capture_parts_matches_full_graph():
     """Forward captured as 3 op-range graphs (dml_plan_capture_parts) == one full graph."""
     g, w = build_model("ResNet50", seed=4, calibrate=False)

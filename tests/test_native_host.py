@@ -15,7 +15,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = shutil.which("hipcc") or ("/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else None)
 SOURCES = ["kernels/conv_dispatch.hip", "kernels/conv_igemm_v2.hip", "kernels/misc.hip",
-           "kernels/stem_fused.hip", "kernels/conv_pool.hip",
+           "kernels/stem_fused.hip", "kernels/conv_pool.hip", "kernels/pool_gemm.hip",
            "kernels/bottleneck_fused.hip", "kernels/block_fused.hip", "kernels/conv_shift.hip", "kernels/expand_reduce_chain.hip",
            "runtime/runtime.hip", "tests/host_checks.cpp"]
 SAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
