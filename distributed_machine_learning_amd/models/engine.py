@@ -263,8 +263,10 @@ class Engine:
         """{pool name: 1x1 conv} for a max pool 3x3/2 (valid) whose output is read only by the
         next node, a 1x1 stride-1 conv or sibling-fused 1x1 GEMM (InceptionV3 max_pooling2d_2 ->
         conv2d_6+conv2d_7+conv2d_9+conv2d_12): the pooled tile goes from LDS straight into the GEMM
-        and the pooled tensor is never written. DML_POOL_GEMM=0: off (A/B)."""
-        if not enabled or self.device.type != "cuda" or os.environ.get("DML_POOL_GEMM", "1") == "0":
+        and the pooled tensor is never written. Opt-in (DML_POOL_GEMM=1): in the pipeline it measured
+        0.3-0.7 % below the two launches (InceptionV3 b128 48.3-48.5k vs 48.6k img/s, profiles/r3_v7)
+        — its pool phase is latency-bound at 64 pooled pixels per workgroup."""
+        if not enabled or self.device.type != "cuda" or os.environ.get("DML_POOL_GEMM", "0") != "1":
             return {}
         out: Dict[str, object] = {}
         nodes = self.g.nodes
@@ -819,7 +821,8 @@ class Engine:
     # ---------------------------------------------------------------- run ----
     def op_node_span(self, i: int) -> Tuple[int, int]:
         """(first, last) graph-node index that op ``i`` of the plan covers (op names join the
-        covered nodes' names with '+' / '|'; 'preprocess' covers node 0)."""
+        covered nodes' names with '+' / '|'; 'preprocess' counts as node 0, 'softmax_top5' as the
+        last node)."""
         index: Dict[str, int] = {}
         for k, n in enumerate(self.g.nodes):
             index[n.name] = k
@@ -828,7 +831,9 @@ class Engine:
         name = self.op_names[i]
         if name in index:
             return index[name], index[name]
-        ks = [index[x] for x in name.replace("|", "+").split("+") if x in index] or [0]
+        ks = [index[x] for x in name.replace("|", "+").split("+") if x in index]
+        if not ks:  # 'preprocess' opens the forward, 'softmax_top5' closes it
+            ks = [0] if name == "preprocess" else [len(self.g.nodes) - 1]
         return min(ks), max(ks)
 
     def set_op_range(self, begin: int, end: int) -> None:
@@ -921,7 +926,11 @@ class Engine:
 
 
 # Split-head / merged-tail serving (SplitEngine(merge_at=...)): the first node of the full-batch
-# tail per model (None: two half-batch engines end to end). DML_MERGE_AT overrides it:
+# tail per model (None: two half-batch engines end to end). Measured slower for both models
+# (profiles/r3_v7, interleaved on one box: InceptionV3 b128 46.4k merged from mixed4 / 47.6k from
+# mixed8 vs 48.3-48.5k; ResNet50 b256 82.2k from stage 4 / 86.2k from stage 5 vs 90.0-90.3k): the
+# caller's stream then runs a head AND the tail per batch while the extra stream runs one head, so
+# the two streams no longer carry equal work. Kept as an option. DML_MERGE_AT overrides it:
 # "InceptionV3=<node>,ResNet50=<node>" (a model left out keeps its default), "0" = off for all.
 MERGE_AT: Dict[str, Optional[str]] = {"ResNet50": None, "InceptionV3": None}
 

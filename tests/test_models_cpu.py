@@ -412,7 +412,45 @@ def test_pool_gemm_plan_inceptionv3(monkeypatch):
     e = Engine.__new__(Engine)
     e.g, e.device = level_order(optimize(g, stride_push=True, weights=w)), torch.device("cuda")
     e.conv_pools = {"conv2d_3": next(n for n in e.g.nodes if n.name == "max_pooling2d_1")}
+    assert e._fusable_pool_gemm(True) == {}  # opt-in
+    monkeypatch.setenv("DML_POOL_GEMM", "1")
     got = {k: v.name for k, v in e._fusable_pool_gemm(True).items()}
     assert got == {"max_pooling2d_2": "conv2d_6+conv2d_7+conv2d_9+conv2d_12"}
     monkeypatch.setenv("DML_POOL_GEMM", "0")
     assert e._fusable_pool_gemm(True) == {}
+
+
+@pytest.mark.parametrize("name,merge_at,want", [
+    ("InceptionV3", "conv2d_31+conv2d_32+conv2d_35+conv2d_40", ["mixed3"]),
+    ("InceptionV3", "conv2d_71+conv2d_73", ["mixed7"]),
+    ("ResNet50", "conv4_block1_1_conv", ["conv4_block1_2"]),
+])
+def test_merged_tail_cut_on_cpu(name, merge_at, want):
+    """Split-head / merged-tail planning, host-only: the tensors live across the cut, the op index
+    where the tail starts (no op straddles it: the head ends with the op before, the tail ends with
+    softmax_top5), and external merge storage that the head engine never recycles."""
+    from distributed_machine_learning_amd import _native as N
+    from distributed_machine_learning_amd.models.engine import Engine, SplitEngine
+
+    try:
+        N.lib()
+    except N.NativeError as e:
+        pytest.skip(f"native library unavailable: {e}")
+    g, w = build_model(name, seed=0, calibrate=False)
+    tail = Engine(g, w, batch=4, device="cpu", autotune=False)
+    names = [n.name for n in tail.g.nodes]
+    cut = names.index(merge_at)
+    assert SplitEngine.live_across(tail.g, cut) == want
+    p = SplitEngine._op_cut(tail, cut)
+    assert 0 < p < len(tail.op_names) and tail.op_names[-1] == "softmax_top5"
+    assert tail.op_node_span(p - 1)[1] < cut <= tail.op_node_span(p)[0]
+    per = tail.buf[want[0]].numel() // 4
+    ext = {want[0]: [tail.buf[want[0]][2 * per:4 * per]]}
+    head = Engine(g, None, batch=2, device="cpu", autotune=False, share=tail, ext_buffers=ext)
+    assert head.buf[want[0]].data_ptr() == tail.buf[want[0]].data_ptr() + 2 * per * 2
+    others = [t for k, t in head.buf.items() if k != want[0] and k != head.g.logits]
+    assert all(t.data_ptr() != head.buf[want[0]].data_ptr() for t in others)
+    head.set_op_range(0, SplitEngine._op_cut(head, cut))
+    tail.set_op_range(p, len(tail.op_names))
+    with pytest.raises(ValueError):
+        head.set_op_range(0, len(head.op_names) + 1)

@@ -480,7 +480,7 @@ def test_pool_gemm_matches_fp32(n, h, w, c, segs):
 def test_engine_pool_gemm_equals_unfused(fuse, monkeypatch):
     """InceptionV3: max_pooling2d_2 + mixed0's sibling 1x1 GEMM as one op (DML_POOL_GEMM) gives the
     unfused plan's mixed0 branch tensors and logits."""
-    monkeypatch.setenv("DML_POOL_GEMM", fuse)
+    monkeypatch.setenv("DML_POOL_GEMM", fuse)  # opt-in (default off)
     g, w = build_model("InceptionV3", seed=5, calibrate=True)
     imgs = torch.randint(0, 256, (2, 299, 299, 3), dtype=torch.uint8, device="cuda")
     ef = Engine(g, w, batch=2, reuse_buffers=False)
