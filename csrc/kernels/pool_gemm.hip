@@ -11,7 +11,8 @@
 //     are conflict-free);
 //  2. GEMM: output-channel fragment f (16 channels) belongs to wave f % 4; each wave runs its
 //     fragments x the 4 pixel fragments over K = C with v_mfma_f32_16x16x32_bf16, weights as A
-//     fragments straight from L2 (every weight is read once per workgroup);
+//     fragments loaded from L2 into VGPRs before the pool phase (their latency hides under it;
+//     every weight is read once per workgroup);
 //  3. epilogue: bias (accumulator start) + per-segment ReLU -> 4 channels (8 B) per lane into the
 //     segment's own destination (a concat slice or a branch buffer), as the v2 conv's segmented
 //     epilogue does.
@@ -26,7 +27,6 @@ namespace dml {
 namespace pgemm {
 
 constexpr int NT = 256, BMP = 64;  // threads, pooled pixels per workgroup
-constexpr int CMAX = 256;          // pooled channels (multiple of 32)
 constexpr int FMAX = 4;            // output-channel fragments per wave (Cout <= 256)
 
 __device__ __forceinline__ void max8(float* m, const uint4& v) {
@@ -38,18 +38,30 @@ __device__ __forceinline__ void max8(float* m, const uint4& v) {
   }
 }
 
+template <int C>
 __global__ __launch_bounds__(NT, 2) void pool_gemm_kernel(DmlPoolGemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const DmlPoolArgs& p = a.p;
   const DmlConvArgs& g = a.g;
-  const int C = p.C, CG = C / 8;
-  const int ROW = C * 2 + 16;  // LDS row bytes (pad: C * 2 = 384 -> 400 B)
+  constexpr int CG = C / 8, KS = C / 32;
+  constexpr int ROW = C * 2 + 16;  // LDS row bytes (pad: C * 2 = 384 -> 400 B)
   const int HWo = p.Ho * p.Wo, M = p.N * HWo;
   const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BMP;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int frow = lane & 15, fq = lane >> 4;
   const unsigned short* x = (const unsigned short*)p.x;
+  const int NF = (g.Cout + 15) / 16;
+
+  // this wave's weight fragments (all K) are loaded first: their L2 latency hides under the pool
+  const bf16* w = (const bf16*)g.w;
+  bf16x8 wa[FMAX][KS];
+#pragma unroll
+  for (int t = 0; t < FMAX; ++t) {
+    const int f = min(wid + 4 * t, NF - 1);  // clamped (a wave past NF loads a valid row, never uses it)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) wa[t][ks] = *(const bf16x8*)(w + (long)(16 * f + frow) * g.Kpad + 32 * ks + 8 * fq);
+  }
 
   // 1. pool into LDS (rows of pixels past M are left as they are: never stored)
   const int items = BMP * CG;
@@ -94,7 +106,6 @@ __global__ __launch_bounds__(NT, 2) void pool_gemm_kernel(DmlPoolGemmArgs a) {
   __syncthreads();
 
   // 2. GEMM: fragments f = wid + 4t of the output channels, 4 pixel fragments
-  const int NF = (g.Cout + 15) / 16;
   f32x4 acc[FMAX][4];
 #pragma unroll
   for (int t = 0; t < FMAX; ++t) {
@@ -104,18 +115,17 @@ __global__ __launch_bounds__(NT, 2) void pool_gemm_kernel(DmlPoolGemmArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[t][j] = (f32x4){bb.x, bb.y, bb.z, bb.w};
   }
-  const bf16* w = (const bf16*)g.w;
-  for (int ks = 0; ks < C / 32; ++ks) {
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
     bf16x8 pb[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) pb[j] = *(const bf16x8*)(smem + (16 * j + frow) * ROW + (4 * ks + fq) * 16);
 #pragma unroll
     for (int t = 0; t < FMAX; ++t) {
-      const int f = wid + 4 * t;
-      if (f < NF) {  // wave-uniform
-        const bf16x8 wa = *(const bf16x8*)(w + (long)(16 * f + frow) * g.Kpad + 32 * ks + 8 * fq);
+      if (wid + 4 * t < NF) {  // wave-uniform
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, pb[j], acc[t][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][ks], pb[j], acc[t][j], 0, 0, 0);
       }
     }
   }
@@ -157,7 +167,7 @@ extern "C" int dml_pool_gemm_supported(const DmlPoolGemmArgs* a) {
   const char* why = nullptr;
   if (p.k != 3 || p.stride != 2 || p.pad != 0 || p.mode != 0 || p.relu) why = "pool must be max 3x3/2 valid";
   else if (p.Ho != (p.H - 3) / 2 + 1 || p.Wo != (p.W - 3) / 2 + 1 || p.N < 1) why = "pool output size";
-  else if (p.C % 32 || p.C < 32 || p.C > dml::pgemm::CMAX || p.ldx % 8 || p.ldx < p.C) why = "pool channels";
+  else if ((p.C != 64 && p.C != 128 && p.C != 192) || p.ldx % 8 || p.ldx < p.C) why = "pool channels (64 / 128 / 192)";
   else if (g.kh != 1 || g.kw != 1 || g.sh != 1 || g.sw != 1 || g.ph || g.pw || g.res || g.out_f32 || g.ksplit > 1)
     why = "GEMM must be a plain 1x1 stride-1 conv";
   else if (g.N != p.N || g.H != p.Ho || g.W != p.Wo || g.Ho != p.Ho || g.Wo != p.Wo || g.Cin != p.C)
@@ -185,7 +195,10 @@ extern "C" int dml_pool_gemm(const DmlPoolGemmArgs* a, hipStream_t s) {
   using namespace dml::pgemm;
   const int lds = BMP * (a->p.C * 2 + 16);
   const long M = (long)a->p.N * a->p.Ho * a->p.Wo;
-  hipLaunchKernelGGL(pool_gemm_kernel, dim3((unsigned)((M + BMP - 1) / BMP)), dim3(NT), lds, s, *a);
+  const dim3 grid((unsigned)((M + BMP - 1) / BMP));
+  if (a->p.C == 64) hipLaunchKernelGGL(pool_gemm_kernel<64>, grid, dim3(NT), lds, s, *a);
+  else if (a->p.C == 128) hipLaunchKernelGGL(pool_gemm_kernel<128>, grid, dim3(NT), lds, s, *a);
+  else hipLaunchKernelGGL(pool_gemm_kernel<192>, grid, dim3(NT), lds, s, *a);
   DML_CHECK_LAUNCH();
   return 0;
 }

@@ -433,7 +433,7 @@ def test_expand_reduce_chain_stage_end(m):
 @pytest.mark.parametrize("n,h,w,c,segs", [
     (2, 71, 71, 192, [(64, True), (48, True), (64, True), (32, False)]),  # InceptionV3 max_pooling2d_2 + mixed0
     (3, 17, 13, 64, [(80, True)]),                                          # one plain segment, partial tile
-    (1, 9, 9, 32, [(16, False), (32, True)]),
+    (1, 9, 9, 128, [(16, False), (32, True)]),
 ])
 def test_pool_gemm_matches_fp32(n, h, w, c, segs):
     """csrc/kernels/pool_gemm.hip: max pool 3x3/2 valid -> bf16 -> 1x1 GEMM with a segmented
@@ -473,6 +473,8 @@ def test_pool_gemm_matches_fp32(n, h, w, c, segs):
         assert (o[..., k:].float() == -7.0).all()  # nothing past the segment's channels
         c0 += k
     pa.mode = 1  # an avg pool is not this kernel's
+    assert N.lib().dml_pool_gemm_supported(C.byref(N.PoolGemmArgs(ga, pa))) == 0
+    pa.mode, pa.C = 0, 32  # nor 32 pooled channels (instantiations: 64 / 128 / 192)
     assert N.lib().dml_pool_gemm_supported(C.byref(N.PoolGemmArgs(ga, pa))) == 0
 
 
