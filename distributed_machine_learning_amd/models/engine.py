@@ -263,9 +263,11 @@ class Engine:
         """{pool name: 1x1 conv} for a max pool 3x3/2 (valid) whose output is read only by the
         next node, a 1x1 stride-1 conv or sibling-fused 1x1 GEMM (InceptionV3 max_pooling2d_2 ->
         conv2d_6+conv2d_7+conv2d_9+conv2d_12): the pooled tile goes from LDS straight into the GEMM
-        and the pooled tensor is never written. Opt-in (DML_POOL_GEMM=1): in the pipeline it measured
-        0.3-0.7 % below the two launches (InceptionV3 b128 48.3-48.5k vs 48.6k img/s, profiles/r3_v7)
-        — its pool phase is latency-bound at 64 pooled pixels per workgroup."""
+        and the pooled tensor is never written. Opt-in (DML_POOL_GEMM=1): serially it is faster (51.4
+        vs 34.7 + 26.4 us per 64 images, profiles/r3_v9) but in the two-stream pipeline it measured
+        0.1-0.8 % below the two launches (InceptionV3 b128 47.7-48.1k vs 48.1-48.2k img/s): the
+        memory-bound pool alone overlaps the other sub-batch's MFMA-bound convs better than the
+        fused kernel at 2 waves per SIMD does."""
         if not enabled or self.device.type != "cuda" or os.environ.get("DML_POOL_GEMM", "0") != "1":
             return {}
         out: Dict[str, object] = {}
@@ -363,9 +365,10 @@ class Engine:
                 continue
             # with its shortcut (K = F), or a merged projection shortcut (K = 2F, no residual; C = 256)
             shortcut = e.residual and e.res_sub == 1 and e.cin * 4 == e.cout
-            # merged: the r1 kernel (C = 256, DML_FUSED_MERGED_BLOCK=1: measured slower) or the
-            # chained kernel (DML_CHAIN_MERGED=1; C = 256 only: stage 3's entry has K = 3F)
-            chain_m = os.environ.get("DML_CHAIN_MERGED", "0") == "1"
+            # merged: the chained kernel (C = 256 only: stage 3's entry has K = 3F; on by default,
+            # ResNet50 b256 91.2-91.3k vs 88.1-89.3k img/s interleaved on one box, profiles/r3_v9;
+            # DML_CHAIN_MERGED=0: off) or the r1 kernel (DML_FUSED_MERGED_BLOCK=1: measured slower)
+            chain_m = os.environ.get("DML_CHAIN_MERGED", "1") == "1"
             merged = (e.residual is None and e.cin * 2 == e.cout
                       and ((e.cout == 256 and (chain_m or os.environ.get("DML_FUSED_MERGED_BLOCK", "0") == "1"))
                            or (e.cout == 512 and chain_m)))

@@ -367,8 +367,11 @@ def test_block_boundary_fusion_plan_resnet50(monkeypatch):
         return e
 
     e = plan()
-    assert sorted(e.exp_red) == ["conv2_block2_3_conv", "conv2_block3_3_conv", "conv3_block2_3_conv",
-                                 "conv3_block3_3_conv"]
+    assert sorted(e.exp_red) == ["conv2_block1_3_conv+conv2_block1_0_conv", "conv2_block2_3_conv",
+                                 "conv2_block3_3_conv", "conv3_block2_3_conv", "conv3_block3_3_conv"]
+    assert e.exp_red["conv2_block1_3_conv+conv2_block1_0_conv"].name == "conv2_block2_1_conv"  # merged entry
+    assert "conv2_block1_3_conv+conv2_block1_0_conv" not in plan(DML_CHAIN_MERGED="0").exp_red
+    monkeypatch.delenv("DML_CHAIN_MERGED")
     assert e.ysub == {"conv2_block2_out": 2, "conv3_block3_out": 2}
     x, r = next(n for n in g2.nodes if n.name == "conv2_block3_3_conv"), e.exp_red["conv2_block3_3_conv"]
     assert r.name == "conv3_block1_1_conv" and r.cout == 2 * x.cin and r.in_coff == x.out_coff == 128

@@ -240,7 +240,7 @@ def test_expand_reduce_matches_fp32(c, m):
 
 
 @pytest.mark.parametrize("maxc,chain,merged,pairs", [(256, "0", "0", 3), (256, "1", "0", 5), (256, "2", "0", 9),
-                                                     (1024, "0", "0", 9), (256, "1", "1", 5)])
+                                                     (1024, "0", "0", 9), (256, "1", "1", 5), (256, "1", "", 5)])
 def test_engine_fused_blocks_equal_unfused(maxc, chain, merged, pairs, monkeypatch):
     """DML_CHAIN=1 (default) adds stage 3's boundaries (C = 512, chained kernel), 2 also stage 4's;
     DML_CHAIN_MERGED=1 routes stage 2's merged entry (K = 2F) to the chained kernel; stage 3's merged
@@ -250,7 +250,10 @@ def test_engine_fused_blocks_equal_unfused(maxc, chain, merged, pairs, monkeypat
     3's first reduce (256 -> 128) in every case (DML_CHAIN_STAGE_END, default on)."""
     monkeypatch.setenv("DML_FUSED_BLOCKS_MAXC", str(maxc))
     monkeypatch.setenv("DML_CHAIN", chain)
-    monkeypatch.setenv("DML_CHAIN_MERGED", merged)
+    if merged:
+        monkeypatch.setenv("DML_CHAIN_MERGED", merged)
+    else:  # the default: the merged stage-2 entry on the chained kernel
+        monkeypatch.delenv("DML_CHAIN_MERGED", raising=False)
     monkeypatch.setenv("DML_FUSED_MERGED_BLOCK", "1")  # opt-in merged-shortcut form, covered here
     g, w = build_model("ResNet50", seed=8, calibrate=True)
     imgs = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda")
