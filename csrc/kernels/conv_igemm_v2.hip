@@ -416,6 +416,10 @@ static int set_attr() {
   X(34, 256, 256, 2, 4, 3, 32, 16, 0, 1)   /* 8 waves, 128px x 64ch per wave, 96 KiB */                      \
   X(36, 128, 32, 2, 1, 3, 32, 16, 0, 1)    /* Cout = 32 layers (InceptionV3 stem): 2 waves, 30 KiB */        \
   X(37, 256, 32, 4, 1, 3, 64, 16, 0, 1)    /* 4 waves, 3-stage */                                     \
+  /* 3-stage BK64 forms of the 64-channel tiles (the stride-1 Cout 64 / 192 layers' 2-stage */     \
+  /* 128x64 tile waits on DRAM latency every K tile: one tap of 64 channels per stage) */         \
+  X(38, 128, 64, 2, 2, 3, 64, 16, 0, 1)    /* 72 KiB: 2 blocks/CU */                                         \
+  X(39, 256, 64, 4, 1, 3, 64, 16, 0, 1)    /* 120 KiB: 1 block/CU */                                         \
   /* v_mfma_f32_32x32x16_bf16 twins (MF 32: 32x32 fragments, f32x16 accumulators) of the two */   \
   /* most-picked tiles; kept as A/B probes, not tuner candidates: over all 64 ResNet50 / */        \
   /* InceptionV3 shapes x 8 tile pairs the MF 32 form ran a median 4-6 % slower (best on 2 */      \

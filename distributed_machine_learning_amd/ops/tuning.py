@@ -21,7 +21,8 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 from .. import _native as N
 
-V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33, 34, 36, 37)  # 23..: BK32
+V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33, 34, 36, 37,
+           38, 39)  # 23..37: BK32; 38 / 39: 3-stage BK64 64-channel tiles (r3)
 # shifted-pixel stride-1 "same" conv configs (csrc/kernels/conv_shift.hip): candidates
 # of the shapes dml_conv_shift_check accepts
 SHIFT_CFGS = (64, 65, 66, 67, 68, 69)

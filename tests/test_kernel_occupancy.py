@@ -31,6 +31,8 @@ PLAIN_FLOORS = {
     (128, 64, 2, 2, 3, 1, 32): 4,    # cfg 27, residual epilogue
     (128, 128, 2, 2, 2, 0, 64): 2,   # cfg 11 (64 KiB)
     (256, 64, 4, 1, 2, 0, 64): 2,    # cfg 12 (80 KiB)
+    (128, 64, 2, 2, 3, 0, 64): 2,    # cfg 38 (72 KiB: 2 workgroups/CU)
+    (256, 64, 4, 1, 3, 0, 64): 1,    # cfg 39 (120 KiB)
 }
 LATE_FLOORS = {  # late-residual twins (residual form): the occupancy their non-residual base has
     (256, 128, 4, 2, 3, 1, 32): 4,   # cfg 56 (min-waves hint 4: 128 VGPRs, no scratch)

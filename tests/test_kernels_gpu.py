@@ -44,7 +44,7 @@ def _pads(kh, kw, pad):
 
 @pytest.mark.parametrize("case", CONV_CASES)
 @pytest.mark.parametrize("cfg", [-1, 10, 11, 12, 13, 14, 15, 16, 17, 18, 23, 24, 25, 26, 27, 28, 29,
-                                 30, 31, 32, 33, 34, 36, 37, 48, 49, 56, 57, 58, 59, 60])
+                                 30, 31, 32, 33, 34, 36, 37, 38, 39, 48, 49, 56, 57, 58, 59, 60])
 def test_conv_matches_fp32(case, cfg):
     n, h, w, cin, cout, kh, kw, s, pad, relu, has_res = case
     ph, pw = (kh // 2, kw // 2) if pad else (0, 0)
@@ -272,7 +272,7 @@ def test_avgpool_relu_flag():
 
 
 @pytest.mark.parametrize("cfg", [10, 11, 12, 13, 14, 15, 16, 17, 18, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33,
-                                 34, 36, 37, 48, 49, 56, 57, 58, 59, 60])
+                                 34, 36, 37, 38, 39, 48, 49, 56, 57, 58, 59, 60])
 @pytest.mark.parametrize("case", [(2, 28, 28, 64, 256, 1, 1), (2, 14, 10, 128, 512, 1, 1), (2, 7, 9, 64, 64, 3, 3)])
 def test_conv_subsampled_residual(case, cfg):
     """Residual read at stride 2 from its full-resolution grid (rsub = 2: the
