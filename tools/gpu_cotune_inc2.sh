@@ -1,0 +1,8 @@
+#!/bin/bash
+# Second pipeline co-tuning pass over InceptionV3 on the adopted r3 table (4 candidates per op).
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+timeout -k 10 800 python -u tools/cotune_pipe.py --model ${MODEL:-InceptionV3} --cands ${CANDS:-4} --budget_s 540 \
+  --out gpurun_out/cotune2_${MODEL:-InceptionV3}.json > gpurun_out/cotune2_${MODEL:-InceptionV3}.log 2>&1 || { tail -20 gpurun_out/cotune2_${MODEL:-InceptionV3}.log; exit 1; }
+tail -1 gpurun_out/cotune2_${MODEL:-InceptionV3}.log | cut -c1-600
