@@ -1,5 +1,5 @@
 #!/bin/bash
-# Second pipeline co-tuning pass over InceptionV3 on the adopted r3 table (4 candidates per op).
+# Pipeline co-tuning pass (tools/cotune_pipe.py) over MODEL (default InceptionV3) with CANDS candidates per op.
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
