@@ -230,6 +230,85 @@ __global__ __launch_bounds__(256) void softmax_top5_kernel(float* logits, int B,
   }
 }
 
+// One WAVE per row (4 rows per 256-thread workgroup), classes <= 1024: lane l owns classes
+// l, l + 64, ... in registers; the split-K slices are summed in slice order (the same fp32
+// additions, in the same order, as softmax_top5_kernel), max / sum / 5 argmax rounds reduce with
+// wave shuffles only — no LDS, no barrier (the workgroup kernel above spends its time in 7
+// barriers and 8 dependent slice loads per row).
+__global__ __launch_bounds__(256) void softmax_top5_wave_kernel(float* logits, int B, int classes, int ld, int nsplit,
+                                                                int split_ld, float* probs, int* top_idx,
+                                                                float* top_p) {
+  constexpr int PER = 16;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;  // wave-uniform
+  float* lr = logits + (long)row * ld;
+  float v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < classes ? lr[c] : -3.0e38f;
+  }
+  if (nsplit > 1) {
+    for (int sp = 1; sp < nsplit; ++sp) {
+      const float* ls = lr + (long)sp * split_ld;
+      float u[PER];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int c = lane + 64 * i;
+        u[i] = c < classes ? ls[c] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < PER; ++i) v[i] += u[i];
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      if (c < classes) lr[c] = v[i];
+    }
+  }
+  float mx = -3.0e38f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) mx = fmaxf(mx, v[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    if (c < classes) sum += __expf(v[i] - mx);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  const float inv = 1.f / sum;
+  if (probs) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      if (c < classes) probs[(long)row * classes + c] = __expf(v[i] - mx) * inv;
+    }
+  }
+  unsigned taken = 0;
+  for (int k = 0; k < 5; ++k) {
+    float bv = -3.0e38f;
+    int bi = 0x7fffffff, bslot = -1;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      if (c < classes && !(taken >> i & 1u) && v[i] > bv) { bv = v[i]; bi = c; bslot = i; }
+    }
+    float wv = bv;
+    int wi = bi;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) argmax_merge(wv, wi, __shfl_xor(wv, o), __shfl_xor(wi, o));
+    if (wi == bi && bslot >= 0) taken |= 1u << bslot;
+    if (lane == 0) {
+      top_idx[row * 5 + k] = wi;
+      top_p[row * 5 + k] = __expf(wv - mx) * inv;
+    }
+  }
+}
+
 // Pillow NEAREST resize (Keras load_img default): src = floor((dst + 0.5) * Ssrc / Sdst).
 __device__ __forceinline__ void preprocess_pixel(const DmlPreprocArgs& a, const unsigned char* src, int n, int oh,
                                                  int ow, float sy, float sx, float* f) {
@@ -297,7 +376,11 @@ extern "C" int dml_softmax_top5_split(float* logits, int B, int classes, int ld,
                                       float* probs, int* top_idx, float* top_p, hipStream_t s) {
   const dim3 grid(B), block(256);
   if (nsplit < 1) nsplit = 1;
-  if (classes <= 4 * 256) {
+  static const bool wg = getenv("DML_SOFTMAX_WG") != nullptr;  // A/B switch: one workgroup per row
+  if (!wg && classes <= 1024) {
+    hipLaunchKernelGGL(dml::softmax_top5_wave_kernel, dim3((unsigned)((B + 3) / 4)), block, 0, s, logits, B, classes,
+                       ld, nsplit, split_ld, probs, top_idx, top_p);
+  } else if (classes <= 4 * 256) {
     hipLaunchKernelGGL(dml::softmax_top5_kernel<4>, grid, block, 0, s, logits, B, classes, ld, nsplit, split_ld,
                        probs, top_idx, top_p);
   } else if (classes <= 8 * 256) {

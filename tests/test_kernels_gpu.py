@@ -199,6 +199,21 @@ def test_softmax_top5():
     assert torch.allclose(p.cpu(), rv, atol=1e-6, rtol=1e-4)
 
 
+@pytest.mark.parametrize("rows,classes", [(5, 1000), (130, 1000), (3, 64), (9, 1024)])
+def test_softmax_top5_ties_lower_id_first(rows, classes):
+    """Coarse logits (many exact ties): top-5 ids in (value desc, id asc) order, the order the
+    serving results have always used — the wave-per-row kernel keeps it."""
+    torch.manual_seed(6)
+    logits = torch.randint(-4, 5, (rows, classes)).float()
+    probs, idx, p = ops.softmax_top5(logits.cuda())
+    torch.cuda.synchronize()
+    for r in range(rows):
+        order = sorted(range(classes), key=lambda c: (-logits[r, c].item(), c))[:5]
+        assert idx[r].cpu().tolist() == order, r
+    ref = torch.softmax(logits, -1)
+    assert torch.allclose(probs.cpu(), ref, atol=1e-6, rtol=1e-4)
+
+
 @pytest.mark.parametrize("mode,hw", [("caffe", (224, 224)), ("tf", (299, 299))])
 def test_preprocess(mode, hw):
     from distributed_machine_learning_amd.models.oracle import preprocess_reference
