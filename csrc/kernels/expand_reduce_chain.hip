@@ -421,7 +421,7 @@ extern "C" int dml_chain_init(void) {
                  chain_attr<256, 4, 1>() | chain_attr<256, 8, 1>() | chain_attr<256, 4, 1, true>() |
                  chain_attr<64, 4, 2>() |
                  chain_attr<64, 4, 2, false, 128, false>() | chain_attr<128, 4, 2, false, 256, false>() |
-                 chain_attr<128, 4, 2, false, 64, true>();
+                 chain_attr<128, 4, 2, false, 64, true>() | chain_attr<256, 4, 1, false, 128, true>();
   if (rc) dml_set_error("dml_chain_init: hipFuncSetAttribute failed");
   return rc ? -1 : 0;
 }
@@ -441,9 +441,11 @@ extern "C" int dml_chain_supported(const DmlExpandReduceArgs* a) {
   const bool merged = a->res == nullptr;
   const int kx = merged ? a->kx : F;
   // a stage's last boundary: expand F = 64 -> C = 256 (+ shortcut) feeding the next stage's
-  // first reduce 256 -> 128 (template F = reduce width 128, KX = 64; a.C = 256 chunks)
+  // first reduce 256 -> 128 (template F = reduce width 128, KX = 64; a.C = 256 chunks), or
+  // F = 128 -> C = 512 -> reduce 256 (16 pixels per wave: the 256 Z accumulators)
   if (FZ != F)
-    return !merged && C == 256 && FZ == 128 && (a->kx == 0 || a->kx == F) && a->M >= 1 && a->ldx % 8 == 0 &&
+    return !merged && ((C == 256 && FZ == 128) || (C == 512 && FZ == 256)) && (a->kx == 0 || a->kx == F) &&
+           a->M >= 1 && a->ldx % 8 == 0 &&
            a->ldx >= F && a->ldw3 % 8 == 0 && a->ldw3 >= F && a->ldr % 8 == 0 && a->ldr >= C &&
            a->ldy % 8 == 0 && a->ldy >= C && a->ldw1 % 8 == 0 && a->ldw1 >= C && a->ldz % 8 == 0 &&
            a->ldz >= FZ && (long)a->M * (a->ldr > a->ldy ? a->ldr : a->ldy) * 2 < 0x7ffffff0L;
@@ -467,8 +469,9 @@ extern "C" int dml_chain(const DmlExpandReduceArgs* a, hipStream_t s) {
   static const int nw = [] { const char* e = getenv("DML_CHAIN_WAVES"); return e && atoi(e) == 8 ? 8 : 4; }();
   static const bool big = env_on("DML_CHAIN_BIG");
   const bool merged = a->res == nullptr;
-  if (a->fz > 0 && a->fz != a->C / 4) {
-    chain_launch<128, 4, 2, false, 64, true>(a, s);  // stage-end boundary (256 -> 128 reduce)
+  if (a->fz > 0 && a->fz != a->C / 4) {  // stage-end boundary
+    if (a->C == 256) chain_launch<128, 4, 2, false, 64, true>(a, s);  // 64 -> 256 -> 128
+    else chain_launch<256, 4, 1, false, 128, true>(a, s);             // 128 -> 512 -> 256
   } else if (merged) {
     if (a->C == 256) chain_launch<64, 4, 2, false, 128, false>(a, s);
     else chain_launch<128, 4, 2, false, 256, false>(a, s);

@@ -393,8 +393,9 @@ class Engine:
         the expand (1x1 F -> C = 4F, + the shortcut, which the previous fused boundary stored
         compactly: ``ysub``) writes its C channels into the next stage's ``[x ; s]`` concat buffer,
         and the next stage's first reduce (C -> 2F) reads exactly that slice. ResNet50:
-        conv2_block3_3 -> conv3_block1_1 (64 -> 256 -> 128 at 28x28; the stage-3/4 ends would need
-        2F = 256 / 512 reduce accumulators per wave). DML_CHAIN_STAGE_END=0: off."""
+        conv2_block3_3 -> conv3_block1_1 (64 -> 256 -> 128 at 28x28). DML_CHAIN_STAGE_END=2 also
+        stage 3's end (128 -> 512 -> 256 at 14x14, 16 pixels per wave: its 256 reduce accumulators);
+        0: off."""
         if (not enabled or self.device.type != "cuda" or os.environ.get("DML_FUSED_BLOCKS") == "0"
                 or os.environ.get("DML_CHAIN_STAGE_END", "1") == "0" or os.environ.get("DML_ER_R1") == "1"):
             return {}
@@ -405,7 +406,8 @@ class Engine:
         for e, r in zip(nodes, nodes[1:]):
             if not (isinstance(e, Conv) and isinstance(r, Conv)) or e.name in taken or r.name in taken:
                 continue
-            if not (e.kh == e.kw == 1 and e.sh == e.sw == 1 and e.cin == 64 and e.cout == 256 and e.relu
+            shapes = {(64, 256)} | ({(128, 512)} if os.environ.get("DML_CHAIN_STAGE_END") == "2" else set())
+            if not (e.kh == e.kw == 1 and e.sh == e.sw == 1 and (e.cin, e.cout) in shapes and e.relu
                     and e.residual in self.ysub and e.in_coff == 0 and not e.out_f32):
                 continue
             if not (r.inp == e.out and r.in_coff == e.out_coff and r.cin == e.cout and r.cout == 2 * e.cin

@@ -376,6 +376,9 @@ def test_block_boundary_fusion_plan_resnet50(monkeypatch):
     x, r = next(n for n in g2.nodes if n.name == "conv2_block3_3_conv"), e.exp_red["conv2_block3_3_conv"]
     assert r.name == "conv3_block1_1_conv" and r.cout == 2 * x.cin and r.in_coff == x.out_coff == 128
     assert x.residual in e.ysub  # the shortcut is read compactly, at the expand's own grid
+    e2 = plan(DML_CHAIN_STAGE_END="2")  # opt-in: stage 3's end too (128 -> 512 -> 256)
+    assert e2.exp_red["conv3_block4_3_conv"].name == "conv4_block1_1_conv"
+    assert "conv4_block6_3_conv" not in e2.exp_red  # stage 4's end (C = 1024) never
     assert "conv2_block3_3_conv" not in plan(DML_CHAIN_STAGE_END="0").exp_red
     assert "conv2_block3_3_conv" not in plan(DML_CHAIN_STAGE_END="1", DML_ER_R1="1").exp_red
 

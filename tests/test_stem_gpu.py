@@ -400,12 +400,13 @@ def test_expand_reduce_chain_subsampled_y(c):
     assert _rel(z.float().cpu(), z_ref) < 1e-2
 
 
-@pytest.mark.parametrize("m", [128, 300, 2 * 28 * 28, 5 * 28 * 28 + 7])
-def test_expand_reduce_chain_stage_end(m):
-    """A stage's last boundary (chained kernel, fz = 2F): y = relu(x W3 + b3 + res) (64 -> 256)
-    stored into channels [128, 384) of a 384-wide concat buffer, z = relu(y W1 + b1) (256 -> 128)."""
+@pytest.mark.parametrize("m,f", [(128, 64), (300, 64), (2 * 28 * 28, 64), (5 * 28 * 28 + 7, 64),
+                                 (64, 128), (3 * 14 * 14 + 5, 128)])
+def test_expand_reduce_chain_stage_end(m, f):
+    """A stage's last boundary (chained kernel, fz = 2F): y = relu(x W3 + b3 + res) (F -> 4F)
+    stored into channels [2F, 6F) of a 6F-wide concat buffer, z = relu(y W1 + b1) (4F -> 2F)."""
     torch.manual_seed(9)
-    f, c, fz, ldy, coff = 64, 256, 128, 384, 128
+    c, fz, ldy, coff = 4 * f, 2 * f, 6 * f, 2 * f
     x = _bf(torch.randn(m, f).clamp(min=0))
     res = _bf(torch.randn(m, c))
     w3 = _bf(torch.randn(c, f) * (2.0 / f) ** 0.5)
