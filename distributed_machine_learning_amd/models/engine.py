@@ -394,8 +394,8 @@ class Engine:
         compactly: ``ysub``) writes its C channels into the next stage's ``[x ; s]`` concat buffer,
         and the next stage's first reduce (C -> 2F) reads exactly that slice. ResNet50:
         conv2_block3_3 -> conv3_block1_1 (64 -> 256 -> 128 at 28x28). DML_CHAIN_STAGE_END=2 also
-        stage 3's end (128 -> 512 -> 256 at 14x14, 16 pixels per wave: its 256 reduce accumulators);
-        0: off."""
+        stage 3's end (128 -> 512 -> 256 at 14x14, 16 pixels per wave: its 256 reduce accumulators;
+        exact, neutral in the pipeline: 90.4-91.1k vs 90.5-90.9k img/s, profiles/r3_v11); 0: off."""
         if (not enabled or self.device.type != "cuda" or os.environ.get("DML_FUSED_BLOCKS") == "0"
                 or os.environ.get("DML_CHAIN_STAGE_END", "1") == "0" or os.environ.get("DML_ER_R1") == "1"):
             return {}
