@@ -124,6 +124,8 @@ for i, name in enumerate(e0.op_names):
         if t < best[0]:
             best = (t, c)
     keep = best[0] < cur * (1 - args.thresh)
+    print(f"[{i}/{len(e0.op_names)}] {name}: {len(cands)} candidates, best {best[1]} {best[0]:.4f} ms/step "
+          f"(current {cur:.4f}, {time.time() - t_start:.0f} s)", flush=True)  # progress (keeps the run visibly alive)
     for p in plans:
         L.dml_plan_set_cfg(p, i, best[1] if keep else c0)
     recapture()
