@@ -80,8 +80,9 @@ def parse_args(argv=None):
     ap.add_argument("--svc-resnet-images", type=int, default=51200, help="ResNet50 images per GPU (service run)")
     ap.add_argument("--svc-inception-images", type=int, default=25600,
                     help="InceptionV3 images per GPU (service run)")
-    ap.add_argument("--svc-outputs", default="/tmp",
-                    help="directory for the service run's output files ('' = outputs off); removed afterwards")
+    ap.add_argument("--svc-outputs", default="",
+                    help="also write the service run's output files to this directory (removed afterwards); "
+                         "every output is always PUT into the ranks' replicated store, as serving.main --role rank")
     ap.add_argument("--kill", action="append", default=[],
                     help="rank:step - inject a rank kill into the service run (BASELINE config 5; needs --gpus > 1)")
     return ap.parse_args(argv)

@@ -53,6 +53,10 @@ typedef struct {
   // stride rsub from its full-resolution grid (rW = its width, rHW = H*W), used
   // when a stride-2 consumer has been pushed up into the block (models/optimize.py).
   int rsub, rW, rHW;
+  // Winograd F(2x2, 3x3) weights (cfg 80, conv_wino.hip): U = G g G^T per (cin, cout), bf16,
+  // host-packed [Cin/32][16 positions][Cout/16 fragments, padded to 4k][64 lanes][8] (ops.pack_wino_weight);
+  // null when the conv has none
+  const void* wu;
 } DmlConvArgs;
 
 
@@ -143,14 +147,6 @@ typedef struct {
   int c4, ldw4;
 } DmlConvPoolArgs;
 
-// Max pool 3x3/2 (valid) + the 1x1 GEMM that is the pooled tensor's only reader, ONE kernel
-// (csrc/kernels/pool_gemm.hip; InceptionV3 max_pooling2d_2 -> mixed0's sibling 1x1 GEMM). p: the
-// pool (its y is never written); g: the 1x1 conv over the pooled grid (g.x unused; segments ok).
-typedef struct {
-  DmlConvArgs g;
-  DmlPoolArgs p;
-} DmlPoolGemmArgs;
-
 // Fused ResNet50 block boundary (csrc/kernels/bottleneck_fused.hip), F = C / 4:
 //   y = relu(w3 . x + b3 + res)  (1x1 expand F -> C + shortcut)
 //   z = relu(w1 . y + b1)        (next block's 1x1 reduce C -> F)
@@ -177,24 +173,6 @@ typedef struct {
   int fz;
 } DmlExpandReduceArgs;
 
-// Whole ResNet50 identity bottleneck block (csrc/kernels/block_fused.hip), C = 4F:
-//   t1 = relu(w1 . x + b1)  (1x1 C -> F),  t2 = relu(w2 * t1 + b2)  (3x3 'same' F -> F),
-//   y  = relu(w3 . t2 + b3 + x)  (1x1 F -> C + identity shortcut); T1/T2 stay on chip.
-typedef struct {
-  const void* x;     // bf16 NHWC [N][H][W][ldx] (C channels): block input and shortcut
-  const void* w1;    // bf16 [>=F][ldw1], K = C
-  const float* b1;   // fp32 [F]
-  const void* w2;    // bf16 [>=F][ldw2], K = 9F in (r, s, c) order
-  const float* b2;   // fp32 [F]
-  const void* w3;    // bf16 [>=C][ldw3], K = F
-  const float* b3;   // fp32 [C]
-  void* y;           // bf16 NHWC [N][H][W][ldy] (C channels), must not alias x
-  int N, H, W, F;
-  int ldx, ldy, ldw1, ldw2, ldw3;
-  long long* stamps;  // diagnostics only (null in the engine): per workgroup 8 x s_memrealtime / s_memtime
-  int kernel;         // 0: persistent warp-specialised (default), 1: phase-serialised (A/B, stamps)
-} DmlBlockArgs;
-
 // ---- single-op launches (used by tests and by the plan executor) ----
 int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s);
 int dml_stem_inception(const DmlIncStemArgs* a, hipStream_t s);
@@ -203,12 +181,8 @@ int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s);
 // chained-GEMM block boundary, F = 128 / C = 512 (expand_reduce_chain.hip); dml_expand_reduce routes to it
 int dml_chain(const DmlExpandReduceArgs* a, hipStream_t s);
 int dml_chain_supported(const DmlExpandReduceArgs* a);
-int dml_pool_gemm(const DmlPoolGemmArgs* a, hipStream_t s);
-int dml_pool_gemm_supported(const DmlPoolGemmArgs* a);
 int dml_chain_init(void);
 int dml_expand_reduce_init(void);
-int dml_block_fused(const DmlBlockArgs* a, hipStream_t s);
-int dml_block_fused_init(void);
 int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_v2_init(void);
@@ -217,11 +191,13 @@ int dml_conv_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s);
 int dml_conv_v2_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s);
 int dml_conv_v2_group_supported(int cfg);
 int dml_conv_v2_bn(int cfg);
-// shifted-pixel stride-1 "same" conv (conv_shift.hip; cfg ids 64..)
-int dml_conv_shift(const DmlConvArgs* a, int cfg, hipStream_t s);
-int dml_conv_shift_bn(int cfg);
-const char* dml_conv_shift_check(const DmlConvArgs* a, int cfg);
-int dml_conv_shift_init(void);
+// Winograd F(2x2, 3x3) stride-1 conv (conv_wino.hip; cfg DML_WINO_CFG = the default
+// configuration, 81 = 64-channel tiles): needs DmlConvArgs.wu
+#define DML_WINO_CFG 80
+int dml_conv_wino_supported(int cfg);  // the config's output-channel tile, 0: not a Winograd config
+int dml_conv_wino(const DmlConvArgs* a, int cfg, hipStream_t s);
+const char* dml_conv_wino_check(const DmlConvArgs* a);
+int dml_conv_wino_init(void);
 int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);
@@ -252,8 +228,6 @@ int dml_plan_add_stem(void* plan, const DmlStemArgs* a);
 int dml_plan_add_inc_stem(void* plan, const DmlIncStemArgs* a);
 int dml_plan_add_conv_pool(void* plan, const DmlConvPoolArgs* a);
 int dml_plan_add_expand_reduce(void* plan, const DmlExpandReduceArgs* a);
-int dml_plan_add_pool_gemm(void* plan, const DmlPoolGemmArgs* a);
-int dml_plan_add_block(void* plan, const DmlBlockArgs* a);
 int dml_plan_size(void* plan);
 int dml_plan_run(void* plan, hipStream_t s);
 int dml_plan_run_range(void* plan, int begin, int end, hipStream_t s);

@@ -4,30 +4,32 @@
 // Serves every convolution of ResNet50 / InceptionV3 and the FC layer
 // (SURVEY §2.7 "conv_igemm_bf16"; the reference runs these inside Keras,
 // models.py:26,51 — it has no kernel of its own). cfg ids 10..63 select a v2
-// tile configuration (dml_conv_v2), ids 64.. a shifted-pixel configuration of
-// the stride-1 "same" conv kernel (conv_shift.hip); they are part of the ABI the
-// plan builder and the autotuner (ops/tuning.py) use.
+// tile configuration (dml_conv_v2), id 80 (DML_WINO_CFG) the Winograd F(2x2, 3x3)
+// kernel of stride-1 3x3 convs (conv_wino.hip); they are part of the ABI the plan
+// builder and the autotuner (ops/tuning.py) use.
 //
-// Removed in r2 (measured never faster, kept only as history in DESIGN.md and
-// profiles/): the register-staged v1 kernel (cfg 0..4, profiles/r1_v2) and the
-// stride-1 halo-tile kernel (cfg 40..47, profiles/r1_v5/halo_vs_v2_*.json: won
-// 0 of 217 tuned shapes).
+// Removed (measured never faster, kept only as history in DESIGN.md and
+// profiles/): the register-staged v1 kernel (cfg 0..4, r1, profiles/r1_v2), the
+// stride-1 halo-tile kernel (cfg 40..47, r2, profiles/r1_v5/halo_vs_v2_*.json: won
+// 0 of 217 tuned shapes) and the shifted-pixel stride-1 kernel (cfg 64..69, r4:
+// never picked by the cold tuner, profiles/r3_v2/shift_vs_igemm.json).
 #include "common.h"
 #include "dml.h"
 #include "pool_shared.h"
 
 static int validate(const DmlConvArgs* a, int cfg) {
-  const int bn = dml_conv_v2_bn(cfg);
-  if (bn <= 0) {
-    dml_set_error("dml_conv: cfg must be a v2 tile config (10..63) or a shifted-pixel config (64..)");
-    return -1;
-  }
-  if (cfg >= 64) {  // shifted-pixel kernel (conv_shift.hip): stride-1 same convs only
-    const char* why = dml_conv_shift_check(a, cfg);
+  if (dml_conv_wino_supported(cfg)) {  // Winograd F(2x2, 3x3) (conv_wino.hip): its own shape gate
+    const char* why = dml_conv_wino_check(a);
     if (why) {
       dml_set_error(why);
       return -1;
     }
+    return 0;
+  }
+  const int bn = dml_conv_v2_bn(cfg);
+  if (bn <= 0) {
+    dml_set_error("dml_conv: cfg must be a v2 tile config (10..63) or a Winograd config (80, 81)");
+    return -1;
   }
   // weights are packed with Cout padded to a multiple of 256 rows; a 96- or
   // 192-wide channel tile must not run past them
@@ -56,7 +58,7 @@ static int validate(const DmlConvArgs* a, int cfg) {
 
 extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
   if (validate(a, cfg) != 0) return -1;
-  return cfg >= 64 ? dml_conv_shift(a, cfg, s) : dml_conv_v2(a, cfg, s);
+  return dml_conv_wino_supported(cfg) ? dml_conv_wino(a, cfg, s) : dml_conv_v2(a, cfg, s);
 }
 
 extern "C" int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg) {

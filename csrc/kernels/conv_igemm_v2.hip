@@ -462,8 +462,7 @@ extern "C" int dml_conv_v2_init(void) {
 #undef DML_SET
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   if (!rc && dml_expand_reduce_init() != 0) return -1;  // fused block-boundary kernels (bottleneck_fused.hip)
-  if (!rc && dml_block_fused_init() != 0) return -1;    // whole fused bottleneck blocks (block_fused.hip)
-  if (!rc && dml_conv_shift_init() != 0) return -1;     // stride-1 shifted-pixel convs (conv_shift.hip)
+  if (!rc && dml_conv_wino_init() != 0) return -1;     // Winograd 3x3 convs (conv_wino.hip)
   return rc ? -1 : 0;
 }
 
@@ -480,7 +479,7 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
 
 // channel-tile width of a config (0: not a config)
 extern "C" int dml_conv_v2_bn(int cfg) {
-  if (cfg >= 64) return dml_conv_shift_bn(cfg);  // shifted-pixel configs (conv_shift.hip)
+  if (dml_conv_wino_supported(cfg)) return dml_conv_wino_supported(cfg);  // Winograd (conv_wino.hip)
   if (cfg < 10) return 0;
   switch (cfg) {
 #define DML_CASE(id, BM, BN, WM, WN, ST, BK, MF, RL, W) \

@@ -45,8 +45,7 @@ extern "C" int dml_device_info(int* cus, int* arch_major, int* arch_minor) {
 extern "C" int dml_abi_sizes(int* out, int n) {
   const int sz[] = {(int)sizeof(DmlConvArgs), (int)sizeof(DmlPoolArgs), (int)sizeof(DmlConvGroupArgs),
                     (int)sizeof(DmlPreprocArgs), (int)sizeof(DmlStemArgs), (int)sizeof(DmlIncStemArgs),
-                    (int)sizeof(DmlConvPoolArgs), (int)sizeof(DmlExpandReduceArgs),
-                    (int)sizeof(DmlBlockArgs), (int)sizeof(DmlPoolGemmArgs)};
+                    (int)sizeof(DmlConvPoolArgs), (int)sizeof(DmlExpandReduceArgs)};
   const int m = (int)(sizeof(sz) / sizeof(sz[0]));
   for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
   return m;
@@ -55,7 +54,7 @@ extern "C" int dml_abi_sizes(int* out, int n) {
 // ----------------------------------------------------------------- plan ----
 namespace {
 enum OpKind { OP_CONV, OP_POOL, OP_GAP, OP_SMTOP5, OP_PREPROC, OP_STEM, OP_INC_STEM, OP_CONV_POOL, OP_EXP_RED,
-              OP_CONV_GROUP, OP_BLOCK, OP_POOL_GEMM };
+              OP_CONV_GROUP };
 struct GapArgs { const void* x; void* y; int N, HW, C, ldx; };
 struct SmArgs { float* logits; int B, classes, ld, nsplit, split_ld; float* probs; int* idx; float* p; };
 struct Op {
@@ -70,9 +69,7 @@ struct Op {
   DmlIncStemArgs istem;
   DmlConvPoolArgs cpool;
   DmlExpandReduceArgs er;
-  DmlBlockArgs blk;
   DmlConvGroupArgs grp;
-  DmlPoolGemmArgs pg;
 };
 struct Plan {
   std::vector<Op> ops;
@@ -107,8 +104,6 @@ int run_op(const Op& o, hipStream_t s) {
     case OP_CONV_POOL: return dml_conv3x3_pool(&o.cpool, s);
     case OP_EXP_RED: return dml_expand_reduce(&o.er, s);
     case OP_CONV_GROUP: return dml_conv_group(&o.grp, o.cfg, s);
-    case OP_BLOCK: return dml_block_fused(&o.blk, s);
-    case OP_POOL_GEMM: return dml_pool_gemm(&o.pg, s);
   }
   return -1;
 }
@@ -190,26 +185,11 @@ extern "C" int dml_plan_add_conv_group(void* p, const DmlConvGroupArgs* g, int c
   ((Plan*)p)->ops.push_back(o);
   return cfg;
 }
-extern "C" int dml_plan_add_pool_gemm(void* p, const DmlPoolGemmArgs* a) {
-  if (!dml_pool_gemm_supported(a)) return -1;  // the error names the unsupported field
-  Op o{};
-  o.kind = OP_POOL_GEMM;
-  o.pg = *a;
-  ((Plan*)p)->ops.push_back(o);
-  return 0;
-}
 
 extern "C" int dml_plan_add_expand_reduce(void* p, const DmlExpandReduceArgs* a) {
   Op o{};
   o.kind = OP_EXP_RED;
   o.er = *a;
-  ((Plan*)p)->ops.push_back(o);
-  return 0;
-}
-extern "C" int dml_plan_add_block(void* p, const DmlBlockArgs* a) {
-  Op o{};
-  o.kind = OP_BLOCK;
-  o.blk = *a;
   ((Plan*)p)->ops.push_back(o);
   return 0;
 }

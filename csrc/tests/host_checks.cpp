@@ -99,22 +99,10 @@ int main() {
   CHECK(dml_conv(&a, 35, nullptr) != 0);        // an unassigned id inside 10..63
   CHECK(dml_conv(&a, 90, nullptr) != 0);        // past the table
   CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
-  // shifted-pixel configs (64..): stride-1 "same" convs only, halo within the config's LDS rows
-  CHECK(dml_conv_v2_bn(64) == 128 && dml_conv_v2_bn(68) == 64 && dml_conv_v2_bn(70) == 0);
-  a.ph = 0;
-  CHECK(dml_conv(&a, 64, nullptr) != 0);        // valid (not same) padding
-  CHECK(std::string(dml_last_error()).find("same padding") != std::string::npos);
-  a = conv_args(64, 64, 3, 3);
-  a.sh = a.sw = 2; a.Ho = a.Wo = 7;
-  CHECK(dml_conv(&a, 65, nullptr) != 0);        // stride 2
-  a = conv_args(48, 64, 3, 3);
-  CHECK(dml_conv(&a, 64, nullptr) != 0);        // Cin % BK
-  a = conv_args(64, 64, 1, 1);
-  CHECK(dml_conv(&a, 66, nullptr) != 0);        // 1 tap < STAGES
-  a = conv_args(64, 64, 5, 5);
-  a.H = a.W = a.Ho = a.Wo = 60;
-  CHECK(dml_conv(&a, 66, nullptr) != 0);        // 128 + 2*(2*60+2) halo rows > 256
-  CHECK(std::string(dml_last_error()).find("halo") != std::string::npos);
+  CHECK(dml_conv_v2_bn(64) == 0 && dml_conv_v2_bn(68) == 0);   // the removed shifted-pixel ids
+  CHECK(dml_conv(&a, 64, nullptr) != 0);
+  CHECK(dml_conv(&a, 80, nullptr) != 0);        // Winograd without transformed weights
+  CHECK(std::string(dml_last_error()).find("Winograd") != std::string::npos);
   a = conv_args(64, 64, 3, 3);
   a.nseg = 5;
   CHECK(dml_conv(&a, 11, nullptr) != 0);        // too many output segments
@@ -207,42 +195,28 @@ int main() {
   er.ldz = 64;
   CHECK(dml_chain_supported(&er) == 0);            // Z rows narrower than the reduce width
   er.fz = 0; er.ldz = 64; er.res = nullptr;
-  {  // max pool 3x3/2 + 1x1 GEMM: shape gate names what it refuses, the plan refuses it too
-    DmlPoolGemmArgs pg{};
-    pg.p.N = 2; pg.p.H = 71; pg.p.W = 71; pg.p.C = 192; pg.p.ldx = 192; pg.p.Ho = 35; pg.p.Wo = 35;
-    pg.p.k = 3; pg.p.stride = 2;
-    pg.g.N = 2; pg.g.H = 35; pg.g.W = 35; pg.g.Ho = 35; pg.g.Wo = 35; pg.g.Cin = 192; pg.g.kh = pg.g.kw = 1;
-    pg.g.sh = pg.g.sw = 1; pg.g.Cout = 208; pg.g.Kpad = 192; pg.g.ldy = 208; pg.g.y = (void*)&pg;
-    CHECK(dml_pool_gemm_supported(&pg) == 1);
-    pg.p.pad = 1;
-    CHECK(dml_pool_gemm_supported(&pg) == 0);
-    CHECK(std::string(dml_last_error()).find("max 3x3/2") != std::string::npos);
-    pg.p.pad = 0; pg.g.Cout = 200;                    // not a multiple of 16
-    CHECK(dml_pool_gemm_supported(&pg) == 0);
-    pg.g.Cout = 208; pg.g.nseg = 2; pg.g.seg_c0[1] = 72; pg.g.seg_ldy[0] = pg.g.seg_ldy[1] = 208;
-    pg.g.seg_y[0] = pg.g.seg_y[1] = (void*)&pg;
-    CHECK(dml_pool_gemm_supported(&pg) == 0);          // segment boundary off the 16-channel grid
-    pg.g.seg_c0[1] = 64;
-    CHECK(dml_pool_gemm_supported(&pg) == 1);
-    void* plan = dml_plan_create();
-    pg.g.Cin = 128;                                     // not the pooled tensor
-    CHECK(dml_plan_add_pool_gemm(plan, &pg) != 0);
-    CHECK(dml_plan_size(plan) == 0);
-    dml_plan_destroy(plan);
-  }
-  {  // whole fused bottleneck block: only F = 64, C = 4F, 8-aligned strides, y != x
-    DmlBlockArgs b{};
+  {  // Winograd F(2x2, 3x3): the shape gate refuses what the kernel cannot run, dml_conv routes cfg 80
+    DmlConvArgs w{};
     char buf[64];
-    b.x = buf; b.y = buf + 16; b.N = 1; b.H = b.W = 14; b.F = 64;
-    b.ldx = b.ldy = b.ldw1 = 256; b.ldw2 = 576; b.ldw3 = 64;
-    b.F = 128;
-    CHECK(dml_block_fused(&b, nullptr) != 0);      // F = 128 not instantiated
-    b.F = 64; b.ldw2 = 512;
-    CHECK(dml_block_fused(&b, nullptr) != 0);      // 3x3 weights shorter than K = 9F
-    b.ldw2 = 576; b.y = buf;
-    CHECK(dml_block_fused(&b, nullptr) != 0);      // in place: other tiles still read x
-    b.y = buf + 16; b.ldx = 260;
-    CHECK(dml_block_fused(&b, nullptr) != 0);      // unaligned channel stride
+    w.x = buf; w.y = buf; w.N = 2; w.H = w.W = 14; w.Cin = 64; w.ldx = 64; w.kh = w.kw = 3; w.sh = w.sw = 1;
+    w.ph = w.pw = 1; w.Ho = w.Wo = 14; w.Cout = 64; w.ldy = 64; w.K = 576; w.Kpad = 576;
+    CHECK(dml_conv_wino_check(&w) != nullptr);                 // no transformed weights
+    w.wu = buf;
+    CHECK(dml_conv_wino_check(&w) == nullptr);
+    w.ph = w.pw = 0;
+    CHECK(dml_conv_wino_check(&w) != nullptr);                 // valid padding with a 'same' output size
+    w.Ho = w.Wo = 12;
+    CHECK(dml_conv_wino_check(&w) == nullptr);                 // valid 3x3
+    w.sh = w.sw = 2; w.Ho = w.Wo = 6;
+    CHECK(dml_conv_wino_check(&w) != nullptr);                 // stride 2
+    w.sh = w.sw = 1; w.Ho = w.Wo = 12; w.res = buf;
+    CHECK(dml_conv_wino_check(&w) != nullptr);                 // residual epilogue not supported
+    CHECK(dml_conv(&w, 80, nullptr) != 0);                     // dml_conv applies the same gate
+    CHECK(std::string(dml_last_error()).find("residual") != std::string::npos);
+    w.res = nullptr; w.Cin = 60; w.ldx = 60;
+    CHECK(dml_conv_wino_check(&w) != nullptr);                 // channels not a multiple of 8
+    CHECK(dml_conv_v2_bn(80) == 32 && dml_conv_v2_bn(81) == 64 && dml_conv_wino_supported(83) == 64);
+    CHECK(dml_conv_wino_supported(84) == 0);
   }
   dml_set_error(nullptr);
   CHECK(std::string(dml_last_error()).empty());

@@ -28,10 +28,8 @@ SOURCES = [
     CSRC / "kernels" / "misc.hip",
     CSRC / "kernels" / "stem_fused.hip",
     CSRC / "kernels" / "conv_pool.hip",
-    CSRC / "kernels" / "pool_gemm.hip",
     CSRC / "kernels" / "bottleneck_fused.hip",
-    CSRC / "kernels" / "block_fused.hip",
-    CSRC / "kernels" / "conv_shift.hip",
+    CSRC / "kernels" / "conv_wino.hip",
     CSRC / "kernels" / "expand_reduce_chain.hip",
     CSRC / "runtime" / "runtime.hip",
 ]

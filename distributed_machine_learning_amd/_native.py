@@ -30,6 +30,7 @@ class ConvArgs(C.Structure):
         ("seg_y", C.c_void_p * 4),
         ("ksplit", C.c_int), ("split_ld", C.c_int),
         ("rsub", C.c_int), ("rW", C.c_int), ("rHW", C.c_int),
+        ("wu", C.c_void_p),   # Winograd F(2x2, 3x3) weights (cfg 80), ops.pack_wino_weight
     ]
 
 
@@ -98,26 +99,7 @@ class ExpandReduceArgs(C.Structure):
     ]
 
 
-class BlockArgs(C.Structure):
-    _fields_ = [
-        ("x", C.c_void_p), ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p),
-        ("w3", C.c_void_p), ("b3", C.c_void_p), ("y", C.c_void_p),
-        ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("F", C.c_int),
-        ("ldx", C.c_int), ("ldy", C.c_int), ("ldw1", C.c_int), ("ldw2", C.c_int), ("ldw3", C.c_int),
-        ("stamps", C.c_void_p), ("kernel", C.c_int),
-    ]
-
-
-class PoolGemmArgs(C.Structure):
-    _fields_ = [("g", ConvArgs), ("p", PoolArgs)]
-
-
 _SIGS = {
-    "dml_pool_gemm": (C.c_int, [C.POINTER(PoolGemmArgs), C.c_void_p]),
-    "dml_pool_gemm_supported": (C.c_int, [C.POINTER(PoolGemmArgs)]),
-    "dml_plan_add_pool_gemm": (C.c_int, [C.c_void_p, C.POINTER(PoolGemmArgs)]),
-    "dml_block_fused": (C.c_int, [C.POINTER(BlockArgs), C.c_void_p]),
-    "dml_plan_add_block": (C.c_int, [C.c_void_p, C.POINTER(BlockArgs)]),
     "dml_expand_reduce": (C.c_int, [C.POINTER(ExpandReduceArgs), C.c_void_p]),
     "dml_chain_supported": (C.c_int, [C.POINTER(ExpandReduceArgs)]),
     "dml_plan_add_expand_reduce": (C.c_int, [C.c_void_p, C.POINTER(ExpandReduceArgs)]),
@@ -131,7 +113,7 @@ _SIGS = {
     "dml_conv_group": (C.c_int, [C.POINTER(ConvGroupArgs), C.c_int, C.c_void_p]),
     "dml_plan_add_conv_group": (C.c_int, [C.c_void_p, C.POINTER(ConvGroupArgs), C.c_int]),
     "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),
-    "dml_conv_shift_check": (C.c_char_p, [C.POINTER(ConvArgs), C.c_int]),
+    "dml_conv_wino_check": (C.c_char_p, [C.POINTER(ConvArgs)]),
     "dml_conv_v2_bn": (C.c_int, [C.c_int]),
     "dml_conv_v2_init": (C.c_int, []),
     "dml_pool": (C.c_int, [C.POINTER(PoolArgs), C.c_void_p]),
@@ -182,7 +164,7 @@ class NativeError(RuntimeError):
 
 
 ABI_STRUCTS = ("ConvArgs", "PoolArgs", "ConvGroupArgs", "PreprocArgs", "StemArgs", "IncStemArgs", "ConvPoolArgs",
-               "ExpandReduceArgs", "BlockArgs", "PoolGemmArgs")
+               "ExpandReduceArgs")
 
 
 def _check_abi(L) -> None:

@@ -96,6 +96,10 @@ class MsgType(IntEnum):
     STANDBY_SYNC = 73        # full coordinator state snapshot to the standby
     JOB_STATUS = 74
     JOB_STATUS_ACK = 75
+    PUT_MANY_REQUEST = 76    # one PUT of several files (an output bundle): one leader round trip
+    PUT_MANY_REPLY = 77      # {"ok": [names], "failed": [names]}
+    DOWNLOAD_MANY = 78       # leader -> replica: pull these (name, version)s from one outbox
+    DOWNLOAD_MANY_REPLY = 79  # {"ok": {name: versions}, "failed": [names]}
     ERROR = 127
 
 

@@ -119,13 +119,8 @@ class Engine:
         # with the 1x1 conv that is the pool's only reader folded in (InceptionV3 conv2d_4)
         self.conv_pools = self._fusable_conv_pools(fuse_stem)
         self.conv_pool_1x1 = self._foldable_pool_1x1(fuse_stem)
-        # a max pool 3x3/2 whose only reader is the next 1x1 GEMM -> ONE kernel (csrc/kernels/pool_gemm.hip)
-        self.pool_gemm = self._fusable_pool_gemm(fuse_stem)
-        # ResNet stage-2 block boundaries: expand (64 -> 256, + shortcut) and the next
-        # block's reduce (256 -> 64) as ONE kernel (csrc/kernels/bottleneck_fused.hip)
-        # whole identity bottleneck blocks (reduce -> 3x3 -> expand + shortcut) as ONE
-        # kernel (csrc/kernels/block_fused.hip); opt-in (DML_BLOCK_FUSED=1) until it wins
-        self.blocks = self._fusable_blocks(fuse_blocks)
+        # ResNet block boundaries: expand (+ shortcut) and the next block's reduce as ONE
+        # kernel (csrc/kernels/bottleneck_fused.hip / expand_reduce_chain.hip)
         self.exp_red = self._fusable_expand_reduce(fuse_blocks)
         # fused pairs whose Y is otherwise only read at stride 2 store just those pixels
         self.ysub = self._subsampled_y()
@@ -139,15 +134,25 @@ class Engine:
         self._tune_range = tune_range
         self.op_range: Optional[Tuple[int, int]] = None
         if share is not None:
-            self.wdev = share.wdev
+            self.wdev, self.wwino = share.wdev, share.wwino
         else:
             self._upload_weights(weights)
         self._alloc_buffers()
         self._build_plan()
 
     # ------------------------------------------------------------ weights ----
+    def _wino_eligible(self, n: Conv) -> bool:
+        """stride-1 undilated 3x3 with 'same' (1) or 'valid' (0) padding: a Winograd
+        F(2x2, 3x3) candidate (csrc/kernels/conv_wino.hip). DML_WINO=0: none (A/B)."""
+        return (os.environ.get("DML_WINO", "1") != "0" and n is not self.stem and n.kh == 3 and n.kw == 3
+                and n.sh == 1 and n.sw == 1 and n.ph == n.pw and n.ph in (0, 1) and n.cin % 8 == 0
+                and n.cout % 8 == 0 and not n.residual)
+
     def _upload_weights(self, w: Weights) -> None:
+        from ..ops import winograd
+
         self.wdev: Dict[str, Tuple[torch.Tensor, torch.Tensor, int, int, int]] = {}
+        self.wwino: Dict[str, torch.Tensor] = {}
         for n in self.g.nodes:
             if isinstance(n, Conv):
                 k, b = fold_conv(n, w)
@@ -179,6 +184,11 @@ class Engine:
                 wk = pack_conv_weight(k, cin_eff, coutp, kpad)
             else:
                 continue
+            if isinstance(n, Conv) and self._wino_eligible(n):
+                # Winograd F(2x2, 3x3) weights U = G g G^T (fp32, rounded once to bf16) for the
+                # conv_wino.hip candidate (cfg 80); the tuner picks per shape
+                self.wwino[n.name] = torch.from_numpy(winograd.pack_kernel(k)).to(
+                    self.device, torch.bfloat16).reshape(-1).contiguous()
             bias = np.zeros(coutp, np.float32)
             bias[: len(b)] = b
             self.wdev[n.name] = (
@@ -259,38 +269,6 @@ class Engine:
                     out[c.name] = p
         return out
 
-    def _fusable_pool_gemm(self, enabled: bool) -> Dict[str, object]:
-        """{pool name: 1x1 conv} for a max pool 3x3/2 (valid) whose output is read only by the
-        next node, a 1x1 stride-1 conv or sibling-fused 1x1 GEMM (InceptionV3 max_pooling2d_2 ->
-        conv2d_6+conv2d_7+conv2d_9+conv2d_12): the pooled tile goes from LDS straight into the GEMM
-        and the pooled tensor is never written. Opt-in (DML_POOL_GEMM=1): serially it is faster (51.4
-        vs 34.7 + 26.4 us per 64 images, profiles/r3_v9) but in the two-stream pipeline it measured
-        0.1-0.8 % below the two launches (InceptionV3 b128 47.7-48.1k vs 48.1-48.2k img/s): the
-        memory-bound pool alone overlaps the other sub-batch's MFMA-bound convs better than the
-        fused kernel at 2 waves per SIMD does."""
-        if not enabled or self.device.type != "cuda" or os.environ.get("DML_POOL_GEMM", "0") != "1":
-            return {}
-        out: Dict[str, object] = {}
-        nodes = self.g.nodes
-        taken = set(self.conv_pools) | {p.name for p in self.conv_pools.values()}
-        for p, k in zip(nodes, nodes[1:]):
-            if not isinstance(p, Pool) or p.name in taken:
-                continue
-            if (p.mode, p.k, p.stride, p.pad, p.relu, p.out_coff) != ("max", 3, 2, 0, False, 0):
-                continue
-            users = [n for n in nodes if p.out in (getattr(n, "inp", None), getattr(n, "residual", None))]
-            if users != [k] or not isinstance(k, (Conv, FusedConv)) or k.inp != p.out:
-                continue
-            m0 = k.members[0] if isinstance(k, FusedConv) else k
-            if not (m0.kh == m0.kw == 1 and m0.sh == m0.sw == 1 and (getattr(k, "in_coff", 0) or 0) == 0
-                    and getattr(k, "residual", None) is None and not getattr(k, "out_f32", False)
-                    and k.cout % 16 == 0 and k.cout <= 256 and self.g.shape(p.out)[2] % 32 == 0):
-                continue
-            if isinstance(k, FusedConv) and any(m.cout % 16 for m in k.members):
-                continue
-            out[p.name] = k
-        return out
-
     def _foldable_pool_1x1(self, enabled: bool) -> Dict[str, Conv]:
         """{conv name: 1x1 conv} for fused conv+pool pairs whose pool output is read only by
         a 1x1 stride-1 conv (64 -> c4, c4 % 16 == 0, <= 128, ReLU, no residual): the conv_pool
@@ -307,40 +285,6 @@ class Engine:
                     and k.residual is None and not k.out_f32 and k.in_coff == 0 and k.out_coff == 0
                     and k.cout % 16 == 0 and k.cout <= 128 and max(getattr(k, "dh", 1), 1) == 1):
                 out[c_name] = k
-        return out
-
-    def _fusable_blocks(self, enabled: bool) -> Dict[str, Tuple[Conv, Conv, Conv]]:
-        """{reduce name: (reduce, 3x3, expand)} for identity bottleneck blocks the
-        fused block kernel supports: 1x1 s1 C -> F (ReLU), 3x3 s1 pad 1 F -> F
-        (ReLU), 1x1 s1 F -> C + the block input as shortcut (ReLU), F = 64, where
-        the two intermediates have no other reader."""
-        if not enabled or self.device.type != "cuda" or os.environ.get("DML_BLOCK_FUSED", "0") != "1":
-            return {}
-        nodes = self.g.nodes
-        readers: Dict[str, List] = {}
-        for n in nodes:
-            for src in (getattr(n, "inp", None), getattr(n, "residual", None)):
-                if src:
-                    readers.setdefault(src, []).append(n)
-        out: Dict[str, Tuple[Conv, Conv, Conv]] = {}
-        for r, c, e in zip(nodes, nodes[1:], nodes[2:]):
-            if not all(isinstance(t, Conv) for t in (r, c, e)):
-                continue
-            f, C4 = r.cout, r.cin
-            if not (f == 64 and C4 == 4 * f and r.kh == r.kw == 1 and r.sh == r.sw == 1 and r.relu
-                    and r.residual is None and r.in_coff == 0 and r.out_coff == 0 and not r.out_f32):
-                continue
-            if not (c.inp == r.out and c.kh == c.kw == 3 and c.sh == c.sw == 1 and c.ph == c.pw == 1
-                    and c.cin == c.cout == f and c.relu and c.residual is None and c.in_coff == 0
-                    and c.out_coff == 0):
-                continue
-            if not (e.inp == c.out and e.kh == e.kw == 1 and e.sh == e.sw == 1 and e.cin == f and e.cout == C4
-                    and e.relu and e.residual == r.inp and e.res_sub == 1 and e.in_coff == 0 and e.out_coff == 0
-                    and not e.out_f32):
-                continue
-            if readers.get(r.out) != [c] or readers.get(c.out) != [e] or self.cbuf_of(r.inp) != C4:
-                continue
-            out[r.name] = (r, c, e)
         return out
 
     def cbuf_of(self, name: str) -> int:
@@ -427,9 +371,7 @@ class Engine:
         taken = {t.name for t in (self.stem, self.stem_conv2, self.stem_pool, self.stem_1x1) if t is not None}
         taken |= set(self.conv_pools) | {p.name for p in self.conv_pools.values()}
         taken |= {k.name for k in self.conv_pool_1x1.values()}
-        taken |= set(self.pool_gemm) | {k.name for k in self.pool_gemm.values()}
         taken |= set(self.exp_red) | {r.name for r in self.exp_red.values()}
-        taken |= {t.name for trip in self.blocks.values() for t in trip}
         return conv_group_runs(self.g, taken, N.GROUP_MAX, N.GROUP_POOL_MAX)
 
     def _subsampled_y(self) -> Dict[str, int]:
@@ -481,7 +423,7 @@ class Engine:
         # position: the first node's inputs stay live through the second node, so
         # the second's output can never be handed a buffer the kernel still reads.
         index = {getattr(n, "name", None): i for i, n in enumerate(nodes)}
-        pairs = {**self.conv_pools, **self.exp_red, **self.pool_gemm}
+        pairs = {**self.conv_pools, **self.exp_red}
         for c_name, k in self.conv_pool_1x1.items():  # conv + pool + folded 1x1 end at the 1x1
             pairs[c_name] = k
             first_def[k.out] = min(first_def[k.out], index[c_name])
@@ -493,10 +435,6 @@ class Engine:
             for src in (first.inp, getattr(first, "residual", None)):
                 if src:
                     last_use[src] = max(last_use[src], index[second.name])
-        # a fused block runs at its reduce's position: its output Y is live from there
-        # (never sharing a buffer with a tensor read between the reduce and the expand)
-        for r_name, (r, c, e) in self.blocks.items():
-            first_def[e.out] = min(first_def[e.out], index[r_name])
         # a conv group runs at its first member's position: every member's input
         # stays live through the last member
         for grp in self.conv_groups:
@@ -669,8 +607,6 @@ class Engine:
         skip |= {p.name for p in self.conv_pools.values()}
         skip |= {k.name for k in self.conv_pool_1x1.values()}
         skip |= {r.name for r in self.exp_red.values()}
-        skip |= {k.name for k in self.pool_gemm.values()}
-        skip |= {t.name for (_, c, e) in self.blocks.values() for t in (c, e)}
         groups = {grp[0].name: grp for grp in self.conv_groups if grp[0].name in self.group_cfg}
         for grp in groups.values():
             skip |= {m.name for m in grp[1:]}
@@ -693,20 +629,6 @@ class Engine:
                 self._keep.append(ga)
                 self.op_names.append("|".join(m.name for m in grp))
                 continue
-            if n.name in self.blocks:
-                r, c, e = self.blocks[n.name]
-                w1, b1, _, kp1, _ = self.wdev[r.name]
-                w2, b2, _, kp2, _ = self.wdev[c.name]
-                w3, b3, _, kp3, _ = self.wdev[e.name]
-                h, w, _ = g.shape(r.inp)
-                ba = N.BlockArgs(self.buf[r.inp].data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
-                                 b2.data_ptr(), w3.data_ptr(), b3.data_ptr(), self.buf[e.out].data_ptr(), B, h, w,
-                                 r.cout, self.cbuf[r.inp], self.cbuf[e.out], kp1, kp2, kp3, None,
-                                 int(os.environ.get("DML_BLOCK_KERNEL", "0")))
-                N.check(L.dml_plan_add_block(plan, C.byref(ba)), "plan fused block")
-                self._keep.append(ba)
-                self.op_names.append(f"{r.name}+{c.name}+{e.name}")
-                continue
             if n.name in self.exp_red:
                 r = self.exp_red[n.name]
                 w3, b3, _, kp3, _ = self.wdev[n.name]
@@ -724,14 +646,6 @@ class Engine:
                     ea.ysub, ea.yH, ea.yW = self.ysub[n.out], h, w
                 N.check(L.dml_plan_add_expand_reduce(plan, C.byref(ea)), "plan expand+reduce")
                 self.op_names.append(f"{n.name}+{r.name}")
-                continue
-            if n.name in self.pool_gemm:
-                k = self.pool_gemm[n.name]
-                pg = N.PoolGemmArgs(self._conv_args(k), self._pool_args(n))
-                N.check(L.dml_plan_add_pool_gemm(plan, C.byref(pg)), f"plan pool+gemm {n.name}")
-                self._keep.append(pg)
-                self.op_cfg[k.name] = -1
-                self.op_names.append(f"{n.name}+{k.name}")
                 continue
             if n.name in self.conv_pools:
                 p = self.conv_pools[n.name]
@@ -821,6 +735,8 @@ class Engine:
         if n.residual and n.res_sub > 1 and n.residual not in self.ysub:  # strided shortcut (models/optimize.py)
             rh, rw, _ = g.shape(n.residual)
             a.rsub, a.rW, a.rHW = n.res_sub, rw, rh * rw
+        if n.name in self.wwino:
+            a.wu = self.wwino[n.name].data_ptr()
         return a
 
     # ---------------------------------------------------------------- run ----

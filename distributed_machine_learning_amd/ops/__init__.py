@@ -15,7 +15,9 @@ import torch
 from .. import _native as N
 
 __all__ = ["conv2d_nhwc", "conv_group", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight",
-           "resnet_stem", "inception_stem", "conv3x3_pool", "expand_reduce", "block_fused"]
+           "resnet_stem", "inception_stem", "conv3x3_pool", "expand_reduce", "pack_wino_weight", "WINO_CFG"]
+
+WINO_CFG = 80  # DML_WINO_CFG: the Winograd F(2x2, 3x3) kernel (csrc/kernels/conv_wino.hip)
 
 
 def _r(x, m):
@@ -34,16 +36,27 @@ def pack_weight(w_oihw: torch.Tensor, cin_eff: Optional[int] = None) -> Tuple[to
     return out.to(torch.bfloat16), K, _r(K, 64)
 
 
+def pack_wino_weight(w_oihw: torch.Tensor) -> torch.Tensor:
+    """OIHW fp32 3x3 -> the Winograd F(2x2, 3x3) weights of conv_wino.hip: U = G g G^T
+    computed in fp32, rounded once to bf16, packed [Cout/64][Cin/32][16][4][64][8]
+    (ops/winograd.py)."""
+    from . import winograd
+
+    k = w_oihw.permute(2, 3, 1, 0).float().cpu().numpy()  # -> HWIO
+    return torch.from_numpy(winograd.pack_kernel(k)).to(torch.bfloat16).reshape(-1)
+
+
 def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cout: int, kh: int, kw: int,
                 stride=(1, 1), pad=(0, 0), relu: bool = False, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, out_coff: int = 0, in_coff: int = 0, cin: Optional[int] = None,
                 out_f32: bool = False, cfg: int = -1, K: Optional[int] = None, dilation=(1, 1),
                 out_hw: Optional[Tuple[int, int]] = None, ksplit: int = 1,
-                defer: Optional[list] = None) -> torch.Tensor:
+                defer: Optional[list] = None, wu: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x: NHWC bf16 [N,H,W,Cbuf] (Cbuf % 8 == 0). Returns/updates NHWC output.
     defer: a list to append the ConvArgs to instead of launching (conv_group).
     ksplit > 1 (fp32 output, v2 cfg): returns the [ksplit, N, Ho, Wo, C] split-K
-    partial sums (slice 0 carries the bias); their sum is the convolution."""
+    partial sums (slice 0 carries the bias); their sum is the convolution.
+    wu: Winograd weights (pack_wino_weight, on the device) for cfg WINO_CFG."""
     n, h, w_, cbuf = x.shape
     cin = cin if cin is not None else cbuf - in_coff
     ho = (h + 2 * pad[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
@@ -71,6 +84,8 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
                    dilation[0], dilation[1])
     if parts is not None:
         a.ksplit, a.split_ld = ksplit, out.numel()
+    if wu is not None:
+        a.wu = wu.data_ptr()
     if residual is not None and residual.shape[1] != ho:  # shortcut read at stride rs (full-res grid)
         rs = residual.shape[1] // ho
         assert residual.shape[1] == ho * rs and residual.shape[2] == wo * rs and residual.is_contiguous()
@@ -257,29 +272,6 @@ def expand_reduce(x: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, res: Opti
     N.check(N.lib().dml_expand_reduce(C.byref(a), N.stream_ptr()), "dml_expand_reduce")
     y._keep = (b3p, b1p)
     return y, z
-
-
-def block_fused(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
-                w3: torch.Tensor, b3: torch.Tensor, out: Optional[torch.Tensor] = None,
-                stamps: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
-    """A whole identity bottleneck block in one kernel (csrc/kernels/block_fused.hip):
-    y = relu(1x1(F -> C) of relu(3x3(F -> F) of relu(1x1(C -> F) of x)) + x), C = 4F.
-    x: bf16 NHWC [N, H, W, C]; w1 [>=F][>=C], w2 [>=F][>=9F] (r, s, c), w3 [>=C][>=F]
-    packed (pack_weight); biases fp32. Returns bf16 NHWC [N, H, W, C].
-    kernel: 0 = persistent warp-specialised (default), 1 = phase-serialised
-    (``stamps``: per-workgroup phase timestamps, phase-serialised form only)."""
-    n, h, w, c = x.shape
-    f = c // 4
-    y = out if out is not None else torch.empty_like(x)
-    bs = [b.to(x.device, torch.float32).contiguous() for b in (b1, b2, b3)]
-    assert x.is_contiguous() and y.is_contiguous() and all(t.is_contiguous() for t in (w1, w2, w3))
-    assert w1.shape[0] >= f and w2.shape[0] >= f and w3.shape[0] >= c and bs[0].numel() >= f and bs[2].numel() >= c
-    a = N.BlockArgs(x.data_ptr(), w1.data_ptr(), bs[0].data_ptr(), w2.data_ptr(), bs[1].data_ptr(), w3.data_ptr(),
-                    bs[2].data_ptr(), y.data_ptr(), n, h, w, f, x.shape[-1], y.shape[-1], w1.shape[1], w2.shape[1],
-                    w3.shape[1], stamps.data_ptr() if stamps is not None else None, kernel)
-    N.check(N.lib().dml_block_fused(C.byref(a), N.stream_ptr()), "dml_block_fused")
-    y._keep = bs
-    return y
 
 
 def fused_conv1x1(x: torch.Tensor, members, stride: int = 1, cfg: int = -1) -> None:

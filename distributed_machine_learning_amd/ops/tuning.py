@@ -23,9 +23,9 @@ from .. import _native as N
 
 V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33, 34, 36, 37,
            38, 39)  # 23..37: BK32; 38 / 39: 3-stage BK64 64-channel tiles (r3)
-# shifted-pixel stride-1 "same" conv configs (csrc/kernels/conv_shift.hip): candidates
-# of the shapes dml_conv_shift_check accepts
-SHIFT_CFGS = (64, 65, 66, 67, 68, 69)
+# Winograd F(2x2, 3x3) (csrc/kernels/conv_wino.hip): a candidate of the stride-1 3x3
+# convs the engine gave transformed weights (ConvArgs.wu) and dml_conv_wino_check accepts
+WINO_CFG = 80
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))
@@ -42,14 +42,14 @@ _lock = threading.Lock()
 CAND_TAG = os.environ.get("DML_TUNING_TAG", "c5cold")
 
 
-def shape_key(a: N.ConvArgs, shift: bool = True) -> str:
-    """Cache key of a conv shape (shift: mark the shapes timed with the
-    shifted-pixel candidates; group keys leave it out, groups never use them)."""
+def shape_key(a: N.ConvArgs, wino: bool = True) -> str:
+    """Cache key of a conv shape (wino: mark the shapes timed with the Winograd
+    candidate; group keys leave it out, groups never use it)."""
     return (f"n{a.N}_h{a.H}_w{a.W}_c{a.Cin}_ld{a.ldx}_k{a.kh}x{a.kw}_s{a.sh}x{a.sw}_p{a.ph}x{a.pw}"
             f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}_d{max(a.dh, 1)}x{max(a.dw, 1)}"
             + (f"_ks{a.ksplit}" if a.ksplit > 1 else "")
             + (f"_rs{a.rsub}" if a.rsub > 1 else "")
-            + ("_sh1" if shift and shift_cfgs(a) else "")
+            + ("_wg1" if wino and wino_ok(a) else "")
             + "_" + CAND_TAG)
 
 
@@ -84,13 +84,12 @@ def _excluded() -> set:
     return {int(c) for c in v.split(",") if c.strip()}
 
 
-def shift_cfgs(a: N.ConvArgs) -> List[int]:
-    """The shifted-pixel configs that can run conv ``a`` (host-side shape check
-    of the native library; never a device call). DML_NO_SHIFT=1: none (A/B)."""
-    if os.environ.get("DML_NO_SHIFT", "0") == "1" or a.sh != 1 or a.sw != 1 or a.kh * a.kw < 3:
-        return []
-    L = N.lib()
-    return [c for c in SHIFT_CFGS if L.dml_conv_shift_check(C.byref(a), c) is None]
+def wino_ok(a: N.ConvArgs) -> bool:
+    """Conv ``a`` can run on the Winograd kernel: it carries transformed weights and
+    passes the library's host-side shape gate (never a device call)."""
+    if not a.wu or a.kh != 3 or a.kw != 3 or a.sh != 1 or a.sw != 1:
+        return False
+    return N.lib().dml_conv_wino_check(C.byref(a)) is None
 
 
 def valid_cfgs(a: N.ConvArgs) -> List[int]:
@@ -98,7 +97,8 @@ def valid_cfgs(a: N.ConvArgs) -> List[int]:
         return []
     ex = _excluded()
     cands = [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)] + (list(LATE_RES_CFGS) if a.res else [])
-    cands += shift_cfgs(a)
+    if wino_ok(a):
+        cands.append(WINO_CFG)
     return [c for c in cands if c not in ex]
 
 
@@ -238,8 +238,8 @@ def autotune_group(args: List[N.ConvArgs], cfgs: List[int], pools: Sequence[N.Po
     grid, or -1 when running them one after another, each conv on its own tuned
     tile ``cfgs``, is faster."""
     k = group_key(args, pools)
-    if any(c in SHIFT_CFGS for c in cfgs):  # the sequential alternative got faster tiles: re-decide
-        k += "_sh1"
+    if any(c == WINO_CFG for c in cfgs):  # the sequential alternative has a Winograd member: re-decide
+        k += "_wg1"
     cache = load_cache() if cache is None else cache
     if k in cache and (cache[k] == -1 or cache[k] in GROUP_CFGS):  # -1: grouping measured slower; a removed tile is re-timed
         return cache[k]

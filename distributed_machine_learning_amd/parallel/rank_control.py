@@ -205,6 +205,33 @@ class RankControl:
             time.sleep(0.1)
         raise RuntimeError(f"store put {name}: {err}")
 
+    def store_put_many_async(self, items, done: Callable[[List[str], List[str]], None],
+                             deadline_s: float = 60.0) -> None:
+        """PUT a bundle of files (store.service.put_many: one leader round trip) without
+        blocking the caller; files the store refused are retried (a store-leader change
+        mid-PUT) until ``deadline_s``. ``done(stored, failed)`` runs on the control loop."""
+        async def go():
+            remaining = dict(items)
+            stored: List[str] = []
+            t0, err = time.monotonic(), ""
+            while remaining and time.monotonic() - t0 < deadline_s:
+                try:
+                    ok, _, err = await self.node.store.put_many(list(remaining.items()))
+                except Exception as e:  # leader unreachable mid-failover
+                    ok, err = [], str(e)
+                for n in ok:
+                    if remaining.pop(n, None) is not None:
+                        stored.append(n)
+                if remaining:
+                    await asyncio.sleep(0.1)
+            if remaining:
+                log.error("rank %d: store put of %d files failed: %s", self.grank, len(remaining), err)
+            try:
+                done(stored, list(remaining))
+            except Exception:
+                log.exception("rank %d: bundle completion callback failed", self.grank)
+        asyncio.run_coroutine_threadsafe(go(), self.loop)
+
     def store_loader(self, names: List[str]) -> Dict[str, Optional[bytes]]:
         """Fetch store images; ``name@v`` is that version exactly (pinned at submit)."""
         async def fetch_all():

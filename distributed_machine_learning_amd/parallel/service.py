@@ -340,22 +340,35 @@ class OutputWriter:
     """This rank's result files, off the serve loop: a thread renders each
     finished batch (native renderer, byte-identical to the reference's
     indent-4 JSON), writes output_<job>_<batch>_<host>.json into ``out_dir``
-    and/or PUTs it into the store, then calls ``on_written(batch, tag)`` —
-    the service reports a batch only after that (reference: PUT, then ACK,
-    worker.py:518-537). A write that fails is logged and still reported (the
-    job must finish); the failure count is kept."""
+    and/or stores it, then calls ``on_written(batch, tag)`` — the service
+    reports a batch only after that (reference: PUT, then ACK,
+    worker.py:518-537). Storing is pipelined: with ``put_many_async`` the
+    finished outputs that are ready are PUT as ONE bundle (up to ``bundle``
+    files; store.service.put_many: one leader round trip for all of them) and
+    up to ``max_inflight`` bundles are in flight while the next ones render;
+    each batch is reported once ITS file is durable (the reference PUT
+    fire-and-forget and ACKed at once). ``put`` (one synchronous PUT per file)
+    stays for callers without the async path. A write that fails is logged and
+    still reported (the job must finish); the failure count is kept."""
 
     def __init__(self, out_dir: Optional[str], put: Optional[Callable[[str, bytes], None]] = None,
-                 host_tag: str = "node", threads: int = 1):
+                 host_tag: str = "node", threads: int = 1,
+                 put_many_async: Optional[Callable[[List[Tuple[str, bytes]], Callable], None]] = None,
+                 bundle: int = 16, max_inflight: int = 4):
         self.out_dir, self.put, self.host_tag = out_dir, put, host_tag
+        self.put_many_async, self.bundle = put_many_async, max(1, bundle)
         if out_dir:
             os.makedirs(out_dir, exist_ok=True)
-        self.renderer = BatchRenderer()
+        self.renderer = BatchRenderer()   # thread-safe: per-thread scratch buffers
         self.q: "queue.Queue" = queue.Queue()
         self.written = 0
         self.failed = 0
         self.bytes = 0
         self.busy_s = 0.0
+        self.bundles = 0
+        self._slots = threading.BoundedSemaphore(max(1, max_inflight))
+        self._cv = threading.Condition()
+        self._inflight = 0
         self._threads = [threading.Thread(target=self._loop, daemon=True, name=f"output-writer-{i}")
                          for i in range(threads)]
         for t in self._threads:
@@ -363,41 +376,102 @@ class OutputWriter:
 
     @property
     def enabled(self) -> bool:
-        return bool(self.out_dir) or self.put is not None
+        return bool(self.out_dir) or self.put is not None or self.put_many_async is not None
 
     def submit(self, b: Batch, idx: np.ndarray, p: np.ndarray, grank: int,
                on_written: Optional[Callable[..., None]] = None, tag=None) -> None:
         self.q.put((b, idx, p, grank, on_written, tag))
 
+    def _render(self, item) -> Optional[Tuple[str, bytes]]:
+        b, idx, p, g, _, _ = item
+        try:
+            data = self.renderer.render(b.images, idx, p)
+            name = output_name(b.job_id, b.batch_id, f"{self.host_tag}-rank{g}")
+            if self.out_dir:
+                with open(os.path.join(self.out_dir, name), "wb") as f:
+                    f.write(data)
+            self.bytes += len(data)
+            return name, data
+        except Exception as e:  # a failed write is logged, never silently skipped
+            self.failed += 1
+            log.error("output %s:%s not written: %s", b.job_id, b.batch_id, e)
+            return None
+
+    @staticmethod
+    def _report(item) -> None:
+        b, _, _, _, on_written, tag = item
+        if on_written is not None:
+            on_written(b, tag)
+
     def _loop(self) -> None:
         while True:
-            item = self.q.get()
-            if item is None:
+            first = self.q.get()
+            if first is None:
                 self.q.task_done()
                 return
-            b, idx, p, g, on_written, tag = item
+            items, stop = [first], False
+            if self.put_many_async is not None:  # every ready output joins the bundle
+                while len(items) < self.bundle:
+                    try:
+                        it = self.q.get_nowait()
+                    except queue.Empty:
+                        break
+                    if it is None:
+                        stop = True
+                        break
+                    items.append(it)
             t0 = time.perf_counter()
-            try:
-                data = self.renderer.render(b.images, idx, p)
-                name = output_name(b.job_id, b.batch_id, f"{self.host_tag}-rank{g}")
-                if self.out_dir:
-                    with open(os.path.join(self.out_dir, name), "wb") as f:
-                        f.write(data)
-                if self.put is not None:
-                    self.put(name, data)
-                self.written += 1
-                self.bytes += len(data)
-            except Exception as e:  # a failed write is logged, never silently skipped
-                self.failed += 1
-                log.error("output %s:%s not written: %s", b.job_id, b.batch_id, e)
+            rendered = [self._render(it) for it in items]
+            if self.put_many_async is not None:
+                ok_items = [(it, r) for it, r in zip(items, rendered) if r is not None]
+                for it, r in zip(items, rendered):
+                    if r is None:
+                        self._report(it)
+                if ok_items:
+                    self._slots.acquire()   # at most max_inflight bundles in flight
+                    with self._cv:
+                        self._inflight += 1
+                    self.bundles += 1
+                    self.put_many_async([r for _, r in ok_items],
+                                        lambda ok, bad, ok_items=ok_items: self._bundle_done(ok_items, bad))
+            else:
+                for it, r in zip(items, rendered):
+                    if r is not None:
+                        try:
+                            if self.put is not None:
+                                self.put(*r)
+                            self.written += 1
+                        except Exception as e:
+                            self.failed += 1
+                            log.error("output %s not stored: %s", r[0], e)
+                    self._report(it)
             self.busy_s += time.perf_counter() - t0
-            if on_written is not None:
-                on_written(b, tag)
-            self.q.task_done()
+            for _ in items:
+                self.q.task_done()
+            if stop:
+                self.q.task_done()
+                return
 
-    def flush(self) -> None:
-        """Block until every queued file is written."""
+    def _bundle_done(self, ok_items, failed_names) -> None:
+        """(the store's thread) a bundle's PUT finished: report its batches."""
+        bad = set(failed_names)
+        for it, (name, _) in ok_items:
+            if name in bad:
+                self.failed += 1
+                log.error("output %s not stored", name)
+            else:
+                self.written += 1
+            self._report(it)
+        with self._cv:
+            self._inflight -= 1
+            self._cv.notify_all()
+        self._slots.release()
+
+    def flush(self, timeout: float = 300.0) -> None:
+        """Block until every queued file is written and every bundle is durable."""
         self.q.join()
+        with self._cv:
+            self._cv.wait_for(lambda: self._inflight == 0, timeout)
 
     def close(self) -> None:
         for _ in self._threads:

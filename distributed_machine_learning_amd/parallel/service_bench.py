@@ -1,8 +1,10 @@
 """BASELINE configs 4 and 5 as a measured run of the real serving product:
 concurrent ResNet50 + InceptionV3 jobs served by the elastic collective service
-(parallel/service.py) on every rank of the job, OUTPUTS ON (every batch's
-output_<job>_<batch>_<host>.json rendered and written by the rank that ran it
-before the batch counts as done), optionally with injected rank kills.
+(parallel/service.py) on every rank of the job, with the product's control plane
+(RankControl: SWIM, election, the replicated store) and OUTPUTS ON: every batch's
+output_<job>_<batch>_<host>.json is rendered by the rank that ran it and PUT into
+the replicated store (bundled, pipelined) before the batch counts as done —
+rank_main's configuration — optionally with injected rank kills.
 
 Used by ``bench.py`` (the ``service`` sub-record of the driver's JSON line) and
 ``tools/serve_bench.py``. Call it in every rank process after the process has
@@ -30,8 +32,8 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
 
     from ..serving.jobs import MODELS
     from .elastic import ElasticGroup
-    from .fd_thread import RankFailureDetector
     from .rank_backend import GpuRankBackend
+    from .rank_control import RankControl
     from .service import CollectiveService, OutputWriter, ReplicatedCoordinator
 
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")  # aborts are ours (parallel/elastic.py)
@@ -41,14 +43,19 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                GpuRankBackend(device, batch_sizes, cap=cap, arena_images=4 * cap, n_synth=2 * cap))
     eg = ElasticGroup(rank, world, store_path=rdzv, backend=comm, device=device if comm == "nccl" else None,
                       timeout_s=120, data_backend=data_backend)
-    fd = RankFailureDetector(rank, world, swim_base, on_dead=eg.dead.add, on_alive=eg.joiners.add).start()
+    # the product's control plane (serving/rank_main.py): SWIM + election + the replicated
+    # store; every output is PUT into the store (bundled, pipelined) before its batch counts
+    store_root = os.path.join(os.environ.get("DML_RDZV_DIR", "/tmp"), os.path.basename(rdzv) + "_store")
+    ctl = RankControl(rank, world, swim_base, store_dir=os.path.join(store_root, f"rank{rank}"),
+                      replication=min(4, world), on_dead=eg.dead.add, on_alive=eg.joiners.add).start()
     kr, ks = -1, -1
     for r, s in kills:
         if r == rank:
             kr, ks = r, s
     coord = ReplicatedCoordinator(batch_sizes, cap=cap, host_tag="mi355x", depth=depth)
-    writer = OutputWriter(os.path.join(out_dir, f"rank{rank}") if out_dir else None, host_tag="mi355x")
-    svc = CollectiveService(eg, backend, coord, writer=writer, kill_rank=kr, kill_at_step=ks,
+    writer = OutputWriter(os.path.join(out_dir, f"rank{rank}") if out_dir else None,
+                          put_many_async=ctl.store_put_many_async, host_tag="mi355x")
+    svc = CollectiveService(eg, backend, coord, control=ctl, writer=writer, kill_rank=kr, kill_at_step=ks,
                             on_device=(comm == "nccl"), watchdog_s=300)
     if svc.is_coordinator():
         if resnet_images:
@@ -100,8 +107,11 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                 "batch_sizes": dict(batch_sizes),
                 "fair_share_splits": [s for _, s in coord.split_log][:16],
                 "batches_per_rank": per_rank,
-                "outputs": {"files": int(sum(int(v[1]) for v in allsv)), "failed": int(sum(int(v[2]) for v in allsv)),
+                "outputs": {"files_stored": int(sum(int(v[1]) for v in allsv)),
+                            "failed": int(sum(int(v[2]) for v in allsv)),
                             "bytes": int(sum(int(v[3]) for v in allsv)), "dir": out_dir or None,
+                            "store": f"replicated store, R = {min(4, world)}, bundled PUTs (put_many)",
+                            "put_bundles_coordinator": writer.bundles,
                             "writer_busy_s_coordinator": round(writer.busy_s, 3)},
                 "steps": steps, "max_batches_per_step": svc.batches_per_step_max,
                 "rebuilds": svc.rebuilds, "preempted_batches": coord.preempted, "requeued_batches": coord.requeued,
@@ -121,11 +131,13 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
             dist.broadcast_object_list(box, src=eg.group_rank_of(svc.coordinator_rank()))
             rec = box[0]
     finally:
-        fd.stop()
         writer.close()
+        ctl.stop()
         eg.close()
-        if out_dir and rank == 0:
-            shutil.rmtree(out_dir, ignore_errors=True)
+        if rank == 0:
+            if out_dir:
+                shutil.rmtree(out_dir, ignore_errors=True)
+            shutil.rmtree(store_root, ignore_errors=True)
     return rec
 
 

@@ -94,7 +94,7 @@ class BatchRenderer:
         off = np.zeros(len(parts) + 1, np.int64)
         np.cumsum([len(p) for p in parts], out=off[1:])
         self.cls_off = off
-        self.buf = C.create_string_buffer(1 << 20)
+        self._tls = threading.local()   # per-thread scratch buffer: the ctypes call releases the GIL
         self.native = self.lib is not None
 
     def _key(self, name: str) -> bytes:
@@ -132,7 +132,9 @@ class BatchRenderer:
         blob = b"".join(keys)
         k = top_idx.shape[1] if top_idx.ndim == 2 else 5
         need = 256 + len(blob) + len(keys) * k * 160
-        buf = self.buf if C.sizeof(self.buf) >= need else C.create_string_buffer(need)
+        buf = getattr(self._tls, "buf", None)
+        if buf is None or C.sizeof(buf) < need:
+            buf = self._tls.buf = C.create_string_buffer(max(need, 1 << 20))
         n = self.lib.dml_render_top5_json(len(keys), blob, koff.ctypes.data, rows.ctypes.data, top_idx.ctypes.data,
                                           top_p.ctypes.data, k, self.cls, self.cls_off.ctypes.data, len(self.idx),
                                           buf, C.sizeof(buf))

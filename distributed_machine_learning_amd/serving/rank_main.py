@@ -157,7 +157,7 @@ def rank_main(a: argparse.Namespace) -> int:
     eg.joiners |= {g for g in early_alive if g not in eg.members}
     holder["eg"] = eg
     coord = ReplicatedCoordinator(bs, cap=cap, host_tag="mi355x", depth=a.depth, preempt=not a.no_preempt)
-    writer = OutputWriter(a.out_dir or None, put=ctl.store_put, host_tag="mi355x")
+    writer = OutputWriter(a.out_dir or None, put_many_async=ctl.store_put_many_async, host_tag="mi355x")
     svc = CollectiveService(eg, backend, coord, control=ctl, writer=writer, on_device=(a.comm == "nccl"),
                             watchdog_s=0.0, rejoined=a.rejoin)
     for sig in (signal.SIGINT, signal.SIGTERM):

@@ -34,7 +34,8 @@ class BlobSource:
         self.store = store
         self.outbox: Dict[str, bytes] = {}
 
-    def stage(self, data: bytes) -> str:
+    def stage(self, data) -> str:
+        """Hold ``data`` (bytes, or {name: bytes} for a multi-file PUT) until unstaged."""
         tok = uuid.uuid4().hex
         self.outbox[tok] = data
         return tok
@@ -47,6 +48,11 @@ class BlobSource:
         if op == "outbox":
             data = self.outbox.get(req["token"])
             return [] if data is None else [(0, data)]
+        if op == "outbox_many":  # the named files of a staged bundle, in request order
+            box = self.outbox.get(req["token"])
+            if not isinstance(box, dict) or any(n not in box for n in req["names"]):
+                return []
+            return [(0, box[n]) for n in req["names"]]
         name = req["name"]
         if op == "get":
             v = req.get("version")

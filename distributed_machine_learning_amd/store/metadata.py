@@ -30,6 +30,16 @@ class StoreMetadata:
     def set_node_files(self, node: str, files: Dict[str, List[int]]) -> None:
         self.file_map[node] = {k: sorted(int(x) for x in v) for k, v in files.items()}
 
+    def update_node_files(self, node: str, files: Dict[str, List[int]]) -> None:
+        """Merge a replica's report about SOME of its files (the names it just stored,
+        deleted or re-replicated): name -> its versions there now ([] = gone)."""
+        fm = self.file_map.setdefault(node, {})
+        for k, v in files.items():
+            if v:
+                fm[k] = sorted(int(x) for x in v)
+            else:
+                fm.pop(k, None)
+
     def remove_node(self, node: str) -> Dict[str, List[int]]:
         return self.file_map.pop(node, {})
 

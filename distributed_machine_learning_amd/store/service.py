@@ -40,6 +40,7 @@ class StoreService:
         on = ep.on
         # leader-side
         on(MsgType.PUT_REQUEST, self._l_put)
+        on(MsgType.PUT_MANY_REQUEST, self._l_put_many)
         on(MsgType.DELETE_FILE_REQUEST, self._l_delete)
         on(MsgType.LIST_FILE_REQUEST, self._l_ls)
         on(MsgType.GET_FILE_REQUEST, self._l_get)
@@ -47,6 +48,7 @@ class StoreService:
         on(MsgType.ALL_LOCAL_FILES, self._l_all_local_files)
         # replica-side
         on(MsgType.DOWNLOAD_FILE, self._r_download)
+        on(MsgType.DOWNLOAD_MANY, self._r_download_many)
         on(MsgType.DELETE_FILE, self._r_delete)
         on(MsgType.REPLICATE_FILE, self._r_replicate)
 
@@ -84,6 +86,25 @@ class StoreService:
         if r is None:
             return False, "leader unreachable"
         return r.type == MsgType.PUT_REQUEST_SUCCESS, r.payload.get("error", "")
+
+    async def put_many(self, items: List[Tuple[str, bytes]]) -> Tuple[List[str], List[str], str]:
+        """PUT several files in ONE leader round trip (the service's output bundles):
+        the leader sends each replica one DOWNLOAD_MANY for all its files of the
+        bundle, which it pulls in one blob request. Returns (stored, failed, error);
+        every file is stored on all of its replicas or reported failed (W = all)."""
+        box = dict(items)
+        tok = self.source.stage(box)
+        me = self.ml.get(self.me)
+        blob = me.meta.get("blob") if me is not None else None
+        try:
+            r = await self._leader_request(MsgType.PUT_MANY_REQUEST,
+                                           {"files": list(box), "token": tok, "blob": blob},
+                                           timeout=self.timeout * 3)
+        finally:
+            self.source.unstage(tok)
+        if r is None:
+            return [], list(box), "leader unreachable"
+        return list(r.payload.get("ok", [])), list(r.payload.get("failed", [])), r.payload.get("error", "")
 
     async def put_file(self, path: str, name: str) -> Tuple[bool, str]:
         with open(path, "rb") as f:
@@ -180,7 +201,7 @@ class StoreService:
             for t, r in zip(pending, rs):
                 ok = r is not None and r.type == MsgType.DOWNLOAD_FILE_SUCCESS
                 if r is not None:
-                    self._learn(t, r.payload.get("all_files", {}))
+                    self._learn_delta(t, r.payload)
                 if not ok and not self.ml.is_alive(t):
                     # replica died mid-PUT: substitute another node
                     self.meta.requests.get(name, {}).pop(t, None)
@@ -197,6 +218,63 @@ class StoreService:
             return SUCCESS
         return FAILED
 
+    async def _l_put_many(self, fr: Frame) -> None:
+        """Leader side of put_many: per-file placement and versions as a single PUT,
+        but one DOWNLOAD_MANY per replica node for all of its files; a replica that
+        dies mid-PUT is replaced per file (as _fan_out)."""
+        names = list(dict.fromkeys(fr.payload.get("files", [])))
+        alive = self.storage_nodes()
+        failed = [n for n in names if self.meta.in_progress(n)]
+        todo: Dict[str, List[str]] = {}
+        for n in names:
+            if n in failed:
+                continue
+            t = self.meta.targets_for_put(n, alive)
+            if not t:
+                failed.append(n)
+                continue
+            todo[n] = t
+        versions = {n: self.meta.latest_version(n) + 1 for n in todo}
+        for n, t in todo.items():
+            self.meta.begin(n, t)
+        src = {"source": fr.sender, "token": fr.payload.get("token"), "source_blob": fr.payload.get("blob")}
+        tried = {n: set(t) for n, t in todo.items()}
+        pending = {n: list(t) for n, t in todo.items()}
+        while pending:
+            per_node: Dict[str, List[str]] = {}
+            for n, ts in pending.items():
+                for t in ts:
+                    per_node.setdefault(t, []).append(n)
+            nodes = sorted(per_node)
+            rs = await asyncio.gather(*(self.ep.request(
+                t, MsgType.DOWNLOAD_MANY, {"files": [[n, versions[n]] for n in per_node[t]], **src},
+                timeout=self.timeout) for t in nodes))
+            pending = {}
+            for t, r in zip(nodes, rs):
+                got = r.payload.get("ok", {}) if r is not None else {}
+                if r is not None:
+                    self._learn_delta(t, {"files": got})
+                dead = r is None and not self.ml.is_alive(t)
+                for n in per_node[t]:
+                    if n in got:
+                        self.meta.update(n, t, True)
+                        continue
+                    if dead:  # replica died mid-PUT: substitute another node for this file
+                        self.meta.requests.get(n, {}).pop(t, None)
+                        subs = [x for x in self.meta.place(n, self.storage_nodes(), 64) if x not in tried[n]]
+                        if subs:
+                            tried[n].add(subs[0])
+                            self.meta.requests.setdefault(n, {})[subs[0]] = "Waiting"
+                            pending.setdefault(n, []).append(subs[0])
+                            continue
+                    self.meta.update(n, t, False)
+        ok = []
+        for n in todo:
+            st = self.meta.requests.get(n, {})
+            (ok if st and all(v == SUCCESS for v in st.values()) else failed).append(n)
+            self.meta.finish(n)
+        await self.ep.reply(fr, MsgType.PUT_MANY_REPLY, {"ok": ok, "failed": failed})
+
     async def _l_delete(self, fr: Frame) -> None:
         name = fr.payload["filename"]
         holders = list(self.meta.holders(name))
@@ -210,7 +288,7 @@ class StoreService:
             if r is None:
                 ok = ok and not self.ml.is_alive(h)
                 continue
-            self._learn(h, r.payload.get("all_files", {}))
+            self._learn_delta(h, r.payload)
             ok = ok and r.type == MsgType.DELETE_FILE_ACK
         await self.ep.reply(fr, MsgType.DELETE_FILE_REQUEST_SUCCESS if ok else MsgType.DELETE_FILE_REQUEST_FAIL,
                             {"filename": name})
@@ -232,6 +310,21 @@ class StoreService:
 
     async def _l_all_local_files(self, fr: Frame) -> None:
         self._learn(fr.sender, fr.payload.get("all_files", {}))
+
+    def _learn_delta(self, node: str, payload: dict) -> None:
+        """A replica's reply names only the files it just touched ("files": name ->
+        its versions there now; the reference sent its whole listing with every
+        reply, worker.py:143, which grows with every output file the service PUTs)."""
+        files = payload.get("files")
+        if files is None:  # a peer that still sends its full listing
+            if "all_files" in payload:
+                self._learn(node, payload["all_files"])
+            return
+        self.meta.update_node_files(node, files)
+        if self._round is not None:
+            rd = self._round.setdefault(node, {})
+            for k, v in files.items():
+                rd[k] = sorted(set(rd.get(k, [])) | {int(x) for x in v})
 
     def _learn(self, node: str, files: Dict[str, list]) -> None:
         """A node's current file list (announce / replica reply); while a
@@ -276,7 +369,7 @@ class StoreService:
                 r = await self.ep.request(t, MsgType.REPLICATE_FILE, {"filename": name, "source": src},
                                           timeout=self.timeout)
                 if r is not None and r.type == MsgType.REPLICATE_FILE_SUCCESS:
-                    self._learn(t, r.payload.get("all_files", {}))
+                    self._learn_delta(t, r.payload)
                     n += 1
         return n
 
@@ -293,12 +386,31 @@ class StoreService:
         except (ConnectionError, OSError, asyncio.TimeoutError) as e:
             log.warning("%s: download %s failed: %s", self.me, p["filename"], e)
             mt = MsgType.DOWNLOAD_FILE_FAIL
-        await self.ep.reply(fr, mt, {"filename": p["filename"], "all_files": self.local.all_files()})
+        await self.ep.reply(fr, mt, {"filename": p["filename"], "files": self._delta(p["filename"])})
+
+    def _delta(self, name: str) -> Dict[str, List[int]]:
+        return {name: self.local.versions(name)}
+
+    async def _r_download_many(self, fr: Frame) -> None:
+        p = fr.payload
+        files = [(n, int(v)) for n, v in p.get("files", [])]
+        ok: Dict[str, List[int]] = {}
+        try:
+            items = await self.blobs.fetch(p["source"], {"op": "outbox_many", "token": p.get("token"),
+                                                         "names": [n for n, _ in files]}, addr=p.get("source_blob"))
+            if len(items) == len(files):
+                for (n, v), (_, data) in zip(files, items):
+                    self.local.put_bytes(n, data, version=v)
+                    ok[n] = self.local.versions(n)
+        except (ConnectionError, OSError, asyncio.TimeoutError) as e:
+            log.warning("%s: download of %d files failed: %s", self.me, len(files), e)
+        await self.ep.reply(fr, MsgType.DOWNLOAD_MANY_REPLY,
+                            {"ok": ok, "failed": [n for n, _ in files if n not in ok]})
 
     async def _r_delete(self, fr: Frame) -> None:
         ok = self.local.delete(fr.payload["filename"])
         await self.ep.reply(fr, MsgType.DELETE_FILE_ACK if ok else MsgType.DELETE_FILE_NAK,
-                            {"filename": fr.payload["filename"], "all_files": self.local.all_files()})
+                            {"filename": fr.payload["filename"], "files": self._delta(fr.payload["filename"])})
 
     async def _r_replicate(self, fr: Frame) -> None:
         p = fr.payload
@@ -309,4 +421,4 @@ class StoreService:
             mt = MsgType.REPLICATE_FILE_SUCCESS if items else MsgType.REPLICATE_FILE_FAIL
         except (ConnectionError, OSError, asyncio.TimeoutError):
             mt = MsgType.REPLICATE_FILE_FAIL
-        await self.ep.reply(fr, mt, {"filename": p["filename"], "all_files": self.local.all_files()})
+        await self.ep.reply(fr, mt, {"filename": p["filename"], "files": self._delta(p["filename"])})

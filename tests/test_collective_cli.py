@@ -52,7 +52,7 @@ def _rank_main(grank, world, rdzv, base, out):
     ctl = RankControl(grank, world, base, store_dir=os.path.join(out, "sdfs"), replication=2,
                       on_dead=eg.dead.add).start()
     coord = ReplicatedCoordinator({"ResNet50": 16, "InceptionV3": 16}, cap=16, host_tag="mi355x")
-    writer = OutputWriter(None, put=ctl.store_put, host_tag="mi355x")
+    writer = OutputWriter(None, put_many_async=ctl.store_put_many_async, host_tag="mi355x")
     svc = CollectiveService(eg, FakeRankBackend(cap=16, loader=ctl.store_loader), coord, control=ctl,
                             writer=writer, idle_sleep=0.005)
 

@@ -33,12 +33,12 @@ def _rank_main(grank, world, rdzv, swim_base, out, kill_rank, kill_step, control
         ctl = RankControl(grank, world, swim_base, store_dir=os.path.join(out, "sdfs"), replication=2,
                           on_dead=eg.dead.add).start()
         fd = None
-        put = ctl.store_put
+        put = ctl.store_put_many_async  # the product path: pipelined bundle PUTs (rank_main)
     else:
         ctl, put = None, None
         fd = RankFailureDetector(grank, world, swim_base, on_dead=eg.dead.add).start()
     coord = ReplicatedCoordinator({"ResNet50": 8, "InceptionV3": 8}, cap=8, host_tag="test")
-    writer = OutputWriter(os.path.join(out, "outputs"), put=put, host_tag="test")
+    writer = OutputWriter(os.path.join(out, "outputs"), put_many_async=put, host_tag="test")
     svc = CollectiveService(eg, FakeRankBackend(cap=8, delay_per_image=0.002), coord, control=ctl, writer=writer,
                             kill_rank=kill_rank, kill_at_step=kill_step)
     if svc.is_coordinator():

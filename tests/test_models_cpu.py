@@ -408,24 +408,6 @@ def test_stem_fold_plan_resnet50(monkeypatch):
     assert e.stem_pool is None and k is None
 
 
-def test_pool_gemm_plan_inceptionv3(monkeypatch):
-    """max_pooling2d_2 (3x3/2 valid) feeds only mixed0's sibling 1x1 GEMM: one pool+GEMM op. The
-    stem's max_pooling2d_1 stays with its conv (conv+pool kernel) when that fusion is on."""
-    from distributed_machine_learning_amd.models.engine import Engine
-    from distributed_machine_learning_amd.models.optimize import level_order, optimize
-
-    g, w = build_model("InceptionV3", seed=0)
-    e = Engine.__new__(Engine)
-    e.g, e.device = level_order(optimize(g, stride_push=True, weights=w)), torch.device("cuda")
-    e.conv_pools = {"conv2d_3": next(n for n in e.g.nodes if n.name == "max_pooling2d_1")}
-    assert e._fusable_pool_gemm(True) == {}  # opt-in
-    monkeypatch.setenv("DML_POOL_GEMM", "1")
-    got = {k: v.name for k, v in e._fusable_pool_gemm(True).items()}
-    assert got == {"max_pooling2d_2": "conv2d_6+conv2d_7+conv2d_9+conv2d_12"}
-    monkeypatch.setenv("DML_POOL_GEMM", "0")
-    assert e._fusable_pool_gemm(True) == {}
-
-
 @pytest.mark.parametrize("name,merge_at,want", [
     ("InceptionV3", "conv2d_31+conv2d_32+conv2d_35+conv2d_40", ["mixed3"]),
     ("InceptionV3", "conv2d_71+conv2d_73", ["mixed7"]),

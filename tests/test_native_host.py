@@ -14,10 +14,10 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = shutil.which("hipcc") or ("/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else None)
-SOURCES = ["kernels/conv_dispatch.hip", "kernels/conv_igemm_v2.hip", "kernels/misc.hip",
-           "kernels/stem_fused.hip", "kernels/conv_pool.hip", "kernels/pool_gemm.hip",
-           "kernels/bottleneck_fused.hip", "kernels/block_fused.hip", "kernels/conv_shift.hip", "kernels/expand_reduce_chain.hip",
-           "runtime/runtime.hip", "tests/host_checks.cpp"]
+# every translation unit of libdml_hip.so (the build's own list) plus the host driver
+from distributed_machine_learning_amd import _build  # noqa: E402
+
+SOURCES = [os.path.relpath(str(p), os.path.join(ROOT, "csrc")) for p in _build.SOURCES] + ["tests/host_checks.cpp"]
 SAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
        "-Xarch_host", "-fno-omit-frame-pointer"]
 

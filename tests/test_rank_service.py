@@ -283,7 +283,7 @@ def test_service_bench_record_world2(tmp_path):
     r1 = json.load(open(tmp_path / "svc_1.json"))
     assert r0 == r1 and r0["jobs_done"]
     assert r0["images"] == {"ResNet50": 640, "InceptionV3": 320}
-    assert r0["outputs"]["files"] == 40 + 40 and r0["outputs"]["failed"] == 0
+    assert r0["outputs"]["files_stored"] == 40 + 40 and r0["outputs"]["failed"] == 0
     assert set(r0["batches_per_rank"]) == {"rank0", "rank1"} and sum(r0["batches_per_rank"].values()) == 80
     assert r0["value"] > 0 and r0["p90_latency_ms"]["ResNet50"] >= r0["p50_latency_ms"]["ResNet50"]
     assert not os.path.exists(tmp_path / "svc_out")            # rank 0 removed the output files

@@ -432,75 +432,3 @@ def test_expand_reduce_chain_stage_end(m, f):
     y2, z2 = ops.expand_reduce(xd, w3d, b3d, rd, w1d, b1d, fz=fz)  # the torch-facing wrapper
     torch.cuda.synchronize()
     assert _rel(y2.float().cpu(), y_ref) < 1e-2 and _rel(z2.float().cpu(), z_ref) < 1e-2
-
-
-@pytest.mark.parametrize("n,h,w,c,segs", [
-    (2, 71, 71, 192, [(64, True), (48, True), (64, True), (32, False)]),  # InceptionV3 max_pooling2d_2 + mixed0
-    (3, 17, 13, 64, [(80, True)]),                                          # one plain segment, partial tile
-    (1, 9, 9, 128, [(16, False), (32, True)]),
-])
-def test_pool_gemm_matches_fp32(n, h, w, c, segs):
-    """csrc/kernels/pool_gemm.hip: max pool 3x3/2 valid -> bf16 -> 1x1 GEMM with a segmented
-    epilogue (each segment its own destination buffer, channel offset and ReLU flag)."""
-    torch.manual_seed(11)
-    x = _bf(torch.randn(n, h, w, c))
-    cout = sum(k for k, _ in segs)
-    wt = _bf(torch.randn(cout, c) * (2.0 / c) ** 0.5)
-    b = torch.randn(cout) * 0.1
-    pooled = _bf(F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2).permute(0, 2, 3, 1))
-    ref = pooled @ wt.T + b
-    ho, wo = (h - 3) // 2 + 1, (w - 3) // 2 + 1
-    xd = x.to(torch.bfloat16).cuda().contiguous()
-    kpad = c
-    wd = torch.zeros(_r(cout, 64), kpad, dtype=torch.bfloat16, device="cuda")
-    wd[:cout, :c] = wt.to(torch.bfloat16)
-    bd = torch.zeros(_r(cout, 64), device="cuda")
-    bd[:cout] = b
-    outs = [torch.full((n, ho, wo, k + 8), -7.0, device="cuda", dtype=torch.bfloat16) for k, _ in segs]  # ld > k
-    ga = N.ConvArgs(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), None, outs[0].data_ptr(), n, ho, wo, c, c,
-                    1, 1, 1, 1, 0, 0, ho, wo, cout, c, kpad, segs[0][0] + 8, 0, int(segs[0][1]), 0, 1, 1)
-    if len(segs) > 1:
-        ga.nseg, c0 = len(segs), 0
-        for s, (k, relu) in enumerate(segs):
-            ga.seg_c0[s], ga.seg_ldy[s], ga.seg_relu[s], ga.seg_y[s] = c0, k + 8, int(relu), outs[s].data_ptr()
-            c0 += k
-    pa = N.PoolArgs(xd.data_ptr(), None, n, h, w, c, c, ho, wo, c, 3, 2, 0, 0, 0)
-    a = N.PoolGemmArgs(ga, pa)
-    assert N.lib().dml_pool_gemm_supported(C.byref(a)) == 1
-    N.check(N.lib().dml_pool_gemm(C.byref(a), N.stream_ptr()), "pool_gemm")
-    torch.cuda.synchronize()
-    c0 = 0
-    for (k, relu), o in zip(segs, outs):
-        want = ref[..., c0:c0 + k]
-        want = F.relu(want) if relu else want
-        assert _rel(o[..., :k].float().cpu(), want) < 1e-2, (k, relu)
-        assert (o[..., k:].float() == -7.0).all()  # nothing past the segment's channels
-        c0 += k
-    pa.mode = 1  # an avg pool is not this kernel's
-    assert N.lib().dml_pool_gemm_supported(C.byref(N.PoolGemmArgs(ga, pa))) == 0
-    pa.mode, pa.C = 0, 32  # nor 32 pooled channels (instantiations: 64 / 128 / 192)
-    assert N.lib().dml_pool_gemm_supported(C.byref(N.PoolGemmArgs(ga, pa))) == 0
-
-
-@pytest.mark.parametrize("fuse", ["1", "0"])
-def test_engine_pool_gemm_equals_unfused(fuse, monkeypatch):
-    """InceptionV3: max_pooling2d_2 + mixed0's sibling 1x1 GEMM as one op (DML_POOL_GEMM) gives the
-    unfused plan's mixed0 branch tensors and logits."""
-    monkeypatch.setenv("DML_POOL_GEMM", fuse)  # opt-in (default off)
-    g, w = build_model("InceptionV3", seed=5, calibrate=True)
-    imgs = torch.randint(0, 256, (2, 299, 299, 3), dtype=torch.uint8, device="cuda")
-    ef = Engine(g, w, batch=2, reuse_buffers=False)
-    monkeypatch.setenv("DML_POOL_GEMM", "0")
-    eu = Engine(g, w, batch=2, reuse_buffers=False)
-    assert bool(ef.pool_gemm) == (fuse == "1") and not eu.pool_gemm
-    if fuse == "1":
-        assert list(ef.pool_gemm) == ["max_pooling2d_2"]
-        assert "max_pooling2d_2+conv2d_6+conv2d_7+conv2d_9+conv2d_12" in ef.op_names
-        assert len(ef.op_names) == len(eu.op_names) - 1
-    ef.infer(imgs)
-    eu.infer(imgs)
-    torch.cuda.synchronize()
-    for name in ("mixed0_b5_1", "mixed0_b3_1", "conv2d_12_prepool", "mixed0"):
-        pf, pu = ef.view(name).float(), eu.view(name).float()
-        assert (pf - pu).abs().max().item() <= 1e-2 * pu.abs().max().item(), name
-    assert _rel(ef.buf[g.logits].cpu(), eu.buf[g.logits].cpu()) < 2e-2

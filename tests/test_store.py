@@ -148,3 +148,39 @@ def test_tcp_blob_server_bad_request_replies_error(tmp_path):
         srv.close()
 
     asyncio.run(main())
+
+
+def test_put_many_one_round_trip_per_bundle(tmp_path):
+    """put_many: every file on its own replicas (placement as a single PUT), versioned,
+    readable; a file already being uploaded is reported failed, not silently dropped;
+    replica replies name only the files they stored (no full listings)."""
+    async def main():
+        net, blobs = LoopbackNetwork(), InProcBlobNetwork()
+        names = [f"n{i}" for i in range(6)]
+        nodes = _mk(net, blobs, tmp_path, names)
+        c, leader = nodes["n4"], nodes["n0"]
+        items = [(f"output_31_{b}_rank0.json", f"batch {b}".encode()) for b in range(12)]
+        sent = []
+        orig = c.ep.request
+
+        async def spy(dest, mtype, payload=None, **kw):
+            sent.append(mtype)
+            return await orig(dest, mtype, payload, **kw)
+        c.ep.request = spy
+        ok, failed, err = await c.put_many(items)
+        assert sorted(ok) == sorted(n for n, _ in items) and failed == [] and not err
+        assert len(sent) == 1  # ONE leader round trip for 12 files
+        for n, data in items:
+            hs = await c.ls(n)
+            assert len(hs) == 4 and set(hs) == set(leader.meta.place(n, names))
+            assert await nodes["n5"].get(n) == (1, data)
+        ok, failed, _ = await c.put_many(items[:3])      # new versions of existing files
+        assert sorted(ok) == sorted(n for n, _ in items[:3])
+        assert (await nodes["n1"].get(items[0][0]))[0] == 2
+        leader.meta.begin("busy.json", ["n1"])           # an upload in progress is refused, per file
+        ok, failed, _ = await c.put_many([("busy.json", b"x"), ("free.json", b"y")])
+        assert ok == ["free.json"] and failed == ["busy.json"]
+        for s in nodes.values():
+            s.ep.stop()
+
+    asyncio.run(main())
