@@ -114,12 +114,12 @@ def _build_locked(stamp: str, stamp_file: Path, verbose: bool) -> Path:
 # Pure C++ host runtime pieces (no HIP): built with g++ in a second, tiny library
 # so that CPU-only processes (the CLI, the coordinator, tests) load it without
 # the HIP runtime, and so a kernel edit never rebuilds it.
-HOST_SOURCES = [CSRC / "host" / "output_json.cpp"]
+HOST_SOURCES = [CSRC / "host" / "output_json.cpp", CSRC / "host" / "shm_exchange.cpp"]
 HOST_LIB_PATH = PKG_DIR / "libdml_host.so"
 
 
 def _host_flags() -> list[str]:
-    return ["-O2", "-std=c++17", "-fPIC", "-shared", "-Wall"]
+    return ["-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-lrt"]
 
 
 def build_host(force: bool = False, verbose: bool = False) -> Path:

@@ -103,6 +103,9 @@ class UdpTransport(Transport):
     async def send(self, dest: str, frame: Frame) -> None:
         if self._tr is None:
             raise RuntimeError("transport not started")
+        if dest == self.name:  # to this node itself (e.g. the store leader is one of the replicas): no socket
+            self._q.put_nowait(frame)
+            return
         if self._drop.drop():
             return
         addr = addr_of(dest)

@@ -27,6 +27,7 @@ Works identically on gloo (CPU tests) and nccl (= RCCL on ROCm).
 from __future__ import annotations
 
 import datetime
+import hashlib
 import json
 import logging
 import os
@@ -44,6 +45,58 @@ class CollectiveFailure(RuntimeError):
     """A collective could not complete (peer died / communicator aborted)."""
 
 
+class ShmExchange:
+    """The per-step control exchange over node-local shared memory
+    (csrc/host/shm_exchange.cpp, libdml_host.so): all-gather semantics for a fixed-size
+    int64 record, waited for in native code with the GIL released. ``poll()`` is called
+    every ``slice_us`` while waiting; it raises CollectiveFailure when the failure
+    detector has confirmed a member dead (a dead rank never publishes)."""
+
+    REC_CAP = 32768
+
+    def __init__(self, name: str, world: int, rank: int):
+        import ctypes as C
+
+        from ..serving.output import _host_lib
+
+        L = _host_lib()
+        if L is None:
+            raise CollectiveFailure("shared-memory exchange needs libdml_host.so")
+        L.dml_shm_open.restype = C.c_void_p
+        L.dml_shm_open.argtypes = [C.c_char_p, C.c_int, C.c_int]
+        L.dml_shm_exchange.restype = C.c_int
+        L.dml_shm_exchange.argtypes = [C.c_void_p, C.c_int, C.c_longlong, C.c_void_p, C.c_int, C.c_void_p, C.c_int]
+        L.dml_shm_close.restype = None
+        L.dml_shm_close.argtypes = [C.c_void_p, C.c_int]
+        self.L, self.name, self.world, self.rank = L, name, world, rank
+        self.h = L.dml_shm_open(name.encode(), world, self.REC_CAP)
+        if not self.h:
+            raise CollectiveFailure(f"shm_open({name}) failed")
+        self.step = 0
+
+    def exchange(self, out: torch.Tensor, t: torch.Tensor, poll, timeout_s: float = 120.0,
+                 slice_us: int = 2000) -> None:
+        nb = t.numel() * t.element_size()
+        if nb > self.REC_CAP or not (t.is_contiguous() and out.is_contiguous()) or t.device.type != "cpu":
+            raise CollectiveFailure("shm exchange: record too large or not a contiguous CPU tensor")
+        self.step += 1
+        t0 = time.monotonic()
+        while True:
+            rc = self.L.dml_shm_exchange(self.h, self.rank, self.step, t.data_ptr(), nb, out.data_ptr(), slice_us)
+            if rc == 0:
+                return
+            if rc < 0:
+                raise CollectiveFailure("shm exchange: bad arguments")
+            poll()
+            if time.monotonic() - t0 > timeout_s:
+                raise CollectiveFailure("shm exchange timeout")
+
+    def close(self, unlink: bool = False) -> None:
+        if self.h:
+            self.L.dml_shm_close(self.h, int(unlink))
+            self.h = None
+
+
 def default_store_path(tag: str) -> str:
     base = os.environ.get("DML_RDZV_DIR", "/tmp")
     return os.path.join(base, f"dml_rdzv_{tag}")
@@ -53,12 +106,15 @@ class ElasticGroup:
     def __init__(self, global_rank: int, world: int, store_path: Optional[str] = None, backend: str = "gloo",
                  device: Optional[torch.device] = None, timeout_s: float = 60.0, store_host: Optional[str] = None,
                  store_port: int = 0, data_backend: Optional[str] = None, join: bool = False,
-                 join_timeout_s: float = 300.0):
+                 join_timeout_s: float = 300.0, shm_exchange: bool = False):
         """``backend``: the default group (control collectives); ``data_backend``:
         a second group over the same members for bulk tensors (e.g. control on
         host gloo, decoded images on RCCL), rebuilt with every epoch.
         ``join``: this process RE-joins a running job (a restarted rank): it
-        waits until the coordinator admits it into a new epoch (``admit``)."""
+        waits until the coordinator admits it into a new epoch (``admit``).
+        ``shm_exchange``: ``exchange`` (the service's per-step control collective) runs
+        over node-local shared memory (ShmExchange), one segment per epoch, instead of
+        the default group — the ranks must share a node (the FileStore already implies it)."""
         self.grank, self.backend, self.device = global_rank, backend, device
         self.data_backend = data_backend or backend
         self.data_group = None
@@ -76,6 +132,11 @@ class ElasticGroup:
         self.dead: Set[int] = set()          # fed by the failure detector (thread-safe set ops)
         self.joiners: Set[int] = set()       # ranks alive again but outside the group (SWIM rejoin)
         self.aborts = 0
+        self.shm_exchange = shm_exchange and store_host is None
+        self._shm: Optional[ShmExchange] = None
+        self._shm_names: List[str] = []
+        # the same name in every rank process (str hash() is salted per process)
+        self._shm_tag = hashlib.sha1(os.path.abspath(store_path or "").encode()).hexdigest()[:12]
         if join:
             self._await_admission(join_timeout_s)
         self._init_pg()
@@ -102,6 +163,12 @@ class ElasticGroup:
         self.data_group = None
         if self.data_backend != self.backend:
             self.data_group = dist.new_group(list(range(self.world)), backend=self.data_backend)
+        if self.shm_exchange:
+            if self._shm is not None:
+                self._shm.close()
+            name = f"/dml_{self._shm_tag}_e{self.epoch}_" + "-".join(map(str, self.members))
+            self._shm_names.append(name)
+            self._shm = ShmExchange(name, self.world, self.rank)
         log.info("rank %d joined epoch %d (%d members)", self.grank, self.epoch, self.world)
 
     def _teardown(self, abort: bool) -> None:
@@ -150,6 +217,11 @@ class ElasticGroup:
         except Exception as e:  # gloo raises when a peer's socket closes
             raise CollectiveFailure(str(e)) from e
 
+    def _poll_dead(self) -> None:
+        """(between shared-memory wait slices) a member SWIM confirmed dead fails the exchange."""
+        if self.dead & set(self.members):
+            raise CollectiveFailure(f"members {sorted(self.dead & set(self.members))} declared dead")
+
     def _run(self, fn, *args, **kw) -> None:
         try:
             w = fn(*args, async_op=True, **kw)
@@ -180,6 +252,9 @@ class ElasticGroup:
         GROUP rank). gloo: a gather to ``root`` plus a broadcast from it - two
         hops instead of a ring's world-1 (world 8 on 8 cores: 0.54 ms vs 2.1 ms
         for a 1.7 KB record); nccl: the ring all-gather."""
+        if self._shm is not None and t.device.type == "cpu":
+            self._shm.exchange(out, t, self._poll_dead, self.timeout.total_seconds())
+            return
         if self.backend != "gloo":
             self.all_gather_into(out, t)
             return
@@ -285,3 +360,11 @@ class ElasticGroup:
 
     def close(self) -> None:
         self._teardown(abort=False)
+        if self._shm is not None:
+            self._shm.close()
+            self._shm = None
+        for name in self._shm_names:  # every epoch's segment (ranks that died never unlink theirs)
+            try:
+                os.unlink("/dev/shm" + name)
+            except OSError:
+                pass

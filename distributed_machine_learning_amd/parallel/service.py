@@ -673,9 +673,13 @@ class CollectiveService:
         out = torch.empty((world, L), dtype=torch.int64, device=self.dev)
         applied_here: List[dict] = []
         try:
-            (eg.all_gather_into(out, rec_t) if os.environ.get('DML_AG') else eg.exchange(out, rec_t, root))
-            h = out.cpu().numpy()
-            n = int(h[root, H_LOGLEN])
+            if world == 1:  # nothing to exchange: a collective would only hand the GIL around
+                h = rec[None]
+                n = 0
+            else:
+                eg.exchange(out, rec_t, root)
+                h = out.cpu().numpy()
+                n = int(h[root, H_LOGLEN])
             if n:
                 buf = torch.zeros(n, dtype=torch.uint8, device=self.dev)
                 if active:

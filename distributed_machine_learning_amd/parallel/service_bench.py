@@ -24,7 +24,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images: int, inception_images: int,
         batch_sizes: Dict[str, int], out_dir: Optional[str], kills: Sequence[Tuple[int, int]] = (),
-        comm: str = "gloo", depth: int = 4, single_rates: Optional[Dict[str, float]] = None,
+        comm: str = "gloo", depth: int = 16, single_rates: Optional[Dict[str, float]] = None,
         make_backend=None, data_backend: str = "nccl") -> Optional[dict]:
     """One rank of the service run; returns the record (on every surviving rank)."""
     import torch
@@ -42,7 +42,7 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
     backend = (make_backend() if make_backend is not None else
                GpuRankBackend(device, batch_sizes, cap=cap, arena_images=4 * cap, n_synth=2 * cap))
     eg = ElasticGroup(rank, world, store_path=rdzv, backend=comm, device=device if comm == "nccl" else None,
-                      timeout_s=120, data_backend=data_backend)
+                      timeout_s=120, data_backend=data_backend, shm_exchange=(comm == "gloo"))
     # the product's control plane (serving/rank_main.py): SWIM + election + the replicated
     # store; every output is PUT into the store (bundled, pipelined) before its batch counts
     store_root = os.path.join(os.environ.get("DML_RDZV_DIR", "/tmp"), os.path.basename(rdzv) + "_store")

@@ -56,7 +56,8 @@ def add_args(ap: argparse.ArgumentParser) -> None:
     g.add_argument("--batch-resnet", type=int, default=256)
     g.add_argument("--batch-inception", type=int, default=128)
     g.add_argument("--comm", default="gloo", choices=("gloo", "nccl"), help="backend of the control collective")
-    g.add_argument("--depth", type=int, default=4, help="batches in flight per rank (2 on the GPU + queued)")
+    g.add_argument("--depth", type=int, default=16,
+                   help="batches in flight per rank: 2 on the GPU, the rest queued or awaiting their output PUT")
     g.add_argument("--replication", type=int, default=4)
     g.add_argument("--arena-images", type=int, default=8192, help="HBM image store capacity per model")
     g.add_argument("--no-preempt", action="store_true")
@@ -152,7 +153,8 @@ def rank_main(a: argparse.Namespace) -> int:
     ctl.start()
     eg = ElasticGroup(grank, world, store_path=a.rdzv, backend=a.comm,
                       device=dev if a.comm == "nccl" else None, timeout_s=120,
-                      data_backend="nccl" if a.backend == "gpu" else a.comm, join=a.rejoin)
+                      data_backend="nccl" if a.backend == "gpu" else a.comm, join=a.rejoin,
+                      shm_exchange=(a.comm == "gloo"))
     eg.dead |= early_dead
     eg.joiners |= {g for g in early_alive if g not in eg.members}
     holder["eg"] = eg

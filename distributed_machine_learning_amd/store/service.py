@@ -395,9 +395,12 @@ class StoreService:
         p = fr.payload
         files = [(n, int(v)) for n, v in p.get("files", [])]
         ok: Dict[str, List[int]] = {}
+        req = {"op": "outbox_many", "token": p.get("token"), "names": [n for n, _ in files]}
         try:
-            items = await self.blobs.fetch(p["source"], {"op": "outbox_many", "token": p.get("token"),
-                                                         "names": [n for n, _ in files]}, addr=p.get("source_blob"))
+            if p["source"] == self.me:  # this node PUT the bundle: take it from its own outbox
+                items = self.source.read(req)
+            else:
+                items = await self.blobs.fetch(p["source"], req, addr=p.get("source_blob"))
             if len(items) == len(files):
                 for (n, v), (_, data) in zip(files, items):
                     self.local.put_bytes(n, data, version=v)
