@@ -118,7 +118,9 @@ class ElasticGroup:
         self.grank, self.backend, self.device = global_rank, backend, device
         self.data_backend = data_backend or backend
         self.data_group = None
+        self._graveyard: list = []
         self.members: List[int] = list(range(world))
+        self.prev_members: List[int] = list(self.members)   # the member list of the previous epoch
         self.epoch = 0
         self.timeout = datetime.timedelta(seconds=timeout_s)
         if store_host is not None:  # multi-node: a TCPStore on one host (that host is then a SPOF)
@@ -160,9 +162,10 @@ class ElasticGroup:
             kw["device_id"] = self.device
         dist.init_process_group(self.backend, store=prefix, rank=self.rank, world_size=self.world,
                                 timeout=self.timeout, **kw)
-        self.data_group = None
-        if self.data_backend != self.backend:
-            self.data_group = dist.new_group(list(range(self.world)), backend=self.data_backend)
+        # the image windows' all-gathers always get a group of their own: they are issued
+        # when a window's decode finishes, which is not ordered against the step's control
+        # exchange across ranks (gloo / RCCL match collectives by issue order per group)
+        self.data_group = dist.new_group(list(range(self.world)), backend=self.data_backend)
         if self.shm_exchange:
             if self._shm is not None:
                 self._shm.close()
@@ -177,12 +180,16 @@ class ElasticGroup:
         nothing waits on it, then destroy the group."""
         if not dist.is_initialized():
             return
-        if abort and self.data_group is not None and self.data_backend == "nccl":
-            c10d._abort_process_group(self.data_group)   # RCCL data group: ncclCommAbort
-            self.aborts += 1
         self.data_group = None
-        if abort and self.backend == "nccl":
-            c10d._abort_process_group()   # NCCL/RCCL backend abort (no hasattr probing)
+        if abort:
+            # every group of the epoch (RCCL: ncclCommAbort; gloo: closes the pairs, so an
+            # image window's all-gather still pending on a peer that went on to rebuild
+            # fails at once instead of holding destroy_process_group for the timeout)
+            # the aborted groups stay referenced: the last reference dropping inside the abort
+            # would run the gloo group's destructor there, which joins its worker threads
+            # behind ops of the failed epoch (observed: minutes inside the abort)
+            self._graveyard.extend(c10d._world.pg_map.keys())
+            c10d._abort_process_group()
             self.aborts += 1
             return  # the abort destroyed the default group
         try:
@@ -200,6 +207,10 @@ class ElasticGroup:
         1.9 ms blocking vs 8-12 ms polled (yield or spin). nccl (RCCL) cannot
         report a dead peer, so it is polled against the SWIM verdicts."""
         if self.backend == "gloo":
+            # a blocking wait (GIL released). A sliced wait (gloo raises "timed out" at the
+            # slice end) left multi-hop collectives broken on the ranks that sliced; the
+            # service's per-step exchange polls the SWIM verdicts on the shared-memory path
+            # instead (ShmExchange), so a hung-but-connected peer no longer stalls the loop
             try:
                 work.wait()
             except Exception as e:  # gloo raises when a peer's socket closes / on its timeout
@@ -270,6 +281,18 @@ class ElasticGroup:
         else:
             self._run(dist.all_gather, list(out.view(self.world, *t.shape).unbind(0)), t, group=self.data_group)
 
+    def all_gather_data_async(self, out: torch.Tensor, t: torch.Tensor):
+        """Issue the data-group all-gather without waiting; returns the Work (RCCL: wait()
+        makes the current stream wait for it; gloo: poll is_completed()). The caller
+        issues these in the same order on every rank."""
+        try:
+            if self.data_backend == "nccl":
+                return dist.all_gather_into_tensor(out, t, group=self.data_group, async_op=True)
+            return dist.all_gather(list(out.view(self.world, *t.shape).unbind(0)), t, group=self.data_group,
+                                   async_op=True)
+        except Exception as e:
+            raise CollectiveFailure(str(e)) from e
+
     def broadcast_data(self, t: torch.Tensor, src: int = 0) -> None:
         """broadcast on the data group (bulk tensors); ``src`` is a GROUP rank."""
         self._run(dist.broadcast, t, src=src, group=self.data_group)
@@ -296,7 +319,7 @@ class ElasticGroup:
         self._teardown(abort=True)
         if self.grank not in members:
             raise CollectiveFailure("this rank was removed from the group")
-        self.members = members
+        self.prev_members, self.members = self.members, members
         self.epoch = nxt
         self.dead.intersection_update(self.members)  # forget the removed ranks
         try:
@@ -334,7 +357,7 @@ class ElasticGroup:
         self._teardown(abort=False)
         if self.grank not in won:
             raise CollectiveFailure("this rank was removed from the group")
-        self.members = won
+        self.prev_members, self.members = self.members, won
         self.epoch = nxt
         self.dead.intersection_update(self.members)
         self.joiners.difference_update(self.members)
@@ -351,6 +374,8 @@ class ElasticGroup:
                 e = int(self.store.get(key).decode())
                 members = json.loads(self.store.get(f"members{e}").decode())
                 if self.grank in members:
+                    prev = self.store.get(f"members{e - 1}").decode() if e > 0 else json.dumps(members)
+                    self.prev_members = json.loads(prev)
                     self.epoch, self.members = e, members
                     log.info("rank %d admitted into epoch %d", self.grank, e)
                     return

@@ -60,15 +60,88 @@ class RankBackend:
             ev.synchronize()
         return res
 
-    # collective hooks (every rank calls them in the same order)
-    def on_submit(self, model: str, names: Sequence[str], eg) -> int:
-        return 0
+    # staging hooks (parallel/image_store.py): every rank calls stage / release /
+    # reset_staging at the same points of the replicated job state; backends that fetch
+    # their images at launch keep these no-ops
+    def attach(self, eg) -> None:
+        """A new communicator epoch (group rank / size, data group)."""
 
-    def backfill(self, model: str, names: Sequence[str], eg, root: int) -> int:
-        return 0
+    def stage(self, model: str, batches) -> bool:
+        """Stage these batches' images (in order) ahead of their launch; False if the
+        arena could not take all of them yet."""
+        return True
+
+    def progress(self) -> None:
+        """Advance staging without blocking (serve loop, every poll)."""
+
+    def ready(self, model: str, names: Sequence[str]) -> bool:
+        return True
+
+    def release(self, model: str, key, names: Sequence[str]) -> None:
+        """A batch completed: its images are no longer pinned."""
+
+    def reset_staging(self) -> None:
+        """Epoch change: forget every staged window (identically on every rank)."""
 
     def drain(self) -> None:
         """Wait for every launched batch (failure recovery reuses the slots)."""
+
+
+class _ArenaStaging:
+    """Window staging over per-model HbmImageStores (shared by StoreRankBackend and
+    GpuRankBackend): decisions from the replicated state, data movement asynchronous."""
+
+    arenas: Dict[str, "object"]
+    staged: Dict[tuple, Tuple[str, List[str]]]
+
+    def _init_staging(self, loader, decode_threads: int = 8) -> None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from .image_store import Stager
+
+        self.loader = loader
+        self.staged = {}
+        self.pool = ThreadPoolExecutor(max_workers=decode_threads)
+        self.stager = Stager()   # one window order (one collective order) for every model's store
+        self.epoch = 0
+
+    def _adopt(self, model: str, arena) -> None:
+        arena.stager = self.stager
+        arena.loader = lambda ns, m=model: self._load(m, ns)
+
+    def attach(self, eg) -> None:
+        self.epoch = eg.epoch
+        self.stager.attach(eg.rank, eg.world, self.pool, eg.all_gather_data_async,
+                           getattr(self, "stage_stream", None))
+
+    def stage(self, model, batches) -> bool:
+        arena = self.arenas[model]
+        for b in batches:
+            if b.key in self.staged:
+                continue
+            if arena.plan(b.images, self.epoch) is None:
+                return False  # later batches wait for completions to free arena slots
+            arena.pin(b.images)
+            self.staged[b.key] = (model, list(b.images))
+        return True
+
+    def progress(self) -> None:
+        if self.stager.queue:
+            self.stager.progress()
+
+    def ready(self, model, names) -> bool:
+        return self.arenas[model].ready(names)
+
+    def release(self, model, key, names) -> None:
+        st = self.staged.pop(key, None)
+        if st is not None:
+            self.arenas[st[0]].unpin(st[1])
+
+    def reset_staging(self) -> None:
+        self.stager.drain()
+        for a in self.arenas.values():
+            a.reset()
+        self.staged.clear()
 
 
 class HostRankBackend(RankBackend):
@@ -137,12 +210,12 @@ class FakeRankBackend(HostRankBackend):
         super().__init__(FakeBackend(), loader=loader, cap=cap, delay_per_image=delay_per_image)
 
 
-class StoreRankBackend(RankBackend):
+class StoreRankBackend(_ArenaStaging, RankBackend):
     """CPU stand-in of GpuRankBackend's data path for multi-rank tests: the same
-    replicated image store (parallel/image_store.py, on a CPU device, all-gather
-    and backfill broadcast over the data group) feeding a deterministic
-    'classifier' of the image bytes (top-5 = a hash of the pixels). Exercises
-    decode-once replication, version pinning and rejoin backfill without a GPU."""
+    window-staged image store (parallel/image_store.py, on a CPU device, all-gather
+    over the data group) feeding a deterministic 'classifier' of the image bytes
+    (top-5 = a hash of the pixels). Exercises decode-once staging, arena eviction,
+    version pinning and rejoin re-staging without a GPU."""
 
     slots = 8   # synchronous
 
@@ -150,14 +223,19 @@ class StoreRankBackend(RankBackend):
                  n_synth: int = 16, delay_per_image: float = 0.0):
         from .image_store import HbmImageStore
 
-        self.cap, self.loader, self.delay = cap, loader, delay_per_image
+        self.cap, self.delay = cap, delay_per_image
         self.arenas = {m: HbmImageStore(arena_images, hw, torch.device("cpu"), n_synth=n_synth,
                                         seed=1000 + MODEL_IDS[m]) for m in MODELS}
+        self._init_staging(loader)
+        for m, a in self.arenas.items():
+            self._adopt(m, a)
         self.launched = 0
+        self.loads = 0
 
     def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
         hw = self.arenas[model].hw
         blobs = self.loader(names) if self.loader else {}
+        self.loads += len(names)
         out: Dict[str, Optional[np.ndarray]] = {}
         for n in names:
             b = blobs.get(n)
@@ -168,13 +246,6 @@ class StoreRankBackend(RankBackend):
             out[n] = np.frombuffer((h * (hw[0] * hw[1] * 3 // 32 + 1))[:hw[0] * hw[1] * 3],
                                    np.uint8).reshape(*hw, 3).copy()
         return out
-
-    def on_submit(self, model, names, eg) -> int:
-        return self.arenas[model].replicate(names, lambda ns: self._load(model, ns), rank=eg.rank, world=eg.world,
-                                            gather=eg.all_gather_data)
-
-    def backfill(self, model, names, eg, root) -> int:
-        return self.arenas[model].backfill(names, eg, root)
 
     @staticmethod
     def classify(img: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
@@ -189,7 +260,7 @@ class StoreRankBackend(RankBackend):
         if self.delay:
             time.sleep(self.delay * len(names))
         arena = self.arenas[model]
-        slots, failed = arena.slots(list(names), lambda ns: self._load(model, ns))
+        slots, failed = arena.slots(list(names))
         bad = set(failed)
         out = torch.zeros((2, self.cap, 5), dtype=torch.int32)
         for i, (n, s) in enumerate(zip(names, slots)):
@@ -203,38 +274,34 @@ class StoreRankBackend(RankBackend):
         return out, None
 
 
-class GpuRankBackend(RankBackend):
-    """Native engines for both models resident in this GPU's HBM, fed from
-    per-model HBM image stores (parallel/image_store.py: store images decoded
-    once per job and replicated to every rank over the data group — RCCL —
-    plus seeded synthetic images). A batch is gathered from the store into the
-    engine's source slot on the compute stream, in order (no PCIe copy per
-    batch, nothing for another queue to starve); its top-5 rows are copied
-    into pinned host memory on the same stream, then an event is recorded. A
-    batch larger than the engine's batch runs as several engine passes into
-    consecutive result rows.
+class GpuRankBackend(_ArenaStaging, RankBackend):
+    """Native engines for both models resident in this GPU's HBM, fed from per-model
+    HBM image stores (parallel/image_store.py: store images staged in windows ahead of
+    dispatch, decoded once per job and replicated to every rank over the data group —
+    RCCL — plus seeded synthetic images). A batch is gathered from the store into the
+    engine's source slot on the compute stream, after waiting on the events of the
+    windows that staged its images; its top-5 rows are copied into pinned host memory
+    on the same stream, then an event is recorded. A batch larger than the engine's
+    batch runs as several engine passes into consecutive result rows.
 
-    Stream order is the only synchronisation of the arena: replication
-    (``on_submit``), backfill, the local fallback decode in ``launch`` and every
-    batch gather run on ``self.stream``, so a gather always reads what the
-    writes before it left, and an eviction write never overtakes a gather
-    queued before it."""
+    Arena writes (window scatters) run on ``stage_stream``; a launch makes the compute
+    stream wait for the windows of its images. A slot is only re-assigned after every
+    batch pinning its old image completed (its gather is done), so a scatter never
+    overtakes a gather that still reads the old image."""
 
     def __init__(self, device: torch.device, batch_sizes: Dict[str, int], cap: int = 0, arena_images: int = 8192,
                  n_synth: int = 512, seed: int = 0, models: Sequence[str] = MODELS, splits: int = 2,
                  loader: Optional[Callable] = None, decode_threads: int = 8):
-        from concurrent.futures import ThreadPoolExecutor
-
         from ..models import build_model
         from ..models.engine import Engine, SplitEngine, merge_point
         from .image_store import HbmImageStore
 
         self.device = device
         self.cap = cap or max(batch_sizes.values())
-        self.loader = loader
         self.engines, self.arenas = {}, {}
         self.stream = torch.cuda.Stream(device)
-        self.pool = ThreadPoolExecutor(max_workers=decode_threads)
+        self.stage_stream = torch.cuda.Stream(device)
+        self._init_staging(loader, decode_threads)
         for m in models:
             g, w = build_model(m, seed=seed, calibrate=True)
             b = batch_sizes[m]
@@ -245,40 +312,30 @@ class GpuRankBackend(RankBackend):
                 self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=SLOTS)
             self.arenas[m] = HbmImageStore(max(arena_images, n_synth + 2 * self.cap), g.input_hw, device,
                                            n_synth=n_synth, seed=1000 + MODEL_IDS[m])
+            self._adopt(m, self.arenas[m])
             self.engines[m].capture(self.stream)  # graphs now, before the service's first collective
         self.out = [torch.zeros((2, self.cap, 5), dtype=torch.int32, device=device) for _ in range(SLOTS)]
         self.host = [torch.zeros((2, self.cap, 5), dtype=torch.int32).pin_memory() for _ in range(SLOTS)]
         self.ev_done = [torch.cuda.Event() for _ in range(SLOTS)]
 
     def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
+        """(decode pool thread) fetch + decode this rank's share of a window."""
         from ..serving.inference import load_image
 
         blobs = self.loader(names) if self.loader else {}
         hw = self.arenas[model].hw
-
-        def dec(n):
+        out: Dict[str, Optional[np.ndarray]] = {}
+        for n in names:
             b = blobs.get(n)
             if b is None:
-                return n, None
+                out[n] = None
+                continue
             try:
-                return n, load_image(b, hw)
+                out[n] = load_image(b, hw)
             except Exception as e:  # undecodable file -> reported as failed
                 log.warning("decode of %s failed: %s", n, e)
-                return n, None
-        return dict(self.pool.map(dec, names))
-
-    def on_submit(self, model: str, names: Sequence[str], eg) -> int:
-        """(collective, every rank) decode this rank's share of the job's new
-        images and all-gather all shares into every rank's HBM store — on the
-        compute stream, ahead of every later batch gather."""
-        with torch.cuda.stream(self.stream):
-            return self.arenas[model].replicate(names, lambda ns: self._load(model, ns), rank=eg.rank,
-                                                world=eg.world, gather=eg.all_gather_data)
-
-    def backfill(self, model: str, names: Sequence[str], eg, root: int) -> int:
-        """(collective) a re-joined rank receives the survivors' decoded images."""
-        with torch.cuda.stream(self.stream):
-            return self.arenas[model].backfill(names, eg, root)
+                out[n] = None
+        return out
 
     def launch(self, model, names, slot):
         if len(names) > self.cap:
@@ -287,10 +344,10 @@ class GpuRankBackend(RankBackend):
         s = self.stream
         out = self.out[slot]
         B = eng.batch
+        slots, failed = arena.slots(list(names))
         with torch.cuda.stream(s):
-            # images never replicated (standalone use, or evicted) are decoded
-            # here; their arena writes are ordered before the gathers below
-            slots, failed = arena.slots(list(names), lambda ns: self._load(model, ns))
+            for ev in arena.events(names):  # the windows that staged these images
+                s.wait_event(ev)
             for off in range(0, len(slots), B):  # one engine pass per B images: never truncated
                 chunk = slots[off:off + B]
                 arena.gather_into(eng.srcs[slot], chunk)
@@ -305,4 +362,7 @@ class GpuRankBackend(RankBackend):
         return self.host[slot], self.ev_done[slot]
 
     def drain(self) -> None:
+        # the compute stream only ever waits on window events that had completed (ready()),
+        # so this returns even when a peer died mid-staging; the staging stream is released by
+        # the communicator abort of the rebuild, never waited for here
         self.stream.synchronize()

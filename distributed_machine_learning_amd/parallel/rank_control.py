@@ -206,17 +206,19 @@ class RankControl:
         raise RuntimeError(f"store put {name}: {err}")
 
     def store_put_many_async(self, items, done: Callable[[List[str], List[str]], None],
-                             deadline_s: float = 60.0) -> None:
+                             deadline_s: float = 60.0, attempt_s: float = 8.0) -> None:
         """PUT a bundle of files (store.service.put_many: one leader round trip) without
         blocking the caller; files the store refused are retried (a store-leader change
-        mid-PUT) until ``deadline_s``. ``done(stored, failed)`` runs on the control loop."""
+        mid-PUT; each attempt bounded by ``attempt_s``) until ``deadline_s``.
+        ``done(stored, failed)`` runs on the control loop."""
         async def go():
             remaining = dict(items)
             stored: List[str] = []
             t0, err = time.monotonic(), ""
             while remaining and time.monotonic() - t0 < deadline_s:
-                try:
-                    ok, _, err = await self.node.store.put_many(list(remaining.items()))
+                try:  # one attempt is bounded: a leader that died mid-PUT must not eat the deadline
+                    ok, _, err = await asyncio.wait_for(self.node.store.put_many(list(remaining.items())),
+                                                        attempt_s)
                 except Exception as e:  # leader unreachable mid-failover
                     ok, err = [], str(e)
                 for n in ok:

@@ -58,16 +58,19 @@ rewritten (at-least-once); every job completes.
 Rejoin: a restarted rank announces itself over SWIM; the coordinator admits it
 at a step boundary (``members<e+1>`` + ``admit<g>`` in the rendezvous store,
 GROW flag in the record); every rank requeues its in-flight batches and moves
-to epoch e+1 with it; the coordinator's state record then brings the joiner's
-replica up to date, and one broadcast over the data group backfills its HBM
-image store with the unfinished jobs' images (parallel/image_store.backfill).
+to epoch e+1 with it; the pre-growth coordinator keeps the role (a joiner stays
+out of it until its replica is in sync) and its state record brings the joiner's
+replica up to date.
 
 Images: a job names store images (cyclic pick over the sorted ``*.jpeg``
 listing, reference worker.py:176-206), pinned to their latest version at submit
 time (``name@v``: a later PUT never changes what a queued job reads), or
-synthetic images. Applying a submit record, every rank decodes only ITS SHARE of
-the job's new images and one all-gather over the data group (RCCL over xGMI)
-replicates them into every rank's HBM image store (parallel/image_store.py).
+synthetic images. They are staged in sliding windows just ahead of dispatch
+(parallel/image_store.py): every step, every rank hands the batches in flight and
+the next queued ones to its backend, which decodes its share of their new images
+off the loop and replicates them with one asynchronous all-gather over the data
+group (RCCL over xGMI) into a bounded HBM arena — any job size, no whole-job
+replication, no stall of the control step. Epoch changes restart the staging.
 """
 from __future__ import annotations
 
@@ -180,16 +183,6 @@ class ReplicatedCoordinator:
 
     def outstanding(self, grank: int) -> int:
         return sum(1 for inf in self.inflight.values() if inf.rank == grank)
-
-    def unfinished_images(self) -> Dict[str, List[str]]:
-        """Images of every queued or in-flight batch, per model (rejoin backfill)."""
-        out: Dict[str, List[str]] = {m: [] for m in MODELS}
-        for m, q in self.jobs.queues.items():
-            for b in q:
-                out[m].extend(b.images)
-        for b in self.jobs.inprogress.values():
-            out[b.model].extend(b.images)
-        return {m: list(dict.fromkeys(v)) for m, v in out.items()}
 
     # ---------------------------------------------------------- planning ----
     def plan(self, members: List[int]) -> Tuple[Dict[int, List[Batch]], List[Tuple[int, tuple]]]:
@@ -525,6 +518,12 @@ class CollectiveService:
         self._inbox: "queue.Queue" = queue.Queue()   # (record, reply callback or None)
         self._stop = False
         self.rejoined = rejoined
+        # ranks whose replica has not yet received a coordinator state record (a re-joined
+        # process, until the first state record of its epoch): never the coordinator
+        self.unsynced: set = {eg.grank} if rejoined else set()
+        if rejoined:
+            self.unsynced |= set(eg.members) - set(eg.prev_members)
+        self.stage_ahead = max(1, eg.world) * coord.depth  # queued batches staged ahead of dispatch
         self.last_progress = time.monotonic()
         self.phase_s: Dict[str, float] = {"poll": 0.0, "plan": 0.0, "collective": 0.0, "apply": 0.0,
                                           "launch": 0.0, "sleep": 0.0}
@@ -535,10 +534,14 @@ class CollectiveService:
             self._watchdog.start()
         if control is not None:
             control.attach(self)
+        backend.attach(eg)
 
     # ------------------------------------------------------------- roles --
     def coordinator_rank(self) -> int:
-        return max(self.eg.members)
+        """The highest member whose replica is in sync (a re-joined rank with a higher id
+        would otherwise plan from an empty replica: ADVICE r3)."""
+        synced = [g for g in self.eg.members if g not in self.unsynced]
+        return max(synced or self.eg.members)
 
     def is_coordinator(self) -> bool:
         return self.eg.grank == self.coordinator_rank()
@@ -595,7 +598,8 @@ class CollectiveService:
                 self.done.append((L.batch, svc, L.epoch))
             self.served_here += 1
             n += 1
-        while self.hostq and self.free_slots:
+        self.be.progress()  # image windows: decode shares, all-gathers, scatters (never blocks)
+        while self.hostq and self.free_slots and self.be.ready(self.hostq[0].model, self.hostq[0].images):
             b = self.hostq.popleft()
             slot = self.free_slots.pop(0)
             rows, ev = self.be.launch(b.model, b.images, slot)
@@ -700,12 +704,10 @@ class CollectiveService:
             for r in applied_here:
                 coord.apply(r)
         applied = recs if active else applied_here
-        for r in applied:  # collectives on every rank: replicate a job's images / backfill a joiner
-            if r["op"] == "submit":
-                self.be.on_submit(r["model"], r["images"], eg)
-            elif r["op"] == "state":
+        for r in applied:
+            if r["op"] == "state":  # every replica now holds the coordinator's state
                 self.rejoined = False
-                self._backfill(root)
+                self.unsynced.clear()
         if active and self.control is not None:
             self.control.committed(replies, results)
         elif active:
@@ -724,6 +726,7 @@ class CollectiveService:
                     b = coord.complete((int(j), int(bt)), service=int(us) * 1e-6)
                     if b is not None:
                         finished.append(b)
+                        self.be.release(b.model, b.key, b.images)  # its images are no longer pinned
             ans = []
             for r in range(world):
                 for i in range(int(h[r, H_NACK])):
@@ -739,6 +742,7 @@ class CollectiveService:
                                                        int(h[root, req + i * REQ_W + 2])))
                       for i in range(int(h[root, H_NREQ]))]
                 coord.apply_requests(rq)
+                self._stage()
         if finished and active and self.control is not None:
             self.control.jobs_progress(finished)
         t4 = time.perf_counter()
@@ -774,14 +778,17 @@ class CollectiveService:
             ph["sleep"] += time.perf_counter() - t5
         return True
 
-    def _backfill(self, root: int) -> None:
-        """(collective, after a state record) the coordinator's HBM images of
-        every unfinished job to the ranks that lack them (a re-joined rank)."""
-        with self.coord.lock:
-            want = self.coord.unfinished_images()
+    def _stage(self) -> None:
+        """(every rank, same step, coordinator lock held) stage the images of the batches
+        in flight and of the next ``stage_ahead`` queued batches of each model, in
+        dispatch order (parallel/image_store.py): identical decisions everywhere."""
+        coord = self.coord
         for m in MODELS:
-            if want.get(m):
-                self.be.backfill(m, want[m], self.eg, root)
+            cand = [inf.batch for inf in coord.inflight.values() if inf.batch.model == m]
+            q = coord.jobs.queues[m]
+            cand += [q[i] for i in range(min(len(q), self.stage_ahead))]
+            if cand:
+                self.be.stage(m, cand)
 
     # -------------------------------------------------------------- serve --
     def serve(self, max_steps: int = 10 ** 9, stop_when_idle: bool = False) -> int:
@@ -807,6 +814,15 @@ class CollectiveService:
         self.answers = []
 
     def _after_epoch(self, was: int) -> None:
+        # ranks new in this epoch (re-joined) and ranks still waiting for their first state
+        # stay out of the coordinator role until the next state record
+        self.unsynced = (self.unsynced & set(self.eg.members)) | (set(self.eg.members) - set(self.eg.prev_members))
+        self.stage_ahead = self.eg.world * self.coord.depth
+        # image windows: every rank forgets its staging at this same boundary and stages
+        # afresh over the new group (a joiner's arena is empty; survivors' collectives of
+        # the failed epoch were aborted)
+        self.be.reset_staging()
+        self.be.attach(self.eg)
         # the new coordinator's state is authoritative: replicas that completed one
         # step more or less than it did are repaired by a state record (and a
         # joiner gets its first state); it is the first record of the next step

@@ -61,7 +61,12 @@ def parse(argv=None) -> argparse.Namespace:
 
     add_args(ap)
     a = ap.parse_args(argv)
-    a.explicit = {k for k, v in vars(a).items() if v != ap.get_default(k)}
+    # flags given on the command line (even when equal to their defaults: ``--backend cpu``
+    # on a rank overrides the rank's own default, its GPU)
+    argv_l = sys.argv[1:] if argv is None else list(argv)
+    given = {t.split("=", 1)[0] for t in argv_l if t.startswith("--")}
+    a.explicit = {k for k, v in vars(a).items()
+                  if v != ap.get_default(k) or "--" + k.replace("_", "-") in given}
     if a.role == "rank":
         return a
     if a.port is None and not (a.config and a.node):

@@ -1,7 +1,7 @@
 """The MI355X serving product: one rank process per GPU, launched by one command.
 
   python -m distributed_machine_learning_amd.serving.main --role rank --gpus 8 \\
-      [--backend gpu|fake|store] [--base-port 8700] [--store-dir ./sdfs] [--out-dir ./outputs] \\
+      [--backend gpu|cpu|fake|store] [--base-port 8700] [--store-dir ./sdfs] [--out-dir ./outputs] \\
       [--batch-resnet 256 --batch-inception 128] [--comm gloo|nccl]
 
   # re-start ONE rank of a running job (after it died): it re-joins the group
@@ -17,8 +17,9 @@ rank); each rank runs, on GPU ``rank``:
     coordinator = highest rank) + the replicated store (blob plane) + the
     job-service handlers the reference leader served (submit-job, C1, C2, C3, C5);
   * ``GpuRankBackend`` (native engines of both models, HBM image stores) fed by
-    the store through ``RankControl.store_loader`` (``fake`` / ``store``: the
-    CPU stand-ins used by tests);
+    the store through ``RankControl.store_loader`` (``cpu``: the fp32 PyTorch
+    executor on the host — BASELINE config 1, the reference's CPU worker;
+    ``fake`` / ``store``: the CPU stand-ins used by tests);
   * ``ElasticGroup`` (control collective on gloo, image replication on RCCL,
     FileStore rendezvous that no rank hosts) + ``CollectiveService`` (replicated
     coordinator, fair-share with preemption, failure rebuild and rejoin);
@@ -59,7 +60,8 @@ def add_args(ap: argparse.ArgumentParser) -> None:
     g.add_argument("--depth", type=int, default=16,
                    help="batches in flight per rank: 2 on the GPU, the rest queued or awaiting their output PUT")
     g.add_argument("--replication", type=int, default=4)
-    g.add_argument("--arena-images", type=int, default=8192, help="HBM image store capacity per model")
+    g.add_argument("--arena-images", type=int, default=0,
+                   help="HBM image store capacity per model (0: 2 x ranks x depth x batch, at least 8192)")
     g.add_argument("--no-preempt", action="store_true")
 
 
@@ -119,9 +121,10 @@ def rank_main(a: argparse.Namespace) -> int:
     import torch
 
     from ..parallel.elastic import ElasticGroup
-    from ..parallel.rank_backend import FakeRankBackend, GpuRankBackend, StoreRankBackend
+    from ..parallel.rank_backend import FakeRankBackend, GpuRankBackend, HostRankBackend, StoreRankBackend
     from ..parallel.rank_control import RankControl
     from ..parallel.service import CollectiveService, OutputWriter, ReplicatedCoordinator
+    from .inference import CpuBackend
 
     if not a.rdzv or not a.base_port:
         raise SystemExit("a rank needs --rdzv and --base-port (use the launcher: --role rank --gpus N)")
@@ -144,11 +147,13 @@ def rank_main(a: argparse.Namespace) -> int:
         (holder["eg"].joiners if "eg" in holder else early_alive).add(g)
     ctl = RankControl(grank, world, a.base_port, store_dir=store_dir, replication=min(a.replication, world),
                       rejoin=a.rejoin, on_dead=on_dead, on_alive=on_alive)
+    # the image windows stage world x depth batches ahead of dispatch: room for twice that
+    arena = a.arena_images or max(8192, 2 * world * a.depth * cap)
     backend = {
-        "gpu": lambda: GpuRankBackend(dev, bs, cap=cap, arena_images=a.arena_images, loader=ctl.store_loader),
+        "gpu": lambda: GpuRankBackend(dev, bs, cap=cap, arena_images=arena, loader=ctl.store_loader),
         "fake": lambda: FakeRankBackend(cap=cap, loader=ctl.store_loader),
         "store": lambda: StoreRankBackend(cap=cap, loader=ctl.store_loader),
-        "cpu": lambda: FakeRankBackend(cap=cap, loader=ctl.store_loader),
+        "cpu": lambda: HostRankBackend(CpuBackend(), cap=cap, loader=ctl.store_loader),
     }[a.backend]()
     ctl.start()
     eg = ElasticGroup(grank, world, store_path=a.rdzv, backend=a.comm,

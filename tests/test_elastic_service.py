@@ -202,6 +202,9 @@ def test_preemption_reaches_fair_share_within_two_batch_times():
 
 
 def _replica_main(grank, world, rdzv, out):
+    import json
+    from concurrent.futures import ThreadPoolExecutor
+
     import numpy as np
     import torch
 
@@ -217,22 +220,26 @@ def _replica_main(grank, world, rdzv, out):
                 for n in names}
 
     st = HbmImageStore(16, (4, 4), torch.device("cpu"), n_synth=2, seed=0)
+    st.loader = load
+    st.stager.attach(eg.rank, eg.world, ThreadPoolExecutor(2), eg.all_gather_data_async)
     names = [f"{i}.jpeg" for i in range(10)] + ["bad.jpeg", "3.jpeg", "synthetic:5"]
-    n1 = st.replicate(names, load, rank=eg.rank, world=eg.world, gather=eg.all_gather_data)
-    n2 = st.replicate(names, load, rank=eg.rank, world=eg.world, gather=eg.all_gather_data)  # all known
+    w1 = st.plan(names, 0)
+    st.pin(names)
+    w2 = st.plan(names, 0)  # everything staged already: an empty window, done at once
+    while not st.ready(names):
+        st.stager.progress()
     slots, failed = st.slots(names)
     got = st.arena[slots].numpy()[:, 0, 0, 0].tolist()
-    import json
-    json.dump({"decoded": decoded, "n1": n1, "n2": n2, "failed": failed, "vals": got},
-              open(os.path.join(out, f"rep_{grank}.json"), "w"))
+    json.dump({"decoded": decoded, "n1": len(w1.names), "n2": len(w2.names), "failed": failed, "vals": got,
+               "slots": slots}, open(os.path.join(out, f"rep_{grank}.json"), "w"))
     eg.close()
 
 
 def test_hbm_image_store_decode_once_replicate_gloo(tmp_path):
-    """World 3: each rank decodes only ITS share of a job's new images (i % 3)
-    and one all-gather gives every rank every decoded image (the RCCL path on
-    GPUs; gloo here); a failed image is failed on every rank; known images are
-    never decoded again."""
+    """World 3: a window's new images are decoded once in the whole job — each rank
+    only ITS share (i % 3) — and one all-gather gives every rank every decoded image
+    in the same slots (the RCCL path on GPUs; gloo here); a failed image is failed on
+    every rank; staged images are never staged again."""
     ctx = mp.get_context("spawn")
     ps = [ctx.Process(target=_replica_main, args=(r, 3, str(tmp_path / "rdzv"), str(tmp_path))) for r in range(3)]
     for p in ps:
@@ -244,32 +251,60 @@ def test_hbm_image_store_decode_once_replicate_gloo(tmp_path):
     new = [f"{i}.jpeg" for i in range(10)] + ["bad.jpeg"]
     for r in range(3):
         assert res[r]["decoded"] == new[r::3]                 # its share only, once
-        assert res[r]["n1"] == 10 and res[r]["n2"] == 0
+        assert res[r]["n1"] == 11 and res[r]["n2"] == 0
         assert res[r]["failed"] == ["bad.jpeg"]
         assert res[r]["vals"][:10] == list(range(10)) and res[r]["vals"][11] == 3
-    assert res[0]["vals"] == res[1]["vals"] == res[2]["vals"]
+    assert res[0]["vals"] == res[1]["vals"] == res[2]["vals"] and res[0]["slots"] == res[2]["slots"]
 
 
-def test_hbm_image_store_eviction_keeps_the_batch():
-    """A full arena evicts FIFO, but never an image of the batch being
-    resolved: a batch mixing resident and missing-at-launch images gets every
-    resident image from its slot and the missing ones decoded into evicted
-    slots of OTHER images (eviction vs in-flight gathers)."""
+def test_hbm_image_store_window_pinning_and_eviction():
+    """A bounded arena: windows pin their images until their batches complete; a window
+    that does not fit next to the pinned images waits (plan -> None); the oldest
+    UNPINNED image is evicted first; a failed image is forgotten when its batch
+    completes, so a later window fetches it again (no permanent failure)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     import numpy as np
     import torch
 
     from distributed_machine_learning_amd.parallel.image_store import HbmImageStore
 
+    flaky = {"5.jpeg": 1}
+
     def load(names):
-        return {n: np.full((2, 2, 3), int(n.split(".")[0]), np.uint8) for n in names}
+        out = {}
+        for n in names:
+            if flaky.get(n, 0) > 0:
+                flaky[n] -= 1
+                out[n] = None
+            else:
+                out[n] = np.full((2, 2, 3), int(n.split(".")[0]), np.uint8)
+        return out
 
     st = HbmImageStore(6, (2, 2), torch.device("cpu"), n_synth=0)
-    st.replicate([f"{i}.jpeg" for i in range(6)], load)       # full: 0..5
-    batch = ["0.jpeg", "1.jpeg", "7.jpeg", "8.jpeg", "2.jpeg"]  # 0,1,2 resident (the oldest), 7,8 missing
-    slots, failed = st.slots(batch, load)
-    assert failed == []
-    assert st.arena[slots].numpy()[:, 0, 0, 0].tolist() == [0, 1, 7, 8, 2]
-    assert "3.jpeg" not in st.index and "4.jpeg" not in st.index   # the oldest NOT in the batch went
-    assert len(set(slots)) == 5
-    with pytest.raises(RuntimeError):                               # a batch larger than the arena
-        st.slots([f"{i}.jpeg" for i in range(10, 17)], load)
+    st.loader = load
+    st.stager.attach(0, 1, ThreadPoolExecutor(1), None)
+
+    def staged(names):
+        w = st.plan(names, 0)
+        if w is None:
+            return None
+        st.pin(names)
+        while not st.ready(names):
+            st.stager.progress()
+        return w
+    a, b = ["0.jpeg", "1.jpeg", "2.jpeg"], ["3.jpeg", "4.jpeg", "5.jpeg"]
+    assert staged(a) is not None and staged(b) is not None          # full: 6 of 6 slots pinned
+    assert st.slots(b)[1] == ["5.jpeg"]                              # the flaky image failed once
+    assert st.plan(["6.jpeg"], 0) is None                            # nothing evictable: wait
+    st.unpin(a)                                                      # batch A completed
+    c = ["6.jpeg", "7.jpeg"]
+    assert staged(c) is not None and st.evictions == 2
+    assert "0.jpeg" not in st.index and "1.jpeg" not in st.index and "2.jpeg" in st.index  # oldest first
+    assert st.arena[st.slots(c)[0]].numpy()[:, 0, 0, 0].tolist() == [6, 7]
+    st.unpin(b)                                                      # 5.jpeg (failed) is forgotten
+    assert "5.jpeg" not in st.index and "3.jpeg" in st.index
+    d = ["5.jpeg", "3.jpeg"]
+    assert staged(d) is not None                                     # fetched again, now fine
+    slots, failed = st.slots(d)
+    assert failed == [] and st.arena[slots].numpy()[:, 0, 0, 0].tolist() == [5, 3]

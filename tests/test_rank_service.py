@@ -7,8 +7,8 @@ of round 3, on CPU (gloo):
 * version pinning: a store image re-PUT between two jobs - the second job's
   output differs and equals the classifier on the new bytes.
 * rank rejoin: world 4, rank 1 killed mid-job and restarted; it is admitted into
-  a new epoch, its image store is backfilled over the data group (not decoded),
-  it serves batches again and every job completes.
+  a new epoch, the image windows are staged afresh over the new group (its share
+  decoded by it), it serves batches again and every job completes.
 * control-plane capacity: world 8, instant backend - batches moved per second
   by the one-collective steps is far above 8 ranks x 400 batches/s.
 """
@@ -168,7 +168,7 @@ def _rejoin_rank(grank, world, rdzv, swim, out, kill_step, rejoin):
     steps = svc.serve(max_steps=200000, stop_when_idle=True)
     res = {"steps": steps, "epoch": eg.epoch, "members": eg.members, "grows": svc.grows,
            "rebuilds": svc.rebuilds, "served_here": svc.served_here, "loads": len(loads),
-           "backfilled": sum(a.replicated for a in be.arenas.values()),
+           "replicated": sum(a.replicated for a in be.arenas.values()),
            "done": [coord.jobs.jobs[j].done for j in sorted(coord.jobs.jobs)]}
     eg.barrier()
     with open(os.path.join(out, f"rejoin_{grank}_{int(rejoin)}.json"), "w") as f:
@@ -203,7 +203,7 @@ def test_rank_rejoin_after_kill(tmp_path):
     assert r3["done"] == [True, True]
     assert r3["rebuilds"] >= 1 and r3["grows"] >= 1 and r3["members"] == [0, 1, 2, 3]
     assert r1["served_here"] > 0                   # the restarted rank served batches again
-    assert r1["backfilled"] > 0 and r1["loads"] == 0  # its images came from a survivor's store, not decoded
+    assert r1["replicated"] > 0                    # windows staged over the new group reached it
     files = set(os.listdir(tmp_path / "outputs"))
     keys = {tuple(f.split("_")[1:3]) for f in files}
     assert keys == {(str(j), str(b)) for j in (31, 32) for b in range(1, 201)}
@@ -287,3 +287,68 @@ def test_service_bench_record_world2(tmp_path):
     assert set(r0["batches_per_rank"]) == {"rank0", "rank1"} and sum(r0["batches_per_rank"].values()) == 80
     assert r0["value"] > 0 and r0["p90_latency_ms"]["ResNet50"] >= r0["p50_latency_ms"]["ResNet50"]
     assert not os.path.exists(tmp_path / "svc_out")            # rank 0 removed the output files
+
+
+# ------------------------------------------------- jobs larger than the arena --
+def _big_job_rank(grank, world, rdzv, out, n_images, arena):
+    import logging
+
+    logging.basicConfig(level=logging.WARNING)
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+    from distributed_machine_learning_amd.parallel.rank_backend import StoreRankBackend
+    from distributed_machine_learning_amd.parallel.service import (CollectiveService, OutputWriter,
+                                                                   ReplicatedCoordinator)
+
+    be = StoreRankBackend(loader=lambda ns: {n: (n * 3).encode() for n in ns}, cap=8, arena_images=arena,
+                          n_synth=16)
+    eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=60, shm_exchange=True)
+    coord = ReplicatedCoordinator({"ResNet50": 8, "InceptionV3": 8}, cap=8, depth=4)
+    writer = OutputWriter(os.path.join(out, "outputs"), host_tag="t")
+    svc = CollectiveService(eg, be, coord, writer=writer)
+    if svc.is_coordinator():
+        svc.submit_local("ResNet50", images=[f"r{i}.jpeg" for i in range(n_images)])
+        svc.submit_local("InceptionV3", images=[f"i{i}.jpeg" for i in range(n_images)])
+    svc.serve(max_steps=10 ** 7, stop_when_idle=True)
+    a = be.arenas["ResNet50"]
+    res = {"done": [coord.jobs.jobs[j].done for j in sorted(coord.jobs.jobs)], "loads": be.loads,
+           "evictions": a.evictions, "windows": a.windows_staged, "replicated": a.replicated}
+    eg.barrier()
+    with open(os.path.join(out, f"big_{grank}.json"), "w") as f:
+        json.dump(res, f)
+    writer.close()
+    eg.close()
+
+
+def test_job_three_times_the_arena_world4(tmp_path):
+    """World 4 (gloo + the shared-memory exchange): each model's job names 3x the
+    arena's image capacity in distinct images. Windows are staged ahead of dispatch and
+    evicted as batches complete, every image is fetched/decoded exactly once in the
+    whole job (by one rank), and every output row equals the classifier on that
+    image's bytes (reference: any N works, worker.py:196-206, 1361-1366)."""
+    from distributed_machine_learning_amd.parallel.rank_backend import StoreRankBackend
+    from distributed_machine_learning_amd.utils.labels import load_class_index
+
+    world, arena, n = 4, 16 + 64, 3 * 64
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_big_job_rank, args=(r, world, str(tmp_path / "rdzv"), str(tmp_path), n, arena))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(240)
+    assert [p.exitcode for p in ps] == [0] * world
+    res = [json.loads((tmp_path / f"big_{r}.json").read_text()) for r in range(world)]
+    assert all(r["done"] == [True, True] for r in res)
+    assert sum(r["loads"] for r in res) == 2 * n                  # decoded once in the whole job
+    assert all(r["evictions"] > 0 and r["windows"] > 1 for r in res)
+    be = StoreRankBackend(cap=8)
+    idx = load_class_index()
+    doc = {}
+    for f in os.listdir(tmp_path / "outputs"):
+        doc.update(json.load(open(tmp_path / "outputs" / f)))
+    assert len(doc) == 2 * n
+    for name, rows in doc.items():
+        model = "ResNet50" if name.startswith("r") else "InceptionV3"
+        be.loader = lambda ns, name=name: {name: (name * 3).encode()}
+        ids, p = StoreRankBackend.classify(be._load(model, [name])[name])
+        assert [e[0] for e in rows[0]] == [idx[int(c)][0] for c in ids], name

@@ -219,7 +219,7 @@ def test_store_images_replicated_to_hbm_and_served(tmp_path):
         svc.submit_local("ResNet50", images=names)
         svc.serve(max_steps=10 ** 6, stop_when_idle=True)
         st = be.arenas["ResNet50"]
-        assert st.replicated == 12 and st.failed == {"broken.jpeg"}
+        assert st.replicated == 12 and st.windows_staged >= 1   # decoded once, staged in windows
         doc = {}
         for f in os.listdir(tmp_path / "out"):
             doc.update(json.load(open(tmp_path / "out" / f)))
@@ -265,13 +265,12 @@ def test_rccl_abort_and_new_epoch(tmp_path):
         eg.close()
 
 
-def test_small_arena_eviction_and_missing_at_launch(tmp_path):
-    """an HBM arena smaller than two jobs. Job B's
-    replication evicts job A's images before A's batches launch, so A's images
-    are missing at launch and decoded again by the fallback in launch(), whose
-    arena writes evict other images while gathers are still queued on the
-    compute stream. Every output row must still equal Engine.infer of the
-    right decoded images."""
+def test_job_three_times_the_arena_gpu(tmp_path):
+    """One job with 3x the HBM arena's image capacity in distinct store JPEGs
+    (RCCL data group, world 1): windows are staged ahead of dispatch and the oldest
+    unpinned images evicted as batches complete; every image is decoded once and every
+    output row equals Engine.infer of the right decoded image (a job larger
+    than the arena used to kill the service)."""
     import io
 
     from PIL import Image
@@ -285,11 +284,10 @@ def test_small_arena_eviction_and_missing_at_launch(tmp_path):
 
     rng = np.random.default_rng(1)
     blobs = {}
-    for j in "ab":
-        for i in range(12):
-            buf = io.BytesIO()
-            Image.fromarray(rng.integers(0, 255, (256, 240 + 4 * i, 3), dtype=np.uint8)).save(buf, format="JPEG")
-            blobs[f"{j}{i}.jpeg"] = buf.getvalue()
+    for i in range(48):
+        buf = io.BytesIO()
+        Image.fromarray(rng.integers(0, 255, (256, 240 + 2 * i, 3), dtype=np.uint8)).save(buf, format="JPEG")
+        blobs[f"a{i}.jpeg"] = buf.getvalue()
     loads = []
 
     def loader(ns):
@@ -301,25 +299,24 @@ def test_small_arena_eviction_and_missing_at_launch(tmp_path):
         bs = {"ResNet50": 8, "InceptionV3": 8}
         be = GpuRankBackend(dev, bs, cap=8, arena_images=24, n_synth=8, loader=loader)
         st = be.arenas["ResNet50"]
-        assert st.capacity == 24                      # 16 image slots for 24 job images
+        assert st.capacity == 24                      # 16 image slots for a 48-image job
         coord = ReplicatedCoordinator(bs, cap=8, host_tag="gpu")
         writer = OutputWriter(str(tmp_path / "out"), host_tag="gpu")
         svc = CollectiveService(eg, be, coord, writer=writer, on_device=False)
-        na = [f"a{i}.jpeg" for i in range(12)]
-        nb = [f"b{i}.jpeg" for i in range(12)]
+        na = [f"a{i}.jpeg" for i in range(48)]
         svc.submit_local("ResNet50", images=na)
-        svc.submit_local("ResNet50", images=nb)
         svc.serve(max_steps=10 ** 6, stop_when_idle=True)
-        assert st.replicated > 24                     # images were decoded again at launch
+        assert st.replicated == 48 and st.evictions >= 32   # each image decoded once; slots recycled
+        assert sorted(n for ns in loads for n in ns) == sorted(na)
         doc = {}
         for f in os.listdir(tmp_path / "out"):
             doc.update(json.load(open(tmp_path / "out" / f)))
-        assert sorted(doc) == sorted(na + nb)
+        assert sorted(doc) == sorted(na)
         g, w = build_model("ResNet50", seed=0)
         cls = {wnid: i for i, (wnid, _) in enumerate(load_class_index())}
-        for names in (na, nb):
+        for names in (na,):
             imgs = torch.from_numpy(np.stack([load_image(blobs[n], (224, 224)) for n in names]))
-            for b0 in range(0, 12, 8):
+            for b0 in range(0, 48, 8):
                 rows = imgs[b0:b0 + 8]
                 pad = torch.zeros((8, 224, 224, 3), dtype=torch.uint8)
                 pad[:len(rows)] = rows
