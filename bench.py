@@ -84,7 +84,11 @@ def parse_args(argv=None):
                     help="also write the service run's output files to this directory (removed afterwards); "
                          "every output is always PUT into the ranks' replicated store, as serving.main --role rank")
     ap.add_argument("--kill", action="append", default=[],
-                    help="rank:step - inject a rank kill into the service run (BASELINE config 5; needs --gpus > 1)")
+                    help="rank:batches - a kill of the config-5 pass: the rank exits once that many batches completed "
+                         "(default: 2 kills, service_bench.default_kills)")
+    ap.add_argument("--kill-pass", default="auto", choices=("auto", "on", "off"),
+                    help="BASELINE config 5: a second service pass with injected rank kills, run in child "
+                         "processes (a killed rank exits 17); auto = on when --gpus >= 4")
     return ap.parse_args(argv)
 
 
@@ -173,7 +177,7 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
     if not args.no_verify:
         # the last timed step's gathered rows vs a fresh Engine.infer of the same images
         last = args.steps - 1
-        got = pipe.host_res[last % 2].clone() if rank == 0 else None
+        got = pipe.results_of(last).clone() if rank == 0 else None
         start = (last * B) % cap
         idx = [(start + i) % cap for i in range(B)]
         ti, tp = eng.infer(torch.from_numpy(store.array[idx]).to(device))
@@ -331,12 +335,26 @@ def bench_service(args, rank: int, world: int, device, recs: dict):
     from distributed_machine_learning_amd.parallel import service_bench
 
     rdzv, port = service_bench.agree(rank)
+    kill_pass = args.kill_pass == "on" or (args.kill_pass == "auto" and world >= 4)
+    if kill_pass:
+        rdzv_k, port_k = service_bench.agree(rank)
     dist.destroy_process_group()  # the service builds its own epoch-versioned groups
     rates = {m: r["value"] for m, r in recs.items() if r and "value" in r}
     out_dir = (os.path.join(args.svc_outputs, os.path.basename(rdzv) + "_outputs") if args.svc_outputs else None)
     rec = service_bench.run(rank, world, device, rdzv, port, args.svc_resnet_images * world,
-                            args.svc_inception_images * world, dict(DEFAULT_BATCH), out_dir,
-                            kills=service_bench.parse_kills(args.kill), single_rates=rates)
+                            args.svc_inception_images * world, dict(DEFAULT_BATCH), out_dir, single_rates=rates)
+    if kill_pass:
+        # BASELINE config 5: the same concurrent jobs with two ranks killed mid-job (SWIM
+        # detects, the survivors rebuild and re-dispatch); each rank's share runs in a child
+        nb = sum(-(-n * world // DEFAULT_BATCH[m]) for m, n in (("ResNet50", args.svc_resnet_images),
+                                                                 ("InceptionV3", args.svc_inception_images)))
+        kills = service_bench.parse_kills(args.kill) or service_bench.default_kills(world, nb)
+        krec = service_bench.run_in_children(rank, world, device.index or 0, rdzv_k, port_k,
+                                             args.svc_resnet_images * world, args.svc_inception_images * world,
+                                             dict(DEFAULT_BATCH), kills)
+        if rec is not None and krec is not None:
+            krec["metric"] = "config 5: " + krec["metric"] + ", 2 ranks killed mid-job"
+            rec["kill_pass"] = krec
     return rec
 
 

@@ -33,6 +33,13 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
   return base + (b >> 3);
 }
 
+// Entry n of an index table in pinned host memory that the host rewrites between
+// launches (the serving path's arena slot table): a system-scope vector load, never
+// served from a stale cache line of an earlier launch.
+__device__ __forceinline__ int dml_host_index(const int* idx, int n) {
+  return __hip_atomic_load(idx + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace dml
 
 // error plumbing for the host API (defined in runtime/errors.hip)

@@ -315,7 +315,8 @@ __device__ __forceinline__ void preprocess_pixel(const DmlPreprocArgs& a, const 
   int iy = (int)(((float)oh + 0.5f) * sy), ix = (int)(((float)ow + 0.5f) * sx);
   iy = min(iy, a.Hs - 1);
   ix = min(ix, a.Ws - 1);
-  const unsigned char* px = src + (((long)n * a.Hs + iy) * a.Ws + ix) * 3;
+  const long img_n = a.idx ? (long)dml_host_index(a.idx, n) : (long)n;  // an HBM arena slot (serving path) or n
+  const unsigned char* px = src + ((img_n * a.Hs + iy) * a.Ws + ix) * 3;
   const float r = px[0], g = px[1], b = px[2];
   if (a.mode == 0) {  // caffe: RGB->BGR, subtract BGR mean, no scaling
     f[0] = b - 103.939f; f[1] = g - 116.779f; f[2] = r - 123.68f;

@@ -95,7 +95,10 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
   // make hipcc wait vmcnt(0) per pixel) and padding is zeroed afterwards.
   {
     const float sy = (float)a.Hs / (float)a.H, sx = (float)a.Ws / (float)a.W;
-    const unsigned char* img = (const unsigned char*)a.src + (long)n * a.Hs * a.Ws * 3;
+    // the serving path reads the image straight from its HBM arena slot (a.idx: the batch's
+    // slot table, pinned host memory written before the launch) - no gather copy in between
+    const long img_n = a.idx ? (long)dml_host_index(a.idx, n) : (long)n;
+    const unsigned char* img = (const unsigned char*)a.src + img_n * a.Hs * a.Ws * 3;
     unsigned char px[FILL][2][3];
     unsigned okm[FILL];
 #pragma unroll
@@ -322,7 +325,10 @@ __global__ __launch_bounds__(NT, 3) void inc_stem_kernel(DmlIncStemArgs a) {
   // 1. input patch (pair-packed; all loads issued before any conversion)
   {
     const float sy = (float)a.Hs / (float)a.H, sx = (float)a.Ws / (float)a.W;
-    const unsigned char* img = (const unsigned char*)a.src + (long)n * a.Hs * a.Ws * 3;
+    // the serving path reads the image straight from its HBM arena slot (a.idx: the batch's
+    // slot table, pinned host memory written before the launch) - no gather copy in between
+    const long img_n = a.idx ? (long)dml_host_index(a.idx, n) : (long)n;
+    const unsigned char* img = (const unsigned char*)a.src + img_n * a.Hs * a.Ws * 3;
     unsigned char px[FILL][2][3];
     unsigned okm[FILL];
 #pragma unroll

@@ -56,7 +56,7 @@ class PreprocArgs(C.Structure):
     _fields_ = [
         ("src", C.c_void_p), ("y", C.c_void_p),
         ("N", C.c_int), ("Hs", C.c_int), ("Ws", C.c_int), ("Ho", C.c_int), ("Wo", C.c_int), ("mode", C.c_int),
-        ("pair", C.c_int), ("lpad", C.c_int),
+        ("pair", C.c_int), ("lpad", C.c_int), ("idx", C.c_void_p),
     ]
 
 
@@ -66,7 +66,7 @@ class StemArgs(C.Structure):
         ("N", C.c_int), ("Hs", C.c_int), ("Ws", C.c_int), ("H", C.c_int), ("W", C.c_int), ("mode", C.c_int),
         ("ldw", C.c_int), ("Hc", C.c_int), ("Wc", C.c_int), ("Ho", C.c_int), ("Wo", C.c_int), ("ldy", C.c_int),
         ("w4", C.c_void_p), ("b4", C.c_void_p), ("z", C.c_void_p), ("c4", C.c_int), ("ldw4", C.c_int),
-        ("ldz", C.c_int),
+        ("ldz", C.c_int), ("idx", C.c_void_p),
     ]
 
 
@@ -76,7 +76,7 @@ class IncStemArgs(C.Structure):
         ("y", C.c_void_p),
         ("N", C.c_int), ("Hs", C.c_int), ("Ws", C.c_int), ("H", C.c_int), ("W", C.c_int), ("mode", C.c_int),
         ("ldw1", C.c_int), ("ldw2", C.c_int), ("H1", C.c_int), ("W1", C.c_int), ("H2", C.c_int), ("W2", C.c_int),
-        ("ldy", C.c_int),
+        ("ldy", C.c_int), ("idx", C.c_void_p),
     ]
 
 

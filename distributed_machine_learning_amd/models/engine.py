@@ -62,11 +62,16 @@ class Engine:
                  result_views: Optional[List[torch.Tensor]] = None, fuse_stem: bool = True,
                  fuse_blocks: bool = True, conv_groups: Optional[bool] = None,
                  ext_buffers: Optional[Dict[str, List[torch.Tensor]]] = None,
-                 tune_range: Optional[Tuple[Optional[str], Optional[str]]] = None):
+                 tune_range: Optional[Tuple[Optional[str], Optional[str]]] = None,
+                 src_index: Optional[List[torch.Tensor]] = None):
         """``share``: reuse another engine's (optimized) graph and resident weights
         (sub-batch engines of a SplitEngine); ``src_tensors`` / ``result_views``:
         external uint8 source slots / per-slot [2, batch, 5] result rows to use
-        instead of allocating them. ``fuse_stem=False`` (or DML_FUSED_STEM=0) keeps the
+        instead of allocating them. ``src_index``: per slot, an int32 [batch] table
+        (pinned host memory, rewritten by the caller before each run): image n of the
+        batch is image src_index[slot][n] of that slot's source tensor — the serving
+        path's HBM arena, read in place by the stem kernel instead of gathered into a
+        batch buffer first. ``fuse_stem=False`` (or DML_FUSED_STEM=0) keeps the
         ResNet stem as three launches (preprocess, conv, pool); ``fuse_blocks=False``
         (or DML_FUSED_BLOCKS=0) keeps every bottleneck 1x1 conv its own launch;
         ``conv_groups=False`` (or DML_CONV_GROUPS=0) launches InceptionV3's
@@ -130,6 +135,10 @@ class Engine:
         # independent residual-free convs of one graph level -> one grouped grid each
         self.conv_groups = self._conv_group_candidates() if conv_groups else []
         self._src_tensors, self._result_views = src_tensors, result_views
+        self.src_index = src_index
+        if src_index is not None:
+            assert len(src_index) == src_slots and all(t.dtype == torch.int32 and t.numel() >= batch
+                                                       and t.is_contiguous() for t in src_index)
         self._ext = ext_buffers or {}
         self._tune_range = tune_range
         self.op_range: Optional[Tuple[int, int]] = None
@@ -556,14 +565,16 @@ class Engine:
         for i in range(self.src_slots):
             for name, ts in self._ext.items():
                 self.buf[name] = ts[i]
-            self.plans.append(self._build_one_plan(self.srcs[i], self.results[i]))
+            self.plans.append(self._build_one_plan(self.srcs[i], self.results[i],
+                                                   self.src_index[i] if self.src_index is not None else None))
         for name, ts in self._ext.items():
             self.buf[name] = ts[0]
         self.plan = self.plans[0]
         self.graph_captured = [False] * self.src_slots
 
-    def _build_one_plan(self, src: torch.Tensor, result: torch.Tensor):
+    def _build_one_plan(self, src: torch.Tensor, result: torch.Tensor, idx: Optional[torch.Tensor] = None):
         g, B, L = self.g, self.batch, self.lib
+        idx_ptr = idx.data_ptr() if idx is not None else None
         plan = L.dml_plan_create()
         self.op_names: List[str] = []
         self.op_cfg: Dict[str, int] = {}
@@ -583,6 +594,7 @@ class Engine:
                 w4, b4, _, kp4, _ = self.wdev[k.name]
                 sa.w4, sa.b4, sa.z, sa.c4, sa.ldw4, sa.ldz = (w4.data_ptr(), b4.data_ptr(), self.buf[k.out].data_ptr(),
                                                               k.cout, kp4, self.cbuf[k.out])
+            sa.idx = idx_ptr
             N.check(L.dml_plan_add_stem(plan, C.byref(sa)), "plan stem")
             self._keep.append(sa)
             self.op_names.append(f"preprocess+{s.name}+{p.name}" + (f"+{k.name}" if k is not None else ""))
@@ -596,12 +608,14 @@ class Engine:
             ia = N.IncStemArgs(src.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
                                self.buf[c.out].data_ptr() + 2 * c.out_coff, B, self.src_hw[0], self.src_hw[1],
                                g.input_hw[0], g.input_hw[1], mode, kp1, kp2, h1, wd1, h2, wd2, self.cbuf[c.out])
+            ia.idx = idx_ptr
             N.check(L.dml_plan_add_inc_stem(plan, C.byref(ia)), "plan inception stem")
             self.op_names.append(f"preprocess+{s.name}+{c.name}")
             skip = {s.name, c.name}
         else:
             pa = N.PreprocArgs(src.data_ptr(), self.buf[g.input].data_ptr(), B, self.src_hw[0], self.src_hw[1],
                                g.input_hw[0], g.input_hw[1], mode, int(self.stem is not None), self.stem_lpad)
+            pa.idx = idx_ptr
             N.check(L.dml_plan_add_preprocess(plan, C.byref(pa)), "plan preprocess")
             self.op_names.append("preprocess")
         skip |= {p.name for p in self.conv_pools.values()}
@@ -826,6 +840,8 @@ class Engine:
 
     def infer(self, images_u8: torch.Tensor, stream=None):
         """images_u8: [B, Hs, Ws, 3] uint8 (any device). Returns (top_idx, top_p) on device."""
+        if self.src_index is not None:
+            raise RuntimeError("infer: this engine reads an arena through its index table; fill it and run()")
         self.src.copy_(images_u8, non_blocking=True)
         self.run(stream)
         return self.top_idx, self.top_p
@@ -881,7 +897,9 @@ class SplitEngine:
 
     def __init__(self, graph: Graph, weights: Weights, batch: int, device: str = "cuda", splits: int = 2,
                  src_slots: int = 1, src_hw: Optional[Tuple[int, int]] = None, streams: int = 0,
-                 merge_at: Optional[str] = None, **kw):
+                 merge_at: Optional[str] = None, src_tensors: Optional[List[torch.Tensor]] = None,
+                 src_index: Optional[List[torch.Tensor]] = None, result_views: Optional[List[torch.Tensor]] = None,
+                 **kw):
         """``streams``: concurrent streams (default = splits); sub-batch i runs on
         stream i % streams, so splits=4, streams=2 runs two half-size sub-batches
         back to back on each of two streams (smaller per-layer working sets that
@@ -889,7 +907,9 @@ class SplitEngine:
         ``merge_at`` (a node name of the optimized graph; splits = 2): split head, merged
         tail — the two half-batch engines run the graph up to that node on two streams and
         ONE full-batch engine runs the rest (the late, small-grid layers at twice the grid),
-        see ``_init_merged``."""
+        see ``_init_merged``. ``src_tensors`` / ``src_index`` / ``result_views``: as
+        Engine's, for the whole batch (with ``src_index`` every sub-batch engine reads the
+        full source tensor through its rows of the index table)."""
         if batch % splits:
             raise ValueError(f"batch {batch} not divisible by splits {splits}")
         sub = batch // splits
@@ -897,11 +917,14 @@ class SplitEngine:
         self.nstreams = max(1, min(streams or splits, splits))
         self.device = torch.device(device)
         hw = src_hw or graph.input_hw
-        self.srcs = [torch.zeros((batch, hw[0], hw[1], 3), device=self.device, dtype=torch.uint8)
-                     for _ in range(src_slots)]
+        self.srcs = (list(src_tensors) if src_tensors is not None else
+                     [torch.zeros((batch, hw[0], hw[1], 3), device=self.device, dtype=torch.uint8)
+                      for _ in range(src_slots)])
         self.src = self.srcs[0]
-        self.results = [torch.zeros((2, batch, 5), device=self.device, dtype=torch.int32)
-                        for _ in range(src_slots)]
+        self.src_index = src_index
+        self.results = (list(result_views) if result_views is not None else
+                        [torch.zeros((2, batch, 5), device=self.device, dtype=torch.int32)
+                         for _ in range(src_slots)])
         self._select_result(0)
         self.tails: List[Engine] = []
         if merge_at:
@@ -912,8 +935,7 @@ class SplitEngine:
             rows = slice(i * sub, (i + 1) * sub)
             self.engines.append(Engine(graph, weights if i == 0 else None, batch=sub, device=device,
                                        src_slots=src_slots, src_hw=hw, share=self.engines[0] if i else None,
-                                       src_tensors=[t[rows] for t in self.srcs],
-                                       result_views=[r[:, rows] for r in self.results],
+                                       **self._sub_src(rows), result_views=[r[:, rows] for r in self.results],
                                        **kw))
         self.g = self.engines[0].g
         # stream 0 is the caller's stream: only nstreams-1 extra streams.
@@ -922,6 +944,13 @@ class SplitEngine:
         self.streams = [torch.cuda.Stream(self.device) for _ in range(self.nstreams - 1)]
         self._fork = torch.cuda.Event()
         self._join = [torch.cuda.Event() for _ in range(self.nstreams - 1)]
+
+    def _sub_src(self, rows: slice) -> dict:
+        """Source arguments of the sub-batch engine of ``rows``: its rows of the batch
+        buffers, or (index mode) the whole source tensor + its rows of the index table."""
+        if self.src_index is None:
+            return {"src_tensors": [t[rows] for t in self.srcs]}
+        return {"src_tensors": list(self.srcs), "src_index": [t[rows] for t in self.src_index]}
 
     def _init_merged(self, graph: Graph, weights: Weights, hw, merge_at: str, kw) -> None:
         """Split head, merged tail. Two half-batch HEAD engines run ops up to ``merge_at`` (the
@@ -941,6 +970,7 @@ class SplitEngine:
             self.tails.append(Engine(graph, weights if s == 0 else None, batch=B, device=str(self.device),
                                      src_slots=1, src_hw=hw, share=self.tails[0] if s else None,
                                      src_tensors=[self.srcs[s]], result_views=[self.results[s]],
+                                     src_index=[self.src_index[s]] if self.src_index is not None else None,
                                      tune_range=(merge_at, None), **kw))
         t0 = self.tails[0]
         g = t0.g
@@ -958,7 +988,7 @@ class SplitEngine:
         for i in range(2):
             ext = {name: [rows(self.tails[s], name, i) for s in range(self.src_slots)] for name in self.merge_tensors}
             self.engines.append(Engine(graph, None, batch=sub, device=str(self.device), src_slots=self.src_slots,
-                                       src_hw=hw, share=t0, src_tensors=[t[i * sub:(i + 1) * sub] for t in self.srcs],
+                                       src_hw=hw, share=t0, **self._sub_src(slice(i * sub, (i + 1) * sub)),
                                        result_views=[r[:, i * sub:(i + 1) * sub] for r in self.results],
                                        ext_buffers=ext, tune_range=(None, merge_at), **kw))
         for e in self.engines:
@@ -1069,6 +1099,8 @@ class SplitEngine:
         self._tail_done[slot].record(main)
 
     def infer(self, images_u8: torch.Tensor, stream=None):
+        if self.src_index is not None:
+            raise RuntimeError("infer: this engine reads an arena through its index table; fill it and run()")
         self.src.copy_(images_u8, non_blocking=True)
         self.run(stream)
         return self.top_idx, self.top_p

@@ -261,16 +261,6 @@ class HbmImageStore:
         w.bufs, w.work, w.flags, w.done = None, None, None, True
         return True
 
-    # ------------------------------------------------------------ batches --
-    def gather_into(self, dst: torch.Tensor, slots: Sequence[int]) -> None:
-        """dst[:len(slots)] = arena[slots] on the current stream. The index list
-        goes up through pinned memory, asynchronously: a pageable copy would make
-        the host wait for everything already queued on this stream."""
-        idx = torch.tensor(list(slots), dtype=torch.long)
-        if self.device.type == "cuda":
-            idx = idx.pin_memory().to(self.device, non_blocking=True)
-        torch.index_select(self.arena, 0, idx, out=dst[:len(slots)])
-
 
 class Stager:
     """The windows of every model's store in ONE plan order: their all-gathers go out

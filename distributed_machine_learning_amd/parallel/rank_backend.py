@@ -58,7 +58,11 @@ class RankBackend:
         res, ev = self.launch(model, names, 0)
         if ev is not None:
             ev.synchronize()
+        self.finalize(0)
         return res
+
+    def finalize(self, slot: int) -> None:
+        """(serve loop, after the slot's launch event completed, before its rows are read)"""
 
     # staging hooks (parallel/image_store.py): every rank calls stage / release /
     # reset_staging at the same points of the replicated job state; backends that fetch
@@ -278,16 +282,19 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
     """Native engines for both models resident in this GPU's HBM, fed from per-model
     HBM image stores (parallel/image_store.py: store images staged in windows ahead of
     dispatch, decoded once per job and replicated to every rank over the data group —
-    RCCL — plus seeded synthetic images). A batch is gathered from the store into the
-    engine's source slot on the compute stream, after waiting on the events of the
-    windows that staged its images; its top-5 rows are copied into pinned host memory
-    on the same stream, then an event is recorded. A batch larger than the engine's
-    batch runs as several engine passes into consecutive result rows.
+    RCCL — plus seeded synthetic images). A batch is never gathered: the engines' stem
+    kernels read its images in place from the arena through a per-slot index table
+    (pinned host memory, written before the launch; Engine ``src_index``), and the
+    top-5 kernel writes the result rows straight into the slot's pinned host buffer
+    (Engine ``result_views``) — a launch is one graph replay and one event, no copy.
+    The compute stream waits on the events of the windows that staged the batch's
+    images. A batch larger than the engine's batch runs as several engine passes, one
+    after the other (the host collects each pass's rows; a rare, blocking path).
 
     Arena writes (window scatters) run on ``stage_stream``; a launch makes the compute
     stream wait for the windows of its images. A slot is only re-assigned after every
-    batch pinning its old image completed (its gather is done), so a scatter never
-    overtakes a gather that still reads the old image."""
+    batch pinning its old image completed, so a scatter never overtakes a forward that
+    still reads the old image."""
 
     def __init__(self, device: torch.device, batch_sizes: Dict[str, int], cap: int = 0, arena_images: int = 8192,
                  n_synth: int = 512, seed: int = 0, models: Sequence[str] = MODELS, splits: int = 2,
@@ -298,25 +305,31 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
 
         self.device = device
         self.cap = cap or max(batch_sizes.values())
-        self.engines, self.arenas = {}, {}
+        self.engines, self.arenas, self.idx = {}, {}, {}
         self.stream = torch.cuda.Stream(device)
         self.stage_stream = torch.cuda.Stream(device)
         self._init_staging(loader, decode_threads)
+        self.host = [torch.zeros((2, self.cap, 5), dtype=torch.int32).pin_memory() for _ in range(SLOTS)]
+        self.ev_done = [torch.cuda.Event() for _ in range(SLOTS)]
+        self.fail_rows: List[Optional[List[int]]] = [None] * SLOTS
         for m in models:
             g, w = build_model(m, seed=seed, calibrate=True)
             b = batch_sizes[m]
+            if b > self.cap:
+                raise ValueError(f"{m}: engine batch {b} exceeds the result capacity {self.cap}")
+            arena = HbmImageStore(max(arena_images, n_synth + 2 * self.cap), g.input_hw, device,
+                                  n_synth=n_synth, seed=1000 + MODEL_IDS[m])
+            self.arenas[m] = arena
+            self._adopt(m, arena)
+            self.idx[m] = [torch.zeros(b, dtype=torch.int32).pin_memory() for _ in range(SLOTS)]
+            src = dict(src_tensors=[arena.arena] * SLOTS, src_index=self.idx[m],
+                       result_views=[h[:, :b] for h in self.host])
             if splits > 1 and b % splits == 0:
                 self.engines[m] = SplitEngine(g, w, batch=b, device=str(device), src_slots=SLOTS, splits=splits,
-                                              merge_at=merge_point(m) if splits == 2 else None)
+                                              merge_at=merge_point(m) if splits == 2 else None, **src)
             else:
-                self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=SLOTS)
-            self.arenas[m] = HbmImageStore(max(arena_images, n_synth + 2 * self.cap), g.input_hw, device,
-                                           n_synth=n_synth, seed=1000 + MODEL_IDS[m])
-            self._adopt(m, self.arenas[m])
+                self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=SLOTS, **src)
             self.engines[m].capture(self.stream)  # graphs now, before the service's first collective
-        self.out = [torch.zeros((2, self.cap, 5), dtype=torch.int32, device=device) for _ in range(SLOTS)]
-        self.host = [torch.zeros((2, self.cap, 5), dtype=torch.int32).pin_memory() for _ in range(SLOTS)]
-        self.ev_done = [torch.cuda.Event() for _ in range(SLOTS)]
 
     def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
         """(decode pool thread) fetch + decode this rank's share of a window."""
@@ -342,24 +355,38 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
         eng, arena = self.engines[model], self.arenas[model]
         s = self.stream
-        out = self.out[slot]
         B = eng.batch
         slots, failed = arena.slots(list(names))
+        bad = set(failed)
+        self.fail_rows[slot] = [i for i, n in enumerate(names) if n in bad] if bad else None
+        iv = self.idx[model][slot].numpy()   # the slot's previous launch has finished: free to rewrite
+        host = self.host[slot]
         with torch.cuda.stream(s):
             for ev in arena.events(names):  # the windows that staged these images
                 s.wait_event(ev)
-            for off in range(0, len(slots), B):  # one engine pass per B images: never truncated
-                chunk = slots[off:off + B]
-                arena.gather_into(eng.srcs[slot], chunk)
+            if len(slots) <= B:
+                iv[:len(slots)] = slots
+                iv[len(slots):] = slots[0] if slots else 0   # padding rows: computed, never reported
                 eng.run(s, use_graph=True, slot=slot)
-                out[:, off:off + len(chunk)].copy_(eng.results[slot][:, :len(chunk)])
-            if failed:  # unfetchable / undecodable images: class id -1 marks the row failed
-                bad = set(failed)
-                rows = torch.tensor([i for i, n in enumerate(names) if n in bad], dtype=torch.long)
-                out[0].index_fill_(0, rows.pin_memory().to(self.device, non_blocking=True), -1)
-            self.host[slot].copy_(out, non_blocking=True)
+            else:  # larger than the engine batch: passes one after the other, rows collected here
+                rows = []
+                for off in range(0, len(slots), B):
+                    chunk = slots[off:off + B]
+                    iv[:len(chunk)] = chunk
+                    iv[len(chunk):] = chunk[0]
+                    eng.run(s, use_graph=True, slot=slot)
+                    s.synchronize()
+                    rows.append(host[:, :len(chunk)].clone())
+                host[:, :len(slots)] = torch.cat(rows, 1)
             self.ev_done[slot].record(s)
-        return self.host[slot], self.ev_done[slot]
+        return host, self.ev_done[slot]
+
+    def finalize(self, slot: int) -> None:
+        """(after the slot's event) unfetchable / undecodable images: class id -1 marks the row failed."""
+        rows = self.fail_rows[slot]
+        if rows:
+            self.host[slot][0, rows] = -1
+            self.fail_rows[slot] = None
 
     def drain(self) -> None:
         # the compute stream only ever waits on window events that had completed (ready()),

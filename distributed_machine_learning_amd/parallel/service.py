@@ -379,7 +379,10 @@ class OutputWriter:
         b, idx, p, g, _, _ = item
         try:
             data = self.renderer.render(b.images, idx, p)
-            name = output_name(b.job_id, b.batch_id, f"{self.host_tag}-rank{g}")
+            # one name per (job, batch) whichever rank ran it: a batch re-run after a rank
+            # died between storing its output and reporting it writes a new VERSION of the
+            # same file, so every output exists exactly once in the store
+            name = output_name(b.job_id, b.batch_id, self.host_tag)
             if self.out_dir:
                 with open(os.path.join(self.out_dir, name), "wb") as f:
                     f.write(data)
@@ -497,10 +500,13 @@ class CollectiveService:
     def __init__(self, eg: ElasticGroup, backend: RankBackend, coord: ReplicatedCoordinator,
                  control=None, writer: Optional[OutputWriter] = None, kill_rank: int = -1, kill_at_step: int = -1,
                  on_device: bool = False, idle_sleep: float = 0.002, poll_sleep: float = 0.0002,
-                 watchdog_s: float = 0.0, rejoined: bool = False):
+                 watchdog_s: float = 0.0, rejoined: bool = False, kill_at_done: int = -1):
         self.eg, self.be, self.coord, self.control = eg, backend, coord, control
         self.writer = writer
-        self.kill_rank, self.kill_at_step = kill_rank, kill_at_step
+        # fault injection (tests, BASELINE config 5): rank kill_rank exits 17 at step
+        # kill_at_step, or once kill_at_done batches have completed (replicated count)
+        self.kill_rank, self.kill_at_step, self.kill_at_done = kill_rank, kill_at_step, kill_at_done
+        self.completed = 0
         self.dev = backend.device if on_device else torch.device("cpu")
         self.steps = 0
         self.rebuilds = 0
@@ -586,6 +592,7 @@ class CollectiveService:
             if L.event is not None and not L.event.query():
                 break
             self.gpu.popleft()
+            self.be.finalize(L.slot)
             svc = time.monotonic() - L.t0
             k = len(L.batch.images)
             rows = L.rows[:, :k].numpy()
@@ -750,8 +757,10 @@ class CollectiveService:
         if mine is None:  # STOP (sent only when nothing is queued or in flight)
             return False
         self.batches_per_step_max = max(self.batches_per_step_max, moved)
-        if self.steps == self.kill_at_step and eg.grank == self.kill_rank:
-            log.warning("rank %d: injected kill at step %d", eg.grank, self.steps)
+        self.completed += len(finished)
+        if eg.grank == self.kill_rank and (self.steps == self.kill_at_step or
+                                           0 <= self.kill_at_done <= self.completed):
+            log.warning("rank %d: injected kill at step %d (%d batches done)", eg.grank, self.steps, self.completed)
             os._exit(17)
         # own new batches, then the revoke requests addressed to this rank (host queue only)
         self.hostq.extend(mine)

@@ -48,14 +48,14 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
     store_root = os.path.join(os.environ.get("DML_RDZV_DIR", "/tmp"), os.path.basename(rdzv) + "_store")
     ctl = RankControl(rank, world, swim_base, store_dir=os.path.join(store_root, f"rank{rank}"),
                       replication=min(4, world), on_dead=eg.dead.add, on_alive=eg.joiners.add).start()
-    kr, ks = -1, -1
-    for r, s in kills:
+    kr, kd = -1, -1   # kills: (rank, batches completed when it dies)
+    for r, d in kills:
         if r == rank:
-            kr, ks = r, s
+            kr, kd = r, d
     coord = ReplicatedCoordinator(batch_sizes, cap=cap, host_tag="mi355x", depth=depth)
     writer = OutputWriter(os.path.join(out_dir, f"rank{rank}") if out_dir else None,
                           put_many_async=ctl.store_put_many_async, host_tag="mi355x")
-    svc = CollectiveService(eg, backend, coord, control=ctl, writer=writer, kill_rank=kr, kill_at_step=ks,
+    svc = CollectiveService(eg, backend, coord, control=ctl, writer=writer, kill_rank=kr, kill_at_done=kd,
                             on_device=(comm == "nccl"), watchdog_s=300)
     if svc.is_coordinator():
         if resnet_images:
@@ -91,6 +91,10 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
         else:
             allsv = [served]
         if svc.is_coordinator():
+            # every batch's output is in the store exactly once (the listing is the store
+            # leader's metadata, i.e. this rank's): one name per (job, batch)
+            listing = ctl.call(ctl.node.store.ls_all("output_*"), timeout=60)
+            pairs = {tuple(nm.split("_")[1:3]) for nm in listing}
             c2 = coord.metrics.c2()
             n = {m: coord.metrics.query_count.get(m, 0) for m in MODELS}
             tot = sum(n.values())
@@ -111,11 +115,13 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                             "failed": int(sum(int(v[2]) for v in allsv)),
                             "bytes": int(sum(int(v[3]) for v in allsv)), "dir": out_dir or None,
                             "store": f"replicated store, R = {min(4, world)}, bundled PUTs (put_many)",
+                            "in_store": len(set(listing)), "distinct_batches_in_store": len(pairs),
+                            "listing_duplicates": len(listing) - len(set(listing)),
                             "put_bundles_coordinator": writer.bundles,
                             "writer_busy_s_coordinator": round(writer.busy_s, 3)},
                 "steps": steps, "max_batches_per_step": svc.batches_per_step_max,
                 "rebuilds": svc.rebuilds, "preempted_batches": coord.preempted, "requeued_batches": coord.requeued,
-                "kills": [f"{r}:{s}" for r, s in kills], "final_members": eg.members,
+                "kills": [f"{r}:{d}" for r, d in kills], "final_members": eg.members,
                 "jobs_done": all(j.done for j in coord.jobs.jobs.values()),
                 "loop_phase_s": {k: round(v, 4) for k, v in svc.phase_s.items()},
                 "comm": comm, "depth": depth, "build_s": round(build_s, 1),
@@ -168,6 +174,86 @@ def agree(rank: int) -> Tuple[str, int]:
 
 def parse_kills(specs: List[str]) -> List[Tuple[int, int]]:
     return [tuple(int(x) for x in k.split(":")) for k in specs if k]  # type: ignore[misc]
+
+
+def default_kills(world: int, total_batches: int) -> List[Tuple[int, int]]:
+    """BASELINE config 5's two worker kills, mid-job: rank 1 once a quarter of the batches
+    completed, rank world-3 at half (never the coordinator world-1, nor rank 0, whose
+    launcher parent reports the record)."""
+    return [(1, total_batches // 4), (world - 3, total_batches // 2)]
+
+
+def run_in_children(rank: int, world: int, local_rank: int, rdzv: str, swim_base: int, resnet_images: int,
+                    inception_images: int, batch_sizes: Dict[str, int], kills: Sequence[Tuple[int, int]],
+                    timeout_s: float = 900.0, backend: str = "gpu", fake_delay: float = 0.0) -> Optional[dict]:
+    """(every launcher rank) run this rank's share of a service pass WITH injected kills in
+    a child process: a killed rank ends with status 17, which a torchrun worker must not
+    (the launcher would tear the whole job down). Never an exec of this process (it holds
+    the GPU): a child interpreter, waited for. Returns the record on rank 0 (its child
+    survives: kills never target rank 0)."""
+    import subprocess
+    import sys
+
+    rec_path = f"{rdzv}_rec_{rank}.json"
+    cmd = [sys.executable, "-m", "distributed_machine_learning_amd.parallel.service_bench", "--rank", str(rank),
+           "--world", str(world), "--rdzv", rdzv, "--port", str(swim_base), "--resnet", str(resnet_images),
+           "--inception", str(inception_images), "--batch-resnet", str(batch_sizes["ResNet50"]),
+           "--batch-inception", str(batch_sizes["InceptionV3"]), "--out", rec_path,
+           "--kills", ",".join(f"{r}:{s}" for r, s in kills), "--backend", backend,
+           "--fake-delay", str(fake_delay)]
+    env = dict(os.environ, LOCAL_RANK=str(local_rank))
+    env.pop("TORCHELASTIC_RUN_ID", None)
+    rc = subprocess.run(cmd, env=env, timeout=timeout_s).returncode
+    expected = {0, 17} if any(r == rank for r, _ in kills) else {0}
+    if rc not in expected:
+        raise RuntimeError(f"service kill pass: rank {rank} child exited {rc}")
+    if rank != 0:
+        return None
+    with open(rec_path) as f:
+        rec = json.load(f)
+    os.remove(rec_path)
+    return rec
+
+
+def _child_main() -> int:
+    """The child of run_in_children (one per launcher rank)."""
+    import argparse
+
+    import torch
+
+    ap = argparse.ArgumentParser()
+    for k in ("--rank", "--world", "--port", "--resnet", "--inception", "--batch-resnet", "--batch-inception"):
+        ap.add_argument(k, type=int, required=True)
+    ap.add_argument("--rdzv", required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--kills", default="")
+    ap.add_argument("--backend", default="gpu", choices=("gpu", "fake"))
+    ap.add_argument("--fake-delay", type=float, default=0.0, help="fake backend: seconds per image")
+    a = ap.parse_args()
+    # the data group stays on gloo in this pass: the bench's images are the seeded synthetic
+    # arena (no window moves a byte), and a gloo group aborts at once on a dead peer
+    device, make_backend, data_backend = None, None, "gloo"
+    if a.backend == "gpu":
+        device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(device)
+    else:
+        from .rank_backend import FakeRankBackend
+
+        make_backend = lambda: FakeRankBackend(cap=max(a.batch_resnet, a.batch_inception),  # noqa: E731
+                                               delay_per_image=a.fake_delay)
+    rec = run(a.rank, a.world, device, a.rdzv, a.port, a.resnet, a.inception,
+              {"ResNet50": a.batch_resnet, "InceptionV3": a.batch_inception}, None,
+              kills=parse_kills(a.kills.split(",")), make_backend=make_backend, data_backend=data_backend)
+    if rec is not None:
+        tmp = a.out + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(rec, f)
+        os.replace(tmp, a.out)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(_child_main())
 
 
 def dumps(rec: dict) -> str:

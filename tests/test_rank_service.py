@@ -352,3 +352,43 @@ def test_job_three_times_the_arena_world4(tmp_path):
         be.loader = lambda ns, name=name: {name: (name * 3).encode()}
         ids, p = StoreRankBackend.classify(be._load(model, [name])[name])
         assert [e[0] for e in rows[0]] == [idx[int(c)][0] for c in ids], name
+
+
+# ---------------------------------------------- config 5: the bench's kill pass --
+def _kill_pass_rank(grank, world, rdzv, port, out, kills):
+    from distributed_machine_learning_amd.parallel import service_bench
+
+    rec = service_bench.run_in_children(grank, world, 0, rdzv, port, 2560, 1280, {"ResNet50": 16, "InceptionV3": 8},
+                                        kills, timeout_s=240, backend="fake", fake_delay=0.0005)
+    if rec is not None:
+        with open(os.path.join(out, "kill_pass.json"), "w") as f:
+            json.dump(rec, f)
+
+
+def test_service_bench_kill_pass_world8(tmp_path):
+    """bench.py's config-5 pass (service_bench.run_in_children) at world 8
+    on gloo with the fake backend: every launcher rank runs its share in a child process,
+    two children are killed mid-job (exit 17, which the parents expect), the survivors
+    rebuild twice and finish both jobs, and every batch's output is in the store exactly
+    once (one name per (job, batch); a re-run batch only adds a version)."""
+    world = 8
+    kills = [(1, 60), (5, 150)]   # rank 1 after 60 of the 320 batches, rank 5 after 150
+    ctx = mp.get_context("spawn")
+    port = _free_port() - world - 1
+    ps = [ctx.Process(target=_kill_pass_rank, args=(r, world, str(tmp_path / "rdzv"), port, str(tmp_path), kills))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert [p.exitcode for p in ps] == [0] * world
+    r = json.load(open(tmp_path / "kill_pass.json"))
+    assert r["jobs_done"] and r["rebuilds"] == 2 and r["kills"] == ["1:60", "5:150"]
+    assert r["final_members"] == [0, 2, 3, 4, 6, 7]
+    assert r["images"] == {"ResNet50": 2560, "InceptionV3": 1280}
+    nb = 2560 // 16 + 1280 // 8
+    o = r["outputs"]
+    assert o["distinct_batches_in_store"] == nb and o["in_store"] == nb and o["listing_duplicates"] == 0, o

@@ -328,3 +328,71 @@ def test_job_three_times_the_arena_gpu(tmp_path):
                                        rtol=0, atol=0), n
     finally:
         eg.close()
+
+
+def test_kill_pass_world4_on_one_gpu(tmp_path):
+    """BASELINE config 5 on the real engines: bench.py's kill pass
+    (service_bench.run_in_children) with 4 ranks sharing this GPU — each rank a child
+    process running GpuRankBackend, control over gloo + shared memory — ranks 1 and 2
+    killed mid-job (exit 17). The survivors rebuild twice, both jobs finish, and every
+    batch's output is in the store exactly once."""
+    import threading
+
+    from distributed_machine_learning_amd.parallel import service_bench
+
+    world, bs = 4, {"ResNet50": 64, "InceptionV3": 32}
+    n_r, n_i = 64 * 48, 32 * 48
+    kills = [(1, 24), (2, 48)]
+    rdzv, port = str(tmp_path / "rdzv"), 20000 + os.getpid() % 20000
+    recs, errs = {}, []
+
+    def one(r):
+        try:
+            recs[r] = service_bench.run_in_children(r, world, 0, rdzv, port, n_r, n_i, bs, kills, timeout_s=400)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append((r, e))
+    ts = [threading.Thread(target=one, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(450)
+    assert not errs, errs
+    rec = recs[0]
+    assert rec["jobs_done"] and rec["rebuilds"] == 2 and rec["final_members"] == [0, 3]
+    nb = 48 + 48
+    o = rec["outputs"]
+    assert o["distinct_batches_in_store"] == nb and o["listing_duplicates"] == 0, o
+
+
+@pytest.mark.parametrize("model", ["ResNet50", "InceptionV3"])
+def test_engine_reads_arena_through_index_table(model):
+    """the serving engines read a batch's images in place from the HBM
+    arena through a per-slot index table in pinned host memory (stem kernels' ``idx``),
+    and write their top-5 rows straight into pinned host result buffers. The rows are
+    bit-identical to the same engine configuration fed a gathered batch buffer."""
+    from distributed_machine_learning_amd.models import build_model
+    from distributed_machine_learning_amd.models.engine import SplitEngine, merge_point
+
+    g, w = build_model(model, seed=0)
+    b = 8
+    dev = torch.device("cuda")
+    gen = torch.Generator().manual_seed(5)
+    arena = torch.randint(0, 256, (40, *g.input_hw, 3), dtype=torch.uint8, generator=gen).to(dev)
+    idx = [torch.zeros(b, dtype=torch.int32).pin_memory() for _ in range(2)]
+    host = [torch.full((2, b, 5), -7, dtype=torch.int32).pin_memory() for _ in range(2)]
+    s = torch.cuda.Stream()
+    kw = dict(batch=b, device="cuda", src_slots=2, splits=2, merge_at=merge_point(model))
+    se = SplitEngine(g, w, src_tensors=[arena] * 2, src_index=idx, result_views=host, **kw)
+    ref = SplitEngine(g, w, **kw)
+    se.capture(s)
+    ref.capture(s)
+    for slot, sel in ((1, [37, 3, 3, 20, 0, 39, 11, 5]), (0, [9, 8, 7, 6, 5, 4, 3, 2])):
+        idx[slot].numpy()[:] = sel
+        with torch.cuda.stream(s):
+            se.run(s, use_graph=True, slot=slot)
+            ref.srcs[slot].copy_(arena[torch.tensor(sel, device=dev)])
+            ref.run(s, use_graph=True, slot=slot)
+        s.synchronize()
+        assert torch.equal(host[slot], ref.results[slot].cpu()), (model, slot)
+    with pytest.raises(RuntimeError, match="index table"):
+        se.infer(arena[:b])

@@ -6,7 +6,7 @@ written by the ranks), optionally with injected rank kills. The same run is the
 ``service`` sub-record of ``bench.py`` (parallel/service_bench.py).
 
   torchrun --nproc-per-node N tools/serve_bench.py --resnet-images 20480 --inception-images 10240 \\
-      [--kill 3:5 --kill 6:9]          # kill global rank 3 at step 5, rank 6 at step 9
+      [--kill 3:100 --kill 6:200]      # rank 3 dies after 100 completed batches, rank 6 after 200
   python tools/serve_bench.py ...      # N = 1
 
 Prints one JSON line (rank 0).
@@ -25,10 +25,12 @@ def main():
     ap.add_argument("--inception-images", type=int, default=10240)
     ap.add_argument("--resnet-batch", type=int, default=256)
     ap.add_argument("--inception-batch", type=int, default=128)
-    ap.add_argument("--kill", action="append", default=[], help="rank:step")
+    ap.add_argument("--kill", action="append", default=[],
+                    help="rank:batches (the rank exits 17 once that many batches completed; the pass then "
+                         "runs in child processes, service_bench.run_in_children)")
     ap.add_argument("--out-dir", default="", help="output files ('' = outputs off)")
     ap.add_argument("--comm", default="gloo", choices=("nccl", "gloo"))
-    ap.add_argument("--depth", type=int, default=4)
+    ap.add_argument("--depth", type=int, default=16)
     a = ap.parse_args()
 
     import torch
@@ -42,9 +44,14 @@ def main():
     torch.cuda.set_device(dev)
     rdzv, port = service_bench.agree(rank)
     dist.destroy_process_group()
-    rec = service_bench.run(rank, world, dev, rdzv, port, a.resnet_images, a.inception_images,
-                            {"ResNet50": a.resnet_batch, "InceptionV3": a.inception_batch}, a.out_dir or None,
-                            kills=service_bench.parse_kills(a.kill), comm=a.comm, depth=a.depth)
+    bs = {"ResNet50": a.resnet_batch, "InceptionV3": a.inception_batch}
+    kills = service_bench.parse_kills(a.kill)
+    if kills:  # a killed rank exits 17: never the launcher's worker itself
+        rec = service_bench.run_in_children(rank, world, local, rdzv, port, a.resnet_images, a.inception_images,
+                                            bs, kills)
+    else:
+        rec = service_bench.run(rank, world, dev, rdzv, port, a.resnet_images, a.inception_images, bs,
+                                a.out_dir or None, comm=a.comm, depth=a.depth)
     if rank == 0 and rec is not None:
         print(json.dumps(rec), flush=True)
 
