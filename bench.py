@@ -86,6 +86,7 @@ def parse_args(argv=None):
     ap.add_argument("--kill", action="append", default=[],
                     help="rank:batches - a kill of the config-5 pass: the rank exits once that many batches completed "
                          "(default: 2 kills, service_bench.default_kills)")
+    ap.add_argument("--kill-pass-timeout", type=float, default=300.0, help="seconds for the config-5 pass")
     ap.add_argument("--kill-pass", default="auto", choices=("auto", "on", "off"),
                     help="BASELINE config 5: a second service pass with injected rank kills, run in child "
                          "processes (a killed rank exits 17); auto = on when --gpus >= 4")
@@ -349,11 +350,16 @@ def bench_service(args, rank: int, world: int, device, recs: dict):
         nb = sum(-(-n * world // DEFAULT_BATCH[m]) for m, n in (("ResNet50", args.svc_resnet_images),
                                                                  ("InceptionV3", args.svc_inception_images)))
         kills = service_bench.parse_kills(args.kill) or service_bench.default_kills(world, nb)
-        krec = service_bench.run_in_children(rank, world, device.index or 0, rdzv_k, port_k,
-                                             args.svc_resnet_images * world, args.svc_inception_images * world,
-                                             dict(DEFAULT_BATCH), kills)
+        try:  # never fails the headline record: a kill-pass failure is reported in it
+            krec = service_bench.run_in_children(rank, world, device.index or 0, rdzv_k, port_k,
+                                                 args.svc_resnet_images * world, args.svc_inception_images * world,
+                                                 dict(DEFAULT_BATCH), kills, timeout_s=args.kill_pass_timeout)
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: rank {rank}: config-5 kill pass failed: {e}", file=sys.stderr, flush=True)
+            krec = {"error": str(e)[:500]}
         if rec is not None and krec is not None:
-            krec["metric"] = "config 5: " + krec["metric"] + ", 2 ranks killed mid-job"
+            if "metric" in krec:
+                krec["metric"] = "config 5: " + krec["metric"] + ", 2 ranks killed mid-job"
             rec["kill_pass"] = krec
     return rec
 

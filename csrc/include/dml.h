@@ -92,7 +92,7 @@ typedef struct {
   int mode;         // 0 = caffe (BGR, minus ImageNet mean), 1 = tf (x/127.5 - 1)
   int pair;         // 1: channels 4..6 hold the NEXT pixel's 3 values (pair-packed stem input)
   int lpad;         // pair mode: zero columns on the left; output width = Wo + lpad
-  const int* idx;   // optional: image n is src image idx[n] (an HBM arena slot); null: n
+  const int* idx;   // optional (device memory): image n is src image idx[n] (an arena slot); null: n
 } DmlPreprocArgs;
 
 // Fused ResNet50 stem (csrc/kernels/stem_fused.hip): uint8 image -> preprocess ->
@@ -115,7 +115,7 @@ typedef struct {
   const float* b4;    // fp32 [64]
   void* z;            // bf16 NHWC [N][Ho][Wo][ldz]
   int c4, ldw4, ldz;
-  const int* idx;     // optional: image n is src image idx[n] (an HBM arena slot); null: n
+  const int* idx;     // optional (device memory): image n is src image idx[n] (an arena slot); null: n
 } DmlStemArgs;
 
 // Fused InceptionV3 stem (csrc/kernels/stem_fused.hip): uint8 image -> preprocess ->
@@ -131,7 +131,7 @@ typedef struct {
   int ldw1, ldw2;
   int H1, W1;          // conv1 output size
   int H2, W2, ldy;     // conv2 output size / channel stride
-  const int* idx;      // optional: image n is src image idx[n] (an HBM arena slot); null: n
+  const int* idx;      // optional (device memory): image n is src image idx[n] (an arena slot); null: n
 } DmlIncStemArgs;
 
 // Fused 3x3 'same' conv (32 -> 64 ch, folded BN) + ReLU + 3x3/2 'valid' max pool
@@ -212,6 +212,7 @@ int dml_softmax_top5(const float* logits, int B, int classes, int ld, float* pro
 int dml_softmax_top5_split(float* logits, int B, int classes, int ld, int nsplit, int split_ld,
                            float* probs_out, int* top_idx, float* top_p, hipStream_t s);
 int dml_preprocess(const DmlPreprocArgs* a, hipStream_t s);
+int dml_index_fetch(const int* host, int* dev, int n, hipStream_t s);  // pinned host table -> device
 
 int dml_abi_sizes(int* out, int n);
 

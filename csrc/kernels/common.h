@@ -33,9 +33,20 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
   return base + (b >> 3);
 }
 
-// Entry n of an index table in pinned host memory that the host rewrites between
-// launches (the serving path's arena slot table): a system-scope vector load, never
-// served from a stale cache line of an earlier launch.
+// Max of 8 bf16 values that are all >= +0 (post-ReLU; the writer clears the sign bit, so no
+// -0): for non-negative IEEE values the bit patterns order like the values, so the max is
+// one packed 16-bit unsigned max per 2 channels (v_pk_max_u16) — no bf16 <-> fp32
+// conversion, exact.
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint4 max_bf16x8_nonneg(uint4 a, uint4 b) {
+  return __builtin_bit_cast(uint4, __builtin_elementwise_max(__builtin_bit_cast(u16x8, a),
+                                                             __builtin_bit_cast(u16x8, b)));
+}
+constexpr unsigned kNoSign2 = 0x7fff7fffu;  // two bf16 with the sign bits cleared (-0 -> +0)
+
+// Entry n of a table in pinned host memory that the host rewrites between launches (the
+// serving path's arena slot table, misc.hip index_fetch_kernel): a system-scope vector load,
+// never served from a stale cache line of an earlier launch.
 __device__ __forceinline__ int dml_host_index(const int* idx, int n) {
   return __hip_atomic_load(idx + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }

@@ -57,11 +57,6 @@ constexpr int FILL = (CHUNKS + NT - 1) / NT; // 6
 // fragment reads of 16 consecutive rows)
 __device__ __forceinline__ int convk_swz(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
 
-__device__ __forceinline__ float bf_at(const uint4& v, int q) {
-  const unsigned w = q < 2 ? v.x : q < 4 ? v.y : q < 6 ? v.z : v.w;
-  return bf2f((q & 1) ? (w >> 16) : (w & 0xffff));
-}
-
 __global__ __launch_bounds__(NT, 3) void conv_pool_kernel(DmlConvPoolArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   char* patch = smem;
@@ -146,7 +141,8 @@ __global__ __launch_bounds__(NT, 3) void conv_pool_kernel(DmlConvPoolArgs a) {
     const f32x4 v = acc[j];
     const float f0 = ok ? fmaxf(v[0] + bias.x, 0.f) : 0.f, f1 = ok ? fmaxf(v[1] + bias.y, 0.f) : 0.f;
     const float f2 = ok ? fmaxf(v[2] + bias.z, 0.f) : 0.f, f3 = ok ? fmaxf(v[3] + bias.w, 0.f) : 0.f;
-    *(uint2*)(tile + p * TROW + (wid * 16 + fq * 4) * 2) = make_uint2(pack2(f0, f1), pack2(f2, f3));
+    *(uint2*)(tile + p * TROW + (wid * 16 + fq * 4) * 2) =
+        make_uint2(pack2(f0, f1) & kNoSign2, pack2(f2, f3) & kNoSign2);  // +0 only: the pool maxes bits
   }
   __syncthreads();
 
@@ -161,16 +157,12 @@ __global__ __launch_bounds__(NT, 3) void conv_pool_kernel(DmlConvPoolArgs a) {
     const int ly = pr / (PB / 2), lx = pr - ly * (PB / 2) + half * (PB / 2);
     const int oy = py0 + ly, ox = px0 + lx;
     if (oy >= a.Ho || ox >= a.Wo) continue;
-    float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    uint4 pv = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const uint4 v = *(const uint4*)(tile + ((2 * ly + dy) * CW + 2 * lx + dx) * TROW + cg * 16);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], bf_at(v, q));
-      }
-    const uint4 pv = make_uint4(pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7]));
+      for (int dx = 0; dx < 3; ++dx)
+        pv = max_bf16x8_nonneg(pv, *(const uint4*)(tile + ((2 * ly + dy) * CW + 2 * lx + dx) * TROW + cg * 16));
     if (a.c4 > 0)
       *(uint4*)(smem + POOLT + convk_swz(ly * PB + lx, cg)) = pv;
     else

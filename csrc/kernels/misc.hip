@@ -315,7 +315,7 @@ __device__ __forceinline__ void preprocess_pixel(const DmlPreprocArgs& a, const 
   int iy = (int)(((float)oh + 0.5f) * sy), ix = (int)(((float)ow + 0.5f) * sx);
   iy = min(iy, a.Hs - 1);
   ix = min(ix, a.Ws - 1);
-  const long img_n = a.idx ? (long)dml_host_index(a.idx, n) : (long)n;  // an HBM arena slot (serving path) or n
+  const long img_n = a.idx ? (long)a.idx[n] : (long)n;  // an HBM arena slot (serving path) or n
   const unsigned char* px = src + ((img_n * a.Hs + iy) * a.Ws + ix) * 3;
   const float r = px[0], g = px[1], b = px[2];
   if (a.mode == 0) {  // caffe: RGB->BGR, subtract BGR mean, no scaling
@@ -346,7 +346,22 @@ __global__ __launch_bounds__(256) void preprocess_kernel(DmlPreprocArgs a) {
   }
 }
 
+// dev[i] = host[i], i < n: the serving path's per-launch arena slot table, fetched from pinned
+// host memory once per batch (system-scope loads) so that the stem kernels' workgroups read
+// it from device memory (a host read per workgroup made the ResNet50 stem 3.8x slower:
+// profiles/r4_service/stem_bench.log)
+__global__ __launch_bounds__(1024) void index_fetch_kernel(const int* __restrict__ host, int* __restrict__ dev, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dev[i] = dml_host_index(host, i);
+}
+
 }  // namespace dml
+
+extern "C" int dml_index_fetch(const int* host, int* dev, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(dml::index_fetch_kernel, dim3(1), dim3(n < 1024 ? ((n + 63) / 64) * 64 : 1024), 0, s, host, dev, n);
+  DML_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int dml_pool(const DmlPoolArgs* a, hipStream_t s) {
   static const bool generic = getenv("DML_POOL_GENERIC") != nullptr;  // A/B switch: the per-tap kernel

@@ -34,6 +34,10 @@
 #include "common.h"
 #include "dml.h"
 
+#ifndef DML_STEM_PROBE
+#define DML_STEM_PROBE 0  // A/B timing probes only (tools/build_variant.py): 1 = no source loads, 2 = no MFMA
+#endif
+
 namespace dml {
 namespace stem {
 
@@ -53,11 +57,6 @@ constexpr int FILL = (IR * PQ + NT - 1) / NT;  // patch chunks per thread (3)
 // pooled tile rows of 128 B (64 bf16), 16-B chunk ^= row & 7 (conflict-free fragment reads)
 __device__ __forceinline__ int pswz(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
 static_assert(PH * PW <= 64 && 64 * 128 <= PATCH_BYTES, "pooled tile: 4 fragments in the patch region");
-
-__device__ __forceinline__ float bf_at(const uint4& v, int q) {
-  const unsigned w = q < 2 ? v.x : q < 4 ? v.y : q < 6 ? v.z : v.w;
-  return bf2f((q & 1) ? (w >> 16) : (w & 0xffff));
-}
 
 __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[PATCH_BYTES + TILE_BYTES];
@@ -96,8 +95,8 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
   {
     const float sy = (float)a.Hs / (float)a.H, sx = (float)a.Ws / (float)a.W;
     // the serving path reads the image straight from its HBM arena slot (a.idx: the batch's
-    // slot table, pinned host memory written before the launch) - no gather copy in between
-    const long img_n = a.idx ? (long)dml_host_index(a.idx, n) : (long)n;
+    // slot table in device memory, dml_index_fetch) - no gather copy in between
+    const long img_n = a.idx ? (long)a.idx[n] : (long)n;
     const unsigned char* img = (const unsigned char*)a.src + img_n * a.Hs * a.Ws * 3;
     unsigned char px[FILL][2][3];
     unsigned okm[FILL];
@@ -113,9 +112,15 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
       for (int h = 0; h < 2; ++h) {
         const int ix = min((int)(((float)min(max(iw + h, 0), a.W - 1) + 0.5f) * sx), a.Ws - 1);
         const unsigned char* p = img + ((long)iy * a.Ws + ix) * 3;
+#if DML_STEM_PROBE == 1
+        px[it][h][0] = (unsigned char)(ix + iy);
+        px[it][h][1] = (unsigned char)ix;
+        px[it][h][2] = (unsigned char)(p - img);
+#else
         px[it][h][0] = p[0];
         px[it][h][1] = p[1];
         px[it][h][2] = p[2];
+#endif
       }
     }
 #pragma unroll
@@ -169,7 +174,8 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          acc[i][jh + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[r][i], pf[j], acc[i][jh + j], 0, 0, 0);
+          acc[i][jh + j] = DML_STEM_PROBE == 2 ? acc[i][jh + j] + (f32x4)(pf[j][0] + wf[r][i][0])
+                                               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[r][i], pf[j], acc[i][jh + j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -187,7 +193,8 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
       const float4 b = bias[i];
       const float f0 = ok ? fmaxf(v[0] + b.x, 0.f) : 0.f, f1 = ok ? fmaxf(v[1] + b.y, 0.f) : 0.f;
       const float f2 = ok ? fmaxf(v[2] + b.z, 0.f) : 0.f, f3 = ok ? fmaxf(v[3] + b.w, 0.f) : 0.f;
-      *(uint2*)(tile + p * SROW + (wc * 32 + i * 16 + fq * 4) * 2) = make_uint2(pack2(f0, f1), pack2(f2, f3));
+      *(uint2*)(tile + p * SROW + (wc * 32 + i * 16 + fq * 4) * 2) =
+          make_uint2(pack2(f0, f1) & kNoSign2, pack2(f2, f3) & kNoSign2);  // +0 only: the pool maxes bits
     }
   }
   __syncthreads();
@@ -200,16 +207,12 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
     const int ly = pr / (PW / 2), lx = pr - ly * (PW / 2) + half * (PW / 2);
     const int oy = py0 + ly, ox = px0 + lx;
     if (oy >= a.Ho || ox >= a.Wo) continue;
-    float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    uint4 pv = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const uint4 v = *(const uint4*)(tile + ((2 * ly + dy) * CC + 2 * lx + dx) * SROW + cg * 16);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], bf_at(v, q));
-      }
-    const uint4 pv = make_uint4(pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7]));
+      for (int dx = 0; dx < 3; ++dx)
+        pv = max_bf16x8_nonneg(pv, *(const uint4*)(tile + ((2 * ly + dy) * CC + 2 * lx + dx) * SROW + cg * 16));
     *(uint4*)((unsigned short*)a.y + ((long)(n * a.Ho + oy) * a.Wo + ox) * a.ldy + cg * 8) = pv;
     if (a.c4 > 0) *(uint4*)(patch + pswz(ly * PW + lx, cg)) = pv;  // the patch is dead since step 3
   }
@@ -326,8 +329,8 @@ __global__ __launch_bounds__(NT, 3) void inc_stem_kernel(DmlIncStemArgs a) {
   {
     const float sy = (float)a.Hs / (float)a.H, sx = (float)a.Ws / (float)a.W;
     // the serving path reads the image straight from its HBM arena slot (a.idx: the batch's
-    // slot table, pinned host memory written before the launch) - no gather copy in between
-    const long img_n = a.idx ? (long)dml_host_index(a.idx, n) : (long)n;
+    // slot table in device memory, dml_index_fetch) - no gather copy in between
+    const long img_n = a.idx ? (long)a.idx[n] : (long)n;
     const unsigned char* img = (const unsigned char*)a.src + img_n * a.Hs * a.Ws * 3;
     unsigned char px[FILL][2][3];
     unsigned okm[FILL];
@@ -343,9 +346,15 @@ __global__ __launch_bounds__(NT, 3) void inc_stem_kernel(DmlIncStemArgs a) {
       for (int h = 0; h < 2; ++h) {
         const int ix = min((int)(((float)min(max(iw + h, 0), a.W - 1) + 0.5f) * sx), a.Ws - 1);
         const unsigned char* p = img + ((long)iy * a.Ws + ix) * 3;
+#if DML_STEM_PROBE == 1
+        px[it][h][0] = (unsigned char)(ix + iy);
+        px[it][h][1] = (unsigned char)ix;
+        px[it][h][2] = (unsigned char)(p - img);
+#else
         px[it][h][0] = p[0];
         px[it][h][1] = p[1];
         px[it][h][2] = p[2];
+#endif
       }
     }
 #pragma unroll

@@ -67,11 +67,11 @@ class Engine:
         """``share``: reuse another engine's (optimized) graph and resident weights
         (sub-batch engines of a SplitEngine); ``src_tensors`` / ``result_views``:
         external uint8 source slots / per-slot [2, batch, 5] result rows to use
-        instead of allocating them. ``src_index``: per slot, an int32 [batch] table
-        (pinned host memory, rewritten by the caller before each run): image n of the
-        batch is image src_index[slot][n] of that slot's source tensor — the serving
-        path's HBM arena, read in place by the stem kernel instead of gathered into a
-        batch buffer first. ``fuse_stem=False`` (or DML_FUSED_STEM=0) keeps the
+        instead of allocating them. ``src_index``: per slot, an int32 [batch] table in
+        device memory (rewritten by the caller before each run, in stream order): image n
+        of the batch is image src_index[slot][n] of that slot's source tensor — the
+        serving path's HBM arena, read in place by the stem kernel instead of gathered
+        into a batch buffer first. ``fuse_stem=False`` (or DML_FUSED_STEM=0) keeps the
         ResNet stem as three launches (preprocess, conv, pool); ``fuse_blocks=False``
         (or DML_FUSED_BLOCKS=0) keeps every bottleneck 1x1 conv its own launch;
         ``conv_groups=False`` (or DML_CONV_GROUPS=0) launches InceptionV3's

@@ -328,6 +328,14 @@ class ReplicatedCoordinator:
         return out
 
 
+def auto_depth(world: int) -> int:
+    """Batches in flight per rank (launched, queued, or awaiting their output PUT): 4 on one
+    GPU (measured r4, 1 x MI355X, outputs PUT, tools/gpu_svc_depth.sh: depth 4 / 8 -> 71.6k /
+    71.1k images/s at p50 10.9 / 21.9 ms for ResNet50), 8 with peers (a PUT then replicates
+    over TCP to other ranks, so more batches wait on it)."""
+    return 4 if world <= 1 else 8
+
+
 # ---------------------------------------------------------- output writer ----
 class OutputWriter:
     """This rank's result files, off the serve loop: a thread renders each

@@ -24,7 +24,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images: int, inception_images: int,
         batch_sizes: Dict[str, int], out_dir: Optional[str], kills: Sequence[Tuple[int, int]] = (),
-        comm: str = "gloo", depth: int = 16, single_rates: Optional[Dict[str, float]] = None,
+        comm: str = "gloo", depth: int = 0, single_rates: Optional[Dict[str, float]] = None,
         make_backend=None, data_backend: str = "nccl") -> Optional[dict]:
     """One rank of the service run; returns the record (on every surviving rank)."""
     import torch
@@ -52,6 +52,9 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
     for r, d in kills:
         if r == rank:
             kr, kd = r, d
+    from .service import auto_depth
+
+    depth = depth or auto_depth(world)
     coord = ReplicatedCoordinator(batch_sizes, cap=cap, host_tag="mi355x", depth=depth)
     writer = OutputWriter(os.path.join(out_dir, f"rank{rank}") if out_dir else None,
                           put_many_async=ctl.store_put_many_async, host_tag="mi355x")

@@ -57,8 +57,9 @@ def add_args(ap: argparse.ArgumentParser) -> None:
     g.add_argument("--batch-resnet", type=int, default=256)
     g.add_argument("--batch-inception", type=int, default=128)
     g.add_argument("--comm", default="gloo", choices=("gloo", "nccl"), help="backend of the control collective")
-    g.add_argument("--depth", type=int, default=16,
-                   help="batches in flight per rank: 2 on the GPU, the rest queued or awaiting their output PUT")
+    g.add_argument("--depth", type=int, default=0,
+                   help="batches in flight per rank: 2 on the GPU, the rest queued or awaiting their output PUT "
+                        "(0: service.auto_depth: 4 on one GPU, 8 with peers)")
     g.add_argument("--replication", type=int, default=4)
     g.add_argument("--arena-images", type=int, default=0,
                    help="HBM image store capacity per model (0: 2 x ranks x depth x batch, at least 8192)")
@@ -147,8 +148,11 @@ def rank_main(a: argparse.Namespace) -> int:
         (holder["eg"].joiners if "eg" in holder else early_alive).add(g)
     ctl = RankControl(grank, world, a.base_port, store_dir=store_dir, replication=min(a.replication, world),
                       rejoin=a.rejoin, on_dead=on_dead, on_alive=on_alive)
+    from ..parallel.service import auto_depth
+
+    depth = a.depth or auto_depth(world)
     # the image windows stage world x depth batches ahead of dispatch: room for twice that
-    arena = a.arena_images or max(8192, 2 * world * a.depth * cap)
+    arena = a.arena_images or max(8192, 2 * world * depth * cap)
     backend = {
         "gpu": lambda: GpuRankBackend(dev, bs, cap=cap, arena_images=arena, loader=ctl.store_loader),
         "fake": lambda: FakeRankBackend(cap=cap, loader=ctl.store_loader),
@@ -163,7 +167,7 @@ def rank_main(a: argparse.Namespace) -> int:
     eg.dead |= early_dead
     eg.joiners |= {g for g in early_alive if g not in eg.members}
     holder["eg"] = eg
-    coord = ReplicatedCoordinator(bs, cap=cap, host_tag="mi355x", depth=a.depth, preempt=not a.no_preempt)
+    coord = ReplicatedCoordinator(bs, cap=cap, host_tag="mi355x", depth=depth, preempt=not a.no_preempt)
     writer = OutputWriter(a.out_dir or None, put_many_async=ctl.store_put_many_async, host_tag="mi355x")
     svc = CollectiveService(eg, backend, coord, control=ctl, writer=writer, on_device=(a.comm == "nccl"),
                             watchdog_s=0.0, rejoined=a.rejoin)

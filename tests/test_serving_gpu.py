@@ -367,9 +367,11 @@ def test_kill_pass_world4_on_one_gpu(tmp_path):
 @pytest.mark.parametrize("model", ["ResNet50", "InceptionV3"])
 def test_engine_reads_arena_through_index_table(model):
     """the serving engines read a batch's images in place from the HBM
-    arena through a per-slot index table in pinned host memory (stem kernels' ``idx``),
-    and write their top-5 rows straight into pinned host result buffers. The rows are
-    bit-identical to the same engine configuration fed a gathered batch buffer."""
+    arena through a per-slot device index table (stem kernels' ``idx``, filled from pinned
+    host memory by dml_index_fetch), and write their top-5 rows straight into pinned host
+    result buffers. The rows are bit-identical to the same engine configuration fed a
+    gathered batch buffer."""
+    from distributed_machine_learning_amd import _native as N
     from distributed_machine_learning_amd.models import build_model
     from distributed_machine_learning_amd.models.engine import SplitEngine, merge_point
 
@@ -378,7 +380,8 @@ def test_engine_reads_arena_through_index_table(model):
     dev = torch.device("cuda")
     gen = torch.Generator().manual_seed(5)
     arena = torch.randint(0, 256, (40, *g.input_hw, 3), dtype=torch.uint8, generator=gen).to(dev)
-    idx = [torch.zeros(b, dtype=torch.int32).pin_memory() for _ in range(2)]
+    hidx = [torch.zeros(b, dtype=torch.int32).pin_memory() for _ in range(2)]
+    idx = [torch.zeros(b, dtype=torch.int32, device=dev) for _ in range(2)]
     host = [torch.full((2, b, 5), -7, dtype=torch.int32).pin_memory() for _ in range(2)]
     s = torch.cuda.Stream()
     kw = dict(batch=b, device="cuda", src_slots=2, splits=2, merge_at=merge_point(model))
@@ -387,8 +390,10 @@ def test_engine_reads_arena_through_index_table(model):
     se.capture(s)
     ref.capture(s)
     for slot, sel in ((1, [37, 3, 3, 20, 0, 39, 11, 5]), (0, [9, 8, 7, 6, 5, 4, 3, 2])):
-        idx[slot].numpy()[:] = sel
+        hidx[slot].numpy()[:] = sel
         with torch.cuda.stream(s):
+            N.check(N.lib().dml_index_fetch(hidx[slot].data_ptr(), idx[slot].data_ptr(), b, s.cuda_stream),
+                    "index fetch")
             se.run(s, use_graph=True, slot=slot)
             ref.srcs[slot].copy_(arena[torch.tensor(sel, device=dev)])
             ref.run(s, use_graph=True, slot=slot)

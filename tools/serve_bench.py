@@ -30,7 +30,7 @@ def main():
                          "runs in child processes, service_bench.run_in_children)")
     ap.add_argument("--out-dir", default="", help="output files ('' = outputs off)")
     ap.add_argument("--comm", default="gloo", choices=("nccl", "gloo"))
-    ap.add_argument("--depth", type=int, default=16)
+    ap.add_argument("--depth", type=int, default=0, help="0: service.auto_depth")
     a = ap.parse_args()
 
     import torch
