@@ -349,12 +349,16 @@ class ElasticGroup:
         return won
 
     def grow(self, members: List[int]) -> List[int]:
-        """Every current member: move to epoch e+1 over ``members`` (no abort:
-        no collective is pending at a step boundary). The list is the one in
-        the store, so every member and the joiners agree on it."""
+        """Every current member: move to epoch e+1 over ``members``. The list is the one
+        in the store, so every member and the joiners agree on it. The old groups are
+        aborted, not destroyed: no control collective is pending at a step boundary, but an
+        image window's data-group all-gather may be — issued here, not yet by a peer whose
+        decode was still running, and dropped by every rank at this boundary (measured: a
+        destroy waited out the 30 s gloo timeout behind it while the others' init of the
+        new epoch timed out)."""
         nxt = self.epoch + 1
         won = json.loads(self.store.compare_set(f"members{nxt}", "", json.dumps(sorted(members))))
-        self._teardown(abort=False)
+        self._teardown(abort=True)
         if self.grank not in won:
             raise CollectiveFailure("this rank was removed from the group")
         self.prev_members, self.members = self.members, won

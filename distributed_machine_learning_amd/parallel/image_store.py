@@ -270,11 +270,16 @@ class Stager:
     def __init__(self):
         self.queue: Deque[Window] = deque()
         self.ctx = (0, 1, None, None, None)
+        self.poll_dead: Callable[[], None] = lambda: None
 
-    def attach(self, rank: int, world: int, pool, gather_async: Callable, stream=None) -> None:
+    def attach(self, rank: int, world: int, pool, gather_async: Callable, stream=None,
+               poll_dead: Optional[Callable[[], None]] = None) -> None:
         """The group the windows replicate over (every epoch): group rank / size, the decode
-        pool, the async all-gather, the staging stream."""
+        pool, the async all-gather, the staging stream; ``poll_dead`` raises CollectiveFailure
+        once a member is confirmed dead (a blocking flush polls it: a collective with a dead
+        peer never completes on RCCL, and a hung peer keeps gloo's sockets open)."""
         self.ctx = (rank, world, pool, gather_async, stream)
+        self.poll_dead = poll_dead or (lambda: None)
 
     def flush_until(self, target: Window) -> None:
         """Block until ``target`` (and every window before it) is resident here."""
@@ -284,12 +289,14 @@ class Stager:
             w = self.queue[0]
             if w.future is not None and not w.future.done():
                 w.future.result()
-            if w.work is not None and w.event is None and w.store.device.type != "cuda":
-                for wk in w.work:
-                    wk.wait()
-            if w.event is not None and not isinstance(w.event, bool):
-                w.event.synchronize()
+            # the window's collective / scatter: polled, never a blocking wait (a dead peer)
+            while ((w.work is not None and w.event is None and w.store.device.type != "cuda"
+                    and not all(wk.is_completed() for wk in w.work)) or
+                   (w.event is not None and not isinstance(w.event, bool) and not w.event.query())):
+                self.poll_dead()
+                time.sleep(0.0002)
             if not self.progress():
+                self.poll_dead()
                 time.sleep(0.0005)
 
     def progress(self) -> int:

@@ -116,7 +116,7 @@ class _ArenaStaging:
     def attach(self, eg) -> None:
         self.epoch = eg.epoch
         self.stager.attach(eg.rank, eg.world, self.pool, eg.all_gather_data_async,
-                           getattr(self, "stage_stream", None))
+                           getattr(self, "stage_stream", None), poll_dead=eg._poll_dead)
 
     def stage(self, model, batches) -> bool:
         arena = self.arenas[model]

@@ -137,7 +137,7 @@ def test_launcher_cli_roundtrip_and_version_pinning(tmp_path):
 
 
 # ------------------------------------------------------------------ rejoin --
-def _rejoin_rank(grank, world, rdzv, swim, out, kill_step, rejoin):
+def _rejoin_rank(grank, world, rdzv, swim, out, kill_step, rejoin, victim=1):
     import logging
 
     logging.basicConfig(level=logging.WARNING)
@@ -156,11 +156,11 @@ def _rejoin_rank(grank, world, rdzv, swim, out, kill_step, rejoin):
         loads.extend(names)
         return {n: (n * 7).encode() for n in names}
     be = StoreRankBackend(loader=loader, cap=8, delay_per_image=0.004, arena_images=4096)
-    eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=30, join=rejoin)
+    eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=30, join=rejoin, shm_exchange=True)
     box["eg"] = eg
     coord = ReplicatedCoordinator({"ResNet50": 8, "InceptionV3": 8}, cap=8, depth=3)
     writer = OutputWriter(os.path.join(out, "outputs"), host_tag="t")
-    svc = CollectiveService(eg, be, coord, writer=writer, kill_rank=1 if not rejoin else -1,
+    svc = CollectiveService(eg, be, coord, writer=writer, kill_rank=victim if not rejoin else -1,
                             kill_at_step=kill_step, rejoined=rejoin)
     if svc.is_coordinator() and not rejoin:
         svc.submit_local("ResNet50", images=[f"r{i}.jpeg" for i in range(1600)])
@@ -178,32 +178,39 @@ def _rejoin_rank(grank, world, rdzv, swim, out, kill_step, rejoin):
     eg.close()
 
 
-def test_rank_rejoin_after_kill(tmp_path):
+@pytest.mark.parametrize("victim", [1, 3])
+def test_rank_rejoin_after_kill(tmp_path, victim):
+    """A rank killed mid-job and restarted with --rejoin is admitted into a new epoch,
+    serves batches again, and every job completes with every output. victim = 3 is the
+    highest rank, i.e. the coordinator: it comes back with an empty
+    replica and must stay out of the coordinator role until the survivors' new
+    coordinator (rank 2) has sent it the job state."""
     world = 4
     rdzv, swim = str(tmp_path / "rdzv"), _free_port() - world - 1
     ctx = mp.get_context("spawn")
-    args = lambda r, rejoin: (r, world, rdzv, swim, str(tmp_path), 3, rejoin)  # noqa: E731
+    args = lambda r, rejoin: (r, world, rdzv, swim, str(tmp_path), 3, rejoin, victim)  # noqa: E731
     ps = [ctx.Process(target=_rejoin_rank, args=args(r, False)) for r in range(world)]
     for p in ps:
         p.start()
-    ps[1].join(120)
-    assert ps[1].exitcode == 17       # the injected kill
-    time.sleep(1.5)                   # survivors detect it and rebuild without it
-    back = ctx.Process(target=_rejoin_rank, args=args(1, True))
+    ps[victim].join(120)
+    assert ps[victim].exitcode == 17       # the injected kill
+    time.sleep(1.5)                        # survivors detect it and rebuild without it
+    back = ctx.Process(target=_rejoin_rank, args=args(victim, True))
     back.start()
-    for p in ps[:1] + ps[2:] + [back]:
+    rest = [p for r, p in enumerate(ps) if r != victim] + [back]
+    for p in rest:
         p.join(240)
-    codes = [p.exitcode for p in ps[:1] + ps[2:] + [back]]
+    codes = [p.exitcode for p in rest]
     for p in ps + [back]:
         if p.is_alive():
             p.kill()
     assert codes == [0, 0, 0, 0], codes
-    r3 = json.load(open(tmp_path / "rejoin_3_0.json"))
-    r1 = json.load(open(tmp_path / "rejoin_1_1.json"))
-    assert r3["done"] == [True, True]
-    assert r3["rebuilds"] >= 1 and r3["grows"] >= 1 and r3["members"] == [0, 1, 2, 3]
-    assert r1["served_here"] > 0                   # the restarted rank served batches again
-    assert r1["replicated"] > 0                    # windows staged over the new group reached it
+    r0 = json.load(open(tmp_path / "rejoin_0_0.json"))
+    rv = json.load(open(tmp_path / f"rejoin_{victim}_1.json"))
+    assert r0["done"] == [True, True] and rv["done"] == [True, True]
+    assert r0["rebuilds"] >= 1 and r0["grows"] >= 1 and r0["members"] == [0, 1, 2, 3]
+    assert rv["served_here"] > 0                   # the restarted rank served batches again
+    assert rv["replicated"] > 0                    # windows staged over the new group reached it
     files = set(os.listdir(tmp_path / "outputs"))
     keys = {tuple(f.split("_")[1:3]) for f in files}
     assert keys == {(str(j), str(b)) for j in (31, 32) for b in range(1, 201)}
