@@ -35,7 +35,8 @@
 #include "dml.h"
 
 #ifndef DML_STEM_PROBE
-#define DML_STEM_PROBE 0  // A/B timing probes only (tools/build_variant.py): 1 = no source loads, 2 = no MFMA
+#define DML_STEM_PROBE 0  // A/B timing probes only (tools/build_variant.py): 1 = no source loads, 2 = no MFMA,
+                          // 3 = ResNet stem without pool / folded 1x1
 #endif
 
 namespace dml {
@@ -199,6 +200,9 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
   }
   __syncthreads();
 
+#if DML_STEM_PROBE == 3
+  if (a.N > 0) return;  // probe: conv only (no pool, no folded 1x1)
+#endif
   // 4. max pool 3x3/2 over the tile: item = (pool pixel, 8-channel group)
   for (int t = tid; t < PH * PW * 8; t += NT) {
     // lanes 0-7 / 8-15 of a lane group read pool pixels lx and lx + 4: conv pixels

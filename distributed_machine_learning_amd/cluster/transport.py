@@ -256,6 +256,8 @@ class Endpoint:
             try:
                 return await asyncio.wait_for(fut, timeout)
             except asyncio.TimeoutError:
+                pass
+            finally:  # timed out, answered or cancelled by the caller: never leave the entry behind
                 self.pending.pop(seq, None)
         return None
 

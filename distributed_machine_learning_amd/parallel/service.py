@@ -515,6 +515,11 @@ class CollectiveService:
         # kill_at_step, or once kill_at_done batches have completed (replicated count)
         self.kill_rank, self.kill_at_step, self.kill_at_done = kill_rank, kill_at_step, kill_at_done
         self.completed = 0
+        # recovery timing: from the last step completed before a failure (a killed rank dies
+        # right after its last step) to the first step after the rebuild that dispatched work
+        self.last_ok_t = time.monotonic()
+        self._recovering_since: Optional[float] = None
+        self.recoveries_s: List[float] = []
         self.dev = backend.device if on_device else torch.device("cpu")
         self.steps = 0
         self.rebuilds = 0
@@ -765,6 +770,11 @@ class CollectiveService:
         if mine is None:  # STOP (sent only when nothing is queued or in flight)
             return False
         self.batches_per_step_max = max(self.batches_per_step_max, moved)
+        now = time.monotonic()
+        if self._recovering_since is not None and moved:
+            self.recoveries_s.append(now - self._recovering_since)
+            self._recovering_since = None
+        self.last_ok_t = now
         self.completed += len(finished)
         if eg.grank == self.kill_rank and (self.steps == self.kill_at_step or
                                            0 <= self.kill_at_done <= self.completed):
@@ -855,6 +865,8 @@ class CollectiveService:
     def _recover(self, e: Exception) -> None:
         eg = self.eg
         log.warning("rank %d: collective failed (%s); rebuilding", eg.grank, e)
+        if self._recovering_since is None:
+            self._recovering_since = self.last_ok_t
         was = self.coordinator_rank()
         self._reset_local()
         for attempt in range(5):

@@ -124,6 +124,7 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                             "writer_busy_s_coordinator": round(writer.busy_s, 3)},
                 "steps": steps, "max_batches_per_step": svc.batches_per_step_max,
                 "rebuilds": svc.rebuilds, "preempted_batches": coord.preempted, "requeued_batches": coord.requeued,
+                "kill_to_redispatch_s": [round(x, 3) for x in svc.recoveries_s],
                 "kills": [f"{r}:{d}" for r, d in kills], "final_members": eg.members,
                 "jobs_done": all(j.done for j in coord.jobs.jobs.values()),
                 "loop_phase_s": {k: round(v, 4) for k, v in svc.phase_s.items()},

@@ -218,6 +218,20 @@ class StoreService:
             return SUCCESS
         return FAILED
 
+    async def _request_unless_dead(self, t: str, mtype, payload: dict, poll_s: float = 0.05):
+        """A request to replica ``t`` that gives up as soon as the membership confirms ``t``
+        dead (None, as on a timeout) instead of waiting out the request timeout: a bundle
+        PUT in flight when a rank dies is re-placed right after the failure detector's
+        verdict, not ``timeout`` seconds later (measured: a 2-kill config-5 pass spent ~10 s
+        of its 12 with batches waiting for PUTs to dead replicas)."""
+        req = asyncio.ensure_future(self.ep.request(t, mtype, payload, timeout=self.timeout))
+        while not req.done():
+            if not self.ml.is_alive(t):
+                req.cancel()
+                return None
+            await asyncio.wait({req}, timeout=poll_s)
+        return req.result()
+
     async def _l_put_many(self, fr: Frame) -> None:
         """Leader side of put_many: per-file placement and versions as a single PUT,
         but one DOWNLOAD_MANY per replica node for all of its files; a replica that
@@ -246,9 +260,8 @@ class StoreService:
                 for t in ts:
                     per_node.setdefault(t, []).append(n)
             nodes = sorted(per_node)
-            rs = await asyncio.gather(*(self.ep.request(
-                t, MsgType.DOWNLOAD_MANY, {"files": [[n, versions[n]] for n in per_node[t]], **src},
-                timeout=self.timeout) for t in nodes))
+            rs = await asyncio.gather(*(self._request_unless_dead(
+                t, MsgType.DOWNLOAD_MANY, {"files": [[n, versions[n]] for n in per_node[t]], **src}) for t in nodes))
             pending = {}
             for t, r in zip(nodes, rs):
                 got = r.payload.get("ok", {}) if r is not None else {}

@@ -21,7 +21,7 @@ from distributed_machine_learning_amd.serving.node import Node, NodeConfig
 
 REF_FILES = "/root/reference/testfiles"
 REF_OUT = "/root/reference/download/output_1_127.json"
-N_IMAGES = 12
+N_IMAGES = 100  # every reference testfile, batch size 1
 
 
 def _free_port():
@@ -93,8 +93,19 @@ def test_rank_launcher_cpu_backend_config1(tmp_path):
         log = open(tmp_path / "rank.log").read()
     assert "finished" in out["wait"], (out, log[-3000:])
     assert json.loads(out["c1"].split("\n[")[0])["ResNet50"]["query_count"] == N_IMAGES
-    final = json.load(open(tmp_path / "download" / f"final_{job}.json"))
+    text = open(tmp_path / "download" / f"final_{job}.json").read()
+    final = json.loads(text)
     assert len(final) == N_IMAGES
+    assert text == json.dumps(final, indent=4)          # the reference's indent-4 layout
+    # the per-batch files the rank PUT into its store: reference-formatted, one per batch
+    import glob
+
+    stored = [f for f in glob.glob(str(tmp_path / "sdfs" / "**" / f"output_{job}_*"), recursive=True)]
+    assert stored
+    from distributed_machine_learning_amd.serving.output import dumps
+
+    one = open(stored[0]).read()
+    assert one == dumps(json.loads(one))
     ref = _ref_format()
     rv = next(iter(ref.values()))
     for name, v in final.items():

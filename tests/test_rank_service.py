@@ -394,6 +394,7 @@ def test_service_bench_kill_pass_world8(tmp_path):
     assert [p.exitcode for p in ps] == [0] * world
     r = json.load(open(tmp_path / "kill_pass.json"))
     assert r["jobs_done"] and r["rebuilds"] == 2 and r["kills"] == ["1:60", "5:150"]
+    assert len(r["kill_to_redispatch_s"]) == 2 and all(0 < x < 60 for x in r["kill_to_redispatch_s"])
     assert r["final_members"] == [0, 2, 3, 4, 6, 7]
     assert r["images"] == {"ResNet50": 2560, "InceptionV3": 1280}
     nb = 2560 // 16 + 1280 // 8

@@ -36,6 +36,9 @@ def cases():
                     112, 112, 56, 56, 64)
     sa.w4, sa.b4, sa.z, sa.c4, sa.ldw4, sa.ldz = w4.data_ptr(), b4.data_ptr(), z.data_ptr(), 64, 64, 64
     out.append(("resnet_stem_b128", "dml_stem_resnet", sa, (img, w, b, y, z, w4, b4)))
+    sn = N.StemArgs(img.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), B, 224, 224, 224, 224, 0, 224,
+                    112, 112, 56, 56, 64)
+    out.append(("resnet_stem_no1x1", "dml_stem_resnet", sn, (img, w, b, y)))
     # the serving form: images read from a 4x larger arena through an index table, the table
     # in pinned host memory (GpuRankBackend) or in device memory
     arena = torch.randint(0, 256, (4 * B, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
