@@ -29,15 +29,6 @@
 #include "conv_shared.h"
 #include "pool_shared.h"
 
-#ifndef DML_V2_WREG
-#define DML_V2_WREG 0  // A/B probe (tools/build_variant.py): weights staged through VGPRs
-                       // (global_load_dwordx4 + ds_write_b128) instead of LDS-DMA
-#endif
-#ifndef DML_V2_XREG
-#define DML_V2_XREG 0  // A/B probe: activations too (buffer_load_dwordx4 + ds_write_b128; needs WREG)
-#endif
-static_assert(!DML_V2_XREG || DML_V2_WREG, "DML_V2_XREG needs DML_V2_WREG");
-
 namespace dml {
 namespace v2 {
 
@@ -177,47 +168,24 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
       (const char*)a.w + ((long)(c0 + wid * T::WI * RW::RP + lrow) * a.Kpad + (long)kbeg * T::BK + lchunk * 8) * 2;
   const long wstep_row = (long)RW::RP * a.Kpad * 2;  // next RP-row piece
 
-  uint4 wst[DML_V2_WREG ? T::WI : 1];  // register-staged weight pieces of the tile in flight
-  uint4 xst[DML_V2_XREG ? T::XI : 1];  // register-staged activation pieces
   auto issue = [&](int kt, int stage) {
     char* sx = smem + stage * T::STAGE_BYTES;
     char* sw = sx + BM * T::ROWB;
-    if constexpr (DML_V2_WREG) {  // weights first: a counted vmcnt(XI) then retires them alone
-#pragma unroll
-      for (int j = 0; j < T::WI; ++j) wst[j] = *(const uint4*)(wbase + j * wstep_row + (long)kt * T::BK * 2);
-    }
 #pragma unroll
     for (int j = 0; j < T::XI; ++j) {
       const int ih = ih0[j] + dih, iw = iw0[j] + diw;
       const unsigned ok = ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
       const unsigned msk = 0u - ok;  // branch-free select (no exec-mask split around the DMA)
       const unsigned off = ((unsigned)((base[j] + koff) * 2) & msk) | (OOB & ~msk);
-      if constexpr (DML_V2_XREG)
-        xst[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 0);
     }
-    if constexpr (!DML_V2_WREG) {
 #pragma unroll
-      for (int j = 0; j < T::WI; ++j) {
-        const char* src = wbase + j * wstep_row + (long)kt * T::BK * 2;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sw + (wid * T::WI + j) * 1024), 16, 0, 0);
-      }
+    for (int j = 0; j < T::WI; ++j) {
+      const char* src = wbase + j * wstep_row + (long)kt * T::BK * 2;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sw + (wid * T::WI + j) * 1024), 16, 0, 0);
     }
     advance(T::BK);
   };
-  // (register staging) the weight pieces of stage `stage` landed: write them where the DMA would
-  auto commit_w = [&](int stage) {
-    char* sw = smem + stage * T::STAGE_BYTES + BM * T::ROWB;
-#pragma unroll
-    for (int j = 0; j < T::WI; ++j) *(uint4*)(sw + (wid * T::WI + j) * 1024 + lane * 16) = wst[j];
-    if constexpr (DML_V2_XREG) {
-      char* sx = smem + stage * T::STAGE_BYTES;
-#pragma unroll
-      for (int j = 0; j < T::XI; ++j) *(uint4*)(sx + (wid * T::XI + j) * 1024 + lane * 16) = xst[j];
-    }
-  };
-  (void)commit_w;
 
   using Acc = typename std::conditional<MF == 32, f32x16, f32x4>::type;
   Acc acc[T::FI][T::FJ];
@@ -234,13 +202,7 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
   // prologue: tiles 0 .. STAGES-2 in flight
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) {
-      issue(s, s);
-      if constexpr (DML_V2_WREG) {
-        wait_vmcnt<DML_V2_XREG ? 0 : T::XI>();
-        commit_w(s);
-      }
-    }
+    if (s < nk) issue(s, s);
 
   // epilogue operands (bias, residual) prefetched behind the first DMA tiles
   convk::Epilogue<BM, BN, T::NT, RES, T::EP, LATE> epi;
@@ -248,9 +210,8 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
 
   for (int kt = 0; kt < nk; ++kt) {
     // retire tile kt (leave the younger STAGES-2 tiles in flight), then barrier
-    if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * (DML_V2_XREG ? 0 : DML_V2_WREG ? T::XI : T::L)>();
+    if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * T::L>();
     else wait_vmcnt<0>();
-    if constexpr (DML_V2_WREG) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // committed weights
     __builtin_amdgcn_s_barrier();
     // Refill the stage freed by tile kt-1 right after the barrier, before the
     // fragment reads. A/B-measured (profiles/r1_v5/sched_ab_v*.json): issuing it
@@ -286,12 +247,6 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
         }
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (DML_V2_WREG) {
-      if (kt + STAGES - 1 < nk) {  // this iteration's weight loads landed (its X DMA may not have)
-        wait_vmcnt<DML_V2_XREG ? 0 : T::XI>();
-        commit_w((kt + STAGES - 1) % STAGES);
-      }
-    }
   }
 
   // all DMA retired (vmcnt(0) on the last tile); epilogue through LDS

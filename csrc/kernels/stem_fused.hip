@@ -198,6 +198,20 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
           make_uint2(pack2(f0, f1) & kNoSign2, pack2(f2, f3) & kNoSign2);  // +0 only: the pool maxes bits
     }
   }
+  // the folded 1x1's operands are fetched now, under the pool phase (the conv's weights and
+  // accumulators are dead here, so this does not raise the register peak): loaded at the 1x1
+  // itself they were an exposed L2 round trip per workgroup (stem_bench: 35 of 110 us)
+  bf16x8 w4f[2][4];
+  float4 b4f[4];
+  if (a.c4 > 0) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      b4f[o] = *(const float4*)(a.b4 + 16 * o + 4 * fq);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        w4f[ks][o] = *(const bf16x8*)((const bf16*)a.w4 + (long)(16 * o + frow) * a.ldw4 + 32 * ks + 8 * fq);
+    }
+  }
   __syncthreads();
 
 #if DML_STEM_PROBE == 3
@@ -227,18 +241,12 @@ __global__ __launch_bounds__(NT, 3) void stem_kernel(DmlStemArgs a) {
   __syncthreads();  // pooled tile complete; every wave's last conv-tile read is behind this barrier
   f32x4 acc4[4];
 #pragma unroll
-  for (int o = 0; o < 4; ++o) {
-    const float4 bb = *(const float4*)(a.b4 + 16 * o + 4 * fq);
-    acc4[o] = (f32x4){bb.x, bb.y, bb.z, bb.w};
-  }
+  for (int o = 0; o < 4; ++o) acc4[o] = (f32x4){b4f[o].x, b4f[o].y, b4f[o].z, b4f[o].w};
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const bf16x8 pb = *(const bf16x8*)(patch + pswz(16 * wid + frow, 4 * ks + fq));
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      const bf16x8 wa = *(const bf16x8*)((const bf16*)a.w4 + (long)(16 * o + frow) * a.ldw4 + 32 * ks + 8 * fq);
-      acc4[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, pb, acc4[o], 0, 0, 0);
-    }
+    for (int o = 0; o < 4; ++o) acc4[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w4f[ks][o], pb, acc4[o], 0, 0, 0);
   }
   // ReLU -> bf16 staging rows in the (free) conv tile region -> 16-B NHWC stores
 #pragma unroll
