@@ -182,9 +182,11 @@ def parse_kills(specs: List[str]) -> List[Tuple[int, int]]:
 
 def default_kills(world: int, total_batches: int) -> List[Tuple[int, int]]:
     """BASELINE config 5's two worker kills, mid-job: rank 1 once a quarter of the batches
-    completed, rank world-3 at half (never the coordinator world-1, nor rank 0, whose
-    launcher parent reports the record)."""
-    return [(1, total_batches // 4), (world - 3, total_batches // 2)]
+    completed, rank max(2, world-3) at half (two distinct ranks from world 4 on; never the
+    coordinator world-1, nor rank 0, whose launcher parent reports the record)."""
+    if world < 4:
+        raise ValueError("two kills need world >= 4 (rank 0 reports, the coordinator stays)")
+    return [(1, total_batches // 4), (max(2, world - 3), total_batches // 2)]
 
 
 def run_in_children(rank: int, world: int, local_rank: int, rdzv: str, swim_base: int, resnet_images: int,
@@ -212,6 +214,8 @@ def run_in_children(rank: int, world: int, local_rank: int, rdzv: str, swim_base
     if rc not in expected:
         raise RuntimeError(f"service kill pass: rank {rank} child exited {rc}")
     if rank != 0:
+        if os.path.exists(rec_path):  # every survivor writes the record; rank 0's parent reports it
+            os.remove(rec_path)
         return None
     with open(rec_path) as f:
         rec = json.load(f)

@@ -404,3 +404,15 @@ def test_service_bench_kill_pass_world8(tmp_path):
     nb = 2560 // 16 + 1280 // 8
     o = r["outputs"]
     assert o["distinct_batches_in_store"] == nb and o["in_store"] == nb and o["listing_duplicates"] == 0, o
+
+
+def test_default_kills_are_two_distinct_workers():
+    from distributed_machine_learning_amd.parallel.service_bench import default_kills
+
+    for world in (4, 5, 8, 16):
+        ks = default_kills(world, 3200)
+        ranks = [r for r, _ in ks]
+        assert len(set(ranks)) == 2 and 0 not in ranks and world - 1 not in ranks, (world, ks)
+        assert [d for _, d in ks] == [800, 1600]
+    with pytest.raises(ValueError):
+        default_kills(3, 100)
