@@ -29,6 +29,17 @@
 #include "conv_shared.h"
 #include "pool_shared.h"
 
+#ifndef DML_V2_XAUX
+#define DML_V2_XAUX 0  // cache-policy bits of the activation LDS-DMA (A/B: 2 = nt, streamed once)
+#endif
+#ifndef DML_V2_WAUX
+#define DML_V2_WAUX 0  // cache-policy bits of the weight LDS-DMA
+#endif
+#ifndef DML_V2_PROBE
+#define DML_V2_PROBE 0  // A/B timing probes only (tools/build_variant.py, tools/conv_ab.py):
+                        // 1 = no operand DMA (MFMAs on stale LDS), 2 = no fragment reads, 3 = no MFMAs
+#endif
+
 namespace dml {
 namespace v2 {
 
@@ -169,6 +180,7 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
   const long wstep_row = (long)RW::RP * a.Kpad * 2;  // next RP-row piece
 
   auto issue = [&](int kt, int stage) {
+    if (DML_V2_PROBE == 1) return;
     char* sx = smem + stage * T::STAGE_BYTES;
     char* sw = sx + BM * T::ROWB;
 #pragma unroll
@@ -177,12 +189,14 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
       const unsigned ok = ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
       const unsigned msk = 0u - ok;  // branch-free select (no exec-mask split around the DMA)
       const unsigned off = ((unsigned)((base[j] + koff) * 2) & msk) | (OOB & ~msk);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0,
+                                                DML_V2_XAUX);
     }
 #pragma unroll
     for (int j = 0; j < T::WI; ++j) {
       const char* src = wbase + j * wstep_row + (long)kt * T::BK * 2;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sw + (wid * T::WI + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sw + (wid * T::WI + j) * 1024), 16, 0,
+                                        DML_V2_WAUX);
     }
     advance(T::BK);
   };
@@ -230,9 +244,13 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
     for (int ks = 0; ks < KSM; ++ks) {
       const int ch = ks * CPS + fq;
 #pragma unroll
-      for (int i = 0; i < T::FI; ++i) fa[ks][i] = *(const bf16x8*)(sw + RW::off(wc * T::WTC + i * MF + frow, ch));
+      for (int i = 0; i < T::FI; ++i)
+        fa[ks][i] = DML_V2_PROBE == 2 ? (bf16x8)(bf16)(float)(kt + i)
+                                      : *(const bf16x8*)(sw + RW::off(wc * T::WTC + i * MF + frow, ch));
 #pragma unroll
-      for (int j = 0; j < T::FJ; ++j) fb[ks][j] = *(const bf16x8*)(sx + RW::off(wp * T::WTP + j * MF + frow, ch));
+      for (int j = 0; j < T::FJ; ++j)
+        fb[ks][j] = DML_V2_PROBE == 2 ? (bf16x8)(bf16)(float)(kt - j)
+                                      : *(const bf16x8*)(sx + RW::off(wp * T::WTP + j * MF + frow, ch));
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -241,7 +259,9 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
       for (int i = 0; i < T::FI; ++i)
 #pragma unroll
         for (int j = 0; j < T::FJ; ++j) {
-          if constexpr (MF == 16)
+          if constexpr (DML_V2_PROBE == 3)
+            acc[i][j][0] += (float)fa[ks][i][0] * (float)fb[ks][j][1];
+          else if constexpr (MF == 16)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
           else
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
