@@ -37,7 +37,9 @@
 #endif
 #ifndef DML_V2_PROBE
 #define DML_V2_PROBE 0  // A/B timing probes only (tools/build_variant.py, tools/conv_ab.py):
-                        // 1 = no operand DMA (MFMAs on stale LDS), 2 = no fragment reads, 3 = no MFMAs
+                        // 1 = no operand DMA (MFMAs on stale LDS), 2 = no fragment reads, 3 = no MFMAs,
+                        // 4 = every DMA reads the same 16-KiB block (L2-resident: issue cost without
+                        //     HBM latency / bandwidth)
 #endif
 
 namespace dml {
@@ -188,13 +190,15 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
       const int ih = ih0[j] + dih, iw = iw0[j] + diw;
       const unsigned ok = ((unsigned)ih < (unsigned)a.H) & ((unsigned)iw < (unsigned)a.W);
       const unsigned msk = 0u - ok;  // branch-free select (no exec-mask split around the DMA)
-      const unsigned off = ((unsigned)((base[j] + koff) * 2) & msk) | (OOB & ~msk);
+      const unsigned off = DML_V2_PROBE == 4 ? ((unsigned)((base[j] + koff) * 2) & 0x3ff0u)
+                                             : (((unsigned)((base[j] + koff) * 2) & msk) | (OOB & ~msk));
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0,
                                                 DML_V2_XAUX);
     }
 #pragma unroll
     for (int j = 0; j < T::WI; ++j) {
-      const char* src = wbase + j * wstep_row + (long)kt * T::BK * 2;
+      const char* src = DML_V2_PROBE == 4 ? (const char*)a.w + ((lrow * 128 + lchunk * 16) & 0x3ff0)
+                                          : wbase + j * wstep_row + (long)kt * T::BK * 2;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sw + (wid * T::WI + j) * 1024), 16, 0,
                                         DML_V2_WAUX);
     }
