@@ -29,12 +29,6 @@
 #include "conv_shared.h"
 #include "pool_shared.h"
 
-#ifndef DML_V2_XAUX
-#define DML_V2_XAUX 0  // cache-policy bits of the activation LDS-DMA (A/B: 2 = nt, streamed once)
-#endif
-#ifndef DML_V2_WAUX
-#define DML_V2_WAUX 0  // cache-policy bits of the weight LDS-DMA
-#endif
 #ifndef DML_V2_PROBE
 #define DML_V2_PROBE 0  // A/B timing probes only (tools/build_variant.py, tools/conv_ab.py):
                         // 1 = no operand DMA (MFMAs on stale LDS), 2 = no fragment reads, 3 = no MFMAs,
@@ -192,15 +186,17 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
       const unsigned msk = 0u - ok;  // branch-free select (no exec-mask split around the DMA)
       const unsigned off = DML_V2_PROBE == 4 ? ((unsigned)((base[j] + koff) * 2) & 0x3ff0u)
                                              : (((unsigned)((base[j] + koff) * 2) & msk) | (OOB & ~msk));
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0,
-                                                DML_V2_XAUX);
+      // a.xnt (wave-uniform): non-temporal activation stream (aux = 2), the 1x1 convs' once-read rows
+      if (a.xnt)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 2);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < T::WI; ++j) {
       const char* src = DML_V2_PROBE == 4 ? (const char*)a.w + ((lrow * 128 + lchunk * 16) & 0x3ff0)
                                           : wbase + j * wstep_row + (long)kt * T::BK * 2;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sw + (wid * T::WI + j) * 1024), 16, 0,
-                                        DML_V2_WAUX);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sw + (wid * T::WI + j) * 1024), 16, 0, 0);
     }
     advance(T::BK);
   };
