@@ -134,8 +134,9 @@ class Engine:
         self.exp_red.update(self._fusable_stage_end(fuse_blocks))
         # independent residual-free convs of one graph level -> one grouped grid each
         self.conv_groups = self._conv_group_candidates() if conv_groups else []
-        # non-temporal activation DMA for the 1x1 convs (DmlConvArgs.xnt; DML_XNT=1: on). Off by
-        # default until its end-to-end A/B is in (per layer it is -5..-33 % on the BK-64 tiles)
+        # non-temporal activation DMA for the 1x1 convs (DmlConvArgs.xnt; DML_XNT=1: on). Off: per
+        # layer (cold) -5..-33 % on the BK-64 tiles, end to end -1 % (the input is warm in L2 /
+        # MALL from its producer inside a forward)
         self._xnt = os.environ.get("DML_XNT", "0") != "0"
         self._src_tensors, self._result_views = src_tensors, result_views
         self.src_index = src_index

@@ -131,11 +131,15 @@ def test_graph_replay_matches_eager():
 
 
 def test_batch_rows_independent():
-    """Row i of a batch-4 run equals the batch-1 run of image i (no cross-image leakage)."""
+    """Row i of a batch-4 run equals the batch-1 run of image i (no cross-image leakage),
+    bit for bit. Both engines use the default tile of every layer: autotuned per batch size
+    they may pick different kernels (at batch 1 the tuner can pick the Winograd tile for the
+    7x7 stage-5 convs, whose rounding differs by design), which is not what this tests."""
     g, w = build_model("ResNet50", seed=2, calibrate=False)
     imgs = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8, device="cuda")
-    e4 = Engine(g, w, batch=4)
-    e1 = Engine(g, w, batch=1)
+    e4 = Engine(g, w, batch=4, autotune=False)
+    e1 = Engine(g, w, batch=1, autotune=False)
+    assert e1.op_cfg == e4.op_cfg
     e4.infer(imgs)
     outs = []
     for i in range(4):
@@ -143,7 +147,7 @@ def test_batch_rows_independent():
         torch.cuda.synchronize()
         outs.append(e1.buf[g.logits].clone())
     torch.cuda.synchronize()
-    assert torch.allclose(torch.cat(outs), e4.buf[g.logits], atol=1e-3, rtol=1e-3)
+    assert torch.equal(torch.cat(outs), e4.buf[g.logits])
 
 
 @pytest.mark.parametrize("use_graph", [False, True])
