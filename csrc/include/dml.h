@@ -57,9 +57,6 @@ typedef struct {
   // host-packed [Cin/32][16 positions][Cout/16 fragments, padded to 4k][64 lanes][8] (ops.pack_wino_weight);
   // null when the conv has none
   const void* wu;
-  // activation LDS-DMA cache policy: 1 = non-temporal (streamed once: the 1x1 convs, whose
-  // activation tile is read by few channel tiles; measured -14..-31 %), 0 = default
-  int xnt;
 } DmlConvArgs;
 
 

@@ -186,11 +186,8 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
       const unsigned msk = 0u - ok;  // branch-free select (no exec-mask split around the DMA)
       const unsigned off = DML_V2_PROBE == 4 ? ((unsigned)((base[j] + koff) * 2) & 0x3ff0u)
                                              : (((unsigned)((base[j] + koff) * 2) & msk) | (OOB & ~msk));
-      // a.xnt (wave-uniform): non-temporal activation stream (aux = 2), the 1x1 convs' once-read rows
-      if (a.xnt)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 2);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 0);
+      // cache policy: default (a non-temporal stream, aux = 2, measured -1 % end to end: DESIGN §2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wid * T::XI + j) * 1024), 16, off, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < T::WI; ++j) {

@@ -31,7 +31,6 @@ class ConvArgs(C.Structure):
         ("ksplit", C.c_int), ("split_ld", C.c_int),
         ("rsub", C.c_int), ("rW", C.c_int), ("rHW", C.c_int),
         ("wu", C.c_void_p),   # Winograd F(2x2, 3x3) weights (cfg 80), ops.pack_wino_weight
-        ("xnt", C.c_int),     # activation DMA non-temporal (1x1 convs)
     ]
 
 

@@ -134,10 +134,6 @@ class Engine:
         self.exp_red.update(self._fusable_stage_end(fuse_blocks))
         # independent residual-free convs of one graph level -> one grouped grid each
         self.conv_groups = self._conv_group_candidates() if conv_groups else []
-        # non-temporal activation DMA for the 1x1 convs (DmlConvArgs.xnt; DML_XNT=1: on). Off: per
-        # layer (cold) -5..-33 % on the BK-64 tiles, end to end -1 % (the input is warm in L2 /
-        # MALL from its producer inside a forward)
-        self._xnt = os.environ.get("DML_XNT", "0") != "0"
         self._src_tensors, self._result_views = src_tensors, result_views
         self.src_index = src_index
         if src_index is not None:
@@ -639,8 +635,6 @@ class Engine:
                 ga.n, ga.npool = len(convs), len(pools)
                 for i, m in enumerate(convs):
                     ga.a[i] = self._conv_args(m)
-                    if cfg in BK32_CFGS:
-                        ga.a[i].xnt = 0
                 for i, m in enumerate(pools):
                     ga.pool[i] = self._pool_args(m)
                 N.check(L.dml_plan_add_conv_group(plan, C.byref(ga), cfg), f"plan conv group {n.name}")
@@ -687,8 +681,6 @@ class Engine:
             if isinstance(n, (Conv, Dense, FusedConv)):
                 cfg = self.cfg_overrides.get(n.name, self.tuned.get(n.name, -1))
                 a = self._conv_args(n)
-                if cfg in BK32_CFGS:  # the non-temporal activation stream only pays on the BK-64 rings
-                    a.xnt = 0
                 used = N.check(L.dml_plan_add_conv(plan, C.byref(a), cfg), f"plan conv {n.name}")
                 self.op_cfg[n.name] = used
                 self._keep.append(a)
@@ -759,7 +751,6 @@ class Engine:
             a.rsub, a.rW, a.rHW = n.res_sub, rw, rh * rw
         if n.name in self.wwino:
             a.wu = self.wwino[n.name].data_ptr()
-        a.xnt = int(self._xnt and n.kh == 1 and n.kw == 1)
         return a
 
     # ---------------------------------------------------------------- run ----
@@ -879,10 +870,6 @@ class Engine:
 # the two streams no longer carry equal work. Kept as an option. DML_MERGE_AT overrides it:
 # "InceptionV3=<node>,ResNet50=<node>" (a model left out keeps its default), "0" = off for all.
 MERGE_AT: Dict[str, Optional[str]] = {"ResNet50": None, "InceptionV3": None}
-
-# tile configs with 32-deep K tiles (csrc/kernels/conv_igemm_v2.hip DML_V2_TILES, BK = 32): on
-# these the non-temporal activation stream was slower (tools/conv_ab.py --xnt)
-BK32_CFGS = frozenset({23, 24, 25, 26, 27, 28, 29, 30, 31, 33, 34, 36, 56, 57, 58, 59, 60})
 
 
 def _extra_stream(device) -> "torch.cuda.Stream":

@@ -2,7 +2,6 @@
 conv tile configs, per layer shape: outputs must be bit-identical; times warm and cold.
 
 python tools/conv_ab.py --lib variants/libdml_x.so [--cfgs 11,14,15,24,25,30,31] [--iters 20] [--out f.json]
-python tools/conv_ab.py --xnt ...   # main library, DmlConvArgs.xnt 0 vs 1 (outputs must match)
 """
 import argparse
 import ctypes as C
@@ -27,19 +26,15 @@ SHAPES = [  # name, batch, h, w, cin, cout, k, stride, pad
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--lib", default="")
-    ap.add_argument("--xnt", action="store_true", help="variant = the main library with xnt = 1")
+    ap.add_argument("--lib", required=True)
     ap.add_argument("--cfgs", default="11,14,15,24,25,30,31")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     N.ensure_device_init()
-    if a.xnt:
-        libs = [("main", N.lib()), ("variant", N.lib())]
-    else:
-        L2 = C.CDLL(a.lib)
-        L2.dml_conv_v2_init()
-        libs = [("main", N.lib()), ("variant", L2)]
+    L2 = C.CDLL(a.lib)
+    L2.dml_conv_v2_init()
+    libs = [("main", N.lib()), ("variant", L2)]
     scrub = torch.zeros(128 << 20, device="cuda")
     s = N.stream_ptr()
     rows, bad = [], 0
@@ -58,7 +53,6 @@ def main():
                 y = torch.empty(B, ho, wo, cout, device="cuda", dtype=torch.bfloat16)
                 args = N.ConvArgs(x.data_ptr(), wp.data_ptr(), bias.data_ptr(), None, y.data_ptr(), B, h, w, cin, cin,
                                   k, k, st, st, pad, pad, ho, wo, cout, K, kp, cout, 0, 1, 0, 1, 1)
-                args.xnt = int(a.xnt and ln == "variant")
 
                 def run():
                     rc = L.dml_conv(C.byref(args), cfg, C.c_void_p(s))
