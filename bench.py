@@ -66,6 +66,9 @@ def parse_args(argv=None):
     ap.add_argument("--streams", type=int, default=0,
                     help="concurrent streams for the sub-batches (default = --splits); sub-batch i on stream i %% S")
     ap.add_argument("--no-verify", action="store_true", help="skip the post-run top-5 self-check")
+    ap.add_argument("--gather-lag", type=int, default=-1, choices=(-1, 0, 1),
+                    help="result gather of batch k after forward k+1 on a comm stream (1) or right behind "
+                         "forward k (0); -1 = auto: 1 on several GPUs, 0 on one")
     ap.add_argument("--lookahead", type=int, default=0, choices=(0, 1, 2),
                     help="dispatch broadcast runs this many steps ahead; 0 = auto: 1 on one GPU (a "
                          "batch-time less query latency at equal throughput, measured), 2 on several "
@@ -150,7 +153,8 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
     store.fill_synthetic(seed=rank)
     dp = DataPlane(device, result_shape=(2, B, 5))
     lookahead = args.lookahead or (1 if world == 1 else 2)
-    pipe = ServingPipeline(eng, store, dp, use_graph=not args.no_graph, lookahead=lookahead)
+    pipe = ServingPipeline(eng, store, dp, use_graph=not args.no_graph, lookahead=lookahead,
+                           gather_lag=None if args.gather_lag < 0 else args.gather_lag)
     cap = store.capacity
 
     def table(k):
@@ -220,7 +224,7 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
             "config": {"model": model, "global_batch": B * world, "seq_len": None,
                        "image_hw": list(g.input_hw), "parallelism": f"dp{world}",
                        "per_worker_batch": B, "graph": not args.no_graph, "stream_splits": splits,
-                       "streams": eng.nstreams if splits > 1 else 1, "dispatch_lookahead": pipe.lookahead,
+                       "streams": eng.nstreams if splits > 1 else 1, "dispatch_lookahead": pipe.lookahead, "gather_lag": pipe.gather_lag,
                        "merged_tail_from": getattr(eng, "merge_at", None)},
             "baseline": {"source": "BASELINE.md scheduler-predicted query rate (cost model, CS425 VMs, TF CPU)",
                          "value": round(ref_rate(model, world), 3), "unit": "images/s"},

@@ -56,11 +56,14 @@ def _split_ref(g, w, imgs, half, parts=2):
     return torch.cat(out, dim=1)
 
 
-@pytest.mark.parametrize("splits,streams,lookahead", [(2, 0, 2), (8, 2, 2), (2, 0, 1)])
-def test_serving_pipeline_matches_engine(rccl_world1, splits, streams, lookahead):
+@pytest.mark.parametrize("splits,streams,lookahead,lag", [(2, 0, 2, None), (8, 2, 2, None), (2, 0, 1, None),
+                                                          (2, 0, 2, 1), (8, 2, 2, 1)])
+def test_serving_pipeline_matches_engine(rccl_world1, splits, streams, lookahead, lag):
     """splits 8 on 2 streams: eight graph captures; captured lazily inside the
     loop they once met the RCCL watchdog querying an event on a capturing stream
-    (hipErrorCapturedEvent), hence Engine.capture() before the first collective."""
+    (hipErrorCapturedEvent), hence Engine.capture() before the first collective.
+    lag 1: the world > 1 schedule (result gather of batch k on the comm stream after
+    forward k+1, rows through the send ring) forced at world 1 on the real engines."""
     from distributed_machine_learning_amd.models import build_model
     from distributed_machine_learning_amd.models.engine import SplitEngine
     from distributed_machine_learning_amd.parallel.dataplane import DESC_FIELDS, DataPlane, init_process_group
@@ -77,7 +80,8 @@ def test_serving_pipeline_matches_engine(rccl_world1, splits, streams, lookahead
     dp = DataPlane(dev, result_shape=(2, B, 5))
     got = {}
     pipe = ServingPipeline(eng, store, dp, use_graph=True, on_results=lambda rec: got.__setitem__(rec.step, rec.results[0]),
-                           lookahead=lookahead)
+                           lookahead=lookahead, gather_lag=lag)
+    assert pipe.gather_lag == (lag or 0)
 
     def table(k):
         t = np.zeros((world, DESC_FIELDS), np.int64)
