@@ -5,7 +5,8 @@
 // (SURVEY §2.7 "conv_igemm_bf16"; the reference runs these inside Keras,
 // models.py:26,51 — it has no kernel of its own). cfg ids 10..63 select a v2
 // tile configuration (dml_conv_v2), id 80 (DML_WINO_CFG) the Winograd F(2x2, 3x3)
-// kernel of stride-1 3x3 convs (conv_wino.hip); they are part of the ABI the plan
+// kernel of stride-1 3x3 convs (conv_wino.hip), ids 84..90 the persistent
+// weight-stationary 1x1 kernel (conv_ws.hip); they are part of the ABI the plan
 // builder and the autotuner (ops/tuning.py) use.
 //
 // Removed (measured never faster, kept only as history in DESIGN.md and
@@ -26,9 +27,17 @@ static int validate(const DmlConvArgs* a, int cfg) {
     }
     return 0;
   }
+  if (dml_conv_ws_supported(cfg)) {  // weight-stationary 1x1 (conv_ws.hip): its own shape gate
+    const char* why = dml_conv_ws_check(a, cfg);
+    if (why) {
+      dml_set_error(why);
+      return -1;
+    }
+    return 0;
+  }
   const int bn = dml_conv_v2_bn(cfg);
   if (bn <= 0) {
-    dml_set_error("dml_conv: cfg must be a v2 tile config (10..63) or a Winograd config (80, 81)");
+    dml_set_error("dml_conv: cfg must be a v2 tile config (10..63), a Winograd config (80..83) or a ws config (84..90)");
     return -1;
   }
   // weights are packed with Cout padded to a multiple of 256 rows; a 96- or
@@ -58,6 +67,7 @@ static int validate(const DmlConvArgs* a, int cfg) {
 
 extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
   if (validate(a, cfg) != 0) return -1;
+  if (dml_conv_ws_supported(cfg)) return dml_conv_ws(a, cfg, s);
   return dml_conv_wino_supported(cfg) ? dml_conv_wino(a, cfg, s) : dml_conv_v2(a, cfg, s);
 }
 
