@@ -201,12 +201,6 @@ int dml_conv_wino_supported(int cfg);  // the config's output-channel tile, 0: n
 int dml_conv_wino(const DmlConvArgs* a, int cfg, hipStream_t s);
 const char* dml_conv_wino_check(const DmlConvArgs* a);
 int dml_conv_wino_init(void);
-// Persistent weight-stationary 1x1 stride-1 conv (conv_ws.hip; cfgs 84..90): the
-// workgroup's weight panel stays in LDS, one LDS-DMA ring runs across its pixel tiles
-int dml_conv_ws_supported(int cfg);  // the config's output-channel tile, 0: not a ws config
-int dml_conv_ws(const DmlConvArgs* a, int cfg, hipStream_t s);
-const char* dml_conv_ws_check(const DmlConvArgs* a, int cfg);
-int dml_conv_ws_init(void);
 int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);

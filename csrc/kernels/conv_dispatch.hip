@@ -5,15 +5,16 @@
 // (SURVEY §2.7 "conv_igemm_bf16"; the reference runs these inside Keras,
 // models.py:26,51 — it has no kernel of its own). cfg ids 10..63 select a v2
 // tile configuration (dml_conv_v2), id 80 (DML_WINO_CFG) the Winograd F(2x2, 3x3)
-// kernel of stride-1 3x3 convs (conv_wino.hip), ids 84..90 the persistent
-// weight-stationary 1x1 kernel (conv_ws.hip); they are part of the ABI the plan
+// kernel of stride-1 3x3 convs (conv_wino.hip); they are part of the ABI the plan
 // builder and the autotuner (ops/tuning.py) use.
 //
 // Removed (measured never faster, kept only as history in DESIGN.md and
 // profiles/): the register-staged v1 kernel (cfg 0..4, r1, profiles/r1_v2), the
 // stride-1 halo-tile kernel (cfg 40..47, r2, profiles/r1_v5/halo_vs_v2_*.json: won
-// 0 of 217 tuned shapes) and the shifted-pixel stride-1 kernel (cfg 64..69, r4:
-// never picked by the cold tuner, profiles/r3_v2/shift_vs_igemm.json).
+// 0 of 217 tuned shapes), the shifted-pixel stride-1 kernel (cfg 64..69, r4:
+// never picked by the cold tuner, profiles/r3_v2/shift_vs_igemm.json) and the
+// persistent weight-stationary 1x1 kernel (cfg 84..90, r4, commit f96f4b1: parity at
+// best, profiles/r4_probes/ws).
 #include "common.h"
 #include "dml.h"
 #include "pool_shared.h"
@@ -27,17 +28,9 @@ static int validate(const DmlConvArgs* a, int cfg) {
     }
     return 0;
   }
-  if (dml_conv_ws_supported(cfg)) {  // weight-stationary 1x1 (conv_ws.hip): its own shape gate
-    const char* why = dml_conv_ws_check(a, cfg);
-    if (why) {
-      dml_set_error(why);
-      return -1;
-    }
-    return 0;
-  }
   const int bn = dml_conv_v2_bn(cfg);
   if (bn <= 0) {
-    dml_set_error("dml_conv: cfg must be a v2 tile config (10..63), a Winograd config (80..83) or a ws config (84..90)");
+    dml_set_error("dml_conv: cfg must be a v2 tile config (10..63) or a Winograd config (80..83)");
     return -1;
   }
   // weights are packed with Cout padded to a multiple of 256 rows; a 96- or
@@ -67,7 +60,6 @@ static int validate(const DmlConvArgs* a, int cfg) {
 
 extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
   if (validate(a, cfg) != 0) return -1;
-  if (dml_conv_ws_supported(cfg)) return dml_conv_ws(a, cfg, s);
   return dml_conv_wino_supported(cfg) ? dml_conv_wino(a, cfg, s) : dml_conv_v2(a, cfg, s);
 }
 

@@ -480,7 +480,6 @@ extern "C" int dml_conv_v2_init(void) {
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   if (!rc && dml_expand_reduce_init() != 0) return -1;  // fused block-boundary kernels (bottleneck_fused.hip)
   if (!rc && dml_conv_wino_init() != 0) return -1;     // Winograd 3x3 convs (conv_wino.hip)
-  if (!rc && dml_conv_ws_init() != 0) return -1;       // weight-stationary 1x1 convs (conv_ws.hip)
   return rc ? -1 : 0;
 }
 
@@ -498,7 +497,6 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
 // channel-tile width of a config (0: not a config)
 extern "C" int dml_conv_v2_bn(int cfg) {
   if (dml_conv_wino_supported(cfg)) return dml_conv_wino_supported(cfg);  // Winograd (conv_wino.hip)
-  if (dml_conv_ws_supported(cfg)) return dml_conv_ws_supported(cfg);      // weight-stationary 1x1 (conv_ws.hip)
   if (cfg < 10) return 0;
   switch (cfg) {
 #define DML_CASE(id, BM, BN, WM, WN, ST, BK, MF, RL, W) \

@@ -30,7 +30,6 @@ SOURCES = [
     CSRC / "kernels" / "conv_pool.hip",
     CSRC / "kernels" / "bottleneck_fused.hip",
     CSRC / "kernels" / "conv_wino.hip",
-    CSRC / "kernels" / "conv_ws.hip",
     CSRC / "kernels" / "expand_reduce_chain.hip",
     CSRC / "runtime" / "runtime.hip",
 ]

@@ -114,7 +114,6 @@ _SIGS = {
     "dml_plan_add_conv_group": (C.c_int, [C.c_void_p, C.POINTER(ConvGroupArgs), C.c_int]),
     "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),
     "dml_conv_wino_check": (C.c_char_p, [C.POINTER(ConvArgs)]),
-    "dml_conv_ws_check": (C.c_char_p, [C.POINTER(ConvArgs), C.c_int]),
     "dml_conv_v2_bn": (C.c_int, [C.c_int]),
     "dml_conv_v2_init": (C.c_int, []),
     "dml_pool": (C.c_int, [C.POINTER(PoolArgs), C.c_void_p]),
