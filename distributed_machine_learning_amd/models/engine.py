@@ -873,11 +873,9 @@ MERGE_AT: Dict[str, Optional[str]] = {"ResNet50": None, "InceptionV3": None}
 
 
 def _extra_stream(device) -> "torch.cuda.Stream":
-    """A sub-batch stream of a SplitEngine. DML_SPLIT_STREAM_PRIO (A/B knob): HIP stream
-    priority of the extra streams relative to the caller's stream (-1 = higher, 1 = lower;
-    unset = the default priority)."""
-    prio = os.environ.get("DML_SPLIT_STREAM_PRIO")
-    return torch.cuda.Stream(device, priority=int(prio)) if prio else torch.cuda.Stream(device)
+    """A sub-batch stream of a SplitEngine, at the caller's stream priority (a higher one
+    for the extra streams measured 5 % slower)."""
+    return torch.cuda.Stream(device)
 
 
 def merge_point(model: str) -> Optional[str]:
