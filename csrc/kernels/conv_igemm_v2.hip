@@ -33,7 +33,8 @@
 #define DML_V2_PROBE 0  // A/B timing probes only (tools/build_variant.py, tools/conv_ab.py):
                         // 1 = no operand DMA (MFMAs on stale LDS), 2 = no fragment reads, 3 = no MFMAs,
                         // 4 = every DMA reads the same 16-KiB block (L2-resident: issue cost without
-                        //     HBM latency / bandwidth)
+                        //     HBM latency / bandwidth), 5 = no per-lane K walk (advance() reduced to
+                        //     one masked add: the address math's cost), 6 = no K-loop barrier
 #endif
 
 namespace dml {
@@ -144,6 +145,10 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
   const int step_r = dh * a.W * a.ldx;           // koff change for rr += 1
   int cc = lchunk * 8, ss = 0, rr = 0, dih = 0, diw = 0, koff = lchunk * 8;
   auto advance = [&](int by) {
+    if (DML_V2_PROBE == 5) {  // stays inside the row's first 64 channels (Cin >= 64): in bounds
+      koff = (koff + by) & 63;
+      return;
+    }
     cc += by;
     koff += by;
     while (cc >= a.Cin) {
@@ -223,7 +228,7 @@ __device__ __forceinline__ void conv_v2_tile(const DmlConvArgs& a, int Lb, int n
     // retire tile kt (leave the younger STAGES-2 tiles in flight), then barrier
     if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * T::L>();
     else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
+    if (DML_V2_PROBE != 6) __builtin_amdgcn_s_barrier();
     // Refill the stage freed by tile kt-1 right after the barrier, before the
     // fragment reads. A/B-measured (profiles/r1_v5/sched_ab_v*.json): issuing it
     // between the two k-steps, or interleaving it among the MFMAs with
