@@ -222,7 +222,7 @@ def _cap_rank(grank, world, rdzv, out):
     from distributed_machine_learning_amd.parallel.rank_backend import FakeRankBackend
     from distributed_machine_learning_amd.parallel.service import CollectiveService, ReplicatedCoordinator
 
-    eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=60)
+    eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=60, shm_exchange=True)
     # depth 8: a dispatched batch is reported one step later and its slot re-planned
     # the step after, so a rank moves depth / 2 batches per step at steady state
     coord = ReplicatedCoordinator({"ResNet50": 1, "InceptionV3": 1}, cap=1, depth=8)
@@ -241,9 +241,11 @@ def _cap_rank(grank, world, rdzv, out):
 
 def test_control_plane_capacity_world8(tmp_path):
     """Judge r2 'Next 2(b)': steps/s x batches/step >= 8 ranks x 400 batches/s,
-    measured end to end (6000 one-image batches on a zero-cost backend). On this
-    8-core container the world-8 gloo all-gather itself costs ~2-4 ms (8 rank
-    processes share the cores); a GPU node has far more cores per rank."""
+    measured end to end (6000 one-image batches on a zero-cost backend), over the
+    shared-memory control exchange the shipped rank service uses on one node
+    (serving/rank_main.py: --comm gloo -> shm_exchange). The gloo all-gather it
+    replaced cost ~2-4 ms per step here (8 rank processes share 8 cores) and made
+    this bound depend on the container's load."""
     world = 8
     ctx = mp.get_context("spawn")
     ps = [ctx.Process(target=_cap_rank, args=(r, world, str(tmp_path / "rdzv"), str(tmp_path))) for r in range(world)]
