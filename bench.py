@@ -270,9 +270,16 @@ def main(argv=None) -> int:
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch(args.gpus, argv)
 
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from distributed_machine_learning_amd.utils import numa
+
+    # NUMA-local placement before any GPU call: this rank's threads (and the pinned arenas
+    # they first-touch) on the cores of its GPU's socket (utils/numa.py)
+    placement = numa.bind_local_rank(int(os.environ.get("LOCAL_RANK", "0")))
+    placement["rank"] = int(os.environ.get("RANK", "0"))
+
     import torch
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from distributed_machine_learning_amd.models import canonical_name
     from distributed_machine_learning_amd.parallel.dataplane import init_process_group
 
@@ -284,6 +291,13 @@ def main(argv=None) -> int:
     if not args.dry_run:
         device = torch.device("cuda", local)
         torch.cuda.set_device(device)
+
+    import torch.distributed as dist
+
+    placements = [placement]
+    if dist.is_initialized() and world > 1:
+        placements = [None] * world
+        dist.all_gather_object(placements, placement)
 
     recs = {}
     for i, m in enumerate(models):
@@ -322,9 +336,8 @@ def main(argv=None) -> int:
             out["models"] = {m: recs[m] for m in models[1:]}
         if svc is not None:
             out["service"] = svc
+        out["placement"] = placements
         print(json.dumps(out), flush=True)
-    import torch.distributed as dist
-
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

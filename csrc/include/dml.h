@@ -53,10 +53,6 @@ typedef struct {
   // stride rsub from its full-resolution grid (rW = its width, rHW = H*W), used
   // when a stride-2 consumer has been pushed up into the block (models/optimize.py).
   int rsub, rW, rHW;
-  // Winograd F(2x2, 3x3) weights (cfg 80, conv_wino.hip): U = G g G^T per (cin, cout), bf16,
-  // host-packed [Cin/32][16 positions][Cout/16 fragments, padded to 4k][64 lanes][8] (ops.pack_wino_weight);
-  // null when the conv has none
-  const void* wu;
 } DmlConvArgs;
 
 
@@ -150,7 +146,7 @@ typedef struct {
   int c4, ldw4;
 } DmlConvPoolArgs;
 
-// Fused ResNet50 block boundary (csrc/kernels/bottleneck_fused.hip), F = C / 4:
+// Fused ResNet50 block boundary (csrc/kernels/expand_reduce_chain.hip), F = C / 4:
 //   y = relu(w3 . x + b3 + res)  (1x1 expand F -> C + shortcut)
 //   z = relu(w1 . y + b1)        (next block's 1x1 reduce C -> F)
 typedef struct {
@@ -180,8 +176,8 @@ typedef struct {
 int dml_stem_resnet(const DmlStemArgs* a, hipStream_t s);
 int dml_stem_inception(const DmlIncStemArgs* a, hipStream_t s);
 int dml_conv3x3_pool(const DmlConvPoolArgs* a, hipStream_t s);
+// chained-GEMM block boundary (expand_reduce_chain.hip); dml_expand_reduce is the same entry
 int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s);
-// chained-GEMM block boundary, F = 128 / C = 512 (expand_reduce_chain.hip); dml_expand_reduce routes to it
 int dml_chain(const DmlExpandReduceArgs* a, hipStream_t s);
 int dml_chain_supported(const DmlExpandReduceArgs* a);
 int dml_chain_init(void);
@@ -193,14 +189,16 @@ int dml_conv_pick_cfg(const DmlConvArgs* a);
 int dml_conv_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s);
 int dml_conv_v2_group(const DmlConvGroupArgs* g, int cfg, hipStream_t s);
 int dml_conv_v2_group_supported(int cfg);
-int dml_conv_v2_bn(int cfg);
-// Winograd F(2x2, 3x3) stride-1 conv (conv_wino.hip; cfg DML_WINO_CFG = the default
-// configuration, 81 = 64-channel tiles): needs DmlConvArgs.wu
-#define DML_WINO_CFG 80
-int dml_conv_wino_supported(int cfg);  // the config's output-channel tile, 0: not a Winograd config
-int dml_conv_wino(const DmlConvArgs* a, int cfg, hipStream_t s);
-const char* dml_conv_wino_check(const DmlConvArgs* a);
-int dml_conv_wino_init(void);
+int dml_conv_v2_bn(int cfg);  // channel-tile width of any tile config (v2 or warp-specialised), 0: none
+// warp-specialised implicit GEMM (conv_igemm_ws.hip; cfg ids 100..119): loader waves + MFMA waves
+int dml_conv_ws(const DmlConvArgs* a, int cfg, hipStream_t s);
+int dml_conv_ws_bn(int cfg);
+int dml_conv_ws_init(void);
+// persistent warp-specialised implicit GEMM (conv_igemm_wsp.hip; cfg ids 120..139): one operand
+// ring over each workgroup's whole tile list (no split-K)
+int dml_conv_wsp(const DmlConvArgs* a, int cfg, hipStream_t s);
+int dml_conv_wsp_bn(int cfg);
+int dml_conv_wsp_init(void);
 int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);

@@ -4,9 +4,10 @@
 // Serves every convolution of ResNet50 / InceptionV3 and the FC layer
 // (SURVEY §2.7 "conv_igemm_bf16"; the reference runs these inside Keras,
 // models.py:26,51 — it has no kernel of its own). cfg ids 10..63 select a v2
-// tile configuration (dml_conv_v2), id 80 (DML_WINO_CFG) the Winograd F(2x2, 3x3)
-// kernel of stride-1 3x3 convs (conv_wino.hip); they are part of the ABI the plan
-// builder and the autotuner (ops/tuning.py) use.
+// tile configuration (dml_conv_v2), ids 100..119 a warp-specialised one (loader +
+// MFMA waves, dml_conv_ws, conv_igemm_ws.hip), ids 120..139 its persistent form
+// (dml_conv_wsp, conv_igemm_wsp.hip); they are part of the ABI the plan builder and the
+// autotuner (ops/tuning.py) use.
 //
 // Removed (measured never faster, kept only as history in DESIGN.md and
 // profiles/): the register-staged v1 kernel (cfg 0..4, r1, profiles/r1_v2), the
@@ -14,23 +15,16 @@
 // 0 of 217 tuned shapes), the shifted-pixel stride-1 kernel (cfg 64..69, r4:
 // never picked by the cold tuner, profiles/r3_v2/shift_vs_igemm.json) and the
 // persistent weight-stationary 1x1 kernel (cfg 84..90, r4, commit f96f4b1: parity at
-// best, profiles/r4_probes/ws).
+// best, profiles/r4_probes/ws) and the Winograd F(2x2, 3x3) kernel (cfg 80..83, r4,
+// removed in r5: slower than the direct tiles on every shape, profiles/r4_wino).
 #include "common.h"
 #include "dml.h"
 #include "pool_shared.h"
 
 static int validate(const DmlConvArgs* a, int cfg) {
-  if (dml_conv_wino_supported(cfg)) {  // Winograd F(2x2, 3x3) (conv_wino.hip): its own shape gate
-    const char* why = dml_conv_wino_check(a);
-    if (why) {
-      dml_set_error(why);
-      return -1;
-    }
-    return 0;
-  }
   const int bn = dml_conv_v2_bn(cfg);
   if (bn <= 0) {
-    dml_set_error("dml_conv: cfg must be a v2 tile config (10..63) or a Winograd config (80..83)");
+    dml_set_error("dml_conv: cfg must be a tile config (v2: 10..63, warp-specialised: 100..119, persistent: 120..139)");
     return -1;
   }
   // weights are packed with Cout padded to a multiple of 256 rows; a 96- or
@@ -60,7 +54,8 @@ static int validate(const DmlConvArgs* a, int cfg) {
 
 extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
   if (validate(a, cfg) != 0) return -1;
-  return dml_conv_wino_supported(cfg) ? dml_conv_wino(a, cfg, s) : dml_conv_v2(a, cfg, s);
+  if (cfg >= 120) return dml_conv_wsp(a, cfg, s);
+  return cfg >= 100 ? dml_conv_ws(a, cfg, s) : dml_conv_v2(a, cfg, s);
 }
 
 extern "C" int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg) {

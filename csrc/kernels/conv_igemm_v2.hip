@@ -483,8 +483,9 @@ extern "C" int dml_conv_v2_init(void) {
   DML_V2_GROUP_TILES(DML_SET)
 #undef DML_SET
   if (rc) dml_set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-  if (!rc && dml_expand_reduce_init() != 0) return -1;  // fused block-boundary kernels (bottleneck_fused.hip)
-  if (!rc && dml_conv_wino_init() != 0) return -1;     // Winograd 3x3 convs (conv_wino.hip)
+  if (!rc && dml_chain_init() != 0) return -1;  // chained block-boundary kernels (expand_reduce_chain.hip)
+  if (!rc && dml_conv_ws_init() != 0) return -1;  // warp-specialised tiles (conv_igemm_ws.hip)
+  if (!rc && dml_conv_wsp_init() != 0) return -1;  // persistent warp-specialised tiles (conv_igemm_wsp.hip)
   return rc ? -1 : 0;
 }
 
@@ -499,9 +500,11 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
   }
 }
 
-// channel-tile width of a config (0: not a config)
+// channel-tile width of a config (0: not a config); ids 100..119: the warp-specialised
+// tiles of conv_igemm_ws.hip, 120..139 their persistent form (conv_igemm_wsp.hip)
 extern "C" int dml_conv_v2_bn(int cfg) {
-  if (dml_conv_wino_supported(cfg)) return dml_conv_wino_supported(cfg);  // Winograd (conv_wino.hip)
+  if (cfg >= 120) return dml_conv_wsp_bn(cfg);
+  if (cfg >= 100) return dml_conv_ws_bn(cfg);
   if (cfg < 10) return 0;
   switch (cfg) {
 #define DML_CASE(id, BM, BN, WM, WN, ST, BK, MF, RL, W) \

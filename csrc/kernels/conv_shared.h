@@ -1,5 +1,5 @@
 // conv_shared.h — pieces shared by the LDS-DMA convolution kernels
-// (conv_igemm_v2.hip: implicit GEMM; bottleneck_fused.hip: fused block boundary).
+// (conv_igemm_v2.hip: implicit GEMM; expand_reduce_chain.hip: chained block boundary).
 //
 //  * counted vmcnt waits (LDS-DMA completes in issue order with other VMEM ops)
 //  * the 16-B-chunk XOR swizzle of a 128-B LDS tile row
@@ -59,7 +59,9 @@ struct Rows {
 // the start of each pass instead of before the main loop, so its EIT x 4 VGPRs
 // are not live across the K loop (the tiles whose residual prefetch costs a
 // workgroup per CU).
-template <int BM, int BN, int NT, bool RES, int P = 1, bool LATE = false>
+// XT: the workgroup has threads beyond the NT output threads (the loader waves of
+// conv_igemm_ws.hip), which skip the residual loads and the output rows.
+template <int BM, int BN, int NT, bool RES, int P = 1, bool LATE = false, bool XT = false>
 struct Epilogue {
   static constexpr int CG = BN / 8;            // 8-channel groups per pixel
   static constexpr int EIT = BM * CG / NT;     // pixels handled per thread
@@ -101,6 +103,7 @@ struct Epilogue {
 
   // residual rows [it0, it1) of this thread's channel group -> rpre
   __device__ __forceinline__ void load_res(const DmlConvArgs& a, int tid, int it0, int it1) {
+    if (XT && tid >= NT) return;  // wave-uniform: no output rows (a loader wave, conv_igemm_ws.hip)
     const unsigned short* __restrict__ rg = (const unsigned short*)a.res;
 #pragma unroll
     for (int it = 0; it < EIT; ++it) {
@@ -122,10 +125,12 @@ struct Epilogue {
   // v_mfma_f32_16x16x32_bf16: lane holds channels 4*(lane>>4)+0..3 of pixel
   // lane&15) or MF = 32 (f32x16 of v_mfma_f32_32x32x16_bf16: register group g
   // holds channels 8g+4*(lane>>5)+0..3 of pixel lane&31). Caller must have
-  // retired all DMA.
+  // retired all DMA. has_acc = false (wave-uniform): the calling wave holds no
+  // accumulators (a loader wave of the warp-specialised kernel, conv_igemm_ws.hip) and
+  // only takes part in the bias / residual / store half.
   template <int MF, int FI, int FJ, int WTP, int WTC, class Acc>
   __device__ __forceinline__ void store(const DmlConvArgs& a, char* smem, Acc (&acc)[FI][FJ], int wp, int wc,
-                                        int lane, int tid) {
+                                        int lane, int tid, bool has_acc = true) {
     static_assert(MF == 16 || MF == 32, "MFMA fragment size");
     static_assert(PB % MF == 0, "an epilogue pass must hold whole pixel fragments");
     const int frow = lane & (MF - 1), fq = lane / MF;
@@ -150,6 +155,7 @@ struct Epilogue {
       __syncthreads();  // operand tiles (pass 0) / the previous pass's staging rows are free
 #pragma unroll
       for (int j = 0; j < FJ; ++j) {
+        if (!has_acc) break;                                       // wave-uniform
         if (P > 1 && (wp * WTP + j * MF) / PB != pass) continue;  // wave-uniform
         const int px = wp * WTP + j * MF + frow - pass * PB;
 #pragma unroll
@@ -170,6 +176,7 @@ struct Epilogue {
       __syncthreads();
 #pragma unroll
       for (int it = pass * (EIT / P); it < (pass + 1) * (EIT / P); ++it) {
+        if (XT && tid >= NT) break;  // a loader wave beyond the NT output threads (conv_igemm_ws.hip)
         const int px = (tid + it * NT) / CG;
         const int m = m0 + px;
         if (m >= M || !ch_ok) continue;

@@ -27,10 +27,11 @@
 // "issued - mark" (stores are buffer stores with out-of-range offsets for the
 // rows not stored, so every counted op really issues).
 //
-// Why not the r1 expand_reduce_kernel<512> (bottleneck_fused.hip): its
-// workgroups of 32 pixels re-read both weight matrices per 32 pixels straight
-// into VGPRs and ran phase-serialised at 1-2 waves/SIMD (123-138 us vs 75-90 us
-// for the two launches, per 128 images).
+// Why not the r1 expand_reduce_kernel<512> (bottleneck_fused.hip, removed in r5;
+// git history): its workgroups of 32 pixels re-read both weight matrices per 32
+// pixels straight into VGPRs and ran phase-serialised at 1-2 waves/SIMD (123-138 us
+// vs 75-90 us for the two launches, per 128 images). This file now serves every
+// block boundary the engine fuses (dml_expand_reduce == dml_chain).
 #include <cstdlib>
 
 #include "conv_shared.h"
@@ -431,11 +432,11 @@ static bool env_on(const char* name) {
   return e && e[0] == '1';
 }
 
-// 1 if the chained kernel serves this block boundary, else 0 (the caller falls back to the
-// phase-serialised kernels): with a shortcut, F = 64 / C = 256 (stage 2: ResNet50 b256 90.3-90.9k
-// vs 88.1-88.7k img/s with the r1 kernel, interleaved on one box, profiles/r3_v6; DML_CHAIN_C256=0:
-// the r1 kernel), F = 128 / C = 512 or F = 256 / C = 1024; merged projection shortcut (T = [x ; s],
-// K = 2F, no residual), F = 64 / C = 256 or F = 128 / C = 512
+// 1 if the chained kernel serves this block boundary, else 0 (the engine then keeps the two
+// 1x1 launches): with a shortcut, F = 64 / C = 256 (stage 2: ResNet50 b256 90.3-90.9k vs
+// 88.1-88.7k img/s with the r1 phase-serialised kernel, interleaved on one box, profiles/r3_v6),
+// F = 128 / C = 512 or F = 256 / C = 1024; merged projection shortcut (T = [x ; s], K = 2F, no
+// residual), F = 64 / C = 256 or F = 128 / C = 512
 extern "C" int dml_chain_supported(const DmlExpandReduceArgs* a) {
   const int C = a->C, F = C / 4, FZ = a->fz > 0 ? a->fz : F;
   const bool merged = a->res == nullptr;
@@ -450,9 +451,8 @@ extern "C" int dml_chain_supported(const DmlExpandReduceArgs* a) {
            a->ldy % 8 == 0 && a->ldy >= C && a->ldw1 % 8 == 0 && a->ldw1 >= C && a->ldz % 8 == 0 &&
            a->ldz >= FZ && (long)a->M * (a->ldr > a->ldy ? a->ldr : a->ldy) * 2 < 0x7ffffff0L;
   const long ld = a->ldx > a->ldr ? (a->ldx > a->ldy ? a->ldx : a->ldy) : (a->ldr > a->ldy ? a->ldr : a->ldy);
-  static const bool c256 = [] { const char* e = getenv("DML_CHAIN_C256"); return !(e && e[0] == '0'); }();
   const bool shape = merged ? ((F == 64 || F == 128) && a->kx == 2 * F)
-                            : ((F == 128 || F == 256 || (F == 64 && c256)) && (a->kx == 0 || a->kx == F));
+                            : ((F == 64 || F == 128 || F == 256) && (a->kx == 0 || a->kx == F));
   return shape && a->M >= 1 && a->ldx % 8 == 0 && a->ldx >= kx && a->ldw3 % 8 == 0 && a->ldw3 >= kx &&
          (merged || (a->ldr % 8 == 0 && a->ldr >= C)) && a->ldy % 8 == 0 && a->ldy >= C && a->ldw1 % 8 == 0 &&
          a->ldw1 >= C && a->ldz % 8 == 0 && a->ldz >= F && (long)a->M * ld * 2 < 0x7ffffff0L;
@@ -489,3 +489,15 @@ extern "C" int dml_chain(const DmlExpandReduceArgs* a, hipStream_t s) {
   DML_CHECK_LAUNCH();
   return 0;
 }
+
+// The block-boundary entry of the plan executor (the r1 phase-serialised kernels of
+// bottleneck_fused.hip were removed in r5; every shape the engine fuses runs chained).
+extern "C" int dml_expand_reduce(const DmlExpandReduceArgs* a, hipStream_t s) {
+  if (a->C != 256 && a->C != 512 && a->C != 1024) {
+    dml_set_error("dml_expand_reduce: unsupported shape (expand width must be 256 / 512 / 1024)");
+    return -1;
+  }
+  return dml_chain(a, s);
+}
+
+extern "C" int dml_expand_reduce_init(void) { return dml_chain_init(); }

@@ -101,8 +101,12 @@ int main() {
   CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
   CHECK(dml_conv_v2_bn(64) == 0 && dml_conv_v2_bn(68) == 0);   // the removed shifted-pixel ids
   CHECK(dml_conv(&a, 64, nullptr) != 0);
-  CHECK(dml_conv(&a, 80, nullptr) != 0);        // Winograd without transformed weights
-  CHECK(std::string(dml_last_error()).find("Winograd") != std::string::npos);
+  CHECK(dml_conv(&a, 80, nullptr) != 0);        // the removed Winograd ids
+  CHECK(dml_conv(&a, 113, nullptr) != 0);       // an unassigned warp-specialised id
+  CHECK(dml_conv(&a, 139, nullptr) != 0);       // an unassigned persistent id
+  CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
+  CHECK(dml_conv_v2_bn(100) == 128 && dml_conv_v2_bn(103) == 64 && dml_conv_v2_bn(120) == 64 &&
+        dml_conv_v2_bn(122) == 128);
   a = conv_args(64, 64, 3, 3);
   a.nseg = 5;
   CHECK(dml_conv(&a, 11, nullptr) != 0);        // too many output segments
@@ -189,34 +193,20 @@ int main() {
   er.ldr = 256; er.fz = 96; er.ldz = 128;
   er.res = (const void*)&er;                       // a shortcut (never dereferenced by the checks)
   CHECK(dml_chain_supported(&er) == 0);            // stage-end reduce width: 128 only
-  CHECK(dml_expand_reduce(&er, nullptr) != 0);    // ... and never the r1 kernel
+  CHECK(dml_expand_reduce(&er, nullptr) != 0);    // ... so dml_expand_reduce refuses it
   er.fz = 128;
   CHECK(dml_chain_supported(&er) == 1);            // 64 -> 256 (+ shortcut) -> 128
   er.ldz = 64;
   CHECK(dml_chain_supported(&er) == 0);            // Z rows narrower than the reduce width
   er.fz = 0; er.ldz = 64; er.res = nullptr;
-  {  // Winograd F(2x2, 3x3): the shape gate refuses what the kernel cannot run, dml_conv routes cfg 80
+  {  // tile-config ids: dml_conv refuses what no config serves
     DmlConvArgs w{};
     char buf[64];
     w.x = buf; w.y = buf; w.N = 2; w.H = w.W = 14; w.Cin = 64; w.ldx = 64; w.kh = w.kw = 3; w.sh = w.sw = 1;
     w.ph = w.pw = 1; w.Ho = w.Wo = 14; w.Cout = 64; w.ldy = 64; w.K = 576; w.Kpad = 576;
-    CHECK(dml_conv_wino_check(&w) != nullptr);                 // no transformed weights
-    w.wu = buf;
-    CHECK(dml_conv_wino_check(&w) == nullptr);
-    w.ph = w.pw = 0;
-    CHECK(dml_conv_wino_check(&w) != nullptr);                 // valid padding with a 'same' output size
-    w.Ho = w.Wo = 12;
-    CHECK(dml_conv_wino_check(&w) == nullptr);                 // valid 3x3
-    w.sh = w.sw = 2; w.Ho = w.Wo = 6;
-    CHECK(dml_conv_wino_check(&w) != nullptr);                 // stride 2
-    w.sh = w.sw = 1; w.Ho = w.Wo = 12; w.res = buf;
-    CHECK(dml_conv_wino_check(&w) != nullptr);                 // residual epilogue not supported
-    CHECK(dml_conv(&w, 80, nullptr) != 0);                     // dml_conv applies the same gate
-    CHECK(std::string(dml_last_error()).find("residual") != std::string::npos);
-    w.res = nullptr; w.Cin = 60; w.ldx = 60;
-    CHECK(dml_conv_wino_check(&w) != nullptr);                 // channels not a multiple of 8
-    CHECK(dml_conv_v2_bn(80) == 32 && dml_conv_v2_bn(81) == 64 && dml_conv_wino_supported(83) == 64);
-    CHECK(dml_conv_wino_supported(84) == 0);
+    CHECK(dml_conv(&w, 80, nullptr) != 0);                     // the removed Winograd ids are no config
+    CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
+    CHECK(dml_conv_v2_bn(80) == 0 && dml_conv_v2_bn(15) == 64 && dml_conv_v2_bn(9) == 0);
   }
   dml_set_error(nullptr);
   CHECK(std::string(dml_last_error()).empty());

@@ -25,11 +25,11 @@ ARCH = os.environ.get("DML_OFFLOAD_ARCH", "gfx950")
 SOURCES = [
     CSRC / "kernels" / "conv_dispatch.hip",
     CSRC / "kernels" / "conv_igemm_v2.hip",
+    CSRC / "kernels" / "conv_igemm_ws.hip",
+    CSRC / "kernels" / "conv_igemm_wsp.hip",
     CSRC / "kernels" / "misc.hip",
     CSRC / "kernels" / "stem_fused.hip",
     CSRC / "kernels" / "conv_pool.hip",
-    CSRC / "kernels" / "bottleneck_fused.hip",
-    CSRC / "kernels" / "conv_wino.hip",
     CSRC / "kernels" / "expand_reduce_chain.hip",
     CSRC / "runtime" / "runtime.hip",
 ]

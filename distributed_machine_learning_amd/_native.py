@@ -30,7 +30,6 @@ class ConvArgs(C.Structure):
         ("seg_y", C.c_void_p * 4),
         ("ksplit", C.c_int), ("split_ld", C.c_int),
         ("rsub", C.c_int), ("rW", C.c_int), ("rHW", C.c_int),
-        ("wu", C.c_void_p),   # Winograd F(2x2, 3x3) weights (cfg 80), ops.pack_wino_weight
     ]
 
 
@@ -113,7 +112,6 @@ _SIGS = {
     "dml_conv_group": (C.c_int, [C.POINTER(ConvGroupArgs), C.c_int, C.c_void_p]),
     "dml_plan_add_conv_group": (C.c_int, [C.c_void_p, C.POINTER(ConvGroupArgs), C.c_int]),
     "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),
-    "dml_conv_wino_check": (C.c_char_p, [C.POINTER(ConvArgs)]),
     "dml_conv_v2_bn": (C.c_int, [C.c_int]),
     "dml_conv_v2_init": (C.c_int, []),
     "dml_pool": (C.c_int, [C.POINTER(PoolArgs), C.c_void_p]),

@@ -100,6 +100,8 @@ class MsgType(IntEnum):
     PUT_MANY_REPLY = 77      # {"ok": [names], "failed": [names]}
     DOWNLOAD_MANY = 78       # leader -> replica: pull these (name, version)s from one outbox
     DOWNLOAD_MANY_REPLY = 79  # {"ok": {name: versions}, "failed": [names]}
+    FILES_STORED = 80        # writer -> leader: files it stored on their replicas itself (put_many_direct)
+    FILES_STORED_ACK = 81
     ERROR = 127
 
 

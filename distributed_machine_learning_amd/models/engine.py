@@ -125,7 +125,7 @@ class Engine:
         self.conv_pools = self._fusable_conv_pools(fuse_stem)
         self.conv_pool_1x1 = self._foldable_pool_1x1(fuse_stem)
         # ResNet block boundaries: expand (+ shortcut) and the next block's reduce as ONE
-        # kernel (csrc/kernels/bottleneck_fused.hip / expand_reduce_chain.hip)
+        # kernel (csrc/kernels/expand_reduce_chain.hip)
         self.exp_red = self._fusable_expand_reduce(fuse_blocks)
         # fused pairs whose Y is otherwise only read at stride 2 store just those pixels
         self.ysub = self._subsampled_y()
@@ -143,25 +143,15 @@ class Engine:
         self._tune_range = tune_range
         self.op_range: Optional[Tuple[int, int]] = None
         if share is not None:
-            self.wdev, self.wwino = share.wdev, share.wwino
+            self.wdev = share.wdev
         else:
             self._upload_weights(weights)
         self._alloc_buffers()
         self._build_plan()
 
     # ------------------------------------------------------------ weights ----
-    def _wino_eligible(self, n: Conv) -> bool:
-        """stride-1 undilated 3x3 with 'same' (1) or 'valid' (0) padding: a Winograd
-        F(2x2, 3x3) candidate (csrc/kernels/conv_wino.hip). DML_WINO=0: none (A/B)."""
-        return (os.environ.get("DML_WINO", "1") != "0" and n is not self.stem and n.kh == 3 and n.kw == 3
-                and n.sh == 1 and n.sw == 1 and n.ph == n.pw and n.ph in (0, 1) and n.cin % 8 == 0
-                and n.cout % 8 == 0 and not n.residual)
-
     def _upload_weights(self, w: Weights) -> None:
-        from ..ops import winograd
-
         self.wdev: Dict[str, Tuple[torch.Tensor, torch.Tensor, int, int, int]] = {}
-        self.wwino: Dict[str, torch.Tensor] = {}
         for n in self.g.nodes:
             if isinstance(n, Conv):
                 k, b = fold_conv(n, w)
@@ -193,11 +183,6 @@ class Engine:
                 wk = pack_conv_weight(k, cin_eff, coutp, kpad)
             else:
                 continue
-            if isinstance(n, Conv) and self._wino_eligible(n):
-                # Winograd F(2x2, 3x3) weights U = G g G^T (fp32, rounded once to bf16) for the
-                # conv_wino.hip candidate (cfg 80); the tuner picks per shape
-                self.wwino[n.name] = torch.from_numpy(winograd.pack_kernel(k)).to(
-                    self.device, torch.bfloat16).reshape(-1).contiguous()
             bias = np.zeros(coutp, np.float32)
             bias[: len(b)] = b
             self.wdev[n.name] = (
@@ -302,11 +287,9 @@ class Engine:
     def _fusable_expand_reduce(self, enabled: bool) -> Dict[str, Conv]:
         """{expand conv name: reduce conv} for adjacent node pairs expand (1x1 s1,
         F -> C, shortcut, ReLU) -> reduce (1x1 s1 reading the expand output, C -> F,
-        ReLU), F = C / 4 — ResNet50's convN_blockK_3 / convN_blockK+1_1. The kernel
-        supports C in {256, 512, 1024}; only C = 256 (stage 2) beats the two separate
-        launches (bottleneck_fused.hip header), so DML_FUSED_BLOCKS_MAXC defaults to 256.
-        The merged-shortcut form (K = 2F, no residual) is opt-in (DML_FUSED_MERGED_BLOCK=1):
-        150 us vs 74 + 55 us for the two launches (profiles/r1_v15)."""
+        ReLU), F = C / 4 — ResNet50's convN_blockK_3 / convN_blockK+1_1, run by the chained
+        kernel (expand_reduce_chain.hip) for C in {256, 512} (C = 1024 with DML_CHAIN=2: no
+        faster than its two launches), with the shortcut or merged (K = 2F, no residual)."""
         if not enabled or self.device.type != "cuda" or os.environ.get("DML_FUSED_BLOCKS") == "0":
             return {}
         maxc = int(os.environ.get("DML_FUSED_BLOCKS_MAXC", "256"))
@@ -318,13 +301,10 @@ class Engine:
                 continue
             # with its shortcut (K = F), or a merged projection shortcut (K = 2F, no residual; C = 256)
             shortcut = e.residual and e.res_sub == 1 and e.cin * 4 == e.cout
-            # merged: the chained kernel (C = 256 only: stage 3's entry has K = 3F; on by default,
-            # ResNet50 b256 91.2-91.3k vs 88.1-89.3k img/s interleaved on one box, profiles/r3_v9;
-            # DML_CHAIN_MERGED=0: off) or the r1 kernel (DML_FUSED_MERGED_BLOCK=1: measured slower)
+            # merged: the chained kernel (ResNet50 b256 91.2-91.3k vs 88.1-89.3k img/s interleaved on
+            # one box, profiles/r3_v9; DML_CHAIN_MERGED=0: off)
             chain_m = os.environ.get("DML_CHAIN_MERGED", "1") == "1"
-            merged = (e.residual is None and e.cin * 2 == e.cout
-                      and ((e.cout == 256 and (chain_m or os.environ.get("DML_FUSED_MERGED_BLOCK", "0") == "1"))
-                           or (e.cout == 512 and chain_m)))
+            merged = e.residual is None and e.cin * 2 == e.cout and e.cout in (256, 512) and chain_m
             # the chained-GEMM kernel (expand_reduce_chain.hip): the C = 512 boundaries (stage 3) by
             # default (ResNet50 b256 87.8-88.3k vs 85.4-86.1k img/s, profiles/r3_v3); DML_CHAIN=2 also
             # C = 1024 (stage 4: no faster than its two launches), DML_CHAIN=0 none
@@ -350,7 +330,7 @@ class Engine:
         stage 3's end (128 -> 512 -> 256 at 14x14, 16 pixels per wave: its 256 reduce accumulators;
         exact, neutral in the pipeline: 90.4-91.1k vs 90.5-90.9k img/s, profiles/r3_v11); 0: off."""
         if (not enabled or self.device.type != "cuda" or os.environ.get("DML_FUSED_BLOCKS") == "0"
-                or os.environ.get("DML_CHAIN_STAGE_END", "1") == "0" or os.environ.get("DML_ER_R1") == "1"):
+                or os.environ.get("DML_CHAIN_STAGE_END", "1") == "0"):
             return {}
         out: Dict[str, Conv] = {}
         nodes = self.g.nodes
@@ -749,8 +729,6 @@ class Engine:
         if n.residual and n.res_sub > 1 and n.residual not in self.ysub:  # strided shortcut (models/optimize.py)
             rh, rw, _ = g.shape(n.residual)
             a.rsub, a.rW, a.rHW = n.res_sub, rw, rh * rw
-        if n.name in self.wwino:
-            a.wu = self.wwino[n.name].data_ptr()
         return a
 
     # ---------------------------------------------------------------- run ----

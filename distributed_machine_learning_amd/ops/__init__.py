@@ -15,9 +15,7 @@ import torch
 from .. import _native as N
 
 __all__ = ["conv2d_nhwc", "conv_group", "pool3x3", "global_avgpool", "softmax_top5", "preprocess", "pack_weight",
-           "resnet_stem", "inception_stem", "conv3x3_pool", "expand_reduce", "pack_wino_weight", "WINO_CFG"]
-
-WINO_CFG = 80  # DML_WINO_CFG: the Winograd F(2x2, 3x3) kernel (csrc/kernels/conv_wino.hip)
+           "resnet_stem", "inception_stem", "conv3x3_pool", "expand_reduce"]
 
 
 def _r(x, m):
@@ -36,27 +34,16 @@ def pack_weight(w_oihw: torch.Tensor, cin_eff: Optional[int] = None) -> Tuple[to
     return out.to(torch.bfloat16), K, _r(K, 64)
 
 
-def pack_wino_weight(w_oihw: torch.Tensor) -> torch.Tensor:
-    """OIHW fp32 3x3 -> the Winograd F(2x2, 3x3) weights of conv_wino.hip: U = G g G^T
-    computed in fp32, rounded once to bf16, packed [Cout/64][Cin/32][16][4][64][8]
-    (ops/winograd.py)."""
-    from . import winograd
-
-    k = w_oihw.permute(2, 3, 1, 0).float().cpu().numpy()  # -> HWIO
-    return torch.from_numpy(winograd.pack_kernel(k)).to(torch.bfloat16).reshape(-1)
-
-
 def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cout: int, kh: int, kw: int,
                 stride=(1, 1), pad=(0, 0), relu: bool = False, residual: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, out_coff: int = 0, in_coff: int = 0, cin: Optional[int] = None,
                 out_f32: bool = False, cfg: int = -1, K: Optional[int] = None, dilation=(1, 1),
                 out_hw: Optional[Tuple[int, int]] = None, ksplit: int = 1,
-                defer: Optional[list] = None, wu: Optional[torch.Tensor] = None) -> torch.Tensor:
+                defer: Optional[list] = None) -> torch.Tensor:
     """x: NHWC bf16 [N,H,W,Cbuf] (Cbuf % 8 == 0). Returns/updates NHWC output.
     defer: a list to append the ConvArgs to instead of launching (conv_group).
     ksplit > 1 (fp32 output, v2 cfg): returns the [ksplit, N, Ho, Wo, C] split-K
-    partial sums (slice 0 carries the bias); their sum is the convolution.
-    wu: Winograd weights (pack_wino_weight, on the device) for cfg WINO_CFG."""
+    partial sums (slice 0 carries the bias); their sum is the convolution."""
     n, h, w_, cbuf = x.shape
     cin = cin if cin is not None else cbuf - in_coff
     ho = (h + 2 * pad[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
@@ -84,8 +71,6 @@ def conv2d_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, cou
                    dilation[0], dilation[1])
     if parts is not None:
         a.ksplit, a.split_ld = ksplit, out.numel()
-    if wu is not None:
-        a.wu = wu.data_ptr()
     if residual is not None and residual.shape[1] != ho:  # shortcut read at stride rs (full-res grid)
         rs = residual.shape[1] // ho
         assert residual.shape[1] == ho * rs and residual.shape[2] == wo * rs and residual.is_contiguous()
@@ -247,7 +232,7 @@ def conv3x3_pool(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor,
 
 def expand_reduce(x: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor, res: Optional[torch.Tensor],
                   w1: torch.Tensor, b1: torch.Tensor, c: Optional[int] = None, fz: int = 0):
-    """Fused ResNet block boundary (csrc/kernels/bottleneck_fused.hip), C = res channels,
+    """Fused ResNet block boundary (csrc/kernels/expand_reduce_chain.hip), C = res channels,
     F = C / 4: y = relu(1x1 conv F -> C of x + b3 + res), z = relu(1x1 conv C -> F of y + b1).
     x: bf16 [..., F]; res: bf16 [..., C], C in {256, 512, 1024}; w3 [>=C][>=F], w1 [>=F][>=C]
     packed (pack_weight). Returns (y, z) with x's leading shape.

@@ -23,9 +23,11 @@ from .. import _native as N
 
 V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33, 34, 36, 37,
            38, 39)  # 23..37: BK32; 38 / 39: 3-stage BK64 64-channel tiles (r3)
-# Winograd F(2x2, 3x3) (csrc/kernels/conv_wino.hip): a candidate of the stride-1 3x3
-# convs the engine gave transformed weights (ConvArgs.wu) and dml_conv_wino_check accepts
-WINO_CFG = 80
+# warp-specialised tiles (csrc/kernels/conv_igemm_ws.hip: loader waves + MFMA waves, r5)
+WS_CFGS = tuple(range(100, 113))
+# their persistent form (csrc/kernels/conv_igemm_wsp.hip: one operand ring over a workgroup's
+# whole tile list; no split-K)
+WSP_CFGS = tuple(range(120, 130))
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))
@@ -42,14 +44,12 @@ _lock = threading.Lock()
 CAND_TAG = os.environ.get("DML_TUNING_TAG", "c5cold")
 
 
-def shape_key(a: N.ConvArgs, wino: bool = True) -> str:
-    """Cache key of a conv shape (wino: mark the shapes timed with the Winograd
-    candidate; group keys leave it out, groups never use it)."""
+def shape_key(a: N.ConvArgs) -> str:
+    """Cache key of a conv shape."""
     return (f"n{a.N}_h{a.H}_w{a.W}_c{a.Cin}_ld{a.ldx}_k{a.kh}x{a.kw}_s{a.sh}x{a.sw}_p{a.ph}x{a.pw}"
             f"_o{a.Cout}_K{a.Kpad}_r{int(bool(a.res))}_f{a.out_f32}_d{max(a.dh, 1)}x{max(a.dw, 1)}"
             + (f"_ks{a.ksplit}" if a.ksplit > 1 else "")
             + (f"_rs{a.rsub}" if a.rsub > 1 else "")
-            + ("_wg1" if wino and wino_ok(a) else "")
             + "_" + CAND_TAG)
 
 
@@ -84,22 +84,22 @@ def _excluded() -> set:
     return {int(c) for c in v.split(",") if c.strip()}
 
 
-def wino_ok(a: N.ConvArgs) -> bool:
-    """Conv ``a`` can run on the Winograd kernel: it carries transformed weights and
-    passes the library's host-side shape gate (never a device call)."""
-    if not a.wu or a.kh != 3 or a.kw != 3 or a.sh != 1 or a.sw != 1:
-        return False
-    return N.lib().dml_conv_wino_check(C.byref(a)) is None
-
-
 def valid_cfgs(a: N.ConvArgs) -> List[int]:
     if a.Cout % 8 or a.Cin % 8 or a.ldx % 8 or a.ldy % 8:
         return []
     ex = _excluded()
     cands = [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)] + (list(LATE_RES_CFGS) if a.res else [])
-    if wino_ok(a):
-        cands.append(WINO_CFG)
+    cands += list(WS_CFGS) + ([] if a.ksplit > 1 else list(WSP_CFGS))
     return [c for c in cands if c not in ex]
+
+
+def _added() -> List[int]:
+    """DML_TUNE_ADD=<cfg,...>: configs new to the table. A cached shape re-times its cached
+    config against these (cold, same method) and switches only when one is >= 3 % faster,
+    so the pipeline-co-tuned entries (tools/cotune_pipe.py) stay unless a new kernel clearly
+    beats them alone."""
+    v = os.environ.get("DML_TUNE_ADD", "")
+    return [int(c) for c in v.split(",") if c.strip()]
 
 
 _scrub = None
@@ -153,10 +153,30 @@ def autotune(args: Iterable[N.ConvArgs], cache: Optional[Dict[str, int]] = None,
     args = list(args)
     cache = dict(load_cache() if cache is None else cache)
     new: Dict[str, int] = {}
+    added = _added()
     for a in args:
         k = shape_key(a)
-        if k in new or (k in cache and cache[k] in valid_cfgs(a)):
-            continue  # a cached cfg that is no longer a candidate (removed / excluded) is re-timed
+        if k in new:
+            continue
+        if k in cache and cache[k] in valid_cfgs(a):
+            adds = [c for c in added if c in valid_cfgs(a) and c != cache[k]]
+            if not adds:
+                continue  # a cached cfg that is no longer a candidate (removed / excluded) is re-timed
+            try:
+                cur = time_cfg(a, cache[k])
+            except N.NativeError:
+                cur = float("inf")
+            best = (cur, cache[k])
+            for cfg in adds:
+                try:
+                    t = time_cfg(a, cfg)
+                except N.NativeError:
+                    continue
+                if t < 0.97 * best[0]:
+                    best = (t, cfg)
+            if best[1] != cache[k]:
+                new[k] = best[1]
+            continue
         best: Tuple[float, int] = (float("inf"), -1)
         for cfg in valid_cfgs(a):
             try:
@@ -189,7 +209,7 @@ GROUP_TAG = os.environ.get("DML_GROUP_TAG", "grp4")
 
 
 def group_key(args: List[N.ConvArgs], pools: Sequence[N.PoolArgs] = ()) -> str:
-    return (GROUP_TAG + "_" + "|".join([shape_key(a, False)[:-len(CAND_TAG) - 1] for a in args] + [pool_key(p) for p in pools])
+    return (GROUP_TAG + "_" + "|".join([shape_key(a)[:-len(CAND_TAG) - 1] for a in args] + [pool_key(p) for p in pools])
             + "_" + CAND_TAG)
 
 
@@ -238,8 +258,6 @@ def autotune_group(args: List[N.ConvArgs], cfgs: List[int], pools: Sequence[N.Po
     grid, or -1 when running them one after another, each conv on its own tuned
     tile ``cfgs``, is faster."""
     k = group_key(args, pools)
-    if any(c == WINO_CFG for c in cfgs):  # the sequential alternative has a Winograd member: re-decide
-        k += "_wg1"
     cache = load_cache() if cache is None else cache
     if k in cache and (cache[k] == -1 or cache[k] in GROUP_CFGS):  # -1: grouping measured slower; a removed tile is re-timed
         return cache[k]

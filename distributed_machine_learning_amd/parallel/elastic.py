@@ -97,6 +97,31 @@ class ShmExchange:
             self.h = None
 
 
+def shm_tag(store_path: str) -> str:
+    """The per-rendezvous prefix of the shared-memory segment names (/dev/shm/dml_<tag>_...)."""
+    return hashlib.sha1(os.path.abspath(store_path).encode()).hexdigest()[:12]
+
+
+def unlink_stale_segments(store_path: str) -> int:
+    """Remove every shared-memory exchange segment of a rendezvous path (the launcher calls
+    this when it (re)creates the path: segments of a killed previous run never unlinked
+    themselves). Returns how many were removed."""
+    pre = f"dml_{shm_tag(store_path)}_"
+    n = 0
+    try:
+        names = os.listdir("/dev/shm")
+    except OSError:
+        return 0
+    for f in names:
+        if f.startswith(pre):
+            try:
+                os.unlink(os.path.join("/dev/shm", f))
+                n += 1
+            except OSError:
+                pass
+    return n
+
+
 def default_store_path(tag: str) -> str:
     base = os.environ.get("DML_RDZV_DIR", "/tmp")
     return os.path.join(base, f"dml_rdzv_{tag}")
@@ -137,11 +162,20 @@ class ElasticGroup:
         self.shm_exchange = shm_exchange and store_host is None
         self._shm: Optional[ShmExchange] = None
         self._shm_names: List[str] = []
-        # the same name in every rank process (str hash() is salted per process)
-        self._shm_tag = hashlib.sha1(os.path.abspath(store_path or "").encode()).hexdigest()[:12]
+        # the same name in every rank process (str hash() is salted per process) AND unique per
+        # job: a rank that was SIGKILLed never unlinks its segments, so a relaunch over a reused
+        # --rdzv path would otherwise open the old segment, whose per-rank step counters are
+        # still high, and apply the previous run's records as this step's. The
+        # first rank to reach the store fixes a random nonce (compare_set); every other rank
+        # and every later joiner of this store reads that one.
+        self._shm_tag = shm_tag(store_path or "") + "_" + self._job_nonce()
         if join:
             self._await_admission(join_timeout_s)
         self._init_pg()
+
+    def _job_nonce(self) -> str:
+        mine = os.urandom(6).hex()
+        return self.store.compare_set("shm_nonce", "", mine).decode()
 
     # --------------------------------------------------------------- group --
     @property
@@ -187,9 +221,15 @@ class ElasticGroup:
             # fails at once instead of holding destroy_process_group for the timeout)
             # the aborted groups stay referenced: the last reference dropping inside the abort
             # would run the gloo group's destructor there, which joins its worker threads
-            # behind ops of the failed epoch (observed: minutes inside the abort)
-            self._graveyard.extend(c10d._world.pg_map.keys())
+            # behind ops of the failed epoch (observed: minutes inside the abort). Only the
+            # last aborted epoch's groups are kept: the ones before it were released at the
+            # previous abort's end, once no op of theirs could still be queued (their epoch's
+            # successor ran whole steps since), so kills and rejoins do not accumulate gloo
+            # threads / sockets / RCCL communicators over a long-running service
+            old = self._graveyard
+            self._graveyard = list(c10d._world.pg_map.keys())
             c10d._abort_process_group()
+            del old
             self.aborts += 1
             return  # the abort destroyed the default group
         try:

@@ -214,6 +214,52 @@ class FakeRankBackend(HostRankBackend):
         super().__init__(FakeBackend(), loader=loader, cap=cap, delay_per_image=delay_per_image)
 
 
+class _Deadline:
+    """A launch 'event' that fires at a given monotonic time (PacedRankBackend)."""
+
+    def __init__(self, t: float):
+        self.t = t
+
+    def query(self) -> bool:
+        return time.monotonic() >= self.t
+
+    def synchronize(self) -> None:
+        d = self.t - time.monotonic()
+        if d > 0:
+            time.sleep(d)
+
+
+class PacedRankBackend(RankBackend):
+    """A GPU stand-in for host-path capacity runs (tools/store_capacity.py): batches
+    complete at a fixed rate per rank (``batches_per_s``, serialised like one GPU's
+    stream, SLOTS in flight) and their rows come from a precomputed random top-5 table,
+    so everything measured is the host side: control exchange, result rendering and the
+    replicated output store. Synthetic image names only."""
+
+    slots = SLOTS
+
+    def __init__(self, cap: int = 256, batches_per_s: float = 370.0, seed: int = 0):
+        self.cap, self.dt = cap, 1.0 / batches_per_s
+        g = np.random.default_rng(seed)
+        self.ids = g.integers(0, 1000, size=(4096, 5), dtype=np.int32)
+        p = np.sort(g.random((4096, 5), dtype=np.float32), axis=1)[:, ::-1]
+        self.p = np.ascontiguousarray(p / p.sum(1, keepdims=True)).view(np.int32)
+        self.busy_until = 0.0
+        self.launched = 0
+
+    def launch(self, model, names, slot):
+        if len(names) > self.cap:
+            raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
+        k = len(names)
+        i0 = (self.launched * 131) % (4096 - self.cap)
+        out = torch.zeros((2, self.cap, 5), dtype=torch.int32)
+        out[0, :k] = torch.from_numpy(self.ids[i0:i0 + k])
+        out[1, :k] = torch.from_numpy(self.p[i0:i0 + k])
+        self.busy_until = max(time.monotonic(), self.busy_until) + self.dt
+        self.launched += 1
+        return out, _Deadline(self.busy_until)
+
+
 class StoreRankBackend(_ArenaStaging, RankBackend):
     """CPU stand-in of GpuRankBackend's data path for multi-rank tests: the same
     window-staged image store (parallel/image_store.py, on a CPU device, all-gather
@@ -322,8 +368,11 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             b = batch_sizes[m]
             if b > self.cap:
                 raise ValueError(f"{m}: engine batch {b} exceeds the result capacity {self.cap}")
-            arena = HbmImageStore(max(arena_images, n_synth + 2 * self.cap), g.input_hw, device,
+            # arena_images counts the slots windows can use: the seeded synthetic images come on
+            # top (plan() never hands those out), so the staging room is what the caller sized
+            arena = HbmImageStore(n_synth + max(arena_images, 2 * self.cap), g.input_hw, device,
                                   n_synth=n_synth, seed=1000 + MODEL_IDS[m])
+            assert arena.capacity - arena.n_synth >= arena_images
             self.arenas[m] = arena
             self._adopt(m, arena)
             self.idx[m] = [torch.zeros(b, dtype=torch.int32).pin_memory() for _ in range(SLOTS)]

@@ -40,6 +40,15 @@ class RankControl:
         self.period, self.ping_timeout, self.suspect_timeout = period, ping_timeout, suspect_timeout
         self.on_dead, self.on_alive, self.rejoin = on_dead, on_alive, rejoin
         self.svc = None  # the CollectiveService it serves
+        self.put_lat: List[float] = []  # output bundle PUT latencies (call -> every replica stored), s
+        # output bundles spooled once for same-machine replicas (hard links, store/service.py);
+        # DML_SPOOL_OUTPUTS=0: every replica pulls over the blob plane (A/B)
+        import os
+
+        self.spool_outputs = os.environ.get("DML_SPOOL_OUTPUTS", "1") != "0"
+        # outputs are PUT leaderless (store.service.put_many_direct: the writer fans out to the
+        # replicas, one FILES_STORED message to the leader); DML_DIRECT_PUTS=0: through the leader
+        self.direct_puts = os.environ.get("DML_DIRECT_PUTS", "1") != "0"
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self.node = None
         self.ready = threading.Event()
@@ -210,15 +219,29 @@ class RankControl:
         """PUT a bundle of files (store.service.put_many: one leader round trip) without
         blocking the caller; files the store refused are retried (a store-leader change
         mid-PUT; each attempt bounded by ``attempt_s``) until ``deadline_s``.
-        ``done(stored, failed)`` runs on the control loop."""
+        ``done(stored, failed)`` runs on the control loop. The bundle is first written
+        once into a spool directory by the CALLING thread (the output writer), so the
+        replicas on this machine hard-link it (store/service.py) and no byte of it crosses
+        the control loop; a spool failure falls back to the blob plane."""
+        import shutil
+
+        spool = None
+        if self.spool_outputs:
+            try:
+                spool = self.node.store.spool(items)
+            except OSError as e:
+                log.warning("rank %d: output spool failed (%s); replicas pull over the blob plane", self.grank, e)
+
+        t_call = time.monotonic()
+
         async def go():
             remaining = dict(items)
             stored: List[str] = []
             t0, err = time.monotonic(), ""
             while remaining and time.monotonic() - t0 < deadline_s:
                 try:  # one attempt is bounded: a leader that died mid-PUT must not eat the deadline
-                    ok, _, err = await asyncio.wait_for(self.node.store.put_many(list(remaining.items())),
-                                                        attempt_s)
+                    put = self.node.store.put_many_direct if self.direct_puts else self.node.store.put_many
+                    ok, _, err = await asyncio.wait_for(put(list(remaining.items()), spool=spool), attempt_s)
                 except Exception as e:  # leader unreachable mid-failover
                     ok, err = [], str(e)
                 for n in ok:
@@ -228,6 +251,9 @@ class RankControl:
                     await asyncio.sleep(0.1)
             if remaining:
                 log.error("rank %d: store put of %d files failed: %s", self.grank, len(remaining), err)
+            if spool is not None:  # every replica linked its copy (or pulled it): the spool entries go
+                self.loop.run_in_executor(None, shutil.rmtree, spool, True)
+            self.put_lat.append(time.monotonic() - t_call)
             try:
                 done(stored, list(remaining))
             except Exception:

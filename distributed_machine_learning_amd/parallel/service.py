@@ -328,12 +328,17 @@ class ReplicatedCoordinator:
         return out
 
 
+STAGE_DEPTH = 8  # batches per rank whose images are staged ahead of dispatch (image windows)
+
+
 def auto_depth(world: int) -> int:
     """Batches in flight per rank (launched, queued, or awaiting their output PUT): 4 on one
-    GPU (measured r4, 1 x MI355X, outputs PUT, tools/gpu_svc_depth.sh: depth 4 / 8 -> 71.6k /
-    71.1k images/s at p50 10.9 / 21.9 ms for ResNet50), 8 with peers (a PUT then replicates
-    over TCP to other ranks, so more batches wait on it)."""
-    return 4 if world <= 1 else 8
+    GPU (measured r4, 1 x MI355X, outputs PUT, depth 4 / 8 -> 71.6k / 71.1k images/s at p50
+    10.9 / 21.9 ms for ResNet50), 16 with peers: a PUT then replicates to R ranks and the
+    step is lockstep over the group, so more batches wait on their output (r5,
+    tools/store_capacity.py at world 8 on 8 shared cores: depth 8 / 32 -> 259 / 503 batches/s).
+    The image staging look-ahead stays at STAGE_DEPTH batches per rank whatever the depth."""
+    return 4 if world <= 1 else 16
 
 
 # ---------------------------------------------------------- output writer ----
@@ -542,7 +547,9 @@ class CollectiveService:
         self.unsynced: set = {eg.grank} if rejoined else set()
         if rejoined:
             self.unsynced |= set(eg.members) - set(eg.prev_members)
-        self.stage_ahead = max(1, eg.world) * coord.depth  # queued batches staged ahead of dispatch
+        # queued batches staged ahead of dispatch (the in-flight ones are staged besides)
+        self.stage_ahead = max(1, eg.world) * min(coord.depth, STAGE_DEPTH)
+        self._rec_bufs: Dict[tuple, torch.Tensor] = {}   # the step's exchange output, per (world, L)
         self.last_progress = time.monotonic()
         self.phase_s: Dict[str, float] = {"poll": 0.0, "plan": 0.0, "collective": 0.0, "apply": 0.0,
                                           "launch": 0.0, "sleep": 0.0}
@@ -694,7 +701,9 @@ class CollectiveService:
         ph["plan"] += t2 - t1
         # ---- the step's collective (+ the log bytes, rarely) ----
         rec_t = torch.from_numpy(rec).to(self.dev)
-        out = torch.empty((world, L), dtype=torch.int64, device=self.dev)
+        out = self._rec_bufs.get((world, L))
+        if out is None:  # one buffer per group shape: no allocation per step
+            out = self._rec_bufs[(world, L)] = torch.empty((world, L), dtype=torch.int64, device=self.dev)
         applied_here: List[dict] = []
         try:
             if world == 1:  # nothing to exchange: a collective would only hand the GIL around
@@ -844,7 +853,7 @@ class CollectiveService:
         # ranks new in this epoch (re-joined) and ranks still waiting for their first state
         # stay out of the coordinator role until the next state record
         self.unsynced = (self.unsynced & set(self.eg.members)) | (set(self.eg.members) - set(self.eg.prev_members))
-        self.stage_ahead = self.eg.world * self.coord.depth
+        self.stage_ahead = self.eg.world * min(self.coord.depth, STAGE_DEPTH)
         # image windows: every rank forgets its staging at this same boundary and stages
         # afresh over the new group (a joiner's arena is empty; survivors' collectives of
         # the failed epoch were aborted)

@@ -22,6 +22,16 @@ import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
 
+def _pcts(xs) -> dict:
+    import numpy as np
+
+    if not xs:
+        return {}
+    a = np.asarray(xs) * 1e3
+    return {"p50": round(float(np.percentile(a, 50)), 2), "p90": round(float(np.percentile(a, 90)), 2),
+            "max": round(float(a.max()), 2), "n": len(xs)}
+
+
 def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images: int, inception_images: int,
         batch_sizes: Dict[str, int], out_dir: Optional[str], kills: Sequence[Tuple[int, int]] = (),
         comm: str = "gloo", depth: int = 0, single_rates: Optional[Dict[str, float]] = None,
@@ -121,6 +131,7 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                             "in_store": len(set(listing)), "distinct_batches_in_store": len(pairs),
                             "listing_duplicates": len(listing) - len(set(listing)),
                             "put_bundles_coordinator": writer.bundles,
+                            "put_latency_ms_coordinator": _pcts(ctl.put_lat),
                             "writer_busy_s_coordinator": round(writer.busy_s, 3)},
                 "steps": steps, "max_batches_per_step": svc.batches_per_step_max,
                 "rebuilds": svc.rebuilds, "preempted_batches": coord.preempted, "requeued_batches": coord.requeued,

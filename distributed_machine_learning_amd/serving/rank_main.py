@@ -62,7 +62,7 @@ def add_args(ap: argparse.ArgumentParser) -> None:
                         "(0: service.auto_depth: 4 on one GPU, 8 with peers)")
     g.add_argument("--replication", type=int, default=4)
     g.add_argument("--arena-images", type=int, default=0,
-                   help="HBM image store capacity per model (0: 2 x ranks x depth x batch, at least 8192)")
+                   help="HBM image store slots per model beyond the synthetic ones (0: ranks x (depth + staged) x batch, at least 8192)")
     g.add_argument("--no-preempt", action="store_true")
 
 
@@ -94,6 +94,8 @@ def launch(a: argparse.Namespace, argv) -> int:
                                   f"dml_rdzv_rank_{os.getpid()}_{int(time.time() * 1e6)}")
     if os.path.exists(rdzv):
         os.remove(rdzv)  # a FileStore never deletes its file: never reuse one (stale epochs / admissions)
+    from ..parallel.elastic import unlink_stale_segments
+    unlink_stale_segments(rdzv)  # shared-memory segments a killed previous run over this path left
     procs = []
     for r in range(a.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus))
@@ -119,6 +121,16 @@ def rank_main(a: argparse.Namespace) -> int:
     if "backend" not in getattr(a, "explicit", ()):
         a.backend = "gpu"  # the product default of a rank: its GPU
     logging.basicConfig(level=logging.WARNING, format=f"%(asctime)s rank{grank} %(levelname)s %(name)s: %(message)s")
+    from ..utils import numa
+
+    # NUMA-local placement before any GPU call (utils/numa.py): the serve loop, the decode
+    # pool, the output writer and the pinned arenas they first-touch on the GPU's socket
+    local = grank % max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+    placement = numa.bind_local_rank(local) if a.backend == "gpu" else {"bound": False}
+    if placement.get("bound"):
+        logging.getLogger(__name__).info("rank %d bound to NUMA node %s cpus %s", grank, placement["numa"],
+                                         placement["cpus"])
+    decode_threads = numa.host_threads(share=numa.ranks_sharing(local, world)) if placement.get("bound") else 8
     import torch
 
     from ..parallel.elastic import ElasticGroup
@@ -151,10 +163,19 @@ def rank_main(a: argparse.Namespace) -> int:
     from ..parallel.service import auto_depth
 
     depth = a.depth or auto_depth(world)
-    # the image windows stage world x depth batches ahead of dispatch: room for twice that
-    arena = a.arena_images or max(8192, 2 * world * depth * cap)
+    # the image windows stage world x min(depth, STAGE_DEPTH) batches ahead of dispatch while
+    # world x depth are in flight (pinned): the usable arena (beyond the backend's synthetic
+    # images) holds both
+    from ..parallel.service import STAGE_DEPTH
+
+    need = world * (depth + min(depth, STAGE_DEPTH)) * cap
+    if a.arena_images and a.arena_images < need:
+        raise SystemExit(f"--arena-images {a.arena_images} < {need} = ranks x (depth + staged) x batch: "
+                         "staged-ahead batches would wait behind pinned in-flight ones")
+    arena = a.arena_images or max(8192, need)
     backend = {
-        "gpu": lambda: GpuRankBackend(dev, bs, cap=cap, arena_images=arena, loader=ctl.store_loader),
+        "gpu": lambda: GpuRankBackend(dev, bs, cap=cap, arena_images=arena, loader=ctl.store_loader,
+                                      decode_threads=decode_threads),
         "fake": lambda: FakeRankBackend(cap=cap, loader=ctl.store_loader),
         "store": lambda: StoreRankBackend(cap=cap, loader=ctl.store_loader),
         "cpu": lambda: HostRankBackend(CpuBackend(), cap=cap, loader=ctl.store_loader),

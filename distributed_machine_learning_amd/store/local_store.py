@@ -62,6 +62,35 @@ class LocalFileStore:
                     pass
             return v
 
+    def put_link(self, name: str, src_path: str, version: Optional[int] = None) -> int:
+        """Store ``src_path`` (a file on this filesystem) as a version of ``name`` by a
+        hard link: the same-node replica path of a bundle PUT (store/service.py) — the
+        bytes were written once by the client into its spool, every replica on the node
+        adds a directory entry of its own, and the file lives while any replica keeps it.
+        The store never rewrites a file in place (new versions are new files), so
+        replicas sharing an inode never see each other's changes."""
+        with self._lock:
+            vers = self.index.setdefault(name, [])
+            v = version if version is not None else (vers[-1] + 1 if vers else 1)
+            path = self._path(name, v)
+            tmp = path + ".lnk"
+            try:
+                os.remove(tmp)
+            except FileNotFoundError:
+                pass
+            os.link(src_path, tmp)
+            os.replace(tmp, path)
+            if v not in vers:
+                vers.append(v)
+                vers.sort()
+            while len(vers) > self.max_versions:
+                old = vers.pop(0)
+                try:
+                    os.remove(self._path(name, old))
+                except FileNotFoundError:
+                    pass
+            return v
+
     def put_file(self, name: str, src_path: str) -> int:
         with open(src_path, "rb") as f:
             return self.put_bytes(name, f.read())

@@ -16,6 +16,10 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
+import shutil
+import socket
+import uuid
 from typing import Callable, Dict, List, Optional, Tuple
 
 from ..cluster.frames import Frame, MsgType
@@ -28,6 +32,20 @@ from .metadata import FAILED, SUCCESS, StoreMetadata
 log = logging.getLogger(__name__)
 
 
+def _host_id() -> str:
+    """This machine's identity for the same-node fast path (hostname + kernel boot id):
+    a spool path is only ever linked by a replica that sees the same filesystem."""
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    return f"{socket.gethostname()}/{boot}"
+
+
+HOST_ID = _host_id()
+
+
 class StoreService:
     def __init__(self, ep: Endpoint, ml: MembershipList, local: LocalFileStore, source: BlobSource, blobs,
                  leader_fn: Callable[[], Optional[str]], replication: int = 4, timeout: float = 10.0,
@@ -37,6 +55,12 @@ class StoreService:
         self.meta = StoreMetadata(replication)
         self.timeout = timeout
         self.storage_role = storage_role or (lambda n: True)
+        # same-node bundle PUTs (put_many with a spool): the client writes each file once
+        # into spool_root/<token>/, every replica on this machine hard-links it into its own
+        # versioned store; replicas elsewhere pull it over the blob plane as before
+        self.spool_root = os.path.join(os.path.dirname(os.path.abspath(local.root)), ".spool")
+        self.linked = 0
+        self.pulled = 0
         on = ep.on
         # leader-side
         on(MsgType.PUT_REQUEST, self._l_put)
@@ -46,6 +70,7 @@ class StoreService:
         on(MsgType.GET_FILE_REQUEST, self._l_get)
         on(MsgType.GET_FILE_NAMES_REQUEST, self._l_ls_all)
         on(MsgType.ALL_LOCAL_FILES, self._l_all_local_files)
+        on(MsgType.FILES_STORED, self._l_files_stored)
         # replica-side
         on(MsgType.DOWNLOAD_FILE, self._r_download)
         on(MsgType.DOWNLOAD_MANY, self._r_download_many)
@@ -87,24 +112,105 @@ class StoreService:
             return False, "leader unreachable"
         return r.type == MsgType.PUT_REQUEST_SUCCESS, r.payload.get("error", "")
 
-    async def put_many(self, items: List[Tuple[str, bytes]]) -> Tuple[List[str], List[str], str]:
+    def spool(self, items: List[Tuple[str, bytes]]) -> str:
+        """(any thread) Write a bundle's files once into a fresh spool directory on this
+        machine's filesystem; put_many(spool=...) then lets same-node replicas hard-link
+        them instead of pulling the bytes over TCP. Returns the directory."""
+        d = os.path.join(self.spool_root, uuid.uuid4().hex)
+        os.makedirs(d)
+        for name, data in items:
+            if "/" in name or name.startswith(".."):
+                raise ValueError(f"bad sdfs name {name!r}")
+            with open(os.path.join(d, name), "wb") as f:
+                f.write(data)
+        return d
+
+    async def put_many(self, items: List[Tuple[str, bytes]], spool: Optional[str] = None
+                       ) -> Tuple[List[str], List[str], str]:
         """PUT several files in ONE leader round trip (the service's output bundles):
         the leader sends each replica one DOWNLOAD_MANY for all its files of the
-        bundle, which it pulls in one blob request. Returns (stored, failed, error);
-        every file is stored on all of its replicas or reported failed (W = all)."""
+        bundle, which it pulls in one blob request — or, when the bundle was spooled on
+        this machine (``spool``, from :meth:`spool`) and the replica runs here too, links
+        from the spool. Returns (stored, failed, error); every file is stored on all of
+        its replicas or reported failed (W = all)."""
         box = dict(items)
         tok = self.source.stage(box)
         me = self.ml.get(self.me)
         blob = me.meta.get("blob") if me is not None else None
+        req = {"files": list(box), "token": tok, "blob": blob}
+        if spool is not None:
+            req.update(spool=spool, host=HOST_ID)
         try:
-            r = await self._leader_request(MsgType.PUT_MANY_REQUEST,
-                                           {"files": list(box), "token": tok, "blob": blob},
-                                           timeout=self.timeout * 3)
+            r = await self._leader_request(MsgType.PUT_MANY_REQUEST, req, timeout=self.timeout * 3)
         finally:
             self.source.unstage(tok)
         if r is None:
             return [], list(box), "leader unreachable"
         return list(r.payload.get("ok", [])), list(r.payload.get("failed", [])), r.payload.get("error", "")
+
+    async def put_many_direct(self, items: List[Tuple[str, bytes]], spool: Optional[str] = None
+                              ) -> Tuple[List[str], List[str], str]:
+        """Leaderless bundle PUT for files whose names no other writer uses at the same time
+        (the collective service's outputs: one name per (job, batch), r5). The writer places
+        each file itself (the same deterministic ring as the leader, over its own view of the
+        alive storage nodes), sends each replica node one DOWNLOAD_MANY for all of its files
+        (hard links from the spool on this machine, else one blob pull), substitutes a replica
+        that dies mid-PUT, and tells the leader what landed where in ONE FILES_STORED message.
+        The leader's event loop, which serves every rank's bundles, then handles one small
+        message per bundle instead of a fan-out (measured at world 8: PUT p50 133 ms through
+        the leader). Versions are assigned by each replica (the next one it holds: a re-run
+        of a batch becomes a new version). W = all: a file is stored once every one of its
+        targets stored it. Returns (stored, failed, error)."""
+        box = dict(items)
+        alive = self.storage_nodes()
+        if not alive:
+            return [], list(box), "no storage nodes"
+        tok = self.source.stage(box)
+        me = self.ml.get(self.me)
+        src = {"source": self.me, "token": tok, "source_blob": me.meta.get("blob") if me is not None else None}
+        if spool is not None:
+            src.update(spool=spool, host=HOST_ID)
+        stored_on: Dict[str, Dict[str, List[int]]] = {n: {} for n in box}
+        tried: Dict[str, set] = {}
+        pending: Dict[str, List[str]] = {}
+        for n in box:
+            t = self.meta.place(n, alive)
+            tried[n] = set(t)
+            for x in t:
+                pending.setdefault(x, []).append(n)
+        bad: set = set()
+        try:
+            while pending:
+                nodes = sorted(pending)
+                rs = await asyncio.gather(*(self._request_unless_dead(
+                    t, MsgType.DOWNLOAD_MANY, {"files": [[n, 0] for n in pending[t]], **src}) for t in nodes))
+                nxt: Dict[str, List[str]] = {}
+                for t, r in zip(nodes, rs):
+                    got = r.payload.get("ok", {}) if r is not None else {}
+                    dead = r is None and not self.ml.is_alive(t)
+                    for n in pending[t]:
+                        if n in got:
+                            stored_on[n][t] = list(got[n])
+                            continue
+                        subs = [x for x in self.meta.place(n, self.storage_nodes(), 64) if x not in tried[n]] \
+                            if dead else []
+                        if subs:  # the replica died mid-PUT: another node takes this file
+                            tried[n].add(subs[0])
+                            nxt.setdefault(subs[0], []).append(n)
+                        else:
+                            bad.add(n)
+                pending = nxt
+        finally:
+            self.source.unstage(tok)
+        ok = [n for n in box if n not in bad and stored_on[n]]
+        failed = [n for n in box if n not in ok]
+        if ok:
+            per_node: Dict[str, Dict[str, List[int]]] = {}
+            for n in ok:
+                for node, vers in stored_on[n].items():
+                    per_node.setdefault(node, {})[n] = vers
+            await self._leader_request(MsgType.FILES_STORED, {"files": per_node})  # None: a new leader adopts
+        return ok, failed, "" if not failed else "replica failed"
 
     async def put_file(self, path: str, name: str) -> Tuple[bool, str]:
         with open(path, "rb") as f:
@@ -252,6 +358,8 @@ class StoreService:
         for n, t in todo.items():
             self.meta.begin(n, t)
         src = {"source": fr.sender, "token": fr.payload.get("token"), "source_blob": fr.payload.get("blob")}
+        if fr.payload.get("spool"):
+            src.update(spool=fr.payload["spool"], host=fr.payload.get("host"))
         tried = {n: set(t) for n, t in todo.items()}
         pending = {n: list(t) for n, t in todo.items()}
         while pending:
@@ -323,6 +431,12 @@ class StoreService:
 
     async def _l_all_local_files(self, fr: Frame) -> None:
         self._learn(fr.sender, fr.payload.get("all_files", {}))
+
+    async def _l_files_stored(self, fr: Frame) -> None:
+        """A writer stored files on their replicas itself (put_many_direct): record them."""
+        for node, files in fr.payload.get("files", {}).items():
+            self._learn_delta(node, {"files": files})
+        await self.ep.reply(fr, MsgType.FILES_STORED_ACK, {})
 
     def _learn_delta(self, node: str, payload: dict) -> None:
         """A replica's reply names only the files it just touched ("files": name ->
@@ -404,22 +518,43 @@ class StoreService:
     def _delta(self, name: str) -> Dict[str, List[int]]:
         return {name: self.local.versions(name)}
 
+    def _link_from_spool(self, spool: str, files: List[Tuple[str, int]]) -> Dict[str, List[int]]:
+        ok: Dict[str, List[int]] = {}
+        for n, v in files:
+            self.local.put_link(n, os.path.join(spool, n), version=v)
+            ok[n] = self.local.versions(n)
+        return ok
+
     async def _r_download_many(self, fr: Frame) -> None:
         p = fr.payload
-        files = [(n, int(v)) for n, v in p.get("files", [])]
+        # version 0 (put_many_direct): this replica assigns the next version of the name
+        files = [(n, int(v) if int(v) > 0 else None) for n, v in p.get("files", [])]
         ok: Dict[str, List[int]] = {}
-        req = {"op": "outbox_many", "token": p.get("token"), "names": [n for n, _ in files]}
-        try:
-            if p["source"] == self.me:  # this node PUT the bundle: take it from its own outbox
-                items = self.source.read(req)
-            else:
-                items = await self.blobs.fetch(p["source"], req, addr=p.get("source_blob"))
-            if len(items) == len(files):
-                for (n, v), (_, data) in zip(files, items):
-                    self.local.put_bytes(n, data, version=v)
-                    ok[n] = self.local.versions(n)
-        except (ConnectionError, OSError, asyncio.TimeoutError) as e:
-            log.warning("%s: download of %d files failed: %s", self.me, len(files), e)
+        loop = asyncio.get_running_loop()
+        spool = p.get("spool")
+        if spool and p.get("host") == HOST_ID and os.path.isdir(spool):
+            try:  # same machine: one hard link per file, no bytes moved (off the event loop)
+                ok = await loop.run_in_executor(None, self._link_from_spool, spool, files)
+                self.linked += len(ok)
+            except OSError as e:  # another filesystem / spool gone: pull the bytes instead
+                log.info("%s: spool link failed (%s); pulling over the blob plane", self.me, e)
+                ok = {}
+        if len(ok) < len(files):
+            req = {"op": "outbox_many", "token": p.get("token"), "names": [n for n, _ in files]}
+            try:
+                if p["source"] == self.me:  # this node PUT the bundle: take it from its own outbox
+                    items = self.source.read(req)
+                else:
+                    items = await self.blobs.fetch(p["source"], req, addr=p.get("source_blob"))
+                if len(items) == len(files):
+                    def write():
+                        for (n, v), (_, data) in zip(files, items):
+                            self.local.put_bytes(n, data, version=v)
+                            ok[n] = self.local.versions(n)
+                    await loop.run_in_executor(None, write)  # file writes never block the SWIM loop
+                    self.pulled += len(files)
+            except (ConnectionError, OSError, asyncio.TimeoutError) as e:
+                log.warning("%s: download of %d files failed: %s", self.me, len(files), e)
         await self.ep.reply(fr, MsgType.DOWNLOAD_MANY_REPLY,
                             {"ok": ok, "failed": [n for n, _ in files if n not in ok]})
 

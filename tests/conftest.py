@@ -11,6 +11,8 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "serial: timing-sensitive CPU test, run first in the session (nothing "
+                                       "left over from other tests shares the cores)")
 
 
 def _has_gpu():
@@ -22,6 +24,8 @@ def _has_gpu():
 
 
 def pytest_collection_modifyitems(config, items):
+    # serial (timing-sensitive) tests first, in their own order; the rest keep theirs
+    items[:] = [it for it in items if "serial" in it.keywords] + [it for it in items if "serial" not in it.keywords]
     if _has_gpu():
         return
     skip = pytest.mark.skip(reason="no HIP device")

@@ -29,6 +29,9 @@ def test_self_launch_three_ranks():
         assert k in out
     # the InceptionV3 sub-record rides in the same line (BASELINE config 3)
     assert out["models"]["InceptionV3"]["config"]["per_worker_batch"] == 128
+    # every rank reports its NUMA placement (utils/numa.py; unbound where sysfs has no KFD GPUs)
+    assert [p["rank"] for p in out["placement"]] == [0, 1, 2]
+    assert all({"local_rank", "numa", "cpus", "bound"} <= set(p) for p in out["placement"])
 
 
 def test_single_rank_unchanged():

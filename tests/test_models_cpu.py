@@ -380,7 +380,6 @@ def test_block_boundary_fusion_plan_resnet50(monkeypatch):
     assert e2.exp_red["conv3_block4_3_conv"].name == "conv4_block1_1_conv"
     assert "conv4_block6_3_conv" not in e2.exp_red  # stage 4's end (C = 1024) never
     assert "conv2_block3_3_conv" not in plan(DML_CHAIN_STAGE_END="0").exp_red
-    assert "conv2_block3_3_conv" not in plan(DML_CHAIN_STAGE_END="1", DML_ER_R1="1").exp_red
 
 
 def test_stem_fold_plan_resnet50(monkeypatch):

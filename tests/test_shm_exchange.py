@@ -64,3 +64,39 @@ def test_shm_exchange_dead_member_fails_the_wait():
     with pytest.raises(CollectiveFailure):  # another geometry under the same name is refused
         ShmExchange(name, 2, 0).close(unlink=False) or ShmExchange(name, 3, 0)
     os.unlink("/dev/shm" + name)
+
+
+def _elastic_round(store, value):
+    """One world-1 ElasticGroup over ``store`` with the shared-memory exchange: returns the
+    exchanged record and the segment name; the group is NOT closed (a SIGKILLed rank never
+    unlinks its segment)."""
+    import torch.distributed as dist
+
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+
+    eg = ElasticGroup(0, 1, store_path=store, backend="gloo", timeout_s=10, shm_exchange=True)
+    out = torch.zeros((1, 4), dtype=torch.int64)
+    for s in range(3):
+        eg.exchange(out, torch.tensor([value, s, 0, 0], dtype=torch.int64), root=0)
+    name = eg._shm_names[-1]
+    eg._shm = None  # abandon the segment like a killed rank (no close, no unlink)
+    dist.destroy_process_group()
+    return out.clone(), name
+
+
+def test_relaunch_over_a_reused_rdzv_path_never_reads_stale_records(tmp_path):
+    """segment names are unique per job (a nonce fixed in the FileStore), so a
+    relaunch over the same --rdzv path (launcher: FileStore file removed) never opens the
+    killed run's segment, whose step counters would make the wait succeed at once with the
+    old records; the launcher also removes the stale segments of the path."""
+    from distributed_machine_learning_amd.parallel.elastic import unlink_stale_segments
+
+    store = str(tmp_path / "rdzv")
+    out1, name1 = _elastic_round(store, 7)
+    assert out1[0, 0] == 7 and os.path.exists("/dev/shm" + name1)
+    os.remove(store)                      # what the launcher does before a relaunch
+    out2, name2 = _elastic_round(store, 42)
+    assert name2 != name1
+    assert out2[0, 0] == 42 and out2[0, 1] == 2
+    assert unlink_stale_segments(store) == 2  # both runs' abandoned segments
+    assert not os.path.exists("/dev/shm" + name1) and not os.path.exists("/dev/shm" + name2)

@@ -254,7 +254,6 @@ def test_engine_fused_blocks_equal_unfused(maxc, chain, merged, pairs, monkeypat
         monkeypatch.setenv("DML_CHAIN_MERGED", merged)
     else:  # the default: the merged stage-2 entry on the chained kernel
         monkeypatch.delenv("DML_CHAIN_MERGED", raising=False)
-    monkeypatch.setenv("DML_FUSED_MERGED_BLOCK", "1")  # opt-in merged-shortcut form, covered here
     g, w = build_model("ResNet50", seed=8, calibrate=True)
     imgs = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device="cuda")
     # no buffer recycling: intermediate tensors are compared after the whole forward

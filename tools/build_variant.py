@@ -1,7 +1,7 @@
 """Build a variant of libdml_hip.so where ONE translation unit is compiled with extra
 -D flags (kernel A/B probes), reusing the other objects of the in-tree build.
 
-python tools/build_variant.py <tag> <source, e.g. kernels/conv_wino.hip> [-DFOO=1 ...]
+python tools/build_variant.py <tag> <source, e.g. kernels/conv_igemm_v2.hip> [-DFOO=1 ...]
 -> variants/libdml_<tag>.so (git-ignored, shipped to the GPU box by gpurun)
 """
 import os

@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """Chained-GEMM block boundary (expand_reduce_chain.hip) vs the two tuned 1x1
-launches it replaces (and the r1 phase-serialised kernel, DML_ER_R1=1 in a
-second process), ResNet50 stage 3 (F = 128, C = 512), 128-image sub-batch,
+launches it replaces, ResNet50 stage 3 (F = 128, C = 512), 128-image sub-batch,
 cold (L2/MALL scrubbed before each launch) and warm.
 
   python tools/chain_bench.py --out gpurun_out/chain.json
@@ -76,7 +75,7 @@ def main():
     torch.cuda.synchronize()
     err_y = ((y2.float() - y.view(m, c).float()).abs().max() / y.float().abs().max()).item()
     err_z = ((z2.float() - z.view(m, f).float()).abs().max() / z.float().abs().max()).item()
-    rec = {"m": m, "C": c, "F": f, "r1_kernel": os.environ.get("DML_ER_R1", "0"), "waves": os.environ.get("DML_CHAIN_WAVES", "4"), "cfgs": [cfg_e, cfg_r],
+    rec = {"m": m, "C": c, "F": f, "waves": os.environ.get("DML_CHAIN_WAVES", "4"), "cfgs": [cfg_e, cfg_r],
            "two_launches_cold_us": timed(two, True), "two_launches_warm_us": timed(two, False),
            "fused_cold_us": timed(fused, True), "fused_warm_us": timed(fused, False),
            "hbm_min_mb_fused": round(m * (f + c + c + f) * 2 / 1e6, 1),

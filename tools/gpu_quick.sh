@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun call for an iteration: selected GPU tests, then short benches of the
 # listed models (service pass off), per-op times, the tuning table back.
-#   TESTS="tests/test_wino_gpu.py"  MODELS="ResNet50 InceptionV3"  STEPS=20  BENCH_ARGS=""
+#   TESTS="tests/test_kernels_gpu.py"  MODELS="ResNet50 InceptionV3"  STEPS=20  BENCH_ARGS=""
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
