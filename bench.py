@@ -83,6 +83,10 @@ def parse_args(argv=None):
     ap.add_argument("--svc-resnet-images", type=int, default=51200, help="ResNet50 images per GPU (service run)")
     ap.add_argument("--svc-inception-images", type=int, default=25600,
                     help="InceptionV3 images per GPU (service run)")
+    ap.add_argument("--svc-store-images", type=int, default=2048,
+                    help="the `service_store` sub-record: the same concurrent jobs over this many distinct JPEGs "
+                         "PUT into the replicated store (fetched, decoded once, staged into HBM on the timed path); "
+                         "0 = skip")
     ap.add_argument("--svc-outputs", default="",
                     help="also write the service run's output files to this directory (removed afterwards); "
                          "every output is always PUT into the ranks' replicated store, as serving.main --role rank")
@@ -356,11 +360,27 @@ def bench_service(args, rank: int, world: int, device, recs: dict):
     kill_pass = args.kill_pass == "on" or (args.kill_pass == "auto" and world >= 4)
     if kill_pass:
         rdzv_k, port_k = service_bench.agree(rank)
+    if args.svc_store_images:
+        rdzv_s, port_s = service_bench.agree(rank)
     dist.destroy_process_group()  # the service builds its own epoch-versioned groups
     rates = {m: r["value"] for m, r in recs.items() if r and "value" in r}
     out_dir = (os.path.join(args.svc_outputs, os.path.basename(rdzv) + "_outputs") if args.svc_outputs else None)
     rec = service_bench.run(rank, world, device, rdzv, port, args.svc_resnet_images * world,
                             args.svc_inception_images * world, dict(DEFAULT_BATCH), out_dir, single_rates=rates)
+    if args.svc_store_images and rec is not None:
+        # the reference's real workload: jobs over store images (worker.py:1361-1386) —
+        # fetched from the replicated store, decoded once per job, staged into HBM windows
+        try:
+            srec = service_bench.run(rank, world, device, rdzv_s, port_s, args.svc_resnet_images * world,
+                                     args.svc_inception_images * world, dict(DEFAULT_BATCH), None,
+                                     single_rates=rates, store_images=args.svc_store_images)
+        except Exception as e:  # noqa: BLE001 - reported in the record, never fails the headline
+            print(f"bench: rank {rank}: store-image service pass failed: {e}", file=sys.stderr, flush=True)
+            srec = {"error": str(e)[:500]}
+        if srec is not None:
+            if "value" in srec and rec.get("value"):
+                srec["vs_synthetic_service"] = round(srec["value"] / rec["value"], 3)
+            rec["store_images_pass"] = srec
     if kill_pass:
         # BASELINE config 5: the same concurrent jobs with two ranks killed mid-job (SWIM
         # detects, the survivors rebuild and re-dispatch); each rank's share runs in a child

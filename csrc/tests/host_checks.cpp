@@ -102,7 +102,7 @@ int main() {
   CHECK(dml_conv_v2_bn(64) == 0 && dml_conv_v2_bn(68) == 0);   // the removed shifted-pixel ids
   CHECK(dml_conv(&a, 64, nullptr) != 0);
   CHECK(dml_conv(&a, 80, nullptr) != 0);        // the removed Winograd ids
-  CHECK(dml_conv(&a, 113, nullptr) != 0);       // an unassigned warp-specialised id
+  CHECK(dml_conv(&a, 119, nullptr) != 0);       // an unassigned warp-specialised id
   CHECK(dml_conv(&a, 139, nullptr) != 0);       // an unassigned persistent id
   CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
   CHECK(dml_conv_v2_bn(100) == 128 && dml_conv_v2_bn(103) == 64 && dml_conv_v2_bn(120) == 64 &&

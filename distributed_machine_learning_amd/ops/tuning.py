@@ -24,7 +24,7 @@ from .. import _native as N
 V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33, 34, 36, 37,
            38, 39)  # 23..37: BK32; 38 / 39: 3-stage BK64 64-channel tiles (r3)
 # warp-specialised tiles (csrc/kernels/conv_igemm_ws.hip: loader waves + MFMA waves, r5)
-WS_CFGS = tuple(range(100, 113))
+WS_CFGS = tuple(range(100, 119))
 # their persistent form (csrc/kernels/conv_igemm_wsp.hip: one operand ring over a workgroup's
 # whole tile list; no split-K)
 WSP_CFGS = tuple(range(120, 130))

@@ -159,6 +159,7 @@ class ElasticGroup:
         self.dead: Set[int] = set()          # fed by the failure detector (thread-safe set ops)
         self.joiners: Set[int] = set()       # ranks alive again but outside the group (SWIM rejoin)
         self.aborts = 0
+        self._moved_t, self._moved_every_s = 0.0, 0.05
         self.shm_exchange = shm_exchange and store_host is None
         self._shm: Optional[ShmExchange] = None
         self._shm_names: List[str] = []
@@ -269,9 +270,19 @@ class ElasticGroup:
             raise CollectiveFailure(str(e)) from e
 
     def _poll_dead(self) -> None:
-        """(between shared-memory wait slices) a member SWIM confirmed dead fails the exchange."""
+        """(between shared-memory wait slices) a member SWIM confirmed dead fails the exchange;
+        so does a next epoch the others fixed WITHOUT this rank (a live rank they declared
+        dead — a false suspicion — would otherwise wait out the whole timeout on a segment
+        nobody else writes any more; a next epoch that holds this rank is a growth, announced
+        by this very exchange). The store is looked at every ``_moved_every_s``."""
         if self.dead & set(self.members):
             raise CollectiveFailure(f"members {sorted(self.dead & set(self.members))} declared dead")
+        now = time.monotonic()
+        if now - self._moved_t >= self._moved_every_s:
+            self._moved_t = now
+            key = f"members{self.epoch + 1}"
+            if self.store.check([key]) and self.grank not in json.loads(self.store.get(key).decode()):
+                raise CollectiveFailure(f"removed from the group: epoch {self.epoch + 1} fixed without this rank")
 
     def _run(self, fn, *args, **kw) -> None:
         try:
@@ -283,6 +294,27 @@ class ElasticGroup:
     def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
         """``src`` is a GROUP rank."""
         self._run(dist.broadcast, t, src=src)
+
+    def broadcast_bytes(self, t: torch.Tensor, src: int = 0) -> None:
+        """Broadcast a uint8 CPU tensor (the service's log bytes) from GROUP rank ``src``.
+        With the shared-memory exchange it goes through that segment in record-sized chunks,
+        waited for with the same dead-member / moved-epoch polling as the step's exchange
+        (a gloo broadcast blocks without either: a peer that left mid-broadcast held this
+        rank for the full collective timeout)."""
+        if self._shm is None or t.device.type != "cpu":
+            self.broadcast(t, src=src)
+            return
+        cap = ShmExchange.REC_CAP
+        n = t.numel()
+        flat = t.view(-1)
+        out = torch.empty((self.world, min(cap, max(n, 1))), dtype=torch.uint8)
+        for o in range(0, n, cap):
+            k = min(cap, n - o)
+            chunk = flat[o:o + k].contiguous() if self.rank == src else torch.zeros(k, dtype=torch.uint8)
+            ob = out[:, :k] if k == out.shape[1] else torch.empty((self.world, k), dtype=torch.uint8)
+            self._shm.exchange(ob, chunk, self._poll_dead, self.timeout.total_seconds())
+            if self.rank != src:
+                flat[o:o + k].copy_(ob[src])
 
     def gather(self, t: torch.Tensor, bufs: Optional[List[torch.Tensor]], dst: int = 0) -> None:
         self._run(dist.gather, t, bufs if self.rank == dst else None, dst=dst)
@@ -330,6 +362,23 @@ class ElasticGroup:
                 return dist.all_gather_into_tensor(out, t, group=self.data_group, async_op=True)
             return dist.all_gather(list(out.view(self.world, *t.shape).unbind(0)), t, group=self.data_group,
                                    async_op=True)
+        except Exception as e:
+            raise CollectiveFailure(str(e)) from e
+
+    def all_to_all_data_async(self, out: torch.Tensor, t: torch.Tensor, out_splits: List[int],
+                              in_splits: List[int]):
+        """Issue an uneven all-to-all on the data group (rows of dim 0: ``in_splits[r]``
+        rows of ``t`` go to group rank r, ``out_splits[s]`` rows arrive from s); returns the
+        Work (same contract as all_gather_data_async)."""
+        try:
+            return dist.all_to_all_single(out, t, out_splits, in_splits, group=self.data_group, async_op=True)
+        except Exception as e:
+            raise CollectiveFailure(str(e)) from e
+
+    def all_reduce_data_async(self, t: torch.Tensor):
+        """Issue a SUM all-reduce on the data group; returns the Work."""
+        try:
+            return dist.all_reduce(t, group=self.data_group, async_op=True)
         except Exception as e:
             raise CollectiveFailure(str(e)) from e
 
@@ -408,7 +457,17 @@ class ElasticGroup:
         self._init_pg()
         return won
 
-    def _await_admission(self, timeout_s: float) -> None:
+    def rejoin(self, timeout_s: float) -> List[int]:
+        """A live rank the others removed (a false suspicion: it was slow, not dead) joins
+        again like a restarted one: it waits for its admission into a later epoch (the
+        coordinator admits it once SWIM sees it alive) and initialises that epoch."""
+        self._teardown(abort=True)
+        self.dead.clear()
+        self._await_admission(timeout_s, after=self.epoch)
+        self._init_pg()
+        return self.members
+
+    def _await_admission(self, timeout_s: float, after: int = -1) -> None:
         """(joiner) Wait for ``admit<g>`` = the epoch whose member list holds
         this rank, then take that epoch's member list from the store."""
         key = f"admit{self.grank}"
@@ -417,7 +476,7 @@ class ElasticGroup:
             if self.store.check([key]):
                 e = int(self.store.get(key).decode())
                 members = json.loads(self.store.get(f"members{e}").decode())
-                if self.grank in members:
+                if self.grank in members and e > after:
                     prev = self.store.get(f"members{e - 1}").decode() if e > 0 else json.dumps(members)
                     self.prev_members = json.loads(prev)
                     self.epoch, self.members = e, members

@@ -1,5 +1,5 @@
-"""HBM-resident decoded-image store, staged in sliding windows ahead of dispatch and
-replicated across the ranks over the data group (RCCL on a GPU node).
+"""HBM-resident decoded-image store, staged in windows ahead of dispatch and delivered only
+to the rank that runs each batch (RCCL over the data group on a GPU node).
 
 Reference: SDFS keeps every JPEG on 4 replicas (``leader.py:45-85``), copied by
 scp (``file_service.py:52-124``), and every worker scp-downloads and decodes each
@@ -8,31 +8,35 @@ image of its batch again, one at a time, when the task arrives
 
 MI355X-native replacement (SURVEY §2.6 "replication multicast" row):
 
-* a job's images are staged in WINDOWS that run just ahead of dispatch: every
-  step the service hands the batches about to be dispatched (and any dispatched
-  batch not staged yet) to ``stage``; their not-yet-resident images form one
-  window. Every rank takes the same decisions from the replicated job state
-  (same queue order, same arena bookkeeping), so windows, slot assignments and
-  evictions are identical everywhere without any extra agreement;
-* a window's images are fetched (store blob plane) and DECODED ONCE IN THE WHOLE
-  JOB — image i of the window by rank i % world, in a host thread pool, off the
-  serve loop — then replicated to every rank's HBM with one all-gather over the
-  data group, issued asynchronously from the serve loop (windows in the same
-  order on every rank) and followed, in stream order, by the scatter into the
-  window's arena slots and an event: a batch launches once its window's event is
-  recorded (the compute stream waits on it), so the serve loop never blocks on
-  staging;
-* arena slots are pinned by the staged, unfinished batches that use them
-  (refcounts) and released when a batch completes; eviction takes the oldest
-  unpinned image; a window that does not fit waits for completions. Any job size
-  runs in a fixed arena (``capacity`` >= the images of the batches in flight);
-* an image that could not be fetched or decoded is failed for the batches of its
-  window only: it is forgotten when its last batch completes, and a later job
-  fetches it again (a transient store miss during a leader fail-over is not
-  permanent);
-* after any epoch change (failure rebuild, rejoin) every rank drops its staging
-  state at the same step boundary (``reset``) and the windows are staged afresh
-  for the new member set — a re-joined rank needs no special backfill.
+* a batch's images are staged in a WINDOW for ONE destination rank — the rank the batch
+  is dispatched to, or, for a batch still queued, the rank the replicated coordinator
+  gave it as its affinity (``ReplicatedCoordinator.assign_affinity``; the plan then
+  dispatches the batch there). Every rank takes the same decisions from the replicated
+  job state (same queue order, same arena bookkeeping, same slot map), so windows, slot
+  assignments and evictions are identical everywhere without any extra agreement; only
+  the pixels differ: a slot holds its image on the ranks that hold it (``holders``);
+* an image new to the job is fetched (store blob plane) and DECODED ONCE, by the
+  destination rank itself, in a host thread pool off the serve loop — nothing crosses
+  xGMI for it. An image another rank already holds (a cyclic job re-using its images, a
+  batch re-dispatched away from its affinity rank) is SHIPPED from the lowest holder's
+  arena by an uneven all-to-all over the data group — HBM to HBM, no second decode —
+  never all-gathered to every rank (all-gather-to-all moved world x
+  the needed bytes). Each window also all-reduces one ok flag per image (a few bytes),
+  so every rank learns the failures and keeps identical bookkeeping;
+* the collectives are issued asynchronously from the serve loop, in plan order on every
+  rank, and followed, in stream order, by the scatter into the window's arena slots and
+  an event: a batch launches once the windows that delivered its images HERE are done
+  (the compute stream waits on their events), so the serve loop never blocks on staging;
+* arena slots are pinned by the staged, unfinished batches that use them (refcounts) and
+  released when a batch completes; eviction takes the oldest unpinned image; a window
+  that does not fit waits for completions. Any job size runs in a fixed arena;
+* an image that could not be fetched or decoded is failed for the batches of its window
+  only: it is forgotten when its last batch completes, and a later job fetches it again
+  (a transient store miss during a leader fail-over is not permanent);
+* after any epoch change (failure rebuild, rejoin) every rank drops its staging state at
+  the same step boundary (``reset``) and the windows are staged afresh for the new member
+  set — a re-joined rank needs no special backfill. (A spare copy on a second rank would
+  therefore buy nothing on failover: the survivors re-stage from the store either way.)
 """
 from __future__ import annotations
 
@@ -53,17 +57,22 @@ class Window:
     store: "HbmImageStore"
     wid: int
     epoch: int
-    names: List[str]          # the new images of this window (replicated by it)
+    dst: int                  # the group rank these images become resident on
+    names: List[str]          # images this window makes resident on dst (new + shipped)
     slots: List[int]          # their arena slots (decided by plan, identical on every rank)
-    mine: List[str] = field(default_factory=list)      # this rank's decode share
+    src: List[int]            # per name: the rank that supplies it (== dst: decoded there)
+    mine: List[str] = field(default_factory=list)      # this rank's decode share (dst == this rank)
     future: Optional[object] = None                    # decode of this rank's share (thread pool)
     work: Optional[list] = None                        # pending async collectives (gloo: polled)
-    bufs: Optional[tuple] = None                       # (send, recv, ok_send, ok_recv) tensors
+    bufs: Optional[tuple] = None                       # (local rows, received rows, flags) tensors
     event: Optional[object] = None                     # recorded after the scatter (CUDA)
-    flags: Optional[torch.Tensor] = None               # ok flag per gathered row (host)
-    src: Optional[List[int]] = None                    # gathered row of each name
+    flags: Optional[torch.Tensor] = None               # ok flag per name (host), after the all-reduce
     failed: Set[str] = field(default_factory=set)
     done: bool = False
+
+    @property
+    def shipped(self) -> int:
+        return sum(1 for s in self.src if s != self.dst)
 
 
 class HbmImageStore:
@@ -86,15 +95,23 @@ class HbmImageStore:
         self.stager = Stager()  # replaced by the backend's shared one (one collective order for all models)
         self.reset()
         self.decoded = 0        # images this rank decoded
-        self.replicated = 0     # images that arrived in this rank's arena
+        self.replicated = 0     # images that became resident in this rank's arena (decoded or shipped here)
+        self.received = 0       # of those, shipped here from another rank's arena
+        self.shipped_out = 0    # rows this rank's arena sent to other ranks
         self.windows_staged = 0
         self.evictions = 0
+
+    @property
+    def me(self) -> int:
+        return self.stager.ctx[0]
 
     # ----------------------------------------------------------- state --
     def reset(self) -> None:
         """Forget every staged image (epoch change): identical on every rank."""
         self.index: "OrderedDict[str, int]" = OrderedDict()   # name -> slot, in staging (FIFO) order
-        self.window_of: Dict[str, Window] = {}                 # name -> the window that stages it
+        self.holders: Dict[str, Set[int]] = {}                 # name -> ranks it is (being) delivered to
+        self.window_of: Dict[str, Window] = {}                 # name -> the latest window that moves it
+        self.here: Dict[str, Window] = {}                      # name -> the window that delivers it HERE
         self.refs: Dict[str, int] = {}
         self.free: List[int] = list(range(self.capacity - 1, self.n_synth - 1, -1))
         self._wid = 0
@@ -102,33 +119,49 @@ class HbmImageStore:
     def _synthetic(self, n: str) -> bool:
         return self.n_synth > 0 and n.startswith(SYNTH)
 
-    def resident(self, name: str) -> bool:
-        return name in self.index
+    def resident(self, name: str, rank: Optional[int] = None) -> bool:
+        """Staged (anywhere), or - with ``rank`` - staged for that rank."""
+        if rank is None:
+            return name in self.index
+        return rank in self.holders.get(name, ())
 
     # ------------------------------------------------- plan (deterministic) --
-    def plan(self, names: Sequence[str], epoch: int) -> Optional[Window]:
-        """(serve loop, every rank, same order) reserve slots for the images of
-        ``names`` that are not staged yet; None if they do not fit next to the
-        pinned images (the caller stages fewer batches and retries later). Returns
-        the window (possibly with no new names)."""
-        new = [n for n in dict.fromkeys(names) if not self._synthetic(n) and n not in self.index]
-        if len(new) > len(self.free) + sum(1 for k in self.index if self.refs.get(k, 0) == 0 and k not in new):
+    def plan(self, names: Sequence[str], epoch: int, dst: int = 0) -> Optional[Window]:
+        """(serve loop, every rank, same order) make the images of ``names`` resident on
+        group rank ``dst``: slots for the ones not staged anywhere (decoded by ``dst``), a
+        shipment from a holder for the ones staged elsewhere; None if the new ones do not
+        fit next to the pinned images (the caller stages fewer batches and retries later).
+        Returns the window (possibly with no names)."""
+        want = [n for n in dict.fromkeys(names) if not self._synthetic(n)]
+        new = [n for n in want if n not in self.index]
+        move = [n for n in want if n in self.index and dst not in self.holders[n]]
+        if len(new) > len(self.free) + sum(1 for k in self.index if self.refs.get(k, 0) == 0 and k not in want):
             return None
-        slots = []
+        slots, src = [], []
         for n in new:
             if not self.free:  # evict the oldest unpinned image
-                victim = next(k for k in self.index if self.refs.get(k, 0) == 0)
+                victim = next(k for k in self.index if self.refs.get(k, 0) == 0 and k not in want)
                 self.free.append(self.index.pop(victim))
+                self.holders.pop(victim, None)
                 self.window_of.pop(victim, None)
+                self.here.pop(victim, None)
                 self.evictions += 1
             s = self.free.pop()
             slots.append(s)
+            src.append(dst)
             self.index[n] = s
-        w = Window(self, self._wid, epoch, new, slots)
+            self.holders[n] = {dst}
+        for n in move:
+            slots.append(self.index[n])
+            src.append(min(self.holders[n]))   # the lowest holder ships it (its copy lands first)
+            self.holders[n].add(dst)
+        w = Window(self, self._wid, epoch, dst, new + move, slots, src)
         self._wid += 1
-        for n in new:
+        for n in w.names:
             self.window_of[n] = w
-        if new:
+            if dst == self.me:
+                self.here[n] = w
+        if w.names:
             self.stager.queue.append(w)
             self.windows_staged += 1
         else:
@@ -157,35 +190,38 @@ class HbmImageStore:
                 continue
             if not w.done:
                 # every rank decides this at the same step: a batch of w completed somewhere,
-                # so every rank has issued w's collective and finishing it here is bounded
+                # so every rank has issued w's collectives and finishing it here is bounded
                 self.stager.flush_until(w)
             if n in w.failed and n in self.index:
                 self.free.append(self.index.pop(n))
+                self.holders.pop(n, None)
                 self.window_of.pop(n, None)
+                self.here.pop(n, None)
 
     # --------------------------------------------------------- readiness --
     def ready(self, names: Sequence[str]) -> bool:
+        """Every image of a batch is resident on THIS rank."""
         for n in names:
             if self._synthetic(n):
                 continue
-            w = self.window_of.get(n)
+            w = self.here.get(n)
             if w is None or not w.done:
                 return False
         return True
 
     def events(self, names: Sequence[str]) -> List[object]:
-        evs = {id(w.event): w.event for w in (self.window_of.get(n) for n in names)
+        evs = {id(w.event): w.event for w in (self.here.get(n) for n in names)
                if w is not None and w.event is not None}
         return list(evs.values())
 
     def slots(self, names: Sequence[str]) -> Tuple[List[int], List[str]]:
-        """Arena slots of a staged batch; failed images get slot 0 and are listed."""
+        """Arena slots of a batch staged here; failed images get slot 0 and are listed."""
         out, failed = [], []
         for n in names:
             if self._synthetic(n):
                 out.append(int(n[len(SYNTH):]) % self.n_synth)
                 continue
-            w = self.window_of.get(n)
+            w = self.here.get(n)
             if n not in self.index or w is None or n in w.failed:
                 failed.append(n)
                 out.append(0)
@@ -193,43 +229,58 @@ class HbmImageStore:
                 out.append(self.index[n])
         return out, failed
 
-    # ------------------------------------------------------ replication --
-    def _issue(self, w: Window, rank: int, world: int, got: Dict[str, Optional[np.ndarray]],
-               gather_async: Callable, stream) -> None:
-        chunk = max(1, -(-len(w.names) // world))
-        stage = torch.zeros((chunk, *self.hw, 3), dtype=torch.uint8)
-        ok = torch.zeros(chunk, dtype=torch.int32)
-        for j, n in enumerate(w.mine):
-            img = got.get(n)
-            if img is not None:
-                stage[j].numpy()[...] = img  # loader arrays may be read-only views
-                ok[j] = 1
-        self.decoded += int(ok.sum())
-        ctx = torch.cuda.stream(stream) if (stream is not None and self.device.type == "cuda") else _null()
+    # ---------------------------------------------------------- delivery --
+    def _issue(self, w: Window, rank: int, world: int, got: Dict[str, Optional[np.ndarray]], comm, stream) -> None:
+        """This rank's part of window ``w``: its decoded images (dst), the rows it ships
+        from its arena (a holder), the all-to-all of the shipped rows and the all-reduce of
+        the ok flags (both skipped when nothing needs them: identical decisions everywhere)."""
+        cuda = self.device.type == "cuda"
+        ok = torch.zeros(len(w.names), dtype=torch.int32)
+        local = None
+        if rank == w.dst and w.mine:
+            local = torch.zeros((len(w.mine), *self.hw, 3), dtype=torch.uint8)
+            for j, n in enumerate(w.mine):
+                img = got.get(n)
+                if img is not None:
+                    local[j].numpy()[...] = img  # loader arrays may be read-only views
+            self.decoded += sum(1 for n in w.mine if got.get(n) is not None)
+        pos = {n: i for i, n in enumerate(w.names)}
+        for n in w.mine:
+            if got.get(n) is not None:
+                ok[pos[n]] = 1
+        out_rows = [i for i, s in enumerate(w.src) if s == rank and s != w.dst]   # shipped from here
+        for i in out_rows:
+            mine = self.here.get(w.names[i])
+            ok[i] = int(mine is not None and w.names[i] not in mine.failed)
+        ctx = torch.cuda.stream(stream) if (stream is not None and cuda) else _null()
         with ctx:
-            if self.device.type == "cuda":
-                send = stage.pin_memory().to(self.device, non_blocking=True)
-                okd = ok.pin_memory().to(self.device, non_blocking=True)
-            else:
-                send, okd = stage, ok
-            if world == 1:
-                w.bufs, w.work = (send, send, okd, okd), []
-                return
-            recv = torch.empty((world * chunk, *self.hw, 3), dtype=torch.uint8, device=self.device)
-            okr = torch.empty(world * chunk, dtype=torch.int32, device=self.device)
-            w.bufs = (send, recv, okd, okr)
-            w.work = [gather_async(recv, send), gather_async(okr, okd)]
+            if cuda and local is not None:
+                local = local.pin_memory().to(self.device, non_blocking=True)
+            recv, work = None, []
+            if world > 1 and w.shipped:
+                in_splits = [len(out_rows) if r == w.dst else 0 for r in range(world)]
+                out_splits = [sum(1 for s in w.src if s == r and s != w.dst) if rank == w.dst else 0
+                              for r in range(world)]
+                send = (self.arena.index_select(0, torch.tensor([w.slots[i] for i in out_rows], device=self.device))
+                        if out_rows else torch.empty((0, *self.hw, 3), dtype=torch.uint8, device=self.device))
+                recv = torch.empty((sum(out_splits), *self.hw, 3), dtype=torch.uint8, device=self.device)
+                work.append(comm.all_to_all_data_async(recv, send, out_splits, in_splits))
+                self.shipped_out += len(out_rows)
+            okd = ok.pin_memory().to(self.device, non_blocking=True) if cuda else ok
+            if world > 1:
+                work.append(comm.all_reduce_data_async(okd))
+            w.bufs, w.work = (local, recv, okd), work
 
     def _finish(self, w: Window, world: int, stream) -> bool:
-        """Once the window's collective is in place: scatter every name's row into its
-        slot (stream order on a GPU; failed rows are zeros) and bring the ok flags to the
-        host asynchronously; the window is done (ready to launch from) when they arrive."""
+        """Once the window's collectives are in place: on its destination, scatter the
+        decoded and the received rows into their slots (stream order on a GPU; failed rows
+        are zeros); everywhere, bring the ok flags to the host asynchronously. The window is
+        done (ready to launch from) when they arrive."""
         cuda = self.device.type == "cuda"
         if w.event is None:
             if not cuda and any(not wk.is_completed() for wk in w.work):
                 return False
-            send, recv, okd, okr = w.bufs
-            chunk = okr.numel() // world
+            local, recv, okd = w.bufs
             ctx = torch.cuda.stream(stream) if (stream is not None and cuda) else _null()
             with ctx:
                 for wk in w.work:
@@ -239,23 +290,31 @@ class HbmImageStore:
                         from .elastic import CollectiveFailure
 
                         raise CollectiveFailure(f"image window collective failed: {e}") from e
-                src = [(i % world) * chunk + i // world for i in range(len(w.names))]
-                self.arena.index_copy_(0, torch.tensor(w.slots, device=self.device),
-                                       recv.index_select(0, torch.tensor(src, device=self.device)))
+                if self.me == w.dst:
+                    # received rows arrive grouped by source rank, each group in window order
+                    order = [i for i, s in enumerate(w.src) if s == w.dst]
+                    order += [i for r in range(world) for i, s in enumerate(w.src) if s == r and s != w.dst]
+                    rows = [t for t in (local, recv) if t is not None and t.shape[0]]
+                    if rows:
+                        data = rows[0] if len(rows) == 1 else torch.cat(rows)
+                        self.arena.index_copy_(0, torch.tensor([w.slots[i] for i in order], device=self.device),
+                                               data)
                 if cuda:
-                    w.flags = okr.to("cpu", non_blocking=True) if okr.is_cuda else okr
+                    w.flags = okd.to("cpu", non_blocking=True)
                     w.event = torch.cuda.Event()
                     w.event.record()
                 else:
-                    w.flags, w.event = okr, True
-            w.src = src
+                    w.flags, w.event = okd, True
         if cuda and not w.event.query():
             return False
         flags = w.flags.numpy()
-        for n, k in zip(w.names, w.src):
-            if not flags[k]:
+        for n, f in zip(w.names, flags):
+            if not f:
                 w.failed.add(n)
-        self.replicated += len(w.names) - len(w.failed)
+        if self.me == w.dst:
+            arrived = len(w.names) - sum(1 for n in w.names if n in w.failed)
+            self.replicated += arrived
+            self.received += sum(1 for n, s in zip(w.names, w.src) if s != w.dst and n not in w.failed)
         if not cuda:
             w.event = None
         w.bufs, w.work, w.flags, w.done = None, None, None, True
@@ -263,33 +322,35 @@ class HbmImageStore:
 
 
 class Stager:
-    """The windows of every model's store in ONE plan order: their all-gathers go out
-    on the data group in that order on every rank (gloo / RCCL match collectives by
-    order, so two models' windows must never be issued in a rank-dependent order)."""
+    """The windows of every model's store in ONE plan order: their collectives go out on
+    the data group in that order on every rank (gloo / RCCL match collectives by order, so
+    two models' windows must never be issued in a rank-dependent order)."""
 
     def __init__(self):
         self.queue: Deque[Window] = deque()
         self.ctx = (0, 1, None, None, None)
         self.poll_dead: Callable[[], None] = lambda: None
 
-    def attach(self, rank: int, world: int, pool, gather_async: Callable, stream=None,
+    def attach(self, rank: int, world: int, pool, comm, stream=None,
                poll_dead: Optional[Callable[[], None]] = None) -> None:
-        """The group the windows replicate over (every epoch): group rank / size, the decode
-        pool, the async all-gather, the staging stream; ``poll_dead`` raises CollectiveFailure
-        once a member is confirmed dead (a blocking flush polls it: a collective with a dead
-        peer never completes on RCCL, and a hung peer keeps gloo's sockets open)."""
-        self.ctx = (rank, world, pool, gather_async, stream)
+        """The group the windows move over (every epoch): group rank / size, the decode
+        pool, the data-group collectives (an ElasticGroup: all_to_all_data_async,
+        all_reduce_data_async; None at world 1), the staging stream; ``poll_dead`` raises
+        CollectiveFailure once a member is confirmed dead (a blocking flush polls it: a
+        collective with a dead peer never completes on RCCL, and a hung peer keeps gloo's
+        sockets open)."""
+        self.ctx = (rank, world, pool, comm, stream)
         self.poll_dead = poll_dead or (lambda: None)
 
     def flush_until(self, target: Window) -> None:
-        """Block until ``target`` (and every window before it) is resident here."""
+        """Block until ``target`` (and every window before it) is done here."""
         import time
 
         while not target.done and self.queue:
             w = self.queue[0]
             if w.future is not None and not w.future.done():
                 w.future.result()
-            # the window's collective / scatter: polled, never a blocking wait (a dead peer)
+            # the window's collectives / scatter: polled, never a blocking wait (a dead peer)
             while ((w.work is not None and w.event is None and w.store.device.type != "cuda"
                     and not all(wk.is_completed() for wk in w.work)) or
                    (w.event is not None and not isinstance(w.event, bool) and not w.event.query())):
@@ -301,21 +362,21 @@ class Stager:
 
     def progress(self) -> int:
         """(serve loop, never blocks) advance the queued windows in order: start this
-        rank's decode share, issue a window's all-gather once its decode finished (in plan
-        order on every rank), finish windows whose collective completed. Returns the
-        windows finished now."""
-        rank, world, pool, gather_async, stream = self.ctx
+        rank's decodes (the windows it is the destination of), issue a window's
+        collectives once its decode finished (in plan order on every rank), finish windows
+        whose collectives completed. Returns the windows finished now."""
+        rank, world, pool, comm, stream = self.ctx
         finished = 0
         for w in self.queue:  # decodes of every queued window may run ahead in the pool
             if w.future is None:
-                w.mine = w.names[rank::world]
+                w.mine = [n for n, s in zip(w.names, w.src) if s == w.dst] if rank == w.dst else []
                 w.future = pool.submit(_safe_load, w.store.loader, list(w.mine))
         while self.queue:
             w = self.queue[0]
             if w.work is None:
                 if not w.future.done():
                     break
-                w.store._issue(w, rank, world, w.future.result(), gather_async, stream)
+                w.store._issue(w, rank, world, w.future.result(), comm, stream)
             if not w.store._finish(w, world, stream):
                 break
             self.queue.popleft()

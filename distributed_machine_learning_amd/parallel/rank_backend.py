@@ -70,9 +70,10 @@ class RankBackend:
     def attach(self, eg) -> None:
         """A new communicator epoch (group rank / size, data group)."""
 
-    def stage(self, model: str, batches) -> bool:
-        """Stage these batches' images (in order) ahead of their launch; False if the
-        arena could not take all of them yet."""
+    def stage(self, model: str, batches, where: Optional[Dict[tuple, int]] = None) -> bool:
+        """Stage these batches' images (in order) ahead of their launch on the rank
+        ``where[batch.key]`` (a GLOBAL rank: the one it was dispatched to, or its affinity);
+        False if the arena could not take all of them yet."""
         return True
 
     def progress(self) -> None:
@@ -96,7 +97,7 @@ class _ArenaStaging:
     GpuRankBackend): decisions from the replicated state, data movement asynchronous."""
 
     arenas: Dict[str, "object"]
-    staged: Dict[tuple, Tuple[str, List[str]]]
+    staged: Dict[tuple, Tuple[str, List[str], int]]   # batch key -> (model, images, destination group rank)
 
     def _init_staging(self, loader, decode_threads: int = 8) -> None:
         from concurrent.futures import ThreadPoolExecutor
@@ -115,18 +116,24 @@ class _ArenaStaging:
 
     def attach(self, eg) -> None:
         self.epoch = eg.epoch
-        self.stager.attach(eg.rank, eg.world, self.pool, eg.all_gather_data_async,
+        self.members = list(eg.members)
+        self.stager.attach(eg.rank, eg.world, self.pool, eg if eg.world > 1 else None,
                            getattr(self, "stage_stream", None), poll_dead=eg._poll_dead)
 
-    def stage(self, model, batches) -> bool:
+    def stage(self, model, batches, where=None) -> bool:
         arena = self.arenas[model]
+        members = getattr(self, "members", [0])
         for b in batches:
-            if b.key in self.staged:
+            g = (where or {}).get(b.key, members[0])
+            dst = members.index(g) if g in members else 0
+            st = self.staged.get(b.key)
+            if st is not None and st[2] == dst:
                 continue
-            if arena.plan(b.images, self.epoch) is None:
+            if arena.plan(b.images, self.epoch, dst) is None:
                 return False  # later batches wait for completions to free arena slots
-            arena.pin(b.images)
-            self.staged[b.key] = (model, list(b.images))
+            if st is None:
+                arena.pin(b.images)   # a batch re-targeted to another rank stays pinned once
+            self.staged[b.key] = (model, list(b.images), dst)
         return True
 
     def progress(self) -> None:
@@ -262,8 +269,8 @@ class PacedRankBackend(RankBackend):
 
 class StoreRankBackend(_ArenaStaging, RankBackend):
     """CPU stand-in of GpuRankBackend's data path for multi-rank tests: the same
-    window-staged image store (parallel/image_store.py, on a CPU device, all-gather
-    over the data group) feeding a deterministic 'classifier' of the image bytes
+    window-staged image store (parallel/image_store.py, on a CPU device, shipments and
+    flags over the gloo data group) feeding a deterministic 'classifier' of the image bytes
     (top-5 = a hash of the pixels). Exercises decode-once staging, arena eviction,
     version pinning and rejoin re-staging without a GPU."""
 
@@ -327,8 +334,9 @@ class StoreRankBackend(_ArenaStaging, RankBackend):
 class GpuRankBackend(_ArenaStaging, RankBackend):
     """Native engines for both models resident in this GPU's HBM, fed from per-model
     HBM image stores (parallel/image_store.py: store images staged in windows ahead of
-    dispatch, decoded once per job and replicated to every rank over the data group —
-    RCCL — plus seeded synthetic images). A batch is never gathered: the engines' stem
+    dispatch, decoded once per job by the rank that runs them and shipped HBM to HBM over
+    the data group — RCCL — only to another rank that re-uses them; plus seeded synthetic
+    images). A batch is never gathered: the engines' stem
     kernels read its images in place from the arena through a per-slot index table
     (Engine ``src_index``: written into pinned host memory, fetched into device memory by
     one tiny kernel in stream order — a host-memory read per stem workgroup made the stem
@@ -360,6 +368,10 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         self.stream = torch.cuda.Stream(device)
         self.stage_stream = torch.cuda.Stream(device)
         self._init_staging(loader, decode_threads)
+        import threading
+
+        self._dcache: "OrderedDict[str, np.ndarray]" = OrderedDict()   # name -> full-res RGB (both models)
+        self._dbytes, self.decode_hits, self._dlock = 0, 0, threading.Lock()
         self.host = [torch.zeros((2, self.cap, 5), dtype=torch.int32).pin_memory() for _ in range(SLOTS)]
         self.ev_done = [torch.cuda.Event() for _ in range(SLOTS)]
         self.fail_rows: List[Optional[List[int]]] = [None] * SLOTS
@@ -386,9 +398,35 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
                 self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=SLOTS, **src)
             self.engines[m].capture(self.stream)  # graphs now, before the service's first collective
 
+    DECODE_CACHE_BYTES = 1 << 30
+
+    def _decoded(self, name: str, data: bytes) -> np.ndarray:
+        """The full-resolution RGB decode of one store image, shared by both models' windows
+        (the JPEG is decoded once per rank, then resized per model: Keras load_img decodes,
+        converts to RGB, then resizes — the same steps in the same order, so the result is
+        byte-identical to serving.inference.load_image)."""
+        import io
+
+        from PIL import Image
+
+        with self._dlock:
+            hit = self._dcache.get(name)
+            if hit is not None:
+                self._dcache.move_to_end(name)
+                self.decode_hits += 1
+                return hit
+        img = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"), dtype=np.uint8)
+        with self._dlock:
+            self._dcache[name] = img
+            self._dbytes += img.nbytes
+            while self._dbytes > self.DECODE_CACHE_BYTES and self._dcache:
+                _, old = self._dcache.popitem(last=False)
+                self._dbytes -= old.nbytes
+        return img
+
     def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
         """(decode pool thread) fetch + decode this rank's share of a window."""
-        from ..serving.inference import load_image
+        from PIL import Image
 
         blobs = self.loader(names) if self.loader else {}
         hw = self.arenas[model].hw
@@ -399,7 +437,10 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
                 out[n] = None
                 continue
             try:
-                out[n] = load_image(b, hw)
+                img = self._decoded(n, b)
+                if img.shape[:2] != tuple(hw):  # Pillow NEAREST, as load_img(target_size)
+                    img = np.asarray(Image.fromarray(img).resize((hw[1], hw[0]), Image.NEAREST), dtype=np.uint8)
+                out[n] = img
             except Exception as e:  # undecodable file -> reported as failed
                 log.warning("decode of %s failed: %s", n, e)
                 out[n] = None

@@ -32,7 +32,7 @@ class RankControl:
     has been broadcast (committed on every rank)."""
 
     def __init__(self, grank: int, world: int, base_port: int, store_dir: str, host: str = "127.0.0.1",
-                 period: float = 0.1, ping_timeout: float = 0.1, suspect_timeout: float = 0.6,
+                 period: float = 0.1, ping_timeout: float = 0.1, suspect_timeout: float = 1.5,
                  replication: int = 4, on_dead: Optional[Callable[[int], None]] = None,
                  on_alive: Optional[Callable[[int], None]] = None, rejoin: bool = False):
         self.grank, self.world, self.base, self.host = grank, world, base_port, host
@@ -40,6 +40,7 @@ class RankControl:
         self.period, self.ping_timeout, self.suspect_timeout = period, ping_timeout, suspect_timeout
         self.on_dead, self.on_alive, self.rejoin = on_dead, on_alive, rejoin
         self.svc = None  # the CollectiveService it serves
+        self.loop_lag_max = 0.0  # the longest this thread's event loop was late for a 20 ms timer, s
         self.put_lat: List[float] = []  # output bundle PUT latencies (call -> every replica stored), s
         # output bundles spooled once for same-machine replicas (hard links, store/service.py);
         # DML_SPOOL_OUTPUTS=0: every replica pulls over the blob plane (A/B)
@@ -63,6 +64,15 @@ class RankControl:
             return int(name.rsplit(":", 1)[1]) - self.base
         except (ValueError, IndexError):
             return None
+
+    async def _lag_monitor(self, tick: float = 0.02) -> None:
+        """How late the loop runs a timer: SWIM acks share this loop with the store's request
+        handlers, so a handler that holds it past the suspicion timeout gets this rank declared
+        dead while it is alive."""
+        while True:
+            t = time.perf_counter()
+            await asyncio.sleep(tick)
+            self.loop_lag_max = max(self.loop_lag_max, time.perf_counter() - t - tick)
 
     # ------------------------------------------------------------ thread --
     def start(self, timeout: float = 30.0) -> "RankControl":
@@ -95,6 +105,7 @@ class RankControl:
                          suspect_timeout=self.suspect_timeout, cleanup_time=30.0, replication=self.replication,
                          meta={"prio": self.grank, "rank": self.grank})
         self.node = n = await Node(cfg).start()
+        spawn(self._lag_monitor(), self.loop)
         on = n.ep.on
         on(MsgType.SUBMIT_JOB_REQUEST, self._on_submit)
         on(MsgType.SET_BATCH_SIZE, self._on_batch_size)
@@ -352,9 +363,11 @@ class RankControl:
         from ..cluster.frames import MsgType
 
         if self._active():
+            p = fr.payload or {}
             with self.svc.coord.lock:
                 a = self.svc.coord.assignments()
-            await self.node.ep.reply(fr, MsgType.GET_ASSIGNMENTS_ACK, {"assignments": a})
+                h = self.svc.coord.recent(int(p.get("history", 16)), p.get("job_id"))
+            await self.node.ep.reply(fr, MsgType.GET_ASSIGNMENTS_ACK, {"assignments": a, "history": h})
 
     async def _on_status(self, fr) -> None:
         from ..cluster.frames import MsgType

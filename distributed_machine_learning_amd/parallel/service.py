@@ -74,6 +74,7 @@ replication, no stall of the control step. Epoch changes restart the staging.
 """
 from __future__ import annotations
 
+import gc
 import json
 import logging
 import os
@@ -82,7 +83,8 @@ import threading
 import time
 from collections import OrderedDict, deque
 from dataclasses import dataclass
-from typing import Callable, Dict, List, Optional, Tuple
+from itertools import islice
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -154,6 +156,13 @@ class ReplicatedCoordinator:
         self.lock = threading.RLock()      # control-thread readers (C1/C2/C5/status) vs the serve loop
         self.split_log: List[Tuple[float, Dict[str, int]]] = []   # (t, ranks per model) when the split changes
         self._last_split: Dict[str, int] = {}
+        # queued batch -> the rank its images are staged for (image windows, parallel/image_store.py):
+        # replicated like the rest (assign_affinity runs at the same point on every rank); the
+        # plan dispatches a batch to its affinity rank first
+        self.affinity: Dict[str, Dict[tuple, int]] = {m: {} for m in MODELS}
+        # C5 history: which rank ran each recent batch and the output file it stored (the
+        # reference named the worker in the file name, worker.py:1580; one name per batch here)
+        self.history: "deque[dict]" = deque(maxlen=4096)
 
     # ------------------------------------------------------------- log ----
     def apply(self, rec: dict) -> dict:
@@ -171,6 +180,7 @@ class ReplicatedCoordinator:
             self.jobs.restore(rec["jobs"], requeue_inprogress=True)
             self.inflight.clear()
             self.revoking.clear()
+            self.reset_affinity()
             return {}
         raise ValueError(f"unknown log record {op}")
 
@@ -183,6 +193,40 @@ class ReplicatedCoordinator:
 
     def outstanding(self, grank: int) -> int:
         return sum(1 for inf in self.inflight.values() if inf.rank == grank)
+
+    # ---------------------------------------------------------- affinity ----
+    def reset_affinity(self) -> None:
+        for a in self.affinity.values():
+            a.clear()
+
+    def assign_affinity(self, model: str, queued: Sequence[Batch], members: List[int]) -> Dict[tuple, int]:
+        """(every rank, same step, same inputs) give each of these queued batches that has
+        none the rank its images will be staged for: among the ranks running ``model`` now
+        (their latest dispatched batch), the one with the fewest batches of it in flight or
+        assigned; none while no rank runs the model (its first batches are staged when they
+        are dispatched). Returns the model's affinity map."""
+        aff = self.affinity[model]
+        todo = [b for b in queued if b.key not in aff]
+        if not todo:
+            return aff
+        last: Dict[int, str] = {}
+        load: Dict[int, int] = {}
+        for inf in self.inflight.values():   # dispatch order: the last one per rank wins
+            last[inf.rank] = inf.batch.model
+            if inf.batch.model == model:
+                load[inf.rank] = load.get(inf.rank, 0) + 1
+        running = [g for g in members if last.get(g) == model]
+        if not running:
+            return aff
+        load = {g: load.get(g, 0) for g in running}
+        for g in aff.values():
+            if g in load:
+                load[g] += 1
+        for b in todo:
+            g = min(running, key=lambda r: (load[r], r))
+            aff[b.key] = g
+            load[g] += 1
+        return aff
 
     # ---------------------------------------------------------- planning ----
     def plan(self, members: List[int]) -> Tuple[Dict[int, List[Batch]], List[Tuple[int, tuple]]]:
@@ -226,7 +270,7 @@ class ReplicatedCoordinator:
                 self.split_log.append((time.monotonic(), dict(have)))
         disp: Dict[int, List[Batch]] = {}
         revokes: List[Tuple[int, tuple]] = []
-        taken = {m: 0 for m in MODELS}
+        free: Dict[int, int] = {}
         for g in members:
             m = target[g]
             if self.preempt and cur[g] is not None and cur[g] != m:
@@ -240,12 +284,32 @@ class ReplicatedCoordinator:
             # (a revoke that comes too late - the batch was launched - overfills the
             # rank's queue by at most that batch)
             gone = {k for gg, k in revokes if gg == g} | self.revoking
-            free = self.depth - sum(1 for inf in mine[g] if inf.batch.key not in gone)
-            q = self.jobs.queues[m]
-            while free > 0 and taken[m] < len(q):
-                disp.setdefault(g, []).append(q[taken[m]])   # popped for real by apply_table
-                taken[m] += 1
-                free -= 1
+            free[g] = self.depth - sum(1 for inf in mine[g] if inf.batch.key not in gone)
+        # every free slot of this step lies within the first world x depth queued batches
+        head = {m: list(islice(self.jobs.queues[m], 0, len(members) * self.depth)) for m in MODELS}
+        used: set = set()
+
+        def take(g: int, want: Callable[[Batch], bool]) -> None:
+            for b in head[target[g]]:
+                if free[g] <= 0:
+                    return
+                if b.key not in used and want(b):
+                    disp.setdefault(g, []).append(b)   # popped for real by apply_table
+                    used.add(b.key)
+                    free[g] -= 1
+        # 1. the queued batches whose images are staged for this rank; 2. (queue order) the
+        # ones staged for no rank, or for a rank that now runs the other model or left;
+        # 3. a rank that would run dry takes any queued batch (its images are shipped to it)
+        for g in members:
+            aff = self.affinity[target[g]]
+            take(g, lambda b, g=g, aff=aff: aff.get(b.key) == g)
+        for g in members:
+            aff = self.affinity[target[g]]
+            take(g, lambda b, g=g, aff=aff: target.get(aff.get(b.key, -1)) != target[g])
+        low = self.depth - max(self.gpu_slots, self.depth // 4)
+        for g in members:
+            if free[g] > low:
+                take(g, lambda b: True)
         return disp, revokes
 
     def table(self, members: List[int], disp: Dict[int, List[Batch]]) -> np.ndarray:
@@ -269,6 +333,7 @@ class ReplicatedCoordinator:
                 b = self.jobs.pop_key(model, (int(table[r, d, 0]), int(table[r, d, 1])))
                 if b is None:
                     raise RuntimeError(f"replica diverged: batch {table[r, d, 0]}:{table[r, d, 1]} not queued")
+                self.affinity[model].pop(b.key, None)   # staged for the rank it now runs on
                 self.inflight[b.key] = Inflight(g, b, now, self.seq)
                 self.seq += 1
                 out.setdefault(g, []).append(b)
@@ -303,6 +368,8 @@ class ReplicatedCoordinator:
             return None
         b = inf.batch
         n = len(b.images)
+        self.history.append({"job_id": b.job_id, "batch_id": b.batch_id, "model": b.model, "rank": inf.rank,
+                             "output": output_name(b.job_id, b.batch_id, self.host_tag)})
         self.metrics.record(b.model, now - inf.t_dispatch, service or now - inf.t_dispatch, n)
         self.cost.observe(b.model, n, service or now - inf.t_dispatch)
         return b
@@ -327,8 +394,25 @@ class ReplicatedCoordinator:
                                                "batch_id": inf.batch.batch_id})
         return out
 
+    def recent(self, n: int = 16, job_id: Optional[int] = None) -> List[dict]:
+        """C5 history: the last ``n`` completed batches (of one job) with the rank that ran each."""
+        h = [e for e in self.history if job_id is None or e["job_id"] == job_id]
+        return h[-n:] if n > 0 else []
+
 
 STAGE_DEPTH = 8  # batches per rank whose images are staged ahead of dispatch (image windows)
+
+
+def rank_switch_interval() -> None:
+    """A rank process runs three Python threads that hand work to each other every batch —
+    the serve loop, the control plane's event loop (SWIM, the store, the output PUTs) and the
+    output writer. CPython hands the GIL to a waiting thread only every switch interval
+    (5 ms by default), so each of those hand-offs could cost milliseconds per batch: 0.5 ms
+    (DML_SWITCH_INTERVAL) measured 111 -> 196 batches/s per rank at world 2
+    (tools/store_capacity.py, 8-core container)."""
+    import sys
+
+    sys.setswitchinterval(float(os.environ.get("DML_SWITCH_INTERVAL", "0.0005")))
 
 
 def auto_depth(world: int) -> int:
@@ -360,8 +444,11 @@ class OutputWriter:
     def __init__(self, out_dir: Optional[str], put: Optional[Callable[[str, bytes], None]] = None,
                  host_tag: str = "node", threads: int = 1,
                  put_many_async: Optional[Callable[[List[Tuple[str, bytes]], Callable], None]] = None,
-                 bundle: int = 16, max_inflight: int = 4):
+                 bundle: Optional[int] = None, max_inflight: Optional[int] = None):
         self.out_dir, self.put, self.host_tag = out_dir, put, host_tag
+        # DML_OUT_BUNDLE / DML_OUT_INFLIGHT: bundle size cap and bundles in flight (A/B)
+        bundle = bundle or int(os.environ.get("DML_OUT_BUNDLE", "16"))
+        max_inflight = max_inflight or int(os.environ.get("DML_OUT_INFLIGHT", "4"))
         self.put_many_async, self.bundle = put_many_async, max(1, bundle)
         if out_dir:
             os.makedirs(out_dir, exist_ok=True)
@@ -513,8 +600,12 @@ class CollectiveService:
     def __init__(self, eg: ElasticGroup, backend: RankBackend, coord: ReplicatedCoordinator,
                  control=None, writer: Optional[OutputWriter] = None, kill_rank: int = -1, kill_at_step: int = -1,
                  on_device: bool = False, idle_sleep: float = 0.002, poll_sleep: float = 0.0002,
-                 watchdog_s: float = 0.0, rejoined: bool = False, kill_at_done: int = -1):
+                 watchdog_s: float = 0.0, rejoined: bool = False, kill_at_done: int = -1,
+                 stall: Tuple[int, int, float] = (-1, -1, 0.0)):
         self.eg, self.be, self.coord, self.control = eg, backend, coord, control
+        # fault injection (tests): (rank, step, seconds) - that rank's serve loop AND control
+        # plane freeze for that long at that step, alive but silent (a false SWIM suspicion)
+        self.stall = stall
         self.writer = writer
         # fault injection (tests, BASELINE config 5): rank kill_rank exits 17 at step
         # kill_at_step, or once kill_at_done batches have completed (replicated count)
@@ -529,6 +620,8 @@ class CollectiveService:
         self.steps = 0
         self.rebuilds = 0
         self.grows = 0
+        self.rejoins = 0   # times this live rank was removed and re-admitted (false suspicion)
+        self._frozen = False
         self.cap = backend.cap
         self.slots = getattr(backend, "slots", SLOTS)
         self.hostq: "deque[Batch]" = deque()             # dispatched to this rank, not launched
@@ -550,6 +643,9 @@ class CollectiveService:
         # queued batches staged ahead of dispatch (the in-flight ones are staged besides)
         self.stage_ahead = max(1, eg.world) * min(coord.depth, STAGE_DEPTH)
         self._rec_bufs: Dict[tuple, torch.Tensor] = {}   # the step's exchange output, per (world, L)
+        # a staging backend (image arenas): queued batches get an affinity rank, their images
+        # are staged there ahead of dispatch and the plan sends them there
+        self._targeted = hasattr(backend, "arenas")
         self.last_progress = time.monotonic()
         self.phase_s: Dict[str, float] = {"poll": 0.0, "plan": 0.0, "collective": 0.0, "apply": 0.0,
                                           "launch": 0.0, "sleep": 0.0}
@@ -717,7 +813,7 @@ class CollectiveService:
                 buf = torch.zeros(n, dtype=torch.uint8, device=self.dev)
                 if active:
                     buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
-                eg.broadcast(buf, src=root)
+                eg.broadcast_bytes(buf, src=root)
                 if not active:
                     applied_here = json.loads(bytes(buf.cpu().numpy()).decode())
         except CollectiveFailure:
@@ -789,6 +885,11 @@ class CollectiveService:
                                            0 <= self.kill_at_done <= self.completed):
             log.warning("rank %d: injected kill at step %d (%d batches done)", eg.grank, self.steps, self.completed)
             os._exit(17)
+        if eg.grank == self.stall[0] and self.steps == self.stall[1]:
+            log.warning("rank %d: injected stall of %.1f s at step %d", eg.grank, self.stall[2], self.steps)
+            if self.control is not None and self.control.loop is not None:
+                self.control.loop.call_soon_threadsafe(time.sleep, self.stall[2])
+            time.sleep(self.stall[2])
         # own new batches, then the revoke requests addressed to this rank (host queue only)
         self.hostq.extend(mine)
         for g, key in rq:
@@ -816,18 +917,42 @@ class CollectiveService:
 
     def _stage(self) -> None:
         """(every rank, same step, coordinator lock held) stage the images of the batches
-        in flight and of the next ``stage_ahead`` queued batches of each model, in
-        dispatch order (parallel/image_store.py): identical decisions everywhere."""
+        in flight - for the rank running each - and of the next ``stage_ahead`` queued
+        batches of each model - for their affinity rank - in dispatch order
+        (parallel/image_store.py): identical decisions everywhere."""
         coord = self.coord
+        members = self.eg.members
         for m in MODELS:
-            cand = [inf.batch for inf in coord.inflight.values() if inf.batch.model == m]
-            q = coord.jobs.queues[m]
-            cand += [q[i] for i in range(min(len(q), self.stage_ahead))]
+            cand, where = [], {}
+            for inf in coord.inflight.values():
+                if inf.batch.model == m:
+                    cand.append(inf.batch)
+                    where[inf.batch.key] = inf.rank
+            if self._targeted:
+                ahead = list(islice(coord.jobs.queues[m], 0, self.stage_ahead))
+                aff = coord.assign_affinity(m, ahead, members)
+                for b in ahead:
+                    g = aff.get(b.key)
+                    if g is not None:
+                        cand.append(b)
+                        where[b.key] = g
             if cand:
-                self.be.stage(m, cand)
+                self.be.stage(m, cand, where)
 
     # -------------------------------------------------------------- serve --
+    def freeze_heap(self) -> None:
+        """Everything set up so far (torch, the engines, the arenas' bookkeeping) is
+        long-lived: moved out of the cyclic collector's generations, a full collection no
+        longer walks it (measured ~100 ms per pass over ~175k objects with the GIL held -
+        every thread of the rank, its SWIM acks included, stalls for it). Once per process;
+        serve() calls it if the caller did not (benches call it before their timer)."""
+        if not self._frozen:
+            gc.collect()
+            gc.freeze()
+            self._frozen = True
+
     def serve(self, max_steps: int = 10 ** 9, stop_when_idle: bool = False) -> int:
+        self.freeze_heap()
         while self.steps < max_steps:
             try:
                 if not self.step(stop_when_idle):
@@ -858,6 +983,8 @@ class CollectiveService:
         # afresh over the new group (a joiner's arena is empty; survivors' collectives of
         # the failed epoch were aborted)
         self.be.reset_staging()
+        with self.coord.lock:
+            self.coord.reset_affinity()
         self.be.attach(self.eg)
         # the new coordinator's state is authoritative: replicas that completed one
         # step more or less than it did are repaired by a state record (and a
@@ -878,6 +1005,9 @@ class CollectiveService:
             self._recovering_since = self.last_ok_t
         was = self.coordinator_rank()
         self._reset_local()
+        if "removed from the group" in str(e) and self.control is not None:
+            self._rejoin_alive()  # the others fixed the next epoch without this (live) rank
+            return
         for attempt in range(5):
             deadline = time.monotonic() + 10
             while not (eg.dead & set(eg.members)) and time.monotonic() < deadline:
@@ -886,10 +1016,28 @@ class CollectiveService:
                 eg.rebuild(set(eg.dead))  # aborts the communicator first (RCCL: ncclCommAbort)
                 break
             except CollectiveFailure as e2:
+                if "removed from the group" in str(e2) and self.control is not None:
+                    self._rejoin_alive()
+                    return
                 if "removed from the group" in str(e2) or attempt == 4:
                     raise
                 log.warning("rank %d: rebuild failed (%s); retrying with the updated dead set", eg.grank, e2)
         self.rebuilds += 1
+        self._after_epoch(was)
+
+    def _rejoin_alive(self) -> None:
+        """The others removed this live rank (SWIM suspected it past the timeout while it was
+        stalled). Its control plane refutes the suspicion, the coordinator admits it again
+        (a SWIM rejoin), and it re-enters as a re-joined process: replica empty until the
+        coordinator's state record, its queued and in-flight work already requeued."""
+        eg = self.eg
+        log.warning("rank %d: removed from the group while alive; waiting for re-admission", eg.grank)
+        was = self.coordinator_rank()
+        eg.rejoin(timeout_s=120.0)
+        self.rejoined = True
+        self.unsynced = {eg.grank} | (set(eg.members) - set(eg.prev_members))
+        self.done.clear()   # reports of the epoch this rank left: requeued by the others
+        self.rejoins += 1
         self._after_epoch(was)
 
     def _grow(self, joiners: List[int]) -> None:
@@ -898,7 +1046,12 @@ class CollectiveService:
         was = self.coordinator_rank()
         log.warning("rank %d: admitting ranks %s into epoch %d", eg.grank, joiners, eg.epoch + 1)
         self._reset_local()
-        eg.grow(sorted(set(eg.members) | set(joiners)))
+        try:
+            eg.grow(sorted(set(eg.members) | set(joiners)))
+        except CollectiveFailure:
+            raise
+        except Exception as e:  # a joiner that never arrived (it died again): rebuild without it
+            raise CollectiveFailure(f"epoch {eg.epoch} growth failed: {e}") from e
         self.grows += 1
         self._after_epoch(was)
 

@@ -32,11 +32,47 @@ def _pcts(xs) -> dict:
             "max": round(float(a.max()), 2), "n": len(xs)}
 
 
+def make_jpegs(n: int, seed: int = 0) -> List[Tuple[str, bytes]]:
+    """``n`` distinct JPEGs shaped like the reference's ``testfiles/`` (height 300, width
+    169-300, ~12 KB): deterministic structured photos — a base colour, two
+    low-frequency gratings and pixel noise — so that decoding costs what a real file costs."""
+    import io
+
+    import numpy as np
+    from PIL import Image
+
+    g = np.random.default_rng(seed)
+    out = []
+    yy = np.linspace(0.0, 1.0, 300, dtype=np.float32)[:, None]
+    noise = g.normal(0, 6, (300, 900, 3)).astype(np.float32)  # one field, a random window per image
+    for i in range(n):
+        w = int(g.integers(169, 301))
+        xx = np.linspace(0.0, 1.0, w, dtype=np.float32)[None, :]
+        base = g.uniform(40, 215, 3).astype(np.float32)
+        f1, f2 = g.uniform(1, 6, 2)
+        ph = g.uniform(0, 6.28, 2)
+        img = np.empty((300, w, 3), np.float32)
+        for c in range(3):
+            img[..., c] = (base[c] + 35 * np.sin(6.28 * f1 * xx + ph[0] + c) + 30 * np.cos(6.28 * f2 * yy + ph[1] - c))
+        x0 = int(g.integers(0, 900 - w))
+        img += noise[:, x0:x0 + w]
+        buf = io.BytesIO()
+        Image.fromarray(np.clip(img, 0, 255).astype(np.uint8)).save(buf, format="JPEG", quality=90)
+        out.append((f"img_{i:05d}.jpeg", buf.getvalue()))
+    return out
+
+
 def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images: int, inception_images: int,
         batch_sizes: Dict[str, int], out_dir: Optional[str], kills: Sequence[Tuple[int, int]] = (),
         comm: str = "gloo", depth: int = 0, single_rates: Optional[Dict[str, float]] = None,
-        make_backend=None, data_backend: str = "nccl") -> Optional[dict]:
-    """One rank of the service run; returns the record (on every surviving rank)."""
+        make_backend=None, data_backend: str = "nccl", store_images: int = 0,
+        decode_threads: int = 0) -> Optional[dict]:
+    """One rank of the service run; returns the record (on every surviving rank).
+    ``store_images`` > 0: the jobs read REAL store images instead of the seeded synthetic
+    arena — that many distinct JPEGs are PUT into the replicated store first (outside the
+    timed region) and each job picks cyclically over them (worker.py:196-206), so every
+    window of images is fetched from the store, decoded once in the whole job and
+    replicated to the ranks' HBM arenas (parallel/image_store.py) on the timed path."""
     import torch
     import torch.distributed as dist
 
@@ -44,13 +80,28 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
     from .elastic import ElasticGroup
     from .rank_backend import GpuRankBackend
     from .rank_control import RankControl
-    from .service import CollectiveService, OutputWriter, ReplicatedCoordinator
+    from .service import CollectiveService, OutputWriter, ReplicatedCoordinator, rank_switch_interval
 
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")  # aborts are ours (parallel/elastic.py)
+    rank_switch_interval()
     cap = max(batch_sizes.values())
     t_build = time.perf_counter()
-    backend = (make_backend() if make_backend is not None else
-               GpuRankBackend(device, batch_sizes, cap=cap, arena_images=4 * cap, n_synth=2 * cap))
+    from .service import STAGE_DEPTH, auto_depth
+    from ..utils import numa
+
+    depth = depth or auto_depth(world)
+    # store images: room for every distinct image next to the pinned in-flight and staged batches
+    arena = max(4 * cap, store_images + world * (depth + min(depth, STAGE_DEPTH)) * cap) if store_images else 4 * cap
+    decode_threads = decode_threads or numa.host_threads(share=1, cap=32)
+    loader = {}   # the store loader exists once the control plane runs (below)
+    lazy_loader = lambda names: loader["fn"](names)  # noqa: E731
+    if make_backend is not None:  # a factory may take the (lazy) store loader
+        import inspect
+
+        backend = make_backend(lazy_loader) if inspect.signature(make_backend).parameters else make_backend()
+    else:
+        backend = GpuRankBackend(device, batch_sizes, cap=cap, arena_images=arena, n_synth=2 * cap,
+                                 loader=lazy_loader, decode_threads=decode_threads)
     eg = ElasticGroup(rank, world, store_path=rdzv, backend=comm, device=device if comm == "nccl" else None,
                       timeout_s=120, data_backend=data_backend, shm_exchange=(comm == "gloo"))
     # the product's control plane (serving/rank_main.py): SWIM + election + the replicated
@@ -58,19 +109,36 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
     store_root = os.path.join(os.environ.get("DML_RDZV_DIR", "/tmp"), os.path.basename(rdzv) + "_store")
     ctl = RankControl(rank, world, swim_base, store_dir=os.path.join(store_root, f"rank{rank}"),
                       replication=min(4, world), on_dead=eg.dead.add, on_alive=eg.joiners.add).start()
+    loader["fn"] = ctl.store_loader
     kr, kd = -1, -1   # kills: (rank, batches completed when it dies)
     for r, d in kills:
         if r == rank:
             kr, kd = r, d
-    from .service import auto_depth
-
-    depth = depth or auto_depth(world)
     coord = ReplicatedCoordinator(batch_sizes, cap=cap, host_tag="mi355x", depth=depth)
     writer = OutputWriter(os.path.join(out_dir, f"rank{rank}") if out_dir else None,
                           put_many_async=ctl.store_put_many_async, host_tag="mi355x")
     svc = CollectiveService(eg, backend, coord, control=ctl, writer=writer, kill_rank=kr, kill_at_done=kd,
                             on_device=(comm == "nccl"), watchdog_s=300)
-    if svc.is_coordinator():
+    put_s = 0.0
+    if store_images:
+        # the JPEGs go into the replicated store first (not timed): the coordinator PUTs them
+        # in bundles, every rank then waits at a barrier before the jobs are submitted
+        from ..serving.jobs import pick_images
+
+        if svc.is_coordinator():
+            t_put = time.perf_counter()
+            files = make_jpegs(store_images, seed=11)
+            for i in range(0, len(files), 128):
+                ok, bad, err = ctl.call(ctl.node.store.put_many(files[i:i + 128]), timeout=120)
+                if bad:
+                    raise RuntimeError(f"store PUT of the bench images failed: {err}")
+            put_s = time.perf_counter() - t_put
+            names = ctl.pin_versions(sorted(n for n, _ in files))
+            if resnet_images:
+                svc.submit_local("ResNet50", images=pick_images(names, resnet_images))
+            if inception_images:
+                svc.submit_local("InceptionV3", images=pick_images(names, inception_images))
+    elif svc.is_coordinator():
         if resnet_images:
             svc.submit_local("ResNet50", resnet_images)
         if inception_images:
@@ -86,6 +154,7 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         build_s = time.perf_counter() - t_build
+        svc.freeze_heap()
         eg.barrier()
         t0 = time.perf_counter()
         steps = svc.serve(stop_when_idle=True)   # drains the writer: every output file is on disk
@@ -97,7 +166,12 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
         if eg.backend == "gloo":
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0])
-        served = torch.tensor([svc.served_here, writer.written, writer.failed, writer.bytes], dtype=torch.int64)
+        ar = getattr(backend, "arenas", {})
+        served = torch.tensor([svc.served_here, writer.written, writer.failed, writer.bytes,
+                               int(ctl.loop_lag_max * 1e6),
+                               sum(a.decoded for a in ar.values()), sum(a.replicated for a in ar.values()),
+                               sum(a.received for a in ar.values()),
+                               sum(a.received * a.hw[0] * a.hw[1] * 3 for a in ar.values())], dtype=torch.int64)
         allsv = [torch.zeros_like(served) for _ in range(eg.world)]
         if eg.backend == "gloo":
             dist.all_gather(allsv, served)
@@ -136,12 +210,32 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                 "steps": steps, "max_batches_per_step": svc.batches_per_step_max,
                 "rebuilds": svc.rebuilds, "preempted_batches": coord.preempted, "requeued_batches": coord.requeued,
                 "kill_to_redispatch_s": [round(x, 3) for x in svc.recoveries_s],
+                "control_loop_lag_max_ms": {f"rank{g}": round(int(v[4]) / 1e3, 1) for g, v in zip(eg.members, allsv)},
                 "kills": [f"{r}:{d}" for r, d in kills], "final_members": eg.members,
                 "jobs_done": all(j.done for j in coord.jobs.jobs.values()),
                 "loop_phase_s": {k: round(v, 4) for k, v in svc.phase_s.items()},
                 "comm": comm, "depth": depth, "build_s": round(build_s, 1),
                 "data": "synthetic uint8 images (seeded HBM arena), random-init weights",
             }
+            if store_images:
+                col = lambda i: [int(v[i]) for v in allsv]  # noqa: E731 - per rank, member order
+                dec = sum(col(5))
+                rec["data"] = (f"{store_images} distinct synthetic JPEGs (300 x 169-300, like testfiles/) in the "
+                               "replicated store; jobs pick cyclically over them; random-init weights")
+                rec["store_path"] = {
+                    "distinct_images": store_images, "put_s_untimed": round(put_s, 2),
+                    "decode_threads": decode_threads,
+                    # whole job: each image decoded once, by the first rank that runs it
+                    "decoded": dec, "decode_rate_img_s": round(dec / el, 1),
+                    "decoded_per_rank": col(5),
+                    "windows_staged_coordinator": int(sum(a.windows_staged for a in ar.values())),
+                    "resident_arrivals_per_rank": col(6),
+                    # targeted staging: rows shipped HBM to HBM to a rank that re-used an image
+                    # another rank held (no all-gather to every rank)
+                    "shipped_images_per_rank": col(7), "shipped_bytes": sum(col(8)),
+                    "evictions_coordinator": int(sum(a.evictions for a in ar.values())),
+                    "decode_cache_hits_coordinator": int(getattr(backend, "decode_hits", 0)),
+                }
             if single_rates:
                 # the same images served one model after the other at the single-model rates
                 serial = sum(n[m] / single_rates[m] for m in MODELS if single_rates.get(m))

@@ -6,7 +6,8 @@ Kept command-for-command:
   C3 <model> <batch>      set the per-model batch size on the coordinator
   submit-job <model> <N>  (C4) submit a job; prints the job id
   get-output <jobid>      (C4) merge output_<jobid>_*.json -> final_<jobid>.json
-  C5                      current assignments {worker: {model, job_id, batch_id}}
+  C5 [n [job]]            current assignments {worker: {model, job_id, batch_id}}; on the rank
+                          service also the last n completed batches with the rank that ran each
   predict-locally <model> <jobid> <N|[a.jpeg,b.jpeg]>
   put <local> <sdfs> | get <sdfs> <local> | get-all <pattern> <dir> | delete <sdfs>
   ls <sdfs> | ls-all <pattern> | store | get-versions <sdfs> <n> <local>
@@ -78,8 +79,20 @@ class Cli:
             r = await n.leader_request(MsgType.SET_BATCH_SIZE, {"model": a[0], "batch_size": int(a[1])})
             return "leader unreachable" if r is None else f"batch size of {a[0]} set to {a[1]}"
         if c == "C5":
-            r = await n.leader_request(MsgType.GET_ASSIGNMENTS)
-            return "leader unreachable" if r is None else json.dumps(r.payload["assignments"], indent=2)
+            # "C5" / "C5 <n>" / "C5 <n> <job>": the running assignments, plus (rank service) the
+            # last n completed batches with the rank that ran each and its output file
+            req = {"history": int(a[0]) if a else 16}
+            if len(a) > 1:
+                req["job_id"] = int(a[1])
+            r = await n.leader_request(MsgType.GET_ASSIGNMENTS, req)
+            if r is None:
+                return "leader unreachable"
+            out = json.dumps(r.payload["assignments"], indent=2)
+            if r.payload.get("history"):
+                out += "\nrecent batches:\n" + "\n".join(
+                    f"  job {e['job_id']} batch {e['batch_id']} ({e['model']}) ran on rank {e['rank']} -> {e['output']}"
+                    for e in r.payload["history"])
+            return out
         if cmd == "submit-job":
             jid = await n.submit_job(a[0], int(a[1]))
             return "submit failed (no leader)" if jid is None else f"submitted job {jid}"

@@ -136,7 +136,7 @@ def rank_main(a: argparse.Namespace) -> int:
     from ..parallel.elastic import ElasticGroup
     from ..parallel.rank_backend import FakeRankBackend, GpuRankBackend, HostRankBackend, StoreRankBackend
     from ..parallel.rank_control import RankControl
-    from ..parallel.service import CollectiveService, OutputWriter, ReplicatedCoordinator
+    from ..parallel.service import CollectiveService, OutputWriter, ReplicatedCoordinator, rank_switch_interval
     from .inference import CpuBackend
 
     if not a.rdzv or not a.base_port:
@@ -144,6 +144,7 @@ def rank_main(a: argparse.Namespace) -> int:
     bs = {"ResNet50": a.batch_resnet, "InceptionV3": a.batch_inception}
     cap = max(bs.values())
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")  # aborts are ours (parallel/elastic.py)
+    rank_switch_interval()
     dev = None
     if a.backend == "gpu":
         dev = torch.device("cuda", grank % max(torch.cuda.device_count(), 1))

@@ -15,6 +15,7 @@ of round 3, on CPU (gloo):
 import asyncio
 import json
 import os
+import re
 import signal
 import socket
 import subprocess
@@ -133,6 +134,11 @@ def test_launcher_cli_roundtrip_and_version_pinning(tmp_path):
     assert [e[2] for e in f2["3.jpeg"][0]] == [float(v) for v in pr]
     c1 = json.loads(out["c1"].split("\n[")[0])
     assert c1["ResNet50"]["query_count"] == 24
+    # C5 history: which rank ran each recent batch, and its output file
+    ran = re.findall(r"job (\d+) batch (\d+) \(ResNet50\) ran on rank (\d) -> (output_\S+)", out["c5"])
+    assert {(j, b) for j, b, _, _ in ran} == {("31", "1"), ("31", "2"), ("31", "3"), ("32", "1"), ("32", "2"),
+                                              ("32", "3")}, out["c5"]
+    assert all(int(g) < world and o.startswith(f"output_{j}_{b}_") for j, b, g, o in ran)
     assert rc == 0, log
 
 
@@ -305,6 +311,46 @@ def test_service_bench_record_world2(tmp_path):
     assert set(r0["batches_per_rank"]) == {"rank0", "rank1"} and sum(r0["batches_per_rank"].values()) == 80
     assert r0["value"] > 0 and r0["p90_latency_ms"]["ResNet50"] >= r0["p50_latency_ms"]["ResNet50"]
     assert not os.path.exists(tmp_path / "svc_out")            # rank 0 removed the output files
+
+
+def _svc_store_rank(grank, world, rdzv, port, out):
+    from distributed_machine_learning_amd.parallel import service_bench
+    from distributed_machine_learning_amd.parallel.rank_backend import StoreRankBackend
+
+    rec = service_bench.run(grank, world, None, rdzv, port, 256, 128, {"ResNet50": 16, "InceptionV3": 8}, None,
+                            make_backend=lambda loader: StoreRankBackend(loader=loader, cap=16, arena_images=256,
+                                                                         n_synth=16),
+                            data_backend="gloo", store_images=48)
+    with open(os.path.join(out, f"svc_store_{grank}.json"), "w") as f:
+        json.dump(rec, f)
+
+
+def test_service_bench_store_images_world2(tmp_path):
+    """bench.py's `store_images_pass`: the jobs read real JPEGs
+    PUT into the replicated store — each window fetched over the store's blob plane,
+    decoded once in the whole job (its images split between the ranks) and all-gathered
+    into both ranks' arenas — and every batch completes with its output stored."""
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_svc_store_rank, args=(r, 2, str(tmp_path / "rdzv"), port, str(tmp_path)))
+          for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(240)
+    assert [p.exitcode for p in ps] == [0, 0]
+    r0 = json.load(open(tmp_path / "svc_store_0.json"))
+    assert r0["jobs_done"] and r0["images"] == {"ResNet50": 256, "InceptionV3": 128}
+    assert r0["outputs"]["files_stored"] == 16 + 16 and r0["outputs"]["failed"] == 0
+    sp = r0["store_path"]
+    assert sp["distinct_images"] == 48 and sp["windows_staged_coordinator"] >= 2
+    # each model's 48 distinct images were decoded once in the whole job, by the rank that
+    # first ran them; a rank re-using an image the other rank held got it shipped (targeted
+    # staging: arrivals = its own decodes + its shipments, never an all-gather to both)
+    assert sp["decoded"] == 2 * 48
+    for d, a, sh in zip(sp["decoded_per_rank"], sp["resident_arrivals_per_rank"], sp["shipped_images_per_rank"]):
+        assert a == d + sh and a <= 2 * 48
+    assert sp["shipped_bytes"] == sum(sp["shipped_images_per_rank"]) * 8 * 8 * 3   # StoreRankBackend hw (8, 8)
 
 
 # ------------------------------------------------- jobs larger than the arena --

@@ -15,4 +15,9 @@ for path in sys.argv[1:]:
         parts.append(f"{m} {r['value']:.0f}")
     if d.get("service"):
         parts.append(f"service {d['service'].get('value', 0):.0f}")
+        sp = d["service"].get("store_images_pass")
+        if sp:
+            parts.append(f"store-images {sp.get('value', 0):.0f} (x{sp.get('vs_synthetic_service')}, "
+                         f"decode {sp.get('store_path', {}).get('decode_rate_img_s')}/s)" if "value" in sp
+                         else f"store-images error {sp.get('error', '')[:120]}")
     print(f"{path}: " + "  ".join(parts))

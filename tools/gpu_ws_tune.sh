@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 cp distributed_machine_learning_amd/tuning/conv_tuning.json /tmp/table_old.json
-ADD=${ADD:-100,101,102,103,104,105,106,107,108,109,110,111,112}
+ADD=${ADD:-100,101,102,103,104,105,106,107,108,109,110,111,112,120,121,122,123,124,125,126,127,128,129}
 STEPS=${STEPS:-20}
 DML_TUNE_ADD=$ADD timeout -k 10 900 python -u bench.py --steps $STEPS --warmup 5 --no-service > gpurun_out/tune_bench.log 2>&1 || { tail -30 gpurun_out/tune_bench.log; exit 1; }
 python tools/bench_summary.py gpurun_out/tune_bench.log
