@@ -199,6 +199,13 @@ int dml_conv_ws_init(void);
 int dml_conv_wsp(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_wsp_bn(int cfg);
 int dml_conv_wsp_init(void);
+// patch-stationary stride-1 implicit GEMM (conv_igemm_pt.hip; cfg ids 140..159): the activation
+// patch of an M tile (whole output rows / images) is DMA'd once per channel chunk and read
+// at a per-tap offset; refuses convs it cannot run (stride / dilation != 1, Cin % BK, split-K)
+int dml_conv_pt(const DmlConvArgs* a, int cfg, hipStream_t s);
+int dml_conv_pt_bn(int cfg);
+int dml_conv_pt_fits(const DmlConvArgs* a, int cfg);
+int dml_conv_pt_init(void);
 int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);

@@ -6,7 +6,8 @@
 // models.py:26,51 — it has no kernel of its own). cfg ids 10..63 select a v2
 // tile configuration (dml_conv_v2), ids 100..119 a warp-specialised one (loader +
 // MFMA waves, dml_conv_ws, conv_igemm_ws.hip), ids 120..139 its persistent form
-// (dml_conv_wsp, conv_igemm_wsp.hip); they are part of the ABI the plan builder and the
+// (dml_conv_wsp, conv_igemm_wsp.hip), ids 140..159 the patch-stationary stride-1 tiles
+// (dml_conv_pt, conv_igemm_pt.hip); they are part of the ABI the plan builder and the
 // autotuner (ops/tuning.py) use.
 //
 // Removed (measured never faster, kept only as history in DESIGN.md and
@@ -24,7 +25,8 @@
 static int validate(const DmlConvArgs* a, int cfg) {
   const int bn = dml_conv_v2_bn(cfg);
   if (bn <= 0) {
-    dml_set_error("dml_conv: cfg must be a tile config (v2: 10..63, warp-specialised: 100..119, persistent: 120..139)");
+    dml_set_error("dml_conv: cfg must be a tile config (v2: 10..63, warp-specialised: 100..119, persistent: "
+                  "120..139, patch-stationary: 140..159)");
     return -1;
   }
   // weights are packed with Cout padded to a multiple of 256 rows; a 96- or
@@ -54,6 +56,7 @@ static int validate(const DmlConvArgs* a, int cfg) {
 
 extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
   if (validate(a, cfg) != 0) return -1;
+  if (cfg >= 140) return dml_conv_pt(a, cfg, s);
   if (cfg >= 120) return dml_conv_wsp(a, cfg, s);
   return cfg >= 100 ? dml_conv_ws(a, cfg, s) : dml_conv_v2(a, cfg, s);
 }

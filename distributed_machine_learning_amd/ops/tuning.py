@@ -28,6 +28,10 @@ WS_CFGS = tuple(range(100, 119))
 # their persistent form (csrc/kernels/conv_igemm_wsp.hip: one operand ring over a workgroup's
 # whole tile list; no split-K)
 WSP_CFGS = tuple(range(120, 130))
+# patch-stationary stride-1 tiles (csrc/kernels/conv_igemm_pt.hip: the activation patch of an
+# M tile of whole output rows is loaded once per channel chunk, r5); they refuse what they
+# cannot run (stride / dilation != 1, Cin % 64, a patch larger than the config's)
+PT_CFGS = (140, 141, 142, 143)
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))
@@ -90,6 +94,8 @@ def valid_cfgs(a: N.ConvArgs) -> List[int]:
     ex = _excluded()
     cands = [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)] + (list(LATE_RES_CFGS) if a.res else [])
     cands += list(WS_CFGS) + ([] if a.ksplit > 1 else list(WSP_CFGS))
+    if a.ksplit <= 1 and a.sh == 1 and a.sw == 1 and max(a.dh, 1) == 1 and max(a.dw, 1) == 1 and a.Cin % 64 == 0:
+        cands += list(PT_CFGS)
     return [c for c in cands if c not in ex]
 
 

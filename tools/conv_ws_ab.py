@@ -30,7 +30,8 @@ SHAPES = [  # name, batch, h, w, cin, cout, kh, kw, stride, ph, pw, residual
     ("inc_m3_3x3s2", 64, 35, 35, 288, 384, 3, 3, 2, 0, 0, 0),
 ]
 V2_DEFAULT = "11,12,14,15,24,25,26,28,30,31,32,33,38"
-WS_DEFAULT = "100,101,102,103,104,105,106,107,108,109,110,111,112,120,121,122,123,124,125,126,127,128,129"
+WS_DEFAULT = ("100,101,102,103,104,105,106,107,108,109,110,111,112,113,114,115,116,117,118,"
+              "120,121,122,123,124,125,126,127,128,129,140,141,142,143")
 
 
 def main():
@@ -79,7 +80,11 @@ def main():
             torch.cuda.synchronize()
             outs[c] = (y, ar)
         ref_cfg = next(c for c in v2 if c in outs)
-        mism = [c for c in outs if not torch.equal(outs[c][0], outs[ref_cfg][0])]
+        # the patch-stationary tiles (140..) sum K chunk-major: equal to the v2 tile within bf16
+        # rounding, not bit for bit; every other tile must be bit-identical
+        refy = outs[ref_cfg][0].float()
+        close = lambda c: ((outs[c][0].float() - refy).abs().max() / (refy.abs().max() + 1e-6)).item() < 1e-2  # noqa: E731
+        mism = [c for c in outs if not (torch.equal(outs[c][0], outs[ref_cfg][0]) or (c >= 140 and close(c)))]
         if mism:
             bad += 1
         for _ in range(a.rounds):

@@ -35,9 +35,52 @@ def _free_udp_base(n: int) -> int:
     raise RuntimeError("no port")
 
 
+class _ThreadCpu:
+    """CPU seconds of every thread of this process (/proc/self/task/*/stat utime + stime),
+    snapshotted every 0.2 s (threads end before the run returns), named by the Python thread
+    that owns it (others: gloo / native pools)."""
+
+    def __init__(self):
+        import threading
+
+        self.last, self.names, self.stop = {}, {}, threading.Event()
+        self.hz = os.sysconf("SC_CLK_TCK")
+        self.t = threading.Thread(target=self._run, daemon=True, name="cpu-snap")
+        self.t.start()
+
+    def _snap(self):
+        import threading
+
+        for t in threading.enumerate():
+            if t.native_id is not None:
+                self.names[t.native_id] = t.name.split(" ")[0].rstrip("-0123456789")
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                st = open(f"/proc/self/task/{tid}/stat").read().rsplit(")", 1)[1].split()
+            except OSError:
+                continue
+            self.last[int(tid)] = (int(st[11]) + int(st[12])) / self.hz
+
+    def _run(self):
+        while not self.stop.wait(0.2):
+            self._snap()
+
+    def result(self) -> dict:
+        self.stop.set()
+        self.t.join()
+        self._snap()
+        out = {}
+        for tid, cpu in self.last.items():
+            name = self.names.get(tid, "native")
+            out[name] = round(out.get(name, 0.0) + cpu, 2)
+        return out
+
+
 class _Sampler:
     """Where every Python thread of a rank is, sampled every 2 ms (DML_SAMPLE_RANK=<rank>):
-    the innermost frame and its caller per thread, counted - waits included."""
+    the innermost frame and three callers per thread, counted; blocked frames skipped."""
+
+    IDLE = {"wait", "select", "_worker", "get", "_watch", "acquire", "sleep"}
 
     def __init__(self, dt: float = 0.002):
         import collections
@@ -58,11 +101,15 @@ class _Sampler:
             for tid, f in sys._current_frames().items():
                 if tid == me:
                     continue
+                if f.f_code.co_name in self.IDLE:
+                    continue   # blocked (a wait, a select, an idle pool worker): not CPU
                 top = f"{os.path.basename(f.f_code.co_filename)}:{f.f_code.co_name}:{f.f_lineno}"
-                up = f.f_back
-                caller = f"{os.path.basename(up.f_code.co_filename)}:{up.f_code.co_name}" if up else ""
+                chain, up = [], f.f_back
+                while up is not None and len(chain) < 3:
+                    chain.append(f"{os.path.basename(up.f_code.co_filename)}:{up.f_code.co_name}")
+                    up = up.f_back
                 name = self.names.get(tid, str(tid)).split("_")[0].rstrip("-0123456789")
-                self.counts[(name, top, caller)] += 1
+                self.counts[(name, top, " <- ".join(chain))] += 1
 
     def report(self, n: int = 40):
         self.stop.set()
@@ -72,7 +119,7 @@ class _Sampler:
             per[name] = per.get(name, 0) + c
         print("sampled threads:", per, file=sys.stderr)
         for (name, top, caller), c in self.counts.most_common(n):
-            print(f"{c:7d} {100.0 * c / per[name]:5.1f}%  {name:24s} {top:55s} <- {caller}", file=sys.stderr)
+            print(f"{c:6d} {100.0 * c / per[name]:5.1f}%  {name:14s} {top:48s} <- {caller}", file=sys.stderr)
 
 
 def _rank(rank, world, rdzv, port, batches, rate, out_json, depth=0):
@@ -94,6 +141,7 @@ def _rank(rank, world, rdzv, port, batches, rate, out_json, depth=0):
             gcp["max"], gcp["n"], gcp["total"] = max(gcp["max"], d), gcp["n"] + 1, gcp["total"] + d
     gc.callbacks.append(_gc_cb)
     sampler = _Sampler() if os.environ.get("DML_SAMPLE_RANK") == str(rank) else None
+    tcpu = _ThreadCpu()
     t0, c0 = time.perf_counter(), time.process_time()
     prof = None
     if os.environ.get("DML_PROFILE_RANK") == str(rank):  # cProfile of this rank's serve-loop thread
@@ -105,13 +153,17 @@ def _rank(rank, world, rdzv, port, batches, rate, out_json, depth=0):
                             make_backend=lambda: PacedRankBackend(cap=256, batches_per_s=rate))
     if sampler is not None:
         sampler.report()
+
     if prof is not None:
         import pstats
         prof.disable()
-        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
+        st = pstats.Stats(prof, stream=sys.stderr)
+        st.sort_stats("tottime").print_stats(30)
+        st.print_callers("acquire|exchange|_poll")
+    threads = tcpu.result()
     with open(f"{out_json}.cpu{rank}", "w") as f:  # this rank's CPU seconds (all its threads), GC pauses
         json.dump({"cpu_s": time.process_time() - c0, "gc_max_ms": gcp["max"] * 1e3, "gc_n": gcp["n"],
-                   "gc_total_ms": gcp["total"] * 1e3, "objects": len(gc.get_objects())}, f)
+                   "gc_total_ms": gcp["total"] * 1e3, "objects": len(gc.get_objects()), "threads": threads}, f)
     if rank == 0 and rec is not None:
         rec["wall_s_incl_build"] = round(time.perf_counter() - t0, 2)
         with open(out_json, "w") as f:
@@ -150,7 +202,8 @@ def measure(world: int = 8, rate: float = 370.0, batches_per_rank: int = 300, tm
                        "cpu_s_per_rank_incl_build": [round(c, 2) for c in cpu], "host_cpus": os.cpu_count(),
                        "gc_max_pause_ms": round(max(p["gc_max_ms"] for p in per), 1),
                        "gc_pause_total_ms_per_rank": [round(p["gc_total_ms"]) for p in per],
-                       "gc_tracked_objects_per_rank": [p["objects"] for p in per]}
+                       "gc_tracked_objects_per_rank": [p["objects"] for p in per],
+                       "thread_cpu_s_rank0": per[0]["threads"], "thread_cpu_s_coordinator": per[-1]["threads"]}
     return rec
 
 
