@@ -34,6 +34,7 @@ import os
 import time
 from typing import List, Optional, Set
 
+import numpy as np
 import torch
 import torch.distributed as dist
 from torch.distributed import distributed_c10d as c10d
@@ -74,15 +75,21 @@ class ShmExchange:
             raise CollectiveFailure(f"shm_open({name}) failed")
         self.step = 0
 
-    def exchange(self, out: torch.Tensor, t: torch.Tensor, poll, timeout_s: float = 120.0,
-                 slice_us: int = 2000) -> None:
-        nb = t.numel() * t.element_size()
-        if nb > self.REC_CAP or not (t.is_contiguous() and out.is_contiguous()) or t.device.type != "cpu":
-            raise CollectiveFailure("shm exchange: record too large or not a contiguous CPU tensor")
+    def exchange(self, out, t, poll, timeout_s: float = 120.0, slice_us: int = 2000) -> None:
+        """``t`` / ``out``: contiguous CPU torch tensors or numpy arrays (numpy: no torch call,
+        so no GIL hand-off to the rank's other threads on the serve loop's path)."""
+        if isinstance(t, np.ndarray):
+            nb, src, dst = t.nbytes, t.ctypes.data, out.ctypes.data
+            ok = t.flags.c_contiguous and out.flags.c_contiguous
+        else:
+            nb, src, dst = t.numel() * t.element_size(), t.data_ptr(), out.data_ptr()
+            ok = t.is_contiguous() and out.is_contiguous() and t.device.type == "cpu"
+        if nb > self.REC_CAP or not ok:
+            raise CollectiveFailure("shm exchange: record too large or not a contiguous CPU buffer")
         self.step += 1
         t0 = time.monotonic()
         while True:
-            rc = self.L.dml_shm_exchange(self.h, self.rank, self.step, t.data_ptr(), nb, out.data_ptr(), slice_us)
+            rc = self.L.dml_shm_exchange(self.h, self.rank, self.step, src, nb, dst, slice_us)
             if rc == 0:
                 return
             if rc < 0:
@@ -295,26 +302,32 @@ class ElasticGroup:
         """``src`` is a GROUP rank."""
         self._run(dist.broadcast, t, src=src)
 
-    def broadcast_bytes(self, t: torch.Tensor, src: int = 0) -> None:
-        """Broadcast a uint8 CPU tensor (the service's log bytes) from GROUP rank ``src``.
-        With the shared-memory exchange it goes through that segment in record-sized chunks,
-        waited for with the same dead-member / moved-epoch polling as the step's exchange
-        (a gloo broadcast blocks without either: a peer that left mid-broadcast held this
-        rank for the full collective timeout)."""
-        if self._shm is None or t.device.type != "cpu":
+    def broadcast_bytes(self, data: Optional[bytes], n: int, src: int = 0) -> bytes:
+        """Broadcast ``n`` bytes (the service's log records; ``data`` on GROUP rank ``src``)
+        and return them on every rank. With the shared-memory exchange they go through that
+        segment in record-sized chunks (numpy, no torch call), waited for with the same
+        dead-member / moved-epoch polling as the step's exchange (a gloo broadcast blocks
+        without either: a peer that left mid-broadcast held this rank for the full
+        collective timeout)."""
+        if self._shm is None:
+            t = torch.zeros(n, dtype=torch.uint8, device=self.device if self.backend == "nccl" else "cpu")
+            if self.rank == src:
+                t.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
             self.broadcast(t, src=src)
-            return
+            return data if self.rank == src else bytes(t.cpu().numpy())
         cap = ShmExchange.REC_CAP
-        n = t.numel()
-        flat = t.view(-1)
-        out = torch.empty((self.world, min(cap, max(n, 1))), dtype=torch.uint8)
+        mine = np.frombuffer(data, np.uint8) if self.rank == src else None
+        got = bytearray(n) if self.rank != src else None
+        out = np.empty((self.world, min(cap, max(n, 1))), np.uint8)
+        zeros = np.zeros(min(cap, max(n, 1)), np.uint8)
         for o in range(0, n, cap):
             k = min(cap, n - o)
-            chunk = flat[o:o + k].contiguous() if self.rank == src else torch.zeros(k, dtype=torch.uint8)
-            ob = out[:, :k] if k == out.shape[1] else torch.empty((self.world, k), dtype=torch.uint8)
+            chunk = np.ascontiguousarray(mine[o:o + k]) if mine is not None else zeros[:k]
+            ob = out if k == out.shape[1] else np.empty((self.world, k), np.uint8)
             self._shm.exchange(ob, chunk, self._poll_dead, self.timeout.total_seconds())
-            if self.rank != src:
-                flat[o:o + k].copy_(ob[src])
+            if got is not None:
+                got[o:o + k] = ob[src].tobytes()
+        return data if got is None else bytes(got)
 
     def gather(self, t: torch.Tensor, bufs: Optional[List[torch.Tensor]], dst: int = 0) -> None:
         self._run(dist.gather, t, bufs if self.rank == dst else None, dst=dst)
@@ -330,13 +343,18 @@ class ElasticGroup:
         else:
             self._run(dist.all_gather, list(out.view(self.world, *t.shape).unbind(0)), t)
 
-    def exchange(self, out: torch.Tensor, t: torch.Tensor, root: int) -> None:
+    def exchange(self, out, t, root: int) -> None:
         """out[r] = rank r's t on every rank (all-gather semantics; ``root`` a
         GROUP rank). gloo: a gather to ``root`` plus a broadcast from it - two
         hops instead of a ring's world-1 (world 8 on 8 cores: 0.54 ms vs 2.1 ms
-        for a 1.7 KB record); nccl: the ring all-gather."""
-        if self._shm is not None and t.device.type == "cpu":
+        for a 1.7 KB record); nccl: the ring all-gather. numpy buffers: the
+        shared-memory exchange only (the service's CPU path)."""
+        if self._shm is not None and (isinstance(t, np.ndarray) or t.device.type == "cpu"):
             self._shm.exchange(out, t, self._poll_dead, self.timeout.total_seconds())
+            return
+        if isinstance(t, np.ndarray):
+            tt, ot = torch.from_numpy(t), torch.from_numpy(out)
+            self.exchange(ot, tt, root)
             return
         if self.backend != "gloo":
             self.all_gather_into(out, t)

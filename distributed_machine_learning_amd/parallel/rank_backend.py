@@ -259,9 +259,9 @@ class PacedRankBackend(RankBackend):
             raise ValueError(f"batch of {len(names)} exceeds the result capacity {self.cap}")
         k = len(names)
         i0 = (self.launched * 131) % (4096 - self.cap)
-        out = torch.zeros((2, self.cap, 5), dtype=torch.int32)
-        out[0, :k] = torch.from_numpy(self.ids[i0:i0 + k])
-        out[1, :k] = torch.from_numpy(self.p[i0:i0 + k])
+        out = np.zeros((2, self.cap, 5), np.int32)   # numpy: no torch call (GIL hand-off) per launch
+        out[0, :k] = self.ids[i0:i0 + k]
+        out[1, :k] = self.p[i0:i0 + k]
         self.busy_until = max(time.monotonic(), self.busy_until) + self.dt
         self.launched += 1
         return out, _Deadline(self.busy_until)
@@ -373,6 +373,7 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         self._dcache: "OrderedDict[str, np.ndarray]" = OrderedDict()   # name -> full-res RGB (both models)
         self._dbytes, self.decode_hits, self._dlock = 0, 0, threading.Lock()
         self.host = [torch.zeros((2, self.cap, 5), dtype=torch.int32).pin_memory() for _ in range(SLOTS)]
+        self.host_np = [h.numpy() for h in self.host]   # the serve loop reads rows without a torch call
         self.ev_done = [torch.cuda.Event() for _ in range(SLOTS)]
         self.fail_rows: List[Optional[List[int]]] = [None] * SLOTS
         for m in models:
@@ -483,13 +484,13 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
                     rows.append(host[:, :len(chunk)].clone())
                 host[:, :len(slots)] = torch.cat(rows, 1)
             self.ev_done[slot].record(s)
-        return host, self.ev_done[slot]
+        return self.host_np[slot], self.ev_done[slot]
 
     def finalize(self, slot: int) -> None:
         """(after the slot's event) unfetchable / undecodable images: class id -1 marks the row failed."""
         rows = self.fail_rows[slot]
         if rows:
-            self.host[slot][0, rows] = -1
+            self.host_np[slot][0, rows] = -1
             self.fail_rows[slot] = None
 
     def drain(self) -> None:

@@ -285,31 +285,50 @@ class ReplicatedCoordinator:
             # rank's queue by at most that batch)
             gone = {k for gg, k in revokes if gg == g} | self.revoking
             free[g] = self.depth - sum(1 for inf in mine[g] if inf.batch.key not in gone)
-        # every free slot of this step lies within the first world x depth queued batches
-        head = {m: list(islice(self.jobs.queues[m], 0, len(members) * self.depth)) for m in MODELS}
+        # every free slot of this step lies within the first world x depth queued batches. One
+        # pass over each model's head sorts them: staged for a rank that takes this model now
+        # (its own), or orphans (staged for nobody, or for a rank that left / switched model)
+        own: Dict[int, List[Batch]] = {}
+        orphans: Dict[str, List[Batch]] = {}
+        rest: Dict[str, List[Batch]] = {}
+        for m in MODELS:
+            if not any(target[g] == m and free[g] > 0 for g in members):
+                continue
+            aff = self.affinity[m]
+            orph = orphans[m] = []
+            head = rest[m] = list(islice(self.jobs.queues[m], 0, len(members) * self.depth))
+            for b in head:
+                g = aff.get(b.key) if aff else None
+                if g is not None and target.get(g) == m:
+                    own.setdefault(g, []).append(b)
+                else:
+                    orph.append(b)
         used: set = set()
 
-        def take(g: int, want: Callable[[Batch], bool]) -> None:
-            for b in head[target[g]]:
-                if free[g] <= 0:
-                    return
-                if b.key not in used and want(b):
+        def take(g: int, cand: List[Batch], i: int = 0) -> int:
+            while free[g] > 0 and i < len(cand):
+                b = cand[i]
+                i += 1
+                if b.key not in used:
                     disp.setdefault(g, []).append(b)   # popped for real by apply_table
                     used.add(b.key)
                     free[g] -= 1
+            return i
         # 1. the queued batches whose images are staged for this rank; 2. (queue order) the
-        # ones staged for no rank, or for a rank that now runs the other model or left;
-        # 3. a rank that would run dry takes any queued batch (its images are shipped to it)
+        # orphans; 3. a rank that would run dry takes any queued batch (its images are then
+        # shipped to it)
         for g in members:
-            aff = self.affinity[target[g]]
-            take(g, lambda b, g=g, aff=aff: aff.get(b.key) == g)
+            if free[g] > 0 and g in own:
+                take(g, own[g])
+        pos = {m: 0 for m in orphans}
         for g in members:
-            aff = self.affinity[target[g]]
-            take(g, lambda b, g=g, aff=aff: target.get(aff.get(b.key, -1)) != target[g])
+            m = target[g]
+            if free[g] > 0 and m in orphans:
+                pos[m] = take(g, orphans[m], pos[m])
         low = self.depth - max(self.gpu_slots, self.depth // 4)
         for g in members:
-            if free[g] > low:
-                take(g, lambda b: True)
+            if free[g] > low and target[g] in rest:
+                take(g, rest[target[g]])
         return disp, revokes
 
     def table(self, members: List[int], disp: Dict[int, List[Batch]]) -> np.ndarray:
@@ -580,7 +599,7 @@ class OutputWriter:
 @dataclass
 class _Launched:
     batch: Batch
-    rows: torch.Tensor
+    rows: object            # [2, cap, 5] int32: a torch tensor or a numpy view (no torch call per poll)
     event: Optional[object]
     slot: int
     t0: float
@@ -642,7 +661,7 @@ class CollectiveService:
             self.unsynced |= set(eg.members) - set(eg.prev_members)
         # queued batches staged ahead of dispatch (the in-flight ones are staged besides)
         self.stage_ahead = max(1, eg.world) * min(coord.depth, STAGE_DEPTH)
-        self._rec_bufs: Dict[tuple, torch.Tensor] = {}   # the step's exchange output, per (world, L)
+        self._rec_bufs: Dict[tuple, object] = {}   # the step's exchange output, per (world, L)
         # a staging backend (image arenas): queued batches get an affinity rank, their images
         # are staged there ahead of dispatch and the plan sends them there
         self._targeted = hasattr(backend, "arenas")
@@ -711,7 +730,7 @@ class CollectiveService:
             self.be.finalize(L.slot)
             svc = time.monotonic() - L.t0
             k = len(L.batch.images)
-            rows = L.rows[:, :k].numpy()
+            rows = L.rows[:, :k] if isinstance(L.rows, np.ndarray) else L.rows[:, :k].numpy()
             idx = rows[0].copy()
             p = rows[1].view(np.float32).copy()
             self.free_slots.append(L.slot)
@@ -796,26 +815,31 @@ class CollectiveService:
         t2 = time.perf_counter()
         ph["plan"] += t2 - t1
         # ---- the step's collective (+ the log bytes, rarely) ----
-        rec_t = torch.from_numpy(rec).to(self.dev)
+        # host path (shared-memory exchange): numpy end to end — every torch call on the serve
+        # loop hands the GIL to the rank's writer / control threads and waits to get it back
+        # (measured: 0.2-0.5 ms per trivial tensor op at world 8)
+        host = self.dev.type == "cpu"
         out = self._rec_bufs.get((world, L))
         if out is None:  # one buffer per group shape: no allocation per step
-            out = self._rec_bufs[(world, L)] = torch.empty((world, L), dtype=torch.int64, device=self.dev)
+            out = self._rec_bufs[(world, L)] = (np.empty((world, L), np.int64) if host else
+                                                torch.empty((world, L), dtype=torch.int64, device=self.dev))
         applied_here: List[dict] = []
         try:
             if world == 1:  # nothing to exchange: a collective would only hand the GIL around
                 h = rec[None]
                 n = 0
             else:
-                eg.exchange(out, rec_t, root)
-                h = out.cpu().numpy()
+                if host:
+                    eg.exchange(out, rec, root)
+                    h = out
+                else:
+                    eg.exchange(out, torch.from_numpy(rec).to(self.dev), root)
+                    h = out.cpu().numpy()
                 n = int(h[root, H_LOGLEN])
             if n:
-                buf = torch.zeros(n, dtype=torch.uint8, device=self.dev)
-                if active:
-                    buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
-                eg.broadcast_bytes(buf, src=root)
+                got = eg.broadcast_bytes(payload if active else None, n, src=root)
                 if not active:
-                    applied_here = json.loads(bytes(buf.cpu().numpy()).decode())
+                    applied_here = json.loads(got.decode())
         except CollectiveFailure:
             # nothing of this step was applied anywhere: its reports and answers go again
             for b, svc in reversed(reports):

@@ -156,8 +156,9 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
         build_s = time.perf_counter() - t_build
         svc.freeze_heap()
         eg.barrier()
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.thread_time()
         steps = svc.serve(stop_when_idle=True)   # drains the writer: every output file is on disk
+        loop_cpu = time.thread_time() - c0       # the serve loop thread's own CPU seconds
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         el = time.perf_counter() - t0
@@ -171,7 +172,8 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                                int(ctl.loop_lag_max * 1e6),
                                sum(a.decoded for a in ar.values()), sum(a.replicated for a in ar.values()),
                                sum(a.received for a in ar.values()),
-                               sum(a.received * a.hw[0] * a.hw[1] * 3 for a in ar.values())], dtype=torch.int64)
+                               sum(a.received * a.hw[0] * a.hw[1] * 3 for a in ar.values()),
+                               int(loop_cpu * 1e6)], dtype=torch.int64)
         allsv = [torch.zeros_like(served) for _ in range(eg.world)]
         if eg.backend == "gloo":
             dist.all_gather(allsv, served)
@@ -211,6 +213,7 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                 "rebuilds": svc.rebuilds, "preempted_batches": coord.preempted, "requeued_batches": coord.requeued,
                 "kill_to_redispatch_s": [round(x, 3) for x in svc.recoveries_s],
                 "control_loop_lag_max_ms": {f"rank{g}": round(int(v[4]) / 1e3, 1) for g, v in zip(eg.members, allsv)},
+                "serve_loop_cpu_s": {f"rank{g}": round(int(v[9]) / 1e6, 3) for g, v in zip(eg.members, allsv)},
                 "kills": [f"{r}:{d}" for r, d in kills], "final_members": eg.members,
                 "jobs_done": all(j.done for j in coord.jobs.jobs.values()),
                 "loop_phase_s": {k: round(v, 4) for k, v in svc.phase_s.items()},

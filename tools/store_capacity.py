@@ -218,7 +218,8 @@ def main():
     rec = measure(a.world, a.rate, a.batches_per_rank, depth=a.depth)
     print(json.dumps(rec["capacity"]), flush=True)
     print(json.dumps({k: rec[k] for k in ("outputs", "loop_phase_s", "steps", "max_batches_per_step",
-                                          "jobs_done", "p50_latency_ms", "control_loop_lag_max_ms")}), flush=True)
+                                          "jobs_done", "p50_latency_ms", "control_loop_lag_max_ms",
+                                          "serve_loop_cpu_s")}), flush=True)
     if a.out:
         with open(a.out, "w") as f:
             json.dump(rec, f, indent=1)
