@@ -35,7 +35,7 @@ using convk::wait_vmcnt;
 
 constexpr int lds_occupancy(int a, int b) { return 163840 / (a > b ? a : b); }
 
-template <int BM, int BN, int WM, int WN, int NL_, int STAGES, int BK_, int PRMAX>
+template <int BM, int BN, int WM, int WN, int NL_, int STAGES, int BK_, int PRMAX, int NPB = 2>
 struct Cfg {
   static constexpr int NC = WM * WN;          // MFMA waves
   static constexpr int NL = NL_;              // loader waves
@@ -55,7 +55,7 @@ struct Cfg {
   static constexpr int PROWS = PP * RP;                   // patch rows (>= PRMAX: dummy pieces land here)
   static constexpr int WSTAGE = BN * ROWB;
   static constexpr int PATCH = PROWS * ROWB;
-  static constexpr int PIPE_BYTES = STAGES * WSTAGE + 2 * PATCH;
+  static constexpr int PIPE_BYTES = STAGES * WSTAGE + NPB * PATCH;  // NPB 1: single-chunk convs only
   static constexpr int CROW = BN * 4 + 16;
   static constexpr bool EP_OK2 = (BM / 2) % 16 == 0 && ((BM * BN / 8) / NTC) % 2 == 0;
   static constexpr bool EP_OK4 = (BM / 4) % 16 == 0 && ((BM * BN / 8) / NTC) % 4 == 0;
@@ -96,9 +96,9 @@ __host__ __device__ inline Geo pt_geometry(const DmlConvArgs& a, int BM) {
   return g;
 }
 
-template <int BM, int BN, int WM, int WN, int NL, int STAGES, bool RES, int BK, bool LATE, int PRMAX>
+template <int BM, int BN, int WM, int WN, int NL, int STAGES, bool RES, int BK, bool LATE, int PRMAX, int NPB>
 __device__ __forceinline__ void conv_pt_tile(const DmlConvArgs& a, int Lb) {
-  using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK, PRMAX>;
+  using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK, PRMAX, NPB>;
   using RW = typename T::R;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const patch0 = smem + STAGES * T::WSTAGE;
@@ -170,7 +170,7 @@ __device__ __forceinline__ void conv_pt_tile(const DmlConvArgs& a, int Lb) {
                                          (lds_void*)(sw + (lw * T::WI + j) * 1024), 16, 0, 0);
     };
     auto issue_p = [&](int cb) {
-      char* dst = patch0 + (cb & 1) * T::PATCH;
+      char* dst = patch0 + (NPB > 1 ? (cb & 1) : 0) * T::PATCH;
 #pragma unroll
       for (int i = 0; i < T::PI; ++i) {
         const unsigned off = poff[i] >= 0 ? (unsigned)(poff[i] + cb * BK) * 2u : OOB;
@@ -196,7 +196,7 @@ __device__ __forceinline__ void conv_pt_tile(const DmlConvArgs& a, int Lb) {
       }
       __builtin_amdgcn_s_barrier();  // K tile kt (and its chunk's patch) published
       const int cb = kt / taps;
-      if (kt == cb * taps && cb + 1 < nchunk) {
+      if (NPB > 1 && kt == cb * taps && cb + 1 < nchunk) {
         issue_p(cb + 1);
         ip = kt;
       }
@@ -226,7 +226,7 @@ __device__ __forceinline__ void conv_pt_tile(const DmlConvArgs& a, int Lb) {
       const int tr = t / a.kw;
       const int toff = tr * g.PW + (t - tr * a.kw);
       const char* sw = smem + (kt % STAGES) * T::WSTAGE;
-      const char* sx = patch0 + (cb & 1) * T::PATCH;
+      const char* sx = patch0 + (NPB > 1 ? (cb & 1) : 0) * T::PATCH;
       bf16x8 fa[KSM][T::FI], fb[KSM][T::FJ];
 #pragma unroll
       for (int ks = 0; ks < KSM; ++ks) {
@@ -250,27 +250,28 @@ __device__ __forceinline__ void conv_pt_tile(const DmlConvArgs& a, int Lb) {
   epi.template store<16, T::FI, T::FJ, T::WTP, T::WTC>(a, smem, acc, wp, wc, lane, tid, wid < T::NC);
 }
 
-template <int BM, int BN, int WM, int WN, int NL, int STAGES, bool RES, int BK, bool LATE, int W, int PRMAX>
+template <int BM, int BN, int WM, int WN, int NL, int STAGES, bool RES, int BK, bool LATE, int W, int PRMAX, int NPB>
 __global__ __launch_bounds__((WM * WN + NL) * 64, W) void conv_pt_kernel(DmlConvArgs a) {
-  conv_pt_tile<BM, BN, WM, WN, NL, STAGES, RES, BK, LATE, PRMAX>(a, xcd_remap(blockIdx.x, gridDim.x));
+  conv_pt_tile<BM, BN, WM, WN, NL, STAGES, RES, BK, LATE, PRMAX, NPB>(a, xcd_remap(blockIdx.x, gridDim.x));
 }
 
 // host: can this config run this conv?
-template <int BM, int BN, int NL, int STAGES, int BK, int PRMAX, int WM, int WN>
+template <int BM, int BN, int NL, int STAGES, int BK, int PRMAX, int WM, int WN, int NPB>
 static bool fits(const DmlConvArgs* a) {
-  using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK, PRMAX>;
+  using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK, PRMAX, NPB>;
   const int dh = a->dh > 0 ? a->dh : 1, dw = a->dw > 0 ? a->dw : 1;
   if (a->sh != 1 || a->sw != 1 || dh != 1 || dw != 1 || a->ksplit > 1) return false;
   if (a->Cin % BK || a->ldx % 8 || a->Wo > BM || a->Kpad < a->kh * a->kw * a->Cin) return false;
   if (a->kh * a->kw < STAGES - 1 && a->Cin / BK > 1) return false;  // patch issue order (see the loaders)
+  if (NPB == 1 && a->Cin != BK) return false;                        // one patch buffer: one chunk
   const Geo g = pt_geometry(*a, BM);
   return g.TH >= 1 && g.PR <= T::PROWS && g.mt > 0;
 }
 
-template <int BM, int BN, int WM, int WN, int NL, int STAGES, int BK, bool LATE, int W, int PRMAX>
+template <int BM, int BN, int WM, int WN, int NL, int STAGES, int BK, bool LATE, int W, int PRMAX, int NPB>
 static int launch(const DmlConvArgs* a, hipStream_t s) {
-  using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK, PRMAX>;
-  if (!fits<BM, BN, NL, STAGES, BK, PRMAX, WM, WN>(a)) {
+  using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK, PRMAX, NPB>;
+  if (!fits<BM, BN, NL, STAGES, BK, PRMAX, WM, WN, NPB>(a)) {
     dml_set_error("dml_conv_pt: needs stride 1, dilation 1, Cin % BK == 0, no split-K, Wo <= BM and a patch "
                   "that fits the config");
     return -1;
@@ -278,23 +279,23 @@ static int launch(const DmlConvArgs* a, hipStream_t s) {
   const Geo g = pt_geometry(*a, BM);
   const long tiles = (long)g.mt * ((a->Cout + BN - 1) / BN);
   if (a->res)
-    hipLaunchKernelGGL((conv_pt_kernel<BM, BN, WM, WN, NL, STAGES, true, BK, LATE, W, PRMAX>), dim3((unsigned)tiles),
-                       dim3(T::NT), T::LDS, s, *a);
+    hipLaunchKernelGGL((conv_pt_kernel<BM, BN, WM, WN, NL, STAGES, true, BK, LATE, W, PRMAX, NPB>),
+                       dim3((unsigned)tiles), dim3(T::NT), T::LDS, s, *a);
   else
-    hipLaunchKernelGGL((conv_pt_kernel<BM, BN, WM, WN, NL, STAGES, false, BK, false, W, PRMAX>),
+    hipLaunchKernelGGL((conv_pt_kernel<BM, BN, WM, WN, NL, STAGES, false, BK, false, W, PRMAX, NPB>),
                        dim3((unsigned)tiles), dim3(T::NT), T::LDS, s, *a);
   DML_CHECK_LAUNCH();
   return 0;
 }
 
-template <int BM, int BN, int WM, int WN, int NL, int STAGES, int BK, bool LATE, int W, int PRMAX>
+template <int BM, int BN, int WM, int WN, int NL, int STAGES, int BK, bool LATE, int W, int PRMAX, int NPB>
 static int set_attr() {
-  using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK, PRMAX>;
+  using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK, PRMAX, NPB>;
   return (int)hipFuncSetAttribute(
-             (const void*)conv_pt_kernel<BM, BN, WM, WN, NL, STAGES, true, BK, LATE, W, PRMAX>,
+             (const void*)conv_pt_kernel<BM, BN, WM, WN, NL, STAGES, true, BK, LATE, W, PRMAX, NPB>,
              hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS) |
          (int)hipFuncSetAttribute(
-             (const void*)conv_pt_kernel<BM, BN, WM, WN, NL, STAGES, false, BK, false, W, PRMAX>,
+             (const void*)conv_pt_kernel<BM, BN, WM, WN, NL, STAGES, false, BK, false, W, PRMAX, NPB>,
              hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
@@ -303,18 +304,23 @@ static int set_attr() {
 
 // Patch-stationary tile configurations: id, BM, BN, WM x WN MFMA waves, NL loader waves,
 // weight-ring STAGES, BK, RL (residual loaded in the epilogue), W (min waves/SIMD hint),
-// PRMAX (patch rows per chunk). Ids 140..159 are part of the tuner ABI (ops/tuning.py
+// PRMAX (patch rows per chunk), NPB (patch buffers: 2 = the next chunk's patch loads during
+// this chunk's taps; 1 = Cin == BK only, half the LDS). Ids 140..159 are part of the tuner ABI (ops/tuning.py
 // PT_CFGS), validated by dml_conv (conv_dispatch.hip).
-#define DML_PT_TILES(X)                                                                           \
-  X(140, 256, 128, 4, 2, 4, 3, 64, 1, 1, 416) /* 8 (64x64) + 4 loaders, 152 KiB */                \
-  X(141, 256, 64, 4, 1, 4, 3, 64, 0, 1, 416)  /* 4 (64x64) + 4, 128 KiB */                         \
-  X(142, 128, 128, 2, 2, 2, 3, 64, 0, 1, 240) /* 4 + 2, 108 KiB */                                 \
-  X(143, 128, 64, 2, 2, 2, 3, 64, 0, 1, 240)  /* 4 (64x32) + 2, 84 KiB */
+#define DML_PT_TILES(X)                                                                             \
+  X(140, 256, 128, 4, 2, 4, 3, 64, 1, 1, 416, 2) /* 8 (64x64) + 4 loaders, 152 KiB */                \
+  X(141, 256, 64, 4, 1, 4, 3, 64, 0, 1, 416, 2)  /* 4 (64x64) + 4, 128 KiB */                         \
+  X(142, 128, 128, 2, 2, 2, 3, 64, 0, 1, 240, 2) /* 4 + 2, 108 KiB */                                 \
+  X(143, 128, 64, 2, 2, 2, 3, 64, 0, 1, 240, 2)  /* 4 (64x32) + 2, 84 KiB */                          \
+  /* one patch buffer (single-chunk convs, Cin == 64): 2-3 workgroups per CU */                      \
+  X(144, 256, 64, 4, 1, 2, 3, 64, 0, 3, 416, 1)  /* 4 (64x64) + 2, 76 KiB: 2 WG/CU */                 \
+  X(145, 128, 64, 2, 2, 2, 3, 64, 0, 4, 240, 1)  /* 4 (64x32) + 2, 54 KiB: 3 WG/CU */                 \
+  X(146, 128, 128, 2, 2, 2, 3, 64, 0, 2, 240, 1) /* 4 (64x64) + 2, 78 KiB: 2 WG/CU */
 
 extern "C" int dml_conv_pt_init(void) {
   using namespace dml::pt;
   int rc = 0;
-#define DML_SET(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PR) rc |= set_attr<BM, BN, WM, WN, NL, ST, BK, RL, W, PR>();
+#define DML_SET(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PR, NPB) rc |= set_attr<BM, BN, WM, WN, NL, ST, BK, RL, W, PR, NPB>();
   DML_PT_TILES(DML_SET)
 #undef DML_SET
   if (rc) dml_set_error("dml_conv_pt_init: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
@@ -324,8 +330,8 @@ extern "C" int dml_conv_pt_init(void) {
 extern "C" int dml_conv_pt(const DmlConvArgs* a, int cfg, hipStream_t s) {
   using namespace dml::pt;
   switch (cfg) {
-#define DML_CASE(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PR) \
-  case id: return launch<BM, BN, WM, WN, NL, ST, BK, RL, W, PR>(a, s);
+#define DML_CASE(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PR, NPB) \
+  case id: return launch<BM, BN, WM, WN, NL, ST, BK, RL, W, PR, NPB>(a, s);
     DML_PT_TILES(DML_CASE)
 #undef DML_CASE
     default: dml_set_error("dml_conv_pt: bad cfg"); return -1;
@@ -334,7 +340,7 @@ extern "C" int dml_conv_pt(const DmlConvArgs* a, int cfg, hipStream_t s) {
 
 extern "C" int dml_conv_pt_bn(int cfg) {
   switch (cfg) {
-#define DML_CASE(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PR) \
+#define DML_CASE(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PR, NPB) \
   case id: return BN;
     DML_PT_TILES(DML_CASE)
 #undef DML_CASE
@@ -346,8 +352,8 @@ extern "C" int dml_conv_pt_bn(int cfg) {
 extern "C" int dml_conv_pt_fits(const DmlConvArgs* a, int cfg) {
   using namespace dml::pt;
   switch (cfg) {
-#define DML_CASE(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PR) \
-  case id: return fits<BM, BN, NL, ST, BK, PR, WM, WN>(a) ? 1 : 0;
+#define DML_CASE(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PR, NPB) \
+  case id: return fits<BM, BN, NL, ST, BK, PR, WM, WN, NPB>(a) ? 1 : 0;
     DML_PT_TILES(DML_CASE)
 #undef DML_CASE
     default: return 0;

@@ -108,7 +108,11 @@ int main() {
   CHECK(dml_conv_v2_bn(100) == 128 && dml_conv_v2_bn(103) == 64 && dml_conv_v2_bn(120) == 64 &&
         dml_conv_v2_bn(122) == 128);
   // patch-stationary tiles (conv_igemm_pt.hip): channel widths, and which convs they take (host code)
-  CHECK(dml_conv_v2_bn(140) == 128 && dml_conv_v2_bn(141) == 64 && dml_conv_v2_bn(144) == 0);
+  CHECK(dml_conv_v2_bn(140) == 128 && dml_conv_v2_bn(141) == 64 && dml_conv_v2_bn(144) == 64 && dml_conv_v2_bn(147) == 0);
+  {
+    DmlConvArgs one = conv_args(128, 64, 3, 3);                     // one patch buffer: a single 64-channel chunk only
+    CHECK(dml_conv_pt_fits(&one, 144) == 0 && dml_conv_pt_fits(&one, 141) == 1);
+  }
   {
     DmlConvArgs p = conv_args(256, 256, 3, 3);                      // ResNet50 stage-4 3x3 (14 x 14)
     CHECK(dml_conv_pt_fits(&p, 140) == 1 && dml_conv_pt_fits(&p, 142) == 1);

@@ -31,7 +31,7 @@ WSP_CFGS = tuple(range(120, 130))
 # patch-stationary stride-1 tiles (csrc/kernels/conv_igemm_pt.hip: the activation patch of an
 # M tile of whole output rows is loaded once per channel chunk, r5); they refuse what they
 # cannot run (stride / dilation != 1, Cin % 64, a patch larger than the config's)
-PT_CFGS = (140, 141, 142, 143)
+PT_CFGS = (140, 141, 142, 143, 144, 145, 146)
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))

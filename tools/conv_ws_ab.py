@@ -31,7 +31,7 @@ SHAPES = [  # name, batch, h, w, cin, cout, kh, kw, stride, ph, pw, residual
 ]
 V2_DEFAULT = "11,12,14,15,24,25,26,28,30,31,32,33,38"
 WS_DEFAULT = ("100,101,102,103,104,105,106,107,108,109,110,111,112,113,114,115,116,117,118,"
-              "120,121,122,123,124,125,126,127,128,129,140,141,142,143")
+              "120,121,122,123,124,125,126,127,128,129,140,141,142,143,144,145,146")
 
 
 def main():

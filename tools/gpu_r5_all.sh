@@ -14,7 +14,7 @@ tail -4 gpurun_out/r5_pytest.log
 timeout -k 10 900 python -u tools/conv_ws_ab.py --out gpurun_out/ws_ab_all.json > gpurun_out/ws_ab_all.log 2>&1 || { tail -20 gpurun_out/ws_ab_all.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/ws_ab_all.log | grep -v "^    "
 if [ -n "$TUNE" ]; then
-  ADD=113,114,115,116,117,118,140,141,142,143 bash tools/gpu_ws_tune.sh || exit 1
+  ADD=113,114,115,116,117,118,140,141,142,143,144,145,146 bash tools/gpu_ws_tune.sh || exit 1
 fi
 timeout -k 10 900 python -u bench.py > gpurun_out/bench_full.log 2>&1 || { tail -30 gpurun_out/bench_full.log; exit 1; }
 python tools/bench_summary.py gpurun_out/bench_full.log
