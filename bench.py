@@ -83,6 +83,9 @@ def parse_args(argv=None):
     ap.add_argument("--svc-resnet-images", type=int, default=51200, help="ResNet50 images per GPU (service run)")
     ap.add_argument("--svc-inception-images", type=int, default=25600,
                     help="InceptionV3 images per GPU (service run)")
+    ap.add_argument("--svc-store-time-limit", type=float, default=300.0,
+                    help="seconds the store-image pass may serve before it is abandoned (reported as an error "
+                         "in its sub-record; the headline record is printed either way)")
     ap.add_argument("--svc-store-images", type=int, default=2048,
                     help="the `service_store` sub-record: the same concurrent jobs over this many distinct JPEGs "
                          "PUT into the replicated store (fetched, decoded once, staged into HBM on the timed path); "
@@ -373,7 +376,8 @@ def bench_service(args, rank: int, world: int, device, recs: dict):
         try:
             srec = service_bench.run(rank, world, device, rdzv_s, port_s, args.svc_resnet_images * world,
                                      args.svc_inception_images * world, dict(DEFAULT_BATCH), None,
-                                     single_rates=rates, store_images=args.svc_store_images)
+                                     single_rates=rates, store_images=args.svc_store_images,
+                                     time_limit_s=args.svc_store_time_limit)
         except Exception as e:  # noqa: BLE001 - reported in the record, never fails the headline
             print(f"bench: rank {rank}: store-image service pass failed: {e}", file=sys.stderr, flush=True)
             srec = {"error": str(e)[:500]}

@@ -791,7 +791,7 @@ class CollectiveService:
         tab, req, rep, ack = _offs(world, depth)
         root = eg.group_rank_of(self.coordinator_rank())
         ph, t0 = self.phase_s, time.perf_counter()
-        self._poll()
+        moved0 = self._poll()
         t1 = time.perf_counter()
         ph["poll"] += t1 - t0
         active = self.is_coordinator()
@@ -925,7 +925,7 @@ class CollectiveService:
             self.answers.append((key, hit is not None))
         if flags & F_GROW:
             self._grow([g for g in range(63) if (int(h[root, H_GROW]) >> g) & 1])
-        self._poll()
+        moved0 += self._poll()
         self.steps += 1
         if os.environ.get("DML_SVC_DEBUG") and self.steps % 200 == 0:
             log.warning("rank %d step %d epoch %d: queued %s inflight %d hostq %d gpu %d done %d root %d",
@@ -936,6 +936,13 @@ class CollectiveService:
         ph["launch"] += t5 - t4
         if not (reports or answers or mine or n or self.done or self.answers or self.gpu or self.hostq):
             time.sleep(self.poll_sleep if coord.inflight else self.idle_sleep)
+            ph["sleep"] += time.perf_counter() - t5
+        elif world == 1 and not (moved0 or reports or answers or mine or n):
+            # world 1 has no exchange to block in: a step that moved nothing (batches waiting on
+            # the GPU or on their image window) would otherwise spin in Python and hold the GIL
+            # against the decode pool, the writer and the control loop (measured: a store-image
+            # window's fetch took 60-110 s behind such a spin, 32 decode threads)
+            time.sleep(self.poll_sleep)
             ph["sleep"] += time.perf_counter() - t5
         return True
 
@@ -975,9 +982,14 @@ class CollectiveService:
             gc.freeze()
             self._frozen = True
 
-    def serve(self, max_steps: int = 10 ** 9, stop_when_idle: bool = False) -> int:
+    def serve(self, max_steps: int = 10 ** 9, stop_when_idle: bool = False, deadline: Optional[float] = None) -> int:
+        """Run steps until STOP (stop_when_idle: once every job is done) or ``max_steps``.
+        ``deadline`` (time.monotonic()): raise TimeoutError past it (a bench pass with a time
+        budget; the product runs without one)."""
         self.freeze_heap()
         while self.steps < max_steps:
+            if deadline is not None and time.monotonic() > deadline:
+                raise TimeoutError(f"rank {self.eg.grank}: serve deadline passed at step {self.steps}")
             try:
                 if not self.step(stop_when_idle):
                     break
