@@ -315,7 +315,11 @@ static int set_attr() {
   /* one patch buffer (single-chunk convs, Cin == 64): 2-3 workgroups per CU */                      \
   X(144, 256, 64, 4, 1, 2, 3, 64, 0, 3, 416, 1)  /* 4 (64x64) + 2, 76 KiB: 2 WG/CU */                 \
   X(145, 128, 64, 2, 2, 2, 3, 64, 0, 4, 240, 1)  /* 4 (64x32) + 2, 54 KiB: 3 WG/CU */                 \
-  X(146, 128, 128, 2, 2, 2, 3, 64, 0, 2, 240, 1) /* 4 (64x64) + 2, 78 KiB: 2 WG/CU */
+  X(146, 128, 128, 2, 2, 2, 3, 64, 0, 2, 240, 1) /* 4 (64x64) + 2, 78 KiB: 2 WG/CU */                 \
+  /* deeper weight rings (more operand bytes in flight per CU): smaller patches */                    \
+  X(147, 256, 128, 4, 2, 4, 6, 64, 1, 1, 256, 2) /* 14x14 and 7x7 (TI 1 / 3 ... ), 160 KiB */        \
+  X(148, 256, 128, 4, 2, 4, 4, 64, 1, 1, 352, 2) /* 56 / 28 / 14 rows, 152 KiB */                     \
+  X(149, 256, 128, 4, 2, 4, 8, 32, 1, 1, 416, 2) /* BK 32: 8-stage ring, 116 KiB */
 
 extern "C" int dml_conv_pt_init(void) {
   using namespace dml::pt;

@@ -378,7 +378,8 @@ static int set_attr() {
   X(115, 256, 64, 4, 1, 4, 3, 64, 0, 1, 2)   /* = 105 + PF 2 */                                  \
   X(116, 64, 128, 1, 4, 2, 3, 64, 0, 1, 1)   /* = 104 + PF */                                    \
   X(117, 128, 64, 2, 2, 2, 3, 64, 0, 1, 1)   /* = 103 + PF */                                    \
-  X(118, 128, 128, 2, 2, 2, 4, 32, 0, 1, 1)  /* = 101 + PF */
+  X(118, 128, 128, 2, 2, 2, 4, 32, 0, 1, 1)  /* = 101 + PF */                                    \
+  X(119, 256, 128, 4, 2, 4, 6, 32, 1, 1, 0)  /* 8 + 4, BK32 6-stage, 144 KiB: 5 tiles in flight */
 
 extern "C" int dml_conv_ws_init(void) {
   using namespace dml::ws;

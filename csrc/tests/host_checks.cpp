@@ -102,13 +102,13 @@ int main() {
   CHECK(dml_conv_v2_bn(64) == 0 && dml_conv_v2_bn(68) == 0);   // the removed shifted-pixel ids
   CHECK(dml_conv(&a, 64, nullptr) != 0);
   CHECK(dml_conv(&a, 80, nullptr) != 0);        // the removed Winograd ids
-  CHECK(dml_conv(&a, 119, nullptr) != 0);       // an unassigned warp-specialised id
+  CHECK(dml_conv(&a, 99, nullptr) != 0);        // an unassigned id
   CHECK(dml_conv(&a, 139, nullptr) != 0);       // an unassigned persistent id
   CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
   CHECK(dml_conv_v2_bn(100) == 128 && dml_conv_v2_bn(103) == 64 && dml_conv_v2_bn(120) == 64 &&
         dml_conv_v2_bn(122) == 128);
   // patch-stationary tiles (conv_igemm_pt.hip): channel widths, and which convs they take (host code)
-  CHECK(dml_conv_v2_bn(140) == 128 && dml_conv_v2_bn(141) == 64 && dml_conv_v2_bn(144) == 64 && dml_conv_v2_bn(147) == 0);
+  CHECK(dml_conv_v2_bn(140) == 128 && dml_conv_v2_bn(141) == 64 && dml_conv_v2_bn(144) == 64 && dml_conv_v2_bn(150) == 0);
   {
     DmlConvArgs one = conv_args(128, 64, 3, 3);                     // one patch buffer: a single 64-channel chunk only
     CHECK(dml_conv_pt_fits(&one, 144) == 0 && dml_conv_pt_fits(&one, 141) == 1);

@@ -24,14 +24,14 @@ from .. import _native as N
 V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33, 34, 36, 37,
            38, 39)  # 23..37: BK32; 38 / 39: 3-stage BK64 64-channel tiles (r3)
 # warp-specialised tiles (csrc/kernels/conv_igemm_ws.hip: loader waves + MFMA waves, r5)
-WS_CFGS = tuple(range(100, 119))
+WS_CFGS = tuple(range(100, 120))
 # their persistent form (csrc/kernels/conv_igemm_wsp.hip: one operand ring over a workgroup's
 # whole tile list; no split-K)
 WSP_CFGS = tuple(range(120, 130))
 # patch-stationary stride-1 tiles (csrc/kernels/conv_igemm_pt.hip: the activation patch of an
 # M tile of whole output rows is loaded once per channel chunk, r5); they refuse what they
 # cannot run (stride / dilation != 1, Cin % 64, a patch larger than the config's)
-PT_CFGS = (140, 141, 142, 143, 144, 145, 146)
+PT_CFGS = tuple(range(140, 150))
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))

@@ -30,8 +30,7 @@ SHAPES = [  # name, batch, h, w, cin, cout, kh, kw, stride, ph, pw, residual
     ("inc_m3_3x3s2", 64, 35, 35, 288, 384, 3, 3, 2, 0, 0, 0),
 ]
 V2_DEFAULT = "11,12,14,15,24,25,26,28,30,31,32,33,38"
-WS_DEFAULT = ("100,101,102,103,104,105,106,107,108,109,110,111,112,113,114,115,116,117,118,"
-              "120,121,122,123,124,125,126,127,128,129,140,141,142,143,144,145,146")
+WS_DEFAULT = ",".join(str(c) for c in list(range(100, 120)) + list(range(120, 130)) + list(range(140, 150)))
 
 
 def main():
