@@ -67,6 +67,7 @@ class Window:
     bufs: Optional[tuple] = None                       # (local rows, received rows, flags) tensors
     event: Optional[object] = None                     # recorded after the scatter (CUDA)
     flags: Optional[torch.Tensor] = None               # ok flag per name (host), after the all-reduce
+    pack: Optional[object] = None                      # GPU backend: the pinned pack of its decodes
     failed: Set[str] = field(default_factory=set)
     done: bool = False
 
@@ -237,12 +238,14 @@ class HbmImageStore:
         cuda = self.device.type == "cuda"
         ok = torch.zeros(len(w.names), dtype=torch.int32)
         local = None
-        if rank == w.dst and w.mine:
+        pack = getattr(got, "pack", None)   # GPU backend: full-resolution decodes, resized on the GPU
+        if rank == w.dst and w.mine and pack is None:
             local = torch.zeros((len(w.mine), *self.hw, 3), dtype=torch.uint8)
             for j, n in enumerate(w.mine):
                 img = got.get(n)
                 if img is not None:
                     local[j].numpy()[...] = img  # loader arrays may be read-only views
+        if rank == w.dst and w.mine:
             self.decoded += sum(1 for n in w.mine if got.get(n) is not None)
         pos = {n: i for i, n in enumerate(w.names)}
         for n in w.mine:
@@ -256,6 +259,12 @@ class HbmImageStore:
         with ctx:
             if cuda and local is not None:
                 local = local.pin_memory().to(self.device, non_blocking=True)
+            if pack is not None and rank == w.dst:
+                # the decoded images land in their slots straight from the pinned pack (one H2D
+                # copy + one resize kernel on the staging stream); no local rows to scatter
+                slot_of = dict(zip(w.names, w.slots))
+                pack.launch([slot_of[n] for n in pack.names], self.arena, stream)
+                w.pack = pack
             recv, work = None, []
             if world > 1 and w.shipped:
                 in_splits = [len(out_rows) if r == w.dst else 0 for r in range(world)]
@@ -292,7 +301,7 @@ class HbmImageStore:
                         raise CollectiveFailure(f"image window collective failed: {e}") from e
                 if self.me == w.dst:
                     # received rows arrive grouped by source rank, each group in window order
-                    order = [i for i, s in enumerate(w.src) if s == w.dst]
+                    order = [i for i, s in enumerate(w.src) if s == w.dst] if local is not None else []
                     order += [i for r in range(world) for i, s in enumerate(w.src) if s == r and s != w.dst]
                     rows = [t for t in (local, recv) if t is not None and t.shape[0]]
                     if rows:
@@ -317,6 +326,9 @@ class HbmImageStore:
             self.received += sum(1 for n, s in zip(w.names, w.src) if s != w.dst and n not in w.failed)
         if not cuda:
             w.event = None
+        if w.pack is not None:   # its H2D copy and resize ran before the window's event
+            w.pack.release()
+            w.pack = None
         w.bufs, w.work, w.flags, w.done = None, None, None, True
         return True
 

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import hashlib
 import logging
+import os
 import time
 from collections import OrderedDict
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -331,6 +332,83 @@ class StoreRankBackend(_ArenaStaging, RankBackend):
         return out, None
 
 
+def nearest_index(n_in: int, n_out: int) -> np.ndarray:
+    """Source index of each output row / column of Pillow's NEAREST resize, byte-identical
+    to Image.resize: Pillow walks the output with a float64 accumulator started at half a
+    step (sequential adds, then truncation) — np.add.accumulate adds in the same order."""
+    a = n_in / n_out
+    steps = np.full(n_out, a, np.float64)
+    steps[0] = a * 0.5
+    return np.add.accumulate(steps).astype(np.int16)
+
+
+class _PackedImages(dict):
+    """A window's decodes (name -> full-resolution RGB, None = failed) plus ``pack``: the
+    decoded images in one pinned buffer, resized into their arena slots by one kernel."""
+
+    pack = None
+
+
+class _Pack:
+    """Full-resolution images of one window in a pinned host buffer (built in the decode
+    pool): n records {pixel offset, h, w, row-table offset, column-table offset, slot} (int32),
+    the int16 nearest-index tables, the pixels. ``launch`` (serve loop, staging stream) fills in
+    the slots, copies it to the device once and resizes every image into its slot
+    (misc.hip resize_nearest_kernel); ``release`` returns the buffer after the window's event."""
+
+    def __init__(self, backend: "GpuRankBackend", names: List[str], imgs: List[np.ndarray], hw: Tuple[int, int]):
+        self.be, self.names, self.hw = backend, names, hw
+        n = len(names)
+        H, W = hw
+        tabs: Dict[Tuple[int, int], int] = {}
+        tab_parts: List[np.ndarray] = []
+        t_len = 0
+        recs = np.zeros((n, 6), np.int32)
+        for i, im in enumerate(imgs):
+            h, w = im.shape[:2]
+            for key, out in (((h, H), 3), ((w, W), 4)):
+                if key not in tabs:
+                    tabs[key] = t_len
+                    t = backend.nearest(*key)
+                    tab_parts.append(t)
+                    t_len += len(t)
+                recs[i, out] = tabs[key]
+            recs[i, 1], recs[i, 2] = h, w
+        pix0 = (n * 24 + t_len * 2 + 15) // 16 * 16
+        off = pix0
+        for i, im in enumerate(imgs):
+            recs[i, 0] = off
+            off += (im.nbytes + 15) // 16 * 16
+        self.nbytes = off
+        self.buf = backend.pinned(self.nbytes)
+        b = self.buf.numpy()
+        self.recs = b[:n * 24].view(np.int32).reshape(n, 6)
+        self.recs[...] = recs
+        if t_len:
+            b[n * 24:n * 24 + t_len * 2].view(np.int16)[...] = np.concatenate(tab_parts)
+        for i, im in enumerate(imgs):
+            o = int(recs[i, 0])
+            b[o:o + im.nbytes] = np.ascontiguousarray(im).reshape(-1)
+        self.dev = None
+
+    def launch(self, slots: List[int], arena: torch.Tensor, stream) -> None:
+        from .. import _native as N
+
+        self.recs[:, 5] = slots
+        H, W = self.hw
+        with torch.cuda.stream(stream):
+            self.dev = torch.empty(self.nbytes, dtype=torch.uint8, device=arena.device)
+            self.dev.copy_(self.buf[:self.nbytes], non_blocking=True)
+            N.check(N.lib().dml_resize_nearest(self.dev.data_ptr(), len(self.names), H, W, arena.data_ptr(),
+                                               stream.cuda_stream), "dml_resize_nearest")
+
+    def release(self) -> None:
+        self.dev = None
+        if self.buf is not None:
+            self.be.unpin(self.buf)
+            self.buf = None
+
+
 class GpuRankBackend(_ArenaStaging, RankBackend):
     """Native engines for both models resident in this GPU's HBM, fed from per-model
     HBM image stores (parallel/image_store.py: store images staged in windows ahead of
@@ -372,6 +450,10 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
 
         self._dcache: "OrderedDict[str, np.ndarray]" = OrderedDict()   # name -> full-res RGB (both models)
         self._dbytes, self.decode_hits, self._dlock = 0, 0, threading.Lock()
+        self._nn: Dict[Tuple[int, int], np.ndarray] = {}    # (n_in, n_out) -> nearest-index table
+        self._pins: List[torch.Tensor] = []                  # free pinned pack buffers
+        # DML_GPU_RESIZE=0: the decode pool resizes on the CPU (Pillow) as before (A/B)
+        self.gpu_resize = os.environ.get("DML_GPU_RESIZE", "1") != "0"
         self.host = [torch.zeros((2, self.cap, 5), dtype=torch.int32).pin_memory() for _ in range(SLOTS)]
         self.host_np = [h.numpy() for h in self.host]   # the serve loop reads rows without a torch call
         self.ev_done = [torch.cuda.Event() for _ in range(SLOTS)]
@@ -400,6 +482,26 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             self.engines[m].capture(self.stream)  # graphs now, before the service's first collective
 
     DECODE_CACHE_BYTES = 1 << 30
+    PIN_BYTES = 64 << 20
+
+    def nearest(self, n_in: int, n_out: int) -> np.ndarray:
+        t = self._nn.get((n_in, n_out))
+        if t is None:
+            t = self._nn[(n_in, n_out)] = nearest_index(n_in, n_out)
+        return t
+
+    def pinned(self, nbytes: int) -> torch.Tensor:
+        """(decode pool) a pinned buffer of at least nbytes: a free one of the pool or a new one."""
+        with self._dlock:
+            for i, b in enumerate(self._pins):
+                if b.numel() >= nbytes:
+                    return self._pins.pop(i)
+        return torch.empty(max(nbytes, self.PIN_BYTES), dtype=torch.uint8).pin_memory()
+
+    def unpin(self, buf: torch.Tensor) -> None:
+        with self._dlock:
+            if len(self._pins) < 32:
+                self._pins.append(buf)
 
     def _decoded(self, name: str, data: bytes) -> np.ndarray:
         """The full-resolution RGB decode of one store image, shared by both models' windows
@@ -416,7 +518,10 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
                 self._dcache.move_to_end(name)
                 self.decode_hits += 1
                 return hit
-        img = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"), dtype=np.uint8)
+        im = Image.open(io.BytesIO(data))
+        if im.mode != "RGB":   # load_img's convert; an RGB JPEG needs no copy
+            im = im.convert("RGB")
+        img = np.asarray(im, dtype=np.uint8)
         with self._dlock:
             self._dcache[name] = img
             self._dbytes += img.nbytes
@@ -426,12 +531,15 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         return img
 
     def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
-        """(decode pool thread) fetch + decode this rank's share of a window."""
+        """(decode pool thread) fetch + decode this rank's share of a window. GPU resize (the
+        default): the full-resolution decodes go into one pinned pack that the staging
+        stream resizes into the arena slots (_Pack); else Pillow NEAREST here, as
+        load_img(target_size)."""
         from PIL import Image
 
         blobs = self.loader(names) if self.loader else {}
         hw = self.arenas[model].hw
-        out: Dict[str, Optional[np.ndarray]] = {}
+        out = _PackedImages() if self.gpu_resize else {}
         for n in names:
             b = blobs.get(n)
             if b is None:
@@ -439,12 +547,16 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
                 continue
             try:
                 img = self._decoded(n, b)
-                if img.shape[:2] != tuple(hw):  # Pillow NEAREST, as load_img(target_size)
+                if not self.gpu_resize and img.shape[:2] != tuple(hw):
                     img = np.asarray(Image.fromarray(img).resize((hw[1], hw[0]), Image.NEAREST), dtype=np.uint8)
                 out[n] = img
             except Exception as e:  # undecodable file -> reported as failed
                 log.warning("decode of %s failed: %s", n, e)
                 out[n] = None
+        if self.gpu_resize:
+            ok = [n for n in names if out.get(n) is not None]
+            if ok:
+                out.pack = _Pack(self, ok, [out[n] for n in ok], hw)
         return out
 
     def launch(self, model, names, slot):
