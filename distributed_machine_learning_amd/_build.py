@@ -114,7 +114,7 @@ def _build_locked(stamp: str, stamp_file: Path, verbose: bool) -> Path:
 # Pure C++ host runtime pieces (no HIP): built with g++ in a second, tiny library
 # so that CPU-only processes (the CLI, the coordinator, tests) load it without
 # the HIP runtime, and so a kernel edit never rebuilds it.
-HOST_SOURCES = [CSRC / "host" / "output_json.cpp", CSRC / "host" / "shm_exchange.cpp"]
+HOST_SOURCES = [CSRC / "host" / "output_json.cpp", CSRC / "host" / "shm_exchange.cpp", CSRC / "host" / "store_io.cpp"]
 HOST_LIB_PATH = PKG_DIR / "libdml_host.so"
 
 

@@ -36,6 +36,8 @@ class NpEncoder(json.JSONEncoder):
 
 def image_key(name: str) -> str:
     """Output key of a batch image: its basename, without a pinned store version."""
+    if "/" not in name and VERSION_SEP not in name:
+        return name
     base = os.path.basename(name)
     head, sep, tail = base.rpartition(VERSION_SEP)
     return head if sep and tail.isdigit() else base
@@ -100,7 +102,11 @@ class BatchRenderer:
     def _key(self, name: str) -> bytes:
         k = self._keys.get(name)
         if k is None:
-            k = json.dumps(image_key(name)).encode()
+            base = image_key(name)
+            # printable ASCII without quote / backslash: json.dumps adds the quotes only
+            # (a job of unique synthetic names missed this cache for every image)
+            k = (b'"' + base.encode() + b'"' if base.isascii() and base.isprintable() and '"' not in base
+                 and "\\" not in base else json.dumps(base).encode())
             with self._lock:
                 if len(self._keys) > 1 << 20:
                     self._keys.clear()

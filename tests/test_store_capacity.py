@@ -32,7 +32,9 @@ def test_output_store_capacity_world8(tmp_path):
     nb = rec["batches"]["ResNet50"]
     print("store capacity", json.dumps(cap))
     assert rec["jobs_done"] and nb == world * 120
-    assert out["files_stored"] == nb and out["failed"] == 0
+    # a batch re-run after a rebuild writes a new version of the same name: >= nb files written,
+    # exactly nb distinct outputs listed
+    assert out["files_stored"] >= nb and out["failed"] == 0, (out, rec.get("rebuilds"))
     assert out["in_store"] == nb and out["distinct_batches_in_store"] == nb and out["listing_duplicates"] == 0
     assert cap["bytes_per_output"] > 120_000                      # real-size outputs
     need = world * 360

@@ -35,6 +35,29 @@ def _free_udp_base(n: int) -> int:
     raise RuntimeError("no port")
 
 
+def _profile_threads() -> None:
+    """DML_PROFILE_THREADS=<rank>: cProfile the rank's control-plane event loop and its output
+    writer thread (each in its own thread), printed when the thread ends."""
+    import cProfile
+    import pstats
+
+    from distributed_machine_learning_amd.parallel import rank_control, service
+
+    def wrap(fn, label):
+        def run(self, *a, **k):
+            prof = cProfile.Profile()
+            prof.enable()
+            try:
+                return fn(self, *a, **k)
+            finally:
+                prof.disable()
+                print(f"===== {label}", file=sys.stderr)
+                pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(25)
+        return run
+    rank_control.RankControl._main = wrap(rank_control.RankControl._main, "control loop")
+    service.OutputWriter._loop = wrap(service.OutputWriter._loop, "output writer")
+
+
 class _ThreadCpu:
     """CPU seconds of every thread of this process (/proc/self/task/*/stat utime + stime),
     snapshotted every 0.2 s (threads end before the run returns), named by the Python thread
@@ -140,6 +163,8 @@ def _rank(rank, world, rdzv, port, batches, rate, out_json, depth=0):
             d = time.perf_counter() - gcp["t"]
             gcp["max"], gcp["n"], gcp["total"] = max(gcp["max"], d), gcp["n"] + 1, gcp["total"] + d
     gc.callbacks.append(_gc_cb)
+    if os.environ.get("DML_PROFILE_THREADS") == str(rank):
+        _profile_threads()
     sampler = _Sampler() if os.environ.get("DML_SAMPLE_RANK") == str(rank) else None
     tcpu = _ThreadCpu()
     t0, c0 = time.perf_counter(), time.process_time()
