@@ -301,9 +301,9 @@ def test_job_three_times_the_arena_gpu(tmp_path):
     eg = ElasticGroup(0, 1, store_path=str(tmp_path / "rdzv"), backend="gloo", data_backend="nccl", timeout_s=120)
     try:
         bs = {"ResNet50": 8, "InceptionV3": 8}
-        be = GpuRankBackend(dev, bs, cap=8, arena_images=24, n_synth=8, loader=loader)
+        be = GpuRankBackend(dev, bs, cap=8, arena_images=16, n_synth=8, loader=loader)
         st = be.arenas["ResNet50"]
-        assert st.capacity == 24                      # 16 image slots for a 48-image job
+        assert st.capacity == 24                      # 16 image slots (+ 8 synthetic) for a 48-image job
         coord = ReplicatedCoordinator(bs, cap=8, host_tag="gpu")
         writer = OutputWriter(str(tmp_path / "out"), host_tag="gpu")
         svc = CollectiveService(eg, be, coord, writer=writer, on_device=False)
