@@ -122,7 +122,8 @@ def test_cli_drives_collective_service_and_matches_host_mode(tmp_path):
     assert c1["ResNet50"]["query_count"] == 100
     c2 = json.loads(out["c2"].split("\n[")[0])
     assert c2["ResNet50"]["batches"] == 10
-    assert json.loads(out["c5"].split("\n[")[0]) == {}
+    assert json.loads(out["c5"].split("\nrecent batches")[0].split("\n[")[0]) == {}
+    assert "(ResNet50) ran on rank" in out["c5"]          # C5 history: which rank ran each batch
     final_c = json.load(open(tmp_path / "dl_collective" / "final_31.json"))
     assert len(final_c) == 100
 
