@@ -108,7 +108,7 @@ int main() {
   CHECK(dml_conv_v2_bn(100) == 128 && dml_conv_v2_bn(103) == 64 && dml_conv_v2_bn(120) == 64 &&
         dml_conv_v2_bn(122) == 128);
   // patch-stationary tiles (conv_igemm_pt.hip): channel widths, and which convs they take (host code)
-  CHECK(dml_conv_v2_bn(140) == 128 && dml_conv_v2_bn(141) == 64 && dml_conv_v2_bn(144) == 64 && dml_conv_v2_bn(150) == 0);
+  CHECK(dml_conv_v2_bn(140) == 128 && dml_conv_v2_bn(141) == 64 && dml_conv_v2_bn(144) == 64 && dml_conv_v2_bn(158) == 0);
   {
     DmlConvArgs one = conv_args(128, 64, 3, 3);                     // one patch buffer: a single 64-channel chunk only
     CHECK(dml_conv_pt_fits(&one, 144) == 0 && dml_conv_pt_fits(&one, 141) == 1);
@@ -124,6 +124,22 @@ int main() {
     r.H = r.W = r.Ho = r.Wo = 35;
     CHECK(dml_conv_pt_fits(&r, 140) == 0);
     CHECK(dml_conv(&p, 140, nullptr) != 0);                          // the launcher refuses what fits() refuses
+  }
+  // row-ring 3x3 kernel (conv_rowring.hip): ResNet50 stage 2 only
+  CHECK(dml_conv_v2_bn(150) == 64 && dml_conv_v2_bn(155) == 64);
+  {
+    DmlConvArgs s2 = conv_args(64, 64, 3, 3);
+    s2.H = s2.W = s2.Ho = s2.Wo = 56;
+    CHECK(dml_conv_rr_fits(&s2) == 1);
+    s2.Cout = 48; s2.ldy = 48;
+    CHECK(dml_conv_rr_fits(&s2) == 1);
+    s2.Cout = 128; s2.ldy = 128;                                      // > 64 output channels: refused
+    CHECK(dml_conv_rr_fits(&s2) == 0);
+    DmlConvArgs s3 = conv_args(128, 128, 3, 3);                       // stage 3 (28 x 28, Cin 128): refused
+    s3.H = s3.W = s3.Ho = s3.Wo = 28;
+    CHECK(dml_conv_rr_fits(&s3) == 0);
+    CHECK(dml_conv(&s3, 150, nullptr) != 0);
+    CHECK(std::string(dml_last_error()).find("dml_conv_rr") != std::string::npos);
   }
   a = conv_args(64, 64, 3, 3);
   a.nseg = 5;

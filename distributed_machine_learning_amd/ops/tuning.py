@@ -32,6 +32,9 @@ WSP_CFGS = tuple(range(120, 130))
 # M tile of whole output rows is loaded once per channel chunk, r5); they refuse what they
 # cannot run (stride / dilation != 1, Cin % 64, a patch larger than the config's)
 PT_CFGS = tuple(range(140, 150))
+# the row-ring 3x3 kernel of ResNet50 stage 2 (csrc/kernels/conv_rowring.hip: weights resident in
+# LDS, input rows streamed once per strip; 2 / 1 / 4 strips per image, LDS-staged / direct epilogue, r5)
+RR_CFGS = (150, 151, 152, 153, 154, 155)
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))
@@ -88,6 +91,14 @@ def _excluded() -> set:
     return {int(c) for c in v.split(",") if c.strip()}
 
 
+def rr_fits(a: N.ConvArgs) -> bool:
+    """The shapes conv_rowring.hip runs (mirrors its launcher's check)."""
+    return (a.kh == 3 and a.kw == 3 and a.ph == 1 and a.pw == 1 and a.sh == 1 and a.sw == 1
+            and max(a.dh, 1) == 1 and max(a.dw, 1) == 1 and a.Cin == 64 and a.Cout <= 64
+            and a.W == 56 and a.Wo == 56 and a.Ho == a.H and a.ksplit <= 1 and a.nseg == 0
+            and a.rsub <= 1 and a.Kpad >= 576)
+
+
 def valid_cfgs(a: N.ConvArgs) -> List[int]:
     if a.Cout % 8 or a.Cin % 8 or a.ldx % 8 or a.ldy % 8:
         return []
@@ -96,6 +107,8 @@ def valid_cfgs(a: N.ConvArgs) -> List[int]:
     cands += list(WS_CFGS) + ([] if a.ksplit > 1 else list(WSP_CFGS))
     if a.ksplit <= 1 and a.sh == 1 and a.sw == 1 and max(a.dh, 1) == 1 and max(a.dw, 1) == 1 and a.Cin % 64 == 0:
         cands += list(PT_CFGS)
+    if rr_fits(a):
+        cands += list(RR_CFGS)
     return [c for c in cands if c not in ex]
 
 
