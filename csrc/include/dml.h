@@ -206,12 +206,13 @@ int dml_conv_pt(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_pt_bn(int cfg);
 int dml_conv_pt_fits(const DmlConvArgs* a, int cfg);
 int dml_conv_pt_init(void);
-// row-ring 3x3 convolution of ResNet50 stage 2 (conv_rowring.hip; cfg ids 150..155 = 2 / 1 / 4
+// row-ring 3x3 convolution of ResNet50 stage 2 (conv_rowring.hip; cfg ids 150..152 = 2 / 1 / 4
 // strips per image): weights LDS-resident, input rows streamed through a 10-row ring; refuses
 // anything but 3x3 pad 1 stride 1, Cin 64, Cout <= 64, width 56
 int dml_conv_rr(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_rr_fits(const DmlConvArgs* a);
 int dml_conv_rr_init(void);
+int dml_conv_rr_stamped(const DmlConvArgs* a, int cfg, void* stamps, hipStream_t s);  // phase probe
 int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);

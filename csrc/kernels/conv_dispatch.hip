@@ -7,7 +7,7 @@
 // tile configuration (dml_conv_v2), ids 100..119 a warp-specialised one (loader +
 // MFMA waves, dml_conv_ws, conv_igemm_ws.hip), ids 120..139 its persistent form
 // (dml_conv_wsp, conv_igemm_wsp.hip), ids 140..159 the patch-stationary stride-1 tiles
-// (dml_conv_pt, conv_igemm_pt.hip), ids 150..155 the row-ring 3x3 kernel of ResNet50 stage 2
+// (dml_conv_pt, conv_igemm_pt.hip), ids 150..152 the row-ring 3x3 kernel of ResNet50 stage 2
 // (dml_conv_rr, conv_rowring.hip); they are part of the ABI the plan builder and the
 // autotuner (ops/tuning.py) use.
 //
@@ -27,7 +27,7 @@ static int validate(const DmlConvArgs* a, int cfg) {
   const int bn = dml_conv_v2_bn(cfg);
   if (bn <= 0) {
     dml_set_error("dml_conv: cfg must be a tile config (v2: 10..63, warp-specialised: 100..119, persistent: "
-                  "120..139, patch-stationary: 140..149, row-ring: 150..155)");
+                  "120..139, patch-stationary: 140..149, row-ring: 150..152)");
     return -1;
   }
   // weights are packed with Cout padded to a multiple of 256 rows; a 96- or

@@ -505,7 +505,7 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
 // channel-tile width of a config (0: not a config); ids 100..119: the warp-specialised
 // tiles of conv_igemm_ws.hip, 120..139 their persistent form (conv_igemm_wsp.hip)
 extern "C" int dml_conv_v2_bn(int cfg) {
-  if (cfg >= 150) return cfg <= 157 ? 64 : 0;  // row-ring 3x3 kernel (conv_rowring.hip); 156 / 157: timing probes
+  if (cfg >= 150) return cfg <= 152 ? 64 : 0;  // row-ring 3x3 kernel (conv_rowring.hip)
   if (cfg >= 140) return dml_conv_pt_bn(cfg);
   if (cfg >= 120) return dml_conv_wsp_bn(cfg);
   if (cfg >= 100) return dml_conv_ws_bn(cfg);

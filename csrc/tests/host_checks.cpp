@@ -108,7 +108,7 @@ int main() {
   CHECK(dml_conv_v2_bn(100) == 128 && dml_conv_v2_bn(103) == 64 && dml_conv_v2_bn(120) == 64 &&
         dml_conv_v2_bn(122) == 128);
   // patch-stationary tiles (conv_igemm_pt.hip): channel widths, and which convs they take (host code)
-  CHECK(dml_conv_v2_bn(140) == 128 && dml_conv_v2_bn(141) == 64 && dml_conv_v2_bn(144) == 64 && dml_conv_v2_bn(158) == 0);
+  CHECK(dml_conv_v2_bn(140) == 128 && dml_conv_v2_bn(141) == 64 && dml_conv_v2_bn(144) == 64 && dml_conv_v2_bn(153) == 0);
   {
     DmlConvArgs one = conv_args(128, 64, 3, 3);                     // one patch buffer: a single 64-channel chunk only
     CHECK(dml_conv_pt_fits(&one, 144) == 0 && dml_conv_pt_fits(&one, 141) == 1);
@@ -126,7 +126,7 @@ int main() {
     CHECK(dml_conv(&p, 140, nullptr) != 0);                          // the launcher refuses what fits() refuses
   }
   // row-ring 3x3 kernel (conv_rowring.hip): ResNet50 stage 2 only
-  CHECK(dml_conv_v2_bn(150) == 64 && dml_conv_v2_bn(155) == 64);
+  CHECK(dml_conv_v2_bn(150) == 64 && dml_conv_v2_bn(152) == 64);
   {
     DmlConvArgs s2 = conv_args(64, 64, 3, 3);
     s2.H = s2.W = s2.Ho = s2.Wo = 56;

@@ -33,8 +33,8 @@ WSP_CFGS = tuple(range(120, 130))
 # cannot run (stride / dilation != 1, Cin % 64, a patch larger than the config's)
 PT_CFGS = tuple(range(140, 150))
 # the row-ring 3x3 kernel of ResNet50 stage 2 (csrc/kernels/conv_rowring.hip: weights resident in
-# LDS, input rows streamed once per strip; 2 / 1 / 4 strips per image, LDS-staged / direct epilogue, r5)
-RR_CFGS = (150, 151, 152, 153, 154, 155)
+# LDS, input rows streamed once per strip; 2 / 1 / 4 strips per image, r5)
+RR_CFGS = (150, 151, 152)
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))

@@ -254,6 +254,11 @@ class PacedRankBackend(RankBackend):
         self.p = np.ascontiguousarray(p / p.sum(1, keepdims=True)).view(np.int32)
         self.busy_until = 0.0
         self.launched = 0
+        self.idle_s, self.idle_n, self.first, self.real = 0.0, 0, 0.0, 0   # gaps the "GPU" sat idle (capacity runs)
+
+    def reset_stats(self) -> None:
+        """(service_bench, after the untimed warm-up launches) idle accounting starts here."""
+        self.idle_s, self.idle_n, self.real = 0.0, 0, 0
 
     def launch(self, model, names, slot):
         if len(names) > self.cap:
@@ -263,7 +268,14 @@ class PacedRankBackend(RankBackend):
         out = np.zeros((2, self.cap, 5), np.int32)   # numpy: no torch call (GIL hand-off) per launch
         out[0, :k] = self.ids[i0:i0 + k]
         out[1, :k] = self.p[i0:i0 + k]
-        self.busy_until = max(time.monotonic(), self.busy_until) + self.dt
+        now = time.monotonic()
+        if self.real == 0:
+            self.first = max(now, self.busy_until)
+        elif now > self.busy_until:
+            self.idle_s += now - self.busy_until
+            self.idle_n += 1
+        self.real += 1
+        self.busy_until = max(now, self.busy_until) + self.dt
         self.launched += 1
         return out, _Deadline(self.busy_until)
 

@@ -980,6 +980,9 @@ class CollectiveService:
         if not self._frozen:
             gc.collect()
             gc.freeze()
+            th = os.environ.get("DML_GC_THRESHOLD", "")
+            if th:   # A/B knob: young-generation collection thresholds while serving
+                gc.set_threshold(*(int(v) for v in th.split(",")))
             self._frozen = True
 
     def serve(self, max_steps: int = 10 ** 9, stop_when_idle: bool = False, deadline: Optional[float] = None) -> int:

@@ -164,6 +164,7 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                     ev.synchronize()
         if torch.cuda.is_available():
             torch.cuda.synchronize()
+        getattr(backend, "reset_stats", lambda: None)()
         build_s = time.perf_counter() - t_build
         svc.freeze_heap()
         eg.barrier()

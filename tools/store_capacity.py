@@ -173,9 +173,15 @@ def _rank(rank, world, rdzv, port, batches, rate, out_json, depth=0):
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    bes = []
+
+    def make_backend():
+        bes.append(PacedRankBackend(cap=256, batches_per_s=rate))
+        return bes[-1]
     rec = service_bench.run(rank, world, None, rdzv, port, batches * 256 * world, 0,
                             {"ResNet50": 256, "InceptionV3": 128}, None, comm="gloo", data_backend="gloo", depth=depth,
-                            make_backend=lambda: PacedRankBackend(cap=256, batches_per_s=rate))
+                            make_backend=make_backend)
+    be = bes[-1] if bes else None
     if sampler is not None:
         sampler.report()
 
@@ -188,7 +194,10 @@ def _rank(rank, world, rdzv, port, batches, rate, out_json, depth=0):
     threads = tcpu.result()
     with open(f"{out_json}.cpu{rank}", "w") as f:  # this rank's CPU seconds (all its threads), GC pauses
         json.dump({"cpu_s": time.process_time() - c0, "gc_max_ms": gcp["max"] * 1e3, "gc_n": gcp["n"],
-                   "gc_total_ms": gcp["total"] * 1e3, "objects": len(gc.get_objects()), "threads": threads}, f)
+                   "gc_total_ms": gcp["total"] * 1e3, "objects": len(gc.get_objects()), "threads": threads,
+                   "idle_s": be.idle_s if be else 0.0, "idle_n": be.idle_n if be else 0,
+                   "span_s": (be.busy_until - be.first) if be and be.real else 0.0,
+                   "launched": be.real if be else 0}, f)
     if rank == 0 and rec is not None:
         rec["wall_s_incl_build"] = round(time.perf_counter() - t0, 2)
         with open(out_json, "w") as f:
@@ -228,7 +237,13 @@ def measure(world: int = 8, rate: float = 370.0, batches_per_rank: int = 300, tm
                        "gc_max_pause_ms": round(max(p["gc_max_ms"] for p in per), 1),
                        "gc_pause_total_ms_per_rank": [round(p["gc_total_ms"]) for p in per],
                        "gc_tracked_objects_per_rank": [p["objects"] for p in per],
-                       "thread_cpu_s_rank0": per[0]["threads"], "thread_cpu_s_coordinator": per[-1]["threads"]}
+                       "thread_cpu_s_rank0": per[0]["threads"], "thread_cpu_s_coordinator": per[-1]["threads"],
+                       # the paced "GPU": launches, first launch -> last completion, and the gaps it sat
+                       # idle between (a rank's host side not feeding it)
+                       "backend_launched_per_rank": [p["launched"] for p in per],
+                       "backend_span_s_per_rank": [round(p["span_s"], 3) for p in per],
+                       "backend_idle_s_per_rank": [round(p["idle_s"], 3) for p in per],
+                       "backend_idle_gaps_per_rank": [p["idle_n"] for p in per]}
     return rec
 
 
@@ -239,6 +254,9 @@ def main():
     ap.add_argument("--batches-per-rank", type=int, default=300)
     ap.add_argument("--depth", type=int, default=0, help="batches in flight per rank (0: service.auto_depth)")
     ap.add_argument("--out", default="")
+    ap.add_argument("--min-rate", type=float, default=-1.0,
+                    help="exit 1 below this many batches/s (-1: 360 x world on a host with >= 64 CPUs, "
+                         "else no rate check); the exactly-once listing is always checked")
     a = ap.parse_args()
     rec = measure(a.world, a.rate, a.batches_per_rank, depth=a.depth)
     print(json.dumps(rec["capacity"]), flush=True)
@@ -248,7 +266,19 @@ def main():
     if a.out:
         with open(a.out, "w") as f:
             json.dump(rec, f, indent=1)
+    nb = a.world * a.batches_per_rank
+    o = rec["outputs"]
+    bad = []
+    if not (o["failed"] == 0 and o["in_store"] == nb and o["distinct_batches_in_store"] == nb
+            and o["listing_duplicates"] == 0):
+        bad.append(f"listing not exactly-once: {nb} batches, outputs {o}")
+    floor = a.min_rate if a.min_rate >= 0 else (360.0 * a.world if (os.cpu_count() or 1) >= 64 else 0.0)
+    if rec["capacity"]["batches_per_s"] < floor:
+        bad.append(f"{rec['capacity']['batches_per_s']} batches/s < {floor}")
+    print("CAPACITY " + ("FAIL: " + "; ".join(bad) if bad else f"OK: >= {floor:.0f} batches/s, "
+                         f"{nb} outputs listed exactly once"), flush=True)
+    return 1 if bad else 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
