@@ -26,17 +26,17 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ..serving.jobs import MODELS
+from ..serving.jobs import MODELS, SYNTH, SynthNames
 from ..serving.output import VERSION_SEP
 
 log = logging.getLogger(__name__)
 MODEL_IDS = {m: i for i, m in enumerate(MODELS)}
-SYNTH = "synthetic:"
 SLOTS = 2   # batches a GPU rank has launched at once (engine source / result slots)
 
 
-def synthetic_names(n: int) -> List[str]:
-    return [f"{SYNTH}{i}" for i in range(n)]
+def synthetic_names(n: int) -> SynthNames:
+    """SYNTH + str(i), i < n, as a lazy sequence (serving/jobs.SynthNames)."""
+    return SynthNames(0, n)
 
 
 def split_version(name: str) -> Tuple[str, Optional[int]]:
@@ -461,14 +461,15 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         import threading
 
         self._dcache: "OrderedDict[str, np.ndarray]" = OrderedDict()   # name -> full-res RGB (both models)
+        self._nprocs, self._dprocs = int(os.environ.get("DML_DECODE_PROCS", "8")), None
         self._dbytes, self.decode_hits, self._dlock = 0, 0, threading.Lock()
         self._nn: Dict[Tuple[int, int], np.ndarray] = {}    # (n_in, n_out) -> nearest-index table
         self._pins: List[torch.Tensor] = []                  # free pinned pack buffers
         # DML_GPU_RESIZE=0: the decode pool resizes on the CPU (Pillow) as before (A/B)
         self.gpu_resize = os.environ.get("DML_GPU_RESIZE", "1") != "0"
-        # a window's images are decoded by this pool, DECODE_CHUNK per task (a window task used to
-        # decode its whole share alone: ~3.3k img/s on the 51,200-distinct run with 32 threads,
-        # bound by the few windows in flight). Pillow releases the GIL inside the JPEG decoder.
+        # a window's images are decoded DECODE_CHUNK per task by this pool, each task handing its
+        # chunk to a decode worker PROCESS (parallel/decode_worker.py; in-process threads held
+        # the GIL for ~0.3 ms per image: ~3.5k img/s on the 51,200-distinct run with 32 threads)
         from concurrent.futures import ThreadPoolExecutor
         self.decode_threads = decode_threads
         self._jpool = ThreadPoolExecutor(max_workers=decode_threads, thread_name_prefix="jpeg")
@@ -522,32 +523,46 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             if len(self._pins) < 32:
                 self._pins.append(buf)
 
-    def _decoded(self, name: str, data: bytes) -> np.ndarray:
-        """The full-resolution RGB decode of one store image, shared by both models' windows
-        (the JPEG is decoded once per rank, then resized per model: Keras load_img decodes,
-        converts to RGB, then resizes — the same steps in the same order, so the result is
-        byte-identical to serving.inference.load_image)."""
-        import io
-
-        from PIL import Image
-
+    def _cached(self, name: str) -> Optional[np.ndarray]:
+        """The full-resolution RGB decode of one store image if this rank holds it (shared by
+        both models' windows: Keras load_img decodes, converts to RGB, then resizes — the same
+        steps in the same order, so the result is byte-identical to
+        serving.inference.load_image)."""
         with self._dlock:
             hit = self._dcache.get(name)
             if hit is not None:
                 self._dcache.move_to_end(name)
                 self.decode_hits += 1
-                return hit
-        im = Image.open(io.BytesIO(data))
-        if im.mode != "RGB":   # load_img's convert; an RGB JPEG needs no copy
-            im = im.convert("RGB")
-        img = np.asarray(im, dtype=np.uint8)
+            return hit
+
+    def _remember(self, name: str, img: np.ndarray) -> None:
         with self._dlock:
             self._dcache[name] = img
             self._dbytes += img.nbytes
             while self._dbytes > self.DECODE_CACHE_BYTES and self._dcache:
                 _, old = self._dcache.popitem(last=False)
                 self._dbytes -= old.nbytes
-        return img
+
+    @staticmethod
+    def _decode_here(data: bytes) -> np.ndarray:
+        import io
+
+        from PIL import Image
+
+        im = Image.open(io.BytesIO(data))
+        if im.mode != "RGB":   # load_img's convert; an RGB JPEG needs no copy
+            im = im.convert("RGB")
+        return np.asarray(im, dtype=np.uint8)
+
+    def _procs(self):
+        """The decode worker processes (parallel/decode_worker.py), started on first use:
+        DML_DECODE_PROCS (default 8; 0 = decode in this process's threads)."""
+        if self._dprocs is None and self._nprocs > 0:
+            with self._dlock:
+                if self._dprocs is None:
+                    from .decode_worker import DecodeProcs
+                    self._dprocs = DecodeProcs(self._nprocs)
+        return self._dprocs
 
     def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
         """(decode pool thread) fetch + decode this rank's share of a window. GPU resize (the
@@ -561,14 +576,31 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         out = _PackedImages() if self.gpu_resize else {}
 
         def decode(chunk):
-            res = []
+            res, miss = [], []
             for n in chunk:
                 b = blobs.get(n)
                 if b is None:
                     res.append((n, None))
                     continue
+                hit = self._cached(n)
+                if hit is not None:
+                    res.append((n, hit))
+                else:
+                    miss.append((n, b))
+            got: Dict[str, Optional[np.ndarray]] = {}
+            procs = self._procs() if miss else None
+            if procs is not None:
                 try:
-                    img = self._decoded(n, b)
+                    got = procs.decode_many(miss)
+                except Exception as e:   # a dead worker: this chunk decodes here
+                    log.warning("decode worker failed (%s); decoding in-process", e)
+                    got = {}
+            for n, b in miss:
+                try:
+                    img = got[n] if n in got else self._decode_here(b)
+                    if img is None:
+                        raise ValueError("undecodable image")
+                    self._remember(n, img)
                     if not self.gpu_resize and img.shape[:2] != tuple(hw):
                         img = np.asarray(Image.fromarray(img).resize((hw[1], hw[0]), Image.NEAREST), dtype=np.uint8)
                     res.append((n, img))

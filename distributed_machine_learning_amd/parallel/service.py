@@ -90,7 +90,7 @@ import numpy as np
 import torch
 
 from ..serving.cost_model import CostModel
-from ..serving.jobs import MODELS, Batch, JobManager
+from ..serving.jobs import MODELS, Batch, JobManager, as_names, json_default
 from ..serving.metrics import Metrics
 from ..serving.output import BatchRenderer, output_name
 from ..serving.scheduler import best_split
@@ -169,7 +169,7 @@ class ReplicatedCoordinator:
         """Apply one replicated log record; returns what the requester is told."""
         op = rec["op"]
         if op == "submit":
-            job = self.jobs.submit_images(rec["model"], list(rec["images"]), rec.get("requester", "client"),
+            job = self.jobs.submit_images(rec["model"], as_names(rec["images"]), rec.get("requester", "client"),
                                           now=time.monotonic(), job_id=int(rec["job_id"]))
             return {"jobid": job.job_id, "batches": job.batches_total}
         if op == "batch_size":
@@ -668,6 +668,7 @@ class CollectiveService:
         self.last_progress = time.monotonic()
         self.phase_s: Dict[str, float] = {"poll": 0.0, "plan": 0.0, "collective": 0.0, "apply": 0.0,
                                           "launch": 0.0, "sleep": 0.0}
+        self.phase_max: Dict[str, float] = dict.fromkeys(self.phase_s, 0.0)   # the longest single step part
         self.batches_per_step_max = 0
         self._watchdog = None
         if watchdog_s > 0:
@@ -691,7 +692,7 @@ class CollectiveService:
     def submit_local(self, model: str, n_images: int = 0, images: Optional[List[str]] = None,
                      requester: str = "local", reply: Optional[Callable[[dict], None]] = None) -> None:
         """Queue a submit on the coordinator (applied at the next step)."""
-        names = list(images) if images is not None else synthetic_names(n_images)
+        names = list(images) if images is not None else synthetic_names(n_images)   # lazy: two ints
         self._inbox.put(({"op": "submit", "model": model, "images": names, "requester": requester}, reply))
 
     def set_batch_size(self, model: str, bs: int, reply: Optional[Callable[[dict], None]] = None) -> None:
@@ -790,10 +791,11 @@ class CollectiveService:
         L = rec_len(world, depth)
         tab, req, rep, ack = _offs(world, depth)
         root = eg.group_rank_of(self.coordinator_rank())
-        ph, t0 = self.phase_s, time.perf_counter()
+        ph, pm, t0 = self.phase_s, self.phase_max, time.perf_counter()
         moved0 = self._poll()
         t1 = time.perf_counter()
         ph["poll"] += t1 - t0
+        pm["poll"] = max(pm["poll"], t1 - t0)
         active = self.is_coordinator()
         payload, recs, replies, results = b"", [], [], []
         table, reqs, grow, stop = None, [], [], False
@@ -810,10 +812,11 @@ class CollectiveService:
                         disp, reqs = coord.plan(eg.members)
                         table = coord.table(eg.members, disp)
             if recs:
-                payload = json.dumps(recs).encode()
+                payload = json.dumps(recs, default=json_default).encode()
         rec, reports, answers = self._record(L, depth, active, len(payload), stop, grow, table, reqs)
         t2 = time.perf_counter()
         ph["plan"] += t2 - t1
+        pm["plan"] = max(pm["plan"], t2 - t1)
         # ---- the step's collective (+ the log bytes, rarely) ----
         # host path (shared-memory exchange): numpy end to end — every torch call on the serve
         # loop hands the GIL to the rank's writer / control threads and waits to get it back
@@ -848,6 +851,7 @@ class CollectiveService:
             raise
         t3 = time.perf_counter()
         ph["collective"] += t3 - t2
+        pm["collective"] = max(pm["collective"], t3 - t2)
         # ---- apply, in the same order on every rank: log, reports, answers, table ----
         with coord.lock:
             for r in applied_here:
@@ -896,6 +900,7 @@ class CollectiveService:
             self.control.jobs_progress(finished)
         t4 = time.perf_counter()
         ph["apply"] += t4 - t3
+        pm["apply"] = max(pm["apply"], t4 - t3)
         if mine is None:  # STOP (sent only when nothing is queued or in flight)
             return False
         self.batches_per_step_max = max(self.batches_per_step_max, moved)
@@ -934,6 +939,7 @@ class CollectiveService:
         self.last_progress = time.monotonic()
         t5 = time.perf_counter()
         ph["launch"] += t5 - t4
+        pm["launch"] = max(pm["launch"], t5 - t4)
         if not (reports or answers or mine or n or self.done or self.answers or self.gpu or self.hostq):
             time.sleep(self.poll_sleep if coord.inflight else self.idle_sleep)
             ph["sleep"] += time.perf_counter() - t5
@@ -980,9 +986,12 @@ class CollectiveService:
         if not self._frozen:
             gc.collect()
             gc.freeze()
-            th = os.environ.get("DML_GC_THRESHOLD", "")
-            if th:   # A/B knob: young-generation collection thresholds while serving
-                gc.set_threshold(*(int(v) for v in th.split(",")))
+            # young-generation passes 100x rarer than CPython's default (700, 10, 10): the serve
+            # loop's garbage is acyclic (freed by refcount), and every pass holds the GIL on a
+            # lockstep rank (world-8 capacity 2500 -> 2614 batches/s, profiles/r5_rr);
+            # DML_GC_THRESHOLD=<g0,g1,g2> overrides (A/B)
+            th = os.environ.get("DML_GC_THRESHOLD", "100000,50,1000")
+            gc.set_threshold(*(int(v) for v in th.split(",")))
             self._frozen = True
 
     def serve(self, max_steps: int = 10 ** 9, stop_when_idle: bool = False, deadline: Optional[float] = None) -> int:

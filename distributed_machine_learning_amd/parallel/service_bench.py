@@ -230,6 +230,7 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                 "kills": [f"{r}:{d}" for r, d in kills], "final_members": eg.members,
                 "jobs_done": all(j.done for j in coord.jobs.jobs.values()),
                 "loop_phase_s": {k: round(v, 4) for k, v in svc.phase_s.items()},
+                "loop_phase_max_ms_coordinator": {k: round(v * 1e3, 2) for k, v in svc.phase_max.items()},
                 "comm": comm, "depth": depth, "build_s": round(build_s, 1),
                 "data": "synthetic uint8 images (seeded HBM arena), random-init weights",
             }

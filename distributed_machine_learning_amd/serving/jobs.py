@@ -12,10 +12,76 @@ from __future__ import annotations
 import itertools
 from collections import deque
 from dataclasses import asdict, dataclass
-from typing import Deque, Dict, List, Optional
+from typing import Deque, Dict, List, Optional, Sequence
 
 MODELS = ("ResNet50", "InceptionV3")
 FIRST_JOB_ID = 31
+SYNTH = "synthetic:"
+
+
+class SynthNames(Sequence):
+    """The synthetic image names SYNTH + str(i) for i in [lo, hi), never materialised: a
+    9,600-batch synthetic job is two integers in the replicated log and per batch, not 2.4M
+    strings JSON-encoded, broadcast and rebuilt on every rank in one step (measured: a 200 ms
+    stall of the whole lockstep group at world 8, tools/store_capacity.py)."""
+
+    __slots__ = ("lo", "hi")
+
+    def __init__(self, lo: int, hi: int):
+        self.lo, self.hi = int(lo), max(int(lo), int(hi))
+
+    def __len__(self) -> int:
+        return self.hi - self.lo
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            a, b, st = i.indices(len(self))
+            if st == 1:
+                return SynthNames(self.lo + a, self.lo + max(a, b))
+            return [self[j] for j in range(a, b, st)]
+        n = len(self)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError(i)
+        return f"{SYNTH}{self.lo + i}"
+
+    def __iter__(self):
+        return (f"{SYNTH}{i}" for i in range(self.lo, self.hi))
+
+    def __eq__(self, other) -> bool:
+        if isinstance(other, SynthNames):
+            return (self.lo, self.hi) == (other.lo, other.hi) or (len(self) == 0 and len(other) == 0)
+        try:
+            return len(other) == len(self) and all(a == b for a, b in zip(self, other))
+        except TypeError:
+            return NotImplemented
+
+    def __hash__(self):
+        return hash((self.lo, self.hi))
+
+    def __repr__(self) -> str:
+        return f"SynthNames({self.lo}, {self.hi})"
+
+    def to_json(self) -> dict:
+        return {"synth": [self.lo, self.hi]}
+
+
+def as_names(x) -> Sequence[str]:
+    """An image list from a log record / snapshot: SynthNames stay lazy ({"synth": [lo, hi]} in
+    JSON), anything else becomes a list."""
+    if isinstance(x, SynthNames):
+        return x
+    if isinstance(x, dict) and "synth" in x:
+        return SynthNames(*x["synth"])
+    return list(x)
+
+
+def json_default(o):
+    """json.dumps(default=...) for records that carry SynthNames."""
+    if isinstance(o, SynthNames):
+        return o.to_json()
+    raise TypeError(f"not JSON serializable: {type(o).__name__}")
 
 
 @dataclass
@@ -23,7 +89,7 @@ class Batch:
     job_id: int
     batch_id: int
     model: str
-    images: List[str]
+    images: Sequence[str]      # a list, or SynthNames (lazy synthetic names)
     attempts: int = 0          # dispatches so far (preemption / failure re-dispatch)
 
     @property
@@ -31,11 +97,13 @@ class Batch:
         return (self.job_id, self.batch_id)
 
     def to_dict(self) -> dict:
-        return asdict(self)
+        return {"job_id": self.job_id, "batch_id": self.batch_id, "model": self.model,
+                "images": self.images.to_json() if isinstance(self.images, SynthNames) else list(self.images),
+                "attempts": self.attempts}
 
     @staticmethod
     def from_dict(d: dict) -> "Batch":
-        return Batch(int(d["job_id"]), int(d["batch_id"]), d["model"], list(d["images"]), int(d.get("attempts", 0)))
+        return Batch(int(d["job_id"]), int(d["batch_id"]), d["model"], as_names(d["images"]), int(d.get("attempts", 0)))
 
 
 @dataclass
@@ -61,7 +129,7 @@ def pick_images(sorted_images: List[str], n: int) -> List[str]:
     return [sorted_images[i % len(sorted_images)] for i in range(n)]
 
 
-def make_batches(job_id: int, model: str, images: List[str], batch_size: int) -> List[Batch]:
+def make_batches(job_id: int, model: str, images: Sequence[str], batch_size: int) -> List[Batch]:
     if batch_size < 1:
         raise ValueError("batch_size must be >= 1")
     return [Batch(job_id, i // batch_size + 1, model, images[i:i + batch_size])
@@ -102,7 +170,8 @@ class JobManager:
         else:
             jid = int(job_id)
             self._ids = itertools.count(max([jid] + list(self.jobs)) + 1)
-        batches = make_batches(jid, model, list(images), self.batch_sizes[model])
+        images = as_names(images)
+        batches = make_batches(jid, model, images, self.batch_sizes[model])
         job = Job(jid, model, len(images), requester, len(batches), 0, now)
         self.jobs[jid] = job
         self.queues[model].extend(batches)

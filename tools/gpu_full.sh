@@ -16,5 +16,5 @@ if [ -n "$DISTINCT" ]; then
   python tools/bench_summary.py gpurun_out/bench_distinct.log
 fi
 if [ -n "$STORECAP" ]; then
-  timeout -k 10 600 python -u tools/store_capacity.py --world 8 --rate 370 --batches-per-rank 300 --out gpurun_out/store_capacity_box4.json > gpurun_out/store_capacity_box4.log 2>&1; echo "storecap rc=$?"; grep world gpurun_out/store_capacity_box4.log | cut -c1-400
+  timeout -k 10 600 python -u tools/store_capacity.py --world 8 --rate 370 --batches-per-rank 1200 --out gpurun_out/store_capacity_box4.json > gpurun_out/store_capacity_box4.log 2>&1; echo "storecap rc=$?"; grep -E "CAPACITY" gpurun_out/store_capacity_box4.log
 fi

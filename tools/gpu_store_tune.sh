@@ -1,0 +1,15 @@
+#!/bin/bash
+# One gpurun call: the default bench (headline + service + store-image pass) and the honest
+# 51,200-distinct-image store pass with the decode worker processes, then tuning-table adoption
+# of ADD=<cfg ids> with an interleaved bench A/B (tools/gpu_ws_tune.sh).
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u bench.py > gpurun_out/bench_full.log 2>&1 || { tail -30 gpurun_out/bench_full.log; exit 1; }
+python tools/bench_summary.py gpurun_out/bench_full.log
+timeout -k 10 900 python -u bench.py --steps 5 --warmup 2 --svc-store-images 51200 --svc-store-time-limit 600 > gpurun_out/bench_distinct.log 2>&1 || { tail -30 gpurun_out/bench_distinct.log; exit 1; }
+python tools/bench_summary.py gpurun_out/bench_distinct.log
+if [ -n "$ADD" ]; then
+  bash tools/gpu_ws_tune.sh || exit 1
+fi
