@@ -442,12 +442,6 @@ static int set_attr() {
   /* 128x64 tile waits on DRAM latency every K tile: one tap of 64 channels per stage) */         \
   X(38, 128, 64, 2, 2, 3, 64, 16, 0, 1)    /* 72 KiB: 2 blocks/CU */                                         \
   X(39, 256, 64, 4, 1, 3, 64, 16, 0, 1)    /* 120 KiB: 1 block/CU */                                         \
-  /* 192-channel tiles (r5): a Cout 192 layer (InceptionV3 conv2d_5 80 -> 192 at 73x73, the 17x17 */ \
-  /* branches) in ONE channel tile, so each activation K tile is DMA'd once instead of 3 x */       \
-  X(40, 96, 192, 2, 3, 3, 64, 16, 0, 1)    /* 6 waves, 48px x 64ch per wave, 108 KiB */                     \
-  X(41, 96, 192, 2, 3, 2, 64, 16, 0, 1)    /* 6 waves, 2-stage, 72 KiB: 2 blocks/CU */                      \
-  X(42, 192, 192, 2, 3, 2, 64, 16, 0, 1)   /* 6 waves, 96px x 64ch per wave, 96 KiB */                      \
-  X(43, 96, 192, 2, 3, 3, 32, 16, 0, 1)    /* BK32 3-stage, 54 KiB: 3 blocks/CU */                          \
   /* v_mfma_f32_32x32x16_bf16 twins (MF 32: 32x32 fragments, f32x16 accumulators) of the two */   \
   /* most-picked tiles; kept as A/B probes, not tuner candidates: over all 64 ResNet50 / */        \
   /* InceptionV3 shapes x 8 tile pairs the MF 32 form ran a median 4-6 % slower (best on 2 */      \

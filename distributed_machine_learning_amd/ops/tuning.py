@@ -22,7 +22,7 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 from .. import _native as N
 
 V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33, 34, 36, 37,
-           38, 39, 40, 41, 42, 43)  # 23..37: BK32; 38 / 39: 3-stage BK64 64-channel tiles (r3); 40..43: 192-ch (r5)
+           38, 39)  # 23..37: BK32; 38 / 39: 3-stage BK64 64-channel tiles (r3)
 # warp-specialised tiles (csrc/kernels/conv_igemm_ws.hip: loader waves + MFMA waves, r5)
 WS_CFGS = tuple(range(100, 120))
 # their persistent form (csrc/kernels/conv_igemm_wsp.hip: one operand ring over a workgroup's
@@ -79,7 +79,7 @@ def save_cache(table: Dict[str, int], path: str = CACHE_PATH) -> None:
         os.replace(tmp, path)
 
 
-NO_RES_CFGS = (34, 42)  # the residual-epilogue instantiations spill (256x256, 192x192 tiles)
+NO_RES_CFGS = (34,)  # the residual-epilogue instantiation spills (256x256 tile)
 # late-residual twins (residual loaded in the epilogue; identical to their base
 # tile on residual-free convs, so timed on residual layers only)
 LATE_RES_CFGS = (56, 57, 58, 59, 60)

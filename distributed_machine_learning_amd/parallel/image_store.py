@@ -114,6 +114,10 @@ class HbmImageStore:
         self.window_of: Dict[str, Window] = {}                 # name -> the latest window that moves it
         self.here: Dict[str, Window] = {}                      # name -> the window that delivers it HERE
         self.refs: Dict[str, int] = {}
+        # resident images no batch pins (refs 0), least recently released first: the eviction
+        # candidates, kept incrementally (plan() used to scan the whole index per batch with a
+        # list membership test per entry: 258 ms steps at 51,200 distinct images)
+        self.idle: "OrderedDict[str, None]" = OrderedDict()
         self.free: List[int] = list(range(self.capacity - 1, self.n_synth - 1, -1))
         self._wid = 0
 
@@ -134,14 +138,16 @@ class HbmImageStore:
         fit next to the pinned images (the caller stages fewer batches and retries later).
         Returns the window (possibly with no names)."""
         want = [n for n in dict.fromkeys(names) if not self._synthetic(n)]
+        wset = set(want)
         new = [n for n in want if n not in self.index]
         move = [n for n in want if n in self.index and dst not in self.holders[n]]
-        if len(new) > len(self.free) + sum(1 for k in self.index if self.refs.get(k, 0) == 0 and k not in want):
+        if len(new) > len(self.free) + len(self.idle) - sum(1 for n in want if n in self.idle):
             return None
         slots, src = [], []
         for n in new:
-            if not self.free:  # evict the oldest unpinned image
-                victim = next(k for k in self.index if self.refs.get(k, 0) == 0 and k not in want)
+            if not self.free:  # evict the least recently released unpinned image
+                victim = next(k for k in self.idle if k not in wset)
+                del self.idle[victim]
                 self.free.append(self.index.pop(victim))
                 self.holders.pop(victim, None)
                 self.window_of.pop(victim, None)
@@ -151,6 +157,7 @@ class HbmImageStore:
             slots.append(s)
             src.append(dst)
             self.index[n] = s
+            self.idle[n] = None   # unpinned until its batch pins it
             self.holders[n] = {dst}
         for n in move:
             slots.append(self.index[n])
@@ -172,7 +179,10 @@ class HbmImageStore:
     def pin(self, names: Sequence[str]) -> None:
         for n in names:
             if not self._synthetic(n):
-                self.refs[n] = self.refs.get(n, 0) + 1
+                r = self.refs.get(n, 0)
+                if r == 0:
+                    self.idle.pop(n, None)
+                self.refs[n] = r + 1
 
     def unpin(self, names: Sequence[str]) -> None:
         """A batch completed (same step on every rank). Its images stay resident
@@ -186,6 +196,8 @@ class HbmImageStore:
                 self.refs[n] = r
                 continue
             self.refs.pop(n, None)
+            if n in self.index:
+                self.idle[n] = None
             w = self.window_of.get(n)
             if w is None:
                 continue
@@ -194,6 +206,7 @@ class HbmImageStore:
                 # so every rank has issued w's collectives and finishing it here is bounded
                 self.stager.flush_until(w)
             if n in w.failed and n in self.index:
+                self.idle.pop(n, None)
                 self.free.append(self.index.pop(n))
                 self.holders.pop(n, None)
                 self.window_of.pop(n, None)

@@ -375,3 +375,39 @@ def test_hbm_image_store_window_pinning_and_eviction():
     assert staged(d) is not None                                     # fetched again, now fine
     slots, failed = st.slots(d)
     assert failed == [] and st.arena[slots].numpy()[:, 0, 0, 0].tolist() == [5, 3]
+
+
+def test_hbm_image_store_plan_cost_is_independent_of_resident_images():
+    """plan() at 51,200 resident images costs what it costs at 512 (the eviction candidates
+    are kept incrementally; a whole-index scan per batch made 258 ms serve-loop steps on the
+    51,200-distinct bench run), and evicts the least recently released image first."""
+    import time
+
+    from distributed_machine_learning_amd.parallel.image_store import HbmImageStore
+
+    def fill(n):   # windows marked delivered by hand: only the bookkeeping is under test
+        a = HbmImageStore(n + 512, (1, 1), "cpu")
+        for i in range(0, n, 256):
+            names = [f"{j}.jpeg" for j in range(i, i + 256)]
+            w = a.plan(names, 0)
+            w.done = True
+            a.pin(names)
+            a.unpin(names)
+        a.stager.queue.clear()
+        return a
+
+    def cost(a, base):
+        t = time.perf_counter()
+        for k in range(8):
+            names = [f"n{base + k * 256 + j}.jpeg" for j in range(256)]
+            w = a.plan(names, 0)
+            w.done = True
+            a.pin(names)
+            a.unpin(names)
+        return time.perf_counter() - t
+
+    small, big = fill(512), fill(51200)
+    assert big.free == [] or len(big.free) < 1024
+    c_small, c_big = cost(small, 0), cost(big, 0)
+    assert c_big < 10 * c_small + 0.05, (c_small, c_big)
+    assert big.evictions >= 1536 and "0.jpeg" not in big.index   # the oldest released went first
