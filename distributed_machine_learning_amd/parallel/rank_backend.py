@@ -461,7 +461,7 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         import threading
 
         self._dcache: "OrderedDict[str, np.ndarray]" = OrderedDict()   # name -> full-res RGB (both models)
-        self._nprocs, self._dprocs = int(os.environ.get("DML_DECODE_PROCS", "8")), None
+        self._nprocs, self._dprocs = int(os.environ.get("DML_DECODE_PROCS", "12")), None
         self._dbytes, self.decode_hits, self._dlock = 0, 0, threading.Lock()
         self._nn: Dict[Tuple[int, int], np.ndarray] = {}    # (n_in, n_out) -> nearest-index table
         self._pins: List[torch.Tensor] = []                  # free pinned pack buffers
@@ -499,6 +499,8 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             else:
                 self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=SLOTS, **src)
             self.engines[m].capture(self.stream)  # graphs now, before the service's first collective
+        if self.loader is not None:
+            self._procs()   # the decode workers start (and import Pillow) now, not inside a timed pass
 
     DECODE_CACHE_BYTES = 1 << 30
     DECODE_CHUNK = 8
@@ -555,8 +557,9 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         return np.asarray(im, dtype=np.uint8)
 
     def _procs(self):
-        """The decode worker processes (parallel/decode_worker.py), started on first use:
-        DML_DECODE_PROCS (default 8; 0 = decode in this process's threads)."""
+        """The decode worker processes (parallel/decode_worker.py), started with a store loader
+        (before any timed work) or on first use: DML_DECODE_PROCS (default 12; 0 = decode in
+        this process's threads)."""
         if self._dprocs is None and self._nprocs > 0:
             with self._dlock:
                 if self._dprocs is None:
