@@ -213,6 +213,16 @@ int dml_conv_rr(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_rr_fits(const DmlConvArgs* a);
 int dml_conv_rr_init(void);
 int dml_conv_rr_stamped(const DmlConvArgs* a, int cfg, void* stamps, hipStream_t s);  // phase probe
+// baseline JPEG decode on the GPU fused with the Pillow-exact nearest resize into arena slots
+// (jpeg_decode.hip): host parse + un-stuffing into one buffer, then three kernels
+long dml_jpeg_prepare(int n, const unsigned char* const* datas, const long* lens, int outH, int outW, void* buf,
+                      long cap, int* status, long* info);
+void dml_jpeg_set_slot(void* buf, int i, int slot);
+int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long maxstream, void* dwork, int H, int W,
+                           void* arena, hipStream_t s);
+int dml_jpeg_init(void);
+long dml_jpeg_desc_size(void);
+int dml_jpeg_decode_host(const unsigned char* data, long len, unsigned char* out, int* hw);
 int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);
 int dml_pool(const DmlPoolArgs* a, hipStream_t s);
 int dml_global_avgpool(const void* x, void* y, int N, int HW, int C, int ldx, hipStream_t s);

@@ -1,0 +1,694 @@
+// jpeg_decode.hip — baseline JPEG decode on the GPU, fused with the Pillow-exact nearest resize
+// into the HBM image arena (the store-image path of parallel/rank_backend.py; gfx950).
+//
+// Why: the store-image pass is bound by the first decode of each distinct image — ~1.1 ms of
+// Pillow / libjpeg-turbo per 300x250 JPEG, ~6.7k images/s from 12 decode worker processes on a
+// 16-CPU share (DESIGN §1 "Store images") against ~75k images/s of model throughput.
+//
+// What: the host parses the headers and un-stuffs each entropy-coded segment (C++ below,
+// dml_jpeg_prepare) into one pinned buffer: per image a fixed-size descriptor (geometry,
+// natural-order quantisation tables, Huffman lookup tables, the output slot's nearest-index
+// tables) and its entropy bytes. On the device:
+//   1. jpeg_huff_kernel: one wave per image copies its entropy bytes into LDS; lane 0 decodes
+//      the MCUs serially (Huffman + DC prediction) into int16 coefficient blocks.
+//   2. jpeg_idct_kernel: one thread per 8x8 block — libjpeg's "islow" integer IDCT
+//      (jidctint.c arithmetic: CONST_BITS 13, PASS1_BITS 2, 64-bit products, its post-IDCT
+//      range-limit table) into per-component sample planes.
+//   3. jpeg_rgb_resize_kernel: per output pixel of the model's size, the source pixel of
+//      Pillow's NEAREST tables; its chroma by libjpeg's h2v2 "fancy" triangle upsampling
+//      (jdsample.c, with its edge and context-row rules) and the jdcolor.c YCbCr->RGB tables
+//      (16-bit fixed point) — written straight into the arena slot. No full-resolution RGB
+//      image is ever materialised.
+// The same __host__ __device__ code decodes on the CPU (dml_jpeg_decode_host), which the CPU
+// tests compare byte for byte with Pillow's decode (tests/test_jpeg_gpu.py).
+//
+// Supported: baseline / extended-sequential Huffman (SOF0 / SOF1), 8-bit, one interleaved
+// scan, grayscale or YCbCr 4:2:0 / 4:4:4, no restart markers. Anything else (progressive,
+// 4:2:2, restart intervals, Adobe RGB / CMYK, arithmetic coding, > 60 KiB of entropy data) is
+// reported unsupported and takes the CPU decode workers.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "common.h"
+#include "dml.h"
+
+#define DMLJ_MAXOUT 320
+#define DMLJ_MAXSTREAM (60 * 1024)
+
+struct DmljHuff {
+  uint16_t look[512];   // 9-bit lookahead: (len << 8) | symbol; 0 = a longer code
+  int32_t maxcode[18];  // largest code of each length (-1: none); [17] = sentinel
+  int32_t valoff[18];   // val index of a code of length l = valoff[l] + code
+  uint8_t val[256];
+};
+
+struct DmljImage {
+  int32_t ok, w, h, ncomp;
+  int32_t hmax, vmax, mcux, mcuy;
+  int32_t hs[3], vs[3], tq[3], td[3], ta[3];
+  int32_t bw[3], bh[3];         // blocks per row / column of the padded MCU grid
+  int32_t dw[3], dh[3];         // libjpeg's downsampled_width / downsampled_height
+  int32_t nblk, slot;           // blocks over all components; arena slot (set at launch)
+  int64_t coef_off[3];          // int16 index of the component's first coefficient (work buffer)
+  int64_t plane_off[3];         // byte offset of the component's sample plane (work buffer)
+  int64_t stream_off;           // byte offset of the entropy bytes (this buffer)
+  int32_t stream_len, outH, outW, pad;
+  int16_t rowtab[DMLJ_MAXOUT], coltab[DMLJ_MAXOUT];
+  uint16_t q[4][64];            // natural order
+  uint8_t nat[80];              // zigzag -> natural order (+ libjpeg's pad)
+  DmljHuff dc[4], ac[4];
+};
+
+namespace dml {
+namespace jpg {
+
+// zigzag index -> natural (row-major) index, + 16 entries of 63 (libjpeg's safety pad); the
+// device reads the copy each descriptor carries
+static const uint8_t kNatural[80] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13,
+    6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31,
+    39, 46, 53, 60, 61, 54, 47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+// ------------------------------------------------------------------ entropy decoding --
+struct Bits {
+  const uint8_t* p;
+  int len, pos, nb;
+  uint64_t buf;
+  __host__ __device__ void fill() {
+    while (nb <= 56) {
+      const uint64_t b = pos < len ? p[pos] : 0;  // past the end: zeros, as libjpeg
+      ++pos;
+      buf |= b << (56 - nb);
+      nb += 8;
+    }
+  }
+  __host__ __device__ uint32_t peek(int n) const { return (uint32_t)(buf >> (64 - n)); }
+  __host__ __device__ void skip(int n) {
+    buf <<= n;
+    nb -= n;
+  }
+  __host__ __device__ int get(int n) {  // n <= 16, after fill()
+    if (n == 0) return 0;
+    const int v = (int)peek(n);
+    skip(n);
+    return v;
+  }
+};
+
+__host__ __device__ static inline int huff_decode(Bits& b, const DmljHuff& t) {
+  b.fill();
+  const uint16_t e = t.look[b.peek(9)];
+  if (e) {
+    b.skip(e >> 8);
+    return e & 255;
+  }
+  int l = 10;
+  int code = (int)b.peek(l);
+  while (l <= 16 && code > t.maxcode[l]) {
+    ++l;
+    code = (int)b.peek(l);
+  }
+  if (l > 16) {  // corrupt data: libjpeg warns and returns 0
+    b.skip(16);
+    return 0;
+  }
+  b.skip(l);
+  return t.val[(t.valoff[l] + code) & 255];
+}
+
+__host__ __device__ static inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
+
+// all MCUs of one image -> int16 coefficient blocks (zero-filled by the caller)
+__host__ __device__ static void decode_entropy(const DmljImage& d, const uint8_t* stream, int16_t* coef) {
+  const uint8_t* nat = d.nat;
+  Bits b{stream, d.stream_len, 0, 0, 0};
+  int pred[3] = {0, 0, 0};
+  const int nc = d.ncomp;
+  for (int my = 0; my < d.mcuy; ++my)
+    for (int mx = 0; mx < d.mcux; ++mx)
+      for (int c = 0; c < nc; ++c) {
+        const int hs = nc == 1 ? 1 : d.hs[c], vs = nc == 1 ? 1 : d.vs[c];
+        const DmljHuff& dct = d.dc[d.td[c]];
+        const DmljHuff& act = d.ac[d.ta[c]];
+        for (int v = 0; v < vs; ++v)
+          for (int h = 0; h < hs; ++h) {
+            const int bx = mx * hs + h, by = my * vs + v;
+            int16_t* blk = coef + d.coef_off[c] + ((int64_t)by * d.bw[c] + bx) * 64;
+            const int s = huff_decode(b, dct);
+            b.fill();
+            const int diff = s ? extend(b.get(s), s) : 0;
+            pred[c] += diff;
+            blk[0] = (int16_t)pred[c];
+            for (int k = 1; k < 64; ++k) {
+              const int rs = huff_decode(b, act);
+              const int r = rs >> 4, sz = rs & 15;
+              if (sz) {
+                k += r;
+                b.fill();
+                const int v2 = extend(b.get(sz), sz);
+                blk[nat[k]] = (int16_t)v2;
+              } else {
+                if (r != 15) break;
+                k += 15;
+              }
+            }
+          }
+      }
+}
+
+// ----------------------------------------------------------------------------- IDCT --
+// libjpeg jidctint.c (jpeg_idct_islow), 64-bit products as its JLONG
+#define DJ_CONST_BITS 13
+#define DJ_PASS1_BITS 2
+#define DJ_DESCALE(x, n) (((x) + ((int64_t)1 << ((n)-1))) >> (n))
+
+__host__ __device__ static inline uint8_t idct_range(int64_t x) {
+  // the post-IDCT range_limit table, indexed by x & RANGE_MASK (1023)
+  const int i = (int)(x & 1023);
+  return (uint8_t)(i < 128 ? 128 + i : (i < 512 ? 255 : (i < 896 ? 0 : i - 896)));
+}
+
+__host__ __device__ static void idct_islow(const int16_t* in, const uint16_t* q, uint8_t* out, int stride) {
+  int ws[64];
+  for (int c = 0; c < 8; ++c) {
+    const int16_t* ip = in + c;
+    const uint16_t* qp = q + c;
+    int* wp = ws + c;
+    if (ip[8] == 0 && ip[16] == 0 && ip[24] == 0 && ip[32] == 0 && ip[40] == 0 && ip[48] == 0 && ip[56] == 0) {
+      const int dc = (int)((int64_t)ip[0] * qp[0]) << DJ_PASS1_BITS;
+      for (int r = 0; r < 8; ++r) wp[r * 8] = dc;
+      continue;
+    }
+    int64_t z2 = (int64_t)ip[16] * qp[16], z3 = (int64_t)ip[48] * qp[48];
+    int64_t z1 = (z2 + z3) * 4433;
+    int64_t tmp2 = z1 + z3 * (-15137);
+    int64_t tmp3 = z1 + z2 * 6270;
+    z2 = (int64_t)ip[0] * qp[0];
+    z3 = (int64_t)ip[32] * qp[32];
+    int64_t tmp0 = (z2 + z3) << DJ_CONST_BITS;
+    int64_t tmp1 = (z2 - z3) << DJ_CONST_BITS;
+    const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+    tmp0 = (int64_t)ip[56] * qp[56];
+    tmp1 = (int64_t)ip[40] * qp[40];
+    tmp2 = (int64_t)ip[24] * qp[24];
+    tmp3 = (int64_t)ip[8] * qp[8];
+    z1 = tmp0 + tmp3;
+    z2 = tmp1 + tmp2;
+    z3 = tmp0 + tmp2;
+    int64_t z4 = tmp1 + tmp3;
+    const int64_t z5 = (z3 + z4) * 9633;
+    tmp0 *= 2446;
+    tmp1 *= 16819;
+    tmp2 *= 25172;
+    tmp3 *= 12299;
+    z1 *= -7373;
+    z2 *= -20995;
+    z3 *= -16069;
+    z4 *= -3196;
+    z3 += z5;
+    z4 += z5;
+    tmp0 += z1 + z3;
+    tmp1 += z2 + z4;
+    tmp2 += z2 + z3;
+    tmp3 += z1 + z4;
+    const int sh = DJ_CONST_BITS - DJ_PASS1_BITS;
+    wp[0] = (int)DJ_DESCALE(tmp10 + tmp3, sh);
+    wp[56] = (int)DJ_DESCALE(tmp10 - tmp3, sh);
+    wp[8] = (int)DJ_DESCALE(tmp11 + tmp2, sh);
+    wp[48] = (int)DJ_DESCALE(tmp11 - tmp2, sh);
+    wp[16] = (int)DJ_DESCALE(tmp12 + tmp1, sh);
+    wp[40] = (int)DJ_DESCALE(tmp12 - tmp1, sh);
+    wp[24] = (int)DJ_DESCALE(tmp13 + tmp0, sh);
+    wp[32] = (int)DJ_DESCALE(tmp13 - tmp0, sh);
+  }
+  for (int r = 0; r < 8; ++r) {
+    const int* wp = ws + r * 8;
+    uint8_t* op = out + r * stride;
+    int64_t z2 = wp[2], z3 = wp[6];
+    int64_t z1 = (z2 + z3) * 4433;
+    int64_t tmp2 = z1 + z3 * (-15137);
+    int64_t tmp3 = z1 + z2 * 6270;
+    int64_t tmp0 = ((int64_t)wp[0] + wp[4]) << DJ_CONST_BITS;
+    int64_t tmp1 = ((int64_t)wp[0] - wp[4]) << DJ_CONST_BITS;
+    const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+    tmp0 = wp[7];
+    tmp1 = wp[5];
+    tmp2 = wp[3];
+    tmp3 = wp[1];
+    z1 = tmp0 + tmp3;
+    z2 = tmp1 + tmp2;
+    z3 = tmp0 + tmp2;
+    int64_t z4 = tmp1 + tmp3;
+    const int64_t z5 = (z3 + z4) * 9633;
+    tmp0 *= 2446;
+    tmp1 *= 16819;
+    tmp2 *= 25172;
+    tmp3 *= 12299;
+    z1 *= -7373;
+    z2 *= -20995;
+    z3 *= -16069;
+    z4 *= -3196;
+    z3 += z5;
+    z4 += z5;
+    tmp0 += z1 + z3;
+    tmp1 += z2 + z4;
+    tmp2 += z2 + z3;
+    tmp3 += z1 + z4;
+    const int sh = DJ_CONST_BITS + DJ_PASS1_BITS + 3;
+    op[0] = idct_range(DJ_DESCALE(tmp10 + tmp3, sh));
+    op[7] = idct_range(DJ_DESCALE(tmp10 - tmp3, sh));
+    op[1] = idct_range(DJ_DESCALE(tmp11 + tmp2, sh));
+    op[6] = idct_range(DJ_DESCALE(tmp11 - tmp2, sh));
+    op[2] = idct_range(DJ_DESCALE(tmp12 + tmp1, sh));
+    op[5] = idct_range(DJ_DESCALE(tmp12 - tmp1, sh));
+    op[3] = idct_range(DJ_DESCALE(tmp13 + tmp0, sh));
+    op[4] = idct_range(DJ_DESCALE(tmp13 - tmp0, sh));
+  }
+}
+
+// ------------------------------------------------------- upsampling + colour conversion --
+__host__ __device__ static inline uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+// chroma sample c at full-resolution (sy, sx): libjpeg h2v2_fancy_upsample (4:2:0) or the
+// sample itself (4:4:4)
+__host__ __device__ static inline int chroma_at(const DmljImage& d, const uint8_t* work, int c, int sy, int sx) {
+  const uint8_t* pl = work + d.plane_off[c];
+  const int pw = d.bw[c] * 8;
+  if (d.hs[c] == d.hmax) return pl[(int64_t)sy * pw + sx];
+  const int r = sy >> 1, k = sx >> 1, dh = d.dh[c], dw = d.dw[c];
+  // libjpeg-turbo (jdsample.c jinit_upsampler) uses the fancy filter only when the downsampled
+  // width exceeds 2; narrower components are box-replicated
+  if (dw <= 2) return pl[(int64_t)r * pw + k];
+  // nearest row r; next nearest: above for the upper output row, below for the lower; the
+  // row above the first and below the last real row are those rows themselves
+  const int r1 = (sy & 1) ? (r + 1 < dh ? r + 1 : dh - 1) : (r > 0 ? r - 1 : 0);
+  const uint8_t* in0 = pl + (int64_t)r * pw;
+  const uint8_t* in1 = pl + (int64_t)r1 * pw;
+  const int s = in0[k] * 3 + in1[k];
+  if (!(sx & 1)) {
+    if (k == 0) return (s * 4 + 8) >> 4;
+    const int sl = in0[k - 1] * 3 + in1[k - 1];
+    return (s * 3 + sl + 8) >> 4;
+  }
+  if (k == dw - 1) return (s * 4 + 7) >> 4;
+  const int sr = in0[k + 1] * 3 + in1[k + 1];
+  return (s * 3 + sr + 7) >> 4;
+}
+
+__host__ __device__ static inline void rgb_at(const DmljImage& d, const uint8_t* work, int sy, int sx, uint8_t* o) {
+  const int y = work[d.plane_off[0] + (int64_t)sy * d.bw[0] * 8 + sx];
+  if (d.ncomp == 1) {
+    o[0] = o[1] = o[2] = (uint8_t)y;
+    return;
+  }
+  const int x1 = chroma_at(d, work, 1, sy, sx) - 128, x2 = chroma_at(d, work, 2, sy, sx) - 128;
+  // jdcolor.c build_ycc_rgb_table, SCALEBITS 16: FIX(1.40200) 91881, FIX(1.77200) 116130,
+  // FIX(0.71414) 46802, FIX(0.34414) 22554, ONE_HALF 32768
+  const int64_t crr = (91881 * (int64_t)x2 + 32768) >> 16;
+  const int64_t cbb = (116130 * (int64_t)x1 + 32768) >> 16;
+  const int64_t g = (-22554 * (int64_t)x1 + 32768 + (-46802) * (int64_t)x2) >> 16;
+  o[0] = clamp255(y + (int)crr);
+  o[1] = clamp255(y + (int)g);
+  o[2] = clamp255(y + (int)cbb);
+}
+
+// ----------------------------------------------------------------------------- kernels --
+__global__ __launch_bounds__(64) void jpeg_huff_kernel(const unsigned char* __restrict__ buf, int n,
+                                                       int16_t* __restrict__ coef) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  const DmljImage& d = ((const DmljImage*)(buf + 16))[i];
+  if (!d.ok) return;
+  const unsigned char* src = buf + d.stream_off;
+  const int n16 = (d.stream_len + 15) / 16;
+  for (int j = threadIdx.x; j < n16; j += 64) *(uint4*)(lds + j * 16) = *(const uint4*)(src + j * 16);
+  __syncthreads();
+  if (threadIdx.x == 0) decode_entropy(d, lds, coef);
+}
+
+__global__ __launch_bounds__(256) void jpeg_idct_kernel(const unsigned char* __restrict__ buf, int n,
+                                                        const int16_t* __restrict__ coef, uint8_t* __restrict__ work) {
+  const int i = blockIdx.y;
+  const DmljImage& d = ((const DmljImage*)(buf + 16))[i];
+  int blk = blockIdx.x * 256 + threadIdx.x;
+  if (!d.ok || blk >= d.nblk) return;
+  int c = 0;
+  while (c + 1 < d.ncomp && blk >= d.bw[c] * d.bh[c]) {
+    blk -= d.bw[c] * d.bh[c];
+    ++c;
+  }
+  const int by = blk / d.bw[c], bx = blk - by * d.bw[c];
+  const int pw = d.bw[c] * 8;
+  idct_islow(coef + d.coef_off[c] + (int64_t)blk * 64, d.q[d.tq[c]],
+             work + d.plane_off[c] + (int64_t)by * 8 * pw + bx * 8, pw);
+}
+
+__global__ __launch_bounds__(256) void jpeg_rgb_resize_kernel(const unsigned char* __restrict__ buf, int n,
+                                                              const uint8_t* __restrict__ work, int H, int W,
+                                                              uint8_t* __restrict__ arena) {
+  const int y = blockIdx.x, i = blockIdx.y;
+  const DmljImage& d = ((const DmljImage*)(buf + 16))[i];
+  if (!d.ok || y >= H) return;
+  const int sy = d.rowtab[y];
+  uint8_t* row = arena + ((int64_t)d.slot * H + y) * W * 3;
+  for (int x = threadIdx.x; x < W; x += 256) {
+    uint8_t o[3];
+    rgb_at(d, work, sy, d.coltab[x], o);
+    row[x * 3] = o[0];
+    row[x * 3 + 1] = o[1];
+    row[x * 3 + 2] = o[2];
+  }
+}
+
+// ------------------------------------------------------------------------ host parser --
+static int build_huff(const uint8_t* counts, const uint8_t* vals, int nvals, DmljHuff& t) {
+  memset(&t, 0, sizeof t);
+  int k = 0, code = 0;
+  for (int l = 1; l <= 16; ++l) {
+    const int cnt = counts[l - 1];
+    if (cnt) {
+      t.valoff[l] = k - code;
+      for (int j = 0; j < cnt; ++j, ++k, ++code) {
+        if (k >= nvals || k >= 256) return -1;
+        if (l <= 9) {
+          const int base = code << (9 - l);
+          for (int e = 0; e < (1 << (9 - l)); ++e) t.look[base + e] = (uint16_t)((l << 8) | vals[k]);
+        }
+      }
+      t.maxcode[l] = code - 1;
+    } else {
+      t.maxcode[l] = -1;
+    }
+    code <<= 1;
+  }
+  t.maxcode[17] = 0x7fffffff;
+  memcpy(t.val, vals, nvals < 256 ? nvals : 256);
+  return 0;
+}
+
+static void nearest_tab(int n_in, int n_out, int16_t* tab) {
+  // Pillow NEAREST: a float64 accumulator started at half a step, sequential adds, truncation
+  // (rank_backend.nearest_index)
+  const double a = (double)n_in / (double)n_out;
+  volatile double acc = a * 0.5;
+  for (int i = 0; i < n_out; ++i) {
+    if (i) acc = acc + a;
+    tab[i] = (int16_t)(int)acc;
+  }
+}
+
+// parse one JPEG into d (+ un-stuffed entropy bytes at out); 0 = supported
+static int parse_one(const uint8_t* p, int64_t len, DmljImage& d, uint8_t* out, int64_t cap, int outH, int outW) {
+  memset(&d, 0, sizeof d);
+  if (len < 4 || p[0] != 0xFF || p[1] != 0xD8) return -1;
+  int64_t i = 2;
+  bool have_sof = false, jfif = false, adobe = false;
+  int adobe_transform = -1;
+  int cid[3] = {0, 0, 0};
+  bool qdef[4] = {false, false, false, false};
+  while (i < len) {
+    if (p[i] != 0xFF) return -1;
+    while (i < len && p[i] == 0xFF) ++i;
+    if (i >= len) return -1;
+    const int m = p[i++];
+    if (m == 0xD9) return -1;                    // EOI before the scan
+    if (m >= 0xD0 && m <= 0xD7) continue;        // stray RST
+    if (i + 2 > len) return -1;
+    const int seglen = (p[i] << 8) | p[i + 1];
+    if (seglen < 2 || i + seglen > len) return -1;
+    const uint8_t* s = p + i + 2;
+    const int sl = seglen - 2;
+    if (m == 0xE0 && sl >= 5 && !memcmp(s, "JFIF", 5)) jfif = true;
+    if (m == 0xEE && sl >= 12 && !memcmp(s, "Adobe", 5)) {
+      adobe = true;
+      adobe_transform = s[11];
+    }
+    if (m == 0xDB) {                             // DQT
+      int o = 0;
+      while (o < sl) {
+        const int pq = s[o] >> 4, tqi = s[o] & 15;
+        if (pq != 0 || tqi > 3 || o + 65 > sl) return -1;  // 16-bit tables: CPU path
+        for (int k = 0; k < 64; ++k) d.q[tqi][kNatural[k]] = s[o + 1 + k];
+        qdef[tqi] = true;
+        o += 65;
+      }
+    } else if (m == 0xC4) {                      // DHT
+      int o = 0;
+      while (o < sl) {
+        if (o + 17 > sl) return -1;
+        const int tc = s[o] >> 4, th = s[o] & 15;
+        if (tc > 1 || th > 3) return -1;
+        int nv = 0;
+        for (int k = 0; k < 16; ++k) nv += s[o + 1 + k];
+        if (o + 17 + nv > sl || nv > 256) return -1;
+        if (build_huff(s + o + 1, s + o + 17, nv, tc ? d.ac[th] : d.dc[th]) != 0) return -1;
+        o += 17 + nv;
+      }
+    } else if (m == 0xC0 || m == 0xC1) {         // baseline / extended sequential, Huffman
+      if (sl < 6 || s[0] != 8) return -1;
+      d.h = (s[1] << 8) | s[2];
+      d.w = (s[3] << 8) | s[4];
+      d.ncomp = s[5];
+      if (d.h <= 0 || d.w <= 0 || (d.ncomp != 1 && d.ncomp != 3) || sl < 6 + 3 * d.ncomp) return -1;
+      for (int c = 0; c < d.ncomp; ++c) {
+        cid[c] = s[6 + 3 * c];
+        d.hs[c] = s[7 + 3 * c] >> 4;
+        d.vs[c] = s[7 + 3 * c] & 15;
+        d.tq[c] = s[8 + 3 * c];
+        if (d.tq[c] > 3 || d.hs[c] < 1 || d.vs[c] < 1) return -1;
+      }
+      have_sof = true;
+    } else if ((m >= 0xC2 && m <= 0xCF) && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+      return -1;                                 // progressive / lossless / arithmetic: CPU path
+    } else if (m == 0xDD) {                      // DRI
+      if (sl < 2) return -1;
+      if (((s[0] << 8) | s[1]) != 0) return -1;  // restart markers: CPU path
+    } else if (m == 0xDA) {                      // SOS
+      if (!have_sof || sl < 1) return -1;
+      const int ns = s[0];
+      if (ns != d.ncomp || sl < 1 + 2 * ns + 3) return -1;
+      for (int j = 0; j < ns; ++j) {
+        const int id = s[1 + 2 * j];
+        int c = -1;
+        for (int k = 0; k < d.ncomp; ++k)
+          if (cid[k] == id) c = k;
+        if (c != j) return -1;
+        d.td[c] = s[2 + 2 * j] >> 4;
+        d.ta[c] = s[2 + 2 * j] & 15;
+        if (d.td[c] > 3 || d.ta[c] > 3) return -1;
+      }
+      const uint8_t* ss = s + 1 + 2 * ns;
+      if (ss[0] != 0 || ss[1] != 63 || ss[2] != 0) return -1;
+      // entropy-coded data: un-stuff FF00 until the next marker (data that just ends —
+      // a truncated file — is left to the CPU path, which reports it failed as Pillow does)
+      int64_t j = i + seglen, o = 0;
+      bool ended = false;
+      while (j < len) {
+        const uint8_t b = p[j];
+        if (b == 0xFF) {
+          if (j + 1 >= len) break;
+          const uint8_t nx = p[j + 1];
+          if (nx == 0x00) {
+            if (o >= cap) return -1;
+            out[o++] = 0xFF;
+            j += 2;
+            continue;
+          }
+          if (nx == 0xFF) {  // fill byte
+            ++j;
+            continue;
+          }
+          if (nx >= 0xD0 && nx <= 0xD7) return -1;  // RST without DRI
+          // any other marker ends the scan: a second SOS (multi-scan) is not supported
+          int64_t k = j + 1;
+          while (k < len && p[k] == 0xFF) ++k;
+          if (k < len && p[k] == 0xDA) return -1;
+          ended = true;
+          break;
+        }
+        if (o >= cap) return -1;
+        out[o++] = b;
+        ++j;
+      }
+      if (!ended) return -1;
+      d.stream_len = (int)o;
+      break;
+    }
+    i += seglen;
+  }
+  if (!have_sof || d.stream_len <= 0) return -1;
+  // colour space as libjpeg guesses it (jdapimin.c): 3 components are YCbCr unless an Adobe
+  // marker says transform 0 or, with neither JFIF nor Adobe, the ids spell R G B
+  if (d.ncomp == 3) {
+    if (adobe && adobe_transform == 0) return -1;
+    if (!jfif && !adobe && cid[0] == 'R' && cid[1] == 'G' && cid[2] == 'B') return -1;
+  }
+  (void)qdef;
+  for (int c = 0; c < d.ncomp; ++c)
+    if (!qdef[d.tq[c]]) return -1;
+  // geometry (jdinput.c)
+  if (d.ncomp == 1) {
+    d.hs[0] = d.vs[0] = 1;
+    d.hmax = d.vmax = 1;
+    d.mcux = (d.w + 7) / 8;
+    d.mcuy = (d.h + 7) / 8;
+    d.bw[0] = d.mcux;
+    d.bh[0] = d.mcuy;
+    d.dw[0] = d.w;
+    d.dh[0] = d.h;
+  } else {
+    const bool s420 = d.hs[0] == 2 && d.vs[0] == 2 && d.hs[1] == 1 && d.vs[1] == 1 && d.hs[2] == 1 && d.vs[2] == 1;
+    const bool s444 = d.hs[0] == 1 && d.vs[0] == 1 && d.hs[1] == 1 && d.vs[1] == 1 && d.hs[2] == 1 && d.vs[2] == 1;
+    if (!s420 && !s444) return -1;  // 4:2:2 / 4:4:0 / exotic: CPU path
+    d.hmax = d.hs[0];
+    d.vmax = d.vs[0];
+    d.mcux = (d.w + 8 * d.hmax - 1) / (8 * d.hmax);
+    d.mcuy = (d.h + 8 * d.vmax - 1) / (8 * d.vmax);
+    for (int c = 0; c < 3; ++c) {
+      d.bw[c] = d.mcux * d.hs[c];
+      d.bh[c] = d.mcuy * d.vs[c];
+      d.dw[c] = (d.w * d.hs[c] + d.hmax - 1) / d.hmax;
+      d.dh[c] = (d.h * d.vs[c] + d.vmax - 1) / d.vmax;
+    }
+  }
+  if (d.stream_len > DMLJ_MAXSTREAM) return -1;
+  if (outH > 0) {
+    if (outH > DMLJ_MAXOUT || outW > DMLJ_MAXOUT) return -1;
+    nearest_tab(d.h, outH, d.rowtab);
+    nearest_tab(d.w, outW, d.coltab);
+  }
+  d.outH = outH;
+  d.outW = outW;
+  memcpy(d.nat, kNatural, sizeof d.nat);
+  d.ok = 1;
+  return 0;
+}
+
+}  // namespace jpg
+}  // namespace dml
+
+using dml::jpg::parse_one;
+
+// Layout of `buf` (pinned host memory, copied to the device as is): int64 n, int64 work bytes,
+// n x DmljImage, then each image's entropy bytes (16-aligned). status[i] = 1: decoded on the
+// GPU; 0: unsupported / corrupt (the caller decodes it on the CPU). Returns the bytes used, or
+// -1 if `cap` is too small. info[0] = bytes of the device work buffer the decode needs
+// (coefficients, then sample planes), info[1] = bytes of its coefficient part (zeroed before the
+// launch), info[2] = the most 8x8 blocks of one image, info[3] = the longest entropy segment.
+extern "C" long dml_jpeg_prepare(int n, const unsigned char* const* datas, const long* lens, int outH, int outW,
+                                 void* buf, long cap, int* status, long* info) {
+  unsigned char* b = (unsigned char*)buf;
+  const long hdr = 16 + (long)n * (long)sizeof(DmljImage);
+  if (cap < hdr) return -1;
+  DmljImage* d = (DmljImage*)(b + 16);
+  long off = (hdr + 15) / 16 * 16;
+  int64_t ncoef = 0;
+  long maxblk = 0, maxstream = 0;
+  for (int i = 0; i < n; ++i) {
+    const long room = cap - off;
+    status[i] = 0;
+    if (room <= 0 || parse_one(datas[i], lens[i], d[i], b + off, room, outH, outW) != 0) {
+      memset(&d[i], 0, sizeof(DmljImage));
+      continue;
+    }
+    d[i].stream_off = off;
+    off += (d[i].stream_len + 15) / 16 * 16;
+    int nb = 0;
+    for (int c = 0; c < d[i].ncomp; ++c) {
+      d[i].coef_off[c] = ncoef;
+      ncoef += (int64_t)d[i].bw[c] * d[i].bh[c] * 64;
+      nb += d[i].bw[c] * d[i].bh[c];
+    }
+    d[i].nblk = nb;
+    maxblk = nb > maxblk ? nb : maxblk;
+    maxstream = d[i].stream_len > maxstream ? d[i].stream_len : maxstream;
+    status[i] = 1;
+  }
+  int64_t pl = (ncoef * 2 + 255) / 256 * 256;
+  info[1] = (long)pl;
+  info[2] = maxblk;
+  info[3] = maxstream;
+  for (int i = 0; i < n; ++i) {
+    if (!d[i].ok) continue;
+    for (int c = 0; c < d[i].ncomp; ++c) {
+      d[i].plane_off[c] = pl;
+      pl += ((int64_t)d[i].bw[c] * 8 * d[i].bh[c] * 8 + 255) / 256 * 256;
+    }
+  }
+  info[0] = (long)pl;
+  ((int64_t*)b)[0] = n;
+  ((int64_t*)b)[1] = pl;
+  return off;
+}
+
+// set the arena slot of image i (host side, before the H2D copy)
+extern "C" void dml_jpeg_set_slot(void* buf, int i, int slot) { ((DmljImage*)((unsigned char*)buf + 16))[i].slot = slot; }
+
+extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long maxstream, void* dwork, int H, int W,
+                                      void* arena, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (H <= 0 || W <= 0 || H > DMLJ_MAXOUT || W > DMLJ_MAXOUT || maxstream > DMLJ_MAXSTREAM) {
+    dml_set_error("dml_jpeg_decode_resize: bad output size or stream");
+    return -1;
+  }
+  const unsigned char* b = (const unsigned char*)dbuf;
+  int16_t* coef = (int16_t*)dwork;
+  const unsigned lds = (unsigned)((maxstream + 15) / 16 * 16);
+  hipLaunchKernelGGL(dml::jpg::jpeg_huff_kernel, dim3(n), dim3(64), lds, s, b, n, coef);
+  DML_CHECK_LAUNCH();
+  hipLaunchKernelGGL(dml::jpg::jpeg_idct_kernel, dim3((maxblk + 255) / 256, n), dim3(256), 0, s, b, n, coef,
+                     (uint8_t*)dwork);
+  DML_CHECK_LAUNCH();
+  hipLaunchKernelGGL(dml::jpg::jpeg_rgb_resize_kernel, dim3(H, n), dim3(256), 0, s, b, n, (const uint8_t*)dwork, H, W,
+                     (uint8_t*)arena);
+  DML_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dml_jpeg_init(void) {
+  const int rc = (int)hipFuncSetAttribute((const void*)dml::jpg::jpeg_huff_kernel,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, DMLJ_MAXSTREAM);
+  if (rc) dml_set_error("dml_jpeg_init: hipFuncSetAttribute failed");
+  return rc ? -1 : 0;
+}
+
+extern "C" long dml_jpeg_desc_size(void) { return (long)sizeof(DmljImage); }
+
+// CPU decode with the same code (tests): full-resolution RGB into out (h*w*3); 0 = ok,
+// -1 = unsupported (the CPU workers' path)
+extern "C" int dml_jpeg_decode_host(const unsigned char* data, long len, unsigned char* out, int* hw) {
+  DmljImage d;
+  static thread_local uint8_t* stream = nullptr;
+  if (!stream) stream = (uint8_t*)malloc(1 << 24);
+  if (parse_one(data, len, d, stream, 1 << 24, 0, 0) != 0) return -1;
+  hw[0] = d.h;
+  hw[1] = d.w;
+  int64_t ncoef = 0;
+  for (int c = 0; c < d.ncomp; ++c) {
+    d.coef_off[c] = ncoef;
+    ncoef += (int64_t)d.bw[c] * d.bh[c] * 64;
+  }
+  int64_t pl = ncoef * 2;
+  for (int c = 0; c < d.ncomp; ++c) {
+    d.plane_off[c] = pl;
+    pl += (int64_t)d.bw[c] * 8 * d.bh[c] * 8;
+  }
+  uint8_t* work = (uint8_t*)calloc((size_t)pl, 1);
+  if (!work) return -1;
+  int16_t* coef = (int16_t*)work;
+  dml::jpg::decode_entropy(d, stream, coef);
+  for (int c = 0; c < d.ncomp; ++c) {
+    const int pw = d.bw[c] * 8;
+    for (int by = 0; by < d.bh[c]; ++by)
+      for (int bx = 0; bx < d.bw[c]; ++bx)
+        dml::jpg::idct_islow(coef + d.coef_off[c] + ((int64_t)by * d.bw[c] + bx) * 64, d.q[d.tq[c]],
+                             work + d.plane_off[c] + (int64_t)by * 8 * pw + bx * 8, pw);
+  }
+  for (int y = 0; y < d.h; ++y)
+    for (int x = 0; x < d.w; ++x) dml::jpg::rgb_at(d, work, y, x, out + ((int64_t)y * d.w + x) * 3);
+  free(work);
+  return 0;
+}

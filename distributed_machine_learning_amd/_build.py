@@ -28,6 +28,7 @@ SOURCES = [
     CSRC / "kernels" / "conv_igemm_ws.hip",
     CSRC / "kernels" / "conv_igemm_wsp.hip", CSRC / "kernels" / "conv_igemm_pt.hip", CSRC / "kernels" / "conv_rowring.hip",
     CSRC / "kernels" / "misc.hip",
+    CSRC / "kernels" / "jpeg_decode.hip",
     CSRC / "kernels" / "stem_fused.hip",
     CSRC / "kernels" / "conv_pool.hip",
     CSRC / "kernels" / "expand_reduce_chain.hip",

@@ -123,6 +123,14 @@ _SIGS = {
     "dml_preprocess": (C.c_int, [C.POINTER(PreprocArgs), C.c_void_p]),
     "dml_index_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "dml_resize_nearest": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
+    "dml_jpeg_prepare": (C.c_long, [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_long,
+                                    C.c_void_p, C.c_void_p]),
+    "dml_jpeg_set_slot": (None, [C.c_void_p, C.c_int, C.c_int]),
+    "dml_jpeg_decode_resize": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_long, C.c_void_p, C.c_int, C.c_int,
+                                         C.c_void_p, C.c_void_p]),
+    "dml_jpeg_init": (C.c_int, []),
+    "dml_jpeg_desc_size": (C.c_long, []),
+    "dml_jpeg_decode_host": (C.c_int, [C.c_char_p, C.c_long, C.c_void_p, C.POINTER(C.c_int)]),
     "dml_plan_create": (C.c_void_p, []),
     "dml_plan_destroy": (None, [C.c_void_p]),
     "dml_plan_add_conv": (C.c_int, [C.c_void_p, C.POINTER(ConvArgs), C.c_int]),

@@ -421,6 +421,84 @@ class _Pack:
             self.buf = None
 
 
+class _JpegPack:
+    """The GPU-decodable JPEGs of one window (csrc/kernels/jpeg_decode.hip): built in the decode
+    pool — one native call parses every header and un-stuffs every entropy segment into a pinned
+    buffer of fixed-size descriptors (with the model size's Pillow-exact nearest tables) and
+    entropy bytes. ``launch`` (serve loop, staging stream) copies it to the device and runs the
+    Huffman, IDCT and colour + resize kernels straight into the arena slots — bit-exact with
+    Pillow's decode + NEAREST resize (tests/test_jpeg_decode.py). ``unsupported``: the names the
+    parser left to the CPU decode (progressive, 4:2:2, restart markers, ...)."""
+
+    def __init__(self, backend: "GpuRankBackend", names: List[str], datas: List[bytes], hw: Tuple[int, int]):
+        import ctypes as C
+
+        from .. import _native as N
+
+        self.be, self.hw = backend, hw
+        L = N.lib()
+        n = len(names)
+        cap = 16 + n * L.dml_jpeg_desc_size() + sum(len(d) + 32 for d in datas) + 256
+        self.buf = backend.pinned(cap)
+        keep = [bytes(d) for d in datas]
+        ptrs = (C.c_char_p * n)(*keep)
+        lens = (C.c_long * n)(*[len(d) for d in keep])
+        status = (C.c_int * n)()
+        info = (C.c_long * 4)()
+        used = L.dml_jpeg_prepare(n, ptrs, lens, hw[0], hw[1], C.c_void_p(self.buf.data_ptr()), cap, status, info)
+        if used < 0:
+            raise RuntimeError("dml_jpeg_prepare: buffer too small")
+        self.used, self.n = int(used), n
+        self.work_bytes, self.coef_bytes, self.maxblk, self.maxstream = (int(v) for v in info)
+        self.idx = [i for i in range(n) if status[i]]
+        self.names = [names[i] for i in self.idx]
+        self.unsupported = [names[i] for i in range(n) if not status[i]]
+        self.dev = self.work = None
+
+    def launch(self, slots: List[int], arena: torch.Tensor, stream) -> None:
+        import ctypes as C
+
+        from .. import _native as N
+
+        L = N.lib()
+        for i, sl in zip(self.idx, slots):
+            L.dml_jpeg_set_slot(C.c_void_p(self.buf.data_ptr()), i, int(sl))
+        H, W = self.hw
+        with torch.cuda.stream(stream):
+            self.dev = torch.empty(self.used, dtype=torch.uint8, device=arena.device)
+            self.dev.copy_(self.buf[:self.used], non_blocking=True)
+            self.work = torch.empty(max(self.work_bytes, 256), dtype=torch.uint8, device=arena.device)
+            self.work[:self.coef_bytes].zero_()
+            N.check(L.dml_jpeg_decode_resize(self.dev.data_ptr(), self.n, self.maxblk, self.maxstream,
+                                             self.work.data_ptr(), H, W, arena.data_ptr(), stream.cuda_stream),
+                    "dml_jpeg_decode_resize")
+
+    def release(self) -> None:
+        self.dev = self.work = None
+        if self.buf is not None:
+            self.be.unpin(self.buf)
+            self.buf = None
+
+
+class _Packs:
+    """Several packs of one window (the GPU-decoded JPEGs and the CPU-decoded rest) behind the
+    one-pack interface the image store uses."""
+
+    def __init__(self, packs: list):
+        self.packs = [p for p in packs if p is not None and p.names]
+        self.names = [n for p in self.packs for n in p.names]
+
+    def launch(self, slots: List[int], arena: torch.Tensor, stream) -> None:
+        o = 0
+        for p in self.packs:
+            p.launch(slots[o:o + len(p.names)], arena, stream)
+            o += len(p.names)
+
+    def release(self) -> None:
+        for p in self.packs:
+            p.release()
+
+
 class GpuRankBackend(_ArenaStaging, RankBackend):
     """Native engines for both models resident in this GPU's HBM, fed from per-model
     HBM image stores (parallel/image_store.py: store images staged in windows ahead of
@@ -467,6 +545,8 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         self._pins: List[torch.Tensor] = []                  # free pinned pack buffers
         # DML_GPU_RESIZE=0: the decode pool resizes on the CPU (Pillow) as before (A/B)
         self.gpu_resize = os.environ.get("DML_GPU_RESIZE", "1") != "0"
+        # DML_GPU_JPEG=0: every JPEG decodes on the CPU (the decode workers), as before (A/B)
+        self.gpu_jpeg = self.gpu_resize and os.environ.get("DML_GPU_JPEG", "1") != "0"
         # a window's images are decoded DECODE_CHUNK per task by this pool, each task handing its
         # chunk to a decode worker PROCESS (parallel/decode_worker.py; in-process threads held
         # the GIL for ~0.3 ms per image: ~3.5k img/s on the 51,200-distinct run with 32 threads)
@@ -499,6 +579,8 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             else:
                 self.engines[m] = Engine(g, w, batch=b, device=str(device), src_slots=SLOTS, **src)
             self.engines[m].capture(self.stream)  # graphs now, before the service's first collective
+        if self.gpu_jpeg:
+            N.check(N.lib().dml_jpeg_init(), "dml_jpeg_init")
         if self.loader is not None:
             self._procs()   # the decode workers start (and import Pillow) now, not inside a timed pass
 
@@ -568,15 +650,31 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         return self._dprocs
 
     def _load(self, model: str, names: List[str]) -> Dict[str, Optional[np.ndarray]]:
-        """(decode pool thread) fetch + decode this rank's share of a window. GPU resize (the
-        default): the full-resolution decodes go into one pinned pack that the staging
-        stream resizes into the arena slots (_Pack); else Pillow NEAREST here, as
-        load_img(target_size)."""
+        """(decode pool thread) fetch + decode this rank's share of a window. Baseline JPEGs
+        decode on the GPU (_JpegPack; DML_GPU_JPEG=0 turns it off); the rest decode on the CPU
+        (decode workers): with GPU resize (the default) their full-resolution decodes go into
+        one pinned pack that the staging stream resizes into the arena slots (_Pack); else
+        Pillow NEAREST here, as load_img(target_size)."""
         from PIL import Image
 
         blobs = self.loader(names) if self.loader else {}
         hw = self.arenas[model].hw
         out = _PackedImages() if self.gpu_resize else {}
+        jp = None
+        if self.gpu_jpeg:
+            # GPU decode (jpeg_decode.hip) for every baseline JPEG; the CPU decodes the rest
+            have = [n for n in names if blobs.get(n) is not None]
+            if have:
+                try:
+                    jp = _JpegPack(self, have, [blobs[n] for n in have], hw)
+                except Exception as e:   # never fatal: the CPU path takes the window
+                    log.warning("GPU JPEG prepare failed (%s); decoding on the CPU", e)
+                    jp = None
+            if jp is not None:
+                for n in jp.names:
+                    out[n] = True   # decoded on the device at launch (the window only needs "ok")
+                gone = set(jp.names)
+                names = [n for n in names if n not in gone]
 
         def decode(chunk):
             res, miss = [], []
@@ -619,8 +717,8 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             out.update(decode(names))
         if self.gpu_resize:
             ok = [n for n in names if out.get(n) is not None]
-            if ok:
-                out.pack = _Pack(self, ok, [out[n] for n in ok], hw)
+            cpu = _Pack(self, ok, [out[n] for n in ok], hw) if ok else None
+            out.pack = _Packs([jp, cpu]) if jp is not None else cpu
         return out
 
     def launch(self, model, names, slot):
