@@ -70,4 +70,44 @@ int dml_link_many(int n, const char* const* srcs, const char* const* dsts, int* 
   return ok;
 }
 
+// Read n whole files into one buffer: sizes first (pass buf = nullptr: lens[i] = size or
+// -errno), then the bytes (buf of at least sum(lens) bytes, offs[i] = where file i starts).
+// Returns the total size, or -errno of the first failure. The image store's local fast path:
+// a window's 256 JPEGs in two GIL releases instead of one event-loop coroutine per file.
+long dml_read_many(int n, const char* const* paths, char* buf, long cap, long* offs, long* lens) {
+  if (!buf) {
+    long total = 0;
+    for (int i = 0; i < n; ++i) {
+      struct stat st;
+      if (stat(paths[i], &st) != 0) return -errno;
+      lens[i] = (long)st.st_size;
+      total += lens[i];
+    }
+    return total;
+  }
+  long off = 0;
+  for (int i = 0; i < n; ++i) {
+    if (off + lens[i] > cap) return -ENOSPC;
+    const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return -errno;
+    long got = 0;
+    while (got < lens[i]) {
+      const ssize_t r = read(fd, buf + off + got, (size_t)(lens[i] - got));
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        const int e = errno;
+        close(fd);
+        return -e;
+      }
+      if (r == 0) break;   // shrank since the stat: a short file
+      got += r;
+    }
+    close(fd);
+    offs[i] = off;
+    lens[i] = got;
+    off += got;
+  }
+  return off;
+}
+
 }  // extern "C"

@@ -172,12 +172,14 @@ __host__ __device__ static inline uint8_t idct_range(int64_t x) {
 
 __host__ __device__ static void idct_islow(const int16_t* in, const uint16_t* q, uint8_t* out, int stride) {
   int ws[64];
+#pragma unroll
   for (int c = 0; c < 8; ++c) {
     const int16_t* ip = in + c;
     const uint16_t* qp = q + c;
     int* wp = ws + c;
     if (ip[8] == 0 && ip[16] == 0 && ip[24] == 0 && ip[32] == 0 && ip[40] == 0 && ip[48] == 0 && ip[56] == 0) {
       const int dc = (int)((int64_t)ip[0] * qp[0]) << DJ_PASS1_BITS;
+#pragma unroll
       for (int r = 0; r < 8; ++r) wp[r * 8] = dc;
       continue;
     }
@@ -223,6 +225,7 @@ __host__ __device__ static void idct_islow(const int16_t* in, const uint16_t* q,
     wp[24] = (int)DJ_DESCALE(tmp13 + tmp0, sh);
     wp[32] = (int)DJ_DESCALE(tmp13 - tmp0, sh);
   }
+#pragma unroll
   for (int r = 0; r < 8; ++r) {
     const int* wp = ws + r * 8;
     uint8_t* op = out + r * stride;

@@ -272,7 +272,27 @@ class RankControl:
         asyncio.run_coroutine_threadsafe(go(), self.loop)
 
     def store_loader(self, names: List[str]) -> Dict[str, Optional[bytes]]:
-        """Fetch store images; ``name@v`` is that version exactly (pinned at submit)."""
+        """Fetch store images; ``name@v`` is that version exactly (pinned at submit). The
+        versions this node holds are read in the calling thread by one native batch
+        (store/fastio.read_many); only the rest go through the control loop."""
+        from ..store import fastio
+
+        local = self.node.local
+        out: Dict[str, Optional[bytes]] = {}
+        here, miss = [], []
+        for nm in names:
+            base, ver = split_version(nm)
+            (here if local.has(base, ver) else miss).append((nm, base, ver))
+        if here:
+            try:
+                blobs = fastio.read_many([local.path(b, v) for _, b, v in here])
+                out.update((nm, blob) for (nm, _, _), blob in zip(here, blobs))
+            except OSError:   # a version removed under us: the control loop sorts it out
+                miss += here
+        if not miss:
+            return out
+        names = [nm for nm, _, _ in miss]
+
         async def fetch_all():
             sem = asyncio.Semaphore(16)
 
@@ -284,7 +304,8 @@ class RankControl:
                     got = await self.node.store.get(base, ver)
                     return nm, None if got is None else got[1]
             return dict(await asyncio.gather(*(one(nm) for nm in names)))
-        return self.call(fetch_all(), timeout=120)
+        out.update(self.call(fetch_all(), timeout=120))
+        return out
 
     def pin_versions(self, names: List[str]) -> List[str]:
         """(coordinator, control thread) name -> name@latest-version from the

@@ -27,6 +27,10 @@ def _lib():
                                           C.POINTER(C.c_long)]
             L.dml_link_many.restype = C.c_int
             L.dml_link_many.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_int)]
+            if hasattr(L, "dml_read_many"):
+                L.dml_read_many.restype = C.c_long
+                L.dml_read_many.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.c_void_p, C.c_long,
+                                            C.POINTER(C.c_long), C.POINTER(C.c_long)]
             _fns = L
     return _fns or None
 
@@ -77,3 +81,30 @@ def link_many(pairs: Sequence[Tuple[str, str]]) -> List[int]:
     st = (C.c_int * n)()
     L.dml_link_many(n, srcs, dsts, st)
     return list(st)
+
+
+def read_many(paths: Sequence[str]) -> List[memoryview]:
+    """The whole contents of each file (one buffer, a memoryview per file): two native calls
+    (sizes, then bytes), the GIL released in each. Raises OSError like open()."""
+    L = _lib()
+    if L is None or not hasattr(L, "dml_read_many"):
+        out = []
+        for p in paths:
+            with open(p, "rb") as f:
+                out.append(memoryview(f.read()))
+        return out
+    n = len(paths)
+    ps = (C.c_char_p * n)(*[p.encode() for p in paths])
+    offs = (C.c_long * n)()
+    lens = (C.c_long * n)()
+    total = L.dml_read_many(n, ps, None, 0, offs, lens)
+    if total < 0:
+        raise OSError(-total, os.strerror(-total))
+    buf = bytearray(max(total, 1))
+    cbuf = (C.c_char * len(buf)).from_buffer(buf)
+    got = L.dml_read_many(n, ps, C.addressof(cbuf), len(buf), offs, lens)
+    del cbuf
+    if got < 0:
+        raise OSError(-got, os.strerror(-got))
+    mv = memoryview(buf)
+    return [mv[offs[i]:offs[i] + lens[i]] for i in range(n)]
