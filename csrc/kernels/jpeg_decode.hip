@@ -27,6 +27,7 @@
 // 4:2:2, restart intervals, Adobe RGB / CMYK, arithmetic coding, > 60 KiB of entropy data) is
 // reported unsupported and takes the CPU decode workers.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -60,6 +61,8 @@ struct DmljImage {
   uint8_t nat[80];              // zigzag -> natural order (+ libjpeg's pad)
   DmljHuff dc[4], ac[4];
 };
+static_assert(sizeof(DmljImage) % 16 == 0 && offsetof(DmljImage, dc) % 16 == 0 && sizeof(DmljHuff) % 16 == 0,
+              "16-B copies of descriptors and Huffman tables");
 
 namespace dml {
 namespace jpg {
@@ -76,12 +79,15 @@ struct Bits {
   const uint8_t* p;
   int len, pos, nb;
   uint64_t buf;
+  // >= 33 bits after a fill: enough for one Huffman code or one coefficient's extra bits.
+  // 4 independent byte reads per refill (one LDS round trip on the device, not four)
   __host__ __device__ void fill() {
-    while (nb <= 56) {
-      const uint64_t b = pos < len ? p[pos] : 0;  // past the end: zeros, as libjpeg
-      ++pos;
-      buf |= b << (56 - nb);
-      nb += 8;
+    while (nb <= 32) {
+      const uint32_t b0 = pos < len ? p[pos] : 0, b1 = pos + 1 < len ? p[pos + 1] : 0;  // past the end:
+      const uint32_t b2 = pos + 2 < len ? p[pos + 2] : 0, b3 = pos + 3 < len ? p[pos + 3] : 0;  // zeros
+      buf |= (uint64_t)((b0 << 24) | (b1 << 16) | (b2 << 8) | b3) << (32 - nb);
+      pos += 4;
+      nb += 32;
     }
   }
   __host__ __device__ uint32_t peek(int n) const { return (uint32_t)(buf >> (64 - n)); }
@@ -120,8 +126,10 @@ __host__ __device__ static inline int huff_decode(Bits& b, const DmljHuff& t) {
 
 __host__ __device__ static inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
-// all MCUs of one image -> int16 coefficient blocks (zero-filled by the caller)
-__host__ __device__ static void decode_entropy(const DmljImage& d, const uint8_t* stream, int16_t* coef) {
+// all MCUs of one image -> int16 coefficient blocks (zero-filled by the caller); dcs / acs: the
+// Huffman tables (LDS copies on the device)
+__host__ __device__ static void decode_entropy(const DmljImage& d, const DmljHuff* dcs, const DmljHuff* acs,
+                                               const uint8_t* stream, int16_t* coef) {
   const uint8_t* nat = d.nat;
   Bits b{stream, d.stream_len, 0, 0, 0};
   int pred[3] = {0, 0, 0};
@@ -130,8 +138,8 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint8_t
     for (int mx = 0; mx < d.mcux; ++mx)
       for (int c = 0; c < nc; ++c) {
         const int hs = nc == 1 ? 1 : d.hs[c], vs = nc == 1 ? 1 : d.vs[c];
-        const DmljHuff& dct = d.dc[d.td[c]];
-        const DmljHuff& act = d.ac[d.ta[c]];
+        const DmljHuff& dct = dcs[d.td[c]];
+        const DmljHuff& act = acs[d.ta[c]];
         for (int v = 0; v < vs; ++v)
           for (int h = 0; h < hs; ++h) {
             const int bx = mx * hs + h, by = my * vs + v;
@@ -325,11 +333,17 @@ __global__ __launch_bounds__(64) void jpeg_huff_kernel(const unsigned char* __re
   if (i >= n) return;
   const DmljImage& d = ((const DmljImage*)(buf + 16))[i];
   if (!d.ok) return;
+  // LDS: the 8 Huffman tables (every lookup of the serial decode is an LDS read, not a global
+  // one), then the entropy bytes
+  DmljHuff* th = (DmljHuff*)lds;
+  unsigned char* st = lds + 8 * sizeof(DmljHuff);
+  const uint4* ht = (const uint4*)&d.dc[0];
+  for (int j = threadIdx.x; j < (int)(8 * sizeof(DmljHuff) / 16); j += 64) ((uint4*)th)[j] = ht[j];
   const unsigned char* src = buf + d.stream_off;
   const int n16 = (d.stream_len + 15) / 16;
-  for (int j = threadIdx.x; j < n16; j += 64) *(uint4*)(lds + j * 16) = *(const uint4*)(src + j * 16);
+  for (int j = threadIdx.x; j < n16; j += 64) *(uint4*)(st + j * 16) = *(const uint4*)(src + j * 16);
   __syncthreads();
-  if (threadIdx.x == 0) decode_entropy(d, lds, coef);
+  if (threadIdx.x == 0) decode_entropy(d, th, th + 4, st, coef);
 }
 
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const unsigned char* __restrict__ buf, int n,
@@ -639,7 +653,7 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
   }
   const unsigned char* b = (const unsigned char*)dbuf;
   int16_t* coef = (int16_t*)dwork;
-  const unsigned lds = (unsigned)((maxstream + 15) / 16 * 16);
+  const unsigned lds = (unsigned)(8 * sizeof(DmljHuff) + (maxstream + 15) / 16 * 16);
   hipLaunchKernelGGL(dml::jpg::jpeg_huff_kernel, dim3(n), dim3(64), lds, s, b, n, coef);
   DML_CHECK_LAUNCH();
   hipLaunchKernelGGL(dml::jpg::jpeg_idct_kernel, dim3((maxblk + 255) / 256, n), dim3(256), 0, s, b, n, coef,
@@ -653,7 +667,8 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
 
 extern "C" int dml_jpeg_init(void) {
   const int rc = (int)hipFuncSetAttribute((const void*)dml::jpg::jpeg_huff_kernel,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, DMLJ_MAXSTREAM);
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)(8 * sizeof(DmljHuff)) + DMLJ_MAXSTREAM);
   if (rc) dml_set_error("dml_jpeg_init: hipFuncSetAttribute failed");
   return rc ? -1 : 0;
 }
@@ -682,7 +697,7 @@ extern "C" int dml_jpeg_decode_host(const unsigned char* data, long len, unsigne
   uint8_t* work = (uint8_t*)calloc((size_t)pl, 1);
   if (!work) return -1;
   int16_t* coef = (int16_t*)work;
-  dml::jpg::decode_entropy(d, stream, coef);
+  dml::jpg::decode_entropy(d, d.dc, d.ac, stream, coef);
   for (int c = 0; c < d.ncomp; ++c) {
     const int pw = d.bw[c] * 8;
     for (int by = 0; by < d.bh[c]; ++by)
