@@ -79,14 +79,15 @@ struct Bits {
   const uint8_t* p;
   int len, pos, nb;
   uint64_t buf;
-  // >= 33 bits after a fill: enough for one Huffman code or one coefficient's extra bits.
-  // 4 independent byte reads per refill (one LDS round trip on the device, not four)
+  // >= 33 bits after a fill: enough for one Huffman code AND its extra bits (<= 16 + 11).
+  // 4 independent byte reads per refill (one LDS round trip on the device, not four); the
+  // stream is followed by >= 8 zero bytes, and reads stop advancing past the end (libjpeg
+  // feeds zeros there too)
   __host__ __device__ void fill() {
-    while (nb <= 32) {
-      const uint32_t b0 = pos < len ? p[pos] : 0, b1 = pos + 1 < len ? p[pos + 1] : 0;  // past the end:
-      const uint32_t b2 = pos + 2 < len ? p[pos + 2] : 0, b3 = pos + 3 < len ? p[pos + 3] : 0;  // zeros
+    if (nb <= 32) {
+      const uint32_t b0 = p[pos], b1 = p[pos + 1], b2 = p[pos + 2], b3 = p[pos + 3];
       buf |= (uint64_t)((b0 << 24) | (b1 << 16) | (b2 << 8) | b3) << (32 - nb);
-      pos += 4;
+      pos = pos + 4 < len ? pos + 4 : len;
       nb += 32;
     }
   }
@@ -145,7 +146,6 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const DmljHuf
             const int bx = mx * hs + h, by = my * vs + v;
             int16_t* blk = coef + d.coef_off[c] + ((int64_t)by * d.bw[c] + bx) * 64;
             const int s = huff_decode(b, dct);
-            b.fill();
             const int diff = s ? extend(b.get(s), s) : 0;
             pred[c] += diff;
             blk[0] = (int16_t)pred[c];
@@ -154,7 +154,6 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const DmljHuf
               const int r = rs >> 4, sz = rs & 15;
               if (sz) {
                 k += r;
-                b.fill();
                 const int v2 = extend(b.get(sz), sz);
                 blk[nat[k]] = (int16_t)v2;
               } else {
@@ -326,24 +325,32 @@ __host__ __device__ static inline void rgb_at(const DmljImage& d, const uint8_t*
 }
 
 // ----------------------------------------------------------------------------- kernels --
+// IPB images per wave: all lanes copy each image's Huffman tables and entropy bytes into its LDS
+// region (`per` bytes), then lane j decodes image j serially — the wave's instruction stream
+// serves IPB decodes at once (every instruction costs the same for 1 or 64 active lanes)
 __global__ __launch_bounds__(64) void jpeg_huff_kernel(const unsigned char* __restrict__ buf, int n,
-                                                       int16_t* __restrict__ coef) {
+                                                       int16_t* __restrict__ coef, int ipb, int per) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int i = blockIdx.x;
-  if (i >= n) return;
-  const DmljImage& d = ((const DmljImage*)(buf + 16))[i];
-  if (!d.ok) return;
-  // LDS: the 8 Huffman tables (every lookup of the serial decode is an LDS read, not a global
-  // one), then the entropy bytes
-  DmljHuff* th = (DmljHuff*)lds;
-  unsigned char* st = lds + 8 * sizeof(DmljHuff);
-  const uint4* ht = (const uint4*)&d.dc[0];
-  for (int j = threadIdx.x; j < (int)(8 * sizeof(DmljHuff) / 16); j += 64) ((uint4*)th)[j] = ht[j];
-  const unsigned char* src = buf + d.stream_off;
-  const int n16 = (d.stream_len + 15) / 16;
-  for (int j = threadIdx.x; j < n16; j += 64) *(uint4*)(st + j * 16) = *(const uint4*)(src + j * 16);
+  const DmljImage* ds = (const DmljImage*)(buf + 16);
+  for (int j = 0; j < ipb; ++j) {
+    const int i = blockIdx.x * ipb + j;
+    if (i >= n || !ds[i].ok) continue;
+    const DmljImage& d = ds[i];
+    unsigned char* reg = lds + (size_t)j * per;
+    const uint4* ht = (const uint4*)&d.dc[0];
+    for (int k = threadIdx.x; k < (int)(8 * sizeof(DmljHuff) / 16); k += 64) ((uint4*)reg)[k] = ht[k];
+    unsigned char* st = reg + 8 * sizeof(DmljHuff);
+    const uint4* src = (const uint4*)(buf + d.stream_off);
+    const int n16 = (d.stream_len + 8 + 15) / 16;   // + the zero padding the bit reader relies on
+    for (int k = threadIdx.x; k < n16; k += 64) ((uint4*)st)[k] = src[k];
+  }
   __syncthreads();
-  if (threadIdx.x == 0) decode_entropy(d, th, th + 4, st, coef);
+  const int j = threadIdx.x;
+  const int i = blockIdx.x * ipb + j;
+  if (j < ipb && i < n && ds[i].ok) {
+    const DmljHuff* th = (const DmljHuff*)(lds + (size_t)j * per);
+    decode_entropy(ds[i], th, th + 4, (const unsigned char*)th + 8 * sizeof(DmljHuff), coef);
+  }
 }
 
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const unsigned char* __restrict__ buf, int n,
@@ -612,7 +619,13 @@ extern "C" long dml_jpeg_prepare(int n, const unsigned char* const* datas, const
       continue;
     }
     d[i].stream_off = off;
-    off += (d[i].stream_len + 15) / 16 * 16;
+    const long padded = (d[i].stream_len + 8 + 15) / 16 * 16;   // >= 8 zero bytes for the bit reader
+    if (off + padded > cap) {
+      memset(&d[i], 0, sizeof(DmljImage));
+      continue;
+    }
+    memset(b + off + d[i].stream_len, 0, (size_t)(padded - d[i].stream_len));
+    off += padded;
     int nb = 0;
     for (int c = 0; c < d[i].ncomp; ++c) {
       d[i].coef_off[c] = ncoef;
@@ -653,8 +666,11 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
   }
   const unsigned char* b = (const unsigned char*)dbuf;
   int16_t* coef = (int16_t*)dwork;
-  const unsigned lds = (unsigned)(8 * sizeof(DmljHuff) + (maxstream + 15) / 16 * 16);
-  hipLaunchKernelGGL(dml::jpg::jpeg_huff_kernel, dim3(n), dim3(64), lds, s, b, n, coef);
+  const int per = (int)(8 * sizeof(DmljHuff) + (maxstream + 8 + 15) / 16 * 16);
+  int ipb = 163840 / per;
+  ipb = ipb < 1 ? 1 : (ipb > 8 ? 8 : ipb);
+  hipLaunchKernelGGL(dml::jpg::jpeg_huff_kernel, dim3((n + ipb - 1) / ipb), dim3(64), (unsigned)(ipb * per), s, b, n,
+                     coef, ipb, per);
   DML_CHECK_LAUNCH();
   hipLaunchKernelGGL(dml::jpg::jpeg_idct_kernel, dim3((maxblk + 255) / 256, n), dim3(256), 0, s, b, n, coef,
                      (uint8_t*)dwork);
@@ -668,7 +684,7 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
 extern "C" int dml_jpeg_init(void) {
   const int rc = (int)hipFuncSetAttribute((const void*)dml::jpg::jpeg_huff_kernel,
                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)(8 * sizeof(DmljHuff)) + DMLJ_MAXSTREAM);
+                                          163840);
   if (rc) dml_set_error("dml_jpeg_init: hipFuncSetAttribute failed");
   return rc ? -1 : 0;
 }
@@ -681,7 +697,8 @@ extern "C" int dml_jpeg_decode_host(const unsigned char* data, long len, unsigne
   DmljImage d;
   static thread_local uint8_t* stream = nullptr;
   if (!stream) stream = (uint8_t*)malloc(1 << 24);
-  if (parse_one(data, len, d, stream, 1 << 24, 0, 0) != 0) return -1;
+  if (parse_one(data, len, d, stream, (1 << 24) - 16, 0, 0) != 0) return -1;
+  memset(stream + d.stream_len, 0, 16);   // the bit reader's zero padding
   hw[0] = d.h;
   hw[1] = d.w;
   int64_t ncoef = 0;
