@@ -39,7 +39,7 @@
 #define DMLJ_MAXSTREAM (60 * 1024)
 
 struct DmljHuff {
-  uint16_t look[512];   // 9-bit lookahead: (len << 8) | symbol; 0 = a longer code
+  uint32_t look[512];   // 9-bit lookahead: (len << 8) | symbol; 0 = a longer code (32-bit: scalar loads)
   int32_t maxcode[18];  // largest code of each length (-1: none); [17] = sentinel
   int32_t valoff[18];   // val index of a code of length l = valoff[l] + code
   uint8_t val[256];
@@ -61,8 +61,9 @@ struct DmljImage {
   uint8_t nat[80];              // zigzag -> natural order (+ libjpeg's pad)
   DmljHuff dc[4], ac[4];
 };
-static_assert(sizeof(DmljImage) % 16 == 0 && offsetof(DmljImage, dc) % 16 == 0 && sizeof(DmljHuff) % 16 == 0,
-              "16-B copies of descriptors and Huffman tables");
+static_assert(sizeof(DmljImage) % 16 == 0 && offsetof(DmljImage, dc) % 16 == 0 && sizeof(DmljHuff) % 16 == 0 &&
+                  offsetof(DmljImage, nat) % 4 == 0 && offsetof(DmljHuff, val) % 4 == 0,
+              "aligned descriptors; 32-bit reads of the byte tables");
 
 namespace dml {
 namespace jpg {
@@ -76,18 +77,17 @@ static const uint8_t kNatural[80] = {
 
 // ------------------------------------------------------------------ entropy decoding --
 struct Bits {
-  const uint8_t* p;
-  int len, pos, nb;
+  const uint32_t* w;   // the entropy bytes as aligned 32-bit words (>= 8 zero bytes past the end)
+  int nw, pos, nb;
   uint64_t buf;
-  // >= 33 bits after a fill: enough for one Huffman code AND its extra bits (<= 16 + 11).
-  // 4 independent byte reads per refill (one LDS round trip on the device, not four); the
-  // stream is followed by >= 8 zero bytes, and reads stop advancing past the end (libjpeg
-  // feeds zeros there too)
+  // >= 33 bits after a fill: enough for one Huffman code AND its extra bits (<= 16 + 11). One
+  // aligned word per refill: in the GPU kernel every lane runs the decode with the same
+  // (wave-uniform) operands, so these reads and the table lookups are scalar loads and the bit
+  // arithmetic scalar instructions; past the end the reader keeps returning zeros, as libjpeg
   __host__ __device__ void fill() {
     if (nb <= 32) {
-      const uint32_t b0 = p[pos], b1 = p[pos + 1], b2 = p[pos + 2], b3 = p[pos + 3];
-      buf |= (uint64_t)((b0 << 24) | (b1 << 16) | (b2 << 8) | b3) << (32 - nb);
-      pos = pos + 4 < len ? pos + 4 : len;
+      buf |= (uint64_t)__builtin_bswap32(w[pos]) << (32 - nb);
+      pos = pos + 1 < nw ? pos + 1 : nw;
       nb += 32;
     }
   }
@@ -104,9 +104,15 @@ struct Bits {
   }
 };
 
+// byte i of a 4-byte-aligned array through a 32-bit read (a scalar load in the uniform kernel;
+// gfx950 has no scalar byte load)
+__host__ __device__ static inline int byte_at(const uint8_t* p, int i) {
+  return (int)((((const uint32_t*)p)[i >> 2] >> ((i & 3) * 8)) & 255);
+}
+
 __host__ __device__ static inline int huff_decode(Bits& b, const DmljHuff& t) {
   b.fill();
-  const uint16_t e = t.look[b.peek(9)];
+  const uint32_t e = t.look[b.peek(9)];
   if (e) {
     b.skip(e >> 8);
     return e & 255;
@@ -122,17 +128,19 @@ __host__ __device__ static inline int huff_decode(Bits& b, const DmljHuff& t) {
     return 0;
   }
   b.skip(l);
-  return t.val[(t.valoff[l] + code) & 255];
+  return byte_at(t.val, (t.valoff[l] + code) & 255);
 }
 
 __host__ __device__ static inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
-// all MCUs of one image -> int16 coefficient blocks (zero-filled by the caller); dcs / acs: the
-// Huffman tables (LDS copies on the device)
-__host__ __device__ static void decode_entropy(const DmljImage& d, const DmljHuff* dcs, const DmljHuff* acs,
-                                               const uint8_t* stream, int16_t* coef) {
+// all MCUs of one image -> int16 coefficient blocks (zero-filled by the caller); only `writer`
+// stores them (the GPU kernel runs this on every lane of a wave, lane 0 writing)
+__host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_t* stream, int16_t* coef,
+                                               bool writer) {
   const uint8_t* nat = d.nat;
-  Bits b{stream, d.stream_len, 0, 0, 0};
+  const DmljHuff* dcs = d.dc;
+  const DmljHuff* acs = d.ac;
+  Bits b{stream, (d.stream_len + 3) / 4, 0, 0, 0};
   int pred[3] = {0, 0, 0};
   const int nc = d.ncomp;
   for (int my = 0; my < d.mcuy; ++my)
@@ -148,14 +156,14 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const DmljHuf
             const int s = huff_decode(b, dct);
             const int diff = s ? extend(b.get(s), s) : 0;
             pred[c] += diff;
-            blk[0] = (int16_t)pred[c];
+            if (writer) blk[0] = (int16_t)pred[c];
             for (int k = 1; k < 64; ++k) {
               const int rs = huff_decode(b, act);
               const int r = rs >> 4, sz = rs & 15;
               if (sz) {
                 k += r;
                 const int v2 = extend(b.get(sz), sz);
-                blk[nat[k]] = (int16_t)v2;
+                if (writer) blk[byte_at(nat, k)] = (int16_t)v2;
               } else {
                 if (r != 15) break;
                 k += 15;
@@ -325,32 +333,15 @@ __host__ __device__ static inline void rgb_at(const DmljImage& d, const uint8_t*
 }
 
 // ----------------------------------------------------------------------------- kernels --
-// IPB images per wave: all lanes copy each image's Huffman tables and entropy bytes into its LDS
-// region (`per` bytes), then lane j decodes image j serially — the wave's instruction stream
-// serves IPB decodes at once (every instruction costs the same for 1 or 64 active lanes)
+// one wave per image; every lane runs the same decode (wave-uniform: scalar loads of the
+// entropy words and the Huffman tables from the descriptor, scalar bit arithmetic), lane 0
+// stores the coefficients
 __global__ __launch_bounds__(64) void jpeg_huff_kernel(const unsigned char* __restrict__ buf, int n,
-                                                       int16_t* __restrict__ coef, int ipb, int per) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+                                                       int16_t* __restrict__ coef) {
+  const int i = blockIdx.x;
   const DmljImage* ds = (const DmljImage*)(buf + 16);
-  for (int j = 0; j < ipb; ++j) {
-    const int i = blockIdx.x * ipb + j;
-    if (i >= n || !ds[i].ok) continue;
-    const DmljImage& d = ds[i];
-    unsigned char* reg = lds + (size_t)j * per;
-    const uint4* ht = (const uint4*)&d.dc[0];
-    for (int k = threadIdx.x; k < (int)(8 * sizeof(DmljHuff) / 16); k += 64) ((uint4*)reg)[k] = ht[k];
-    unsigned char* st = reg + 8 * sizeof(DmljHuff);
-    const uint4* src = (const uint4*)(buf + d.stream_off);
-    const int n16 = (d.stream_len + 8 + 15) / 16;   // + the zero padding the bit reader relies on
-    for (int k = threadIdx.x; k < n16; k += 64) ((uint4*)st)[k] = src[k];
-  }
-  __syncthreads();
-  const int j = threadIdx.x;
-  const int i = blockIdx.x * ipb + j;
-  if (j < ipb && i < n && ds[i].ok) {
-    const DmljHuff* th = (const DmljHuff*)(lds + (size_t)j * per);
-    decode_entropy(ds[i], th, th + 4, (const unsigned char*)th + 8 * sizeof(DmljHuff), coef);
-  }
+  if (i >= n || !ds[i].ok) return;
+  decode_entropy(ds[i], (const uint32_t*)(buf + ds[i].stream_off), coef, threadIdx.x == 0);
 }
 
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const unsigned char* __restrict__ buf, int n,
@@ -399,7 +390,7 @@ static int build_huff(const uint8_t* counts, const uint8_t* vals, int nvals, Dml
         if (k >= nvals || k >= 256) return -1;
         if (l <= 9) {
           const int base = code << (9 - l);
-          for (int e = 0; e < (1 << (9 - l)); ++e) t.look[base + e] = (uint16_t)((l << 8) | vals[k]);
+          for (int e = 0; e < (1 << (9 - l)); ++e) t.look[base + e] = (uint32_t)((l << 8) | vals[k]);
         }
       }
       t.maxcode[l] = code - 1;
@@ -666,11 +657,7 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
   }
   const unsigned char* b = (const unsigned char*)dbuf;
   int16_t* coef = (int16_t*)dwork;
-  const int per = (int)(8 * sizeof(DmljHuff) + (maxstream + 8 + 15) / 16 * 16);
-  int ipb = 163840 / per;
-  ipb = ipb < 1 ? 1 : (ipb > 8 ? 8 : ipb);
-  hipLaunchKernelGGL(dml::jpg::jpeg_huff_kernel, dim3((n + ipb - 1) / ipb), dim3(64), (unsigned)(ipb * per), s, b, n,
-                     coef, ipb, per);
+  hipLaunchKernelGGL(dml::jpg::jpeg_huff_kernel, dim3(n), dim3(64), 0, s, b, n, coef);
   DML_CHECK_LAUNCH();
   hipLaunchKernelGGL(dml::jpg::jpeg_idct_kernel, dim3((maxblk + 255) / 256, n), dim3(256), 0, s, b, n, coef,
                      (uint8_t*)dwork);
@@ -681,13 +668,7 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
   return 0;
 }
 
-extern "C" int dml_jpeg_init(void) {
-  const int rc = (int)hipFuncSetAttribute((const void*)dml::jpg::jpeg_huff_kernel,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          163840);
-  if (rc) dml_set_error("dml_jpeg_init: hipFuncSetAttribute failed");
-  return rc ? -1 : 0;
-}
+extern "C" int dml_jpeg_init(void) { return 0; }   // nothing to set up (kept for the backend's init order)
 
 extern "C" long dml_jpeg_desc_size(void) { return (long)sizeof(DmljImage); }
 
@@ -714,7 +695,7 @@ extern "C" int dml_jpeg_decode_host(const unsigned char* data, long len, unsigne
   uint8_t* work = (uint8_t*)calloc((size_t)pl, 1);
   if (!work) return -1;
   int16_t* coef = (int16_t*)work;
-  dml::jpg::decode_entropy(d, d.dc, d.ac, stream, coef);
+  dml::jpg::decode_entropy(d, (const uint32_t*)stream, coef, true);
   for (int c = 0; c < d.ncomp; ++c) {
     const int pw = d.bw[c] * 8;
     for (int by = 0; by < d.bh[c]; ++by)
