@@ -464,14 +464,25 @@ class _JpegPack:
         for i, sl in zip(self.idx, slots):
             L.dml_jpeg_set_slot(C.c_void_p(self.buf.data_ptr()), i, int(sl))
         H, W = self.hw
-        with torch.cuda.stream(stream):
+        # on a side stream of its own: the serial Huffman decode of one window (one wave per
+        # image, milliseconds) overlaps the next windows' instead of queueing behind it on the
+        # staging stream, which only waits for it before the window's event
+        side = self.be.jpeg_stream()
+        side.wait_stream(stream)
+        with torch.cuda.stream(side):
             self.dev = torch.empty(self.used, dtype=torch.uint8, device=arena.device)
             self.dev.copy_(self.buf[:self.used], non_blocking=True)
             self.work = torch.empty(max(self.work_bytes, 256), dtype=torch.uint8, device=arena.device)
             self.work[:self.coef_bytes].zero_()
             N.check(L.dml_jpeg_decode_resize(self.dev.data_ptr(), self.n, self.maxblk, self.maxstream,
-                                             self.work.data_ptr(), H, W, arena.data_ptr(), stream.cuda_stream),
+                                             self.work.data_ptr(), H, W, arena.data_ptr(), side.cuda_stream),
                     "dml_jpeg_decode_resize")
+            done = torch.cuda.Event()
+            done.record(side)
+        stream.wait_event(done)
+        # the caching allocator must not hand these buffers out before `side` is done with them
+        self.dev.record_stream(side)
+        self.work.record_stream(side)
 
     def release(self) -> None:
         self.dev = self.work = None
@@ -543,6 +554,8 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         self._dbytes, self.decode_hits, self._dlock = 0, 0, threading.Lock()
         self._nn: Dict[Tuple[int, int], np.ndarray] = {}    # (n_in, n_out) -> nearest-index table
         self._pins: List[torch.Tensor] = []                  # free pinned pack buffers
+        self._jstreams: List[torch.cuda.Stream] = []         # side streams of the GPU JPEG decodes
+        self._jnext = 0
         # DML_GPU_RESIZE=0: the decode pool resizes on the CPU (Pillow) as before (A/B)
         self.gpu_resize = os.environ.get("DML_GPU_RESIZE", "1") != "0"
         # DML_GPU_JPEG=0: every JPEG decodes on the CPU (the decode workers), as before (A/B)
@@ -593,6 +606,15 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         if t is None:
             t = self._nn[(n_in, n_out)] = nearest_index(n_in, n_out)
         return t
+
+    JPEG_STREAMS = 4
+
+    def jpeg_stream(self) -> torch.cuda.Stream:
+        """(serve loop) the next of JPEG_STREAMS side streams for GPU JPEG decodes."""
+        if not self._jstreams:
+            self._jstreams = [torch.cuda.Stream(self.device) for _ in range(self.JPEG_STREAMS)]
+        self._jnext = (self._jnext + 1) % len(self._jstreams)
+        return self._jstreams[self._jnext]
 
     def pinned(self, nbytes: int) -> torch.Tensor:
         """(decode pool) a pinned buffer of at least nbytes: a free one of the pool or a new one."""
