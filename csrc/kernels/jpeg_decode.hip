@@ -77,17 +77,24 @@ static const uint8_t kNatural[80] = {
 
 // ------------------------------------------------------------------ entropy decoding --
 struct Bits {
-  const uint32_t* w;   // the entropy bytes as aligned 32-bit words (>= 8 zero bytes past the end)
+  const uint32_t* w;   // the entropy bytes as aligned 32-bit words, byte-swapped by the host (a
+                       // little-endian read gives the stream's big-endian bits); >= 8 zero bytes
+                       // past the end
   int nw, pos, nb;
   uint64_t buf;
-  // >= 33 bits after a fill: enough for one Huffman code AND its extra bits (<= 16 + 11). One
-  // aligned word per refill: in the GPU kernel every lane runs the decode with the same
-  // (wave-uniform) operands, so these reads and the table lookups are scalar loads and the bit
-  // arithmetic scalar instructions; past the end the reader keeps returning zeros, as libjpeg
+  uint32_t nextw;      // the next refill's word, loaded one refill ahead (its latency hidden)
+  __host__ __device__ Bits(const uint32_t* words, int nwords) : w(words), nw(nwords), pos(0), nb(0), buf(0) {
+    nextw = w[0];
+  }
+  // >= 33 bits after a fill: enough for one Huffman code AND its extra bits (<= 16 + 11). In
+  // the GPU kernel every lane runs the decode with the same (wave-uniform) operands, so these
+  // reads and the table lookups are scalar loads and the bit arithmetic scalar instructions;
+  // past the end the reader keeps returning zeros, as libjpeg
   __host__ __device__ void fill() {
     if (nb <= 32) {
-      buf |= (uint64_t)__builtin_bswap32(w[pos]) << (32 - nb);
+      buf |= (uint64_t)nextw << (32 - nb);
       pos = pos + 1 < nw ? pos + 1 : nw;
+      nextw = w[pos];
       nb += 32;
     }
   }
@@ -103,6 +110,17 @@ struct Bits {
     return v;
   }
 };
+
+// the host side of the word reads above: swap each 4-byte group of the (zero-padded) stream
+static void swap_words(uint8_t* p, long len) {
+  for (long i = 0; i + 4 <= len; i += 4) {
+    const uint8_t a = p[i], b = p[i + 1];
+    p[i] = p[i + 3];
+    p[i + 1] = p[i + 2];
+    p[i + 2] = b;
+    p[i + 3] = a;
+  }
+}
 
 // byte i of a 4-byte-aligned array through a 32-bit read (a scalar load in the uniform kernel;
 // gfx950 has no scalar byte load)
@@ -140,7 +158,7 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_
   const uint8_t* nat = d.nat;
   const DmljHuff* dcs = d.dc;
   const DmljHuff* acs = d.ac;
-  Bits b{stream, (d.stream_len + 3) / 4, 0, 0, 0};
+  Bits b(stream, (d.stream_len + 3) / 4);
   int pred[3] = {0, 0, 0};
   const int nc = d.ncomp;
   for (int my = 0; my < d.mcuy; ++my)
@@ -616,6 +634,7 @@ extern "C" long dml_jpeg_prepare(int n, const unsigned char* const* datas, const
       continue;
     }
     memset(b + off + d[i].stream_len, 0, (size_t)(padded - d[i].stream_len));
+    dml::jpg::swap_words(b + off, padded);
     off += padded;
     int nb = 0;
     for (int c = 0; c < d[i].ncomp; ++c) {
@@ -680,6 +699,7 @@ extern "C" int dml_jpeg_decode_host(const unsigned char* data, long len, unsigne
   if (!stream) stream = (uint8_t*)malloc(1 << 24);
   if (parse_one(data, len, d, stream, (1 << 24) - 16, 0, 0) != 0) return -1;
   memset(stream + d.stream_len, 0, 16);   // the bit reader's zero padding
+  dml::jpg::swap_words(stream, (d.stream_len + 8 + 15) / 16 * 16);
   hw[0] = d.h;
   hw[1] = d.w;
   int64_t ncoef = 0;
