@@ -467,8 +467,9 @@ class _JpegPack:
         # on a side stream of its own: the serial Huffman decode of one window (one wave per
         # image, milliseconds) overlaps the next windows' instead of queueing behind it on the
         # staging stream, which only waits for it before the window's event
+        # (no wait on `stream`: it has waited on the previous windows' decodes, which would chain
+        # them again; nothing before this on `stream` touches this window's slots or buffers)
         side = self.be.jpeg_stream()
-        side.wait_stream(stream)
         with torch.cuda.stream(side):
             self.dev = torch.empty(self.used, dtype=torch.uint8, device=arena.device)
             self.dev.copy_(self.buf[:self.used], non_blocking=True)
