@@ -58,11 +58,12 @@ struct DmljImage {
   int32_t stream_len, outH, outW, pad;
   int16_t rowtab[DMLJ_MAXOUT], coltab[DMLJ_MAXOUT];
   uint16_t q[4][64];            // natural order
-  uint8_t nat[80];              // zigzag -> natural order (+ libjpeg's pad)
+  uint8_t izz[64];              // natural -> zigzag index (the IDCT's gather of a zigzag block)
+  uint8_t pad2[16];
   DmljHuff dc[4], ac[4];
 };
 static_assert(sizeof(DmljImage) % 16 == 0 && offsetof(DmljImage, dc) % 16 == 0 && sizeof(DmljHuff) % 16 == 0 &&
-                  offsetof(DmljImage, nat) % 4 == 0 && offsetof(DmljHuff, val) % 4 == 0,
+                  offsetof(DmljImage, izz) % 4 == 0 && offsetof(DmljHuff, val) % 4 == 0,
               "aligned descriptors; 32-bit reads of the byte tables");
 
 namespace dml {
@@ -151,11 +152,12 @@ __host__ __device__ static inline int huff_decode(Bits& b, const DmljHuff& t) {
 
 __host__ __device__ static inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
-// all MCUs of one image -> int16 coefficient blocks (zero-filled by the caller); only `writer`
-// stores them (the GPU kernel runs this on every lane of a wave, lane 0 writing)
+// all MCUs of one image -> int16 coefficient blocks in ZIGZAG order (zero-filled by the caller;
+// the IDCT reads them through the inverse table: no dependent table load per coefficient
+// here). In the GPU kernel every lane runs this and stores the same value to the same address
+// (no divergent branch around the stores)
 __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_t* stream, int16_t* coef,
                                                bool writer) {
-  const uint8_t* nat = d.nat;
   const DmljHuff* dcs = d.dc;
   const DmljHuff* acs = d.ac;
   Bits b(stream, (d.stream_len + 3) / 4);
@@ -181,7 +183,7 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_
               if (sz) {
                 k += r;
                 const int v2 = extend(b.get(sz), sz);
-                if (writer) blk[byte_at(nat, k)] = (int16_t)v2;
+                if (writer) blk[k < 64 ? k : 63] = (int16_t)v2;   // corrupt runs: libjpeg's pad maps to 63
               } else {
                 if (r != 15) break;
                 k += 15;
@@ -352,14 +354,13 @@ __host__ __device__ static inline void rgb_at(const DmljImage& d, const uint8_t*
 
 // ----------------------------------------------------------------------------- kernels --
 // one wave per image; every lane runs the same decode (wave-uniform: scalar loads of the
-// entropy words and the Huffman tables from the descriptor, scalar bit arithmetic), lane 0
-// stores the coefficients
+// entropy words and the Huffman tables from the descriptor, scalar bit arithmetic)
 __global__ __launch_bounds__(64) void jpeg_huff_kernel(const unsigned char* __restrict__ buf, int n,
                                                        int16_t* __restrict__ coef) {
   const int i = blockIdx.x;
   const DmljImage* ds = (const DmljImage*)(buf + 16);
   if (i >= n || !ds[i].ok) return;
-  decode_entropy(ds[i], (const uint32_t*)(buf + ds[i].stream_off), coef, threadIdx.x == 0);
+  decode_entropy(ds[i], (const uint32_t*)(buf + ds[i].stream_off), coef, true);
 }
 
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const unsigned char* __restrict__ buf, int n,
@@ -375,8 +376,11 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const unsigned char* __r
   }
   const int by = blk / d.bw[c], bx = blk - by * d.bw[c];
   const int pw = d.bw[c] * 8;
-  idct_islow(coef + d.coef_off[c] + (int64_t)blk * 64, d.q[d.tq[c]],
-             work + d.plane_off[c] + (int64_t)by * 8 * pw + bx * 8, pw);
+  const int16_t* zz = coef + d.coef_off[c] + (int64_t)blk * 64;
+  int16_t in[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) in[j] = zz[d.izz[j]];   // zigzag -> natural
+  idct_islow(in, d.q[d.tq[c]], work + d.plane_off[c] + (int64_t)by * 8 * pw + bx * 8, pw);
 }
 
 __global__ __launch_bounds__(256) void jpeg_rgb_resize_kernel(const unsigned char* __restrict__ buf, int n,
@@ -595,7 +599,7 @@ static int parse_one(const uint8_t* p, int64_t len, DmljImage& d, uint8_t* out, 
   }
   d.outH = outH;
   d.outW = outW;
-  memcpy(d.nat, kNatural, sizeof d.nat);
+  for (int k = 0; k < 64; ++k) d.izz[kNatural[k]] = (uint8_t)k;
   d.ok = 1;
   return 0;
 }
@@ -720,8 +724,12 @@ extern "C" int dml_jpeg_decode_host(const unsigned char* data, long len, unsigne
     const int pw = d.bw[c] * 8;
     for (int by = 0; by < d.bh[c]; ++by)
       for (int bx = 0; bx < d.bw[c]; ++bx)
-        dml::jpg::idct_islow(coef + d.coef_off[c] + ((int64_t)by * d.bw[c] + bx) * 64, d.q[d.tq[c]],
-                             work + d.plane_off[c] + (int64_t)by * 8 * pw + bx * 8, pw);
+      {
+        const int16_t* zz = coef + d.coef_off[c] + ((int64_t)by * d.bw[c] + bx) * 64;
+        int16_t in[64];
+        for (int j = 0; j < 64; ++j) in[j] = zz[d.izz[j]];
+        dml::jpg::idct_islow(in, d.q[d.tq[c]], work + d.plane_off[c] + (int64_t)by * 8 * pw + bx * 8, pw);
+      }
   }
   for (int y = 0; y < d.h; ++y)
     for (int x = 0; x < d.w; ++x) dml::jpg::rgb_at(d, work, y, x, out + ((int64_t)y * d.w + x) * 3);
