@@ -597,10 +597,15 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             N.check(N.lib().dml_jpeg_init(), "dml_jpeg_init")
         if self.loader is not None:
             self._procs()   # the decode workers start (and import Pillow) now, not inside a timed pass
+            # and the windows' pinned buffers: pinning host memory mid-pass (64 MB at a time) held
+            # up the serve loop's launches for 20-50 ms
+            self._pins = [torch.empty(self.PIN_BYTES, dtype=torch.uint8).pin_memory()
+                          for _ in range(self.PIN_PREALLOC)]
 
     DECODE_CACHE_BYTES = 1 << 30
     DECODE_CHUNK = 8
-    PIN_BYTES = 64 << 20
+    PIN_BYTES = 16 << 20   # a GPU-JPEG window of 256 images needs ~9.5 MB (descriptors + entropy bytes)
+    PIN_PREALLOC = 16      # pinned buffers allocated with the store loader (host-pinning stalls every HIP call)
 
     def nearest(self, n_in: int, n_out: int) -> np.ndarray:
         t = self._nn.get((n_in, n_out))

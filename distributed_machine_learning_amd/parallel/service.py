@@ -440,7 +440,9 @@ def auto_depth(world: int) -> int:
     10.9 / 21.9 ms for ResNet50), 16 with peers: a PUT then replicates to R ranks and the
     step is lockstep over the group, so more batches wait on their output (r5,
     tools/store_capacity.py at world 8 on 8 shared cores: depth 8 / 32 -> 259 / 503 batches/s).
-    The image staging look-ahead stays at STAGE_DEPTH batches per rank whatever the depth."""
+    The image staging look-ahead is STAGE_DEPTH batches per rank whatever the depth (a window
+    takes ~10 ms from fetch to resident; at world 1 the depth of 4 left the first pass over new
+    images waiting on its windows)."""
     return 4 if world <= 1 else 16
 
 
@@ -660,7 +662,7 @@ class CollectiveService:
         if rejoined:
             self.unsynced |= set(eg.members) - set(eg.prev_members)
         # queued batches staged ahead of dispatch (the in-flight ones are staged besides)
-        self.stage_ahead = max(1, eg.world) * min(coord.depth, STAGE_DEPTH)
+        self.stage_ahead = max(1, eg.world) * STAGE_DEPTH
         self._rec_bufs: Dict[tuple, object] = {}   # the step's exchange output, per (world, L)
         # a staging backend (image arenas): queued batches get an affinity rank, their images
         # are staged there ahead of dispatch and the plan sends them there
@@ -1026,7 +1028,7 @@ class CollectiveService:
         # ranks new in this epoch (re-joined) and ranks still waiting for their first state
         # stay out of the coordinator role until the next state record
         self.unsynced = (self.unsynced & set(self.eg.members)) | (set(self.eg.members) - set(self.eg.prev_members))
-        self.stage_ahead = self.eg.world * min(self.coord.depth, STAGE_DEPTH)
+        self.stage_ahead = self.eg.world * STAGE_DEPTH
         # image windows: every rank forgets its staging at this same boundary and stages
         # afresh over the new group (a joiner's arena is empty; survivors' collectives of
         # the failed epoch were aborted)

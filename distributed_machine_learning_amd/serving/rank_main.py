@@ -164,12 +164,12 @@ def rank_main(a: argparse.Namespace) -> int:
     from ..parallel.service import auto_depth
 
     depth = a.depth or auto_depth(world)
-    # the image windows stage world x min(depth, STAGE_DEPTH) batches ahead of dispatch while
+    # the image windows stage world x STAGE_DEPTH batches ahead of dispatch while
     # world x depth are in flight (pinned): the usable arena (beyond the backend's synthetic
     # images) holds both
     from ..parallel.service import STAGE_DEPTH
 
-    need = world * (depth + min(depth, STAGE_DEPTH)) * cap
+    need = world * (depth + STAGE_DEPTH) * cap
     if a.arena_images and a.arena_images < need:
         raise SystemExit(f"--arena-images {a.arena_images} < {need} = ranks x (depth + staged) x batch: "
                          "staged-ahead batches would wait behind pinned in-flight ones")
