@@ -691,6 +691,37 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
   return 0;
 }
 
+// a decoded image's descriptor re-targeted to another output size (the other model's window):
+// dst <- src with that size's NEAREST tables and ABSOLUTE plane addresses (base + plane_off), for
+// dml_jpeg_resize_only — the image is decoded once for both models
+extern "C" void dml_jpeg_retarget(void* dst, const void* src, int outH, int outW, long base) {
+  DmljImage* d = (DmljImage*)dst;
+  memcpy(d, src, sizeof(DmljImage));
+  if (!d->ok || outH <= 0 || outW <= 0 || outH > DMLJ_MAXOUT || outW > DMLJ_MAXOUT) {
+    d->ok = 0;
+    return;
+  }
+  dml::jpg::nearest_tab(d->h, outH, d->rowtab);
+  dml::jpg::nearest_tab(d->w, outW, d->coltab);
+  d->outH = outH;
+  d->outW = outW;
+  for (int c = 0; c < d->ncomp; ++c) d->plane_off[c] += base;
+}
+
+// colour + resize only, from planes a dml_jpeg_decode_resize launch left (descriptors from
+// dml_jpeg_retarget, in a buffer laid out as dml_jpeg_prepare's: int64 n, int64 0, records)
+extern "C" int dml_jpeg_resize_only(const void* dbuf, int n, int H, int W, void* arena, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (H <= 0 || W <= 0 || H > DMLJ_MAXOUT || W > DMLJ_MAXOUT) {
+    dml_set_error("dml_jpeg_resize_only: bad output size");
+    return -1;
+  }
+  hipLaunchKernelGGL(dml::jpg::jpeg_rgb_resize_kernel, dim3(H, n), dim3(256), 0, s, (const unsigned char*)dbuf, n,
+                     (const uint8_t*)nullptr, H, W, (uint8_t*)arena);
+  DML_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int dml_jpeg_init(void) { return 0; }   // nothing to set up (kept for the backend's init order)
 
 extern "C" long dml_jpeg_desc_size(void) { return (long)sizeof(DmljImage); }

@@ -453,7 +453,12 @@ class _JpegPack:
         self.idx = [i for i in range(n) if status[i]]
         self.names = [names[i] for i in self.idx]
         self.unsupported = [names[i] for i in range(n) if not status[i]]
-        self.dev = self.work = None
+        self.dev = None
+        self.done = None   # the decode's completion event (set at launch)
+        self.desc = L.dml_jpeg_desc_size()
+        # the device work buffer now (coefficients, then the sample planes the other model's
+        # window re-uses: GpuRankBackend.planes_for)
+        self.work = torch.empty(max(self.work_bytes, 256), dtype=torch.uint8, device=backend.device)
 
     def launch(self, slots: List[int], arena: torch.Tensor, stream) -> None:
         import ctypes as C
@@ -470,10 +475,10 @@ class _JpegPack:
         # (no wait on `stream`: it has waited on the previous windows' decodes, which would chain
         # them again; nothing before this on `stream` touches this window's slots or buffers)
         side = self.be.jpeg_stream()
+        side.wait_stream(torch.cuda.current_stream())   # `work` was allocated on the pool thread's stream
         with torch.cuda.stream(side):
             self.dev = torch.empty(self.used, dtype=torch.uint8, device=arena.device)
             self.dev.copy_(self.buf[:self.used], non_blocking=True)
-            self.work = torch.empty(max(self.work_bytes, 256), dtype=torch.uint8, device=arena.device)
             self.work[:self.coef_bytes].zero_()
             N.check(L.dml_jpeg_decode_resize(self.dev.data_ptr(), self.n, self.maxblk, self.maxstream,
                                              self.work.data_ptr(), H, W, arena.data_ptr(), side.cuda_stream),
@@ -484,9 +489,65 @@ class _JpegPack:
         # the caching allocator must not hand these buffers out before `side` is done with them
         self.dev.record_stream(side)
         self.work.record_stream(side)
+        self.done = done
+        b = self.buf.numpy()
+        self.be.remember_planes(self, {nm: b[16 + i * self.desc:16 + (i + 1) * self.desc].copy()
+                                       for i, nm in zip(self.idx, self.names)})
 
     def release(self) -> None:
-        self.dev = self.work = None
+        self.dev = None   # `work` stays while the plane cache holds this window
+        if self.buf is not None:
+            self.be.unpin(self.buf)
+            self.buf = None
+
+
+class _ResizePack:
+    """The other model's window over images a _JpegPack already decoded on this GPU: their
+    descriptors re-targeted to this model's size (dml_jpeg_retarget: NEAREST tables, absolute
+    plane addresses) and one colour + resize launch after those decodes' events — each image
+    is decoded once for both models."""
+
+    def __init__(self, backend: "GpuRankBackend", names: List[str], entries: list, hw: Tuple[int, int]):
+        import ctypes as C
+
+        from .. import _native as N
+
+        L = N.lib()
+        self.be, self.hw, self.names = backend, hw, names
+        desc = L.dml_jpeg_desc_size()
+        self.used = 16 + len(names) * desc
+        self.buf = backend.pinned(self.used)
+        b = self.buf.numpy()
+        b[:16].view(np.int64)[:] = (len(names), 0)
+        base = self.buf.data_ptr()
+        self.packs, self.works = [], []
+        for i, (rec, pk, work) in enumerate(entries):
+            L.dml_jpeg_retarget(C.c_void_p(base + 16 + i * desc), rec.ctypes.data, hw[0], hw[1], work.data_ptr())
+            if pk not in self.packs:
+                self.packs.append(pk)
+                self.works.append(work)
+        self.desc, self.dev = desc, None
+
+    def launch(self, slots: List[int], arena: torch.Tensor, stream) -> None:
+        import ctypes as C
+
+        from .. import _native as N
+
+        L = N.lib()
+        for i, sl in enumerate(slots):
+            L.dml_jpeg_set_slot(C.c_void_p(self.buf.data_ptr()), i, int(sl))
+        with torch.cuda.stream(stream):
+            for pk, work in zip(self.packs, self.works):
+                stream.wait_event(pk.done)
+                work.record_stream(stream)   # an eviction from the cache must not free it under us
+            self.dev = torch.empty(self.used, dtype=torch.uint8, device=arena.device)
+            self.dev.copy_(self.buf[:self.used], non_blocking=True)
+            N.check(L.dml_jpeg_resize_only(self.dev.data_ptr(), len(self.names), self.hw[0], self.hw[1],
+                                           arena.data_ptr(), stream.cuda_stream), "dml_jpeg_resize_only")
+
+    def release(self) -> None:
+        self.dev = None
+        self.packs, self.works = [], []
         if self.buf is not None:
             self.be.unpin(self.buf)
             self.buf = None
@@ -557,6 +618,9 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         self._pins: List[torch.Tensor] = []                  # free pinned pack buffers
         self._jstreams: List[torch.cuda.Stream] = []         # side streams of the GPU JPEG decodes
         self._jnext = 0
+        self._planes: "OrderedDict[str, tuple]" = OrderedDict()   # name -> (descriptor, decoded window)
+        self._plane_packs: "OrderedDict[int, object]" = OrderedDict()
+        self._plane_bytes = 0
         # DML_GPU_RESIZE=0: the decode pool resizes on the CPU (Pillow) as before (A/B)
         self.gpu_resize = os.environ.get("DML_GPU_RESIZE", "1") != "0"
         # DML_GPU_JPEG=0: every JPEG decodes on the CPU (the decode workers), as before (A/B)
@@ -614,6 +678,31 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         return t
 
     JPEG_STREAMS = 4
+    PLANE_CACHE_BYTES = 4 << 30   # device work buffers of decoded windows kept for the other model
+
+    def remember_planes(self, pack: "_JpegPack", recs: Dict[str, np.ndarray]) -> None:
+        """(serve loop, after a GPU decode's launch) the window's planes serve the other
+        model's windows of the same images (planes_for); least recently decoded windows go first."""
+        with self._dlock:
+            self._plane_packs[id(pack)] = pack
+            self._plane_bytes += pack.work.numel()
+            for nm, rec in recs.items():
+                self._planes[nm] = (rec, pack)
+                self._planes.move_to_end(nm)
+            while self._plane_bytes > self.PLANE_CACHE_BYTES and self._plane_packs:
+                old_id, old = next(iter(self._plane_packs.items()))
+                del self._plane_packs[old_id]
+                self._plane_bytes -= old.work.numel()
+                for nm in [k for k, (_, pk) in self._planes.items() if pk is old]:
+                    del self._planes[nm]
+                old.work = None
+
+    def planes_for(self, names: List[str]) -> Dict[str, tuple]:
+        """(decode pool) {name: (descriptor, decoded window)} for the names a launched GPU decode
+        already holds on this device."""
+        with self._dlock:   # (descriptor, window, its work tensor: held, an eviction cannot free it)
+            return {nm: (self._planes[nm][0], self._planes[nm][1], self._planes[nm][1].work)
+                    for nm in names if nm in self._planes and self._planes[nm][1].work is not None}
 
     def jpeg_stream(self) -> torch.cuda.Stream:
         """(serve loop) the next of JPEG_STREAMS side streams for GPU JPEG decodes."""
@@ -688,9 +777,17 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         blobs = self.loader(names) if self.loader else {}
         hw = self.arenas[model].hw
         out = _PackedImages() if self.gpu_resize else {}
-        jp = None
+        jp = rp = None
         if self.gpu_jpeg:
-            # GPU decode (jpeg_decode.hip) for every baseline JPEG; the CPU decodes the rest
+            # decoded on this GPU already (the other model's window): colour + resize only
+            cached = self.planes_for([n for n in names if blobs.get(n) is not None])
+            if cached:
+                hit = [n for n in names if n in cached]
+                rp = _ResizePack(self, hit, [cached[n] for n in hit], hw)
+                for n in hit:
+                    out[n] = True
+                names = [n for n in names if n not in cached]
+            # GPU decode (jpeg_decode.hip) for every other baseline JPEG; the CPU decodes the rest
             have = [n for n in names if blobs.get(n) is not None]
             if have:
                 try:
@@ -746,7 +843,7 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         if self.gpu_resize:
             ok = [n for n in names if out.get(n) is not None]
             cpu = _Pack(self, ok, [out[n] for n in ok], hw) if ok else None
-            out.pack = _Packs([jp, cpu]) if jp is not None else cpu
+            out.pack = _Packs([rp, jp, cpu]) if (jp is not None or rp is not None) else cpu
         return out
 
     def launch(self, model, names, slot):

@@ -64,3 +64,51 @@ def test_gpu_jpeg_matches_pillow_decode_and_nearest_resize(hw):
         assert np.array_equal(got[slot_of[n]], ref), n
     assert not got[0].any() and not got[1].any()
     pack.release()
+
+
+def test_second_model_reuses_the_decoded_planes():
+    """A window of the other model over images a GPU decode already holds: colour + resize only
+    (_ResizePack: re-targeted descriptors, one launch after the decode's event), byte-identical
+    to Pillow's decode + NEAREST at that size; the plane cache evicts whole windows."""
+    from collections import OrderedDict
+    import threading
+
+    from distributed_machine_learning_amd import _native as N
+    from distributed_machine_learning_amd.parallel.rank_backend import GpuRankBackend, _ResizePack
+
+    class _Be(_Pins):
+        PLANE_CACHE_BYTES = GpuRankBackend.PLANE_CACHE_BYTES
+        remember_planes = GpuRankBackend.remember_planes
+        planes_for = GpuRankBackend.planes_for
+
+        def __init__(self):
+            self.device = torch.device("cuda")
+            self._dlock = threading.Lock()
+            self._planes, self._plane_packs, self._plane_bytes = OrderedDict(), OrderedDict(), 0
+
+    N.check(N.lib().dml_jpeg_init(), "dml_jpeg_init")
+    be = _Be()
+    files = _files()
+    names, datas = [n for n, _ in files], [d for _, d in files]
+    pack = _JpegPack(be, names, datas, (224, 224))
+    a224 = torch.zeros((len(files), 224, 224, 3), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    pack.launch(list(range(len(pack.names))), a224, stream)
+    hits = be.planes_for(names)
+    assert sorted(hits) == sorted(pack.names)
+    rp = _ResizePack(be, pack.names, [hits[n] for n in pack.names], (299, 299))
+    a299 = torch.zeros((len(pack.names), 299, 299, 3), dtype=torch.uint8, device="cuda")
+    rp.launch(list(range(len(pack.names))), a299, stream)
+    stream.synchronize()
+    got = a299.cpu().numpy()
+    blobs = dict(files)
+    for i, n in enumerate(pack.names):
+        ref = np.asarray(Image.open(io.BytesIO(blobs[n])).convert("RGB").resize((299, 299), Image.NEAREST))
+        assert np.array_equal(got[i], ref), n
+    rp.release()
+    pack.release()
+    be.PLANE_CACHE_BYTES = 0   # the next decoded window evicts this one
+    pack2 = _JpegPack(be, names[:4], datas[:4], (224, 224))
+    pack2.launch(list(range(len(pack2.names))), a224, stream)
+    stream.synchronize()
+    assert pack.work is None and be.planes_for(names[4:]) == {}
