@@ -19,6 +19,11 @@ class _Pins:   # the GpuRankBackend methods a pack uses
     def jpeg_stream(self):
         return torch.cuda.current_stream()
 
+    device = torch.device("cuda")
+
+    def remember_planes(self, pack, recs):
+        pass
+
     def pinned(self, nbytes):
         return torch.empty(nbytes, dtype=torch.uint8).pin_memory()
 

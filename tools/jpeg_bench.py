@@ -28,6 +28,11 @@ class _Pins:
         self.i = (self.i + 1) % len(self.streams)
         return self.streams[self.i]
 
+    device = torch.device("cuda")
+
+    def remember_planes(self, pack, recs):
+        pass
+
     def pinned(self, nbytes):
         return torch.empty(nbytes, dtype=torch.uint8).pin_memory()
 
