@@ -40,6 +40,8 @@
 
 struct DmljHuff {
   uint32_t look[512];   // 9-bit lookahead: (len << 8) | symbol; 0 = a longer code (32-bit: scalar loads)
+  uint32_t fast[512];   // AC only: code + extra bits within the 9-bit lookahead, decoded in one step:
+                        // (coefficient << 16) | (run << 4) | total bits; 0 = the general path
   int32_t maxcode[18];  // largest code of each length (-1: none); [17] = sentinel
   int32_t valoff[18];   // val index of a code of length l = valoff[l] + code
   uint8_t val[256];
@@ -178,6 +180,14 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_
             pred[c] += diff;
             if (writer) blk[0] = (int16_t)pred[c];
             for (int k = 1; k < 64; ++k) {
+              b.fill();
+              const uint32_t f = act.fast[b.peek(9)];
+              if (f) {   // the common short code with a small coefficient: one lookup, one skip
+                b.skip(f & 15);
+                k += (f >> 4) & 15;
+                if (writer) blk[k < 64 ? k : 63] = (int16_t)((int32_t)f >> 16);
+                continue;
+              }
               const int rs = huff_decode(b, act);
               const int r = rs >> 4, sz = rs & 15;
               if (sz) {
@@ -423,6 +433,14 @@ static int build_huff(const uint8_t* counts, const uint8_t* vals, int nvals, Dml
   }
   t.maxcode[17] = 0x7fffffff;
   memcpy(t.val, vals, nvals < 256 ? nvals : 256);
+  for (int i = 0; i < 512; ++i) {   // fast AC entries (harmless, unused, for DC tables)
+    const uint32_t e = t.look[i];
+    const int len = (int)(e >> 8), sym = (int)(e & 255), run = sym >> 4, size = sym & 15;
+    if (!e || size == 0 || len + size > 9) continue;
+    const int extra = (i >> (9 - len - size)) & ((1 << size) - 1);
+    const int v = extend(extra, size);
+    t.fast[i] = (uint32_t)((int32_t)v * 65536) | (uint32_t)(run << 4) | (uint32_t)(len + size);
+  }
   return 0;
 }
 

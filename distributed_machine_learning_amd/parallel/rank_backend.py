@@ -677,7 +677,7 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             t = self._nn[(n_in, n_out)] = nearest_index(n_in, n_out)
         return t
 
-    JPEG_STREAMS = 4
+    JPEG_STREAMS = 8
     PLANE_CACHE_BYTES = 4 << 30   # device work buffers of decoded windows kept for the other model
 
     def remember_planes(self, pack: "_JpegPack", recs: Dict[str, np.ndarray]) -> None:
