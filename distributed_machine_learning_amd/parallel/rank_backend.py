@@ -665,6 +665,12 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             # up the serve loop's launches for 20-50 ms
             self._pins = [torch.empty(self.PIN_BYTES, dtype=torch.uint8).pin_memory()
                           for _ in range(self.PIN_PREALLOC)]
+            if self.gpu_jpeg:
+                # and the device work buffers of the GPU decodes: one block the caching allocator
+                # keeps and splits, so no window allocates device memory from the driver mid-pass
+                # (each hipMalloc also stalls the serve loop's HIP calls)
+                reserve = torch.empty(self.PLANE_CACHE_BYTES + (512 << 20), dtype=torch.uint8, device=device)
+                del reserve
 
     DECODE_CACHE_BYTES = 1 << 30
     DECODE_CHUNK = 8
