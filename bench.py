@@ -38,6 +38,12 @@ import subprocess
 import sys
 import time
 
+# one HIP hardware queue per stream (HIP's default is 4 per process): streams sharing a queue run
+# in order, so a multi-millisecond JPEG Huffman launch on a side stream held up the compute
+# stream mapped to the same queue (rocprofv3, profiles/r5_store). Set before HIP initialises;
+# DML_HW_QUEUES overrides.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("DML_HW_QUEUES", "16")
+
 # the reference's only per-N rates: the scheduler cost model's predicted query
 # rate n * batch / time(batch) at batch 10 (worker.py:316-317, models.py:128-139,
 # constants worker.py:57-84; BASELINE.md row "Scheduler-predicted query rate").

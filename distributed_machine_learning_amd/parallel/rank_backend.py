@@ -459,6 +459,12 @@ class _JpegPack:
         # the device work buffer now (coefficients, then the sample planes the other model's
         # window re-uses: GpuRankBackend.planes_for)
         self.work = torch.empty(max(self.work_bytes, 256), dtype=torch.uint8, device=backend.device)
+        # the stream `work` was allocated on (this pool thread's): the side stream waits on this
+        # event only - waiting on the serve loop's current stream (the staging stream, which has
+        # waited on every earlier window's decode) chained all decodes one after the other
+        # (rocprofv3: 400 Huffman launches on 8 queues, zero overlap, profiles/r5_store)
+        self.alloc_ev = torch.cuda.Event()
+        self.alloc_ev.record(torch.cuda.current_stream(backend.device))
 
     def launch(self, slots: List[int], arena: torch.Tensor, stream) -> None:
         import ctypes as C
@@ -472,10 +478,13 @@ class _JpegPack:
         # on a side stream of its own: the serial Huffman decode of one window (one wave per
         # image, milliseconds) overlaps the next windows' instead of queueing behind it on the
         # staging stream, which only waits for it before the window's event
-        # (no wait on `stream`: it has waited on the previous windows' decodes, which would chain
-        # them again; nothing before this on `stream` touches this window's slots or buffers)
+        # (no wait on `stream` - the current stream here: it has waited on the previous windows'
+        # decodes, which would chain them again; nothing before this on `stream` touches this
+        # window's slots or buffers)
         side = self.be.jpeg_stream()
-        side.wait_stream(torch.cuda.current_stream())   # `work` was allocated on the pool thread's stream
+        side.wait_event(self.alloc_ev)
+        for ev in getattr(self, "after", ()):   # image_store: earlier windows writing these slots
+            side.wait_event(ev)
         with torch.cuda.stream(side):
             self.dev = torch.empty(self.used, dtype=torch.uint8, device=arena.device)
             self.dev.copy_(self.buf[:self.used], non_blocking=True)
@@ -564,6 +573,7 @@ class _Packs:
     def launch(self, slots: List[int], arena: torch.Tensor, stream) -> None:
         o = 0
         for p in self.packs:
+            p.after = getattr(self, "after", [])
             p.launch(slots[o:o + len(p.names)], arena, stream)
             o += len(p.names)
 

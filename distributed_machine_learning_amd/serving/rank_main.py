@@ -43,6 +43,12 @@ import subprocess
 import sys
 import time
 
+# one HIP hardware queue per stream (HIP's default is 4 per process): streams sharing a queue run
+# in order, so a multi-millisecond JPEG Huffman launch on a side stream held up the compute
+# stream mapped to the same queue (rocprofv3, profiles/r5_store). Set before HIP initialises;
+# DML_HW_QUEUES overrides.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("DML_HW_QUEUES", "16")
+
 log = logging.getLogger(__name__)
 
 

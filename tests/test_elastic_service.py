@@ -377,6 +377,34 @@ def test_hbm_image_store_window_pinning_and_eviction():
     assert failed == [] and st.arena[slots].numpy()[:, 0, 0, 0].tolist() == [5, 3]
 
 
+def test_hbm_image_store_windows_issue_ahead_but_never_overtake_a_slot_writer():
+    """Windows are issued as soon as their decode is in (GPU: the JPEG decodes of several
+    windows overlap on side streams); a window re-using the slot of an evicted image whose
+    window has not finished lists that window as a dependency (its decode waits on it); a
+    host arena still issues in order (its scatter happens at the finish)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    import torch
+
+    from distributed_machine_learning_amd.parallel.image_store import HbmImageStore
+
+    st = HbmImageStore(3, (1, 1), torch.device("cpu"), n_synth=0)
+    st.loader = lambda names: {n: np.full((1, 1, 3), int(n[0]), np.uint8) for n in names}
+    st.stager.attach(0, 1, ThreadPoolExecutor(1), None)
+    w1 = st.plan(["1a", "2a"], 0)
+    w2 = st.plan(["3a"], 0)
+    w3 = st.plan(["4a"], 0)            # evicts 1a (idle: never pinned) while w1 is unfinished
+    assert st.evictions == 1 and w3.slots[0] == w1.slots[0]
+    assert w3.deps == [w1] and w2.deps == [] and w1.deps == []
+    while not w3.done:
+        assert not (w2.work is not None and not w1.done)   # host arena: in-order issue
+        st.stager.progress()
+    assert st.arena[w3.slots[0]].numpy()[0, 0, 0] == 4 and not st.stager.queue
+    w4 = st.plan(["5a"], 0)            # its slot's writer finished: no dependency
+    assert w4.deps == []
+
+
 def test_hbm_image_store_plan_cost_is_independent_of_resident_images():
     """plan() at 51,200 resident images costs what it costs at 512 (the eviction candidates
     are kept incrementally; a whole-index scan per batch made 258 ms serve-loop steps on the
