@@ -419,7 +419,7 @@ class ReplicatedCoordinator:
         return h[-n:] if n > 0 else []
 
 
-STAGE_DEPTH = 8  # batches per rank whose images are staged ahead of dispatch (image windows)
+STAGE_DEPTH = int(os.environ.get("DML_STAGE_DEPTH", "8"))  # batches per rank whose images are staged ahead of dispatch (image windows)
 
 
 def rank_switch_interval() -> None:
