@@ -78,7 +78,16 @@ def test_rank_launcher_cpu_backend_config1(tmp_path):
             job = int(out["submit"].split("submitted job ")[1].split()[0])
             out["wait"] = await cli.run_line(f"wait-job {job} 240")
             out["get"] = await cli.run_line(f"get-output {job}")
-            out["c1"] = await cli.run_line("C1")
+            # the rank's metrics follow the completions its control loop applies (a relayed
+            # transition, not the job table the wait reads): poll C1 a little under load
+            for _ in range(40):
+                out["c1"] = await cli.run_line("C1")
+                try:
+                    if json.loads(out["c1"].split("\n[")[0])["ResNet50"]["query_count"] == N_IMAGES:
+                        break
+                except (ValueError, KeyError):
+                    pass
+                await asyncio.sleep(0.25)
             await client.stop()
             return job, out
         job, out = asyncio.run(run())
