@@ -222,6 +222,7 @@ int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long maxstream, 
                            void* arena, hipStream_t s);
 int dml_jpeg_init(void);
 long dml_jpeg_desc_size(void);
+long dml_jpeg_head_size(void);
 void dml_jpeg_retarget(void* dst, const void* src, int outH, int outW, long base);
 int dml_jpeg_resize_only(const void* dbuf, int n, int H, int W, void* arena, hipStream_t s);
 int dml_jpeg_decode_host(const unsigned char* data, long len, unsigned char* out, int* hw);

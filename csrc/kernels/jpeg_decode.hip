@@ -714,7 +714,7 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
 // dml_jpeg_resize_only — the image is decoded once for both models
 extern "C" void dml_jpeg_retarget(void* dst, const void* src, int outH, int outW, long base) {
   DmljImage* d = (DmljImage*)dst;
-  memcpy(d, src, sizeof(DmljImage));
+  memcpy(d, src, offsetof(DmljImage, q));   // the colour + resize kernel reads nothing past it
   if (!d->ok || outH <= 0 || outW <= 0 || outH > DMLJ_MAXOUT || outW > DMLJ_MAXOUT) {
     d->ok = 0;
     return;
@@ -743,6 +743,10 @@ extern "C" int dml_jpeg_resize_only(const void* dbuf, int n, int H, int W, void*
 extern "C" int dml_jpeg_init(void) { return 0; }   // nothing to set up (kept for the backend's init order)
 
 extern "C" long dml_jpeg_desc_size(void) { return (long)sizeof(DmljImage); }
+
+// the descriptor's leading part a re-target needs (geometry, plane offsets, NEAREST tables): the
+// plane cache keeps only this much per image
+extern "C" long dml_jpeg_head_size(void) { return (long)offsetof(DmljImage, q); }
 
 // CPU decode with the same code (tests): full-resolution RGB into out (h*w*3); 0 = ok,
 // -1 = unsupported (the CPU workers' path)

@@ -132,6 +132,7 @@ _SIGS = {
     "dml_jpeg_retarget": (None, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_long]),
     "dml_jpeg_resize_only": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "dml_jpeg_desc_size": (C.c_long, []),
+    "dml_jpeg_head_size": (C.c_long, []),
     "dml_jpeg_decode_host": (C.c_int, [C.c_char_p, C.c_long, C.c_void_p, C.POINTER(C.c_int)]),
     "dml_plan_create": (C.c_void_p, []),
     "dml_plan_destroy": (None, [C.c_void_p]),
