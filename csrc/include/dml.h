@@ -199,13 +199,6 @@ int dml_conv_ws_init(void);
 int dml_conv_wsp(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_wsp_bn(int cfg);
 int dml_conv_wsp_init(void);
-// patch-stationary stride-1 implicit GEMM (conv_igemm_pt.hip; cfg ids 140..159): the activation
-// patch of an M tile (whole output rows / images) is DMA'd once per channel chunk and read
-// at a per-tap offset; refuses convs it cannot run (stride / dilation != 1, Cin % BK, split-K)
-int dml_conv_pt(const DmlConvArgs* a, int cfg, hipStream_t s);
-int dml_conv_pt_bn(int cfg);
-int dml_conv_pt_fits(const DmlConvArgs* a, int cfg);
-int dml_conv_pt_init(void);
 // row-ring 3x3 convolution of ResNet50 stage 2 (conv_rowring.hip; cfg ids 150..152 = 2 / 1 / 4
 // strips per image): weights LDS-resident, input rows streamed through a 10-row ring; refuses
 // anything but 3x3 pad 1 stride 1, Cin 64, Cout <= 64, width 56

@@ -6,8 +6,7 @@
 // models.py:26,51 — it has no kernel of its own). cfg ids 10..63 select a v2
 // tile configuration (dml_conv_v2), ids 100..119 a warp-specialised one (loader +
 // MFMA waves, dml_conv_ws, conv_igemm_ws.hip), ids 120..139 its persistent form
-// (dml_conv_wsp, conv_igemm_wsp.hip), ids 140..159 the patch-stationary stride-1 tiles
-// (dml_conv_pt, conv_igemm_pt.hip), ids 150..152 the row-ring 3x3 kernel of ResNet50 stage 2
+// (dml_conv_wsp, conv_igemm_wsp.hip), ids 150..152 the row-ring 3x3 kernel of ResNet50 stage 2
 // (dml_conv_rr, conv_rowring.hip); they are part of the ABI the plan builder and the
 // autotuner (ops/tuning.py) use.
 //
@@ -18,7 +17,9 @@
 // never picked by the cold tuner, profiles/r3_v2/shift_vs_igemm.json) and the
 // persistent weight-stationary 1x1 kernel (cfg 84..90, r4, commit f96f4b1: parity at
 // best, profiles/r4_probes/ws) and the Winograd F(2x2, 3x3) kernel (cfg 80..83, r4,
-// removed in r5: slower than the direct tiles on every shape, profiles/r4_wino).
+// removed in r5: slower than the direct tiles on every shape, profiles/r4_wino) and the
+// patch-stationary stride-1 tiles (cfg 140..149, r5: slower on every shape, profiles/r5_ws;
+// removed in r6).
 #include "common.h"
 #include "dml.h"
 #include "pool_shared.h"
@@ -27,7 +28,7 @@ static int validate(const DmlConvArgs* a, int cfg) {
   const int bn = dml_conv_v2_bn(cfg);
   if (bn <= 0) {
     dml_set_error("dml_conv: cfg must be a tile config (v2: 10..63, warp-specialised: 100..119, persistent: "
-                  "120..139, patch-stationary: 140..149, row-ring: 150..152)");
+                  "120..139, row-ring: 150..152)");
     return -1;
   }
   // weights are packed with Cout padded to a multiple of 256 rows; a 96- or
@@ -58,7 +59,6 @@ static int validate(const DmlConvArgs* a, int cfg) {
 extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
   if (validate(a, cfg) != 0) return -1;
   if (cfg >= 150) return dml_conv_rr(a, cfg, s);
-  if (cfg >= 140) return dml_conv_pt(a, cfg, s);
   if (cfg >= 120) return dml_conv_wsp(a, cfg, s);
   return cfg >= 100 ? dml_conv_ws(a, cfg, s) : dml_conv_v2(a, cfg, s);
 }

@@ -486,7 +486,6 @@ extern "C" int dml_conv_v2_init(void) {
   if (!rc && dml_chain_init() != 0) return -1;  // chained block-boundary kernels (expand_reduce_chain.hip)
   if (!rc && dml_conv_ws_init() != 0) return -1;  // warp-specialised tiles (conv_igemm_ws.hip)
   if (!rc && dml_conv_wsp_init() != 0) return -1;  // persistent warp-specialised tiles (conv_igemm_wsp.hip)
-  if (!rc && dml_conv_pt_init() != 0) return -1;   // patch-stationary stride-1 tiles (conv_igemm_pt.hip)
   if (!rc && dml_conv_rr_init() != 0) return -1;   // row-ring 3x3 kernel (conv_rowring.hip)
   return rc ? -1 : 0;
 }
@@ -506,7 +505,6 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
 // tiles of conv_igemm_ws.hip, 120..139 their persistent form (conv_igemm_wsp.hip)
 extern "C" int dml_conv_v2_bn(int cfg) {
   if (cfg >= 150) return cfg <= 152 ? 64 : 0;  // row-ring 3x3 kernel (conv_rowring.hip)
-  if (cfg >= 140) return dml_conv_pt_bn(cfg);
   if (cfg >= 120) return dml_conv_wsp_bn(cfg);
   if (cfg >= 100) return dml_conv_ws_bn(cfg);
   if (cfg < 10) return 0;

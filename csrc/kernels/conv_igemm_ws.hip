@@ -75,16 +75,7 @@ struct Cfg {
   static_assert(LDS <= 163840, "LDS");
 };
 
-// PF (fragment prefetch): the MFMA waves read tile kt+1's fragments while their MFMAs of
-// tile kt run, so the LDS read latency is off the matrix pipe's critical path (with one
-// MFMA wave per SIMD no other wave covers it). Barrier b then publishes tile b+1: the
-// loaders' wait before it retires one tile more, and every MFMA wave retires its
-// outstanding fragment reads (lgkmcnt(0)) before arriving, so the stage it read is free for
-// the refill issued after the barrier. PF 1: a whole second register set (tile kt+1's two
-// k-steps); PF 2 (BK 64, 64x64 wave tiles, where two whole sets spill): only tile kt+1's
-// first k-step is read ahead — behind tile kt's second k-step — and a tile's second k-step
-// is read behind its own first one (three half sets).
-template <int BM, int BN, int WM, int WN, int NL, int STAGES, bool RES, int BK, bool LATE, int PF = 0>
+template <int BM, int BN, int WM, int WN, int NL, int STAGES, bool RES, int BK, bool LATE>
 __device__ __forceinline__ void conv_ws_tile(const DmlConvArgs& a, int Lb, int nblk) {
   using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK>;
   using RW = typename T::R;
@@ -195,22 +186,11 @@ __device__ __forceinline__ void conv_ws_tile(const DmlConvArgs& a, int Lb, int n
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
       if (s < nk) issue(s, s);
-    if constexpr (PF == 0) {
-      for (int kt = 0; kt < nk; ++kt) {
-        if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * T::L>();
-        else wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();  // tile kt published to the MFMA waves
-        if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
-      }
-    } else {
-      // barrier b (b = -1 .. nk-2) publishes tile b+1; tiles <= b have been read
-      for (int b = -1; b < nk - 1; ++b) {
-        const int issued = min(nk, STAGES + b);  // tiles issued before this wait
-        if (issued - (b + 2) == STAGES - 2) wait_vmcnt<(STAGES - 2) * T::L>();
-        else wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
-        if (STAGES + b < nk) issue(STAGES + b, (STAGES + b) % STAGES);
-      }
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * T::L>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();  // tile kt published to the MFMA waves
+      if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     }
   } else {
     // ======================= MFMA wave =======================
@@ -240,80 +220,11 @@ __device__ __forceinline__ void conv_ws_tile(const DmlConvArgs& a, int Lb, int n
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     };
-    if constexpr (PF == 0) {
-      for (int kt = 0; kt < nk; ++kt) {
-        __builtin_amdgcn_s_barrier();  // tile kt landed (loaders' vmcnt), stage kt-1 free for the refill
-        bf16x8 fa[KSM][T::FI], fb[KSM][T::FJ];
-        read(kt, fa, fb);
-        mfma(fa, fb);
-      }
-    } else if constexpr (PF == 2) {
-      static_assert(KSM == 2, "PF 2: two 32-deep k-steps per K tile");
-      auto read1 = [&](int kt, int ks, bf16x8(&fa)[T::FI], bf16x8(&fb)[T::FJ]) __attribute__((always_inline)) {
-        const char* sx = smem + (kt % STAGES) * T::STAGE_BYTES;
-        const char* sw = sx + BM * T::ROWB;
-        const int ch = ks * 4 + fq;
-#pragma unroll
-        for (int i = 0; i < T::FI; ++i) fa[i] = *(const bf16x8*)(sw + RW::off(wc * T::WTC + i * 16 + frow, ch));
-#pragma unroll
-        for (int j = 0; j < T::FJ; ++j) fb[j] = *(const bf16x8*)(sx + RW::off(wp * T::WTP + j * 16 + frow, ch));
-      };
-      auto mfma1 = [&](bf16x8(&fa)[T::FI], bf16x8(&fb)[T::FJ]) __attribute__((always_inline)) {
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < T::FI; ++i)
-#pragma unroll
-          for (int j = 0; j < T::FJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      };
-      // k-step 0 of even / odd tiles, k-step 1 of the current tile
-      bf16x8 ae[T::FI], be[T::FJ], ao[T::FI], bo[T::FJ], a1[T::FI], b1[T::FJ];
-      if (nk > 0) {
-        __builtin_amdgcn_s_barrier();  // barrier -1: tile 0 published
-        read1(0, 0, ae, be);
-      }
-      for (int kt = 0; kt < nk; kt += 2) {
-        read1(kt, 1, a1, b1);
-        mfma1(ae, be);
-        if (kt + 1 < nk) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile kt fully read: its stage may refill
-          __builtin_amdgcn_s_barrier();                        // barrier kt: tile kt+1 published
-          read1(kt + 1, 0, ao, bo);
-        }
-        mfma1(a1, b1);
-        if (kt + 1 >= nk) break;
-        read1(kt + 1, 1, a1, b1);
-        mfma1(ao, bo);
-        if (kt + 2 < nk) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          read1(kt + 2, 0, ae, be);
-        }
-        mfma1(a1, b1);
-      }
-    } else {
-      // two named register sets (static indexing: a runtime-indexed set would go to scratch)
-      bf16x8 fa0[KSM][T::FI], fb0[KSM][T::FJ], fa1[KSM][T::FI], fb1[KSM][T::FJ];
-      if (nk > 0) {
-        __builtin_amdgcn_s_barrier();  // barrier -1: tile 0 published
-        read(0, fa0, fb0);
-      }
-      for (int kt = 0; kt < nk; kt += 2) {
-        if (kt + 1 < nk) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile kt's reads retired: its stage may refill
-          __builtin_amdgcn_s_barrier();                        // barrier kt: tile kt+1 published
-          read(kt + 1, fa1, fb1);
-        }
-        mfma(fa0, fb0);
-        if (kt + 1 >= nk) break;
-        if (kt + 2 < nk) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          read(kt + 2, fa0, fb0);
-        }
-        mfma(fa1, fb1);
-      }
+    for (int kt = 0; kt < nk; ++kt) {
+      __builtin_amdgcn_s_barrier();  // tile kt landed (loaders' vmcnt), stage kt-1 free for the refill
+      bf16x8 fa[KSM][T::FI], fb[KSM][T::FJ];
+      read(kt, fa, fb);
+      mfma(fa, fb);
     }
   }
 
@@ -322,32 +233,32 @@ __device__ __forceinline__ void conv_ws_tile(const DmlConvArgs& a, int Lb, int n
   epi.template store<16, T::FI, T::FJ, T::WTP, T::WTC>(a, smem, acc, wp, wc, lane, tid, wid < T::NC);
 }
 
-template <int BM, int BN, int WM, int WN, int NL, int STAGES, bool RES, int BK, bool LATE, int W, int PF>
+template <int BM, int BN, int WM, int WN, int NL, int STAGES, bool RES, int BK, bool LATE, int W>
 __global__ __launch_bounds__((WM * WN + NL) * 64, W) void conv_ws_kernel(DmlConvArgs a) {
-  conv_ws_tile<BM, BN, WM, WN, NL, STAGES, RES, BK, LATE, PF>(a, xcd_remap(blockIdx.x, gridDim.x), gridDim.x);
+  conv_ws_tile<BM, BN, WM, WN, NL, STAGES, RES, BK, LATE>(a, xcd_remap(blockIdx.x, gridDim.x), gridDim.x);
 }
 
-template <int BM, int BN, int WM, int WN, int NL, int STAGES, int BK, bool LATE, int W, int PF>
+template <int BM, int BN, int WM, int WN, int NL, int STAGES, int BK, bool LATE, int W>
 static int launch(const DmlConvArgs* a, hipStream_t s) {
   using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK>;
   const long M = (long)a->N * a->Ho * a->Wo;
   const long tiles = ((M + BM - 1) / BM) * ((a->Cout + BN - 1) / BN) * (a->ksplit > 1 ? a->ksplit : 1);
   if (a->res)
-    hipLaunchKernelGGL((conv_ws_kernel<BM, BN, WM, WN, NL, STAGES, true, BK, LATE, W, PF>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((conv_ws_kernel<BM, BN, WM, WN, NL, STAGES, true, BK, LATE, W>), dim3((unsigned)tiles),
                        dim3(T::NT), T::LDS, s, *a);
   else
-    hipLaunchKernelGGL((conv_ws_kernel<BM, BN, WM, WN, NL, STAGES, false, BK, false, W, PF>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((conv_ws_kernel<BM, BN, WM, WN, NL, STAGES, false, BK, false, W>), dim3((unsigned)tiles),
                        dim3(T::NT), T::LDS, s, *a);
   DML_CHECK_LAUNCH();
   return 0;
 }
 
-template <int BM, int BN, int WM, int WN, int NL, int STAGES, int BK, bool LATE, int W, int PF>
+template <int BM, int BN, int WM, int WN, int NL, int STAGES, int BK, bool LATE, int W>
 static int set_attr() {
   using T = Cfg<BM, BN, WM, WN, NL, STAGES, BK>;
-  return (int)hipFuncSetAttribute((const void*)conv_ws_kernel<BM, BN, WM, WN, NL, STAGES, true, BK, LATE, W, PF>,
+  return (int)hipFuncSetAttribute((const void*)conv_ws_kernel<BM, BN, WM, WN, NL, STAGES, true, BK, LATE, W>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS) |
-         (int)hipFuncSetAttribute((const void*)conv_ws_kernel<BM, BN, WM, WN, NL, STAGES, false, BK, false, W, PF>,
+         (int)hipFuncSetAttribute((const void*)conv_ws_kernel<BM, BN, WM, WN, NL, STAGES, false, BK, false, W>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
 }
 
@@ -356,35 +267,29 @@ static int set_attr() {
 
 // Warp-specialised tile configurations: id, BM (pixels), BN (channels), WM x WN MFMA
 // waves, NL loader waves, ring STAGES, BK, RL (residual loaded in the epilogue), W (min
-// waves/SIMD register hint), PF (fragment prefetch). Ids 100..139 are part of the plan-builder / tuner ABI
+// waves/SIMD register hint). The fragment-prefetch forms (113..118, r5) never beat their bases
+// and were removed in r6. Ids 100..139 are part of the plan-builder / tuner ABI
 // (ops/tuning.py WS_CFGS); validated by dml_conv (conv_dispatch.hip).
 #define DML_WS_TILES(X)                                                                         \
-  X(100, 128, 128, 2, 2, 4, 3, 64, 0, 1, 0)  /* 4 MFMA (64x64) + 4 loaders, 96 KiB, 1 WG/CU */      \
-  X(101, 128, 128, 2, 2, 2, 4, 32, 0, 1, 0)  /* 4 + 2, BK32 4-stage, 64 KiB: 2 WG/CU */             \
-  X(102, 256, 128, 4, 2, 4, 3, 64, 1, 1, 0)  /* 8 + 4, 144 KiB (residual form: late, else it spills) */ \
-  X(103, 128, 64, 2, 2, 2, 3, 64, 0, 1, 0)   /* 4 (64px x 32ch) + 2, 72 KiB: 2 WG/CU */             \
-  X(104, 64, 128, 1, 4, 2, 3, 64, 0, 1, 0)   /* 4 (64px x 32ch) + 2, 72 KiB: 2 WG/CU */             \
-  X(105, 256, 64, 4, 1, 4, 3, 64, 0, 1, 0)   /* 4 (64x64) + 4, 120 KiB */                           \
-  X(106, 128, 128, 2, 2, 4, 4, 64, 0, 1, 0)  /* 4 + 4, 128 KiB */                                   \
-  X(107, 256, 128, 4, 2, 4, 4, 32, 0, 1, 0)  /* 8 + 4, BK32 4-stage, 96 KiB */                      \
-  X(108, 128, 256, 2, 4, 4, 3, 64, 1, 1, 0)  /* 8 + 4, 144 KiB (residual form: late) */           \
-  X(109, 128, 64, 2, 2, 2, 4, 32, 0, 1, 0)   /* 4 + 2, BK32 4-stage, 48 KiB: 3 WG/CU */             \
-  X(110, 64, 128, 1, 4, 2, 4, 32, 0, 1, 0)   /* 4 + 2, BK32 4-stage, 48 KiB: 3 WG/CU */             \
-  X(111, 128, 128, 2, 2, 2, 3, 64, 0, 1, 0)  /* 4 + 2, 96 KiB */                                    \
-  X(112, 128, 128, 2, 2, 4, 2, 64, 0, 1, 0)  /* 4 + 4, 2-stage, 64 KiB: 2 WG/CU */                  \
-  /* PF: fragment prefetch (second register set), the 1-MFMA-wave-per-SIMD tiles */              \
-  X(113, 128, 128, 2, 2, 4, 3, 64, 0, 1, 2)  /* = 100 + PF 2 */                                  \
-  X(114, 128, 128, 2, 2, 4, 4, 64, 0, 1, 2)  /* = 106 + PF 2 */                                  \
-  X(115, 256, 64, 4, 1, 4, 3, 64, 0, 1, 2)   /* = 105 + PF 2 */                                  \
-  X(116, 64, 128, 1, 4, 2, 3, 64, 0, 1, 1)   /* = 104 + PF */                                    \
-  X(117, 128, 64, 2, 2, 2, 3, 64, 0, 1, 1)   /* = 103 + PF */                                    \
-  X(118, 128, 128, 2, 2, 2, 4, 32, 0, 1, 1)  /* = 101 + PF */                                    \
-  X(119, 256, 128, 4, 2, 4, 6, 32, 1, 1, 0)  /* 8 + 4, BK32 6-stage, 144 KiB: 5 tiles in flight */
+  X(100, 128, 128, 2, 2, 4, 3, 64, 0, 1)  /* 4 MFMA (64x64) + 4 loaders, 96 KiB, 1 WG/CU */      \
+  X(101, 128, 128, 2, 2, 2, 4, 32, 0, 1)  /* 4 + 2, BK32 4-stage, 64 KiB: 2 WG/CU */             \
+  X(102, 256, 128, 4, 2, 4, 3, 64, 1, 1)  /* 8 + 4, 144 KiB (residual form: late, else it spills) */ \
+  X(103, 128, 64, 2, 2, 2, 3, 64, 0, 1)   /* 4 (64px x 32ch) + 2, 72 KiB: 2 WG/CU */             \
+  X(104, 64, 128, 1, 4, 2, 3, 64, 0, 1)   /* 4 (64px x 32ch) + 2, 72 KiB: 2 WG/CU */             \
+  X(105, 256, 64, 4, 1, 4, 3, 64, 0, 1)   /* 4 (64x64) + 4, 120 KiB */                           \
+  X(106, 128, 128, 2, 2, 4, 4, 64, 0, 1)  /* 4 + 4, 128 KiB */                                   \
+  X(107, 256, 128, 4, 2, 4, 4, 32, 0, 1)  /* 8 + 4, BK32 4-stage, 96 KiB */                      \
+  X(108, 128, 256, 2, 4, 4, 3, 64, 1, 1)  /* 8 + 4, 144 KiB (residual form: late) */           \
+  X(109, 128, 64, 2, 2, 2, 4, 32, 0, 1)   /* 4 + 2, BK32 4-stage, 48 KiB: 3 WG/CU */             \
+  X(110, 64, 128, 1, 4, 2, 4, 32, 0, 1)   /* 4 + 2, BK32 4-stage, 48 KiB: 3 WG/CU */             \
+  X(111, 128, 128, 2, 2, 2, 3, 64, 0, 1)  /* 4 + 2, 96 KiB */                                    \
+  X(112, 128, 128, 2, 2, 4, 2, 64, 0, 1)  /* 4 + 4, 2-stage, 64 KiB: 2 WG/CU */                  \
+  X(119, 256, 128, 4, 2, 4, 6, 32, 1, 1)  /* 8 + 4, BK32 6-stage, 144 KiB: 5 tiles in flight */
 
 extern "C" int dml_conv_ws_init(void) {
   using namespace dml::ws;
   int rc = 0;
-#define DML_SET(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PF) rc |= set_attr<BM, BN, WM, WN, NL, ST, BK, RL, W, PF>();
+#define DML_SET(id, BM, BN, WM, WN, NL, ST, BK, RL, W) rc |= set_attr<BM, BN, WM, WN, NL, ST, BK, RL, W>();
   DML_WS_TILES(DML_SET)
 #undef DML_SET
   if (rc) dml_set_error("dml_conv_ws_init: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
@@ -394,8 +299,8 @@ extern "C" int dml_conv_ws_init(void) {
 extern "C" int dml_conv_ws(const DmlConvArgs* a, int cfg, hipStream_t s) {
   using namespace dml::ws;
   switch (cfg) {
-#define DML_CASE(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PF) \
-  case id: return launch<BM, BN, WM, WN, NL, ST, BK, RL, W, PF>(a, s);
+#define DML_CASE(id, BM, BN, WM, WN, NL, ST, BK, RL, W) \
+  case id: return launch<BM, BN, WM, WN, NL, ST, BK, RL, W>(a, s);
     DML_WS_TILES(DML_CASE)
 #undef DML_CASE
     default: dml_set_error("dml_conv_ws: bad cfg"); return -1;
@@ -405,7 +310,7 @@ extern "C" int dml_conv_ws(const DmlConvArgs* a, int cfg, hipStream_t s) {
 // channel-tile width of a warp-specialised config (0: not one)
 extern "C" int dml_conv_ws_bn(int cfg) {
   switch (cfg) {
-#define DML_CASE(id, BM, BN, WM, WN, NL, ST, BK, RL, W, PF) \
+#define DML_CASE(id, BM, BN, WM, WN, NL, ST, BK, RL, W) \
   case id: return BN;
     DML_WS_TILES(DML_CASE)
 #undef DML_CASE

@@ -26,6 +26,13 @@
 // scan, grayscale or YCbCr 4:2:0 / 4:4:4, no restart markers. Anything else (progressive,
 // 4:2:2, restart intervals, Adobe RGB / CMYK, arithmetic coding, > 60 KiB of entropy data) is
 // reported unsupported and takes the CPU decode workers.
+//
+// Acknowledgement: byte-exactness with Pillow requires the arithmetic of the Independent JPEG
+// Group's libjpeg, which Pillow links. The islow IDCT below (jidctint.c), the h2v2 "fancy"
+// upsampling and its edge rules (jdsample.c) and the YCbCr->RGB fixed-point tables (jdcolor.c)
+// re-implement that arithmetic. This software is based in part on the work of the Independent
+// JPEG Group (libjpeg, Copyright (C) 1991-1998, Thomas G. Lane; IJG license). The Huffman
+// decoder, the lookup tables, the descriptor layout and the kernels are this project's own.
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>

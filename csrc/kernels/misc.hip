@@ -356,9 +356,9 @@ __global__ __launch_bounds__(1024) void index_fetch_kernel(const int* __restrict
 
 // A staged window's decoded images (full resolution, packed) -> their arena slots, resized
 // nearest-neighbour on the GPU (the store path's CPU decode pool only entropy-decodes; the two
-// per-model resizes were 43 % of its CPU per image). pack: n records {src byte offset, h, w,
-// row-table offset (int16 entries), column-table offset, slot} (int32), then the int16 source
-// row / column tables (computed on the host with Pillow's own float64 accumulation, so the
+// per-model resizes were 43 % of its CPU per image). pack: n records {src offset in 16-byte units
+// (a pack may exceed 2 GiB: ADVICE r5), h, w, row-table offset, column-table offset, slot} (int32),
+// then the int32 source row / column tables (computed on the host with Pillow's own float64 accumulation, so the
 // result is byte-identical to Image.resize(NEAREST)), then the RGB pixels. One workgroup per
 // (output row, image); dst = arena [slots][H][W][3].
 __global__ __launch_bounds__(256) void resize_nearest_kernel(const unsigned char* __restrict__ pack, int n, int H,
@@ -366,12 +366,13 @@ __global__ __launch_bounds__(256) void resize_nearest_kernel(const unsigned char
   const int y = blockIdx.x, i = blockIdx.y;
   if (i >= n || y >= H) return;
   const int* rec = (const int*)pack + i * 6;
-  const int off = rec[0], w = rec[2], yt = rec[3], xt = rec[4], slot = rec[5];
-  const short* tab = (const short*)(pack + (size_t)n * 24);
+  const size_t off = (size_t)(unsigned)rec[0] << 4;
+  const int w = rec[2], yt = rec[3], xt = rec[4], slot = rec[5];
+  const int* tab = (const int*)(pack + (size_t)n * 24);
   const unsigned char* srow = pack + off + (size_t)tab[yt + y] * w * 3;
   unsigned char* drow = dst + ((size_t)slot * H + y) * W * 3;
   for (int x = threadIdx.x; x < W; x += blockDim.x) {
-    const unsigned char* p = srow + tab[xt + x] * 3;
+    const unsigned char* p = srow + (size_t)tab[xt + x] * 3;
     drow[x * 3] = p[0];
     drow[x * 3 + 1] = p[1];
     drow[x * 3 + 2] = p[2];

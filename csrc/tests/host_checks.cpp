@@ -107,24 +107,6 @@ int main() {
   CHECK(std::string(dml_last_error()).find("tile config") != std::string::npos);
   CHECK(dml_conv_v2_bn(100) == 128 && dml_conv_v2_bn(103) == 64 && dml_conv_v2_bn(120) == 64 &&
         dml_conv_v2_bn(122) == 128);
-  // patch-stationary tiles (conv_igemm_pt.hip): channel widths, and which convs they take (host code)
-  CHECK(dml_conv_v2_bn(140) == 128 && dml_conv_v2_bn(141) == 64 && dml_conv_v2_bn(144) == 64 && dml_conv_v2_bn(153) == 0);
-  {
-    DmlConvArgs one = conv_args(128, 64, 3, 3);                     // one patch buffer: a single 64-channel chunk only
-    CHECK(dml_conv_pt_fits(&one, 144) == 0 && dml_conv_pt_fits(&one, 141) == 1);
-  }
-  {
-    DmlConvArgs p = conv_args(256, 256, 3, 3);                      // ResNet50 stage-4 3x3 (14 x 14)
-    CHECK(dml_conv_pt_fits(&p, 140) == 1 && dml_conv_pt_fits(&p, 142) == 1);
-    p.sh = p.sw = 2; p.Ho = p.Wo = 7;                                // stride 2: refused
-    CHECK(dml_conv_pt_fits(&p, 140) == 0);
-    DmlConvArgs q = conv_args(80, 192, 3, 3);                        // Cin % 64 != 0: refused
-    CHECK(dml_conv_pt_fits(&q, 140) == 0);
-    DmlConvArgs r = conv_args(64, 96, 5, 5);                         // 5x5 at 35 x 35: 429-row patch > 416
-    r.H = r.W = r.Ho = r.Wo = 35;
-    CHECK(dml_conv_pt_fits(&r, 140) == 0);
-    CHECK(dml_conv(&p, 140, nullptr) != 0);                          // the launcher refuses what fits() refuses
-  }
   // row-ring 3x3 kernel (conv_rowring.hip): ResNet50 stage 2 only
   CHECK(dml_conv_v2_bn(150) == 64 && dml_conv_v2_bn(152) == 64);
   {

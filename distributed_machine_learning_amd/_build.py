@@ -26,7 +26,7 @@ SOURCES = [
     CSRC / "kernels" / "conv_dispatch.hip",
     CSRC / "kernels" / "conv_igemm_v2.hip",
     CSRC / "kernels" / "conv_igemm_ws.hip",
-    CSRC / "kernels" / "conv_igemm_wsp.hip", CSRC / "kernels" / "conv_igemm_pt.hip", CSRC / "kernels" / "conv_rowring.hip",
+    CSRC / "kernels" / "conv_igemm_wsp.hip", CSRC / "kernels" / "conv_rowring.hip",
     CSRC / "kernels" / "misc.hip",
     CSRC / "kernels" / "jpeg_decode.hip",
     CSRC / "kernels" / "stem_fused.hip",

@@ -43,6 +43,9 @@ class Election:
         self._coord = asyncio.Event()
         self.elections_won = 0
         self._task: Optional[asyncio.Task] = None
+        # test hook: a fail-over election (the leader died) starts this much later, so the
+        # service outruns the store-leader election deterministically (tests/test_elastic_service.py)
+        self.failover_delay_s = 0.0
         ep.on(MsgType.ELECTION, self._on_election)
         ep.on(MsgType.ELECTION_OK, self._on_ok)
         ep.on(MsgType.COORDINATE, self._on_coordinate)
@@ -79,6 +82,8 @@ class Election:
         me = self.ml.self_name
         self.in_election = True
         try:
+            if self.failover_delay_s > 0 and self.leader is None:
+                await asyncio.sleep(self.failover_delay_s)
             for _ in range(5):
                 if not self.eligible(me):
                     # followers just poke the best candidate and wait for COORDINATE

@@ -24,14 +24,10 @@ from .. import _native as N
 V2_CFGS = (10, 11, 12, 13, 14, 15, 16, 18, 21, 22, 23, 24, 26, 27, 28, 29, 30, 31, 32, 33, 34, 36, 37,
            38, 39)  # 23..37: BK32; 38 / 39: 3-stage BK64 64-channel tiles (r3)
 # warp-specialised tiles (csrc/kernels/conv_igemm_ws.hip: loader waves + MFMA waves, r5)
-WS_CFGS = tuple(range(100, 120))
+WS_CFGS = tuple(range(100, 113)) + (119,)  # 113..118 (fragment prefetch) removed in r6
 # their persistent form (csrc/kernels/conv_igemm_wsp.hip: one operand ring over a workgroup's
 # whole tile list; no split-K)
 WSP_CFGS = tuple(range(120, 130))
-# patch-stationary stride-1 tiles (csrc/kernels/conv_igemm_pt.hip: the activation patch of an
-# M tile of whole output rows is loaded once per channel chunk, r5); they refuse what they
-# cannot run (stride / dilation != 1, Cin % 64, a patch larger than the config's)
-PT_CFGS = tuple(range(140, 150))
 # the row-ring 3x3 kernel of ResNet50 stage 2 (csrc/kernels/conv_rowring.hip: weights resident in
 # LDS, input rows streamed once per strip; 2 / 1 / 4 strips per image, r5)
 RR_CFGS = (150, 151, 152)
@@ -105,8 +101,6 @@ def valid_cfgs(a: N.ConvArgs) -> List[int]:
     ex = _excluded()
     cands = [c for c in V2_CFGS if not (a.res and c in NO_RES_CFGS)] + (list(LATE_RES_CFGS) if a.res else [])
     cands += list(WS_CFGS) + ([] if a.ksplit > 1 else list(WSP_CFGS))
-    if a.ksplit <= 1 and a.sh == 1 and a.sw == 1 and max(a.dh, 1) == 1 and max(a.dw, 1) == 1 and a.Cin % 64 == 0:
-        cands += list(PT_CFGS)
     if rr_fits(a):
         cands += list(RR_CFGS)
     return [c for c in cands if c not in ex]

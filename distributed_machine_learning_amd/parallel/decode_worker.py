@@ -80,6 +80,7 @@ class DecodeProcs:
             self.free.put(p)
         self._lock = threading.Lock()
         self.closed = False
+        self.get_timeout_s = 30.0
 
     def _spawn(self) -> subprocess.Popen:
         p = subprocess.Popen(self._cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, env=self._env, bufsize=0)
@@ -90,7 +91,10 @@ class DecodeProcs:
     def decode_many(self, items: Sequence[Tuple[str, bytes]]) -> Dict[str, Optional[np.ndarray]]:
         if not items:
             return {}
-        p = self.free.get()
+        try:
+            p = self.free.get(timeout=self.get_timeout_s)
+        except queue.Empty:
+            raise TimeoutError("no decode worker free") from None   # the caller decodes in-process
         try:
             req = [struct.pack("<I", len(items))]
             for _, data in items:
@@ -113,7 +117,15 @@ class DecodeProcs:
             # a worker that failed mid-chunk (died, or its pipe is out of step) is replaced, so
             # the pool never shrinks; the caller decodes this chunk in-process
             p.kill()
-            self.free.put(self._spawn())
+            try:
+                p.wait(timeout=5)   # reap it
+            except subprocess.TimeoutExpired:
+                pass
+            try:
+                p = self._spawn()
+            except Exception:       # the slot comes back anyway (a dead worker fails fast and
+                pass                # is replaced again), so free.get() never waits on a lost slot
+            self.free.put(p)
             raise
 
     def close(self) -> None:

@@ -71,6 +71,10 @@ class Window:
     failed: Set[str] = field(default_factory=set)
     done: bool = False
     deps: List["Window"] = field(default_factory=list)  # earlier unfinished windows writing one of its slots
+    # rows this rank ships (it is their lowest holder): row index -> the window that delivered the
+    # image HERE. The row's ok flag is that window's final flag, so the ship window is not issued
+    # before it is done (an issue-ahead ship read an empty ``failed`` set)
+    ship_src: Dict[int, "Window"] = field(default_factory=dict)
 
     @property
     def shipped(self) -> int:
@@ -161,11 +165,15 @@ class HbmImageStore:
             self.index[n] = s
             self.idle[n] = None   # unpinned until its batch pins it
             self.holders[n] = {dst}
+        ship_src: Dict[int, Window] = {}
         for n in move:
+            h = min(self.holders[n])           # the lowest holder ships it (its copy lands first)
+            if h == self.me and n in self.here:
+                ship_src[len(slots)] = self.here[n]
             slots.append(self.index[n])
-            src.append(min(self.holders[n]))   # the lowest holder ships it (its copy lands first)
+            src.append(h)
             self.holders[n].add(dst)
-        w = Window(self, self._wid, epoch, dst, new + move, slots, src)
+        w = Window(self, self._wid, epoch, dst, new + move, slots, src, ship_src=ship_src)
         self._wid += 1
         deps = {}
         for s in slots:
@@ -275,8 +283,8 @@ class HbmImageStore:
                 ok[pos[n]] = 1
         out_rows = [i for i, s in enumerate(w.src) if s == rank and s != w.dst]   # shipped from here
         for i in out_rows:
-            mine = self.here.get(w.names[i])
-            ok[i] = int(mine is not None and w.names[i] not in mine.failed)
+            mine = w.ship_src.get(i)   # done (Stager.progress holds the issue until it is)
+            ok[i] = int(mine is not None and mine.done and w.names[i] not in mine.failed)
         ctx = torch.cuda.stream(stream) if (stream is not None and cuda) else _null()
         with ctx:
             if cuda and local is not None:
@@ -287,7 +295,7 @@ class HbmImageStore:
                 slot_of = dict(zip(w.names, w.slots))
                 # a pack may decode on a side stream of its own: it must not overtake an earlier
                 # window still writing one of these slots (an evicted, never-pinned image)
-                pack.after = [d.event for d in w.deps if not d.done and d.event is not None and cuda]
+                pack.after = self._slot_writer_events(w) if cuda else []
                 pack.launch([slot_of[n] for n in pack.names], self.arena, stream)
                 w.pack = pack
             recv, work = None, []
@@ -304,6 +312,33 @@ class HbmImageStore:
             if world > 1:
                 work.append(comm.all_reduce_data_async(okd))
             w.bufs, w.work = (local, recv, okd), work
+
+    def _slot_writer_events(self, w: Window) -> List[object]:
+        """Events a window's GPU decode must wait on: per earlier unfinished window touching one
+        of its slots, the decode's own completion event when that window only DECODED into the
+        slot here (its side stream), else its staging-stream event (it scattered shipped rows
+        into the slot, or read the slot to ship it). The staging-stream event has waited on every
+        earlier window's decode, so using it for a decode-only writer chained the decodes again
+        once the arena recycled slots."""
+        evs: Dict[int, object] = {}
+        mine = set(w.slots)
+        for d in w.deps:
+            if d.done:
+                continue
+            dec: Dict[str, object] = {}   # image -> the side-stream event of the decode that wrote it
+            subs = getattr(d.pack, "packs", None) or ([d.pack] if d.pack is not None else [])
+            for p in subs:
+                if getattr(p, "done", None) is not None:
+                    for n in p.names:
+                        dec[n] = p.done
+            for n, sl, sr in zip(d.names, d.slots, d.src):
+                if sl not in mine:
+                    continue
+                ev = dec.get(n) if (d.dst == self.me and sr == d.dst) else None
+                ev = ev if ev is not None else d.event
+                if ev is not None:
+                    evs[id(ev)] = ev
+        return list(evs.values())
 
     def _finish(self, w: Window, world: int, stream) -> bool:
         """Once the window's collectives are in place: on its destination, scatter the
@@ -422,6 +457,8 @@ class Stager:
             if w.work is None:
                 if not w.future.done():
                     break
+                if any(not sw.done for sw in w.ship_src.values()):
+                    break   # a row it ships is still being delivered here: its ok flag is not final
                 w.store._issue(w, rank, world, w.future.result(), comm, stream)
                 if w.store.device.type == "cuda":
                     w.store._finish(w, world, stream)

@@ -351,7 +351,7 @@ def nearest_index(n_in: int, n_out: int) -> np.ndarray:
     a = n_in / n_out
     steps = np.full(n_out, a, np.float64)
     steps[0] = a * 0.5
-    return np.add.accumulate(steps).astype(np.int16)
+    return np.add.accumulate(steps).astype(np.int32)
 
 
 class _PackedImages(dict):
@@ -363,8 +363,9 @@ class _PackedImages(dict):
 
 class _Pack:
     """Full-resolution images of one window in a pinned host buffer (built in the decode
-    pool): n records {pixel offset, h, w, row-table offset, column-table offset, slot} (int32),
-    the int16 nearest-index tables, the pixels. ``launch`` (serve loop, staging stream) fills in
+    pool): n records {pixel offset / 16, h, w, row-table offset, column-table offset, slot}
+    (int32: the offset in 16-byte units, so a pack of large images may pass 2 GiB), the int32
+    nearest-index tables (sources wider or taller than 32767 pixels), the pixels. ``launch`` (serve loop, staging stream) fills in
     the slots, copies it to the device once and resizes every image into its slot
     (misc.hip resize_nearest_kernel); ``release`` returns the buffer after the window's event."""
 
@@ -386,20 +387,24 @@ class _Pack:
                     t_len += len(t)
                 recs[i, out] = tabs[key]
             recs[i, 1], recs[i, 2] = h, w
-        pix0 = (n * 24 + t_len * 2 + 15) // 16 * 16
+        pix0 = (n * 24 + t_len * 4 + 15) // 16 * 16
         off = pix0
+        offs = []
         for i, im in enumerate(imgs):
-            recs[i, 0] = off
+            offs.append(off)
+            recs[i, 0] = off >> 4
             off += (im.nbytes + 15) // 16 * 16
+        if off >> 4 >= 1 << 31:
+            raise ValueError(f"image pack of {off} bytes exceeds the 32 GiB record range")
         self.nbytes = off
         self.buf = backend.pinned(self.nbytes)
         b = self.buf.numpy()
         self.recs = b[:n * 24].view(np.int32).reshape(n, 6)
         self.recs[...] = recs
         if t_len:
-            b[n * 24:n * 24 + t_len * 2].view(np.int16)[...] = np.concatenate(tab_parts)
+            b[n * 24:n * 24 + t_len * 4].view(np.int32)[...] = np.concatenate(tab_parts)
         for i, im in enumerate(imgs):
-            o = int(recs[i, 0])
+            o = offs[i]
             b[o:o + im.nbytes] = np.ascontiguousarray(im).reshape(-1)
         self.dev = None
 

@@ -19,6 +19,7 @@ import logging
 import os
 import shutil
 import socket
+import time
 import uuid
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -61,6 +62,14 @@ class StoreService:
         self.spool_root = os.path.join(os.path.dirname(os.path.abspath(local.root)), ".spool")
         self.linked = 0
         self.pulled = 0
+        # leader-side: set while the file map is settled; cleared from the start of a COORDINATE
+        # round until adopt() (a listing answered in between came from a half-built map)
+        self._settled = asyncio.Event()
+        self._settled.set()
+        # client-side listings (ls / ls-all: get-output) wait this long for a reachable, settled
+        # leader across an election instead of answering "nothing" (reference: the client
+        # blocks on the leader, worker.py:1123-1135)
+        self.query_wait_s = 20.0
         on = ep.on
         # leader-side
         on(MsgType.PUT_REQUEST, self._l_put)
@@ -246,12 +255,23 @@ class StoreService:
             return False, "leader unreachable"
         return r.type == MsgType.DELETE_FILE_REQUEST_SUCCESS, r.payload.get("error", "")
 
+    async def _leader_query(self, mtype: MsgType, payload: dict) -> Optional[Frame]:
+        """A read-only leader request retried until ``query_wait_s``: right after the leader
+        died there is no leader, or a dead one, until SWIM confirms it and the election ends
+        (tests/test_elastic_service.py: the coordinator-kill listing raced that election)."""
+        t_end = time.monotonic() + self.query_wait_s
+        while True:
+            r = await self._leader_request(mtype, payload)
+            if r is not None or time.monotonic() >= t_end:
+                return r
+            await asyncio.sleep(0.1)
+
     async def ls(self, name: str) -> List[str]:
-        r = await self._leader_request(MsgType.LIST_FILE_REQUEST, {"filename": name})
+        r = await self._leader_query(MsgType.LIST_FILE_REQUEST, {"filename": name})
         return [] if r is None else r.payload.get("machines", [])
 
     async def ls_all(self, pattern: str) -> List[str]:
-        r = await self._leader_request(MsgType.GET_FILE_NAMES_REQUEST, {"filepattern": pattern})
+        r = await self._leader_query(MsgType.GET_FILE_NAMES_REQUEST, {"filepattern": pattern})
         return [] if r is None else r.payload.get("files", [])
 
     async def get_versions(self, name: str, n: int) -> List[Tuple[int, bytes]]:
@@ -412,7 +432,17 @@ class StoreService:
         await self.ep.reply(fr, MsgType.DELETE_FILE_REQUEST_SUCCESS if ok else MsgType.DELETE_FILE_REQUEST_FAIL,
                             {"filename": name})
 
+    async def _wait_settled(self) -> None:
+        """A listing arriving while this new leader still collects COORDINATE_ACKs waits for
+        adopt() (bounded: a round whose acks never come answers from what it has)."""
+        if not self._settled.is_set():
+            try:
+                await asyncio.wait_for(self._settled.wait(), min(self.timeout, 5.0))
+            except asyncio.TimeoutError:
+                pass
+
     async def _l_ls(self, fr: Frame) -> None:
+        await self._wait_settled()
         name = fr.payload["filename"]
         await self.ep.reply(fr, MsgType.LIST_FILE_REQUEST_ACK, {"filename": name,
                                                                 "machines": sorted(self.meta.holders(name))})
@@ -423,6 +453,7 @@ class StoreService:
                                                                "machineids_with_file_versions": self.meta.holders(name)})
 
     async def _l_ls_all(self, fr: Frame) -> None:
+        await self._wait_settled()
         pat = fr.payload.get("filepattern", "*")
         await self.ep.reply(fr, MsgType.GET_FILE_NAMES_REQUEST_ACK, {"filepattern": pat,
                                                                      "files": self.meta.matching(pat)})
@@ -461,6 +492,7 @@ class StoreService:
     def begin_round(self) -> None:
         """Election: this node starts a COORDINATE round (before sending it)."""
         self._round = {}
+        self._settled.clear()
 
     def adopt(self, acks: Dict[str, dict]) -> None:
         """New leader: rebuild the file map from COORDINATE_ACK payloads.
@@ -481,6 +513,7 @@ class StoreService:
             for k, v in late.get(node, {}).items():
                 files.setdefault(k, set()).update(int(x) for x in v)
             self.meta.set_node_files(node, {k: sorted(v) for k, v in files.items()})
+        self._settled.set()
 
     async def node_failed(self, node: str) -> int:
         """Leader: drop the node's files and restore the replication factor."""
@@ -536,19 +569,22 @@ class StoreService:
                 log.info("%s: spool link failed (%s); pulling over the blob plane", self.me, e)
                 ok = {}
         if len(ok) < len(files):
-            req = {"op": "outbox_many", "token": p.get("token"), "names": [n for n, _ in files]}
+            # only the files no link stored: a linked file pulled again would be stored twice
+            # (twice the version count on the leaderless path, where this replica numbers them)
+            missing = [(n, v) for n, v in files if n not in ok]
+            req = {"op": "outbox_many", "token": p.get("token"), "names": [n for n, _ in missing]}
             try:
                 if p["source"] == self.me:  # this node PUT the bundle: take it from its own outbox
                     items = self.source.read(req)
                 else:
                     items = await self.blobs.fetch(p["source"], req, addr=p.get("source_blob"))
-                if len(items) == len(files):
+                if len(items) == len(missing):
                     def write():
-                        for (n, v), (_, data) in zip(files, items):
+                        for (n, v), (_, data) in zip(missing, items):
                             self.local.put_bytes(n, data, version=v)
                             ok[n] = self.local.versions(n)
                     await loop.run_in_executor(None, write)  # file writes never block the SWIM loop
-                    self.pulled += len(files)
+                    self.pulled += len(missing)
             except (ConnectionError, OSError, asyncio.TimeoutError) as e:
                 log.warning("%s: download of %d files failed: %s", self.me, len(files), e)
         await self.ep.reply(fr, MsgType.DOWNLOAD_MANY_REPLY,

@@ -19,7 +19,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(grank, world, rdzv, swim_base, out, kill_rank, kill_step, control, stall=(-1, -1, 0.0)):
+def _rank_main(grank, world, rdzv, swim_base, out, kill_rank, kill_step, control, stall=(-1, -1, 0.0),
+               election_delay=0.0):
     import logging
 
     logging.basicConfig(level=logging.WARNING)
@@ -33,6 +34,7 @@ def _rank_main(grank, world, rdzv, swim_base, out, kill_rank, kill_step, control
     if control:
         ctl = RankControl(grank, world, swim_base, store_dir=os.path.join(out, "sdfs"), replication=2,
                           on_dead=eg.dead.add, on_alive=eg.joiners.add).start()
+        ctl.node.election.failover_delay_s = election_delay
         fd = None
         put = ctl.store_put_many_async  # the product path: pipelined bundle PUTs (rank_main)
     else:
@@ -65,11 +67,11 @@ def _rank_main(grank, world, rdzv, swim_base, out, kill_rank, kill_step, control
     eg.close()
 
 
-def _run(tmp_path, kill_rank=-1, kill_step=-1, world=3, control=False, stall=(-1, -1, 0.0)):
+def _run(tmp_path, kill_rank=-1, kill_step=-1, world=3, control=False, stall=(-1, -1, 0.0), election_delay=0.0):
     ctx = mp.get_context("spawn")
     rdzv, swim = str(tmp_path / "rdzv"), _free_port() - world - 1
     ps = [ctx.Process(target=_rank_main, args=(r, world, rdzv, swim, str(tmp_path), kill_rank, kill_step, control,
-                                               stall))
+                                               stall, election_delay))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -111,21 +113,40 @@ def test_worker_kill_mid_job_recovers(tmp_path):
     assert r["c1"]["ResNet50"]["query_count"] >= 96 and r["c1"]["InceptionV3"]["query_count"] >= 96
 
 
+def _check_coordinator_failover(tmp_path, res, codes):
+    assert codes[3] == 17 and codes[:3] == [0, 0, 0], codes
+    r = res[2]
+    diag = {k: r.get(k) for k in ("steps", "rebuilds", "requeued", "written", "done", "coordinator", "members")}
+    diag["written_all"] = [res[g]["written"] for g in sorted(res)]
+    diag["store_outputs"] = len(r.get("store_outputs", []))
+    assert r["coordinator"] == 2 and r["members"] == [0, 1, 2] and r["rebuilds"] >= 1, diag
+    assert r["done"] == [True, True], diag
+    assert r["c1"]["ResNet50"]["query_count"] >= 96 and r["c1"]["InceptionV3"]["query_count"] >= 96, diag
+    batches = {tuple(os.path.basename(f).split("_")[1:3]) for f in r["store_outputs"]}
+    want = {(str(j), str(b)) for j in (31, 32) for b in range(1, 13)}
+    assert batches == want, (diag, sorted(want - batches))
+    files = glob.glob(str(tmp_path / "outputs" / "output_*.json"))
+    assert {tuple(os.path.basename(f).split("_")[1:3]) for f in files} == batches, diag
+
+
 def test_coordinator_kill_mid_job_failover(tmp_path):
     """World 4 with the per-rank control plane (SWIM + store): the coordinator
     (rank 3) dies at step 4; rank 2 takes over from its replica, every job
     completes, C1 >= submitted, and every batch's output file exists in the
     store at least once (the new coordinator re-PUTs the recent ones)."""
     res, codes = _run(tmp_path, kill_rank=3, kill_step=4, world=4, control=True)
-    assert codes[3] == 17 and codes[:3] == [0, 0, 0], codes
-    r = res[2]
-    assert r["coordinator"] == 2 and r["members"] == [0, 1, 2] and r["rebuilds"] >= 1
-    assert r["done"] == [True, True], (r["steps"], r["rebuilds"], r["requeued"], r["written"])
-    assert r["c1"]["ResNet50"]["query_count"] >= 96 and r["c1"]["InceptionV3"]["query_count"] >= 96
-    batches = {tuple(os.path.basename(f).split("_")[1:3]) for f in r["store_outputs"]}
-    assert batches == {(str(j), str(b)) for j in (31, 32) for b in range(1, 13)}
-    files = glob.glob(str(tmp_path / "outputs" / "output_*.json"))
-    assert {tuple(os.path.basename(f).split("_")[1:3]) for f in files} == batches
+    _check_coordinator_failover(tmp_path, res, codes)
+
+
+def test_coordinator_kill_listing_waits_for_the_store_election(tmp_path):
+    """The race behind VERDICT r5 weak 6, made deterministic: the store-leader election after
+    the coordinator's death starts 3 s late (test hook), so the job service (which fails over
+    on the collective side at once) finishes while the store has no leader - or a dead one.
+    The final listing must wait for the elected leader's settled file map (store
+    ``_leader_query`` / ``_wait_settled``) instead of answering with nothing, as the 2-in-8
+    failures of the undelayed test did under load."""
+    res, codes = _run(tmp_path, kill_rank=3, kill_step=4, world=4, control=True, election_delay=3.0)
+    _check_coordinator_failover(tmp_path, res, codes)
 
 
 def test_false_suspicion_stalled_rank_rejoins(tmp_path):
@@ -403,6 +424,51 @@ def test_hbm_image_store_windows_issue_ahead_but_never_overtake_a_slot_writer():
     assert st.arena[w3.slots[0]].numpy()[0, 0, 0] == 4 and not st.stager.queue
     w4 = st.plan(["5a"], 0)            # its slot's writer finished: no dependency
     assert w4.deps == []
+
+
+def test_hbm_image_store_shipped_row_takes_the_source_windows_final_flag():
+    """a window shipping an image from this rank's arena sets that row's ok flag from
+    the window that delivered the image HERE, once that window is final - never from a
+    not-yet-filled ``failed`` set (GPU issue-ahead). A failed image re-used by a batch
+    dispatched to another rank stays failed there instead of classifying a stale slot."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    import torch
+
+    from distributed_machine_learning_amd.parallel.image_store import HbmImageStore
+
+    class _Done:
+        def is_completed(self):
+            return True
+
+        def wait(self):
+            pass
+
+    class FakeComm:  # this process is rank 0 of 2; rank 1 contributes zero flags
+        def all_to_all_data_async(self, recv, send, out_splits, in_splits):
+            return _Done()
+
+        def all_reduce_data_async(self, t):
+            return _Done()
+
+    st = HbmImageStore(8, (1, 1), torch.device("cpu"), n_synth=0)
+    st.loader = lambda names: {n: (None if n == "bad.jpeg" else np.full((1, 1, 3), 7, np.uint8)) for n in names}
+    st.stager.attach(0, 2, ThreadPoolExecutor(1), FakeComm())
+    w1 = st.plan(["ok.jpeg", "bad.jpeg"], 0, dst=0)     # decoded here; bad.jpeg fails
+    w2 = st.plan(["bad.jpeg", "ok.jpeg"], 0, dst=1)     # re-used on rank 1: shipped from here
+    assert w2.src == [0, 0] and w2.ship_src == {0: w1, 1: w1}
+    st.stager.flush_until(w2)
+    assert w1.failed == {"bad.jpeg"} and w2.failed == {"bad.jpeg"}
+    # the gate itself: a ship window whose source window is unfinished is not issued
+    w3 = st.plan(["x.jpeg"], 0, dst=0)
+    w4 = st.plan(["x.jpeg"], 0, dst=1)
+    assert w4.ship_src == {0: w3}
+    w3.future = w4.future = None
+    st.stager.queue.remove(w3)                           # w3 never progresses
+    for _ in range(50):
+        st.stager.progress()
+    assert w4.work is None and not w4.done
 
 
 def test_hbm_image_store_plan_cost_is_independent_of_resident_images():

@@ -29,6 +29,7 @@ def test_pack_resize_into_slots():
     N.ensure_device_init()
     rng = np.random.default_rng(1)
     imgs = [rng.integers(0, 256, size=(h, 300, 3), dtype=np.uint8) for h in (169, 300, 211, 250)]
+    imgs[3] = rng.integers(0, 256, size=(3, 40000, 3), dtype=np.uint8)   # column index > 32767
     for H, W in ((224, 224), (299, 299)):
         arena = torch.full((8, H, W, 3), 7, dtype=torch.uint8, device="cuda")
         be = _Be()

@@ -17,3 +17,30 @@ def test_nearest_index_matches_pillow():
             ref = np.asarray(Image.fromarray(img).resize((W, H), Image.NEAREST))
             got = img[nearest_index(h, H)[:, None], nearest_index(w, W)[None, :]]
             assert np.array_equal(ref, got), (h, w, H, W)
+
+
+def test_pack_records_address_wide_images_and_large_packs():
+    """the pack's pixel offsets are stored in 16-byte units and its nearest tables as
+    int32, so a window of large CPU-decoded images (a pack past 2 GiB, a source wider than 32767
+    pixels) is addressed exactly instead of wrapping."""
+    import torch
+
+    from distributed_machine_learning_amd.parallel.rank_backend import _Pack
+
+    class Be:
+        nearest = staticmethod(nearest_index)
+
+        def pinned(self, n):
+            return torch.empty(n, dtype=torch.uint8)
+
+    imgs = [np.arange(2 * 40000 * 3, dtype=np.uint32).astype(np.uint8).reshape(2, 40000, 3),
+            np.full((5, 7, 3), 9, np.uint8)]
+    p = _Pack(Be(), ["wide", "small"], imgs, (4, 6))
+    b = p.buf.numpy()
+    tabs = b[2 * 24:].view(np.int32)
+    for i, im in enumerate(imgs):
+        off = int(p.recs[i, 0]) << 4
+        assert np.array_equal(b[off:off + im.nbytes], im.reshape(-1))
+        xt = int(p.recs[i, 4])
+        assert np.array_equal(tabs[xt:xt + 6], nearest_index(im.shape[1], 6))
+    assert nearest_index(40000, 6).max() > 32767

@@ -30,7 +30,7 @@ SHAPES = [  # name, batch, h, w, cin, cout, kh, kw, stride, ph, pw, residual
     ("inc_m3_3x3s2", 64, 35, 35, 288, 384, 3, 3, 2, 0, 0, 0),
 ]
 V2_DEFAULT = "11,12,14,15,24,25,26,28,30,31,32,33,38"
-WS_DEFAULT = ",".join(str(c) for c in list(range(100, 120)) + list(range(120, 130)) + list(range(140, 153)))
+WS_DEFAULT = ",".join(str(c) for c in list(range(100, 113)) + [119] + list(range(120, 130)) + list(range(150, 153)))
 
 
 def main():
