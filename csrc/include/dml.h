@@ -206,13 +206,6 @@ int dml_conv_rr(const DmlConvArgs* a, int cfg, hipStream_t s);
 int dml_conv_rr_fits(const DmlConvArgs* a);
 int dml_conv_rr_init(void);
 int dml_conv_rr_stamped(const DmlConvArgs* a, int cfg, void* stamps, hipStream_t s);  // phase probe
-// generic row-ring family (conv_rowring.hip; cfg ids 160..177): any kh x kw, stride 1, 'same' /
-// 'valid', Cin % 8 == 0, Cout in chunks of the config's width; weight block + 2-tile row ring in LDS
-int dml_conv_rrg(const DmlConvArgs* a, int cfg, hipStream_t s);
-int dml_conv_rrg_fits(const DmlConvArgs* a, int cfg);
-int dml_conv_rrg_bn(int cfg);
-int dml_conv_rrg_geometry(const DmlConvArgs* a, int cfg, int* out12);
-int dml_conv_rrg_init(void);
 // baseline JPEG decode on the GPU fused with the Pillow-exact nearest resize into arena slots
 // (jpeg_decode.hip): host parse + un-stuffing into one buffer, then three kernels
 long dml_jpeg_prepare(int n, const unsigned char* const* datas, const long* lens, int outH, int outW, void* buf,

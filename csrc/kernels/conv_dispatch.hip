@@ -7,8 +7,7 @@
 // tile configuration (dml_conv_v2), ids 100..119 a warp-specialised one (loader +
 // MFMA waves, dml_conv_ws, conv_igemm_ws.hip), ids 120..139 its persistent form
 // (dml_conv_wsp, conv_igemm_wsp.hip), ids 150..152 the row-ring 3x3 kernel of ResNet50 stage 2
-// (dml_conv_rr, conv_rowring.hip), ids 160..177 the generic row-ring family (dml_conv_rrg, same
-// file); they are part of the ABI the plan builder and the
+// (dml_conv_rr, conv_rowring.hip); they are part of the ABI the plan builder and the
 // autotuner (ops/tuning.py) use.
 //
 // Removed (measured never faster, kept only as history in DESIGN.md and
@@ -29,7 +28,7 @@ static int validate(const DmlConvArgs* a, int cfg) {
   const int bn = dml_conv_v2_bn(cfg);
   if (bn <= 0) {
     dml_set_error("dml_conv: cfg must be a tile config (v2: 10..63, warp-specialised: 100..119, persistent: "
-                  "120..139, row-ring: 150..152, generic row-ring: 160..177)");
+                  "120..139, row-ring: 150..152)");
     return -1;
   }
   // weights are packed with Cout padded to a multiple of 256 rows; a 96- or
@@ -59,7 +58,6 @@ static int validate(const DmlConvArgs* a, int cfg) {
 
 extern "C" int dml_conv(const DmlConvArgs* a, int cfg, hipStream_t s) {
   if (validate(a, cfg) != 0) return -1;
-  if (cfg >= 160) return dml_conv_rrg(a, cfg, s);
   if (cfg >= 150) return dml_conv_rr(a, cfg, s);
   if (cfg >= 120) return dml_conv_wsp(a, cfg, s);
   return cfg >= 100 ? dml_conv_ws(a, cfg, s) : dml_conv_v2(a, cfg, s);

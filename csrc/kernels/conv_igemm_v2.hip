@@ -487,7 +487,6 @@ extern "C" int dml_conv_v2_init(void) {
   if (!rc && dml_conv_ws_init() != 0) return -1;  // warp-specialised tiles (conv_igemm_ws.hip)
   if (!rc && dml_conv_wsp_init() != 0) return -1;  // persistent warp-specialised tiles (conv_igemm_wsp.hip)
   if (!rc && dml_conv_rr_init() != 0) return -1;   // row-ring 3x3 kernel (conv_rowring.hip)
-  if (!rc && dml_conv_rrg_init() != 0) return -1;  // generic row-ring family (conv_rowring.hip)
   return rc ? -1 : 0;
 }
 
@@ -505,7 +504,6 @@ extern "C" int dml_conv_v2(const DmlConvArgs* a, int cfg, hipStream_t s) {
 // channel-tile width of a config (0: not a config); ids 100..119: the warp-specialised
 // tiles of conv_igemm_ws.hip, 120..139 their persistent form (conv_igemm_wsp.hip)
 extern "C" int dml_conv_v2_bn(int cfg) {
-  if (cfg >= 160) return dml_conv_rrg_bn(cfg);  // generic row-ring family (conv_rowring.hip)
   if (cfg >= 150) return cfg <= 152 ? 64 : 0;  // row-ring 3x3 kernel (conv_rowring.hip)
   if (cfg >= 120) return dml_conv_wsp_bn(cfg);
   if (cfg >= 100) return dml_conv_ws_bn(cfg);

@@ -241,202 +241,6 @@ __global__ __launch_bounds__(NT) void conv_rr_kernel(DmlConvArgs a, int strips, 
 }
 
 }  // namespace rr
-
-// ============================================================================================
-// Generic row-ring family (cfg 160..): the stage-2 kernel's structure for any kh x kw, stride 1,
-// 'same' or 'valid' padding, any width, any Cin (multiple of 8), Cout in chunks of COUT_WG.
-//
-// LDS: the workgroup's weight block [tap][channel group g][cout] and a ring of RING = 2 TH + kh - 1
-// image rows, both in 64-B rows (32 channels of bf16): the ring is stored as CG channel-group
-// PLANES of RING x SLOTP pixels (SLOTP = W + 2 pw rounded up to 16), so any Cin costs
-// ceil(Cin / 32) planes instead of a power-of-two row (Cin 80: 3 planes, the last half zero; the
-// DMA's range check writes the zeros). 64-B rows are XOR-swizzled by key(row) = (row >> 1) & 2
-// on the chunk: a brute-force search over the ds_read_b128 lane groups (MI355X_MICROARCH LDS
-// table) found this key conflict-free for 16 consecutive rows at ANY start offset - needed
-// because a tap's 16-pixel fragment starts at an arbitrary column (the 128-B stage-2 kernel's
-// row & 7 key has the same property; the {0,2,3,1} key of the BK32 tiles does not).
-//
-// Block b -> (strip, cout chunk) with the cout chunks of one strip consecutive on one XCD (they
-// stream the same input rows: the second..last fetch them from that XCD's L2). A strip is a run of
-// TH-row tiles of one image; the host picks TH (as large as the registers and the 160 KiB allow)
-// and the strip count (grid >= the CU count). K order = tap-major then channel, as the packed
-// weights. MFMA waves: WC x WP, each FI cout fragments x FJ pixel fragments (pixel fragment f of
-// a tile goes to wave f % WP), fragments of the next (tap, g) step read behind the current
-// step's MFMAs; stores straight from the accumulators (bias, ReLU, channel offset).
-namespace rrg {
-
-using convk::lds_void;
-using convk::wait_vmcnt;
-constexpr unsigned OOB = 0x80000000u;
-
-__device__ __forceinline__ int key(int row) { return (row >> 1) & 2; }
-
-struct Geo {
-  int CG, SLOTP, RING, TH, strips, ncc, wbytes, plane, ntile, taps;
-};
-
-template <int WC, int WP, int FI, int FJ, int NL>
-__global__ __launch_bounds__((WC * WP + NL) * 64) void conv_rrg_kernel(DmlConvArgs a, Geo g) {
-  constexpr int NC = WC * WP;
-  constexpr int COUT_WG = WC * FI * 16;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const wl = smem;
-  char* const ring = smem + g.wbytes;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int cc = L % g.ncc, sidx = L / g.ncc;
-  const int n = sidx / g.strips, sp = sidx - n * g.strips;
-  const int t0 = sp * g.ntile / g.strips, t1 = (sp + 1) * g.ntile / g.strips;
-  const int TH = g.TH, RING = g.RING, SLOTP = g.SLOTP;
-  const int gbase = t0 * TH - a.ph;  // image row held by ring slot 0 at the strip's start
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int c0 = cc * COUT_WG;
-
-  if (wid >= NC) {
-    // ================================ loader wave ================================
-    const int lw = wid - NC;
-    const int lrow = lane >> 2, lq = lane & 3;
-    const int lchunk = lq ^ key(lrow);  // pieces start at rows % 16 == 0
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, 0x7ffffff0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7ffffff0, 0x00020000);
-    // weights: LDS row ((tap * CG + gg) * COUT_WG + cl) <- cout c0 + cl, K tap * Cin + gg * 32 + chunk * 8
-    const int wpieces = g.taps * g.CG * COUT_WG / 16;
-    for (int p = lw; p < wpieces; p += NL) {
-      const int row = p * 16 + lrow;
-      const int tg = row / COUT_WG, cl = row - tg * COUT_WG;
-      const int tap = tg / g.CG, gg = tg - tap * g.CG;
-      const int ch = gg * 32 + lchunk * 8, co = c0 + cl;
-      const bool ok = ch < a.Cin && co < a.Cout;
-      const unsigned off = ok ? (unsigned)(((long)co * a.Kpad + tap * a.Cin + ch) * 2) : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)(wl + p * 1024), 16, off, 0, 0, 0);
-    }
-    // image rows [r0, r0 + cnt) of image n into their ring slots, every channel-group plane
-    const int ppr = SLOTP / 16;  // 1-KiB pieces per ring row and plane
-    auto rows = [&](int r0, int cnt) __attribute__((always_inline)) {
-      const int npiece = cnt * g.CG * ppr;
-      for (int p = lw; p < npiece; p += NL) {  // wave-uniform decomposition
-        const int rr = p / (g.CG * ppr), rem = p - rr * (g.CG * ppr);
-        const int gg = rem / ppr, pc = rem - gg * ppr;
-        const int gr = r0 + rr;
-        const int slot = (gr - gbase) % RING;
-        const int col = pc * 16 + lrow;  // LDS column c holds input column c - pw
-        const int iw = col - a.pw, ch = gg * 32 + lchunk * 8;
-        const bool ok = (unsigned)gr < (unsigned)a.H && (unsigned)iw < (unsigned)a.W && ch < a.Cin;
-        const unsigned off = ok ? (unsigned)((((long)n * a.H + gr) * a.W + iw) * a.ldx + ch) * 2u : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            xrs, (lds_void*)(ring + gg * g.plane + (slot * SLOTP + pc * 16) * 64), 16, off, 0, 0, 0);
-      }
-    };
-    if (t0 < t1) rows(gbase, TH + a.kh - 1);
-    for (int t = t0; t < t1; ++t) {
-      wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();  // tile t's rows (and the weights) published; tile t-1 read
-      if (t + 1 < t1) rows((t + 1) * TH - a.ph + a.kh - 1, TH);  // the slots only tile t-1 used
-    }
-    return;
-  }
-
-  // ================================== MFMA wave ==================================
-  const int wc = wid % WC, wp = wid / WC;
-  const int frow = lane & 15, fq = lane >> 4;
-  const int tpx = TH * a.Wo;  // pixels of a full tile
-  int ohl[FJ], ow[FJ];
-#pragma unroll
-  for (int j = 0; j < FJ; ++j) {
-    int p = (j * WP + wp) * 16 + frow;
-    p = p < tpx ? p : 0;  // fragment rows past the tile: computed on pixel 0, never stored
-    ohl[j] = p / a.Wo;
-    ow[j] = p - ohl[j] * a.Wo;
-  }
-  const int cw = c0 + wc * FI * 16;  // this wave's first cout
-  float4 bv[FI];
-  bool cok[FI];
-#pragma unroll
-  for (int i = 0; i < FI; ++i) {
-    const int ccx = cw + i * 16 + fq * 4;
-    cok[i] = ccx < a.Cout;
-    bv[i] = cok[i] ? *(const float4*)(a.bias + ccx) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  // A fragment offsets: row base multiple of 16 -> the key is the lane's own
-  const int aoff = (wc * FI * 16 + frow) * 64 + ((fq ^ key(frow)) << 4);
-  const int nfrag_all = (tpx + 15) >> 4;
-  const int nsteps = g.taps * g.CG;
-  for (int t = t0; t < t1; ++t) {
-    const int r0 = t * TH;
-    const int rows_here = min(TH, a.Ho - r0);
-    const int cnt = rows_here * a.Wo;
-    f32x4 acc[FI][FJ];
-#pragma unroll
-    for (int i = 0; i < FI; ++i)
-#pragma unroll
-      for (int j = 0; j < FJ; ++j) acc[i][j] = (f32x4)(0.f);
-    __builtin_amdgcn_s_barrier();
-    const int s0 = ((t - t0) * TH) % RING;  // slot of input row r0 - ph
-    int sl[FJ];                             // ring slot of tap row 0 per fragment
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      int v = s0 + ohl[j];
-      sl[j] = v >= RING ? v - RING : v;
-    }
-    bf16x8 fa[2][FI], fb[2][FJ];
-    // B fragment address of (r, s, gg) for fragment j
-    auto boff = [&](int j, int r, int sx, int gg) __attribute__((always_inline)) {
-      int v = sl[j] + r;
-      v = v >= RING ? v - RING : v;
-      const int P = v * SLOTP + ow[j] + sx;
-      return gg * g.plane + P * 64 + ((fq ^ key(P)) << 4);
-    };
-    auto load = [&](int st, int buf) __attribute__((always_inline)) {
-      const int tap = st / g.CG, gg = st - tap * g.CG;
-      const int r = tap / a.kw, sx = tap - r * a.kw;
-      const char* wt = wl + st * COUT_WG * 64 + aoff;
-#pragma unroll
-      for (int i = 0; i < FI; ++i) fa[buf][i] = *(const bf16x8*)(wt + i * 16 * 64);
-#pragma unroll
-      for (int j = 0; j < FJ; ++j) fb[buf][j] = *(const bf16x8*)(ring + boff(j, r, sx, gg));
-    };
-    auto mfma = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-      for (int j = 0; j < FJ; ++j) {
-        if (j * WP + wp >= nfrag_all) continue;  // wave-uniform
-#pragma unroll
-        for (int i = 0; i < FI; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[buf][i], fb[buf][j], acc[i][j], 0, 0, 0);
-      }
-    };
-    load(0, 0);
-    int st = 0;
-    for (; st + 2 <= nsteps; st += 2) {
-      load(st + 1, 1);
-      mfma(0);
-      if (st + 2 < nsteps) load(st + 2, 0);
-      mfma(1);
-    }
-    if (st < nsteps) mfma(0);
-    // ---- epilogue straight from the accumulators (lane: 4 channels of one pixel)
-    const long m0 = ((long)n * a.Ho + r0) * a.Wo;
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const int lp = (j * WP + wp) * 16 + frow;
-      if (lp >= cnt) continue;
-      const long m = m0 + lp;
-#pragma unroll
-      for (int i = 0; i < FI; ++i) {
-        if (!cok[i]) continue;
-        const int ccx = cw + i * 16 + fq * 4;
-        float v[4] = {acc[i][j][0] + bv[i].x, acc[i][j][1] + bv[i].y, acc[i][j][2] + bv[i].z,
-                      acc[i][j][3] + bv[i].w};
-        if (a.relu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        *(uint2*)((unsigned short*)a.y + m * a.ldy + ccx) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      }
-    }
-  }
-}
-
-}  // namespace rrg
 }  // namespace dml
 
 static bool rr_fits(const DmlConvArgs* a) {
@@ -479,137 +283,3 @@ extern "C" int dml_conv_rr_stamped(const DmlConvArgs* a, int cfg, void* stamps, 
 }
 
 extern "C" int dml_conv_rr(const DmlConvArgs* a, int cfg, hipStream_t s) { return dml_conv_rr_stamped(a, cfg, nullptr, s); }
-
-// ------------------------------------------------------------------ generic row-ring family --
-// id, WC, WP, FI, FJ, NL: cout chunk WC x FI x 16, at most WP x FJ x 16 pixels per tile.
-// cfg = 160 + 2 * instance + strip mode (0: grid ~ one workgroup per CU, 1: twice that).
-#define DML_RRG_CFGS(X)                                                  \
-  X(0, 2, 2, 2, 7, 2)   /* 64 couts, <= 224 px (the stage-2 layout) */   \
-  X(1, 1, 4, 2, 3, 2)   /* 32 couts, <= 192 px */                        \
-  X(2, 1, 4, 3, 2, 2)   /* 48 couts, <= 128 px */                        \
-  X(3, 1, 4, 4, 2, 2)   /* 64 couts, <= 128 px */                        \
-  X(4, 2, 2, 1, 5, 2)   /* 32 couts, <= 160 px */                        \
-  X(5, 1, 4, 2, 4, 2)   /* 32 couts, <= 256 px */                        \
-  X(6, 2, 4, 2, 2, 2)   /* 64 couts, <= 128 px, 8 MFMA waves */          \
-  X(7, 1, 8, 2, 2, 2)   /* 32 couts, <= 256 px, 8 MFMA waves */          \
-  X(8, 1, 4, 3, 3, 2)   /* 48 couts, <= 192 px */
-#define DML_RRG_N 9
-
-static const int kRrgLds = 163840;
-
-struct RrgShape {
-  int WC, WP, FI, FJ, NL;
-};
-static RrgShape rrg_shape(int inst) {
-  switch (inst) {
-#define DML_SH(i, WC, WP, FI, FJ, NL) \
-  case i: return RrgShape{WC, WP, FI, FJ, NL};
-    DML_RRG_CFGS(DML_SH)
-#undef DML_SH
-    default: return RrgShape{0, 0, 0, 0, 0};
-  }
-}
-
-// geometry of a launch (false: this config cannot run the conv)
-static bool rrg_geo(const DmlConvArgs* a, int cfg, dml::rrg::Geo* g, int* lds, int* nthreads) {
-  if (cfg < 160 || cfg >= 160 + 2 * DML_RRG_N) return false;
-  const RrgShape sh = rrg_shape((cfg - 160) / 2);
-  const int smode = (cfg - 160) % 2;
-  const int dh = a->dh > 0 ? a->dh : 1, dw = a->dw > 0 ? a->dw : 1;
-  if (a->sh != 1 || a->sw != 1 || dh != 1 || dw != 1 || a->res || a->out_f32 || a->nseg || a->ksplit > 1 ||
-      a->rsub > 1 || a->Cin % 8 || a->ldx % 8 || a->Cout % 4 || a->ldy % 4 || a->kh < 1 || a->kw < 1)
-    return false;
-  const bool same = a->ph == (a->kh - 1) / 2 && a->pw == (a->kw - 1) / 2 && (a->kh & 1) && (a->kw & 1);
-  const bool valid = a->ph == 0 && a->pw == 0;
-  if (!same && !valid) return false;
-  if (a->Ho != a->H + 2 * a->ph - a->kh + 1 || a->Wo != a->W + 2 * a->pw - a->kw + 1 || a->Ho < 1 || a->Wo < 1)
-    return false;
-  const int taps = a->kh * a->kw;
-  if (a->Kpad < taps * a->Cin) return false;
-  if ((long)a->N * a->H * a->W * a->ldx * 2 >= 0x7ffffff0L || (long)a->Kpad * ((a->Cout + 255) / 256 * 256) * 2 >= 0x7ffffff0L)
-    return false;  // 32-bit buffer offsets
-  const int cout_wg = sh.WC * sh.FI * 16;
-  g->CG = (a->Cin + 31) / 32;
-  g->SLOTP = (a->W + 2 * a->pw + 15) / 16 * 16;
-  g->taps = taps;
-  g->wbytes = taps * g->CG * cout_wg * 64;
-  const int rowb = g->SLOTP * g->CG * 64;  // one ring row, every plane
-  const int th_reg = sh.WP * sh.FJ * 16 / a->Wo;
-  const int room = kRrgLds - g->wbytes;
-  if (room <= 0) return false;
-  const int th_lds = (room / rowb - (a->kh - 1)) / 2;
-  int th = th_reg < th_lds ? th_reg : th_lds;
-  th = th < a->Ho ? th : a->Ho;
-  if (th < 1) return false;
-  g->TH = th;
-  g->RING = 2 * th + a->kh - 1;
-  g->plane = g->RING * g->SLOTP * 64;
-  g->ncc = (a->Cout + cout_wg - 1) / cout_wg;
-  g->ntile = (a->Ho + th - 1) / th;
-  const int target = 256 * (smode + 1);
-  int strips = (target + a->N * g->ncc - 1) / (a->N * g->ncc);
-  strips = strips < 1 ? 1 : (strips > g->ntile ? g->ntile : strips);
-  g->strips = strips;
-  *lds = g->wbytes + g->CG * g->plane;
-  *nthreads = (sh.WC * sh.WP + sh.NL) * 64;
-  return *lds <= kRrgLds;
-}
-
-extern "C" int dml_conv_rrg_fits(const DmlConvArgs* a, int cfg) {
-  dml::rrg::Geo g;
-  int lds, nt;
-  return rrg_geo(a, cfg, &g, &lds, &nt) ? 1 : 0;
-}
-
-// cout chunk of a generic row-ring config (0: not one)
-extern "C" int dml_conv_rrg_bn(int cfg) {
-  if (cfg < 160 || cfg >= 160 + 2 * DML_RRG_N) return 0;
-  const RrgShape sh = rrg_shape((cfg - 160) / 2);
-  return sh.WC * sh.FI * 16;
-}
-
-// the launch's geometry for tests / tools: {CG, SLOTP, RING, TH, strips, ncc, wbytes, plane, ntile, taps, lds, grid}
-extern "C" int dml_conv_rrg_geometry(const DmlConvArgs* a, int cfg, int* out12) {
-  dml::rrg::Geo g;
-  int lds, nt;
-  if (!rrg_geo(a, cfg, &g, &lds, &nt)) return -1;
-  const int v[12] = {g.CG, g.SLOTP, g.RING, g.TH, g.strips, g.ncc, g.wbytes, g.plane, g.ntile, g.taps, lds,
-                     a->N * g.strips * g.ncc};
-  for (int i = 0; i < 12; ++i) out12[i] = v[i];
-  return 0;
-}
-
-extern "C" int dml_conv_rrg_init(void) {
-  using namespace dml::rrg;
-  int rc = 0;
-#define DML_SET(i, WC, WP, FI, FJ, NL)                                                                          \
-  rc |= (int)hipFuncSetAttribute((const void*)conv_rrg_kernel<WC, WP, FI, FJ, NL>,                              \
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, kRrgLds);
-  DML_RRG_CFGS(DML_SET)
-#undef DML_SET
-  if (rc) dml_set_error("dml_conv_rrg_init: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-  return rc ? -1 : 0;
-}
-
-extern "C" int dml_conv_rrg(const DmlConvArgs* a, int cfg, hipStream_t s) {
-  using namespace dml::rrg;
-  Geo g;
-  int lds, nt;
-  if (!rrg_geo(a, cfg, &g, &lds, &nt)) {
-    dml_set_error("dml_conv_rrg: needs stride 1, 'same' (odd kernel) or 'valid' padding, Cin % 8 == 0, no residual / "
-                  "fp32 output / split-K / segments, and a weight block + 2-tile row ring within 160 KiB");
-    return -1;
-  }
-  const unsigned grid = (unsigned)(a->N * g.strips * g.ncc);
-  switch ((cfg - 160) / 2) {
-#define DML_CASE(i, WC, WP, FI, FJ, NL)                                                     \
-  case i:                                                                                  \
-    hipLaunchKernelGGL((conv_rrg_kernel<WC, WP, FI, FJ, NL>), dim3(grid), dim3(nt), lds, s, *a, g); \
-    break;
-    DML_RRG_CFGS(DML_CASE)
-#undef DML_CASE
-    default: dml_set_error("dml_conv_rrg: bad cfg"); return -1;
-  }
-  DML_CHECK_LAUNCH();
-  return 0;
-}

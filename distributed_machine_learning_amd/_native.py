@@ -109,9 +109,6 @@ _SIGS = {
     "dml_plan_add_inc_stem": (C.c_int, [C.c_void_p, C.POINTER(IncStemArgs)]),
     "dml_plan_add_stem": (C.c_int, [C.c_void_p, C.POINTER(StemArgs)]),
     "dml_conv": (C.c_int, [C.POINTER(ConvArgs), C.c_int, C.c_void_p]),
-    "dml_conv_rrg_fits": (C.c_int, [C.POINTER(ConvArgs), C.c_int]),
-    "dml_conv_rrg_bn": (C.c_int, [C.c_int]),
-    "dml_conv_rrg_geometry": (C.c_int, [C.POINTER(ConvArgs), C.c_int, C.POINTER(C.c_int)]),
     "dml_conv_group": (C.c_int, [C.POINTER(ConvGroupArgs), C.c_int, C.c_void_p]),
     "dml_plan_add_conv_group": (C.c_int, [C.c_void_p, C.POINTER(ConvGroupArgs), C.c_int]),
     "dml_conv_pick_cfg": (C.c_int, [C.POINTER(ConvArgs)]),

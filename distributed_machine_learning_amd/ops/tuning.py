@@ -31,9 +31,6 @@ WSP_CFGS = tuple(range(120, 130))
 # the row-ring 3x3 kernel of ResNet50 stage 2 (csrc/kernels/conv_rowring.hip: weights resident in
 # LDS, input rows streamed once per strip; 2 / 1 / 4 strips per image, r5)
 RR_CFGS = (150, 151, 152)
-# the generic row-ring family (same file, r6): any kh x kw, stride 1, 'same' / 'valid', Cin % 8, Cout
-# in chunks; 9 register layouts x 2 strip modes. The launcher refuses what does not fit 160 KiB.
-RRG_CFGS = tuple(range(160, 178))
 CACHE_PATH = os.environ.get(
     "DML_TUNING_CACHE",
     os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "conv_tuning.json"))
@@ -98,14 +95,6 @@ def rr_fits(a: N.ConvArgs) -> bool:
             and a.rsub <= 1 and a.Kpad >= 576)
 
 
-def rrg_cfgs(a: N.ConvArgs) -> List[int]:
-    """Generic row-ring configs whose launcher accepts this conv (asks the library)."""
-    if a.kh * a.kw == 1 or a.sh != 1 or a.sw != 1 or a.res or a.out_f32 or a.nseg or a.ksplit > 1:
-        return []   # 1x1 convs are plain GEMMs: no tap re-use for the ring to save
-    L = N.lib()
-    return [c for c in RRG_CFGS if L.dml_conv_rrg_fits(C.byref(a), c) == 1]
-
-
 def valid_cfgs(a: N.ConvArgs) -> List[int]:
     if a.Cout % 8 or a.Cin % 8 or a.ldx % 8 or a.ldy % 8:
         return []
@@ -114,7 +103,6 @@ def valid_cfgs(a: N.ConvArgs) -> List[int]:
     cands += list(WS_CFGS) + ([] if a.ksplit > 1 else list(WSP_CFGS))
     if rr_fits(a):
         cands += list(RR_CFGS)
-    cands += rrg_cfgs(a)
     return [c for c in cands if c not in ex]
 
 

@@ -32,8 +32,7 @@ SHAPES = [  # name, batch, h, w, cin, cout, kh, kw, stride, ph, pw, residual
     ("inc_17_7x1_192", 64, 17, 17, 192, 192, 7, 1, 1, 3, 0, 0), ("inc_8_3x1", 64, 8, 8, 384, 384, 3, 1, 1, 1, 0, 0),
 ]
 V2_DEFAULT = "11,12,14,15,24,25,26,28,30,31,32,33,38"
-WS_DEFAULT = ",".join(str(c) for c in list(range(100, 113)) + [119] + list(range(120, 130)) + list(range(150, 153))
-                      + list(range(160, 178)))
+WS_DEFAULT = ",".join(str(c) for c in list(range(100, 113)) + [119] + list(range(120, 130)) + list(range(150, 153)))
 
 
 def main():
@@ -82,12 +81,11 @@ def main():
             torch.cuda.synchronize()
             outs[c] = (y, ar)
         ref_cfg = next(c for c in v2 if c in outs)
-        # the generic row-ring configs (160..) pad each tap's channels to 32 (Cin 80: a different
-        # summation order than the v2 tiles' flattened K): equal within bf16 rounding, not bit for
-        # bit; every other tile must be bit-identical
+        # the patch-stationary tiles (140..) sum K chunk-major: equal to the v2 tile within bf16
+        # rounding, not bit for bit; every other tile must be bit-identical
         refy = outs[ref_cfg][0].float()
         close = lambda c: ((outs[c][0].float() - refy).abs().max() / (refy.abs().max() + 1e-6)).item() < 1e-2  # noqa: E731
-        mism = [c for c in outs if not (torch.equal(outs[c][0], outs[ref_cfg][0]) or (c >= 160 and close(c)))]
+        mism = [c for c in outs if not (torch.equal(outs[c][0], outs[ref_cfg][0]) or (c >= 140 and close(c)))]
         if mism:
             bad += 1
         for _ in range(a.rounds):
