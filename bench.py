@@ -176,6 +176,12 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
             t[r] = (31, k * world + r, 0, (k * B) % cap, B, dp.epoch)
         return t
 
+    # spin-up (A/B knob, default off): untimed steps for this many seconds before the warmup
+    spin = float(os.environ.get("DML_BENCH_SPINUP_S", "0"))
+    t_end = time.perf_counter() + spin
+    while time.perf_counter() < t_end:
+        pipe.run(4, table, record=False)
+        torch.cuda.synchronize()
     # warmup (graph capture, clocks, caches)
     pipe.run(max(args.warmup, 1), table, record=False)
     pipe.stats.latencies_s.clear()

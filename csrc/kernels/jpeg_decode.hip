@@ -9,8 +9,10 @@
 // dml_jpeg_prepare) into one pinned buffer: per image a fixed-size descriptor (geometry,
 // natural-order quantisation tables, Huffman lookup tables, the output slot's nearest-index
 // tables) and its entropy bytes. On the device:
-//   1. jpeg_huff_kernel: one wave per image copies its entropy bytes into LDS; lane 0 decodes
-//      the MCUs serially (Huffman + DC prediction) into int16 coefficient blocks.
+//   1. jpeg_huff_par_kernel (r6): a 256-thread workgroup per image decodes the entropy stream in
+//      256 bit segments at once, self-synchronising (see "parallel entropy decoding" below), into
+//      int16 coefficient blocks; the r5 serial one-wave decode (jpeg_huff_kernel) stays as the
+//      A/B reference (DML_JPEG_SERIAL=1) and as the code the CPU tests compare against.
 //   2. jpeg_idct_kernel: one thread per 8x8 block — libjpeg's "islow" integer IDCT
 //      (jidctint.c arithmetic: CONST_BITS 13, PASS1_BITS 2, 64-bit products, its post-IDCT
 //      range-limit table) into per-component sample planes.
@@ -34,6 +36,8 @@
 // JPEG Group (libjpeg, Copyright (C) 1991-1998, Thomas G. Lane; IJG license). The Huffman
 // decoder, the lookup tables, the descriptor layout and the kernels are this project's own.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -138,9 +142,10 @@ __host__ __device__ static inline int byte_at(const uint8_t* p, int i) {
   return (int)((((const uint32_t*)p)[i >> 2] >> ((i & 3) * 8)) & 255);
 }
 
-__host__ __device__ static inline int huff_decode(Bits& b, const DmljHuff& t) {
+template <class BR>
+__host__ __device__ static inline int huff_decode(BR& b, const DmljHuff& t, const uint32_t* look = nullptr) {
   b.fill();
-  const uint32_t e = t.look[b.peek(9)];
+  const uint32_t e = (look ? look : t.look)[b.peek(9)];
   if (e) {
     b.skip(e >> 8);
     return e & 255;
@@ -208,6 +213,175 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_
             }
           }
       }
+}
+
+// --------------------------------------------------------- parallel entropy decoding --
+// one wave decoding each image serially put ~one wave per CU to work for ~7 ms per
+// 256-image window. Here a workgroup of DMLJ_PT threads decodes one image: thread t owns the
+// symbols that START in bit segment t of the entropy stream. Huffman codes self-synchronise, so
+//   1. every thread decodes its segment from a guessed state (MCU slot 0, coefficient 0) and
+//      records its EXIT: the first symbol boundary at or past the segment end, with the decoder
+//      state (MCU block slot u, next coefficient k) there, and the blocks it completed;
+//   2. thread t re-decodes from thread t-1's exit until no exit changes (Jacobi rounds; the
+//      chain from the exact thread 0 converges in a few rounds: a wrong start re-joins the true
+//      symbol sequence within a few symbols, and from there its exit equals the true one);
+//   3. a prefix sum over the block counts gives each thread the decode-order index of its first
+//      block; every thread decodes its segment once more, now writing coefficients and DC
+//      DIFFERENCES, and stops at the image's last block;
+//   4. the DC predictions are rebuilt per component by a block-wide prefix sum in decode order.
+// The per-symbol code (tables, fast AC path, corrupt-code handling) is the serial decoder's,
+// so the coefficients are identical to it (tests/test_jpeg_decode.py compares every block).
+#define DMLJ_PT 256
+
+struct PState {
+  int pos, u, k;   // bit position of the next symbol; MCU block slot; next coefficient (0 = DC)
+};
+
+struct McuMap {
+  int U, total;                  // block slots per MCU; blocks in the image
+  // slot u -> component (2 bits at 2u) and its block offset inside the MCU (bit u): packed, so
+  // the per-symbol lookups are shifts, not a runtime-indexed array (which goes to scratch)
+  int comp, dv, dh;
+  __host__ __device__ int comp_of(int u) const { return (comp >> (2 * u)) & 3; }
+};
+
+__host__ __device__ static inline McuMap mcu_map(const DmljImage& d) {
+  McuMap m;
+  m.U = m.comp = m.dv = m.dh = 0;
+  const int nc = d.ncomp;
+  for (int c = 0; c < nc; ++c) {
+    const int hs = nc == 1 ? 1 : d.hs[c], vs = nc == 1 ? 1 : d.vs[c];
+    for (int v = 0; v < vs; ++v)
+      for (int h = 0; h < hs; ++h) {
+        m.comp |= c << (2 * m.U);
+        m.dv |= v << m.U;
+        m.dh |= h << m.U;
+        ++m.U;
+      }
+  }
+  m.total = d.mcux * d.mcuy * m.U;
+  return m;
+}
+
+// coefficient block of decode-order block gb
+__host__ __device__ static inline int16_t* block_at(const DmljImage& d, const McuMap& m, int16_t* coef, int gb) {
+  const int mcu = gb / m.U, u = gb - mcu * m.U;
+  const int my = mcu / d.mcux, mx = mcu - my * d.mcux;
+  const int c = m.comp_of(u);
+  const int hs = d.ncomp == 1 ? 1 : d.hs[c], vs = d.ncomp == 1 ? 1 : d.vs[c];
+  const int by = my * vs + ((m.dv >> u) & 1), bx = mx * hs + ((m.dh >> u) & 1);
+  return coef + d.coef_off[c] + ((int64_t)by * d.bw[c] + bx) * 64;
+}
+
+// a bit reader that starts at any bit (the serial Bits starts at 0); same word layout
+struct BitsAt {
+  const uint32_t* w;
+  int nw, wpos, nb;
+  uint64_t buf;
+  __host__ __device__ BitsAt(const uint32_t* words, int nwords, int bit) : w(words), nw(nwords) {
+    wpos = bit >> 5;
+    const uint32_t cur = wpos < nw ? w[wpos] : 0u;
+    buf = ((uint64_t)cur << 32) << (bit & 31);
+    nb = 32 - (bit & 31);
+    ++wpos;
+  }
+  __host__ __device__ int pos() const { return wpos * 32 - nb; }
+  __host__ __device__ void fill() {
+    if (nb <= 32) {
+      const uint32_t nx = wpos < nw ? w[wpos] : 0u;
+      buf |= (uint64_t)nx << (32 - nb);
+      ++wpos;
+      nb += 32;
+    }
+  }
+  __host__ __device__ uint32_t peek(int n) const { return (uint32_t)(buf >> (64 - n)); }
+  __host__ __device__ void skip(int n) {
+    buf <<= n;
+    nb -= n;
+  }
+  __host__ __device__ int get(int n) {
+    if (n == 0) return 0;
+    const int v = (int)peek(n);
+    skip(n);
+    return v;
+  }
+};
+
+// the lookup tables one thread decodes with (LDS copies on the GPU, the descriptor's on the host):
+// component c's table is base + ((idx >> 2c) & 3) * stride words
+struct SegTabs {
+  const uint32_t *look_dc, *look_ac, *fast_ac;
+  int stride, idx_dc, idx_ac;
+  __host__ __device__ const uint32_t* dc(int c) const { return look_dc + ((idx_dc >> (2 * c)) & 3) * stride; }
+  __host__ __device__ int ac_off(int c) const { return ((idx_ac >> (2 * c)) & 3) * stride; }
+};
+
+// decode the symbols starting in [st.pos, end) from state st; returns the exit state and the
+// blocks completed. WRITE: block gb onwards gets its AC coefficients and its DC DIFFERENCE, and
+// decoding stops at the image's last block.
+template <bool WRITE>
+__host__ __device__ static PState seg_decode(const DmljImage& d, const McuMap& m, const SegTabs& tb,
+                                             const uint32_t* stream, int nw, PState st, int end, int* nblocks,
+                                             int gb, int16_t* coef) {
+  BitsAt b(stream, nw, st.pos);
+  int u = st.u, k = st.k, cnt = 0;
+  int16_t* blk = WRITE && gb < m.total ? block_at(d, m, coef, gb) : nullptr;
+  while (b.pos() < end) {
+    if (WRITE && gb >= m.total) break;
+    const int c = m.comp_of(u);
+    bool done;
+    if (k == 0) {
+      const int s = huff_decode(b, d.dc[d.td[c]], tb.dc(c));
+      const int diff = s ? extend(b.get(s), s) : 0;
+      if (WRITE) blk[0] = (int16_t)diff;
+      k = 1;
+      done = false;
+    } else {
+      b.fill();
+      const int ao = tb.ac_off(c);
+      const uint32_t f = tb.fast_ac[ao + b.peek(9)];
+      if (f) {
+        b.skip(f & 15);
+        k += (f >> 4) & 15;
+        if (WRITE) blk[k < 64 ? k : 63] = (int16_t)((int32_t)f >> 16);
+        ++k;
+        done = k >= 64;
+      } else {
+        const int rs = huff_decode(b, d.ac[d.ta[c]], tb.look_ac + ao);
+        const int r = rs >> 4, sz = rs & 15;
+        if (sz) {
+          k += r;
+          const int v2 = extend(b.get(sz), sz);
+          if (WRITE) blk[k < 64 ? k : 63] = (int16_t)v2;
+          ++k;
+          done = k >= 64;
+        } else if (r != 15) {
+          done = true;   // EOB
+        } else {
+          k += 16;
+          done = k >= 64;
+        }
+      }
+    }
+    if (done) {
+      k = 0;
+      u = u + 1 == m.U ? 0 : u + 1;
+      ++cnt;
+      if (WRITE) {
+        ++gb;
+        blk = gb < m.total ? block_at(d, m, coef, gb) : nullptr;
+      }
+    }
+  }
+  *nblocks = cnt;
+  return PState{b.pos(), u, k};
+}
+
+__host__ __device__ static inline int seg_bits(const DmljImage& d) {
+  const int nbits = d.stream_len * 8;
+  int seg = (nbits + DMLJ_PT - 1) / DMLJ_PT;
+  seg = (seg + 31) / 32 * 32;
+  return seg < 64 ? 64 : seg;
 }
 
 // ----------------------------------------------------------------------------- IDCT --
@@ -378,6 +552,109 @@ __global__ __launch_bounds__(64) void jpeg_huff_kernel(const unsigned char* __re
   const DmljImage* ds = (const DmljImage*)(buf + 16);
   if (i >= n || !ds[i].ok) return;
   decode_entropy(ds[i], (const uint32_t*)(buf + ds[i].stream_off), coef, true);
+}
+
+// the parallel decode of one image per workgroup (see "parallel entropy decoding" above)
+__global__ __launch_bounds__(DMLJ_PT) void jpeg_huff_par_kernel(const unsigned char* __restrict__ buf, int n,
+                                                                int16_t* __restrict__ coef) {
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  const DmljImage& d = ((const DmljImage*)(buf + 16))[i];
+  if (!d.ok) return;   // uniform over the workgroup
+  __shared__ uint32_t lk_dc[3][512], lk_ac[3][512], fs_ac[3][512];
+  __shared__ int ex_pos[2][DMLJ_PT], ex_u[2][DMLJ_PT], ex_k[2][DMLJ_PT], scan[2][DMLJ_PT];
+  __shared__ int chg[3];
+  const int t = threadIdx.x;
+  const int nc = d.ncomp;
+  for (int c = 0; c < nc; ++c)
+    for (int j = t; j < 512; j += DMLJ_PT) {
+      lk_dc[c][j] = d.dc[d.td[c]].look[j];
+      lk_ac[c][j] = d.ac[d.ta[c]].look[j];
+      fs_ac[c][j] = d.ac[d.ta[c]].fast[j];
+    }
+  if (t < 3) chg[t] = 0;
+  const SegTabs tb = {&lk_dc[0][0], &lk_ac[0][0], &fs_ac[0][0], 512, (2 << 4) | (1 << 2), (2 << 4) | (1 << 2)};
+  const McuMap m = mcu_map(d);
+  const uint32_t* stream = (const uint32_t*)(buf + d.stream_off);
+  const int nw = (d.stream_len + 3) / 4;
+  const int SEG = seg_bits(d), nbits = d.stream_len * 8;
+  const int nseg = (nbits + SEG - 1) / SEG;
+  const bool live = t < nseg;
+  const int end = live ? min((t + 1) * SEG, nbits) : 0;
+  __syncthreads();
+  // 1. every segment from a guessed state
+  PState start = {t * SEG, 0, 0}, ex = {0, 0, 0};
+  int nb = 0;
+  if (live) ex = seg_decode<false>(d, m, tb, stream, nw, start, end, &nb, 0, nullptr);
+  ex_pos[0][t] = ex.pos;
+  ex_u[0][t] = ex.u;
+  ex_k[0][t] = ex.k;
+  __syncthreads();
+  // 2. Jacobi rounds: re-decode from the predecessor's exit until no exit changes. Flags rotate
+  // over three slots: round r sets chg[r % 3]; thread 0 clears round r+1's slot before round r's
+  // barrier, when every thread has read it for the last time (round r-2)
+  int cur = 0;
+  for (int r = 0; r < nseg; ++r) {
+    if (t == 0) chg[(r + 1) % 3] = 0;
+    if (live && t > 0) {
+      const PState st = {ex_pos[cur][t - 1], ex_u[cur][t - 1], ex_k[cur][t - 1]};
+      if (st.pos != start.pos || st.u != start.u || st.k != start.k) {
+        start = st;
+        const PState e2 = seg_decode<false>(d, m, tb, stream, nw, start, end, &nb, 0, nullptr);
+        if (e2.pos != ex.pos || e2.u != ex.u || e2.k != ex.k) chg[r % 3] = 1;
+        ex = e2;
+      }
+    }
+    ex_pos[cur ^ 1][t] = ex.pos;
+    ex_u[cur ^ 1][t] = ex.u;
+    ex_k[cur ^ 1][t] = ex.k;
+    __syncthreads();
+    cur ^= 1;
+    if (!chg[r % 3]) break;   // uniform: every thread reads the slot after the same barrier
+  }
+  // 3. exclusive prefix of the block counts -> each thread's first block; decode and write
+  int sc = 0;
+  scan[0][t] = live ? nb : 0;
+  __syncthreads();
+  for (int off = 1; off < DMLJ_PT; off <<= 1) {
+    const int v = scan[sc][t] + (t >= off ? scan[sc][t - off] : 0);
+    scan[sc ^ 1][t] = v;
+    __syncthreads();
+    sc ^= 1;
+  }
+  const int gb0 = t > 0 ? scan[sc][t - 1] : 0;
+  if (live) seg_decode<true>(d, m, tb, stream, nw, start, end, &nb, gb0, coef);
+  __syncthreads();
+  // 4. DC predictions per component: block-wide prefix over the differences in decode order
+  for (int c = 0; c < nc; ++c) {
+    const int hs = nc == 1 ? 1 : d.hs[c], vs = nc == 1 ? 1 : d.vs[c];
+    const int nbc = d.bw[c] * d.bh[c], per = (nbc + DMLJ_PT - 1) / DMLJ_PT;
+    const int j0 = min(t * per, nbc), j1 = min(j0 + per, nbc);
+    auto dcp = [&](int j) -> int16_t* {
+      const int mcu = j / (hs * vs), w = j - mcu * (hs * vs);
+      const int v = w / hs, h = w - v * hs;
+      const int my = mcu / d.mcux, mx = mcu - my * d.mcux;
+      return coef + d.coef_off[c] + ((int64_t)(my * vs + v) * d.bw[c] + (mx * hs + h)) * 64;
+    };
+    int sum = 0;
+    for (int j = j0; j < j1; ++j) sum += *dcp(j);
+    scan[0][t] = sum;
+    __syncthreads();
+    sc = 0;
+    for (int off = 1; off < DMLJ_PT; off <<= 1) {
+      const int v = scan[sc][t] + (t >= off ? scan[sc][t - off] : 0);
+      scan[sc ^ 1][t] = v;
+      __syncthreads();
+      sc ^= 1;
+    }
+    int pred = t > 0 ? scan[sc][t - 1] : 0;
+    for (int j = j0; j < j1; ++j) {
+      int16_t* p = dcp(j);
+      pred += *p;
+      *p = (int16_t)pred;
+    }
+    __syncthreads();
+  }
 }
 
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const unsigned char* __restrict__ buf, int n,
@@ -705,7 +982,13 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
   }
   const unsigned char* b = (const unsigned char*)dbuf;
   int16_t* coef = (int16_t*)dwork;
-  hipLaunchKernelGGL(dml::jpg::jpeg_huff_kernel, dim3(n), dim3(64), 0, s, b, n, coef);
+  // the parallel segment decode (a workgroup per image); DML_JPEG_SERIAL=1: the r5 one-wave serial
+  // decode (A/B)
+  static const bool serial = getenv("DML_JPEG_SERIAL") && getenv("DML_JPEG_SERIAL")[0] == '1';
+  if (serial)
+    hipLaunchKernelGGL(dml::jpg::jpeg_huff_kernel, dim3(n), dim3(64), 0, s, b, n, coef);
+  else
+    hipLaunchKernelGGL(dml::jpg::jpeg_huff_par_kernel, dim3(n), dim3(DMLJ_PT), 0, s, b, n, coef);
   DML_CHECK_LAUNCH();
   hipLaunchKernelGGL(dml::jpg::jpeg_idct_kernel, dim3((maxblk + 255) / 256, n), dim3(256), 0, s, b, n, coef,
                      (uint8_t*)dwork);
@@ -754,6 +1037,82 @@ extern "C" long dml_jpeg_desc_size(void) { return (long)sizeof(DmljImage); }
 // the descriptor's leading part a re-target needs (geometry, plane offsets, NEAREST tables): the
 // plane cache keeps only this much per image
 extern "C" long dml_jpeg_head_size(void) { return (long)offsetof(DmljImage, q); }
+
+// CPU replay of jpeg_huff_par_kernel's algorithm (tests): the coefficient blocks of the parallel
+// decode (coef_par) and of the serial one (coef_ser), each ncoef int16; info = {ncoef, Jacobi
+// rounds, segments}. 0 = ok, -1 = unsupported, -2 = the buffers are too small.
+extern "C" int dml_jpeg_parallel_host(const unsigned char* data, long len, short* coef_par, short* coef_ser,
+                                      long cap, long* info) {
+  using namespace dml::jpg;
+  DmljImage d;
+  static thread_local uint8_t* stream = nullptr;
+  if (!stream) stream = (uint8_t*)malloc(1 << 24);
+  if (parse_one(data, len, d, stream, (1 << 24) - 16, 0, 0) != 0) return -1;
+  memset(stream + d.stream_len, 0, 16);
+  swap_words(stream, (d.stream_len + 8 + 15) / 16 * 16);
+  int64_t ncoef = 0;
+  for (int c = 0; c < d.ncomp; ++c) {
+    d.coef_off[c] = ncoef;
+    ncoef += (int64_t)d.bw[c] * d.bh[c] * 64;
+  }
+  info[0] = (long)ncoef;
+  if (ncoef > cap) return -2;
+  memset(coef_par, 0, (size_t)ncoef * 2);
+  memset(coef_ser, 0, (size_t)ncoef * 2);
+  decode_entropy(d, (const uint32_t*)stream, coef_ser, true);
+  const McuMap m = mcu_map(d);
+  SegTabs tb = {d.dc[0].look, d.ac[0].look, d.ac[0].fast, (int)(sizeof(DmljHuff) / 4), 0, 0};
+  for (int c = 0; c < d.ncomp; ++c) {
+    tb.idx_dc |= d.td[c] << (2 * c);
+    tb.idx_ac |= d.ta[c] << (2 * c);
+  }
+  const uint32_t* w = (const uint32_t*)stream;
+  const int nw = (d.stream_len + 3) / 4;
+  const int SEG = seg_bits(d), nbits = d.stream_len * 8, nseg = (nbits + SEG - 1) / SEG;
+  PState start[DMLJ_PT], ex[DMLJ_PT], nex[DMLJ_PT];
+  int nb[DMLJ_PT] = {0};
+  for (int t = 0; t < nseg; ++t) {
+    start[t] = PState{t * SEG, 0, 0};
+    ex[t] = seg_decode<false>(d, m, tb, w, nw, start[t], std::min((t + 1) * SEG, nbits), &nb[t], 0, nullptr);
+  }
+  int rounds = 0;
+  for (int r = 0; r < nseg; ++r) {
+    bool changed = false;
+    for (int t = 0; t < nseg; ++t) {
+      nex[t] = ex[t];
+      if (t == 0) continue;
+      const PState st = ex[t - 1];
+      if (st.pos == start[t].pos && st.u == start[t].u && st.k == start[t].k) continue;
+      start[t] = st;
+      nex[t] = seg_decode<false>(d, m, tb, w, nw, st, std::min((t + 1) * SEG, nbits), &nb[t], 0, nullptr);
+      changed |= nex[t].pos != ex[t].pos || nex[t].u != ex[t].u || nex[t].k != ex[t].k;
+    }
+    for (int t = 0; t < nseg; ++t) ex[t] = nex[t];
+    ++rounds;
+    if (!changed) break;
+  }
+  int gb = 0;
+  for (int t = 0; t < nseg; ++t) {
+    int dummy;
+    seg_decode<true>(d, m, tb, w, nw, start[t], std::min((t + 1) * SEG, nbits), &dummy, gb, coef_par);
+    gb += nb[t];
+  }
+  for (int c = 0; c < d.ncomp; ++c) {
+    const int hs = d.ncomp == 1 ? 1 : d.hs[c], vs = d.ncomp == 1 ? 1 : d.vs[c];
+    int pred = 0;
+    for (int j = 0; j < d.bw[c] * d.bh[c]; ++j) {
+      const int mcu = j / (hs * vs), ww = j - mcu * (hs * vs);
+      const int v = ww / hs, h = ww - v * hs;
+      const int my = mcu / d.mcux, mx = mcu - my * d.mcux;
+      int16_t* p = coef_par + d.coef_off[c] + ((int64_t)(my * vs + v) * d.bw[c] + (mx * hs + h)) * 64;
+      pred += *p;
+      *p = (int16_t)pred;
+    }
+  }
+  info[1] = rounds;
+  info[2] = nseg;
+  return 0;
+}
 
 // CPU decode with the same code (tests): full-resolution RGB into out (h*w*3); 0 = ok,
 // -1 = unsupported (the CPU workers' path)

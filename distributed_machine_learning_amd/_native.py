@@ -134,6 +134,8 @@ _SIGS = {
     "dml_jpeg_desc_size": (C.c_long, []),
     "dml_jpeg_head_size": (C.c_long, []),
     "dml_jpeg_decode_host": (C.c_int, [C.c_char_p, C.c_long, C.c_void_p, C.POINTER(C.c_int)]),
+    "dml_jpeg_parallel_host": (C.c_int, [C.c_char_p, C.c_long, C.c_void_p, C.c_void_p, C.c_long,
+                                         C.POINTER(C.c_long)]),
     "dml_plan_create": (C.c_void_p, []),
     "dml_plan_destroy": (None, [C.c_void_p]),
     "dml_plan_add_conv": (C.c_int, [C.c_void_p, C.POINTER(ConvArgs), C.c_int]),

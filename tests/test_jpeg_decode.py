@@ -92,3 +92,27 @@ def test_descriptors_carry_pillows_nearest_tables():
     row = buf[off:off + 640].view(np.int16)[:299]
     col = buf[off + 640:off + 1280].view(np.int16)[:224]
     assert np.array_equal(row, nearest_index(250, 299)) and np.array_equal(col, nearest_index(169, 224))
+
+
+def _par_and_serial(data: bytes):
+    cap = 1 << 22
+    par = np.zeros(cap, np.int16)
+    ser = np.zeros(cap, np.int16)
+    info = (C.c_long * 3)()
+    rc = N.lib().dml_jpeg_parallel_host(data, len(data), par.ctypes.data, ser.ctypes.data, cap, info)
+    return rc, par[:info[0]], ser[:info[0]], info[1], info[2]
+
+
+@pytest.mark.parametrize("name,data", _cases())
+def test_parallel_entropy_decode_equals_the_serial_one(name, data):
+    """The self-synchronising segment decode (jpeg_huff_par_kernel's algorithm, replayed on the
+    CPU with the same __host__ __device__ code): every coefficient of every block equals the
+    serial decoder's, including the DC predictions rebuilt by the prefix sum; the Jacobi rounds
+    converge in a few rounds."""
+    rc, par, ser, rounds, nseg = _par_and_serial(data)
+    if rc == -1:
+        assert len(data) > 60 * 1024 or _host_decode(data) is None, name
+        return
+    assert rc == 0 and par.size > 0
+    assert np.array_equal(par, ser), (name, int((par != ser).sum()), rounds, nseg)
+    assert rounds <= max(6, nseg), (name, rounds, nseg)
