@@ -21,6 +21,9 @@ network here). After the timed steps every rank re-runs its last batch through
 
   python bench.py --gpus N --steps K --warmup W [--models ResNet50,InceptionV3]
 
+Timing: per model, --spinup-s seconds of untimed steps (clock ramp), then W untimed warmup
+steps, then EXACTLY K timed steps between a barrier + device sync on both sides (max over ranks).
+
 Launch: under torchrun (WORLD_SIZE set) each process is one rank. Without it and
 with ``--gpus N > 1`` this process becomes a launcher: it spawns N rank
 processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* env, 127.0.0.1 rendezvous) before
@@ -61,6 +64,10 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=120, help="timed steps (120: >= 100 latency samples for p99)")
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--spinup-s", type=float, default=float(os.environ.get("DML_BENCH_SPINUP_S", "1.0")),
+                    help="seconds of untimed steps BEFORE the W warmup steps: the GPU's clocks ramp during the "
+                         "first tens of milliseconds of load (per-step kernel time falls ~5 %% over the first "
+                         "steps, rocprofv3 trace in profiles/r6_final); reported as `spinup_s`; 0 = off")
     ap.add_argument("--models", default="ResNet50,InceptionV3",
                     help="comma list; the first is the headline `value`, the rest are sub-records")
     ap.add_argument("--model", default="", help="alias: measure only this model")
@@ -176,9 +183,11 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
             t[r] = (31, k * world + r, 0, (k * B) % cap, B, dp.epoch)
         return t
 
-    # spin-up (A/B knob, default off): untimed steps for this many seconds before the warmup
-    spin = float(os.environ.get("DML_BENCH_SPINUP_S", "0"))
-    t_end = time.perf_counter() + spin
+    # spin-up (--spinup-s): untimed steps for this many seconds before the warmup, so the timed
+    # steps run at the steady clock a serving GPU runs at (20 timed steps at a cold clock measured
+    # 47.6k / 90.6-91.1k img/s, 200 steps 50.0k / 93.5-96.0k, 20 after a 1 s spin-up 48.9-49.4k /
+    # 93.3-94.6k, InceptionV3 / ResNet50, same box: profiles/r6_final/short_runs.txt)
+    t_end = time.perf_counter() + max(args.spinup_s, 0.0)
     while time.perf_counter() < t_end:
         pipe.run(4, table, record=False)
         torch.cuda.synchronize()
@@ -339,6 +348,7 @@ def main(argv=None) -> int:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "spinup_s": args.spinup_s,
             "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
