@@ -124,17 +124,25 @@ class BatchRenderer:
             doc = decode_top5([images[i] for i in ok], top_idx[ok], top_p[ok],
                               [images[i] for i in range(len(images)) if failed[i]], self.idx)
             return dumps(doc).encode()
-        ent: Dict[bytes, int] = {}  # decode_top5's dict: first-occurrence order, last assignment wins
-        for i, nm in enumerate(images):
-            if not failed[i]:
-                ent[self._key(nm)] = i
-        for i, nm in enumerate(images):
-            if failed[i]:
-                ent[self._key(nm)] = -1
+        kc = self._keys
+        names_k = [kc[nm] if nm in kc else self._key(nm) for nm in images]
+        # decode_top5's dict: first-occurrence order, last assignment wins (a batch may repeat an
+        # image: jobs pick cyclically); failed images are assigned after every decoded one
+        if failed.any():
+            fl = failed.tolist()
+            ent: Dict[bytes, int] = {}
+            for i, k in enumerate(names_k):
+                if not fl[i]:
+                    ent[k] = i
+            for i, k in enumerate(names_k):
+                if fl[i]:
+                    ent[k] = -1
+        else:
+            ent = dict(zip(names_k, range(len(names_k))))
         keys = list(ent)
         rows = np.fromiter(ent.values(), np.int32, len(keys))
         koff = np.zeros(len(keys) + 1, np.int64)
-        np.cumsum([len(k) for k in keys], out=koff[1:])
+        np.cumsum(np.fromiter(map(len, keys), np.int64, len(keys)), out=koff[1:])
         blob = b"".join(keys)
         k = top_idx.shape[1] if top_idx.ndim == 2 else 5
         need = 256 + len(blob) + len(keys) * k * 160
@@ -146,7 +154,7 @@ class BatchRenderer:
                                           buf, C.sizeof(buf))
         if n < 0:
             raise RuntimeError("output render buffer too small")
-        return buf.raw[:n]
+        return C.string_at(buf, n)   # copies n bytes (buf.raw copied the whole 1 MiB scratch first)
 
 
 _host = None

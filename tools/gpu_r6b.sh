@@ -1,0 +1,12 @@
+#!/bin/bash
+# r6 call B: the driver's exact bench command (twice), then the 51,200-distinct store-image pass.
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for r in 1 2; do
+  timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/driver_cmd_r$r.log 2>&1 || { tail -20 gpurun_out/driver_cmd_r$r.log; exit 1; }
+  python tools/bench_summary.py gpurun_out/driver_cmd_r$r.log 2>/dev/null || tail -1 gpurun_out/driver_cmd_r$r.log | cut -c1-400
+done
+timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 --models ResNet50 --svc-store-images 51200 --kill-pass off > gpurun_out/distinct51200.log 2>&1 || { tail -20 gpurun_out/distinct51200.log; exit 1; }
+python tools/bench_summary.py gpurun_out/distinct51200.log 2>/dev/null || tail -1 gpurun_out/distinct51200.log | cut -c1-600
