@@ -9,8 +9,8 @@
 // dml_jpeg_prepare) into one pinned buffer: per image a fixed-size descriptor (geometry,
 // natural-order quantisation tables, Huffman lookup tables, the output slot's nearest-index
 // tables) and its entropy bytes. On the device:
-//   1. jpeg_huff_par_kernel (r6): a 256-thread workgroup per image decodes the entropy stream in
-//      256 bit segments at once, self-synchronising (see "parallel entropy decoding" below), into
+//   1. jpeg_huff_par_kernel (r6): a 64-lane wave per image decodes the entropy stream in 64 bit
+//      segments at once, self-synchronising (see "parallel entropy decoding" below), into
 //      int16 coefficient blocks; the r5 serial one-wave decode (jpeg_huff_kernel) stays as the
 //      A/B reference (DML_JPEG_SERIAL=1) and as the code the CPU tests compare against.
 //   2. jpeg_idct_kernel: one thread per 8x8 block — libjpeg's "islow" integer IDCT
@@ -217,7 +217,7 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_
 
 // --------------------------------------------------------- parallel entropy decoding --
 // one wave decoding each image serially put ~one wave per CU to work for ~7 ms per
-// 256-image window. Here a workgroup of DMLJ_PT threads decodes one image: thread t owns the
+// 256-image window. Here DMLJ_PT threads (one wave) decode one image: thread t owns the
 // symbols that START in bit segment t of the entropy stream. Huffman codes self-synchronise, so
 //   1. every thread decodes its segment from a guessed state (MCU slot 0, coefficient 0) and
 //      records its EXIT: the first symbol boundary at or past the segment end, with the decoder
@@ -231,7 +231,12 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_
 //   4. the DC predictions are rebuilt per component by a block-wide prefix sum in decode order.
 // The per-symbol code (tables, fast AC path, corrupt-code handling) is the serial decoder's,
 // so the coefficients are identical to it (tests/test_jpeg_decode.py compares every block).
-#define DMLJ_PT 256
+// 64 segments (one wave per image): a decoder started in the wrong state re-joins the true symbol
+// AND block-slot sequence after ~5,000 bits on the bench / reference photos (CPU replay, 40
+// images), so the Jacobi rounds x segment length is ~5,500 bits whatever the segment count
+// (256 / 128 / 64 / 32 segments: 12.9 / 6.2 / 3.1 / 1.6 rounds); fewer segments cut the total
+// work (rounds x stream) 4x against 256 at the same latency, and one wave needs no LDS barrier
+#define DMLJ_PT 64
 
 struct PState {
   int pos, u, k;   // bit position of the next symbol; MCU block slot; next coefficient (0 = DC)
@@ -377,9 +382,9 @@ __host__ __device__ static PState seg_decode(const DmljImage& d, const McuMap& m
   return PState{b.pos(), u, k};
 }
 
-__host__ __device__ static inline int seg_bits(const DmljImage& d) {
+__host__ __device__ static inline int seg_bits(const DmljImage& d, int nseg_max = DMLJ_PT) {
   const int nbits = d.stream_len * 8;
-  int seg = (nbits + DMLJ_PT - 1) / DMLJ_PT;
+  int seg = (nbits + nseg_max - 1) / nseg_max;
   seg = (seg + 31) / 32 * 32;
   return seg < 64 ? 64 : seg;
 }
@@ -1040,7 +1045,8 @@ extern "C" long dml_jpeg_head_size(void) { return (long)offsetof(DmljImage, q); 
 
 // CPU replay of jpeg_huff_par_kernel's algorithm (tests): the coefficient blocks of the parallel
 // decode (coef_par) and of the serial one (coef_ser), each ncoef int16; info = {ncoef, Jacobi
-// rounds, segments}. 0 = ok, -1 = unsupported, -2 = the buffers are too small.
+// rounds, segments}; info[1] on entry: at most this many segments (0 = DMLJ_PT). 0 = ok,
+// -1 = unsupported, -2 = the buffers are too small.
 extern "C" int dml_jpeg_parallel_host(const unsigned char* data, long len, short* coef_par, short* coef_ser,
                                       long cap, long* info) {
   using namespace dml::jpg;
@@ -1068,7 +1074,8 @@ extern "C" int dml_jpeg_parallel_host(const unsigned char* data, long len, short
   }
   const uint32_t* w = (const uint32_t*)stream;
   const int nw = (d.stream_len + 3) / 4;
-  const int SEG = seg_bits(d), nbits = d.stream_len * 8, nseg = (nbits + SEG - 1) / SEG;
+  const int want = info[1] > 0 && info[1] <= DMLJ_PT ? (int)info[1] : DMLJ_PT;   // segments (A/B)
+  const int SEG = seg_bits(d, want), nbits = d.stream_len * 8, nseg = (nbits + SEG - 1) / SEG;
   PState start[DMLJ_PT], ex[DMLJ_PT], nex[DMLJ_PT];
   int nb[DMLJ_PT] = {0};
   for (int t = 0; t < nseg; ++t) {

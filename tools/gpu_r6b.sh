@@ -4,6 +4,10 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_jpeg_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/jpeg_pytest.log 2>&1; rc=$?
+tail -2 gpurun_out/jpeg_pytest.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/jpeg_bench.py > gpurun_out/jpeg_par64.log 2>&1 && grep -v amdgpu.ids gpurun_out/jpeg_par64.log || exit 1
 for r in 1 2; do
   timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/driver_cmd_r$r.log 2>&1 || { tail -20 gpurun_out/driver_cmd_r$r.log; exit 1; }
   python tools/bench_summary.py gpurun_out/driver_cmd_r$r.log 2>/dev/null || tail -1 gpurun_out/driver_cmd_r$r.log | cut -c1-400
