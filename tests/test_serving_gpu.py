@@ -366,6 +366,11 @@ def test_kill_pass_world4_on_one_gpu(tmp_path):
     nb = 48 + 48
     o = rec["outputs"]
     assert o["distinct_batches_in_store"] == nb and o["listing_duplicates"] == 0, o
+    # the fair-share split on the real engines (at world 1 it is degenerate):
+    # with both jobs queued every split gives each model at least one of the live ranks
+    splits = rec["fair_share_splits"]
+    assert splits and any(s.get("ResNet50", 0) >= 1 and s.get("InceptionV3", 0) >= 1 for s in splits), splits
+    assert rec["images"]["ResNet50"] >= n_r and rec["images"]["InceptionV3"] >= n_i, rec["images"]
 
 
 @pytest.mark.parametrize("model", ["ResNet50", "InceptionV3"])
