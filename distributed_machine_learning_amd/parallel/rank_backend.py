@@ -632,6 +632,8 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         self._dcache: "OrderedDict[str, np.ndarray]" = OrderedDict()   # name -> full-res RGB (both models)
         self._nprocs, self._dprocs = int(os.environ.get("DML_DECODE_PROCS", "12")), None
         self._dbytes, self.decode_hits, self._dlock = 0, 0, threading.Lock()
+        self.plane_hits = 0     # images a window took from another model's GPU decode (resize only)
+        self.gpu_decodes = 0    # images decoded on the GPU (jpeg_decode.hip)
         self._nn: Dict[Tuple[int, int], np.ndarray] = {}    # (n_in, n_out) -> nearest-index table
         self._pins: List[torch.Tensor] = []                  # free pinned pack buffers
         self._jstreams: List[torch.cuda.Stream] = []         # side streams of the GPU JPEG decodes
@@ -702,7 +704,11 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         return t
 
     JPEG_STREAMS = 8
-    PLANE_CACHE_BYTES = 4 << 30   # device work buffers of decoded windows kept for the other model
+    # device work buffers of decoded windows kept for the other model (DML_PLANE_CACHE_GB). A
+    # 256-image window holds ~90 MB (coefficients + planes): 4 GiB kept ~11k images, so on the
+    # 51,200-distinct run the second job re-decoded every image the first had decoded long before
+    # (decode cache hits 0, 76,800 decodes for 51,200 images); 24 GiB (of 288 GB HBM) keeps ~68k
+    PLANE_CACHE_BYTES = int(float(os.environ.get("DML_PLANE_CACHE_GB", "24")) * (1 << 30))
 
     def remember_planes(self, pack: "_JpegPack", recs: Dict[str, np.ndarray]) -> None:
         """(serve loop, after a GPU decode's launch) the window's planes serve the other
@@ -808,6 +814,7 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             if cached:
                 hit = [n for n in names if n in cached]
                 rp = _ResizePack(self, hit, [cached[n] for n in hit], hw)
+                self.plane_hits += len(hit)
                 for n in hit:
                     out[n] = True
                 names = [n for n in names if n not in cached]
@@ -820,6 +827,7 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
                     log.warning("GPU JPEG prepare failed (%s); decoding on the CPU", e)
                     jp = None
             if jp is not None:
+                self.gpu_decodes += len(jp.names)
                 for n in jp.names:
                     out[n] = True   # decoded on the device at launch (the window only needs "ok")
                 gone = set(jp.names)

@@ -252,6 +252,8 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                     "shipped_images_per_rank": col(7), "shipped_bytes": sum(col(8)),
                     "evictions_coordinator": int(sum(a.evictions for a in ar.values())),
                     "decode_cache_hits_coordinator": int(getattr(backend, "decode_hits", 0)),
+                    "gpu_jpeg_decodes_coordinator": int(getattr(backend, "gpu_decodes", 0)),
+                    "gpu_plane_reuse_coordinator": int(getattr(backend, "plane_hits", 0)),
                 }
             if single_rates:
                 # the same images served one model after the other at the single-model rates
