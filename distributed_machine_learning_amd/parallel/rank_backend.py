@@ -633,6 +633,8 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         self._nprocs, self._dprocs = int(os.environ.get("DML_DECODE_PROCS", "12")), None
         self._dbytes, self.decode_hits, self._dlock = 0, 0, threading.Lock()
         self.plane_hits = 0     # images a window took from another model's GPU decode (resize only)
+        # decode-pool seconds per window phase (summed over windows; the store-image pass reports them)
+        self.load_s = {"fetch": 0.0, "gpu_prepare": 0.0, "cpu_decode": 0.0, "windows": 0}
         self.gpu_decodes = 0    # images decoded on the GPU (jpeg_decode.hip)
         self._nn: Dict[Tuple[int, int], np.ndarray] = {}    # (n_in, n_out) -> nearest-index table
         self._pins: List[torch.Tensor] = []                  # free pinned pack buffers
@@ -804,7 +806,10 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         Pillow NEAREST here, as load_img(target_size)."""
         from PIL import Image
 
+        t0 = time.perf_counter()
         blobs = self.loader(names) if self.loader else {}
+        t1 = time.perf_counter()
+        t_fetch = t1 - t0
         hw = self.arenas[model].hw
         out = _PackedImages() if self.gpu_resize else {}
         jp = rp = None
@@ -826,6 +831,10 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
                 except Exception as e:   # never fatal: the CPU path takes the window
                     log.warning("GPU JPEG prepare failed (%s); decoding on the CPU", e)
                     jp = None
+            t2 = time.perf_counter()
+            with self._dlock:
+                self.load_s["gpu_prepare"] += t2 - t1
+            t1 = t2
             if jp is not None:
                 self.gpu_decodes += len(jp.names)
                 for n in jp.names:
@@ -876,6 +885,11 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             ok = [n for n in names if out.get(n) is not None]
             cpu = _Pack(self, ok, [out[n] for n in ok], hw) if ok else None
             out.pack = _Packs([rp, jp, cpu]) if (jp is not None or rp is not None) else cpu
+        t3 = time.perf_counter()
+        with self._dlock:
+            self.load_s["fetch"] += t_fetch
+            self.load_s["cpu_decode"] += t3 - t1
+            self.load_s["windows"] += 1
         return out
 
     def launch(self, model, names, slot):

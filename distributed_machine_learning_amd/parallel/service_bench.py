@@ -254,6 +254,7 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                     "decode_cache_hits_coordinator": int(getattr(backend, "decode_hits", 0)),
                     "gpu_jpeg_decodes_coordinator": int(getattr(backend, "gpu_decodes", 0)),
                     "gpu_plane_reuse_coordinator": int(getattr(backend, "plane_hits", 0)),
+                    "decode_pool_s_coordinator": {k: round(v, 3) for k, v in getattr(backend, "load_s", {}).items()},
                 }
             if single_rates:
                 # the same images served one model after the other at the single-model rates
