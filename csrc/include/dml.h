@@ -211,12 +211,14 @@ int dml_conv_rr_stamped(const DmlConvArgs* a, int cfg, void* stamps, hipStream_t
 long dml_jpeg_prepare(int n, const unsigned char* const* datas, const long* lens, int outH, int outW, void* buf,
                       long cap, int* status, long* info);
 void dml_jpeg_set_slot(void* buf, int i, int slot);
+void dml_jpeg_set_slots(void* buf, const int* idx, const int* slots, int n);
 int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long maxstream, void* dwork, int H, int W,
                            void* arena, hipStream_t s);
 int dml_jpeg_init(void);
 long dml_jpeg_desc_size(void);
 long dml_jpeg_head_size(void);
 void dml_jpeg_retarget(void* dst, const void* src, int outH, int outW, long base);
+void dml_jpeg_retarget_many(void* dst, const void* const* srcs, const long* bases, int n, int outH, int outW);
 int dml_jpeg_resize_only(const void* dbuf, int n, int H, int W, void* arena, hipStream_t s);
 int dml_jpeg_decode_host(const unsigned char* data, long len, unsigned char* out, int* hw);
 int dml_conv_group_validate(const DmlConvGroupArgs* g, int cfg);

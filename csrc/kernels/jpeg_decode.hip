@@ -978,6 +978,13 @@ extern "C" long dml_jpeg_prepare(int n, const unsigned char* const* datas, const
 // set the arena slot of image i (host side, before the H2D copy)
 extern "C" void dml_jpeg_set_slot(void* buf, int i, int slot) { ((DmljImage*)((unsigned char*)buf + 16))[i].slot = slot; }
 
+// the same for n images in one call (idx == null: images 0..n-1): the serve loop issued one ctypes
+// call per image, holding the GIL between them (256 per window)
+extern "C" void dml_jpeg_set_slots(void* buf, const int* idx, const int* slots, int n) {
+  DmljImage* d = (DmljImage*)((unsigned char*)buf + 16);
+  for (int j = 0; j < n; ++j) d[idx ? idx[j] : j].slot = slots[j];
+}
+
 extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long maxstream, void* dwork, int H, int W,
                                       void* arena, hipStream_t s) {
   if (n <= 0) return 0;
@@ -1019,6 +1026,14 @@ extern "C" void dml_jpeg_retarget(void* dst, const void* src, int outH, int outW
   d->outH = outH;
   d->outW = outW;
   for (int c = 0; c < d->ncomp; ++c) d->plane_off[c] += base;
+}
+
+// n re-targets in one call: dst + 16 + j * desc <- srcs[j] with base bases[j] (the other model's
+// window: one native call instead of one per image from the decode pool)
+extern "C" void dml_jpeg_retarget_many(void* dst, const void* const* srcs, const long* bases, int n, int outH,
+                                       int outW) {
+  unsigned char* b = (unsigned char*)dst + 16;
+  for (int j = 0; j < n; ++j) dml_jpeg_retarget(b + (long)j * (long)sizeof(DmljImage), srcs[j], outH, outW, bases[j]);
 }
 
 // colour + resize only, from planes a dml_jpeg_decode_resize launch left (descriptors from

@@ -477,8 +477,9 @@ class _JpegPack:
         from .. import _native as N
 
         L = N.lib()
-        for i, sl in zip(self.idx, slots):
-            L.dml_jpeg_set_slot(C.c_void_p(self.buf.data_ptr()), i, int(sl))
+        idx = np.asarray(self.idx, np.int32)
+        sl = np.asarray(slots, np.int32)
+        L.dml_jpeg_set_slots(C.c_void_p(self.buf.data_ptr()), idx.ctypes.data, sl.ctypes.data, len(sl))
         H, W = self.hw
         # on a side stream of its own: the serial Huffman decode of one window (one wave per
         # image, milliseconds) overlaps the next windows' instead of queueing behind it on the
@@ -536,11 +537,15 @@ class _ResizePack:
         self.buf = backend.pinned(self.used)
         b = self.buf.numpy()
         b[:16].view(np.int64)[:] = (len(names), 0)
-        base = self.buf.data_ptr()
         self.packs, self.works = [], []
-        for i, (rec, pk, work) in enumerate(entries):
-            L.dml_jpeg_retarget(C.c_void_p(base + 16 + i * desc), rec.ctypes.data, hw[0], hw[1], work.data_ptr())
-            if pk not in self.packs:
+        srcs = np.fromiter((rec.ctypes.data for rec, _, _ in entries), np.uint64, len(entries))
+        bases = np.fromiter((work.data_ptr() for _, _, work in entries), np.int64, len(entries))
+        L.dml_jpeg_retarget_many(C.c_void_p(self.buf.data_ptr()), srcs.ctypes.data, bases.ctypes.data, len(entries),
+                                 hw[0], hw[1])
+        seen = set()
+        for _, pk, work in entries:
+            if id(pk) not in seen:
+                seen.add(id(pk))
                 self.packs.append(pk)
                 self.works.append(work)
         self.desc, self.dev = desc, None
@@ -551,8 +556,8 @@ class _ResizePack:
         from .. import _native as N
 
         L = N.lib()
-        for i, sl in enumerate(slots):
-            L.dml_jpeg_set_slot(C.c_void_p(self.buf.data_ptr()), i, int(sl))
+        sl = np.asarray(slots, np.int32)
+        L.dml_jpeg_set_slots(C.c_void_p(self.buf.data_ptr()), None, sl.ctypes.data, len(sl))
         with torch.cuda.stream(stream):
             for pk, work in zip(self.packs, self.works):
                 stream.wait_event(pk.done)

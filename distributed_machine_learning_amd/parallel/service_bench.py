@@ -169,9 +169,20 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
         svc.freeze_heap()
         eg.barrier()
         t0, c0 = time.perf_counter(), time.thread_time()
+        prof = None
+        if os.environ.get("DML_PROFILE_SERVE") and store_images:   # cProfile of the serve loop (A/B tool)
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         steps = svc.serve(stop_when_idle=True,   # drains the writer: every output file is on disk
                           deadline=time.monotonic() + time_limit_s if time_limit_s > 0 else None)
         loop_cpu = time.thread_time() - c0       # the serve loop thread's own CPU seconds
+        if prof is not None:
+            import pstats
+            prof.disable()
+            with open(os.environ["DML_PROFILE_SERVE"], "w") as f:
+                pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
+                pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(40)
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         el = time.perf_counter() - t0
