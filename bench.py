@@ -187,9 +187,17 @@ def bench_model(model: str, B: int, args, rank: int, world: int, device, headlin
     # steps run at the steady clock a serving GPU runs at (20 timed steps at a cold clock measured
     # 47.6k / 90.6-91.1k img/s, 200 steps 50.0k / 93.5-96.0k, 20 after a 1 s spin-up 48.9-49.4k /
     # 93.3-94.6k, InceptionV3 / ResNet50, same box: profiles/r6_final/short_runs.txt)
-    t_end = time.perf_counter() + max(args.spinup_s, 0.0)
-    while time.perf_counter() < t_end:
-        pipe.run(4, table, record=False)
+    # The step count is agreed by every rank (each step runs collectives: a rank-local clock loop
+    # would leave the ranks in different collectives): time two steps after a first pair (graph
+    # capture), take the slowest rank's, run that many steps.
+    if args.spinup_s > 0:
+        pipe.run(2, table, record=False)
+        torch.cuda.synchronize()
+        t_s = time.perf_counter()
+        pipe.run(2, table, record=False)
+        torch.cuda.synchronize()
+        per = dp.max_over_ranks((time.perf_counter() - t_s) / 2)
+        pipe.run(max(1, int(min(4000, args.spinup_s / max(per, 1e-4)))), table, record=False)
         torch.cuda.synchronize()
     # warmup (graph capture, clocks, caches)
     pipe.run(max(args.warmup, 1), table, record=False)
