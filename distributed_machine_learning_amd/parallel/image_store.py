@@ -143,7 +143,7 @@ class HbmImageStore:
         shipment from a holder for the ones staged elsewhere; None if the new ones do not
         fit next to the pinned images (the caller stages fewer batches and retries later).
         Returns the window (possibly with no names)."""
-        want = [n for n in dict.fromkeys(names) if not self._synthetic(n)]
+        want = [n for n in dict.fromkeys(names) if not n.startswith(SYNTH)] if self.n_synth else list(dict.fromkeys(names))
         wset = set(want)
         new = [n for n in want if n not in self.index]
         move = [n for n in want if n in self.index and dst not in self.holders[n]]
@@ -193,21 +193,24 @@ class HbmImageStore:
             w.done = True
         return w
 
+    def _real(self, names: Sequence[str]) -> Sequence[str]:
+        """The store images of a batch (its synthetic rows live in the arena's seeded slots);
+        one pass, not a method call per name (these run per batch on the serve loop)."""
+        return [n for n in names if not n.startswith(SYNTH)] if self.n_synth else names
+
     def pin(self, names: Sequence[str]) -> None:
-        for n in names:
-            if not self._synthetic(n):
-                r = self.refs.get(n, 0)
-                if r == 0:
-                    self.idle.pop(n, None)
-                self.refs[n] = r + 1
+        refs, idle = self.refs, self.idle
+        for n in self._real(names):
+            r = refs.get(n, 0)
+            if r == 0:
+                idle.pop(n, None)
+            refs[n] = r + 1
 
     def unpin(self, names: Sequence[str]) -> None:
         """A batch completed (same step on every rank). Its images stay resident
         (evictable once unpinned) — except failed ones, which are forgotten so a
         later window fetches them again."""
-        for n in names:
-            if self._synthetic(n):
-                continue
+        for n in self._real(names):
             r = self.refs.get(n, 0) - 1
             if r > 0:
                 self.refs[n] = r
@@ -232,10 +235,9 @@ class HbmImageStore:
     # --------------------------------------------------------- readiness --
     def ready(self, names: Sequence[str]) -> bool:
         """Every image of a batch is resident on THIS rank."""
-        for n in names:
-            if self._synthetic(n):
-                continue
-            w = self.here.get(n)
+        here = self.here
+        for n in self._real(names):
+            w = here.get(n)
             if w is None or not w.done:
                 return False
         return True
@@ -248,12 +250,13 @@ class HbmImageStore:
     def slots(self, names: Sequence[str]) -> Tuple[List[int], List[str]]:
         """Arena slots of a batch staged here; failed images get slot 0 and are listed."""
         out, failed = [], []
+        syn, here, index = self.n_synth > 0, self.here, self.index
         for n in names:
-            if self._synthetic(n):
+            if syn and n.startswith(SYNTH):
                 out.append(int(n[len(SYNTH):]) % self.n_synth)
                 continue
-            w = self.here.get(n)
-            if n not in self.index or w is None or n in w.failed:
+            w = here.get(n)
+            if n not in index or w is None or n in w.failed:
                 failed.append(n)
                 out.append(0)
             else:
@@ -266,7 +269,7 @@ class HbmImageStore:
         from its arena (a holder), the all-to-all of the shipped rows and the all-reduce of
         the ok flags (both skipped when nothing needs them: identical decisions everywhere)."""
         cuda = self.device.type == "cuda"
-        ok = torch.zeros(len(w.names), dtype=torch.int32)
+        okn = np.zeros(len(w.names), np.int32)   # numpy: a torch __setitem__ per image cost ~1 ms per window
         local = None
         pack = getattr(got, "pack", None)   # GPU backend: full-resolution decodes, resized on the GPU
         if rank == w.dst and w.mine and pack is None:
@@ -275,16 +278,20 @@ class HbmImageStore:
                 img = got.get(n)
                 if img is not None:
                     local[j].numpy()[...] = img  # loader arrays may be read-only views
-        if rank == w.dst and w.mine:
-            self.decoded += sum(1 for n in w.mine if got.get(n) is not None)
-        pos = {n: i for i, n in enumerate(w.names)}
-        for n in w.mine:
-            if got.get(n) is not None:
-                ok[pos[n]] = 1
+        if w.mine:
+            good = [got.get(n) is not None for n in w.mine]
+            if rank == w.dst:
+                self.decoded += sum(good)
+            if len(w.mine) == len(w.names) and w.mine == w.names:   # a window of new images only
+                okn[:] = good
+            else:
+                pos = {n: i for i, n in enumerate(w.names)}
+                okn[[pos[n] for n, g in zip(w.mine, good) if g]] = 1
         out_rows = [i for i, s in enumerate(w.src) if s == rank and s != w.dst]   # shipped from here
         for i in out_rows:
             mine = w.ship_src.get(i)   # done (Stager.progress holds the issue until it is)
-            ok[i] = int(mine is not None and mine.done and w.names[i] not in mine.failed)
+            okn[i] = int(mine is not None and mine.done and w.names[i] not in mine.failed)
+        ok = torch.from_numpy(okn)
         ctx = torch.cuda.stream(stream) if (stream is not None and cuda) else _null()
         with ctx:
             if cuda and local is not None:
