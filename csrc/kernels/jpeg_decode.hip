@@ -278,25 +278,29 @@ __host__ __device__ static inline int16_t* block_at(const DmljImage& d, const Mc
   return coef + d.coef_off[c] + ((int64_t)by * d.bw[c] + bx) * 64;
 }
 
-// a bit reader that starts at any bit (the serial Bits starts at 0); same word layout
+// a bit reader that starts at any bit (the serial Bits starts at 0); same word layout. The next
+// refill's word is loaded one refill ahead (`nextw`), so its global-memory latency is off the
+// per-symbol dependency chain
 struct BitsAt {
   const uint32_t* w;
   int nw, wpos, nb;
   uint64_t buf;
+  uint32_t nextw;
   __host__ __device__ BitsAt(const uint32_t* words, int nwords, int bit) : w(words), nw(nwords) {
     wpos = bit >> 5;
     const uint32_t cur = wpos < nw ? w[wpos] : 0u;
     buf = ((uint64_t)cur << 32) << (bit & 31);
     nb = 32 - (bit & 31);
     ++wpos;
+    nextw = wpos < nw ? w[wpos] : 0u;
   }
   __host__ __device__ int pos() const { return wpos * 32 - nb; }
   __host__ __device__ void fill() {
     if (nb <= 32) {
-      const uint32_t nx = wpos < nw ? w[wpos] : 0u;
-      buf |= (uint64_t)nx << (32 - nb);
+      buf |= (uint64_t)nextw << (32 - nb);
       ++wpos;
       nb += 32;
+      nextw = wpos < nw ? w[wpos] : 0u;
     }
   }
   __host__ __device__ uint32_t peek(int n) const { return (uint32_t)(buf >> (64 - n)); }
