@@ -233,7 +233,6 @@ int dml_softmax_top5_split(float* logits, int B, int classes, int ld, int nsplit
                            float* probs_out, int* top_idx, float* top_p, hipStream_t s);
 int dml_preprocess(const DmlPreprocArgs* a, hipStream_t s);
 int dml_index_fetch(const int* host, int* dev, int n, hipStream_t s);  // pinned host table -> device
-int dml_gpu_delay(int us, hipStream_t s);  // stream-ordered delay (one sleeping wave)
 // packed full-resolution RGB images -> arena slots, nearest resize (misc.hip resize_nearest_kernel)
 int dml_resize_nearest(const void* pack, int n, int H, int W, void* dst, hipStream_t s);
 

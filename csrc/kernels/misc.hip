@@ -393,26 +393,6 @@ extern "C" int dml_resize_nearest(const void* pack, int n, int H, int W, void* d
   return 0;
 }
 
-// One wave that sleeps for `us` microseconds of the 100 MHz real-time counter (s_memrealtime, a
-// read): a stream-ordered delay, used to put one sub-batch stream half a forward behind the
-// other (SplitEngine phase shift: their large-grid early layers then overlap the other's
-// small-grid late layers instead of each other)
-__global__ __launch_bounds__(64) void dml_delay_kernel(long ticks) {
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while ((long)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(64);
-}
-
-extern "C" int dml_gpu_delay(int us, hipStream_t s) {
-  if (us <= 0) return 0;
-  if (us > 100000) {
-    dml_set_error("dml_gpu_delay: at most 100 ms");
-    return -1;
-  }
-  hipLaunchKernelGGL(dml_delay_kernel, dim3(1), dim3(64), 0, s, (long)us * 100);
-  DML_CHECK_LAUNCH();
-  return 0;
-}
-
 extern "C" int dml_index_fetch(const int* host, int* dev, int n, hipStream_t s) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(dml::index_fetch_kernel, dim3(1), dim3(n < 1024 ? ((n + 63) / 64) * 64 : 1024), 0, s, host, dev, n);

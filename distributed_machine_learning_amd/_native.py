@@ -122,7 +122,6 @@ _SIGS = {
                                          C.c_void_p, C.c_void_p, C.c_void_p]),
     "dml_preprocess": (C.c_int, [C.POINTER(PreprocArgs), C.c_void_p]),
     "dml_index_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
-    "dml_gpu_delay": (C.c_int, [C.c_int, C.c_void_p]),
     "dml_resize_nearest": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "dml_jpeg_prepare": (C.c_long, [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_long,
                                     C.c_void_p, C.c_void_p]),

@@ -926,10 +926,6 @@ class SplitEngine:
         # Measured in the serving pipeline (copy / compute / dispatch / RCCL
         # streams already live): 2 extra streams 49.1k img/s, 1 extra 58.3k.
         self.streams = [_extra_stream(self.device) for _ in range(self.nstreams - 1)]
-        # DML_PHASE_SHIFT_US: delay the extra streams once per serving run (pipeline.run sets
-        # _shift_pending); 0 = off
-        self.phase_shift_us = float(os.environ.get("DML_PHASE_SHIFT_US", "0"))
-        self._shift_pending = False
         self._fork = torch.cuda.Event()
         self._join = [torch.cuda.Event() for _ in range(self.nstreams - 1)]
 
@@ -1060,12 +1056,6 @@ class SplitEngine:
         for s in self.streams:
             for ev in deps:
                 s.wait_event(ev)
-        if self.phase_shift_us > 0 and self._shift_pending:
-            # once per serving run: the extra streams start this much behind the caller's, so in
-            # steady state one sub-batch's early layers overlap the other's late ones (A/B knob)
-            self._shift_pending = False
-            for s in self.streams:
-                N.check(N.lib().dml_gpu_delay(int(self.phase_shift_us), N.stream_ptr(s)), "dml_gpu_delay")
         for i in range(1, self.splits):  # extra streams' sub-batches first, then the caller's
             if i % self.nstreams:
                 self.engines[i].run(lanes[i % self.nstreams], use_graph=use_graph, slot=slot)

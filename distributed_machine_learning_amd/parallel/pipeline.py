@@ -172,8 +172,6 @@ class ServingPipeline:
         consumes batch k's rows once the gather after it has been issued, so it never
         waits behind a forward it has not yet queued a successor for."""
         dp, eng = self.dp, self.eng
-        if hasattr(eng, "_shift_pending"):   # SplitEngine phase shift (DML_PHASE_SHIFT_US): once per run
-            eng._shift_pending = True
         tr = _trace.get_tracer()
         is0 = dp.rank == 0
         recs: List[BatchRecord] = []
