@@ -97,8 +97,8 @@ def parse_args(argv=None):
     ap.add_argument("--svc-inception-images", type=int, default=25600,
                     help="InceptionV3 images per GPU (service run)")
     ap.add_argument("--svc-store-time-limit", type=float, default=300.0,
-                    help="seconds the store-image pass may serve before it is abandoned (reported as an error "
-                         "in its sub-record; the headline record is printed either way)")
+                    help="seconds each service pass (synthetic, store-image) may serve before it stops (its "
+                         "sub-record then covers what completed; the headline record is printed either way)")
     ap.add_argument("--svc-store-images", type=int, default=2048,
                     help="the `service_store` sub-record: the same concurrent jobs over this many distinct JPEGs "
                          "PUT into the replicated store (fetched, decoded once, staged into HBM on the timed path); "
@@ -345,7 +345,11 @@ def main(argv=None) -> int:
 
     svc = None
     if not args.dry_run and not args.no_service:
-        svc = bench_service(args, rank, world, device, recs)
+        try:  # the headline line is printed whatever happens in the service passes
+            svc = bench_service(args, rank, world, device, recs)
+        except Exception as e:  # noqa: BLE001 - reported in the record
+            print(f"bench: rank {rank}: service pass failed: {e}", file=sys.stderr, flush=True)
+            svc = {"error": str(e)[:500]}
 
     if rank == 0:
         head = recs[models[0]]
@@ -399,7 +403,8 @@ def bench_service(args, rank: int, world: int, device, recs: dict):
     rates = {m: r["value"] for m, r in recs.items() if r and "value" in r}
     out_dir = (os.path.join(args.svc_outputs, os.path.basename(rdzv) + "_outputs") if args.svc_outputs else None)
     rec = service_bench.run(rank, world, device, rdzv, port, args.svc_resnet_images * world,
-                            args.svc_inception_images * world, dict(DEFAULT_BATCH), out_dir, single_rates=rates)
+                            args.svc_inception_images * world, dict(DEFAULT_BATCH), out_dir, single_rates=rates,
+                            time_limit_s=args.svc_store_time_limit)
     if args.svc_store_images and rec is not None:
         # the reference's real workload: jobs over store images (worker.py:1361-1386) —
         # fetched from the replicated store, decoded once per job, staged into HBM windows
