@@ -102,6 +102,8 @@ class MsgType(IntEnum):
     DOWNLOAD_MANY_REPLY = 79  # {"ok": {name: versions}, "failed": [names]}
     FILES_STORED = 80        # writer -> leader: files it stored on their replicas itself (put_many_direct)
     FILES_STORED_ACK = 81
+    GET_OUTPUT = 82          # get-output at the coordinator: final_<job>.json from its gathered results
+    GET_OUTPUT_ACK = 83      # {"name": store name of the rendered final file, or None}
     ERROR = 127
 
 

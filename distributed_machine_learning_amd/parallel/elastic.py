@@ -150,6 +150,7 @@ class ElasticGroup:
         self.grank, self.backend, self.device = global_rank, backend, device
         self.data_backend = data_backend or backend
         self.data_group = None
+        self.result_group = None
         self._graveyard: list = []
         self.members: List[int] = list(range(world))
         self.prev_members: List[int] = list(self.members)   # the member list of the previous epoch
@@ -208,6 +209,9 @@ class ElasticGroup:
         # when a window's decode finishes, which is not ordered against the step's control
         # exchange across ranks (gloo / RCCL match collectives by issue order per group)
         self.data_group = dist.new_group(list(range(self.world)), backend=self.data_backend)
+        # the service's per-step result gather (top-5 rows -> the coordinator) on a group of its
+        # own too: it is issued at the same step on every rank, the windows' collectives are not
+        self.result_group = dist.new_group(list(range(self.world)), backend=self.data_backend)
         if self.shm_exchange:
             if self._shm is not None:
                 self._shm.close()
@@ -223,6 +227,7 @@ class ElasticGroup:
         if not dist.is_initialized():
             return
         self.data_group = None
+        self.result_group = None
         if abort:
             # every group of the epoch (RCCL: ncclCommAbort; gloo: closes the pairs, so an
             # image window's all-gather still pending on a peer that went on to rebuild
@@ -397,6 +402,20 @@ class ElasticGroup:
         """Issue a SUM all-reduce on the data group; returns the Work."""
         try:
             return dist.all_reduce(t, group=self.data_group, async_op=True)
+        except Exception as e:
+            raise CollectiveFailure(str(e)) from e
+
+    def gather_result(self, t: torch.Tensor, outs: Optional[List[torch.Tensor]], dst: int) -> None:
+        """gather on the result group (RCCL on a GPU node): ``outs`` (on ``dst`` only) <- every
+        rank's ``t``; ``dst`` is a GROUP rank."""
+        self._run(dist.gather, t, outs if self.rank == dst else None, dst=dst, group=self.result_group)
+
+    def gather_result_async(self, t, outs, dst):
+        """The result gather, not waited for (the service polls ``is_completed``); the
+        epoch's result group orders it against the other result gathers only."""
+        try:
+            return dist.gather(t, outs if self.rank == dst else None, dst=dst, group=self.result_group,
+                               async_op=True)
         except Exception as e:
             raise CollectiveFailure(str(e)) from e
 

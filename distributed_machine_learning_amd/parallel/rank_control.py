@@ -113,6 +113,7 @@ class RankControl:
         on(MsgType.GET_C2_COMMAND, self._on_c2)
         on(MsgType.GET_ASSIGNMENTS, self._on_c5)
         on(MsgType.JOB_STATUS, self._on_status)
+        on(MsgType.GET_OUTPUT, self._on_get_output)
         on(MsgType.FETCH_INTRODUCER, self._on_fetch_leader)   # every rank is an introducer for clients
         n.ml.on_fail.append(self._member_failed)
         n.ml.on_join.append(self._member_joined)
@@ -389,6 +390,28 @@ class RankControl:
                 a = self.svc.coord.assignments()
                 h = self.svc.coord.recent(int(p.get("history", 16)), p.get("job_id"))
             await self.node.ep.reply(fr, MsgType.GET_ASSIGNMENTS_ACK, {"assignments": a, "history": h})
+
+    async def _on_get_output(self, fr) -> None:
+        """get-output at the coordinator: final_<job>.json rendered once from the top-5 rows the
+        service gathered over the data group (CollectiveService.final_output), stored in the
+        replicated store; the requester fetches it by name. {"name": None} (not the coordinator,
+        or a batch of the job not gathered here, e.g. after a fail-over): the requester merges
+        the output files instead (the reference's get-output, worker.py:1617-1627)."""
+        from ..cluster.frames import MsgType
+
+        if not self._active() or self.svc is None:
+            await self.node.ep.reply(fr, MsgType.GET_OUTPUT_ACK, {"name": None})
+            return
+        jid = int(fr.payload["jobid"])
+        tag = self.svc.writer.host_tag if getattr(self.svc, "writer", None) is not None else "node"
+        loop = asyncio.get_running_loop()
+        data = await loop.run_in_executor(None, self.svc.final_output, jid, tag, 2.0)   # native render, GIL released
+        name = None
+        if data is not None:
+            name = f"final_{jid}.json"
+            ok, _ = await self.node.store.put(data, name)
+            name = name if ok else None
+        await self.node.ep.reply(fr, MsgType.GET_OUTPUT_ACK, {"name": name})
 
     async def _on_status(self, fr) -> None:
         from ..cluster.frames import MsgType

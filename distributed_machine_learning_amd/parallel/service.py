@@ -104,7 +104,7 @@ log = logging.getLogger(__name__)
 # Every rank contributes one int64 record of rec_len(world, depth) words per step.
 H_VALID, H_LOGLEN, H_STEP, H_FLAGS, H_NREP, H_NACK, H_NREQ, H_GROW = range(8)
 HDR = 8
-F_STOP, F_GROW = 1, 2
+F_STOP, F_GROW, F_FLUSH = 1, 2, 4   # F_FLUSH: every rank flushes its result rows this step
 RP_MAX = 16          # reports per rank per step (more wait for the next step)
 RV_MAX = 8           # revoke requests per step / answers per rank per step
 REP_W = 4            # report: job, batch, service_us, attempts
@@ -648,7 +648,33 @@ class CollectiveService:
         self.hostq: "deque[Batch]" = deque()             # dispatched to this rank, not launched
         self.gpu: "deque[_Launched]" = deque()           # launched, not finished (launch order)
         self.free_slots = list(range(self.slots))
-        self.done: "deque[Tuple[Batch, float, int]]" = deque()   # finished + written: (batch, service s, epoch)
+        # finished + written: (batch, service s, epoch, top-5 ids [n, 5] int32, probs [n, 5] fp32)
+        self.done: "deque[tuple]" = deque()
+        # the result collect (SURVEY §2.6 "gather: results"): each rank's reported batches' packed
+        # top-5 rows (40 B per image) go to the coordinator by a gather on the epoch's result group
+        # (RCCL over xGMI on a GPU node). Ranks hold their rows until some rank has
+        # ``collect_every`` reports pending, a job has finished, or the service stops: the
+        # coordinator decides and sets F_FLUSH in its record, so every rank flushes on the same
+        # step, with the same buffer shape (read off the step's exchange). The
+        # coordinator keeps the rows per job, so get-output renders final_<job>.json once from
+        # them (RankControl GET_OUTPUT) instead of listing and fetching every output file from
+        # the store. DML_COLLECT_RESULTS=0: off (the same value on every rank).
+        self.collect = os.environ.get("DML_COLLECT_RESULTS", "1") != "0"
+        # ~8k images a flush (32 b256 batches; 40 B an image, 320 KiB a rank's buffer)
+        self.collect_every = max(1, int(os.environ.get("DML_COLLECT_EVERY", "0")) or 8192 // max(1, backend.cap))
+        self.collect_flushes = 0
+        self._pend_epoch = -1
+        self._pend_rows: List[tuple] = []              # this rank's reports since the last flush
+        self._pend_keys: List[List[tuple]] = []        # per group rank: the (job, batch) keys it reported
+        self._pend_imgs: Dict[tuple, list] = {}        # (coordinator) finished batch -> its image names
+        # gathers in flight, oldest first: (work, done-event or None, tensors kept alive, host rows
+        # on the coordinator, keys, images); drained each step, so a flush never blocks the loop
+        self._gathers: "deque[tuple]" = deque()
+        self._flush_due = False
+        self.results: "OrderedDict[int, Dict[int, tuple]]" = OrderedDict()   # job -> batch -> (images, ids, probs)
+        self.results_jobs_max = 64
+        self.collected_rows = 0
+        self._results_lock = threading.Lock()   # the serve loop inserts, the control loop renders
         self.answers: List[Tuple[tuple, bool]] = []       # revoke answers for the next record
         self.launched = 0
         self.served_here = 0
@@ -719,7 +745,7 @@ class CollectiveService:
     # ----------------------------------------------------------- own work --
     def _written(self, b: Batch, tag) -> None:
         """(writer thread) output durable: reportable at the next step."""
-        self.done.append((b, tag[0], tag[1]))
+        self.done.append((b, tag[0], tag[1], tag[2], tag[3]))
 
     def _poll(self) -> int:
         """Finished GPU batches -> writer (or straight to the report list);
@@ -738,9 +764,10 @@ class CollectiveService:
             p = rows[1].view(np.float32).copy()
             self.free_slots.append(L.slot)
             if self.writer is not None and self.writer.enabled:
-                self.writer.submit(L.batch, idx, p, self.eg.grank, on_written=self._written, tag=(svc, L.epoch))
+                self.writer.submit(L.batch, idx, p, self.eg.grank, on_written=self._written,
+                                   tag=(svc, L.epoch, idx, p))
             else:
-                self.done.append((L.batch, svc, L.epoch))
+                self.done.append((L.batch, svc, L.epoch, idx, p))
             self.served_here += 1
             n += 1
         self.be.progress()  # image windows: decode shares, all-gathers, scatters (never blocks)
@@ -762,13 +789,13 @@ class CollectiveService:
         r[H_VALID] = 1
         reports = []
         while self.done and len(reports) < RP_MAX:
-            b, svc, ep = self.done.popleft()
+            b, svc, ep, ids, probs = self.done.popleft()
             if ep != self.eg.epoch:
                 continue  # requeued by a rebuild since: it runs again
-            reports.append((b, svc))
+            reports.append((b, svc, ids, probs))
         answers, self.answers = self.answers[:RV_MAX], self.answers[RV_MAX:]
         r[H_NREP] = len(reports)
-        for i, (b, svc) in enumerate(reports):
+        for i, (b, svc, _, _) in enumerate(reports):
             r[rep + i * REP_W: rep + (i + 1) * REP_W] = (b.job_id, b.batch_id, int(svc * 1e6), b.attempts)
         r[H_NACK] = len(answers)
         for i, (key, ok) in enumerate(answers):
@@ -776,7 +803,7 @@ class CollectiveService:
         if active:
             r[H_LOGLEN] = loglen
             r[H_STEP] = self.steps
-            r[H_FLAGS] = (F_STOP if stop else 0) | (F_GROW if grow else 0)
+            r[H_FLAGS] = (F_STOP if stop else 0) | (F_GROW if grow else 0) | (F_FLUSH if self._flush_wanted(stop) else 0)
             r[H_GROW] = sum(1 << g for g in grow)
             if table is not None:
                 r[tab:req] = table.reshape(-1)
@@ -847,8 +874,8 @@ class CollectiveService:
                     applied_here = json.loads(got.decode())
         except CollectiveFailure:
             # nothing of this step was applied anywhere: its reports and answers go again
-            for b, svc in reversed(reports):
-                self.done.appendleft((b, svc, self.eg.epoch))
+            for b, svc, ids, probs in reversed(reports):
+                self.done.appendleft((b, svc, self.eg.epoch, ids, probs))
             self.answers = answers + self.answers
             raise
         t3 = time.perf_counter()
@@ -898,6 +925,8 @@ class CollectiveService:
                       for i in range(int(h[root, H_NREQ]))]
                 coord.apply_requests(rq)
                 self._stage()
+        if self.collect:
+            self._collect(h, rep, world, root, active, reports, finished, bool(flags & F_FLUSH))
         if finished and active and self.control is not None:
             self.control.jobs_progress(finished)
         t4 = time.perf_counter()
@@ -954,6 +983,145 @@ class CollectiveService:
             ph["sleep"] += time.perf_counter() - t5
         return True
 
+    def _collect(self, h: np.ndarray, rep: int, world: int, root: int, active: bool, reports: list,
+                 finished: List[Batch], flush: bool) -> None:
+        """Queue the step's reported rows; on a flush step gather every rank's queued rows to
+        the coordinator (same step, same [k, cap, 10] int32 shape everywhere: k and the flush
+        decision come from the step's exchange, which every rank holds identically)."""
+        if self._pend_epoch != self.eg.epoch:   # a new group: every member starts empty
+            self._pend_epoch = self.eg.epoch
+            self._pend_rows, self._pend_imgs = [], {}
+            self._pend_keys = [[] for _ in range(world)]
+            self._gathers.clear()               # the old group's gathers died with it
+        self._drain_gathers()
+        n_new = 0
+        for r in range(world):
+            nr = int(h[r, H_NREP])
+            n_new += nr
+            for i in range(nr):
+                self._pend_keys[r].append((int(h[r, rep + i * REP_W]), int(h[r, rep + i * REP_W + 1])))
+        for b, _, ids, probs in reports:
+            self._pend_rows.append((len(b.images), ids, probs))
+        if active:
+            for b in finished:
+                self._pend_imgs[b.key] = list(b.images)
+                j = self.coord.jobs.jobs.get(b.key[0])
+                if j is not None and j.done:
+                    self._flush_due = True   # get-output of that job wants its last rows
+        k = max(len(p) for p in self._pend_keys)
+        if k == 0 or not flush:
+            return
+        self._flush_due = False
+        buf = np.zeros((k, self.cap, 10), np.int32)
+        for i, (n, ids, probs) in enumerate(self._pend_rows):
+            if ids is None or not n:
+                buf[i, :, 0] = -1        # no rows for this report: the coordinator skips it
+                continue
+            buf[i, :n, :5] = ids[:n]
+            buf[i, :n, 5:] = np.ascontiguousarray(probs[:n], dtype=np.float32).view(np.int32)
+        keys, imgs = self._pend_keys, self._pend_imgs
+        self._pend_rows, self._pend_imgs = [], {}
+        self._pend_keys = [[] for _ in range(world)]
+        self.collect_flushes += 1
+        if world == 1:
+            self._take_rows([buf], keys, imgs)
+            return
+        if getattr(self.eg, "data_backend", "gloo") == "nccl":
+            # a side stream: the gather and the coordinator's device->host copy wait for each
+            # other only, not for the model work queued on the serving streams
+            st = getattr(self, "_collect_stream", None)
+            if st is None:
+                st = self._collect_stream = torch.cuda.Stream(device=self.eg.device)
+            with torch.cuda.stream(st):
+                t = torch.from_numpy(buf).to(self.eg.device)
+                outs = [torch.empty_like(t) for _ in range(world)] if self.eg.rank == root else None
+                w = self.eg.gather_result_async(t, outs, root)
+                host, ev = None, None
+                if active:
+                    w.wait()   # stream-ordered: the copies below run after the gather
+                    host = torch.empty((world,) + tuple(buf.shape), dtype=torch.int32, pin_memory=True)
+                    for r in range(world):
+                        host[r].copy_(outs[r], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+            self._gathers.append((w, ev, (t, outs), host, keys if active else None, imgs))
+        else:
+            t = torch.from_numpy(buf)
+            outs = [torch.empty_like(t) for _ in range(world)] if self.eg.rank == root else None
+            w = self.eg.gather_result_async(t, outs, root)
+            self._gathers.append((w, None, (t, outs), outs if active else None, keys if active else None, imgs))
+
+    def _flush_wanted(self, stop: bool) -> bool:
+        """(coordinator, building its record) flush the result rows this step?"""
+        if not self.collect or not self._pend_keys:
+            return False
+        return stop or self._flush_due or max(len(p) for p in self._pend_keys) >= self.collect_every
+
+    def _drain_gathers(self, block: bool = False) -> None:
+        """Apply the finished result gathers, oldest first (``block``: wait for all of them:
+        the end of ``serve``)."""
+        while self._gathers:
+            w, ev, _, host, keys, imgs = self._gathers[0]
+            if not block and not (ev.query() if ev is not None else w.is_completed()):
+                return
+            self._gathers.popleft()
+            try:
+                if ev is not None:
+                    ev.synchronize()
+                else:
+                    w.wait()
+            except Exception as e:   # the group failed under it: those batches fall back to the files
+                log.warning("result gather failed: %s", e)
+                continue
+            if keys is not None:
+                got = host.numpy() if ev is not None else [o.numpy() for o in host]
+                self._take_rows(got, keys, imgs)
+
+    def _take_rows(self, got, keys: List[List[tuple]], imgs: Dict[tuple, list]) -> None:
+        for r in range(len(keys)):
+            for i, key in enumerate(keys[r]):
+                names = imgs.pop(key, None)
+                if names is None:   # a duplicate report (a re-run batch): the first one counted
+                    continue
+                rows = got[r][i, :len(names)]
+                if rows.shape[0] == 0 or rows[0, 0] < 0:
+                    continue
+                with self._results_lock:
+                    per = self.results.get(key[0])
+                    if per is None:
+                        per = self.results[key[0]] = {}
+                        while len(self.results) > self.results_jobs_max:
+                            self.results.popitem(last=False)
+                    per[key[1]] = (names, rows[:, :5].copy(), rows[:, 5:].copy().view(np.float32))
+                self.collected_rows += len(names)
+
+    def final_output(self, job_id: int, host_tag: str, wait_s: float = 0.0) -> Optional[bytes]:
+        """(coordinator) final_<job>.json from the gathered rows, byte-identical to get-output's
+        merge of the job's output files in store-listing order (worker.py:1617-1627); None until
+        every batch of the job has been collected here."""
+        from ..serving.output import output_name
+        end = time.monotonic() + wait_s   # a just-finished job's last rows flush within a few steps
+        while True:
+            with self.coord.lock:
+                j = self.coord.jobs.jobs.get(job_id)
+                total = j.batches_total if j is not None else -1
+            with self._results_lock:
+                per = dict(self.results.get(job_id) or {})
+            if per and total >= 0 and len(per) == total:
+                break
+            if time.monotonic() >= end or j is None or not j.done:
+                return None
+            time.sleep(0.01)
+        order = sorted(per, key=lambda bt: output_name(job_id, bt, host_tag))
+        return self._renderer().render_merged([per[bt] for bt in order])
+
+    def _renderer(self):
+        r = getattr(self, "_render", None)
+        if r is None:
+            from ..serving.output import BatchRenderer
+            r = self._render = BatchRenderer()
+        return r
+
     def _stage(self) -> None:
         """(every rank, same step, coordinator lock held) stage the images of the batches
         in flight - for the rank running each - and of the next ``stage_ahead`` queued
@@ -1009,6 +1177,7 @@ class CollectiveService:
                     break
             except CollectiveFailure as e:
                 self._recover(e)
+        self._drain_gathers(block=True)
         self.be.drain()
         if self.writer is not None:
             self.writer.flush()

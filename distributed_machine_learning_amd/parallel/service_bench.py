@@ -18,6 +18,7 @@ from __future__ import annotations
 import json
 import os
 import shutil
+import tempfile
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -210,6 +211,27 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
             pairs = {tuple(nm.split("_")[1:3]) for nm in listing}
             c2 = coord.metrics.c2()
             n = {m: coord.metrics.query_count.get(m, 0) for m in MODELS}
+            # get-output both ways: rendered at the coordinator from the rows the
+            # ranks gathered to it, against the reference's ls-all + fetch + merge of the files
+            go = {"collected_rows": svc.collected_rows, "flushes": svc.collect_flushes, "jobs": {}}
+            # (the file merge is Python json: bounded to jobs of at most 400k images)
+            for jid in sorted(j for j, jb in coord.jobs.jobs.items() if jb.n_images <= 400_000):
+                tg = time.perf_counter()
+                data = svc.final_output(jid, writer.host_tag, wait_s=2.0)
+                tg = time.perf_counter() - tg
+                ts = time.perf_counter()
+                path = ctl.call(ctl.node.merge_output_files(jid, os.path.join(tempfile.gettempdir(),
+                                                                             f"dml_final_{os.getpid()}_{jid}.json")),
+                                timeout=300)
+                ts = time.perf_counter() - ts
+                same = None
+                if data is not None and path:
+                    with open(path, "rb") as f:
+                        same = f.read() == data
+                    os.unlink(path)
+                go["jobs"][str(jid)] = {"gathered_render_ms": round(tg * 1e3, 2) if data is not None else None,
+                                        "merge_files_ms": round(ts * 1e3, 2), "bytes": len(data) if data else 0,
+                                        "identical": same}
             tot = sum(n.values())
             per_rank = {f"rank{g}": int(v[0]) for g, v in zip(eg.members, allsv)}
             rec = {
@@ -233,6 +255,7 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
                             "put_bundles_coordinator": writer.bundles,
                             "put_latency_ms_coordinator": _pcts(ctl.put_lat),
                             "writer_busy_s_coordinator": round(writer.busy_s, 3)},
+                "get_output": go,
                 "steps": steps, "max_batches_per_step": svc.batches_per_step_max,
                 "rebuilds": svc.rebuilds, "preempted_batches": coord.preempted, "requeued_batches": coord.requeued,
                 "kill_to_redispatch_s": [round(x, 3) for x in svc.recoveries_s],

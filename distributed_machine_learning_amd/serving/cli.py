@@ -5,7 +5,8 @@ Kept command-for-command:
   C2                      per-image processing time: mean, stdev, quartiles (+ p50/p90/p99)
   C3 <model> <batch>      set the per-model batch size on the coordinator
   submit-job <model> <N>  (C4) submit a job; prints the job id
-  get-output <jobid>      (C4) merge output_<jobid>_*.json -> final_<jobid>.json
+  get-output <jobid>      (C4) final_<jobid>.json: the rank service's coordinator renders it from the
+                          top-5 rows gathered over the data group; else merge output_<jobid>_*.json
   C5 [n [job]]            current assignments {worker: {model, job_id, batch_id}}; on the rank
                           service also the last n completed batches with the rank that ran each
   predict-locally <model> <jobid> <N|[a.jpeg,b.jpeg]>

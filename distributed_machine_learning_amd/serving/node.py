@@ -74,6 +74,7 @@ class Node:
         self._name = name
         self._backend = backend
         self.job_done: Dict[int, asyncio.Event] = {}
+        self.last_output_fast = False    # the last get_output came from the coordinator's gathered results
         self.started_at = time.monotonic()
 
     # ---------------------------------------------------------------- start --
@@ -119,6 +120,8 @@ class Node:
             self.worker = WorkerRole(self.ep, self.store, be, self.leader, self.name.replace(":", "_"),
                                      out_dir=cfg.out_dir)
         self.ep.on(MsgType.SUBMIT_JOB_REQUEST_SUCCESS, self._on_job_success)
+        # a rank-service RankControl replaces this with its gathered-results fast path
+        self.ep.on(MsgType.GET_OUTPUT, self._on_get_output)
         self.ml.on_fail.append(self._on_member_failed)
         self.ml.on_join.append(self._on_member_joined)
         self.ep.start()
@@ -188,6 +191,9 @@ class Node:
         jid = int(fr.payload["jobid"])
         self.job_done.setdefault(jid, asyncio.Event()).set()
 
+    async def _on_get_output(self, fr: Frame) -> None:
+        await self.ep.reply(fr, MsgType.GET_OUTPUT_ACK, {"name": None})
+
     # ------------------------------------------------------------- client --
     async def submit_job(self, model: str, n_images: int, timeout: float = 5.0) -> Optional[int]:
         leader = self.leader()
@@ -217,7 +223,28 @@ class Node:
 
     async def get_output(self, jid: int, dest_dir: str) -> Optional[str]:
         """Reference get-output (worker.py:1617-1627): ls-all output_<job>_*.json,
-        fetch all, merge into final_<job>.json."""
+        fetch all, merge into final_<job>.json. Under the rank service the coordinator
+        already holds every batch's top-5 (gathered over the data group) and returns the
+        store name of final_<job>.json rendered from them; the merge here is the fallback."""
+        os.makedirs(dest_dir, exist_ok=True)
+        path = os.path.join(dest_dir, f"final_{jid}.json")
+        # the rank service's coordinator renders final_<job>.json once from the results it
+        # gathered (RankControl GET_OUTPUT); anything else answers None: merge the files here
+        leader = self.leader()
+        if leader is not None:
+            r = await self.ep.request(leader, MsgType.GET_OUTPUT, {"jobid": jid}, timeout=self.store.timeout)
+            name = r.payload.get("name") if r is not None else None
+            if name:
+                got = await self.store.get(name)
+                if got:
+                    with open(path, "wb") as f:
+                        f.write(got[1])
+                    self.last_output_fast = True
+                    return path
+        self.last_output_fast = False
+        return await self.merge_output_files(jid, path)
+
+    async def merge_output_files(self, jid: int, path: str) -> Optional[str]:
         import json
 
         from .output import merge_outputs
@@ -230,8 +257,6 @@ class Node:
                 docs.append(json.loads(got[1]))
         if not docs:
             return None
-        os.makedirs(dest_dir, exist_ok=True)
-        path = os.path.join(dest_dir, f"final_{jid}.json")
         with open(path, "w") as f:
             json.dump(merge_outputs(docs), f, indent=4)
         return path

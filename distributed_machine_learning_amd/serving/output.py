@@ -157,6 +157,54 @@ class BatchRenderer:
         return C.string_at(buf, n)   # copies n bytes (buf.raw copied the whole 1 MiB scratch first)
 
 
+    def render_merged(self, batches: Sequence[Tuple[Sequence[str], np.ndarray, np.ndarray]]) -> bytes:
+        """final_<job>.json straight from the batches' top-5 rows (images, ids [n, 5], probs
+        [n, 5]; ids[i, 0] < 0 = failed), in the order get-output merges their files:
+        byte-identical to ``json.dump(merge_outputs([doc(b) for b in batches]), indent=4)``
+        where doc(b) is the batch's own output document (decoded images first, then the
+        failed ones; dict update keeps a key's first position, the last value wins)."""
+        if not batches:
+            return b"{}"
+        if not self.native:
+            docs = []
+            for names, ids, probs in batches:
+                bad = ids[:, 0] < 0
+                ok = [i for i in range(len(names)) if not bad[i]]
+                docs.append(decode_top5([names[i] for i in ok], ids[ok], probs[ok],
+                                        [names[i] for i in range(len(names)) if bad[i]], self.idx))
+            return dumps(merge_outputs(docs)).encode()
+        kc = self._keys
+        merged: Dict[bytes, int] = {}
+        off = 0
+        for names, ids, _ in batches:
+            keys = [kc[nm] if nm in kc else self._key(nm) for nm in names]
+            fl = (np.asarray(ids)[:, 0] < 0).tolist() if len(names) else []
+            ent: Dict[bytes, int] = {}
+            for i, k in enumerate(keys):
+                if not fl[i]:
+                    ent[k] = off + i
+            for i, k in enumerate(keys):
+                if fl[i]:
+                    ent[k] = -1
+            merged.update(ent)
+            off += len(names)
+        top_idx = np.ascontiguousarray(np.concatenate([np.asarray(b[1], np.int32) for b in batches]), np.int32)
+        top_p = np.ascontiguousarray(np.concatenate([np.asarray(b[2], np.float32) for b in batches]), np.float32)
+        keys = list(merged)
+        rows = np.fromiter(merged.values(), np.int32, len(keys))
+        koff = np.zeros(len(keys) + 1, np.int64)
+        np.cumsum(np.fromiter(map(len, keys), np.int64, len(keys)), out=koff[1:])
+        blob = b"".join(keys)
+        need = 256 + len(blob) + len(keys) * 5 * 160
+        buf = C.create_string_buffer(need)
+        n = self.lib.dml_render_top5_json(len(keys), blob, koff.ctypes.data, rows.ctypes.data, top_idx.ctypes.data,
+                                          top_p.ctypes.data, 5, self.cls, self.cls_off.ctypes.data, len(self.idx),
+                                          buf, need)
+        if n < 0:
+            raise RuntimeError("final output render buffer too small")
+        return C.string_at(buf, n)
+
+
 _host = None
 _host_lock = threading.Lock()
 

@@ -98,6 +98,10 @@ def test_launcher_cli_roundtrip_and_version_pinning(tmp_path):
                    "submit": await cli.run_line("submit-job ResNet50 12"),
                    "wait": await cli.run_line("wait-job 31 120"),
                    "get": await cli.run_line("get-output 31")}
+            # get-output came from the coordinator's gathered top-5, byte-identical
+            # to merging the per-batch output files from the store
+            out["fast"] = client.last_output_fast
+            out["slow"] = await client.merge_output_files(31, str(tmp_path / "slow_31.json"))
             # a new version of 3.jpeg, then a second job over the same images
             from PIL import Image
 
@@ -117,6 +121,8 @@ def test_launcher_cli_roundtrip_and_version_pinning(tmp_path):
     assert "loaded 12/12" in out["load"], out
     assert "submitted job 31" in out["submit"] and "finished" in out["wait"], out
     assert "submitted job 32" in out["submit2"] and "finished" in out["wait2"], out
+    assert out["fast"] is True, out
+    assert open(out["slow"], "rb").read() == open(tmp_path / "dl" / "final_31.json", "rb").read()
     f1 = json.load(open(tmp_path / "dl" / "final_31.json"))
     f2 = json.load(open(tmp_path / "dl" / "final_32.json"))
     assert len(f1) == len(f2) == 12
@@ -222,6 +228,65 @@ def test_rank_rejoin_after_kill(tmp_path, victim):
     assert keys == {(str(j), str(b)) for j in (31, 32) for b in range(1, 201)}
 
 
+# --------------------------------------------------------- result collect --
+def _collect_rank(grank, world, rdzv, out, every):
+    os.environ["DML_COLLECT_EVERY"] = str(every)
+    from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
+    from distributed_machine_learning_amd.parallel.rank_backend import StoreRankBackend
+    from distributed_machine_learning_amd.parallel.service import (CollectiveService, OutputWriter,
+                                                                   ReplicatedCoordinator)
+
+    be = StoreRankBackend(loader=lambda ns: {n: (n * 7).encode() for n in ns}, cap=8, arena_images=4096)
+    eg = ElasticGroup(grank, world, store_path=rdzv, backend="gloo", timeout_s=60, shm_exchange=True)
+    coord = ReplicatedCoordinator({"ResNet50": 8, "InceptionV3": 6}, cap=8, depth=3)
+    writer = OutputWriter(os.path.join(out, "outputs"), host_tag="t")
+    svc = CollectiveService(eg, be, coord, writer=writer)
+    if svc.is_coordinator():
+        svc.submit_local("ResNet50", images=[f"r{i}.jpeg" for i in range(203)])     # a partial last batch
+        svc.submit_local("InceptionV3", images=[f"i{i}.jpeg" for i in range(97)])
+    svc.serve(stop_when_idle=True)
+    writer.close()
+    if svc.is_coordinator():
+        for j in sorted(coord.jobs.jobs):
+            data = svc.final_output(j, "t")
+            with open(os.path.join(out, f"gathered_{j}.json"), "wb") as f:
+                f.write(data if data is not None else b"")
+        json.dump({"flushes": svc.collect_flushes, "rows": svc.collected_rows, "steps": svc.steps},
+                  open(os.path.join(out, "collect.json"), "w"))
+    eg.barrier()
+    eg.close()
+
+
+@pytest.mark.parametrize("every", [1, 32])
+def test_result_collect_matches_output_files_world3(tmp_path, every):
+    """SURVEY §2.6 'gather: results': the coordinator's final_<job>.json, rendered from the
+    top-5 rows every rank gathered to it over the result group, is byte-identical to the
+    reference's get-output merge of the per-batch output files (worker.py:1617-1627).
+    every = 1: a gather on every step with reports; 32: rows held until a rank has 32
+    pending or a job finishes."""
+    from distributed_machine_learning_amd.serving.output import merge_outputs
+
+    world = 3
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_collect_rank, args=(r, world, str(tmp_path / "rdzv"), str(tmp_path), every))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(180)
+    assert [p.exitcode for p in ps] == [0] * world
+    st = json.load(open(tmp_path / "collect.json"))
+    assert st["rows"] == 203 + 97, st
+    if every == 32:
+        assert st["flushes"] < st["steps"] / 4, st
+    files = sorted(os.listdir(tmp_path / "outputs"))
+    for j in (31, 32):
+        docs = [json.load(open(tmp_path / "outputs" / f)) for f in files if f.startswith(f"output_{j}_")]
+        want = json.dumps(merge_outputs(docs), indent=4).encode()
+        got = open(tmp_path / f"gathered_{j}.json", "rb").read()
+        assert got == want, (j, len(got), len(want))
+
+
 # ------------------------------------------------------ control capacity --
 def _cap_rank(grank, world, rdzv, out):
     from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
@@ -311,6 +376,10 @@ def test_service_bench_record_world2(tmp_path):
     assert set(r0["batches_per_rank"]) == {"rank0", "rank1"} and sum(r0["batches_per_rank"].values()) == 80
     assert r0["value"] > 0 and r0["p90_latency_ms"]["ResNet50"] >= r0["p50_latency_ms"]["ResNet50"]
     assert not os.path.exists(tmp_path / "svc_out")            # rank 0 removed the output files
+    # get-output from the rows gathered to the coordinator == the merge of the stored files
+    go = r0["get_output"]
+    assert go["collected_rows"] == 960 and len(go["jobs"]) == 2, go
+    assert all(j["identical"] is True and j["bytes"] > 0 for j in go["jobs"].values()), go
 
 
 def _svc_store_rank(grank, world, rdzv, port, out):

@@ -225,3 +225,33 @@ def test_coordinator_failover_to_standby(tmp_path):
         await _stop(nodes)
 
     asyncio.run(main())
+
+
+def test_render_merged_equals_get_output_merge():
+    """final_<job>.json rendered once from the gathered top-5 rows (BatchRenderer.render_merged)
+    is byte-identical to get-output's merge of the batches' output files (json.dump of
+    merge_outputs, indent 4): duplicates across and within batches (cyclic picks), failed
+    images, the batches' file order."""
+    import json
+
+    import numpy as np
+
+    from distributed_machine_learning_amd.serving.output import BatchRenderer, merge_outputs
+
+    r = BatchRenderer()
+    rng = np.random.default_rng(3)
+    batches = []
+    for b in range(5):
+        names = [f"{(b * 7 + i) % 23}.jpeg" for i in range(9)] + ["dup.jpeg"]
+        ids = rng.integers(0, 1000, (10, 5)).astype(np.int32)
+        probs = rng.random((10, 5)).astype(np.float32)
+        if b % 2:
+            ids[3, 0] = -1          # a failed image
+        if b == 3:
+            ids[9, 0] = -1          # dup.jpeg fails in one batch only
+        batches.append((names, ids, probs))
+    docs = [json.loads(r.render(n, i, p)) for n, i, p in batches]
+    want = json.dumps(merge_outputs(docs), indent=4).encode()
+    assert r.render_merged(batches) == want
+    r.native = False
+    assert r.render_merged(batches) == want
