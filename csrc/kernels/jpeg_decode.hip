@@ -217,7 +217,7 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_
 
 // --------------------------------------------------------- parallel entropy decoding --
 // one wave decoding each image serially put ~one wave per CU to work for ~7 ms per
-// 256-image window. Here DMLJ_PT threads (one wave) decode one image: thread t owns the
+// 256-image window. Here a workgroup of PT threads decodes one image: thread t owns the
 // symbols that START in bit segment t of the entropy stream. Huffman codes self-synchronise, so
 //   1. every thread decodes its segment from a guessed state (MCU slot 0, coefficient 0) and
 //      records its EXIT: the first symbol boundary at or past the segment end, with the decoder
@@ -231,12 +231,16 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_
 //   4. the DC predictions are rebuilt per component by a block-wide prefix sum in decode order.
 // The per-symbol code (tables, fast AC path, corrupt-code handling) is the serial decoder's,
 // so the coefficients are identical to it (tests/test_jpeg_decode.py compares every block).
-// 64 segments (one wave per image): a decoder started in the wrong state re-joins the true symbol
-// AND block-slot sequence after ~5,000 bits on the bench / reference photos (CPU replay, 40
-// images), so the Jacobi rounds x segment length is ~5,500 bits whatever the segment count
-// (256 / 128 / 64 / 32 segments: 12.9 / 6.2 / 3.1 / 1.6 rounds); fewer segments cut the total
-// work (rounds x stream) 4x against 256 at the same latency, and one wave needs no LDS barrier
+// Segments per image: a decoder started in the wrong state re-joins the true symbol AND
+// block-slot sequence after ~5,000 bits (CPU replay, 40 bench images: 64 / 128 / 256 segments
+// take 2.5 / 4.7 / 9.5 rounds), so a lane's bits (2 + rounds) x segment fall only 10.6k -> 7.0k
+// from 64 to 256 segments. But the kernel is latency-bound with one image per workgroup and only
+// 256 images a window: 64 threads leave three of a CU's four SIMDs idle. 256 threads (4 waves)
+// won on the box (r6, profiles/r6_pt): window 2.96-3.00 -> 2.08-2.11 ms, 4 windows in flight
+// 4.02-4.11 -> 2.97-2.99 ms, the 51,200-distinct pass 48.3k -> 52.5k images/s.
+// DMLJ_PT stays the CPU replay's default; the GPU launch takes DMLJ_PT_GPU (DML_JPEG_PT: A/B)
 #define DMLJ_PT 64
+#define DMLJ_PT_GPU 256
 
 struct PState {
   int pos, u, k;   // bit position of the next symbol; MCU block slot; next coefficient (0 = DC)
@@ -563,20 +567,37 @@ __global__ __launch_bounds__(64) void jpeg_huff_kernel(const unsigned char* __re
   decode_entropy(ds[i], (const uint32_t*)(buf + ds[i].stream_off), coef, true);
 }
 
-// the parallel decode of one image per workgroup (see "parallel entropy decoding" above)
-__global__ __launch_bounds__(DMLJ_PT) void jpeg_huff_par_kernel(const unsigned char* __restrict__ buf, int n,
-                                                                int16_t* __restrict__ coef) {
+// the parallel decode of one image per workgroup of PT threads = PT segments (see "parallel
+// entropy decoding" above). r6 A/B: staging the image's entropy words in LDS first changed
+// nothing (window 3.13-3.22 vs 3.21-3.28 ms, profiles/r6_lds): the per-symbol chain is not
+// waiting on the stream reads
+template <int PT>
+struct ParLds {
+  uint32_t lk_dc[3][512], lk_ac[3][512], fs_ac[3][512];
+  int ex_pos[2][PT], ex_u[2][PT], ex_k[2][PT], scan[2][PT];
+  int chg[3];
+};
+
+template <int PT>
+__global__ __launch_bounds__(PT) void jpeg_huff_par_kernel(const unsigned char* __restrict__ buf, int n,
+                                                           int16_t* __restrict__ coef) {
   const int i = blockIdx.x;
   if (i >= n) return;
   const DmljImage& d = ((const DmljImage*)(buf + 16))[i];
   if (!d.ok) return;   // uniform over the workgroup
-  __shared__ uint32_t lk_dc[3][512], lk_ac[3][512], fs_ac[3][512];
-  __shared__ int ex_pos[2][DMLJ_PT], ex_u[2][DMLJ_PT], ex_k[2][DMLJ_PT], scan[2][DMLJ_PT];
-  __shared__ int chg[3];
+  __shared__ ParLds<PT> L;
+  auto& lk_dc = L.lk_dc;
+  auto& lk_ac = L.lk_ac;
+  auto& fs_ac = L.fs_ac;
+  auto& ex_pos = L.ex_pos;
+  auto& ex_u = L.ex_u;
+  auto& ex_k = L.ex_k;
+  auto& scan = L.scan;
+  auto& chg = L.chg;
   const int t = threadIdx.x;
   const int nc = d.ncomp;
   for (int c = 0; c < nc; ++c)
-    for (int j = t; j < 512; j += DMLJ_PT) {
+    for (int j = t; j < 512; j += PT) {
       lk_dc[c][j] = d.dc[d.td[c]].look[j];
       lk_ac[c][j] = d.ac[d.ta[c]].look[j];
       fs_ac[c][j] = d.ac[d.ta[c]].fast[j];
@@ -586,7 +607,7 @@ __global__ __launch_bounds__(DMLJ_PT) void jpeg_huff_par_kernel(const unsigned c
   const McuMap m = mcu_map(d);
   const uint32_t* stream = (const uint32_t*)(buf + d.stream_off);
   const int nw = (d.stream_len + 3) / 4;
-  const int SEG = seg_bits(d), nbits = d.stream_len * 8;
+  const int SEG = seg_bits(d, PT), nbits = d.stream_len * 8;
   const int nseg = (nbits + SEG - 1) / SEG;
   const bool live = t < nseg;
   const int end = live ? min((t + 1) * SEG, nbits) : 0;
@@ -625,7 +646,7 @@ __global__ __launch_bounds__(DMLJ_PT) void jpeg_huff_par_kernel(const unsigned c
   int sc = 0;
   scan[0][t] = live ? nb : 0;
   __syncthreads();
-  for (int off = 1; off < DMLJ_PT; off <<= 1) {
+  for (int off = 1; off < PT; off <<= 1) {
     const int v = scan[sc][t] + (t >= off ? scan[sc][t - off] : 0);
     scan[sc ^ 1][t] = v;
     __syncthreads();
@@ -637,7 +658,7 @@ __global__ __launch_bounds__(DMLJ_PT) void jpeg_huff_par_kernel(const unsigned c
   // 4. DC predictions per component: block-wide prefix over the differences in decode order
   for (int c = 0; c < nc; ++c) {
     const int hs = nc == 1 ? 1 : d.hs[c], vs = nc == 1 ? 1 : d.vs[c];
-    const int nbc = d.bw[c] * d.bh[c], per = (nbc + DMLJ_PT - 1) / DMLJ_PT;
+    const int nbc = d.bw[c] * d.bh[c], per = (nbc + PT - 1) / PT;
     const int j0 = min(t * per, nbc), j1 = min(j0 + per, nbc);
     auto dcp = [&](int j) -> int16_t* {
       const int mcu = j / (hs * vs), w = j - mcu * (hs * vs);
@@ -650,7 +671,7 @@ __global__ __launch_bounds__(DMLJ_PT) void jpeg_huff_par_kernel(const unsigned c
     scan[0][t] = sum;
     __syncthreads();
     sc = 0;
-    for (int off = 1; off < DMLJ_PT; off <<= 1) {
+    for (int off = 1; off < PT; off <<= 1) {
       const int v = scan[sc][t] + (t >= off ? scan[sc][t - off] : 0);
       scan[sc ^ 1][t] = v;
       __syncthreads();
@@ -665,6 +686,7 @@ __global__ __launch_bounds__(DMLJ_PT) void jpeg_huff_par_kernel(const unsigned c
     __syncthreads();
   }
 }
+
 
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const unsigned char* __restrict__ buf, int n,
                                                         const int16_t* __restrict__ coef, uint8_t* __restrict__ work) {
@@ -1001,10 +1023,16 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
   // the parallel segment decode (a workgroup per image); DML_JPEG_SERIAL=1: the r5 one-wave serial
   // decode (A/B)
   static const bool serial = getenv("DML_JPEG_SERIAL") && getenv("DML_JPEG_SERIAL")[0] == '1';
+  // DML_JPEG_PT=64/128/256: segments (threads) per image (A/B; default DMLJ_PT_GPU)
+  static const int pt = getenv("DML_JPEG_PT") ? atoi(getenv("DML_JPEG_PT")) : DMLJ_PT_GPU;
   if (serial)
     hipLaunchKernelGGL(dml::jpg::jpeg_huff_kernel, dim3(n), dim3(64), 0, s, b, n, coef);
+  else if (pt == 256)
+    hipLaunchKernelGGL(dml::jpg::jpeg_huff_par_kernel<256>, dim3(n), dim3(256), 0, s, b, n, coef);
+  else if (pt == 128)
+    hipLaunchKernelGGL(dml::jpg::jpeg_huff_par_kernel<128>, dim3(n), dim3(128), 0, s, b, n, coef);
   else
-    hipLaunchKernelGGL(dml::jpg::jpeg_huff_par_kernel, dim3(n), dim3(DMLJ_PT), 0, s, b, n, coef);
+    hipLaunchKernelGGL(dml::jpg::jpeg_huff_par_kernel<64>, dim3(n), dim3(64), 0, s, b, n, coef);
   DML_CHECK_LAUNCH();
   hipLaunchKernelGGL(dml::jpg::jpeg_idct_kernel, dim3((maxblk + 255) / 256, n), dim3(256), 0, s, b, n, coef,
                      (uint8_t*)dwork);
@@ -1093,10 +1121,10 @@ extern "C" int dml_jpeg_parallel_host(const unsigned char* data, long len, short
   }
   const uint32_t* w = (const uint32_t*)stream;
   const int nw = (d.stream_len + 3) / 4;
-  const int want = info[1] > 0 && info[1] <= DMLJ_PT ? (int)info[1] : DMLJ_PT;   // segments (A/B)
+  const int want = info[1] > 0 && info[1] <= 256 ? (int)info[1] : DMLJ_PT;   // segments (A/B: up to 256)
   const int SEG = seg_bits(d, want), nbits = d.stream_len * 8, nseg = (nbits + SEG - 1) / SEG;
-  PState start[DMLJ_PT], ex[DMLJ_PT], nex[DMLJ_PT];
-  int nb[DMLJ_PT] = {0};
+  PState start[256], ex[256], nex[256];
+  int nb[256] = {0};
   for (int t = 0; t < nseg; ++t) {
     start[t] = PState{t * SEG, 0, 0};
     ex[t] = seg_decode<false>(d, m, tb, w, nw, start[t], std::min((t + 1) * SEG, nbits), &nb[t], 0, nullptr);
