@@ -994,17 +994,16 @@ class CollectiveService:
             self._pend_keys = [[] for _ in range(world)]
             self._gathers.clear()               # the old group's gathers died with it
         self._drain_gathers()
-        n_new = 0
+        nreps = h[:, H_NREP].tolist()
         for r in range(world):
-            nr = int(h[r, H_NREP])
-            n_new += nr
-            for i in range(nr):
-                self._pend_keys[r].append((int(h[r, rep + i * REP_W]), int(h[r, rep + i * REP_W + 1])))
+            if nreps[r]:
+                v = h[r, rep: rep + nreps[r] * REP_W].tolist()
+                self._pend_keys[r].extend(zip(v[0::REP_W], v[1::REP_W]))
         for b, _, ids, probs in reports:
             self._pend_rows.append((len(b.images), ids, probs))
         if active:
             for b in finished:
-                self._pend_imgs[b.key] = list(b.images)
+                self._pend_imgs[b.key] = b.images   # a batch's names are never mutated (lazy for synthetic jobs)
                 j = self.coord.jobs.jobs.get(b.key[0])
                 if j is not None and j.done:
                     self._flush_due = True   # get-output of that job wants its last rows
@@ -1074,7 +1073,8 @@ class CollectiveService:
                 log.warning("result gather failed: %s", e)
                 continue
             if keys is not None:
-                got = host.numpy() if ev is not None else [o.numpy() for o in host]
+                # (pinned staging is copied out once: the kept rows must not pin host memory)
+                got = host.numpy().copy() if ev is not None else [o.numpy() for o in host]
                 self._take_rows(got, keys, imgs)
 
     def _take_rows(self, got, keys: List[List[tuple]], imgs: Dict[tuple, list]) -> None:
@@ -1092,7 +1092,7 @@ class CollectiveService:
                         per = self.results[key[0]] = {}
                         while len(self.results) > self.results_jobs_max:
                             self.results.popitem(last=False)
-                    per[key[1]] = (names, rows[:, :5].copy(), rows[:, 5:].copy().view(np.float32))
+                    per[key[1]] = (names, rows[:, :5], rows[:, 5:].view(np.float32))   # views of the gathered buffer
                 self.collected_rows += len(names)
 
     def final_output(self, job_id: int, host_tag: str, wait_s: float = 0.0) -> Optional[bytes]:
