@@ -128,11 +128,10 @@ struct Bits {
 // the host side of the word reads above: swap each 4-byte group of the (zero-padded) stream
 static void swap_words(uint8_t* p, long len) {
   for (long i = 0; i + 4 <= len; i += 4) {
-    const uint8_t a = p[i], b = p[i + 1];
-    p[i] = p[i + 3];
-    p[i + 1] = p[i + 2];
-    p[i + 2] = b;
-    p[i + 3] = a;
+    uint32_t w;
+    memcpy(&w, p + i, 4);
+    w = __builtin_bswap32(w);
+    memcpy(p + i, &w, 4);
   }
 }
 
@@ -759,6 +758,32 @@ static int build_huff(const uint8_t* counts, const uint8_t* vals, int nvals, Dml
   return 0;
 }
 
+// the same tables recur across a window (encoders write their standard or per-quality tables):
+// a small per-thread cache keyed by the DHT bytes (counts + values) copies a built table instead
+// of rebuilding its 512-entry lookups
+static int build_huff_cached(const uint8_t* counts, const uint8_t* vals, int nvals, DmljHuff& t) {
+  struct Ent {
+    int n = -1;
+    uint8_t key[16 + 256];
+    DmljHuff tab;
+  };
+  static thread_local Ent cache[8];
+  static thread_local int next = 0;
+  for (Ent& e : cache)
+    if (e.n == nvals && !memcmp(e.key, counts, 16) && !memcmp(e.key + 16, vals, nvals)) {
+      memcpy(&t, &e.tab, sizeof t);
+      return 0;
+    }
+  if (build_huff(counts, vals, nvals, t) != 0) return -1;
+  Ent& e = cache[next];
+  next = (next + 1) & 7;
+  e.n = nvals;
+  memcpy(e.key, counts, 16);
+  memcpy(e.key + 16, vals, nvals);
+  memcpy(&e.tab, &t, sizeof t);
+  return 0;
+}
+
 static void nearest_tab(int n_in, int n_out, int16_t* tab) {
   // Pillow NEAREST: a float64 accumulator started at half a step, sequential adds, truncation
   // (rank_backend.nearest_index)
@@ -814,7 +839,7 @@ static int parse_one(const uint8_t* p, int64_t len, DmljImage& d, uint8_t* out, 
         int nv = 0;
         for (int k = 0; k < 16; ++k) nv += s[o + 1 + k];
         if (o + 17 + nv > sl || nv > 256) return -1;
-        if (build_huff(s + o + 1, s + o + 17, nv, tc ? d.ac[th] : d.dc[th]) != 0) return -1;
+        if (build_huff_cached(s + o + 1, s + o + 17, nv, tc ? d.ac[th] : d.dc[th]) != 0) return -1;
         o += 17 + nv;
       }
     } else if (m == 0xC0 || m == 0xC1) {         // baseline / extended sequential, Huffman
@@ -857,6 +882,16 @@ static int parse_one(const uint8_t* p, int64_t len, DmljImage& d, uint8_t* out, 
       int64_t j = i + seglen, o = 0;
       bool ended = false;
       while (j < len) {
+        // copy the run up to the next 0xFF at once (entropy bytes are mostly not 0xFF)
+        const uint8_t* ff = (const uint8_t*)memchr(p + j, 0xFF, (size_t)(len - j));
+        const int64_t run = ff ? ff - (p + j) : len - j;
+        if (run > 0) {
+          if (o + run > cap) return -1;
+          memcpy(out + o, p + j, (size_t)run);
+          o += run;
+          j += run;
+          if (j >= len) break;
+        }
         const uint8_t b = p[j];
         if (b == 0xFF) {
           if (j + 1 >= len) break;
