@@ -631,7 +631,12 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         self._fetch = N.lib().dml_index_fetch
         self.stream = torch.cuda.Stream(device)
         self.stage_stream = torch.cuda.Stream(device)
-        self._init_staging(loader, decode_threads)
+        # the staging pool (a window's fetch + GPU-JPEG prepare each) shares the interpreter with
+        # the serve loop: 4 threads, not decode_threads (51,200-distinct pass on one box, 2 rounds:
+        # 4 threads 54.6k / 55.0k images/s, serve-loop launch phase 0.18 s; 32 threads 53.7k /
+        # 51.2k, 0.35-0.40 s; profiles/r6_n). DML_STAGING_THREADS overrides; the CPU decode pool
+        # (_jpool, decode worker processes behind it) keeps decode_threads
+        self._init_staging(loader, int(os.environ.get("DML_STAGING_THREADS", "4")))
         import threading
 
         self._dcache: "OrderedDict[str, np.ndarray]" = OrderedDict()   # name -> full-res RGB (both models)

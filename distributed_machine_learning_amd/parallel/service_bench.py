@@ -102,7 +102,8 @@ def run(rank: int, world: int, device, rdzv: str, swim_base: int, resnet_images:
     depth = depth or auto_depth(world)
     # store images: room for every distinct image next to the pinned in-flight and staged batches
     arena = max(4 * cap, store_images + world * (depth + STAGE_DEPTH) * cap) if store_images else 4 * cap
-    decode_threads = decode_threads or numa.host_threads(share=1, cap=32)
+    # DML_DECODE_THREADS: the staging pool's size (A/B)
+    decode_threads = decode_threads or int(os.environ.get("DML_DECODE_THREADS", "0")) or numa.host_threads(share=1, cap=32)
     loader = {}   # the store loader exists once the control plane runs (below)
     lazy_loader = lambda names: loader["fn"](names)  # noqa: E731
     if make_backend is not None:  # a factory may take the (lazy) store loader
