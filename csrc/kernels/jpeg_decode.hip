@@ -237,6 +237,8 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_
 // 256 images a window: 64 threads leave three of a CU's four SIMDs idle. 256 threads (4 waves)
 // won on the box (r6, profiles/r6_pt): window 2.96-3.00 -> 2.08-2.11 ms, 4 windows in flight
 // 4.02-4.11 -> 2.97-2.99 ms, the 51,200-distinct pass 48.3k -> 52.5k images/s.
+// 512 threads (replay: 18.7 rounds, 6.5k bits a lane) measured the same as 256 on the box
+// (window 2.10-2.17 vs 2.14-2.45 ms, profiles/r6_p): 256 stays.
 // DMLJ_PT stays the CPU replay's default; the GPU launch takes DMLJ_PT_GPU (DML_JPEG_PT: A/B)
 #define DMLJ_PT 64
 #define DMLJ_PT_GPU 256
@@ -1062,6 +1064,8 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
   static const int pt = getenv("DML_JPEG_PT") ? atoi(getenv("DML_JPEG_PT")) : DMLJ_PT_GPU;
   if (serial)
     hipLaunchKernelGGL(dml::jpg::jpeg_huff_kernel, dim3(n), dim3(64), 0, s, b, n, coef);
+  else if (pt == 512)
+    hipLaunchKernelGGL(dml::jpg::jpeg_huff_par_kernel<512>, dim3(n), dim3(512), 0, s, b, n, coef);
   else if (pt == 256)
     hipLaunchKernelGGL(dml::jpg::jpeg_huff_par_kernel<256>, dim3(n), dim3(256), 0, s, b, n, coef);
   else if (pt == 128)
@@ -1156,10 +1160,10 @@ extern "C" int dml_jpeg_parallel_host(const unsigned char* data, long len, short
   }
   const uint32_t* w = (const uint32_t*)stream;
   const int nw = (d.stream_len + 3) / 4;
-  const int want = info[1] > 0 && info[1] <= 256 ? (int)info[1] : DMLJ_PT;   // segments (A/B: up to 256)
+  const int want = info[1] > 0 && info[1] <= 512 ? (int)info[1] : DMLJ_PT;   // segments (A/B: up to 512)
   const int SEG = seg_bits(d, want), nbits = d.stream_len * 8, nseg = (nbits + SEG - 1) / SEG;
-  PState start[256], ex[256], nex[256];
-  int nb[256] = {0};
+  PState start[512], ex[512], nex[512];
+  int nb[512] = {0};
   for (int t = 0; t < nseg; ++t) {
     start[t] = PState{t * SEG, 0, 0};
     ex[t] = seg_decode<false>(d, m, tb, w, nw, start[t], std::min((t + 1) * SEG, nbits), &nb[t], 0, nullptr);
