@@ -1056,13 +1056,23 @@ class CollectiveService:
             return False
         return stop or self._flush_due or max(len(p) for p in self._pend_keys) >= self.collect_every
 
-    def _drain_gathers(self, block: bool = False) -> None:
-        """Apply the finished result gathers, oldest first (``block``: wait for all of them:
-        the end of ``serve``)."""
+    def _drain_gathers(self, block: bool = False, limit_s: float = 30.0) -> None:
+        """Apply the finished result gathers, oldest first (``block``: wait for all of them, at
+        most ``limit_s``: the end of ``serve``; a gather still pending then is dropped, and
+        get-output for its batches falls back to the output files)."""
+        end = time.monotonic() + limit_s
         while self._gathers:
             w, ev, _, host, keys, imgs = self._gathers[0]
-            if not block and not (ev.query() if ev is not None else w.is_completed()):
-                return
+            if not (ev.query() if ev is not None else w.is_completed()):
+                if not block:
+                    return
+                if time.monotonic() > end:
+                    log.warning("rank %d: %d result gathers still pending at the end of serve; dropped",
+                                self.eg.grank, len(self._gathers))
+                    self._gathers.clear()
+                    return
+                time.sleep(0.001)
+                continue
             self._gathers.popleft()
             try:
                 if ev is not None:
