@@ -663,6 +663,9 @@ class CollectiveService:
         # ~8k images a flush (32 b256 batches; 40 B an image, 320 KiB a rank's buffer)
         self.collect_every = max(1, int(os.environ.get("DML_COLLECT_EVERY", "0")) or 8192 // max(1, backend.cap))
         self.collect_flushes = 0
+        # DML_COLLECT_FORCE_GATHER=1: gather over the result group at world 1 too (a one-rank
+        # RCCL gather: the GPU test of the collective path on a one-GPU box)
+        self._force_gather = os.environ.get("DML_COLLECT_FORCE_GATHER") == "1"
         self._pend_epoch = -1
         self._pend_rows: List[tuple] = []              # this rank's reports since the last flush
         self._pend_keys: List[List[tuple]] = []        # per group rank: the (job, batch) keys it reported
@@ -926,7 +929,14 @@ class CollectiveService:
                 coord.apply_requests(rq)
                 self._stage()
         if self.collect:
-            self._collect(h, rep, world, root, active, reports, finished, bool(flags & F_FLUSH))
+            try:
+                self._collect(h, rep, world, root, active, reports, finished, bool(flags & F_FLUSH))
+            except CollectiveFailure:
+                raise
+            except Exception as e:   # the same code on every rank: it fails everywhere alike
+                log.error("rank %d: result collect disabled: %s", eg.grank, e)
+                self.collect = False
+                self._gathers.clear()
         if finished and active and self.control is not None:
             self.control.jobs_progress(finished)
         t4 = time.perf_counter()
@@ -1022,17 +1032,20 @@ class CollectiveService:
         self._pend_rows, self._pend_imgs = [], {}
         self._pend_keys = [[] for _ in range(world)]
         self.collect_flushes += 1
-        if world == 1:
+        if world == 1 and not self._force_gather:
             self._take_rows([buf], keys, imgs)
             return
         if getattr(self.eg, "data_backend", "gloo") == "nccl":
             # a side stream: the gather and the coordinator's device->host copy wait for each
             # other only, not for the model work queued on the serving streams
+            # the backend's GPU (the control group may be gloo, with no device of its own: the
+            # bench's service passes run --comm gloo with an RCCL data group)
+            dev = self.be.device
             st = getattr(self, "_collect_stream", None)
             if st is None:
-                st = self._collect_stream = torch.cuda.Stream(device=self.eg.device)
+                st = self._collect_stream = torch.cuda.Stream(device=dev)
             with torch.cuda.stream(st):
-                t = torch.from_numpy(buf).to(self.eg.device)
+                t = torch.from_numpy(buf).to(dev)
                 outs = [torch.empty_like(t) for _ in range(world)] if self.eg.rank == root else None
                 w = self.eg.gather_result_async(t, outs, root)
                 host, ev = None, None

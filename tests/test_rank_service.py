@@ -229,8 +229,10 @@ def test_rank_rejoin_after_kill(tmp_path, victim):
 
 
 # --------------------------------------------------------- result collect --
-def _collect_rank(grank, world, rdzv, out, every):
+def _collect_rank(grank, world, rdzv, out, every, force=False):
     os.environ["DML_COLLECT_EVERY"] = str(every)
+    if force:
+        os.environ["DML_COLLECT_FORCE_GATHER"] = "1"
     from distributed_machine_learning_amd.parallel.elastic import ElasticGroup
     from distributed_machine_learning_amd.parallel.rank_backend import StoreRankBackend
     from distributed_machine_learning_amd.parallel.service import (CollectiveService, OutputWriter,
@@ -257,18 +259,17 @@ def _collect_rank(grank, world, rdzv, out, every):
     eg.close()
 
 
-@pytest.mark.parametrize("every", [1, 32])
-def test_result_collect_matches_output_files_world3(tmp_path, every):
+@pytest.mark.parametrize("every,world,force", [(1, 3, False), (32, 3, False), (32, 1, True)])
+def test_result_collect_matches_output_files(tmp_path, every, world, force):
     """SURVEY §2.6 'gather: results': the coordinator's final_<job>.json, rendered from the
     top-5 rows every rank gathered to it over the result group, is byte-identical to the
     reference's get-output merge of the per-batch output files (worker.py:1617-1627).
     every = 1: a gather on every step with reports; 32: rows held until a rank has 32
-    pending or a job finishes."""
+    pending or a job finishes. world 1 + force: the one-rank gather (DML_COLLECT_FORCE_GATHER)."""
     from distributed_machine_learning_amd.serving.output import merge_outputs
 
-    world = 3
     ctx = mp.get_context("spawn")
-    ps = [ctx.Process(target=_collect_rank, args=(r, world, str(tmp_path / "rdzv"), str(tmp_path), every))
+    ps = [ctx.Process(target=_collect_rank, args=(r, world, str(tmp_path / "rdzv"), str(tmp_path), every, force))
           for r in range(world)]
     for p in ps:
         p.start()

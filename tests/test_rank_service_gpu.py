@@ -98,11 +98,16 @@ def _engine_rows(blobs, names):
 
 
 @pytest.mark.timeout(900)
-def test_gpu_rank_launcher_cli_roundtrip(tmp_path):
+@pytest.mark.parametrize("force_gather", [False, True])
+def test_gpu_rank_launcher_cli_roundtrip(tmp_path, monkeypatch, force_gather):
+    """force_gather: the result rows reach the coordinator through a one-rank RCCL gather on
+    the result group (DML_COLLECT_FORCE_GATHER: the collective path of get-output on one GPU)."""
     import os
 
     from PIL import Image
 
+    if force_gather:
+        monkeypatch.setenv("DML_COLLECT_FORCE_GATHER", "1")
     files = _jpegs(str(tmp_path / "testfiles"))
     p, base = _launch_logged(tmp_path, 1)
     try:
@@ -115,6 +120,8 @@ def test_gpu_rank_launcher_cli_roundtrip(tmp_path):
                    "submit": await cli.run_line("submit-job ResNet50 12"),
                    "wait": await cli.run_line("wait-job 31 300"),
                    "get": await cli.run_line("get-output 31")}
+            out["fast"] = client.last_output_fast   # rendered at the coordinator from gathered rows
+            out["slow"] = await client.merge_output_files(31, str(tmp_path / "slow_31.json"))
             v2 = str(tmp_path / "3v2.jpeg")
             Image.fromarray(np.full((40, 30, 3), 200, np.uint8)).save(v2)
             out["put"] = await cli.run_line(f"put {v2} 3.jpeg")
@@ -129,6 +136,8 @@ def test_gpu_rank_launcher_cli_roundtrip(tmp_path):
         rc, log = _stop_logged(p, tmp_path)
     assert "loaded 12/12" in out["load"], (out, log)
     assert "finished" in out["wait"] and "finished" in out["wait2"], (out, log)
+    assert out["fast"] is True, (out, log)
+    assert open(out["slow"], "rb").read() == open(tmp_path / "dl" / "final_31.json", "rb").read()
     f1 = json.load(open(tmp_path / "dl" / "final_31.json"))
     f2 = json.load(open(tmp_path / "dl" / "final_32.json"))
     assert sorted(f1) == sorted(f2) == sorted(f"{i}.jpeg" for i in range(1, 13))
