@@ -405,7 +405,7 @@ class RankControl:
         jid = int(fr.payload["jobid"])
         tag = self.svc.writer.host_tag if getattr(self.svc, "writer", None) is not None else "node"
         loop = asyncio.get_running_loop()
-        data = await loop.run_in_executor(None, self.svc.final_output, jid, tag, 2.0)   # native render, GIL released
+        data = await loop.run_in_executor(None, self.svc.final_output, jid, tag, 5.0)   # native render, GIL released
         name = None
         if data is not None:
             name = f"final_{jid}.json"

@@ -708,6 +708,17 @@ class CollectiveService:
         if control is not None:
             control.attach(self)
         backend.attach(eg)
+        # RCCL creates a communicator at its first collective (seconds on a cold node): a first
+        # flush at a job's end then held the serve loop, and get-output fell back to the files.
+        # Every rank builds its service at the same point, so the result group's communicator is
+        # made here (a re-joining rank skips it: the survivors are serving; its new epoch's group
+        # comes up at that epoch's first flush, on every member at once)
+        if (self.collect and not rejoined and getattr(eg, "data_backend", "gloo") == "nccl"
+                and getattr(eg, "result_group", None) is not None and (eg.world > 1 or self._force_gather)
+                and self.be.device.type == "cuda"):
+            t = torch.zeros((1, 1, 10), dtype=torch.int32, device=self.be.device)
+            eg.gather_result(t, [torch.empty_like(t) for _ in range(eg.world)] if eg.rank == 0 else None, 0)
+            torch.cuda.synchronize(self.be.device)
 
     # ------------------------------------------------------------- roles --
     def coordinator_rank(self) -> int:
