@@ -262,6 +262,8 @@ int dml_plan_replay(void* plan, hipStream_t s);    // launch the captured graph
 // capture op ranges [bounds[i], bounds[i+1]) as separate graphs / launch graph i
 int dml_plan_capture_parts(void* plan, const int* bounds, int nparts, hipStream_t s);
 int dml_plan_replay_part(void* plan, int i, hipStream_t s);
+// a batch's event records / stream waits / index fetches / graph replays in one call (5 int64 per op)
+int dml_launch_seq(const int64_t* ops, int n);
 int dml_plan_time_ops(void* plan, hipStream_t s, float* ms_out, int n);  // per-op hipEvent timing
 int dml_plan_set_cfg(void* plan, int i, int cfg);  // re-point conv op i at config cfg; returns the old one
 int dml_plan_get_cfg(void* plan, int i);

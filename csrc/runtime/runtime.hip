@@ -253,6 +253,34 @@ extern "C" int dml_plan_replay(void* p, hipStream_t s) {
   return 0;
 }
 
+// One batch launch of the serving loop in one call (GpuRankBackend.launch): the sequence of
+// event records, stream waits, index-table fetches and graph replays that Engine / SplitEngine
+// .run issue one Python call each (8-10 HIP calls a batch, ~0.8 ms of serve-loop time under the
+// decode pool's GIL traffic). ops: n records of 5 int64 {kind, a, b, c, d}:
+//   0 record event a on stream b        1 stream a waits on event b
+//   2 replay plan a on stream b         3 replay part b of plan a on stream c
+//   4 index fetch host a -> device b, c entries, on stream d
+// Returns 0, or -1 - i for the first op i that failed.
+extern "C" int dml_launch_seq(const int64_t* ops, int n) {
+  for (int i = 0; i < n; ++i) {
+    const int64_t* o = ops + 5 * i;
+    int rc = 0;
+    switch (o[0]) {
+      case 0: rc = hipEventRecord((hipEvent_t)o[1], (hipStream_t)o[2]) == hipSuccess ? 0 : -1; break;
+      case 1: rc = hipStreamWaitEvent((hipStream_t)o[1], (hipEvent_t)o[2], 0) == hipSuccess ? 0 : -1; break;
+      case 2: rc = dml_plan_replay((void*)o[1], (hipStream_t)o[2]); break;
+      case 3: rc = dml_plan_replay_part((void*)o[1], (int)o[2], (hipStream_t)o[3]); break;
+      case 4: rc = dml_index_fetch((const int*)o[1], (int*)o[2], (int)o[3], (hipStream_t)o[4]); break;
+      default: g_err = "dml_launch_seq: bad op"; rc = -1;
+    }
+    if (rc) {
+      if (o[0] <= 1) g_err = "dml_launch_seq: event op failed";
+      return -1 - i;
+    }
+  }
+  return 0;
+}
+
 // Re-point conv op i at tile config cfg (joint tuning of co-scheduled
 // sub-batch plans). Returns the previous cfg, or -1 if op i is not a conv or
 // cfg is not a tile config. A captured graph must be re-captured.

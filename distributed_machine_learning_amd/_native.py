@@ -153,6 +153,7 @@ _SIGS = {
     "dml_plan_run_range": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "dml_plan_capture": (C.c_int, [C.c_void_p, C.c_void_p]),
     "dml_plan_replay": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dml_launch_seq": (C.c_int, [C.c_void_p, C.c_int]),
     "dml_plan_capture_parts": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_int, C.c_void_p]),
     "dml_plan_replay_part": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
     "dml_plan_time_ops": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_float), C.c_int]),

@@ -779,6 +779,20 @@ class Engine:
         else:
             N.check(self.lib.dml_plan_run(plan, s), "plan run")
 
+    def select(self, slot: int) -> None:
+        self._select_result(slot)
+
+    def launch_ops(self, stream, slot: int = 0) -> Optional[List[tuple]]:
+        """``run(stream, use_graph=True, slot=slot)`` as dml_launch_seq records (the graph
+        replay only), or None while that slot's graph is not captured."""
+        if not self.graph_captured[slot]:
+            return None
+        s = N.stream_ptr(stream)
+        plan = int(self.plans[slot])
+        if self.op_range is not None:
+            return [(3, plan, 0, s, 0)]
+        return [(2, plan, s, 0, 0)]
+
     def capture(self, stream=None) -> None:
         """Capture every source slot's forward as a hipGraph NOW, with the device
         idle, on ``stream`` — pass the stream the graphs will be replayed on.
@@ -1064,6 +1078,59 @@ class SplitEngine:
         for s, ev in zip(self.streams, self._join):
             ev.record(s)
             main.wait_event(ev)
+
+    def launch_ops(self, stream, slot: int = 0) -> Optional[List[tuple]]:
+        """``run(stream, use_graph=True, slot=slot)`` (deps None) as dml_launch_seq records:
+        the same event records, stream waits and graph replays in the same order; None while
+        a graph is not captured. The events are created here (a torch Event's handle exists
+        from its first record)."""
+        main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        evs = [self._fork] + list(self._join) + ([self._head_done] if self.tails else [])
+        for ev in evs:
+            if ev.cuda_event == 0:
+                ev.record(main)
+        ptr = lambda ev: int(ev.cuda_event)  # noqa: E731
+        sp = lambda st: int(st.cuda_stream)  # noqa: E731
+        ops: List[tuple] = []
+        if self.tails:
+            x = self.streams[0]
+            if self._tail_done[slot].cuda_event == 0:
+                return None
+            h1 = self.engines[1].launch_ops(x, slot)
+            h0 = self.engines[0].launch_ops(main, slot)
+            tl = self.tails[slot].launch_ops(main, 0)
+            if h1 is None or h0 is None or tl is None:
+                return None
+            ops += [(0, ptr(self._fork), sp(main), 0, 0), (1, sp(x), ptr(self._fork), 0, 0),
+                    (1, sp(x), ptr(self._tail_done[slot]), 0, 0)]
+            ops += h1 + [(0, ptr(self._head_done), sp(x), 0, 0)]
+            ops += h0 + [(1, sp(main), ptr(self._head_done), 0, 0)]
+            ops += tl + [(0, ptr(self._tail_done[slot]), sp(main), 0, 0)]
+            return ops
+        lanes = [main] + self.streams
+        ops.append((0, ptr(self._fork), sp(main), 0, 0))
+        for st in self.streams:
+            ops.append((1, sp(st), ptr(self._fork), 0, 0))
+        for i in range(1, self.splits):
+            if i % self.nstreams:
+                o = self.engines[i].launch_ops(lanes[i % self.nstreams], slot)
+                if o is None:
+                    return None
+                ops += o
+        for i in range(0, self.splits, self.nstreams):
+            o = self.engines[i].launch_ops(main, slot)
+            if o is None:
+                return None
+            ops += o
+        for st, ev in zip(self.streams, self._join):
+            ops += [(0, ptr(ev), sp(st), 0, 0), (1, sp(main), ptr(ev), 0, 0)]
+        return ops
+
+    def select(self, slot: int) -> None:
+        """The result views of source slot ``slot`` (what ``run`` selects first)."""
+        self._select_result(slot)
+        for e in self.engines:
+            e._select_result(slot)
 
     def _run_merged(self, main, use_graph: bool, slot: int, deps) -> None:
         """Head 1 on the extra stream (after its inputs and the tail that last read this slot's

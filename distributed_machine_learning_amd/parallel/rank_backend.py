@@ -62,6 +62,26 @@ class RankBackend:
         self.finalize(0)
         return res
 
+    def _launch_ops(self, model: str, slot: int) -> Optional[np.ndarray]:
+        """(model, slot)'s launch after the window waits, as dml_launch_seq records: the index
+        fetch, the engine's replays (Engine/SplitEngine.launch_ops), the slot's done event.
+        Built once; None (the Python path) while a graph is not captured."""
+        key = (model, slot)
+        ops = self._lops.get(key)
+        if ops is None:
+            eng, s = self.engines[model], self.stream
+            sp = int(s.cuda_stream)
+            eo = eng.launch_ops(s, slot)
+            if eo is None:
+                return None
+            if self.ev_done[slot].cuda_event == 0:
+                self.ev_done[slot].record(s)
+            hidx, didx = self.idx[model][slot], self.idx_dev[model][slot]
+            rows = [(4, hidx.data_ptr(), didx.data_ptr(), eng.batch, sp)] + eo + \
+                [(0, int(self.ev_done[slot].cuda_event), sp, 0, 0)]
+            ops = self._lops[key] = np.asarray(rows, np.int64)
+        return ops
+
     def finalize(self, slot: int) -> None:
         """(serve loop, after the slot's launch event completed, before its rows are read)"""
 
@@ -629,6 +649,10 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         from .. import _native as N
 
         self._fetch = N.lib().dml_index_fetch
+        # DML_NATIVE_LAUNCH=0: a batch launch issues its HIP calls one Python call each (A/B)
+        self.native_launch = os.environ.get("DML_NATIVE_LAUNCH", "1") != "0"
+        self._launch_seq = N.lib().dml_launch_seq
+        self._lops: Dict[Tuple[str, int], np.ndarray] = {}
         self.stream = torch.cuda.Stream(device)
         self.stage_stream = torch.cuda.Stream(device)
         # the staging pool (a window's fetch + GPU-JPEG prepare each) shares the interpreter with
@@ -919,6 +943,19 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         def fetch():  # host table -> the device table the stems read (stream order)
             if self._fetch(hidx.data_ptr(), didx.data_ptr(), B, sp) != 0:
                 raise RuntimeError("dml_index_fetch failed")
+        if len(slots) <= B and self.native_launch:
+            ops = self._launch_ops(model, slot)
+            if ops is not None:
+                iv[:len(slots)] = slots
+                iv[len(slots):] = slots[0] if slots else 0   # padding rows: computed, never reported
+                waits = [(1, sp, int(ev.cuda_event), 0, 0) for ev in arena.events(names) if ev.cuda_event]
+                seq = np.asarray(waits, np.int64).reshape(-1, 5)
+                seq = np.concatenate([seq, ops]) if len(waits) else ops
+                eng.select(slot)
+                rc = self._launch_seq(seq.ctypes.data, len(seq))
+                if rc != 0:
+                    N.check(rc, "dml_launch_seq")
+                return self.host_np[slot], self.ev_done[slot]
         with torch.cuda.stream(s):
             for ev in arena.events(names):  # the windows that staged these images
                 s.wait_event(ev)
