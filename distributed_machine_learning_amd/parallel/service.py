@@ -156,6 +156,7 @@ class ReplicatedCoordinator:
         self.lock = threading.RLock()      # control-thread readers (C1/C2/C5/status) vs the serve loop
         self.split_log: List[Tuple[float, Dict[str, int]]] = []   # (t, ranks per model) when the split changes
         self._last_split: Dict[str, int] = {}
+        self._slice_imgs: Dict[str, int] = dict.fromkeys(MODELS, 0)   # one-rank time slice: images dispatched
         # queued batch -> the rank its images are staged for (image windows, parallel/image_store.py):
         # replicated like the rest (assign_affinity runs at the same point on every rank); the
         # plan dispatches a batch to its affinity rank first
@@ -248,6 +249,19 @@ class ReplicatedCoordinator:
         target: Dict[int, str] = {}
         if len(active) == 1:
             target = {g: active[0] for g in members}
+            self._slice_imgs = dict.fromkeys(MODELS, 0)
+        elif len(members) == 1:
+            # one rank, both models: the reference's split needs two workers (worker.py:303-324
+            # gives one worker to one model until its queue drains). The rank is time-sliced
+            # instead: each step's free slots go to the model with fewer images dispatched since
+            # both were queued, so the two jobs advance together at equal image rates (its two
+            # GPU slots may hold one batch of each); no revokes between the two
+            g = members[0]
+            target = {g: min(active, key=lambda m: (self._slice_imgs.get(m, 0), m))}
+            shared = {"InceptionV3": 1, "ResNet50": 1, "time_sliced": 1}
+            if self._last_split != shared:
+                self._last_split = dict(shared)
+                self.split_log.append((time.monotonic(), dict(shared)))
         else:
             a, b = "InceptionV3", "ResNet50"
             bs = self.jobs.batch_sizes
@@ -273,7 +287,7 @@ class ReplicatedCoordinator:
         free: Dict[int, int] = {}
         for g in members:
             m = target[g]
-            if self.preempt and cur[g] is not None and cur[g] != m:
+            if self.preempt and len(members) > 1 and cur[g] is not None and cur[g] != m:
                 # this rank's batches of the old model beyond its GPU slots are
                 # still in its host queue: revoke them
                 old = [inf for inf in mine[g] if inf.batch.model != m]
@@ -329,6 +343,10 @@ class ReplicatedCoordinator:
         for g in members:
             if free[g] > low and target[g] in rest:
                 take(g, rest[target[g]])
+        if len(members) == 1 and len(active) == 2:
+            for bs in disp.values():
+                for b in bs:
+                    self._slice_imgs[b.model] = self._slice_imgs.get(b.model, 0) + len(b.images)
         return disp, revokes
 
     def table(self, members: List[int], disp: Dict[int, List[Batch]]) -> np.ndarray:

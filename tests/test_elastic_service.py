@@ -237,6 +237,36 @@ def test_affinity_staging_and_dispatch():
     assert [b.key for b in disp[0]] == own[0] + own[1]
 
 
+def test_one_rank_time_slices_both_models():
+    """with one rank the reference's fair-share split is degenerate (the
+    one worker runs one model until its queue drains). The plan time-slices the rank: free
+    slots go to the model with fewer images dispatched, so both jobs advance together at equal
+    image rates (ResNet50 batches of 8 images, InceptionV3 of 4: two InceptionV3 batches per
+    ResNet50 batch), without revokes."""
+    from distributed_machine_learning_amd.parallel.service import ReplicatedCoordinator, synthetic_names
+
+    c = ReplicatedCoordinator({"ResNet50": 8, "InceptionV3": 4}, cap=8, depth=4)
+    c.apply({"op": "submit", "model": "ResNet50", "images": synthetic_names(8 * 20), "job_id": 31})
+    c.apply({"op": "submit", "model": "InceptionV3", "images": synthetic_names(4 * 40), "job_id": 32})
+    members = [0]
+    order = []
+    inflight = []
+    for _ in range(40):
+        disp, rq = c.plan(members)
+        assert not rq
+        got = c.apply_table(c.table(members, disp), members)
+        inflight += got.get(0, [])
+        if inflight:   # the rank finishes its oldest batch each step
+            b = inflight.pop(0)
+            c.complete(b.key)
+            order.append(b.model)
+    first = order[:24]
+    assert "ResNet50" in first and "InceptionV3" in first, order
+    imgs = {m: sum(8 if m == "ResNet50" else 4 for x in first if x == m) for m in ("ResNet50", "InceptionV3")}
+    assert abs(imgs["ResNet50"] - imgs["InceptionV3"]) <= 16, (imgs, order)
+    assert c.split_log and c.split_log[-1][1].get("time_sliced") == 1
+
+
 def test_preemption_reaches_fair_share_within_two_batch_times():
     """A ResNet50 job saturates both ranks (depth 4: 2 launched + 2 queued per
     rank); an InceptionV3 job arrives. The plan moves one rank to InceptionV3,
