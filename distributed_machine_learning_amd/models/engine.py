@@ -867,7 +867,14 @@ MERGE_AT: Dict[str, Optional[str]] = {"ResNet50": None, "InceptionV3": None}
 def _extra_stream(device) -> "torch.cuda.Stream":
     """A sub-batch stream of a SplitEngine, at the caller's stream priority (a higher one
     for the extra streams measured 5 % slower)."""
-    return torch.cuda.Stream(device)
+    return torch.cuda.Stream(device, priority=serve_stream_priority())
+
+
+def serve_stream_priority() -> int:
+    """DML_SERVE_STREAM_PRIO (A/B; default 0 = the default priority): the priority of the
+    serving engines' streams, e.g. -1 (high) to run the model ahead of the GPU JPEG decodes
+    sharing the device in a store-image pass."""
+    return int(os.environ.get("DML_SERVE_STREAM_PRIO", "0"))
 
 
 def merge_point(model: str) -> Optional[str]:

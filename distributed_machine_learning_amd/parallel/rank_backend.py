@@ -653,7 +653,8 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
         self.native_launch = os.environ.get("DML_NATIVE_LAUNCH", "1") != "0"
         self._launch_seq = N.lib().dml_launch_seq
         self._lops: Dict[Tuple[str, int], np.ndarray] = {}
-        self.stream = torch.cuda.Stream(device)
+        from ..models.engine import serve_stream_priority
+        self.stream = torch.cuda.Stream(device, priority=serve_stream_priority())
         self.stage_stream = torch.cuda.Stream(device)
         # the staging pool (a window's fetch + GPU-JPEG prepare each) shares the interpreter with
         # the serve loop: 4 threads, not decode_threads (51,200-distinct pass on one box, 2 rounds:
