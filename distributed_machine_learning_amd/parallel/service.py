@@ -250,7 +250,7 @@ class ReplicatedCoordinator:
         if len(active) == 1:
             target = {g: active[0] for g in members}
             self._slice_imgs = dict.fromkeys(MODELS, 0)
-        elif len(members) == 1:
+        elif len(members) == 1 and ONE_RANK_SLICE:
             # one rank, both models: the reference's split needs two workers (worker.py:303-324
             # gives one worker to one model until its queue drains). The rank is time-sliced
             # instead: each step's free slots go to the model with fewer images dispatched since
@@ -437,6 +437,8 @@ class ReplicatedCoordinator:
         return h[-n:] if n > 0 else []
 
 
+# DML_ONE_RANK_SLICE=0: a lone rank runs one model at a time, as the reference's split (A/B)
+ONE_RANK_SLICE = os.environ.get("DML_ONE_RANK_SLICE", "1") != "0"
 STAGE_DEPTH = int(os.environ.get("DML_STAGE_DEPTH", "8"))  # batches per rank whose images are staged ahead of dispatch (image windows)
 
 
