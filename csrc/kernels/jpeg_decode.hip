@@ -141,10 +141,13 @@ __host__ __device__ static inline int byte_at(const uint8_t* p, int i) {
   return (int)((((const uint32_t*)p)[i >> 2] >> ((i & 3) * 8)) & 255);
 }
 
+// `look`: the 9-bit lookahead table to use (the parallel kernel's LDS copy; the descriptor's own
+// otherwise). Always a valid pointer: a select between an LDS and a global table made the
+// per-symbol lookup a FLAT load (counted with the global loads, waited for with them)
 template <class BR>
-__host__ __device__ static inline int huff_decode(BR& b, const DmljHuff& t, const uint32_t* look = nullptr) {
+__host__ __device__ static inline int huff_decode_lk(BR& b, const DmljHuff& t, const uint32_t* look) {
   b.fill();
-  const uint32_t e = (look ? look : t.look)[b.peek(9)];
+  const uint32_t e = look[b.peek(9)];
   if (e) {
     b.skip(e >> 8);
     return e & 255;
@@ -161,6 +164,11 @@ __host__ __device__ static inline int huff_decode(BR& b, const DmljHuff& t, cons
   }
   b.skip(l);
   return byte_at(t.val, (t.valoff[l] + code) & 255);
+}
+
+template <class BR>
+__host__ __device__ static inline int huff_decode(BR& b, const DmljHuff& t) {
+  return huff_decode_lk(b, t, t.look);
 }
 
 __host__ __device__ static inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
@@ -339,13 +347,18 @@ __host__ __device__ static PState seg_decode(const DmljImage& d, const McuMap& m
                                              int gb, int16_t* coef) {
   BitsAt b(stream, nw, st.pos);
   int u = st.u, k = st.k, cnt = 0;
+  // component -> Huffman table ids, packed once (2 bits each): `d.td[c]` with a per-lane c was a
+  // vector load from the descriptor on every symbol (rocprofv3: ~4 VMEM per symbol, 5x the LDS
+  // lookups; profiles/r6_pmc)
+  const int tdp = d.td[0] | (d.ncomp > 1 ? (d.td[1] << 2) | (d.td[2] << 4) : 0);
+  const int tap = d.ta[0] | (d.ncomp > 1 ? (d.ta[1] << 2) | (d.ta[2] << 4) : 0);
   int16_t* blk = WRITE && gb < m.total ? block_at(d, m, coef, gb) : nullptr;
   while (b.pos() < end) {
     if (WRITE && gb >= m.total) break;
     const int c = m.comp_of(u);
     bool done;
     if (k == 0) {
-      const int s = huff_decode(b, d.dc[d.td[c]], tb.dc(c));
+      const int s = huff_decode_lk(b, d.dc[(tdp >> (2 * c)) & 3], tb.dc(c));
       const int diff = s ? extend(b.get(s), s) : 0;
       if (WRITE) blk[0] = (int16_t)diff;
       k = 1;
@@ -361,7 +374,7 @@ __host__ __device__ static PState seg_decode(const DmljImage& d, const McuMap& m
         ++k;
         done = k >= 64;
       } else {
-        const int rs = huff_decode(b, d.ac[d.ta[c]], tb.look_ac + ao);
+        const int rs = huff_decode_lk(b, d.ac[(tap >> (2 * c)) & 3], tb.look_ac + ao);
         const int r = rs >> 4, sz = rs & 15;
         if (sz) {
           k += r;
