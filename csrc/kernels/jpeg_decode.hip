@@ -329,14 +329,25 @@ struct BitsAt {
   }
 };
 
-// the lookup tables one thread decodes with (LDS copies on the GPU, the descriptor's on the host):
-// component c's table is base + ((idx >> 2c) & 3) * stride words
+// the lookup tables one thread decodes with: an 11-bit lookahead per component and class,
+// (code length << 8) | symbol, 0 = a longer code (LDS on the GPU; built per image by the kernel).
+// Slot c: component c's DC table, slot 3 + c: its AC table.
+#define DMLJ_LA 11
 struct SegTabs {
-  const uint32_t *look_dc, *look_ac, *fast_ac;
-  int stride, idx_dc, idx_ac;
-  __host__ __device__ const uint32_t* dc(int c) const { return look_dc + ((idx_dc >> (2 * c)) & 3) * stride; }
-  __host__ __device__ int ac_off(int c) const { return ((idx_ac >> (2 * c)) & 3) * stride; }
+  const uint16_t* t11;
 };
+
+// entry i of the 11-bit lookahead of table t (the 9-bit one extended by the canonical
+// length-10 / 11 codes; huff_decode's search order)
+__host__ __device__ static inline uint16_t t11_entry(const DmljHuff& t, int i) {
+  const uint32_t e9 = t.look[i >> (DMLJ_LA - 9)];
+  if (e9) return (uint16_t)e9;
+  for (int l = 10; l <= DMLJ_LA; ++l) {
+    const int code = i >> (DMLJ_LA - l);
+    if (code <= t.maxcode[l]) return (uint16_t)((l << 8) | byte_at(t.val, (t.valoff[l] + code) & 255));
+  }
+  return 0;
+}
 
 // decode the symbols starting in [st.pos, end) from state st; returns the exit state and the
 // blocks completed. WRITE: block gb onwards gets its AC coefficients and its DC DIFFERENCE, and
@@ -356,39 +367,36 @@ __host__ __device__ static PState seg_decode(const DmljImage& d, const McuMap& m
   while (b.pos() < end) {
     if (WRITE && gb >= m.total) break;
     const int c = m.comp_of(u);
+    // one path for every symbol (r6: with 64 lanes at different block positions the wave ran
+    // the DC, the fast-AC and the general-AC branch on nearly every symbol; PMC profiles/r6_pmc):
+    // an 11-bit lookahead gives code length + symbol for all but the rare longer codes, the
+    // symbol's run / size / extra bits are then decoded the same way for DC and AC
+    const bool dcs = k == 0;
+    b.fill();
+    const uint32_t e = tb.t11[(dcs ? c : 3 + c) * (1 << DMLJ_LA) + b.peek(DMLJ_LA)];
+    int sym;
+    if (e) {
+      b.skip(e >> 8);
+      sym = e & 255;
+    } else {
+      sym = dcs ? huff_decode(b, d.dc[(tdp >> (2 * c)) & 3]) : huff_decode(b, d.ac[(tap >> (2 * c)) & 3]);
+    }
+    const int run = dcs ? 0 : sym >> 4, size = dcs ? sym : sym & 15;
+    const int v = size ? extend(b.get(size), size) : 0;
+    const int kk = dcs ? 0 : k + run;
+    if (WRITE && (dcs || size)) blk[kk < 64 ? kk : 63] = (int16_t)v;   // corrupt runs: libjpeg's pad -> 63
     bool done;
-    if (k == 0) {
-      const int s = huff_decode_lk(b, d.dc[(tdp >> (2 * c)) & 3], tb.dc(c));
-      const int diff = s ? extend(b.get(s), s) : 0;
-      if (WRITE) blk[0] = (int16_t)diff;
+    if (dcs) {
       k = 1;
       done = false;
+    } else if (size) {
+      k = kk + 1;
+      done = k >= 64;
+    } else if (run != 15) {
+      done = true;   // EOB
     } else {
-      b.fill();
-      const int ao = tb.ac_off(c);
-      const uint32_t f = tb.fast_ac[ao + b.peek(9)];
-      if (f) {
-        b.skip(f & 15);
-        k += (f >> 4) & 15;
-        if (WRITE) blk[k < 64 ? k : 63] = (int16_t)((int32_t)f >> 16);
-        ++k;
-        done = k >= 64;
-      } else {
-        const int rs = huff_decode_lk(b, d.ac[(tap >> (2 * c)) & 3], tb.look_ac + ao);
-        const int r = rs >> 4, sz = rs & 15;
-        if (sz) {
-          k += r;
-          const int v2 = extend(b.get(sz), sz);
-          if (WRITE) blk[k < 64 ? k : 63] = (int16_t)v2;
-          ++k;
-          done = k >= 64;
-        } else if (r != 15) {
-          done = true;   // EOB
-        } else {
-          k += 16;
-          done = k >= 64;
-        }
-      }
+      k += 16;
+      done = k >= 64;
     }
     if (done) {
       k = 0;
@@ -587,7 +595,7 @@ __global__ __launch_bounds__(64) void jpeg_huff_kernel(const unsigned char* __re
 // waiting on the stream reads
 template <int PT>
 struct ParLds {
-  uint32_t lk_dc[3][512], lk_ac[3][512], fs_ac[3][512];
+  uint16_t t11[6][1 << DMLJ_LA];
   int ex_pos[2][PT], ex_u[2][PT], ex_k[2][PT], scan[2][PT];
   int chg[3];
 };
@@ -600,9 +608,6 @@ __global__ __launch_bounds__(PT) void jpeg_huff_par_kernel(const unsigned char* 
   const DmljImage& d = ((const DmljImage*)(buf + 16))[i];
   if (!d.ok) return;   // uniform over the workgroup
   __shared__ ParLds<PT> L;
-  auto& lk_dc = L.lk_dc;
-  auto& lk_ac = L.lk_ac;
-  auto& fs_ac = L.fs_ac;
   auto& ex_pos = L.ex_pos;
   auto& ex_u = L.ex_u;
   auto& ex_k = L.ex_k;
@@ -610,14 +615,17 @@ __global__ __launch_bounds__(PT) void jpeg_huff_par_kernel(const unsigned char* 
   auto& chg = L.chg;
   const int t = threadIdx.x;
   const int nc = d.ncomp;
-  for (int c = 0; c < nc; ++c)
-    for (int j = t; j < 512; j += PT) {
-      lk_dc[c][j] = d.dc[d.td[c]].look[j];
-      lk_ac[c][j] = d.ac[d.ta[c]].look[j];
-      fs_ac[c][j] = d.ac[d.ta[c]].fast[j];
+  for (int c = 0; c < nc; ++c) {
+    const DmljHuff& hd = d.dc[d.td[c]];
+    const DmljHuff& ha = d.ac[d.ta[c]];
+#pragma unroll 4
+    for (int j = t; j < (1 << DMLJ_LA); j += PT) {
+      L.t11[c][j] = t11_entry(hd, j);
+      L.t11[3 + c][j] = t11_entry(ha, j);
     }
+  }
   if (t < 3) chg[t] = 0;
-  const SegTabs tb = {&lk_dc[0][0], &lk_ac[0][0], &fs_ac[0][0], 512, (2 << 4) | (1 << 2), (2 << 4) | (1 << 2)};
+  const SegTabs tb = {&L.t11[0][0]};
   const McuMap m = mcu_map(d);
   const uint32_t* stream = (const uint32_t*)(buf + d.stream_off);
   const int nw = (d.stream_len + 3) / 4;
@@ -1166,11 +1174,13 @@ extern "C" int dml_jpeg_parallel_host(const unsigned char* data, long len, short
   memset(coef_ser, 0, (size_t)ncoef * 2);
   decode_entropy(d, (const uint32_t*)stream, coef_ser, true);
   const McuMap m = mcu_map(d);
-  SegTabs tb = {d.dc[0].look, d.ac[0].look, d.ac[0].fast, (int)(sizeof(DmljHuff) / 4), 0, 0};
-  for (int c = 0; c < d.ncomp; ++c) {
-    tb.idx_dc |= d.td[c] << (2 * c);
-    tb.idx_ac |= d.ta[c] << (2 * c);
-  }
+  static thread_local uint16_t t11[6][1 << DMLJ_LA];
+  for (int c = 0; c < d.ncomp; ++c)
+    for (int j = 0; j < (1 << DMLJ_LA); ++j) {
+      t11[c][j] = t11_entry(d.dc[d.td[c]], j);
+      t11[3 + c][j] = t11_entry(d.ac[d.ta[c]], j);
+    }
+  const SegTabs tb = {&t11[0][0]};
   const uint32_t* w = (const uint32_t*)stream;
   const int nw = (d.stream_len + 3) / 4;
   const int want = info[1] > 0 && info[1] <= 512 ? (int)info[1] : DMLJ_PT;   // segments (A/B: up to 512)
