@@ -236,8 +236,10 @@ __host__ __device__ static void decode_entropy(const DmljImage& d, const uint32_
 //      block; every thread decodes its segment once more, now writing coefficients and DC
 //      DIFFERENCES, and stops at the image's last block;
 //   4. the DC predictions are rebuilt per component by a block-wide prefix sum in decode order.
-// The per-symbol code (tables, fast AC path, corrupt-code handling) is the serial decoder's,
-// so the coefficients are identical to it (tests/test_jpeg_decode.py compares every block).
+// Per symbol: one 11-bit lookahead (code length + symbol) and the same run / size / extra-bits
+// arithmetic for DC and AC; codes longer than 11 bits and corrupt codes take the serial
+// decoder's general path, so the coefficients are identical to it (tests/test_jpeg_decode.py
+// compares every block).
 // Segments per image: a decoder started in the wrong state re-joins the true symbol AND
 // block-slot sequence after ~5,000 bits (CPU replay, 40 bench images: 64 / 128 / 256 segments
 // take 2.5 / 4.7 / 9.5 rounds), so a lane's bits (2 + rounds) x segment fall only 10.6k -> 7.0k
