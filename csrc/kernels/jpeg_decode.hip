@@ -376,15 +376,19 @@ __host__ __device__ static PState seg_decode(const DmljImage& d, const McuMap& m
     const bool dcs = k == 0;
     b.fill();
     const uint32_t e = tb.t11[(dcs ? c : 3 + c) * (1 << DMLJ_LA) + b.peek(DMLJ_LA)];
-    int sym;
+    int sym, len;
     if (e) {
-      b.skip(e >> 8);
+      len = e >> 8;   // skipped together with the extra bits below (one shift of the buffer)
       sym = e & 255;
     } else {
       sym = dcs ? huff_decode(b, d.dc[(tdp >> (2 * c)) & 3]) : huff_decode(b, d.ac[(tap >> (2 * c)) & 3]);
+      len = 0;        // the general path consumed the code
     }
     const int run = dcs ? 0 : sym >> 4, size = dcs ? sym : sym & 15;
-    const int v = size ? extend(b.get(size), size) : 0;
+    const int tot = len + size;   // <= 11 + 15 bits: the fill left >= 33
+    const uint32_t bits = tot ? b.peek(tot) : 0u;
+    b.skip(tot);
+    const int v = size ? extend((int)(bits & ((1u << size) - 1u)), size) : 0;
     const int kk = dcs ? 0 : k + run;
     if (WRITE && (dcs || size)) blk[kk < 64 ? kk : 63] = (int16_t)v;   // corrupt runs: libjpeg's pad -> 63
     bool done;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r6 call AA: the single-path 11-bit Huffman symbol decode: numerics (Pillow byte-exact), the
+# r6 call AA (re-run after the merged code / extra-bit shift): the single-path 11-bit Huffman symbol decode: numerics (Pillow byte-exact), the
 # window bench twice, one PMC pass, then the 51,200-distinct pass twice.
 set -o pipefail
 cd "$(dirname "$0")/.."
