@@ -490,10 +490,10 @@ class Engine:
         self.probs = torch.zeros((B, g.classes), device=self.device, dtype=torch.float32)
 
     def _select_result(self, slot: int) -> None:
-        """result / top_idx / top_p name the result rows of the last-run slot."""
-        self.result = self.results[slot]
-        self.top_idx = self.result[0]
-        self.top_p = self.result[1].view(torch.float32)
+        """result / top_idx / top_p name the result rows of the last-run slot (the views made
+        once per slot: a serving loop selects per batch, and each tensor view was a ~60 us torch
+        call next to the decode pool's threads)."""
+        self.result, self.top_idx, self.top_p = _result_views(self, slot)
 
     def view(self, name: str) -> torch.Tensor:
         """NHWC view of a tensor buffer (for tests / debugging)."""
@@ -864,6 +864,17 @@ class Engine:
 MERGE_AT: Dict[str, Optional[str]] = {"ResNet50": None, "InceptionV3": None}
 
 
+def _result_views(eng, slot: int) -> tuple:
+    """(result, top-5 ids, top-5 probs as fp32) of ``eng.results[slot]``, cached per slot (the
+    cache follows the tensor object, so a replaced result tensor gets new views)."""
+    cache = eng.__dict__.setdefault("_views", {})
+    r = eng.results[slot]
+    hit = cache.get(slot)
+    if hit is None or hit[0] is not r:
+        hit = cache[slot] = (r, r[0], r[1].view(torch.float32))
+    return hit
+
+
 def _extra_stream(device) -> "torch.cuda.Stream":
     """A sub-batch stream of a SplitEngine, at the caller's stream priority (a higher one
     for the extra streams measured 5 % slower)."""
@@ -1049,9 +1060,7 @@ class SplitEngine:
             t.capture(main)
 
     def _select_result(self, slot: int) -> None:
-        self.result = self.results[slot]
-        self.top_idx = self.result[0]
-        self.top_p = self.result[1].view(torch.float32)
+        self.result, self.top_idx, self.top_p = _result_views(self, slot)
 
     def run(self, stream=None, use_graph: bool = False, slot: int = 0,
             deps: Optional[List[torch.cuda.Event]] = None) -> None:
