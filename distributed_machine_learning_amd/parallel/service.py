@@ -257,11 +257,12 @@ class ReplicatedCoordinator:
             # both were queued, so the two jobs advance together at equal image rates (its two
             # GPU slots may hold one batch of each); no revokes between the two
             g = members[0]
-            target = {g: min(active, key=lambda m: (self._slice_imgs.get(m, 0), m))}
             shared = {"InceptionV3": 1, "ResNet50": 1, "time_sliced": 1}
-            if self._last_split != shared:
+            if self._last_split != shared:   # entering the slice: counts from here on
                 self._last_split = dict(shared)
                 self.split_log.append((time.monotonic(), dict(shared)))
+                self._slice_imgs = dict.fromkeys(MODELS, 0)
+            target = {g: min(active, key=lambda m: (self._slice_imgs.get(m, 0), m))}
         else:
             a, b = "InceptionV3", "ResNet50"
             bs = self.jobs.batch_sizes
