@@ -214,6 +214,8 @@ void dml_jpeg_set_slot(void* buf, int i, int slot);
 void dml_jpeg_set_slots(void* buf, const int* idx, const int* slots, int n);
 int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long maxstream, void* dwork, int H, int W,
                            void* arena, hipStream_t s);
+int dml_jpeg_launch(const void* host, void* dev, long used, void* dwork, long coef_bytes, int n, int maxblk,
+                    long maxstream, int H, int W, void* arena, hipStream_t s);   // H2D + zero + decode_resize
 int dml_jpeg_init(void);
 long dml_jpeg_desc_size(void);
 long dml_jpeg_head_size(void);

@@ -1109,6 +1109,23 @@ extern "C" int dml_jpeg_decode_resize(const void* dbuf, int n, int maxblk, long 
   return 0;
 }
 
+// the whole GPU decode of a window in one call (GpuRankBackend's serve loop issued the H2D copy,
+// the coefficient zeroing and the launch as three Python calls): pinned pack -> device copy,
+// zeroed coefficient region, then the decode kernels, all on stream s
+extern "C" int dml_jpeg_launch(const void* host, void* dev, long used, void* dwork, long coef_bytes, int n, int maxblk,
+                               long maxstream, int H, int W, void* arena, hipStream_t s) {
+  if (used <= 0 || coef_bytes < 0) {
+    dml_set_error("dml_jpeg_launch: bad sizes");
+    return -1;
+  }
+  if (hipMemcpyAsync(dev, host, (size_t)used, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemsetAsync(dwork, 0, (size_t)coef_bytes, s) != hipSuccess) {
+    dml_set_error("dml_jpeg_launch: copy / memset failed");
+    return -1;
+  }
+  return dml_jpeg_decode_resize(dev, n, maxblk, maxstream, dwork, H, W, arena, s);
+}
+
 // a decoded image's descriptor re-targeted to another output size (the other model's window):
 // dst <- src with that size's NEAREST tables and ABSOLUTE plane addresses (base + plane_off), for
 // dml_jpeg_resize_only — the image is decoded once for both models

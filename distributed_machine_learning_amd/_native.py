@@ -130,6 +130,8 @@ _SIGS = {
     "dml_jpeg_decode_resize": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_long, C.c_void_p, C.c_int, C.c_int,
                                          C.c_void_p, C.c_void_p]),
     "dml_jpeg_init": (C.c_int, []),
+    "dml_jpeg_launch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_long, C.c_void_p, C.c_long, C.c_int, C.c_int, C.c_long,
+                                  C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "dml_jpeg_retarget": (None, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_long]),
     "dml_jpeg_retarget_many": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "dml_jpeg_resize_only": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),

@@ -484,6 +484,8 @@ class _JpegPack:
         # the device work buffer now (coefficients, then the sample planes the other model's
         # window re-uses: GpuRankBackend.planes_for)
         self.work = torch.empty(max(self.work_bytes, 256), dtype=torch.uint8, device=backend.device)
+        # and the device copy of the pack (here, not on the serve loop at launch)
+        self.dev = torch.empty(max(self.used, 256), dtype=torch.uint8, device=backend.device)
         # the stream `work` was allocated on (this pool thread's): the side stream waits on this
         # event only - waiting on the serve loop's current stream (the staging stream, which has
         # waited on every earlier window's decode) chained all decodes one after the other
@@ -511,15 +513,13 @@ class _JpegPack:
         side.wait_event(self.alloc_ev)
         for ev in getattr(self, "after", ()):   # image_store: earlier windows writing these slots
             side.wait_event(ev)
-        with torch.cuda.stream(side):
-            self.dev = torch.empty(self.used, dtype=torch.uint8, device=arena.device)
-            self.dev.copy_(self.buf[:self.used], non_blocking=True)
-            self.work[:self.coef_bytes].zero_()
-            N.check(L.dml_jpeg_decode_resize(self.dev.data_ptr(), self.n, self.maxblk, self.maxstream,
-                                             self.work.data_ptr(), H, W, arena.data_ptr(), side.cuda_stream),
-                    "dml_jpeg_decode_resize")
-            done = torch.cuda.Event()
-            done.record(side)
+        # H2D copy of the pack, zeroed coefficients and the decode kernels: one native call
+        N.check(L.dml_jpeg_launch(C.c_void_p(self.buf.data_ptr()), C.c_void_p(self.dev.data_ptr()), self.used,
+                                  C.c_void_p(self.work.data_ptr()), self.coef_bytes, self.n, self.maxblk,
+                                  self.maxstream, H, W, C.c_void_p(arena.data_ptr()), C.c_void_p(side.cuda_stream)),
+                "dml_jpeg_launch")
+        done = torch.cuda.Event()
+        done.record(side)
         stream.wait_event(done)
         # the caching allocator must not hand these buffers out before `side` is done with them
         self.dev.record_stream(side)
