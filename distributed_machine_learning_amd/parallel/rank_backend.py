@@ -740,7 +740,11 @@ class GpuRankBackend(_ArenaStaging, RankBackend):
             t = self._nn[(n_in, n_out)] = nearest_index(n_in, n_out)
         return t
 
-    JPEG_STREAMS = 8
+    # side streams of the GPU JPEG decodes (DML_JPEG_STREAMS: A/B). 2, not 8: fewer decodes in
+    # flight at once leave the model kernels more of the GPU; the 51,200-distinct pass measured
+    # 58.0-58.9k images/s with 2 against 57.1-57.9k with 8 over 4 interleaved rounds
+    # (profiles/r6_ah, r6_ai), the window bench with 4 windows on 4 streams being its own setup
+    JPEG_STREAMS = int(os.environ.get("DML_JPEG_STREAMS", "2"))
     # device work buffers of decoded windows kept for the other model (DML_PLANE_CACHE_GB). A
     # 256-image window holds ~90 MB (coefficients + planes): 4 GiB kept ~11k images, so on the
     # 51,200-distinct run the second job re-decoded every image the first had decoded long before
