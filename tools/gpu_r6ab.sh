@@ -2,7 +2,7 @@
 # r6 call AB (final tree): the full GPU suite, the driver's bench command, the 51,200-distinct pass twice.
 set -o pipefail
 cd "$(dirname "$0")/.."
-O=gpurun_out/r6_final3
+O=gpurun_out/r6_final4
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
